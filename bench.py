@@ -1,0 +1,323 @@
+#!/usr/bin/env python3
+"""bench.py — headline benchmark of the MI355X SpMV suite.
+
+Metric (BASELINE.json): effective HBM GB/s (+ GFLOP/s) of fp64 y = A·x per
+format on cant.mtx.  The real cant.mtx is a Git-LFS pointer in the
+reference, so the matrix is the cant-like stand-in
+(spmv_gen_cantlike: N = 62,451, Z = 4,007,383, the real cant's counts).
+
+Step = ONE SpMV launch over a batch of B independent cant-like matrices
+stacked block-diagonally (default B = 32: 1.58 GB of CSR, 6x the 256 MiB
+Infinity Cache, so the stream comes from HBM, not from the cache), all
+arrays resident in HBM before timing starts.  Default format: CSR-vector
+(BASELINE.json configs[1]).  At N=1 the other four formats are measured on
+the same batch too (`per_format`), plus a single cant-like copy cold
+(512 MiB flush before every launch) and warm (`cant_single`).
+
+Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): rows are
+sharded — rank r owns copies [r·B, (r+1)·B) of an N·B-copy matrix (weak
+scaling, no collective in the timed step).  The y all-gather over RCCL that
+concatenates the shards is timed separately (`allgather`).
+
+value = algorithmic bytes of all ranks / (max over ranks of the wall time
+of K steps / K).  bytes_alg = 12·Z + 4·(N+1) + 8·M + 8·N per copy
+(SURVEY.md §8d): values, columns, row offsets, x and y once each.
+roofline.achieved uses the same bytes over the kernel's mean duration from
+HIP events recorded on the launch stream; roofline.traffic comes from the
+rocprofv3 PMC passes committed in profiles/ (tools/pmc_traffic.py).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+REPO = Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO / "opencl-spmv-algorithms_amd"))
+sys.path.insert(0, str(REPO))
+
+import spmv_amd as sa  # noqa: E402
+
+METRIC = "effective HBM GB/s + GFLOP/s per format on cant.mtx, 1/2/4/8 MI355X"
+KERNEL_NAMES = {  # dominant kernel per format (as rocprofv3 names it)
+    "csr": "csr_vector_kernel",
+    "sell": "sell_kernel",
+    "ell": "ell_kernel",
+    "coo": "coo_tile_kernel",
+    "cmrs": "cmrs_kernel",
+}
+
+
+def parse():
+    p = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--format", default="csr", choices=sa.FORMATS)
+    p.add_argument("--copies", type=int, default=32, help="cant-like copies per GPU (batch)")
+    p.add_argument("--per-format", default="auto", choices=["auto", "yes", "no"],
+                   help="also measure the other formats (default: at N=1 only)")
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0: skip)")
+    p.add_argument("--lanes", type=int, default=0)
+    p.add_argument("--ki", type=int, default=2)
+    p.add_argument("--C", type=int, default=64)
+    p.add_argument("--sigma", type=int, default=1024)
+    p.add_argument("--h", type=int, default=8)
+    p.add_argument("--profile", action="store_true", help="only the timed loop (for rocprofv3 passes)")
+    return p.parse_args()
+
+
+def fmt_kwargs(args, fmt):
+    if fmt == "csr":
+        return {"lanes": args.lanes}
+    if fmt == "ell":
+        return {"ki": args.ki}
+    if fmt == "sell":
+        return {"C": args.C, "sigma": args.sigma, "ki": args.ki}
+    if fmt == "cmrs":
+        return {"h": args.h}
+    return {}
+
+
+def time_steps(torch, dm, x, y, steps, warmup, dist=None):
+    """W warm-up launches, then exactly `steps` launches bracketed by a
+    barrier + synchronize; per-launch HIP events on the launch stream."""
+    stream = torch.cuda.current_stream()
+    for _ in range(warmup):
+        dm.run(x, y, stream)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev[0].record(stream)
+    for i in range(steps):
+        dm.run(x, y, stream)
+        ev[i + 1].record(stream)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    kern = [ev[i].elapsed_time(ev[i + 1]) for i in range(steps)]  # ms, back-to-back launches
+    return wall, kern
+
+
+def cold_single(torch, dm, x, y, reps=30):
+    """Single-matrix launch after a 512 MiB flush (cold) and back-to-back (warm)."""
+    stream = torch.cuda.current_stream()
+    cold = []
+    for _ in range(reps):
+        sa.flush_cache(stream)
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        dm.run(x, y, stream)
+        b.record(stream)
+        torch.cuda.synchronize()
+        cold.append(a.elapsed_time(b))
+    _, warm = time_steps(torch, dm, x, y, reps, 3)
+    return float(np.median(cold)), float(np.median(warm))
+
+
+def traffic_for(fmt, workload_bytes):
+    """HBM bytes per launch from the committed PMC passes, if they match."""
+    f = REPO / "profiles" / "traffic.json"
+    if not f.exists():
+        return None
+    try:
+        t = json.loads(f.read_text()).get(fmt)
+    except (ValueError, AttributeError):
+        return None
+    if not t or int(t.get("bytes_alg", -1)) != int(workload_bytes):
+        return None
+    return t.get("hbm_bytes_per_launch")
+
+
+def cpu_baseline(m_single_csr, copies, budget_s):
+    """The oracle's restatement of the reference's OpenMP CSR loop
+    (reference csr.c:285-309) on the same batch, bounded to ~budget_s."""
+    from oracle import oracle
+
+    ptr, col, val, n_rows, n_cols = m_single_csr
+    # the batch is `copies` identical block-diagonal copies: time whole
+    # passes over a host batch built the same way as the device one
+    B = copies
+    bptr = np.concatenate([ptr[:-1] + k * ptr[-1] for k in range(B)] + [np.array([B * ptr[-1]], np.int64)])
+    bcol = np.concatenate([col + k * n_cols for k in range(B)]).astype(np.int32)
+    bval = np.tile(val, B)
+    x = np.arange(B * n_cols, dtype=np.float64)
+    y = np.empty(B * n_rows, np.float64)
+    threads = oracle.max_threads()
+    times = []
+    t_end = time.perf_counter() + budget_s
+    while time.perf_counter() < t_end or len(times) < 3:
+        times.append(oracle.cpu_csr_omp(B * n_rows, bptr, bcol, bval, x, y, threads))
+        if len(times) >= 1000:
+            break
+    t = float(np.median(times))
+    b = sa.bytes_alg(B * n_rows, B * n_cols, B * int(ptr[-1]))
+    return {"value": round(b / t * 1e-9, 2), "unit": "GB/s", "cores": threads, "kind": "port",
+            "sample": f"oracle OpenMP CSR loop (reference csr.c:285-309) over the same {B}-copy batch, "
+                      f"{len(times)} passes in ~{sum(times):.1f} s, median {t * 1e3:.2f} ms/pass",
+            "gflops": round(2 * B * int(ptr[-1]) / t * 1e-9, 2)}
+
+
+def main():
+    args = parse()
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    # ---- the batch: B cant-like copies, this rank's row shard
+    B = args.copies
+    single = sa.gen_cantlike(0, 1)
+    m = sa.gen_cantlike(0, B)
+    n_rows, n_cols, nnz = m.n_rows, m.n_cols, m.nnz
+    bytes_step = sa.bytes_alg(n_rows, n_cols, nnz)
+    x = torch.from_numpy(sa.ramp_x(n_cols) + rank * n_cols).to(dev)  # this shard's block of x
+    y = torch.empty(n_rows, dtype=torch.float64, device=dev)
+
+    dm = sa.to_device(m, args.format, dev, **fmt_kwargs(args, args.format))
+    wall, kern = time_steps(torch, dm, x, y, args.steps, args.warmup, dist)
+    if args.profile:
+        if rank == 0:
+            print(json.dumps({"profile_run": args.format, "ms_per_launch": float(np.mean(kern))}))
+        return
+
+    # parity spot check of this step's output against the host check
+    yh = y.cpu().numpy()
+    xh = x.cpu().numpy()
+    bad, first = sa.check(single, xh[:single.n_cols], yh[:single.n_rows])
+    if bad:
+        raise SystemExit(f"rank {rank}: parity failure at row {first}")
+
+    wall_t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    kern_mean = float(np.mean(kern))
+    kern_t = torch.tensor([kern_mean], dtype=torch.float64, device=dev)
+    if dist is not None:
+        dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(kern_t, op=dist.ReduceOp.MAX)
+    wall_max = float(wall_t.item())
+    ms_per_step = wall_max / args.steps * 1e3
+    total_bytes = bytes_step * world
+    value = total_bytes / (ms_per_step * 1e-3) * 1e-9
+    gflops = 2.0 * nnz * world / (ms_per_step * 1e-3) * 1e-9
+
+    # ---- y all-gather over RCCL (timed separately, not in `value`)
+    allgather = None
+    if dist is not None:
+        y_all = torch.empty(n_rows * world, dtype=torch.float64, device=dev)
+        for _ in range(3):
+            dist.all_gather_into_tensor(y_all, y)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        reps = 20
+        for _ in range(reps):
+            dist.all_gather_into_tensor(y_all, y)
+        torch.cuda.synchronize()
+        ag = torch.tensor([(time.perf_counter() - t0) / reps], dtype=torch.float64, device=dev)
+        dist.all_reduce(ag, op=dist.ReduceOp.MAX)
+        ag_ms = float(ag.item()) * 1e3
+        allgather = {"ms": round(ag_ms, 4), "bytes_per_rank": 8 * n_rows,
+                     "value_with_allgather_GBs": round(total_bytes / ((ms_per_step + ag_ms) * 1e-3) * 1e-9, 1)}
+
+    kern_ms = float(kern_t.item())
+    achieved = bytes_step / (kern_ms * 1e-3) * 1e-9
+    traffic = traffic_for(args.format, bytes_step)
+    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": sa.HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / sa.HBM_PEAK_GBS, 4), "traffic": traffic,
+                "kernel": KERNEL_NAMES[args.format], "kernel_ms": round(kern_ms, 5),
+                "bytes_alg_per_launch": bytes_step}
+
+    per_format = None
+    cant_single = None
+    cpu = None
+    do_pf = args.per_format == "yes" or (args.per_format == "auto" and world == 1)
+    if rank == 0 and do_pf:
+        del dm
+        torch.cuda.empty_cache()
+        per_format = {}
+        cant_single = {}
+        xs = torch.from_numpy(sa.ramp_x(single.n_cols)).to(dev)
+        ys = torch.empty(single.n_rows, dtype=torch.float64, device=dev)
+        bs = sa.bytes_alg(single.n_rows, single.n_cols, single.nnz)
+        for fmt in sa.FORMATS:
+            kw = fmt_kwargs(args, fmt)
+            d2 = sa.to_device(m, fmt, dev, **kw)
+            w2, k2 = time_steps(torch, d2, x, y, max(20, args.steps // 2), 5)
+            km = float(np.mean(k2))
+            per_format[fmt] = {"GBs": round(bytes_step / (km * 1e-3) * 1e-9, 1),
+                               "GFLOPs": round(2 * nnz / (km * 1e-3) * 1e-9, 1),
+                               "frac": round(bytes_step / (km * 1e-3) * 1e-9 / sa.HBM_PEAK_GBS, 4),
+                               "kernel_ms": round(km, 5),
+                               "stored_MB": round(d2.stored_bytes * 1e-6, 1), "params": kw or None}
+            del d2
+            torch.cuda.empty_cache()
+            d1 = sa.to_device(single, fmt, dev, **kw)
+            c_ms, w_ms = cold_single(torch, d1, xs, ys)
+            bad1, _ = sa.check(single, sa.ramp_x(single.n_cols), ys.cpu().numpy())
+            cant_single[fmt] = {"cold_ms": round(c_ms, 5), "cold_GBs": round(bs / (c_ms * 1e-3) * 1e-9, 1),
+                                "warm_ms": round(w_ms, 5), "warm_GBs_cache_resident": round(bs / (w_ms * 1e-3) * 1e-9, 1),
+                                "parity_ok": bad1 == 0}
+            del d1
+        if args.cpu_seconds > 0:
+            ptr, col, val = sa.csr_from_coo(single)
+            cpu = cpu_baseline((ptr, col, val, single.n_rows, single.n_cols), B, args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: cant-like stand-in (62,451 rows, 4,007,383 entries = SuiteSparse cant's counts; "
+                    "the reference's cant.mtx is an unfetched Git-LFS pointer), x[j] = j",
+            "config": {"workload": f"{args.format} SpMV on a block-diagonal batch of {B} cant-like copies per GPU "
+                                   f"(BASELINE.json configs[1]" + (")" if args.format == "csr" else "-style)"),
+                       "format": args.format, "params": fmt_kwargs(args, args.format) or None,
+                       "copies_per_gpu": B, "rows_per_gpu": n_rows, "nnz_per_gpu": nnz,
+                       "bytes_alg_per_gpu_step": bytes_step, "parallelism": f"row-shard x{world}"},
+            "gflops": round(gflops, 1),
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "per_format": per_format,
+            "cant_single": cant_single,
+            "allgather": allgather,
+            "device": sa.device_name(local),
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

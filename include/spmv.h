@@ -1,0 +1,150 @@
+/*
+ * spmv.h — C-ABI of the MI355X (gfx950) fp64 SpMV kernels: y = A·x.
+ *
+ * This is the drop-in boundary that replaces the reference's
+ * "clSetKernelArg ×k → clEnqueueNDRangeKernel" call sites
+ * (reference coo.c:163-194, csr.c:170-201, ell.c:242-273,
+ *  sigma_c.c:280-311, cmrs.c:195-232) and the five OpenCL kernels
+ * (reference kernels/{Coo,Csr,Ell,Sigma_C,Cmrs}.cl).  Everything here is
+ * plain C: device pointers, sizes, a hipStream_t passed as `void *`.
+ *
+ * Conventions (all entry points):
+ *   - Every array argument is a DEVICE pointer on `d.device`, owned by the
+ *     caller.  The library only owns scratch it allocates itself
+ *     (spmv_flush_cache's buffer) and frees it in spmv_release().
+ *   - y is FULLY overwritten (rows without entries get 0.0).  The reference
+ *     COO relied on fresh device memory being zero (reference coo.c:120);
+ *     here no pre-zeroing is required.
+ *   - Calls are asynchronous on `d.stream` (NULL = the device's default
+ *     stream).  No hidden device-wide synchronisation, no allocation inside
+ *     a *_run call, so a caller may capture them into a hipGraph.
+ *   - Return value: 0 on success, otherwise a code of spmv_rc.h with the
+ *     reference's numeric meaning (reference inc/enums.h:4-11):
+ *     1 device error, 2 launch/copy error, 4 bad arguments.
+ *     spmv_last_error() returns a human readable message for the last
+ *     failure on the calling thread.
+ *   - Indices are 0-based.  Column indices are int32 (as the reference);
+ *     offsets into the value arrays are int64 (the reference's int32
+ *     offsets overflow past 2^31 entries).
+ */
+#ifndef SPMV_H
+#define SPMV_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "spmv_rc.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct spmv_dims {
+    int64_t n_rows; /* N: rows of A, length of y            */
+    int64_t n_cols; /* M: columns of A, length of x         */
+    int64_t nnz;    /* Z: stored entries that are multiplied */
+    int device;     /* HIP device ordinal holding the arrays */
+    void *stream;   /* hipStream_t (NULL: default stream)    */
+} spmv_dims;
+
+/* ---------------------------------------------------------------- COO ---
+ * Replaces kernel `coo(row,col,val,x,y,int Z)` (reference kernels/Coo.cl:24)
+ * and its launch (reference coo.c:47-48,68-73,163-168,194).
+ * Entries MUST be sorted by row (any order inside a row); build them with
+ * spmv_coo_sort_by_row() (spmv_host.h).  Wave-level segmented reduction
+ * over fixed tiles of entries; rows that straddle tiles are finished by a
+ * second, deterministic carry pass — no atomics, bitwise reproducible.
+ * `ws` is device scratch of at least spmv_coo_ws_bytes(nnz) bytes.       */
+size_t spmv_coo_ws_bytes(int64_t nnz);
+int spmv_coo_run(spmv_dims d, const int32_t *row, const int32_t *col,
+                 const double *val, const double *x, double *y, void *ws,
+                 size_t ws_bytes);
+
+/* ---------------------------------------------------------------- CSR ---
+ * Replaces kernel `csr(ptr,col,val,x,y,int N)` (reference kernels/Csr.cl:1)
+ * and its launch (reference csr.c:47-48,170-175,201).
+ * CSR-vector: a group of `lanes_per_row` lanes (2..64, power of two) works
+ * on one row; the block's row_ptr window is staged in LDS; partial sums are
+ * reduced with cross-lane shuffles.  lanes_per_row = 0 picks from the mean
+ * row length (spmv_csr_auto_lanes).                                      */
+int spmv_csr_auto_lanes(int64_t n_rows, int64_t nnz);
+int spmv_csr_run(spmv_dims d, const int64_t *row_ptr, const int32_t *col,
+                 const double *val, const double *x, double *y,
+                 int lanes_per_row);
+
+/* ---------------------------------------------------------------- ELL ---
+ * Replaces kernel `ell(val,idx,x,y,int N,int K,__local)` (reference
+ * kernels/Ell.cl:1) and its launch (reference ell.c:47-48,242-248,273).
+ * Column-major, leading dimension `ld` (>= N, multiple of 64), with a
+ * k-interleave `ki` in {1,2}: entry (row i, slot k) lives at
+ *     (k / ki) * ld * ki + i * ki + (k % ki)
+ * so one lane per row reads 8·ki contiguous bytes per step (ki = 2: 16-byte
+ * dwordx4 value loads).  K (a multiple of ki) slots per row; padding slots
+ * hold value 0.0 and a column already used by the row.                   */
+int spmv_ell_run(spmv_dims d, int32_t K, int64_t ld, int32_t ki,
+                 const int32_t *col, const double *val, const double *x,
+                 double *y);
+
+/* -------------------------------------------------------- SELL-C-sigma ---
+ * Replaces kernel `sigma_c(val,idx,x,y,slice_ptr,int C)` (reference
+ * kernels/Sigma_C.cl:1) and its launch (reference sigma_c.c:50-51,71-72,
+ * 280-285,311).  Slices of C rows (C = 64 = one wave by default), rows
+ * sorted by length inside windows of sigma rows (builder only), slice s
+ * occupies [slice_ptr[s], slice_ptr[s+1]) with entry (slot r, k) at
+ *     slice_ptr[s] + (k / ki) * C * ki + r * ki + (k % ki)
+ * perm[s*C + r] is the original row of slot r of slice s (-1 = padding
+ * slot); y[perm[.]] is written directly, no un-permute pass.             */
+int spmv_sell_run(spmv_dims d, int32_t C, int32_t ki, int64_t n_slices,
+                  const int64_t *slice_ptr, const int32_t *perm,
+                  const int32_t *col, const double *val, const double *x,
+                  double *y);
+
+/* --------------------------------------------------------------- CMRS ---
+ * Replaces kernel `cmrs(val,idx,strip_ptr,row_in_strip,x,y,N,h,__local)`
+ * (reference kernels/Cmrs.cl:1) and its launch (reference cmrs.c:51-52,
+ * 195-205,232).  Strips of h consecutive rows (1 <= h <= 64); strip s
+ * holds entries [strip_ptr[s], strip_ptr[s+1]) in row order and
+ * row_in_strip[j] in [0,h) (uint8, the reference used int32).  One wave
+ * per strip: a segmented reduction whose per-row results are gathered in
+ * a per-wave LDS strip buffer and written as h contiguous y values; the
+ * tail strip is bounds-checked (reference Cmrs.cl:38-42 wrote past y).   */
+int spmv_cmrs_run(spmv_dims d, int32_t h, int64_t n_strips,
+                  const int64_t *strip_ptr, const uint8_t *row_in_strip,
+                  const int32_t *col, const double *val, const double *x,
+                  double *y);
+
+/* ------------------------------------------------------------ helpers ---
+ * Device discovery (replaces reference inc/helper_functions.h:76-129),
+ * memory (replaces clCreateBuffer / clEnqueueWriteBuffer /
+ * clEnqueueReadBuffer, reference csr.c:123-127,183-186,220), timing.    */
+int spmv_device_count(int *count);
+int spmv_set_device(int device);
+int spmv_device_name(int device, char *buf, size_t len);
+int spmv_malloc(void **dptr, size_t bytes);
+int spmv_free(void *dptr);
+int spmv_memset(void *dptr, int value, size_t bytes, void *stream);
+int spmv_upload(void *dptr, const void *host, size_t bytes, void *stream);
+int spmv_download(void *host, const void *dptr, size_t bytes, void *stream);
+int spmv_stream_create(void **stream);
+int spmv_stream_destroy(void *stream);
+int spmv_sync(void *stream);
+/* Write `bytes` (0 = 512 MiB) of library-owned scratch on `stream` so the
+ * 256 MiB Infinity Cache and the per-XCD L2s hold no SpMV operand.      */
+int spmv_flush_cache(void *stream, size_t bytes);
+/* Time one launch: record an event, call launch(arg), record an event,
+ * synchronise, return elapsed milliseconds in *ms.                      */
+typedef int (*spmv_launch_fn)(void *arg);
+int spmv_time_launch(spmv_launch_fn launch, void *arg, void *stream,
+                     double *ms);
+/* Frees library-owned scratch on the current device. */
+int spmv_release(void);
+const char *spmv_strerror(int rc);
+const char *spmv_last_error(void);
+/* Version string of the library build, e.g. "spmv-hip 0.1 gfx950". */
+const char *spmv_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SPMV_H */

@@ -1,0 +1,170 @@
+/*
+ * spmv_host.h — host side of the MI355X SpMV suite (libspmv_host.so).
+ *
+ * Replaces the reference's host layers L1-L3:
+ *   - Matrix Market reading with the reference's acceptance semantics
+ *     (reference inc/helper_functions.h:134-165, mmio/mmio.c:96-217,
+ *      entry lines "%d %d %lg", csr.c:81);
+ *   - the per-format builders that the reference interleaves with fscanf
+ *     (reference coo.c:79-84, csr.c:68-91, ell.c:68-164,
+ *      sigma_c.c:71-202, cmrs.c:72-117), re-designed for wave64 layouts
+ *     and without the reference's empty-row / last-row assumptions;
+ *   - the OpenMP CPU loops (reference coo.c:280-300, csr.c:285-309,
+ *     ell.c:357-383, cmrs.c:319-345; the reference has none for SELL);
+ *   - the run-time result check (reference inc/helper_functions.h:184-236);
+ *   - synthetic generators for the configs in BASELINE.json.
+ *
+ * All functions take caller-allocated arrays ("plan" functions return the
+ * sizes to allocate) so the same calls serve the C drivers and ctypes.
+ * Return values are spmv_rc.h codes unless stated otherwise.
+ */
+#ifndef SPMV_HOST_H
+#define SPMV_HOST_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "spmv_rc.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------ Matrix Market ---*/
+typedef struct spmv_mtx_info {
+    int64_t n_rows;
+    int64_t n_cols;
+    int64_t nnz;   /* entries listed in the file (= entries multiplied)   */
+    int symmetric; /* symmetric / skew / hermitian banner: entries are    */
+                   /* taken literally, never mirrored (reference A12)     */
+    int pattern;   /* pattern banner: every entry's value is 1.0          */
+    int integer;   /* integer banner: values parsed as numbers            */
+} spmv_mtx_info;
+
+/* Banner + size line only.  SPMV_FILE_ERROR if the file is missing, the
+ * banner is malformed, or the matrix is complex or dense (array).       */
+int spmv_mtx_read_info(const char *path, spmv_mtx_info *info);
+/* Banner + size + exactly info->nnz entries in FILE ORDER, converted to
+ * 0-based.  row/col/val must hold info->nnz elements (read_info first).
+ * Out-of-range indices or a short file give SPMV_FILE_ERROR.            */
+int spmv_mtx_read(const char *path, spmv_mtx_info *info, int32_t *row,
+                  int32_t *col, double *val);
+/* Writes a coordinate real file with %.17g values (exact round trip).   */
+int spmv_mtx_write(const char *path, int64_t n_rows, int64_t n_cols,
+                   int64_t nnz, const int32_t *row, const int32_t *col,
+                   const double *val, int symmetric);
+
+/* ------------------------------------------------------------ formats ---*/
+/* COO sorted by row, stable (file order kept inside a row).             */
+int spmv_coo_sort_by_row(int64_t n_rows, int64_t nnz, const int32_t *row,
+                         const int32_t *col, const double *val,
+                         int32_t *row_out, int32_t *col_out, double *val_out);
+/* CSR from COO in any order: stable counting sort by row; empty rows ok.
+ * row_ptr[n_rows+1], col_out[nnz], val_out[nnz].                        */
+int spmv_csr_from_coo(int64_t n_rows, int64_t nnz, const int32_t *row,
+                      const int32_t *col, const double *val,
+                      int64_t *row_ptr, int32_t *col_out, double *val_out);
+/* Row-length statistics of a CSR matrix. */
+int spmv_csr_row_stats(int64_t n_rows, const int64_t *row_ptr,
+                       int64_t *min_len, int64_t *max_len, double *mean_len);
+
+/* ELL, column-major with leading dimension ld = round_up(N, 64) and
+ * k-interleave ki (spmv.h).  K = round_up(max row length, ki).
+ * spmv_ell_plan gives K and ld; arrays are ld*K elements.               */
+int spmv_ell_plan(int64_t n_rows, const int64_t *row_ptr, int32_t ki,
+                  int32_t *K, int64_t *ld);
+int spmv_ell_fill(int64_t n_rows, const int64_t *row_ptr, const int32_t *col,
+                  const double *val, int32_t K, int64_t ld, int32_t ki,
+                  int32_t *col_out, double *val_out);
+
+/* SELL-C-sigma: rows sorted by decreasing length inside windows of sigma
+ * rows (sigma = 1: no sorting, the reference's sigma_c.c:48 behaviour;
+ * sigma must be 1 or a multiple of C), slices of C rows, slice width =
+ * round_up(longest row of the slice, ki).  Plan returns n_slices and the
+ * stored element count; perm has n_slices*C entries.                    */
+int spmv_sell_plan(int64_t n_rows, const int64_t *row_ptr, int32_t C,
+                   int32_t sigma, int32_t ki, int64_t *n_slices,
+                   int64_t *stored);
+int spmv_sell_fill(int64_t n_rows, const int64_t *row_ptr, const int32_t *col,
+                   const double *val, int32_t C, int32_t sigma, int32_t ki,
+                   int64_t n_slices, int64_t *slice_ptr, int32_t *perm,
+                   int32_t *col_out, double *val_out);
+
+/* CMRS: strips of h rows (1..64), n_strips = ceil(N/h).  The CSR arrays
+ * are reused unchanged; this builds strip_ptr[n_strips+1] and
+ * row_in_strip[nnz].                                                    */
+int spmv_cmrs_build(int64_t n_rows, const int64_t *row_ptr, int32_t h,
+                    int64_t *strip_ptr, uint8_t *row_in_strip);
+
+/* ---------------------------------------------------------- CPU loops ---
+ * OpenMP restatements of the reference's compute_using_cpu loops, with
+ * zero-initialised output (the reference accumulated into malloc'd
+ * memory, reference csr.c:102).  `threads` <= 0 uses omp_get_max_threads.
+ * They are the CPU baseline the drivers print, never a device fallback. */
+int spmv_cpu_coo(int64_t n_rows, int64_t nnz, const int32_t *row,
+                 const int32_t *col, const double *val, const double *x,
+                 double *y, int threads);
+int spmv_cpu_csr(int64_t n_rows, const int64_t *row_ptr, const int32_t *col,
+                 const double *val, const double *x, double *y, int threads);
+int spmv_cpu_ell(int64_t n_rows, int32_t K, int64_t ld, int32_t ki,
+                 const int32_t *col, const double *val, const double *x,
+                 double *y, int threads);
+int spmv_cpu_sell(int64_t n_rows, int32_t C, int32_t ki, int64_t n_slices,
+                  const int64_t *slice_ptr, const int32_t *perm,
+                  const int32_t *col, const double *val, const double *x,
+                  double *y, int threads);
+int spmv_cpu_cmrs(int64_t n_rows, int32_t h, int64_t n_strips,
+                  const int64_t *strip_ptr, const uint8_t *row_in_strip,
+                  const int32_t *col, const double *val, const double *x,
+                  double *y, int threads);
+int spmv_cpu_threads(void);
+
+/* ------------------------------------------------------ result check ---
+ * The reference's check_result (inc/helper_functions.h:184-236): y_ref
+ * is accumulated sequentially in FILE ORDER.  Returns the number of rows
+ * that fail; *first_bad gets the first failing row (-1 if none).
+ * abs_tol > 0: the reference's |y - y_ref| <= 1e-6 rule;
+ * rel_tol > 0: |y - y_ref| <= rel_tol * max(|y_ref|, sum_j |a_ij x_j|).  */
+int64_t spmv_check(int64_t n_rows, int64_t nnz, const int32_t *row,
+                   const int32_t *col, const double *val, const double *x,
+                   const double *y, double abs_tol, double rel_tol,
+                   int64_t *first_bad, double *y_ref_at_bad);
+
+/* --------------------------------------------------------- generators ---
+ * Deterministic (splitmix64 counter-based), identical on every host.
+ *
+ * cant-like stand-in for SuiteSparse cant (N = M = 62,451 = 3 dof x
+ * 9x9x257 nodes, 27-node neighbourhood).  The pattern is thinned
+ * symmetrically to exactly 4,007,383 entries (2,034,917 in the lower
+ * triangle incl. diagonal) — the real cant's counts.  mode:
+ *   0 = full pattern, row-major order          ("cant-sorted" shape)
+ *   1 = full pattern, column-major order       ("cant" shape)
+ *   2 = lower triangle only, column-major order (SuiteSparse storage;
+ *       banner symmetric — the reference multiplies it literally)
+ * `copies` > 1 stacks that many independent copies block-diagonally.
+ * Call with row == NULL to get *nnz only.                              */
+int spmv_gen_cantlike(int mode, int64_t copies, int64_t *n_rows,
+                      int64_t *nnz, int32_t *row, int32_t *col, double *val);
+/* R-MAT (a,b,c,d) = (0.57,0.19,0.19,0.05) on 2^scale ids, rejection to
+ * [0,n); exactly nnz entries, duplicates kept; values uniform [-1,1).
+ * Entries in generation order.                                         */
+int spmv_gen_rmat(int64_t n, int64_t nnz, int scale, uint64_t seed,
+                  int32_t *row, int32_t *col, double *val);
+/* Banded: row i has 16 entries at columns (i + o) mod n, o in -8..7,
+ * directly in CSR form (row_ptr[n+1], col[16n], val[16n]).             */
+int spmv_gen_banded_csr(int64_t n, uint64_t seed, int64_t row_begin,
+                        int64_t row_end, int64_t *row_ptr, int32_t *col,
+                        double *val);
+/* Uniformly random sparse matrix with row lengths in [min_len,max_len]
+ * (test helper for ragged inputs), CSR order.                          */
+int spmv_gen_random(int64_t n_rows, int64_t n_cols, int64_t min_len,
+                    int64_t max_len, uint64_t seed, int64_t *nnz,
+                    int32_t *row, int32_t *col, double *val);
+/* splitmix64 of (seed, index), exported for tests. */
+uint64_t spmv_splitmix64(uint64_t seed, uint64_t index);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SPMV_HOST_H */

@@ -1,0 +1,73 @@
+// common.h — shared device helpers and launch plumbing for the gfx950
+// SpMV kernels (see include/spmv.h for the C-ABI they implement).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "spmv.h"
+
+namespace spmv {
+
+constexpr int kWave = 64;    // CDNA wavefront width
+constexpr int kBlock = 256;  // 4 waves per workgroup for every kernel
+
+// ---------------------------------------------------------------- errors
+int fail(int rc, const char *where, hipError_t e);
+int fail_msg(int rc, const char *msg);
+
+// Sets the device for the duration of one C-ABI call and restores the
+// caller's device afterwards.
+class DeviceGuard {
+  public:
+    explicit DeviceGuard(int dev);
+    ~DeviceGuard();
+    int rc() const { return rc_; }
+
+  private:
+    int prev_ = -1;
+    int rc_ = SPMV_SUCCESS;
+};
+
+// Blocks per XCD remap switch (SPMV_XCD_REMAP=0 disables; read once).
+bool xcd_remap_enabled();
+
+// ------------------------------------------------------- device helpers
+// Bijective blockIdx remap: blocks b and b+8 are dealt to the same XCD
+// (MI355X_MICROARCH.md §Workgroup dispatch), so give each such group a
+// CONTIGUOUS range of logical blocks.  Neighbouring rows/slices then read
+// neighbouring x entries through one XCD's L2.  Placement only changes
+// speed, never results.
+__device__ __forceinline__ int64_t xcd_block(int remap)
+{
+    const int64_t b = blockIdx.x;
+    if (!remap)
+        return b;
+    const int64_t nb = gridDim.x;
+    const int64_t q = nb >> 3, r = nb & 7;
+    const int64_t xcd = b & 7, idx = b >> 3;
+    return xcd < r ? xcd * (q + 1) + idx : r * (q + 1) + (xcd - r) * q + idx;
+}
+
+template <int W>
+__device__ __forceinline__ double group_sum(double v)
+{
+#pragma unroll
+    for (int off = W / 2; off > 0; off >>= 1)
+        v += __shfl_xor(v, off, W);
+    return v;
+}
+
+}  // namespace spmv
+
+#define SPMV_CHECK_LAUNCH(where)                                              \
+    do {                                                                      \
+        hipError_t e_ = hipGetLastError();                                    \
+        if (e_ != hipSuccess)                                                 \
+            return ::spmv::fail(SPMV_PROGRAM_ERROR, where, e_);              \
+    } while (0)
+
+#define SPMV_GUARD(dims)                                                      \
+    ::spmv::DeviceGuard guard_((dims).device);                                \
+    if (guard_.rc() != SPMV_SUCCESS)                                          \
+        return guard_.rc()

@@ -1,0 +1,253 @@
+// coo.hip — atomic-free COO SpMV and CMRS SpMV for gfx950.
+//
+// COO replaces the reference's coo kernel (reference kernels/Coo.cl:4-32:
+// one work-item per entry, fp64 add built from a 64-bit compare-and-swap
+// retry loop, y assumed pre-zeroed).  Entries are sorted by row on the
+// host (spmv_coo_sort_by_row), then:
+//   pass 1  each wave owns a tile of kTile consecutive entries.  Per
+//           64-entry step it forms the products, runs a wave-wide
+//           segmented inclusive scan keyed by row (6 shuffle steps), and
+//           the last lane of every finished row segment stores y[row].
+//           A row running past the step is carried in registers.  A row
+//           that began in an EARLIER tile is not stored: its partial sum
+//           goes to carry[tile].  Rows with no entries get 0.0 from the
+//           tile that holds the next non-empty row (and the last tile).
+//   pass 2  one thread per tile: the first tile of every run of carries
+//           for the same row adds the run, in tile order, to y[row].
+// No atomics, every y element written by exactly one pass-1 store (plus
+// at most one pass-2 update): results are bitwise reproducible.
+//
+// CMRS replaces the reference's cmrs kernel (reference kernels/Cmrs.cl:
+// 1-46: per-lane private LDS row vectors of h doubles, three barriers
+// per strip, uninitialised LDS on the first strip, and an out-of-bounds
+// y store in the tail strip).  Here one wave owns one strip: the same
+// segmented scan keyed by row_in_strip reduces each 64-entry step, the
+// segment tails add into a per-wave LDS strip accumulator of h doubles
+// (zeroed first; keys are sorted so the tails of one step hit distinct
+// slots), and lanes 0..h-1 store the strip's h contiguous y values,
+// bounds-checked.  No barrier: each wave only touches its own LDS slots.
+#include <limits.h>
+
+#include "common.h"
+
+namespace spmv {
+
+constexpr int kCooIter = 16;                  // 64-entry steps per tile
+constexpr int64_t kTile = kWave * kCooIter;  // entries per wave
+
+// Inclusive segmented scan over one wave; `key` is non-decreasing across
+// lanes, so lane l - off having the same key means every lane between
+// does too.
+template <typename K>
+__device__ __forceinline__ double seg_scan(double p, K key, int lane)
+{
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+        const double pu = __shfl_up(p, off, kWave);
+        const K ku = __shfl_up(key, off, kWave);
+        if (lane >= off && ku == key)
+            p += pu;
+    }
+    return p;
+}
+
+__global__ __launch_bounds__(kBlock) void coo_tile_kernel(
+    int64_t n_rows, int64_t nnz, int64_t n_tiles,
+    const int32_t *__restrict__ row, const int32_t *__restrict__ col,
+    const double *__restrict__ val, const double *__restrict__ x,
+    double *__restrict__ y, int32_t *__restrict__ carry_row,
+    double *__restrict__ carry_val, int remap)
+{
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t tile = xcd_block(remap) * (kBlock / kWave) + (threadIdx.x >> 6);
+    if (tile >= n_tiles)
+        return;
+    const int64_t t0 = tile * kTile;
+    const int64_t t1 = t0 + kTile < nnz ? t0 + kTile : nnz;
+    const int32_t first_row = row[t0];
+    const int32_t before = t0 > 0 ? row[t0 - 1] : -1;
+    const bool first_continues = before == first_row;
+
+    double run = 0.0;      // wave-uniform running sum of row `run_row`
+    int32_t run_row = -1;
+    double pref = 0.0;     // this lane's share of a continued first row
+
+    for (int it = 0; it < kCooIter; ++it) {
+        const int64_t j0 = t0 + (int64_t)it * kWave;
+        if (j0 >= t1)
+            break;
+        const int64_t j = j0 + lane;
+        const int nvalid = (int)(t1 - j0 < kWave ? t1 - j0 : kWave);
+        const bool valid = lane < nvalid;
+        const int32_t r = valid ? row[j] : INT_MAX;
+        double p = valid ? val[j] * x[col[j]] : 0.0;
+
+        // The row carried from the previous step is finished unless this
+        // step starts with the same row.
+        const int32_t r0 = __shfl(r, 0, kWave);
+        if (lane == 0 && run_row >= 0 && r0 != run_row &&
+            !(first_continues && run_row == first_row))
+            y[run_row] = run;
+
+        // Rows strictly between the previous entry's row and r are empty.
+        int32_t rp = __shfl_up(r, 1, kWave);
+        if (lane == 0)
+            rp = j0 > 0 ? row[j0 - 1] : -1;
+        if (valid)
+            for (int32_t g = rp + 1; g < r; ++g)
+                y[g] = 0.0;
+
+        if (first_continues && r == first_row) {
+            pref += p;  // goes to the carry, not through the scan
+            p = 0.0;
+        }
+        p = seg_scan(p, r, lane);
+        if (r == run_row)
+            p += run;
+        const int32_t rn = __shfl_down(r, 1, kWave);
+        const bool tail = valid && lane < nvalid - 1 && rn != r;
+        if (tail && !(first_continues && r == first_row))
+            y[r] = p;
+        run_row = __shfl(r, nvalid - 1, kWave);
+        run = __shfl(p, nvalid - 1, kWave);
+    }
+    if (lane == 0 && run_row >= 0 && !(first_continues && run_row == first_row))
+        y[run_row] = run;
+
+    // trailing empty rows after the last entry of the matrix
+    if (t1 == nnz) {
+        const int32_t last = row[nnz - 1];
+        for (int64_t g = (int64_t)last + 1 + lane; g < n_rows; g += kWave)
+            y[g] = 0.0;
+    }
+
+    pref = group_sum<kWave>(pref);
+    if (lane == 0) {
+        carry_row[tile] = first_continues ? first_row : -1;
+        carry_val[tile] = pref;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void coo_carry_kernel(
+    int64_t n_tiles, const int32_t *__restrict__ carry_row,
+    const double *__restrict__ carry_val, double *__restrict__ y)
+{
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= n_tiles)
+        return;
+    const int32_t r = carry_row[t];
+    if (r < 0 || (t > 0 && carry_row[t - 1] == r))
+        return;  // not a carry, or not the head of its run
+    double s = 0.0;
+    for (int64_t u = t; u < n_tiles && carry_row[u] == r; ++u)
+        s += carry_val[u];
+    y[r] += s;
+}
+
+// ------------------------------------------------------------------ CMRS
+__global__ __launch_bounds__(kBlock) void cmrs_kernel(
+    int64_t n_rows, int32_t h, int64_t n_strips,
+    const int64_t *__restrict__ strip_ptr,
+    const uint8_t *__restrict__ row_in_strip,
+    const int32_t *__restrict__ col, const double *__restrict__ val,
+    const double *__restrict__ x, double *__restrict__ y, int remap)
+{
+    __shared__ double s_acc[kBlock / kWave][kWave];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int w = threadIdx.x >> 6;
+    const int64_t s = xcd_block(remap) * (kBlock / kWave) + w;
+    if (s >= n_strips)
+        return;
+    double *acc = s_acc[w];
+    acc[lane] = 0.0;
+    __builtin_amdgcn_wave_barrier();
+
+    const int64_t beg = strip_ptr[s], end = strip_ptr[s + 1];
+    for (int64_t j0 = beg; j0 < end; j0 += kWave) {
+        const int64_t j = j0 + lane;
+        const int nvalid = (int)(end - j0 < kWave ? end - j0 : kWave);
+        const bool valid = lane < nvalid;
+        const int key = valid ? (int)row_in_strip[j] : INT_MAX;
+        double p = valid ? val[j] * x[col[j]] : 0.0;
+        p = seg_scan(p, key, lane);
+        const int kn = __shfl_down(key, 1, kWave);
+        const bool tail = valid && (lane == nvalid - 1 || kn != key);
+        if (tail)
+            acc[key] += p;  // distinct keys per step: no two tails collide
+        __builtin_amdgcn_wave_barrier();
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (lane < h) {
+        const int64_t r = s * h + lane;
+        if (r < n_rows)  // reference Cmrs.cl:38-42 stored past y here
+            y[r] = acc[lane];
+    }
+}
+
+}  // namespace spmv
+
+using namespace spmv;
+
+extern "C" size_t spmv_coo_ws_bytes(int64_t nnz)
+{
+    const int64_t tiles = nnz > 0 ? (nnz + kTile - 1) / kTile : 0;
+    // carry_val (8-byte aligned) first, then carry_row
+    return (size_t)(tiles * (int64_t)sizeof(double) + tiles * (int64_t)sizeof(int32_t) + 16);
+}
+
+extern "C" int spmv_coo_run(spmv_dims d, const int32_t *row,
+                            const int32_t *col, const double *val,
+                            const double *x, double *y, void *ws,
+                            size_t ws_bytes)
+{
+    if (d.n_rows < 0 || d.nnz < 0 || d.n_rows > INT32_MAX)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_coo_run: bad sizes");
+    if (d.n_rows == 0)
+        return SPMV_SUCCESS;
+    SPMV_GUARD(d);
+    if (d.nnz == 0) {
+        hipError_t e = hipMemsetAsync(y, 0, (size_t)d.n_rows * sizeof(double),
+                                      (hipStream_t)d.stream);
+        return e == hipSuccess ? SPMV_SUCCESS : fail(SPMV_PROGRAM_ERROR, "memset y", e);
+    }
+    if (!ws || ws_bytes < spmv_coo_ws_bytes(d.nnz))
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_coo_run: workspace too small");
+    const int64_t tiles = (d.nnz + kTile - 1) / kTile;
+    double *carry_val = (double *)ws;
+    int32_t *carry_row = (int32_t *)(carry_val + tiles);
+    const int64_t blocks = (tiles + (kBlock / kWave) - 1) / (kBlock / kWave);
+    if (blocks > INT32_MAX)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_coo_run: grid too large");
+    hipLaunchKernelGGL(coo_tile_kernel, dim3((unsigned)blocks), dim3(kBlock), 0,
+                       (hipStream_t)d.stream, d.n_rows, d.nnz, tiles, row, col,
+                       val, x, y, carry_row, carry_val,
+                       xcd_remap_enabled() ? 1 : 0);
+    SPMV_CHECK_LAUNCH("coo_tile_kernel");
+    const int64_t cblocks = (tiles + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL(coo_carry_kernel, dim3((unsigned)cblocks), dim3(kBlock), 0,
+                       (hipStream_t)d.stream, tiles, carry_row, carry_val, y);
+    SPMV_CHECK_LAUNCH("coo_carry_kernel");
+    return SPMV_SUCCESS;
+}
+
+extern "C" int spmv_cmrs_run(spmv_dims d, int32_t h, int64_t n_strips,
+                             const int64_t *strip_ptr,
+                             const uint8_t *row_in_strip, const int32_t *col,
+                             const double *val, const double *x, double *y)
+{
+    if (d.n_rows < 0 || h < 1 || h > 64)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_cmrs_run: h must be in [1,64]");
+    if (n_strips != (d.n_rows + h - 1) / h)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_cmrs_run: n_strips != ceil(N/h)");
+    if (d.n_rows == 0)
+        return SPMV_SUCCESS;
+    SPMV_GUARD(d);
+    const int64_t blocks = (n_strips + (kBlock / kWave) - 1) / (kBlock / kWave);
+    if (blocks > INT32_MAX)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_cmrs_run: grid too large");
+    hipLaunchKernelGGL(cmrs_kernel, dim3((unsigned)blocks), dim3(kBlock), 0,
+                       (hipStream_t)d.stream, d.n_rows, h, n_strips, strip_ptr,
+                       row_in_strip, col, val, x, y, xcd_remap_enabled() ? 1 : 0);
+    SPMV_CHECK_LAUNCH("cmrs_kernel");
+    return SPMV_SUCCESS;
+}

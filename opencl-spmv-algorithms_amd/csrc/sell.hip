@@ -1,0 +1,162 @@
+// sell.hip — SELL-C-sigma and ELL SpMV for gfx950.
+//
+// SELL replaces the reference's sigma_c kernel (reference
+// kernels/Sigma_C.cl:1-18: 32-lane work-groups = half a wave64, no row
+// sorting, y padded to the slice count).  ELL replaces the reference's
+// ell kernel (reference kernels/Ell.cl:1-39: 16 lanes per row over a
+// ROW-major N x K array, then an LDS barrier tree).
+//
+// Both are "one lane per row, column-major slots": at every step the C
+// lanes of a slice (or all lanes, for ELL) read C consecutive values, so a
+// wave issues one fully coalesced 512-byte (ki = 1) or 1 KiB (ki = 2,
+// dwordx4) value load and the matching column load.  No reduction, no
+// LDS, no barrier.  SELL writes y[perm[slot]] directly (the sigma-sort is
+// undone in the store, not in an extra pass).
+// Bytes per slice step: C·ki·(8 + 4) + x gathers; padding slots are
+// loaded (that is the format's cost) but re-use the row's own column.
+#include "common.h"
+
+namespace spmv {
+
+template <int KI>
+struct Step;
+
+template <>
+struct Step<1> {
+    static __device__ __forceinline__ double fma(const double *vp,
+                                                 const int32_t *cp,
+                                                 const double *__restrict__ x,
+                                                 double acc)
+    {
+        return acc + vp[0] * x[cp[0]];
+    }
+};
+
+template <>
+struct Step<2> {
+    static __device__ __forceinline__ double fma(const double *vp,
+                                                 const int32_t *cp,
+                                                 const double *__restrict__ x,
+                                                 double acc)
+    {
+        const double2 v = *reinterpret_cast<const double2 *>(vp);
+        const int2 c = *reinterpret_cast<const int2 *>(cp);
+        return acc + v.x * x[c.x] + v.y * x[c.y];
+    }
+};
+
+// Slot-per-lane loop over `w` slots (a multiple of KI) with stride
+// `step` elements between consecutive KI-groups; 4 groups in flight.
+template <int KI>
+__device__ __forceinline__ double slot_dot(const double *__restrict__ vp,
+                                           const int32_t *__restrict__ cp,
+                                           int64_t w, int64_t step,
+                                           const double *__restrict__ x)
+{
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    const int64_t groups = w / KI;
+    int64_t g = 0;
+    for (; g + 4 <= groups; g += 4) {
+        a0 = Step<KI>::fma(vp + (g + 0) * step, cp + (g + 0) * step, x, a0);
+        a1 = Step<KI>::fma(vp + (g + 1) * step, cp + (g + 1) * step, x, a1);
+        a2 = Step<KI>::fma(vp + (g + 2) * step, cp + (g + 2) * step, x, a2);
+        a3 = Step<KI>::fma(vp + (g + 3) * step, cp + (g + 3) * step, x, a3);
+    }
+    for (; g < groups; ++g)
+        a0 = Step<KI>::fma(vp + g * step, cp + g * step, x, a0);
+    return (a0 + a1) + (a2 + a3);
+}
+
+template <int KI>
+__global__ __launch_bounds__(kBlock) void sell_kernel(
+    int32_t C, int64_t n_slices, const int64_t *__restrict__ slice_ptr,
+    const int32_t *__restrict__ perm, const int32_t *__restrict__ col,
+    const double *__restrict__ val, const double *__restrict__ x,
+    double *__restrict__ y, int remap)
+{
+    const int64_t slot = xcd_block(remap) * kBlock + threadIdx.x;
+    const int64_t s = slot / C;
+    if (s >= n_slices)
+        return;
+    const int64_t r = slot - s * C;
+    const int64_t base = slice_ptr[s];
+    const int64_t w = (slice_ptr[s + 1] - base) / C;
+    const int64_t off = base + r * KI;
+    const double sum = slot_dot<KI>(val + off, col + off, w, (int64_t)C * KI, x);
+    const int32_t row = perm[slot];
+    if (row >= 0)
+        y[row] = sum;
+}
+
+template <int KI>
+__global__ __launch_bounds__(kBlock) void ell_kernel(
+    int64_t n_rows, int32_t K, int64_t ld, const int32_t *__restrict__ col,
+    const double *__restrict__ val, const double *__restrict__ x,
+    double *__restrict__ y, int remap)
+{
+    const int64_t i = xcd_block(remap) * kBlock + threadIdx.x;
+    if (i >= n_rows)
+        return;
+    const int64_t off = i * KI;
+    y[i] = slot_dot<KI>(val + off, col + off, K, ld * KI, x);
+}
+
+}  // namespace spmv
+
+using namespace spmv;
+
+extern "C" int spmv_sell_run(spmv_dims d, int32_t C, int32_t ki,
+                             int64_t n_slices, const int64_t *slice_ptr,
+                             const int32_t *perm, const int32_t *col,
+                             const double *val, const double *x, double *y)
+{
+    if (d.n_rows < 0 || C <= 0 || C > 1024 || n_slices < 0)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_run: bad C / sizes");
+    if (ki != 1 && ki != 2)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_run: ki must be 1 or 2");
+    if (n_slices * C < d.n_rows)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_run: n_slices*C < n_rows");
+    if (d.n_rows == 0 || n_slices == 0)
+        return SPMV_SUCCESS;
+    SPMV_GUARD(d);
+    const int64_t slots = n_slices * C;
+    const int64_t blocks = (slots + kBlock - 1) / kBlock;
+    if (blocks > INT32_MAX)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_run: grid too large");
+    const int remap = xcd_remap_enabled() ? 1 : 0;
+    if (ki == 2)
+        hipLaunchKernelGGL(sell_kernel<2>, dim3((unsigned)blocks), dim3(kBlock), 0,
+                           (hipStream_t)d.stream, C, n_slices, slice_ptr, perm,
+                           col, val, x, y, remap);
+    else
+        hipLaunchKernelGGL(sell_kernel<1>, dim3((unsigned)blocks), dim3(kBlock), 0,
+                           (hipStream_t)d.stream, C, n_slices, slice_ptr, perm,
+                           col, val, x, y, remap);
+    SPMV_CHECK_LAUNCH("sell_kernel");
+    return SPMV_SUCCESS;
+}
+
+extern "C" int spmv_ell_run(spmv_dims d, int32_t K, int64_t ld, int32_t ki,
+                            const int32_t *col, const double *val,
+                            const double *x, double *y)
+{
+    if (d.n_rows < 0 || K < 0 || ld < d.n_rows || ld % 64 != 0)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_ell_run: bad K / ld");
+    if ((ki != 1 && ki != 2) || K % ki != 0)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_ell_run: ki must be 1 or 2 and divide K");
+    if (d.n_rows == 0)
+        return SPMV_SUCCESS;
+    SPMV_GUARD(d);
+    const int64_t blocks = (d.n_rows + kBlock - 1) / kBlock;
+    const int remap = xcd_remap_enabled() ? 1 : 0;
+    if (ki == 2)
+        hipLaunchKernelGGL(ell_kernel<2>, dim3((unsigned)blocks), dim3(kBlock), 0,
+                           (hipStream_t)d.stream, d.n_rows, K, ld, col, val, x, y,
+                           remap);
+    else
+        hipLaunchKernelGGL(ell_kernel<1>, dim3((unsigned)blocks), dim3(kBlock), 0,
+                           (hipStream_t)d.stream, d.n_rows, K, ld, col, val, x, y,
+                           remap);
+    SPMV_CHECK_LAUNCH("ell_kernel");
+    return SPMV_SUCCESS;
+}

@@ -1,0 +1,4 @@
+/* ./bin/cmrs — see driver.c; replaces the reference's cmrs.c main(). */
+#include "driver.h"
+
+int main(int argc, char **argv) { return spmv_driver_main(argc, argv, FMT_CMRS); }

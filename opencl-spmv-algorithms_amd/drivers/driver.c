@@ -1,0 +1,524 @@
+/*
+ * driver.c — the per-format SpMV programs (./bin/coo, csr, ell, sigma_c,
+ * cmrs), drop-in replacements of the reference's drivers
+ * (reference coo.c, csr.c, ell.c, sigma_c.c, cmrs.c: main()).
+ *
+ * With no arguments a program behaves like the reference one: it reads
+ * databases/cant.mtx (coo, reference coo.c:43) or
+ * databases/cant-sorted.mtx (the others, reference csr.c:43), uses
+ * x[j] = j (reference csr.c:95-99), runs the kernel, prints the
+ * reference's lines (reference inc/helper_functions.h:167-182, the COO
+ * "GPU calculations" line coo.c:201, ELL's row statistics ell.c:104),
+ * checks the device result against the file-order sum ("result is ok",
+ * reference csr.c:229-236), then times the OpenMP CPU loop and checks it
+ * ("cpu result is ok", reference csr.c:244-255; none for sigma_c, like
+ * the reference).  Exit codes are the reference's (inc/enums.h).
+ *
+ * Differences, all deliberate:
+ *   - the time is the median of --reps hipEvent-timed launches, each after
+ *     a 512 MiB cache flush (cold HBM; --warm skips the flush), instead of
+ *     one cold launch under a host wall clock (reference csr.c:198-206);
+ *   - extra lines after the reference's: algorithmic bytes, effective GB/s,
+ *     fraction of the 8 TB/s HBM3E roofline, stored bytes of the format;
+ *   - the check uses the suite's 1e-6 relative criterion and also reports
+ *     the reference's absolute 1e-6 rule;
+ *   - --strict turns a failed check into exit code 4 (the reference always
+ *     returns Success, reference csr.c:282).
+ * Options: --matrix PATH  --gen cantlike[0|1|2]|rmat|banded|random
+ *          --copies B  --reps N  --warmup W  --warm  --device D
+ *          --C C --sigma S --ki K --h H --lanes L  --threads T
+ *          --cpu / --no-cpu  --strict  --write-mtx PATH  --help
+ */
+#define _POSIX_C_SOURCE 200809L
+#include <errno.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "driver.h"
+#include "spmv.h"
+#include "spmv_host.h"
+
+#define HBM_PEAK_GBS 8000.0
+
+typedef struct {
+    const char *matrix;
+    const char *gen;
+    const char *write_mtx;
+    int64_t copies;
+    int reps, warmup, warm, device, C, sigma, ki, h, lanes, threads, cpu, strict;
+} opts_t;
+
+static void usage(const char *prog)
+{
+    printf("usage: %s [--matrix PATH | --gen cantlike[0|1|2]|rmat|banded|random]\n"
+           "          [--copies B] [--reps N] [--warmup W] [--warm] [--device D]\n"
+           "          [--C C] [--sigma S] [--ki 1|2] [--h H] [--lanes L]\n"
+           "          [--threads T] [--cpu|--no-cpu] [--strict] [--write-mtx PATH]\n",
+           prog);
+}
+
+static int parse_opts(int argc, char **argv, spmv_format fmt, opts_t *o)
+{
+    memset(o, 0, sizeof *o);
+    o->matrix = fmt == FMT_COO ? "databases/cant.mtx" : "databases/cant-sorted.mtx";
+    o->copies = 1;
+    o->reps = 50;
+    o->warmup = 5;
+    o->C = 64;
+    o->sigma = 1024;
+    o->ki = 2;
+    o->h = 8;
+    o->cpu = fmt != FMT_SELL;
+    for (int i = 1; i < argc; ++i) {
+        const char *a = argv[i];
+        const char *v = i + 1 < argc ? argv[i + 1] : NULL;
+#define NEEDV()                                                               \
+    do {                                                                      \
+        if (!v) {                                                             \
+            fprintf(stderr, "%s needs a value\n", a);                        \
+            return SPMV_OTHER_ERROR;                                          \
+        }                                                                     \
+        ++i;                                                                  \
+    } while (0)
+        if (!strcmp(a, "--matrix")) { NEEDV(); o->matrix = v; }
+        else if (!strcmp(a, "--gen")) { NEEDV(); o->gen = v; }
+        else if (!strcmp(a, "--write-mtx")) { NEEDV(); o->write_mtx = v; }
+        else if (!strcmp(a, "--copies")) { NEEDV(); o->copies = atoll(v); }
+        else if (!strcmp(a, "--reps")) { NEEDV(); o->reps = atoi(v); }
+        else if (!strcmp(a, "--warmup")) { NEEDV(); o->warmup = atoi(v); }
+        else if (!strcmp(a, "--device")) { NEEDV(); o->device = atoi(v); }
+        else if (!strcmp(a, "--C")) { NEEDV(); o->C = atoi(v); }
+        else if (!strcmp(a, "--sigma")) { NEEDV(); o->sigma = atoi(v); }
+        else if (!strcmp(a, "--ki")) { NEEDV(); o->ki = atoi(v); }
+        else if (!strcmp(a, "--h")) { NEEDV(); o->h = atoi(v); }
+        else if (!strcmp(a, "--lanes")) { NEEDV(); o->lanes = atoi(v); }
+        else if (!strcmp(a, "--threads")) { NEEDV(); o->threads = atoi(v); }
+        else if (!strcmp(a, "--warm")) o->warm = 1;
+        else if (!strcmp(a, "--cpu")) o->cpu = 1;
+        else if (!strcmp(a, "--no-cpu")) o->cpu = 0;
+        else if (!strcmp(a, "--strict")) o->strict = 1;
+        else if (!strcmp(a, "--help") || !strcmp(a, "-h")) { usage(argv[0]); exit(0); }
+        else {
+            fprintf(stderr, "unknown option %s\n", a);
+            usage(argv[0]);
+            return SPMV_OTHER_ERROR;
+        }
+#undef NEEDV
+    }
+    if (o->reps < 1 || o->warmup < 0 || o->copies < 1 || (o->ki != 1 && o->ki != 2) ||
+        o->h < 1 || o->h > 64 || o->C < 1 || o->C > 1024)
+        return SPMV_OTHER_ERROR;
+    return SPMV_SUCCESS;
+}
+
+/* ------------------------------------------------------------- input */
+
+typedef struct {
+    int64_t n_rows, n_cols, nnz;
+    int32_t *row, *col;
+    double *val;
+    const char *label;
+} coo_t;
+
+static int load_input(const opts_t *o, spmv_format fmt, coo_t *m)
+{
+    memset(m, 0, sizeof *m);
+    if (!o->gen) {
+        spmv_mtx_info info;
+        int rc = spmv_mtx_read_info(o->matrix, &info);
+        if (rc != SPMV_SUCCESS) {
+            if (errno)
+                perror(o->matrix); /* reference csr.c:56 */
+            else
+                printf("Could not process Matrix Market file %s.\n", o->matrix);
+            return SPMV_FILE_ERROR;
+        }
+        m->n_rows = info.n_rows;
+        m->n_cols = info.n_cols;
+        m->nnz = info.nnz;
+        m->row = malloc((size_t)(m->nnz + 1) * sizeof(int32_t));
+        m->col = malloc((size_t)(m->nnz + 1) * sizeof(int32_t));
+        m->val = malloc((size_t)(m->nnz + 1) * sizeof(double));
+        if (!m->row || !m->col || !m->val)
+            return SPMV_OTHER_ERROR;
+        if (spmv_mtx_read(o->matrix, &info, m->row, m->col, m->val) != SPMV_SUCCESS) {
+            printf("Could not read the entries of %s.\n", o->matrix);
+            return SPMV_FILE_ERROR;
+        }
+        m->label = o->matrix;
+        return SPMV_SUCCESS;
+    }
+    int rc = SPMV_OTHER_ERROR;
+    if (!strncmp(o->gen, "cantlike", 8)) {
+        /* coo reads the column-major file, the others the row-sorted one */
+        int mode = o->gen[8] ? atoi(o->gen + 8) : (fmt == FMT_COO ? 1 : 0);
+        rc = spmv_gen_cantlike(mode, o->copies, &m->n_rows, &m->nnz, NULL, NULL, NULL);
+        if (rc)
+            return rc;
+        m->row = malloc((size_t)m->nnz * sizeof(int32_t));
+        m->col = malloc((size_t)m->nnz * sizeof(int32_t));
+        m->val = malloc((size_t)m->nnz * sizeof(double));
+        rc = spmv_gen_cantlike(mode, o->copies, &m->n_rows, &m->nnz, m->row, m->col, m->val);
+        m->n_cols = m->n_rows;
+        m->label = "cant-like stand-in (synthetic; real cant.mtx is an LFS pointer)";
+    } else if (!strcmp(o->gen, "rmat")) {
+        m->n_rows = m->n_cols = 10000000;
+        m->nnz = 100000000;
+        m->row = malloc((size_t)m->nnz * sizeof(int32_t));
+        m->col = malloc((size_t)m->nnz * sizeof(int32_t));
+        m->val = malloc((size_t)m->nnz * sizeof(double));
+        rc = spmv_gen_rmat(m->n_rows, m->nnz, 24, 1, m->row, m->col, m->val);
+        m->label = "R-MAT 1e7 x 1e7, 1e8 entries (synthetic)";
+    } else if (!strcmp(o->gen, "random")) {
+        m->n_rows = m->n_cols = 100000;
+        rc = spmv_gen_random(m->n_rows, m->n_cols, 0, 64, 3, &m->nnz, NULL, NULL, NULL);
+        m->row = malloc((size_t)m->nnz * sizeof(int32_t));
+        m->col = malloc((size_t)m->nnz * sizeof(int32_t));
+        m->val = malloc((size_t)m->nnz * sizeof(double));
+        rc = spmv_gen_random(m->n_rows, m->n_cols, 0, 64, 3, &m->nnz, m->row, m->col, m->val);
+        m->label = "random ragged 1e5 x 1e5 (synthetic)";
+    } else {
+        fprintf(stderr, "unknown generator %s\n", o->gen);
+    }
+    return rc;
+}
+
+/* ----------------------------------------------------- device format */
+
+typedef struct {
+    spmv_format fmt;
+    spmv_dims d;
+    /* device arrays (unused ones stay NULL) */
+    int64_t *d_ptr;   /* CSR row_ptr / SELL slice_ptr / CMRS strip_ptr */
+    int32_t *d_row, *d_col, *d_perm;
+    uint8_t *d_rin;
+    double *d_val, *d_x, *d_y;
+    void *d_ws;
+    size_t ws_bytes;
+    int32_t K, C, ki, h, lanes;
+    int64_t ld, n_slices, n_strips;
+    /* host copies for the CPU loop */
+    int64_t *h_ptr;
+    int32_t *h_row, *h_col, *h_perm;
+    uint8_t *h_rin;
+    double *h_val;
+    int64_t stored; /* stored entries (incl. padding) */
+    size_t stored_bytes;
+} dev_fmt_t;
+
+static int upload(void **dst, const void *src, size_t bytes, void *stream)
+{
+    int rc = spmv_malloc(dst, bytes);
+    if (rc == SPMV_SUCCESS)
+        rc = spmv_upload(*dst, src, bytes, stream);
+    return rc;
+}
+
+static int build_format(const opts_t *o, spmv_format fmt, const coo_t *m, dev_fmt_t *f)
+{
+    memset(f, 0, sizeof *f);
+    f->fmt = fmt;
+    f->d.n_rows = m->n_rows;
+    f->d.n_cols = m->n_cols;
+    f->d.nnz = m->nnz;
+    f->d.device = o->device;
+    f->d.stream = NULL;
+    const int64_t N = m->n_rows, Z = m->nnz;
+    int rc;
+    if (fmt == FMT_COO) {
+        f->h_row = malloc((size_t)(Z + 1) * sizeof(int32_t));
+        f->h_col = malloc((size_t)(Z + 1) * sizeof(int32_t));
+        f->h_val = malloc((size_t)(Z + 1) * sizeof(double));
+        rc = spmv_coo_sort_by_row(N, Z, m->row, m->col, m->val, f->h_row, f->h_col, f->h_val);
+        if (rc)
+            return rc;
+        f->ws_bytes = spmv_coo_ws_bytes(Z);
+        f->stored = Z;
+        f->stored_bytes = (size_t)Z * 16;
+        if ((rc = upload((void **)&f->d_row, f->h_row, (size_t)Z * 4, NULL)) ||
+            (rc = upload((void **)&f->d_col, f->h_col, (size_t)Z * 4, NULL)) ||
+            (rc = upload((void **)&f->d_val, f->h_val, (size_t)Z * 8, NULL)) ||
+            (rc = spmv_malloc(&f->d_ws, f->ws_bytes)))
+            return rc;
+        return SPMV_SUCCESS;
+    }
+    /* every other format starts from CSR */
+    int64_t *ptr = malloc((size_t)(N + 1) * sizeof(int64_t));
+    int32_t *col = malloc((size_t)(Z + 1) * sizeof(int32_t));
+    double *val = malloc((size_t)(Z + 1) * sizeof(double));
+    if (!ptr || !col || !val)
+        return SPMV_OTHER_ERROR;
+    if ((rc = spmv_csr_from_coo(N, Z, m->row, m->col, m->val, ptr, col, val)))
+        return rc;
+    if (fmt == FMT_CSR || fmt == FMT_CMRS) {
+        f->h_ptr = ptr;
+        f->h_col = col;
+        f->h_val = val;
+        f->stored = Z;
+        if (fmt == FMT_CSR) {
+            f->lanes = o->lanes > 0 ? o->lanes : spmv_csr_auto_lanes(N, Z);
+            f->stored_bytes = (size_t)Z * 12 + (size_t)(N + 1) * 8;
+            if ((rc = upload((void **)&f->d_ptr, ptr, (size_t)(N + 1) * 8, NULL)))
+                return rc;
+        } else {
+            f->h = o->h;
+            f->n_strips = (N + o->h - 1) / o->h;
+            int64_t *sp = malloc((size_t)(f->n_strips + 1) * sizeof(int64_t));
+            f->h_rin = malloc((size_t)(Z + 1));
+            if ((rc = spmv_cmrs_build(N, ptr, o->h, sp, f->h_rin)))
+                return rc;
+            free(f->h_ptr);
+            f->h_ptr = sp;
+            f->stored_bytes = (size_t)Z * 13 + (size_t)(f->n_strips + 1) * 8;
+            if ((rc = upload((void **)&f->d_ptr, sp, (size_t)(f->n_strips + 1) * 8, NULL)) ||
+                (rc = upload((void **)&f->d_rin, f->h_rin, (size_t)Z, NULL)))
+                return rc;
+        }
+        if ((rc = upload((void **)&f->d_col, col, (size_t)Z * 4, NULL)) ||
+            (rc = upload((void **)&f->d_val, val, (size_t)Z * 8, NULL)))
+            return rc;
+        return SPMV_SUCCESS;
+    }
+    if (fmt == FMT_ELL) {
+        int64_t mn, mx;
+        double mean;
+        spmv_csr_row_stats(N, ptr, &mn, &mx, &mean);
+        /* reference ell.c:104 */
+        printf("average column length %lf, shortest col %lld, longest col %lld\n", mean,
+               (long long)mn, (long long)mx);
+        f->ki = o->ki;
+        if ((rc = spmv_ell_plan(N, ptr, o->ki, &f->K, &f->ld)))
+            return rc;
+        f->stored = f->ld * f->K;
+        if (Z > 0 && (double)f->stored / (double)Z > 64.0) {
+            printf("ELL not applicable: padding factor %.1f (stored %lld / %lld entries)\n",
+                   (double)f->stored / (double)Z, (long long)f->stored, (long long)Z);
+            return SPMV_OTHER_ERROR;
+        }
+        f->h_col = malloc((size_t)(f->stored + 1) * sizeof(int32_t));
+        f->h_val = malloc((size_t)(f->stored + 1) * sizeof(double));
+        if ((rc = spmv_ell_fill(N, ptr, col, val, f->K, f->ld, f->ki, f->h_col, f->h_val)))
+            return rc;
+        f->stored_bytes = (size_t)f->stored * 12;
+    } else { /* SELL */
+        f->C = o->C;
+        f->ki = o->ki;
+        if ((rc = spmv_sell_plan(N, ptr, o->C, o->sigma, o->ki, &f->n_slices, &f->stored)))
+            return rc;
+        f->h_ptr = malloc((size_t)(f->n_slices + 1) * sizeof(int64_t));
+        f->h_perm = malloc((size_t)(f->n_slices * o->C + 1) * sizeof(int32_t));
+        f->h_col = malloc((size_t)(f->stored + 1) * sizeof(int32_t));
+        f->h_val = malloc((size_t)(f->stored + 1) * sizeof(double));
+        if ((rc = spmv_sell_fill(N, ptr, col, val, o->C, o->sigma, o->ki, f->n_slices, f->h_ptr,
+                                 f->h_perm, f->h_col, f->h_val)))
+            return rc;
+        f->stored_bytes = (size_t)f->stored * 12 + (size_t)(f->n_slices + 1) * 8 +
+                          (size_t)f->n_slices * o->C * 4;
+        if ((rc = upload((void **)&f->d_ptr, f->h_ptr, (size_t)(f->n_slices + 1) * 8, NULL)) ||
+            (rc = upload((void **)&f->d_perm, f->h_perm, (size_t)f->n_slices * o->C * 4, NULL)))
+            return rc;
+    }
+    free(ptr);
+    free(col);
+    free(val);
+    if ((rc = upload((void **)&f->d_col, f->h_col, (size_t)f->stored * 4, NULL)) ||
+        (rc = upload((void **)&f->d_val, f->h_val, (size_t)f->stored * 8, NULL)))
+        return rc;
+    return SPMV_SUCCESS;
+}
+
+static int launch(void *arg)
+{
+    dev_fmt_t *f = (dev_fmt_t *)arg;
+    switch (f->fmt) {
+    case FMT_COO:
+        return spmv_coo_run(f->d, f->d_row, f->d_col, f->d_val, f->d_x, f->d_y, f->d_ws,
+                            f->ws_bytes);
+    case FMT_CSR:
+        return spmv_csr_run(f->d, f->d_ptr, f->d_col, f->d_val, f->d_x, f->d_y, f->lanes);
+    case FMT_ELL:
+        return spmv_ell_run(f->d, f->K, f->ld, f->ki, f->d_col, f->d_val, f->d_x, f->d_y);
+    case FMT_SELL:
+        return spmv_sell_run(f->d, f->C, f->ki, f->n_slices, f->d_ptr, f->d_perm, f->d_col,
+                             f->d_val, f->d_x, f->d_y);
+    case FMT_CMRS:
+        return spmv_cmrs_run(f->d, f->h, f->n_strips, f->d_ptr, f->d_rin, f->d_col, f->d_val,
+                             f->d_x, f->d_y);
+    }
+    return SPMV_OTHER_ERROR;
+}
+
+static int run_cpu(const dev_fmt_t *f, const double *x, double *y, int threads)
+{
+    const int64_t N = f->d.n_rows;
+    switch (f->fmt) {
+    case FMT_COO:
+        return spmv_cpu_coo(N, f->d.nnz, f->h_row, f->h_col, f->h_val, x, y, threads);
+    case FMT_CSR:
+        return spmv_cpu_csr(N, f->h_ptr, f->h_col, f->h_val, x, y, threads);
+    case FMT_ELL:
+        return spmv_cpu_ell(N, f->K, f->ld, f->ki, f->h_col, f->h_val, x, y, threads);
+    case FMT_SELL:
+        return spmv_cpu_sell(N, f->C, f->ki, f->n_slices, f->h_ptr, f->h_perm, f->h_col,
+                             f->h_val, x, y, threads);
+    case FMT_CMRS:
+        return spmv_cpu_cmrs(N, f->h, f->n_strips, f->h_ptr, f->h_rin, f->h_col, f->h_val, x,
+                             y, threads);
+    }
+    return SPMV_OTHER_ERROR;
+}
+
+/* ------------------------------------------------------------ output */
+
+/* reference inc/helper_functions.h:167-173 (2*nnz widened past int32) */
+static void print_performance(double ms, int64_t nnz)
+{
+    printf("Your calculations took %.2lf ms to run.\n", ms);
+    printf("Number of operations %lld, PERFORMANCE %lf GFlops\n", (long long)(2 * nnz),
+           (2.0 * (double)nnz) / ms * 1e-6);
+}
+
+/* reference inc/helper_functions.h:175-182 */
+static void print_speed(double ms, int64_t nnz)
+{
+    printf("GBytes transferred to processor %lf - %lf, speed %lf - %lf GB/s\n",
+           (double)nnz * 8 * 1e-9, (double)(2 * nnz) * 8 * 1e-9, (double)nnz * 8 / ms * 1e-6,
+           (double)(2 * nnz) * 8 / ms * 1e-6);
+}
+
+static int check_and_report(const coo_t *m, const double *x, const double *y, const char *who)
+{
+    int64_t first_bad = -1;
+    double ref_at_bad = 0.0;
+    int64_t bad_rel = spmv_check(m->n_rows, m->nnz, m->row, m->col, m->val, x, y, 0.0, 1e-6,
+                                 &first_bad, &ref_at_bad);
+    int64_t first_abs = -1;
+    int64_t bad_abs = spmv_check(m->n_rows, m->nnz, m->row, m->col, m->val, x, y, 1e-6, 0.0,
+                                 &first_abs, NULL);
+    if (bad_rel != 0 && first_bad >= 0) /* reference helper_functions.h:225 */
+        printf("wrong value at index %lld: expected %f - calculated %f\n", (long long)first_bad,
+               ref_at_bad, y[first_bad]);
+    printf("%sresult is %s\n", who, bad_rel == 0 ? "ok" : "wrong");
+    printf("  [check] rel-1e-6: %lld bad rows; reference abs-1e-6 rule: %s (%lld rows)\n",
+           (long long)bad_rel, bad_abs == 0 ? "pass" : "fail", (long long)bad_abs);
+    return bad_rel == 0;
+}
+
+static int cmp_double(const void *a, const void *b)
+{
+    double x = *(const double *)a, y = *(const double *)b;
+    return x < y ? -1 : (x > y);
+}
+
+static double now_s(void)
+{
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
+
+static const char *fmt_name(spmv_format f)
+{
+    static const char *n[] = {"coo", "csr", "ell", "sigma_c", "cmrs"};
+    return n[f];
+}
+
+int spmv_driver_main(int argc, char **argv, spmv_format fmt)
+{
+    setvbuf(stdout, NULL, _IOLBF, 0);
+    opts_t o;
+    if (parse_opts(argc, argv, fmt, &o) != SPMV_SUCCESS)
+        return SPMV_OTHER_ERROR;
+
+    int ndev = 0;
+    if (spmv_device_count(&ndev) != SPMV_SUCCESS || ndev <= o.device) {
+        printf("No HIP GPU device found (%s)\n", spmv_last_error());
+        return SPMV_DEVICE_ERROR; /* reference csr.c:25-28 */
+    }
+    if (spmv_set_device(o.device) != SPMV_SUCCESS)
+        return SPMV_DEVICE_ERROR;
+
+    coo_t m;
+    errno = 0;
+    int rc = load_input(&o, fmt, &m);
+    if (rc != SPMV_SUCCESS)
+        return rc;
+    if (o.write_mtx)
+        spmv_mtx_write(o.write_mtx, m.n_rows, m.n_cols, m.nnz, m.row, m.col, m.val, 0);
+
+    double *x = malloc((size_t)(m.n_cols + 1) * sizeof(double));
+    double *y = malloc((size_t)(m.n_rows + 1) * sizeof(double));
+    double *y_cpu = malloc((size_t)(m.n_rows + 1) * sizeof(double));
+    if (!x || !y || !y_cpu)
+        return SPMV_OTHER_ERROR;
+    for (int64_t j = 0; j < m.n_cols; ++j)
+        x[j] = (double)j; /* reference csr.c:95-99 */
+
+    dev_fmt_t f;
+    rc = build_format(&o, fmt, &m, &f);
+    if (rc != SPMV_SUCCESS) {
+        printf("format build/upload failed: %s %s\n", spmv_strerror(rc), spmv_last_error());
+        return rc == SPMV_OTHER_ERROR ? SPMV_OTHER_ERROR : SPMV_PROGRAM_ERROR;
+    }
+    if ((rc = upload((void **)&f.d_x, x, (size_t)m.n_cols * 8, NULL)) ||
+        (rc = spmv_malloc((void **)&f.d_y, (size_t)m.n_rows * 8)) ||
+        (rc = spmv_memset(f.d_y, 0xFF, (size_t)m.n_rows * 8, NULL))) /* NaN: y must be written */
+        return SPMV_PROGRAM_ERROR;
+
+    for (int i = 0; i < o.warmup; ++i)
+        if ((rc = launch(&f)) != SPMV_SUCCESS) {
+            printf("kernel launch error: %s\n", spmv_last_error());
+            return SPMV_PROGRAM_ERROR;
+        }
+    double *t = malloc((size_t)o.reps * sizeof(double));
+    for (int i = 0; i < o.reps; ++i) {
+        if (!o.warm && spmv_flush_cache(NULL, 0) != SPMV_SUCCESS)
+            return SPMV_PROGRAM_ERROR;
+        if (spmv_time_launch(launch, &f, NULL, &t[i]) != SPMV_SUCCESS) {
+            printf("kernel launch error: %s\n", spmv_last_error());
+            return SPMV_PROGRAM_ERROR;
+        }
+    }
+    qsort(t, (size_t)o.reps, sizeof(double), cmp_double);
+    double ms = t[o.reps / 2];
+
+    if (fmt == FMT_COO)
+        printf("GPU calculations\n"); /* reference coo.c:201 */
+    print_performance(ms, m.nnz);
+    print_speed(ms, m.nnz);
+
+    const double bytes_alg = 12.0 * (double)m.nnz + 4.0 * (double)(m.n_rows + 1) +
+                             8.0 * (double)m.n_cols + 8.0 * (double)m.n_rows;
+    char dev[128] = "";
+    spmv_device_name(o.device, dev, sizeof dev);
+    printf("  [%s] %s | N=%lld M=%lld Z=%lld | median of %d %s reps (min %.4f ms)\n",
+           fmt_name(fmt), m.label, (long long)m.n_rows, (long long)m.n_cols, (long long)m.nnz,
+           o.reps, o.warm ? "warm (cache-resident)" : "cold (512 MiB flush)", t[0]);
+    printf("  [%s] effective %.1f GB/s (bytes_alg %.1f MB) = %.1f%% of %.0f GB/s HBM3E peak; "
+           "stored %.1f MB; %s\n",
+           fmt_name(fmt), bytes_alg / ms * 1e-6, bytes_alg * 1e-6,
+           100.0 * bytes_alg / ms * 1e-6 / HBM_PEAK_GBS, HBM_PEAK_GBS,
+           (double)f.stored_bytes * 1e-6, dev);
+
+    if (spmv_download(y, f.d_y, (size_t)m.n_rows * 8, NULL) != SPMV_SUCCESS) {
+        printf("read back error: %s\n", spmv_last_error());
+        return SPMV_PROGRAM_ERROR;
+    }
+    int ok = check_and_report(&m, x, y, "");
+
+    if (o.cpu) {
+        int threads = o.threads > 0 ? o.threads : spmv_cpu_threads();
+        double t0 = now_s();
+        run_cpu(&f, x, y_cpu, threads);
+        double cms = (now_s() - t0) * 1e3;
+        printf("\nCPU calculations\n"); /* reference csr.c:306 */
+        print_performance(cms, m.nnz);
+        printf("  [cpu] %d OpenMP threads, effective %.1f GB/s\n", threads,
+               bytes_alg / cms * 1e-6);
+        ok &= check_and_report(&m, x, y_cpu, "cpu ");
+    }
+    return (o.strict && !ok) ? SPMV_OTHER_ERROR : SPMV_SUCCESS;
+}

@@ -1,0 +1,314 @@
+/*
+ * formats.c — host builders for the five storage formats.
+ *
+ * The reference builds every format inside its fscanf loop and assumes a
+ * row-sorted file without empty rows (reference csr.c:68-91 leaves ptr[]
+ * slots unset after an empty row; sigma_c.c:93-139 and cmrs.c:84-113
+ * count any row change as +1 row; ell.c:73-101 drops the last row from
+ * K).  Here every builder starts from a CSR produced by a stable counting
+ * sort, so any entry order and any number of empty rows is accepted, and
+ * the layouts are the wave64 ones documented in spmv.h:
+ *   ELL   column-major, ld = round_up(N,64), k-interleave ki
+ *         (reference ell.c:118-164 was row-major N x K)
+ *   SELL  C-row slices, rows sorted by length inside sigma windows,
+ *         column-major inside a slice with k-interleave ki
+ *         (reference sigma_c.c:71-202: C = 32, sigma = 1)
+ *   CMRS  strips of h rows over the unchanged CSR arrays, uint8
+ *         row_in_strip (reference cmrs.c:72-117: int32)
+ * Padding slots carry value 0.0 and a column the row already reads (its
+ * last real column), so they add no x traffic; the reference left ELL
+ * padding values uninitialised (reference ell.c:119) and relied on
+ * x[0] == 0.
+ */
+#include <stdlib.h>
+#include <string.h>
+
+#include "spmv_host.h"
+
+static inline int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
+
+int spmv_coo_sort_by_row(int64_t n_rows, int64_t nnz, const int32_t *row,
+                         const int32_t *col, const double *val,
+                         int32_t *row_out, int32_t *col_out, double *val_out)
+{
+    if (n_rows < 0 || nnz < 0)
+        return SPMV_OTHER_ERROR;
+    int64_t *cursor = (int64_t *)calloc((size_t)n_rows + 1, sizeof(int64_t));
+    if (!cursor)
+        return SPMV_OTHER_ERROR;
+    for (int64_t i = 0; i < nnz; ++i) {
+        if (row[i] < 0 || row[i] >= n_rows) {
+            free(cursor);
+            return SPMV_OTHER_ERROR;
+        }
+        cursor[row[i] + 1]++;
+    }
+    for (int64_t r = 0; r < n_rows; ++r)
+        cursor[r + 1] += cursor[r];
+    for (int64_t i = 0; i < nnz; ++i) {
+        int64_t p = cursor[row[i]]++;
+        row_out[p] = row[i];
+        col_out[p] = col[i];
+        val_out[p] = val[i];
+    }
+    free(cursor);
+    return SPMV_SUCCESS;
+}
+
+int spmv_csr_from_coo(int64_t n_rows, int64_t nnz, const int32_t *row,
+                      const int32_t *col, const double *val,
+                      int64_t *row_ptr, int32_t *col_out, double *val_out)
+{
+    if (n_rows < 0 || nnz < 0)
+        return SPMV_OTHER_ERROR;
+    memset(row_ptr, 0, ((size_t)n_rows + 1) * sizeof(int64_t));
+    for (int64_t i = 0; i < nnz; ++i) {
+        if (row[i] < 0 || row[i] >= n_rows)
+            return SPMV_OTHER_ERROR;
+        row_ptr[row[i] + 1]++;
+    }
+    for (int64_t r = 0; r < n_rows; ++r)
+        row_ptr[r + 1] += row_ptr[r];
+    /* stable scatter: reuse row_ptr[r] as the cursor, then shift back */
+    for (int64_t i = 0; i < nnz; ++i) {
+        int64_t p = row_ptr[row[i]]++;
+        col_out[p] = col[i];
+        val_out[p] = val[i];
+    }
+    for (int64_t r = n_rows; r > 0; --r)
+        row_ptr[r] = row_ptr[r - 1];
+    row_ptr[0] = 0;
+    return SPMV_SUCCESS;
+}
+
+int spmv_csr_row_stats(int64_t n_rows, const int64_t *row_ptr,
+                       int64_t *min_len, int64_t *max_len, double *mean_len)
+{
+    int64_t mn = n_rows > 0 ? INT64_MAX : 0, mx = 0;
+    for (int64_t r = 0; r < n_rows; ++r) {
+        int64_t l = row_ptr[r + 1] - row_ptr[r];
+        if (l < mn)
+            mn = l;
+        if (l > mx)
+            mx = l;
+    }
+    if (min_len)
+        *min_len = mn;
+    if (max_len)
+        *max_len = mx;
+    if (mean_len)
+        *mean_len = n_rows > 0 ? (double)row_ptr[n_rows] / (double)n_rows : 0.0;
+    return SPMV_SUCCESS;
+}
+
+/* ------------------------------------------------------------------ ELL */
+
+int spmv_ell_plan(int64_t n_rows, const int64_t *row_ptr, int32_t ki,
+                  int32_t *K, int64_t *ld)
+{
+    if (ki != 1 && ki != 2)
+        return SPMV_OTHER_ERROR;
+    int64_t mx = 0;
+    spmv_csr_row_stats(n_rows, row_ptr, NULL, &mx, NULL);
+    int64_t k = round_up(mx, ki);
+    if (k > INT32_MAX)
+        return SPMV_OTHER_ERROR;
+    *K = (int32_t)k;
+    *ld = round_up(n_rows, 64);
+    return SPMV_SUCCESS;
+}
+
+int spmv_ell_fill(int64_t n_rows, const int64_t *row_ptr, const int32_t *col,
+                  const double *val, int32_t K, int64_t ld, int32_t ki,
+                  int32_t *col_out, double *val_out)
+{
+    if ((ki != 1 && ki != 2) || K % ki != 0 || ld < n_rows || ld % 64 != 0)
+        return SPMV_OTHER_ERROR;
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < ld; ++i) {
+        int64_t b = 0, e = 0;
+        if (i < n_rows) {
+            b = row_ptr[i];
+            e = row_ptr[i + 1];
+        }
+        int32_t pad_col = e > b ? col[e - 1] : 0;
+        for (int64_t k = 0; k < K; ++k) {
+            int64_t pos = (k / ki) * ld * ki + i * ki + (k % ki);
+            if (b + k < e) {
+                col_out[pos] = col[b + k];
+                val_out[pos] = val[b + k];
+            } else {
+                col_out[pos] = pad_col;
+                val_out[pos] = 0.0;
+            }
+        }
+    }
+    return SPMV_SUCCESS;
+}
+
+/* ------------------------------------------------------------- SELL-C-σ */
+
+typedef struct {
+    int64_t len;
+    int64_t row;
+} len_row_t;
+
+static int cmp_len_desc(const void *a, const void *b)
+{
+    const len_row_t *x = (const len_row_t *)a, *y = (const len_row_t *)b;
+    if (x->len != y->len)
+        return x->len > y->len ? -1 : 1;
+    return x->row < y->row ? -1 : (x->row > y->row);
+}
+
+/* perm over n_slices*C slots; -1 marks padding slots. */
+static int sell_perm(int64_t n_rows, const int64_t *row_ptr, int32_t C,
+                     int32_t sigma, int64_t n_slices, int32_t *perm)
+{
+    int64_t slots = n_slices * C;
+    for (int64_t i = 0; i < slots; ++i)
+        perm[i] = i < n_rows ? (int32_t)i : -1;
+    if (sigma <= 1)
+        return SPMV_SUCCESS;
+    int64_t n_win = (n_rows + sigma - 1) / sigma;
+    int fail = 0;
+#pragma omp parallel
+    {
+        len_row_t *tmp = (len_row_t *)malloc((size_t)sigma * sizeof(len_row_t));
+        if (!tmp) {
+#pragma omp atomic write
+            fail = 1;
+        }
+#pragma omp for schedule(dynamic, 16)
+        for (int64_t w = 0; w < n_win; ++w) {
+            if (!tmp)
+                continue;
+            int64_t r0 = w * sigma;
+            int64_t r1 = r0 + sigma < n_rows ? r0 + sigma : n_rows;
+            int64_t n = r1 - r0;
+            for (int64_t i = 0; i < n; ++i) {
+                tmp[i].row = r0 + i;
+                tmp[i].len = row_ptr[r0 + i + 1] - row_ptr[r0 + i];
+            }
+            qsort(tmp, (size_t)n, sizeof(len_row_t), cmp_len_desc);
+            for (int64_t i = 0; i < n; ++i)
+                perm[r0 + i] = (int32_t)tmp[i].row;
+        }
+        free(tmp);
+    }
+    return fail ? SPMV_OTHER_ERROR : SPMV_SUCCESS;
+}
+
+static int sell_check(int64_t n_rows, int32_t C, int32_t sigma, int32_t ki)
+{
+    if (n_rows < 0 || n_rows > INT32_MAX || C <= 0 || C > 1024)
+        return SPMV_OTHER_ERROR;
+    if (ki != 1 && ki != 2)
+        return SPMV_OTHER_ERROR;
+    if (sigma > 1 && sigma % C != 0)
+        return SPMV_OTHER_ERROR;
+    return SPMV_SUCCESS;
+}
+
+int spmv_sell_plan(int64_t n_rows, const int64_t *row_ptr, int32_t C,
+                   int32_t sigma, int32_t ki, int64_t *n_slices,
+                   int64_t *stored)
+{
+    int rc = sell_check(n_rows, C, sigma, ki);
+    if (rc)
+        return rc;
+    int64_t ns = (n_rows + C - 1) / C;
+    int32_t *perm = (int32_t *)malloc((size_t)(ns * C > 0 ? ns * C : 1) * sizeof(int32_t));
+    if (!perm)
+        return SPMV_OTHER_ERROR;
+    rc = sell_perm(n_rows, row_ptr, C, sigma, ns, perm);
+    int64_t total = 0;
+    for (int64_t s = 0; s < ns && rc == 0; ++s) {
+        int64_t w = 0;
+        for (int64_t r = 0; r < C; ++r) {
+            int32_t row = perm[s * C + r];
+            if (row >= 0) {
+                int64_t l = row_ptr[row + 1] - row_ptr[row];
+                if (l > w)
+                    w = l;
+            }
+        }
+        total += round_up(w, ki) * C;
+    }
+    free(perm);
+    *n_slices = ns;
+    *stored = total;
+    return rc;
+}
+
+int spmv_sell_fill(int64_t n_rows, const int64_t *row_ptr, const int32_t *col,
+                   const double *val, int32_t C, int32_t sigma, int32_t ki,
+                   int64_t n_slices, int64_t *slice_ptr, int32_t *perm,
+                   int32_t *col_out, double *val_out)
+{
+    int rc = sell_check(n_rows, C, sigma, ki);
+    if (rc)
+        return rc;
+    if (n_slices != (n_rows + C - 1) / C)
+        return SPMV_OTHER_ERROR;
+    rc = sell_perm(n_rows, row_ptr, C, sigma, n_slices, perm);
+    if (rc)
+        return rc;
+    slice_ptr[0] = 0;
+    for (int64_t s = 0; s < n_slices; ++s) {
+        int64_t w = 0;
+        for (int64_t r = 0; r < C; ++r) {
+            int32_t row = perm[s * C + r];
+            if (row >= 0) {
+                int64_t l = row_ptr[row + 1] - row_ptr[row];
+                if (l > w)
+                    w = l;
+            }
+        }
+        slice_ptr[s + 1] = slice_ptr[s] + round_up(w, ki) * C;
+    }
+#pragma omp parallel for schedule(dynamic, 64)
+    for (int64_t s = 0; s < n_slices; ++s) {
+        int64_t base = slice_ptr[s];
+        int64_t w = (slice_ptr[s + 1] - base) / C;
+        for (int64_t r = 0; r < C; ++r) {
+            int32_t row = perm[s * C + r];
+            int64_t b = 0, e = 0;
+            if (row >= 0) {
+                b = row_ptr[row];
+                e = row_ptr[row + 1];
+            }
+            int32_t pad_col = e > b ? col[e - 1] : 0;
+            for (int64_t k = 0; k < w; ++k) {
+                int64_t pos = base + (k / ki) * (int64_t)C * ki + r * ki + (k % ki);
+                if (b + k < e) {
+                    col_out[pos] = col[b + k];
+                    val_out[pos] = val[b + k];
+                } else {
+                    col_out[pos] = pad_col;
+                    val_out[pos] = 0.0;
+                }
+            }
+        }
+    }
+    return SPMV_SUCCESS;
+}
+
+/* ----------------------------------------------------------------- CMRS */
+
+int spmv_cmrs_build(int64_t n_rows, const int64_t *row_ptr, int32_t h,
+                    int64_t *strip_ptr, uint8_t *row_in_strip)
+{
+    if (h < 1 || h > 64 || n_rows < 0)
+        return SPMV_OTHER_ERROR;
+    int64_t ns = (n_rows + h - 1) / h;
+    for (int64_t s = 0; s <= ns; ++s) {
+        int64_t r = s * h < n_rows ? s * h : n_rows;
+        strip_ptr[s] = row_ptr[r];
+    }
+#pragma omp parallel for schedule(static)
+    for (int64_t r = 0; r < n_rows; ++r)
+        for (int64_t j = row_ptr[r]; j < row_ptr[r + 1]; ++j)
+            row_in_strip[j] = (uint8_t)(r % h);
+    return SPMV_SUCCESS;
+}

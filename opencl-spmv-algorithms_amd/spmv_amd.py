@@ -1,0 +1,472 @@
+"""spmv_amd — Python host mirror of the MI355X SpMV suite's C-ABI.
+
+The product is C/HIP: ``lib/libspmv_hip.so`` (gfx950 kernels behind the
+``extern "C"`` entry points of ``include/spmv.h``) and ``lib/libspmv_host.so``
+(Matrix Market reader, format builders, generators, CPU loops; declared in
+``include/spmv_host.h``).  This module binds both with ctypes so tests and
+``bench.py`` drive exactly the calls the C drivers make.  PyTorch is used
+only as plumbing: device memory (CUDA tensors on ROCm), the current HIP
+stream and ``torch.distributed``.
+
+There is no fallback: if ``libspmv_hip.so`` is missing or a HIP call fails,
+``SpmvError`` is raised.  The five formats mirror the reference's five
+programs (reference coo.c, csr.c, ell.c, sigma_c.c, cmrs.c) and kernels
+(reference kernels/{Coo,Csr,Ell,Sigma_C,Cmrs}.cl).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass, field
+from pathlib import Path
+
+import numpy as np
+
+PKG_DIR = Path(__file__).resolve().parent
+LIB_DIR = PKG_DIR / "lib"
+REPO_DIR = PKG_DIR.parent
+
+FORMATS = ("coo", "csr", "ell", "sell", "cmrs")
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+# The reference's ReturnCode values (reference inc/enums.h:4-11).
+SUCCESS, DEVICE_ERROR, PROGRAM_ERROR, FILE_ERROR, OTHER_ERROR = range(5)
+
+
+class SpmvError(RuntimeError):
+    """A C-ABI call returned a non-zero spmv_rc code."""
+
+    def __init__(self, rc: int, what: str, detail: str = ""):
+        super().__init__(f"{what} failed: rc={rc} {detail}".strip())
+        self.rc = rc
+
+
+# --------------------------------------------------------------- loading
+_c_i64 = ctypes.c_int64
+_c_i32 = ctypes.c_int32
+_vp = ctypes.c_void_p
+
+
+class Dims(ctypes.Structure):
+    """``spmv_dims`` (include/spmv.h)."""
+
+    _fields_ = [
+        ("n_rows", _c_i64),
+        ("n_cols", _c_i64),
+        ("nnz", _c_i64),
+        ("device", ctypes.c_int),
+        ("stream", _vp),
+    ]
+
+
+class MtxInfo(ctypes.Structure):
+    """``spmv_mtx_info`` (include/spmv_host.h)."""
+
+    _fields_ = [
+        ("n_rows", _c_i64),
+        ("n_cols", _c_i64),
+        ("nnz", _c_i64),
+        ("symmetric", ctypes.c_int),
+        ("pattern", ctypes.c_int),
+        ("integer", ctypes.c_int),
+    ]
+
+
+# name -> (restype, argtypes)
+HIP_SYMBOLS = {
+    "spmv_coo_ws_bytes": (ctypes.c_size_t, [_c_i64]),
+    "spmv_coo_run": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t]),
+    "spmv_csr_auto_lanes": (ctypes.c_int, [_c_i64, _c_i64]),
+    "spmv_csr_run": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, ctypes.c_int]),
+    "spmv_ell_run": (ctypes.c_int, [Dims, _c_i32, _c_i64, _c_i32, _vp, _vp, _vp, _vp]),
+    "spmv_sell_run": (ctypes.c_int, [Dims, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "spmv_cmrs_run": (ctypes.c_int, [Dims, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "spmv_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    "spmv_set_device": (ctypes.c_int, [ctypes.c_int]),
+    "spmv_device_name": (ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t]),
+    "spmv_malloc": (ctypes.c_int, [ctypes.POINTER(_vp), ctypes.c_size_t]),
+    "spmv_free": (ctypes.c_int, [_vp]),
+    "spmv_memset": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_size_t, _vp]),
+    "spmv_upload": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t, _vp]),
+    "spmv_download": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t, _vp]),
+    "spmv_stream_create": (ctypes.c_int, [ctypes.POINTER(_vp)]),
+    "spmv_stream_destroy": (ctypes.c_int, [_vp]),
+    "spmv_sync": (ctypes.c_int, [_vp]),
+    "spmv_flush_cache": (ctypes.c_int, [_vp, ctypes.c_size_t]),
+    "spmv_time_launch": (ctypes.c_int, [_vp, _vp, _vp, ctypes.POINTER(ctypes.c_double)]),
+    "spmv_release": (ctypes.c_int, []),
+    "spmv_strerror": (ctypes.c_char_p, [ctypes.c_int]),
+    "spmv_last_error": (ctypes.c_char_p, []),
+    "spmv_version": (ctypes.c_char_p, []),
+}
+
+HOST_SYMBOLS = {
+    "spmv_mtx_read_info": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(MtxInfo)]),
+    "spmv_mtx_read": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(MtxInfo), _vp, _vp, _vp]),
+    "spmv_mtx_write": (ctypes.c_int, [ctypes.c_char_p, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, ctypes.c_int]),
+    "spmv_coo_sort_by_row": (ctypes.c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "spmv_csr_from_coo": (ctypes.c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "spmv_csr_row_stats": (ctypes.c_int, [_c_i64, _vp, ctypes.POINTER(_c_i64), ctypes.POINTER(_c_i64), ctypes.POINTER(ctypes.c_double)]),
+    "spmv_ell_plan": (ctypes.c_int, [_c_i64, _vp, _c_i32, ctypes.POINTER(_c_i32), ctypes.POINTER(_c_i64)]),
+    "spmv_ell_fill": (ctypes.c_int, [_c_i64, _vp, _vp, _vp, _c_i32, _c_i64, _c_i32, _vp, _vp]),
+    "spmv_sell_plan": (ctypes.c_int, [_c_i64, _vp, _c_i32, _c_i32, _c_i32, ctypes.POINTER(_c_i64), ctypes.POINTER(_c_i64)]),
+    "spmv_sell_fill": (ctypes.c_int, [_c_i64, _vp, _vp, _vp, _c_i32, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, _vp]),
+    "spmv_cmrs_build": (ctypes.c_int, [_c_i64, _vp, _c_i32, _vp, _vp]),
+    "spmv_cpu_coo": (ctypes.c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, ctypes.c_int]),
+    "spmv_cpu_csr": (ctypes.c_int, [_c_i64, _vp, _vp, _vp, _vp, _vp, ctypes.c_int]),
+    "spmv_cpu_ell": (ctypes.c_int, [_c_i64, _c_i32, _c_i64, _c_i32, _vp, _vp, _vp, _vp, ctypes.c_int]),
+    "spmv_cpu_sell": (ctypes.c_int, [_c_i64, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_int]),
+    "spmv_cpu_cmrs": (ctypes.c_int, [_c_i64, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_int]),
+    "spmv_cpu_threads": (ctypes.c_int, []),
+    "spmv_check": (_c_i64, [_c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, ctypes.c_double, ctypes.c_double, ctypes.POINTER(_c_i64), ctypes.POINTER(ctypes.c_double)]),
+    "spmv_gen_cantlike": (ctypes.c_int, [ctypes.c_int, _c_i64, ctypes.POINTER(_c_i64), ctypes.POINTER(_c_i64), _vp, _vp, _vp]),
+    "spmv_gen_rmat": (ctypes.c_int, [_c_i64, _c_i64, ctypes.c_int, ctypes.c_uint64, _vp, _vp, _vp]),
+    "spmv_gen_banded_csr": (ctypes.c_int, [_c_i64, ctypes.c_uint64, _c_i64, _c_i64, _vp, _vp, _vp]),
+    "spmv_gen_random": (ctypes.c_int, [_c_i64, _c_i64, _c_i64, _c_i64, ctypes.c_uint64, ctypes.POINTER(_c_i64), _vp, _vp, _vp]),
+    "spmv_splitmix64": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_uint64]),
+}
+
+_LAUNCH_FN = ctypes.CFUNCTYPE(ctypes.c_int, _vp)
+
+_hip = None
+_host = None
+
+
+def _bind(lib: ctypes.CDLL, table: dict) -> ctypes.CDLL:
+    for name, (res, args) in table.items():
+        fn = getattr(lib, name)  # AttributeError = symbol missing: loud
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+def hip_lib() -> ctypes.CDLL:
+    """libspmv_hip.so — raises if it was not built (no CPU fallback)."""
+    global _hip
+    if _hip is None:
+        path = LIB_DIR / "libspmv_hip.so"
+        if not path.exists():
+            raise SpmvError(PROGRAM_ERROR, "load libspmv_hip.so", f"{path} missing: run `make lib`")
+        _hip = _bind(ctypes.CDLL(str(path), mode=ctypes.RTLD_GLOBAL), HIP_SYMBOLS)
+    return _hip
+
+
+def host_lib() -> ctypes.CDLL:
+    global _host
+    if _host is None:
+        path = LIB_DIR / "libspmv_host.so"
+        if not path.exists():
+            raise SpmvError(PROGRAM_ERROR, "load libspmv_host.so", f"{path} missing: run `make lib`")
+        _host = _bind(ctypes.CDLL(str(path)), HOST_SYMBOLS)
+    return _host
+
+
+def _ptr(a) -> int | None:
+    """Raw address of a numpy array or torch tensor (None for empty)."""
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    return a.data_ptr()
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != SUCCESS:
+        detail = hip_lib().spmv_last_error().decode() if _hip is not None else ""
+        raise SpmvError(rc, what, detail)
+
+
+# --------------------------------------------------------- host: inputs
+@dataclass
+class Coo:
+    """Entries in FILE order (the order check_result accumulates in)."""
+
+    n_rows: int
+    n_cols: int
+    row: np.ndarray
+    col: np.ndarray
+    val: np.ndarray
+    symmetric: bool = False
+    label: str = ""
+
+    @property
+    def nnz(self) -> int:
+        return int(self.row.shape[0])
+
+
+def read_mtx(path: str | os.PathLike) -> Coo:
+    """Matrix Market reader with the reference's acceptance rules
+    (reference inc/helper_functions.h:134-165, csr.c:77-91)."""
+    lib = host_lib()
+    info = MtxInfo()
+    p = str(path).encode()
+    rc = lib.spmv_mtx_read_info(p, ctypes.byref(info))
+    if rc != SUCCESS:
+        raise SpmvError(rc, f"read {path}")
+    z = info.nnz
+    row = np.empty(z, np.int32)
+    col = np.empty(z, np.int32)
+    val = np.empty(z, np.float64)
+    _check_host(lib.spmv_mtx_read(p, ctypes.byref(info), _ptr(row), _ptr(col), _ptr(val)), f"read {path}")
+    return Coo(info.n_rows, info.n_cols, row, col, val, bool(info.symmetric), str(path))
+
+
+def _check_host(rc: int, what: str) -> None:
+    if rc != SUCCESS:
+        raise SpmvError(rc, what)
+
+
+def write_mtx(path, m: Coo) -> None:
+    _check_host(host_lib().spmv_mtx_write(str(path).encode(), m.n_rows, m.n_cols, m.nnz,
+                                          _ptr(m.row), _ptr(m.col), _ptr(m.val), int(m.symmetric)),
+                f"write {path}")
+
+
+def gen_cantlike(mode: int = 0, copies: int = 1) -> Coo:
+    """cant-like stand-in (include/spmv_host.h: spmv_gen_cantlike)."""
+    lib = host_lib()
+    n = _c_i64()
+    z = _c_i64()
+    _check_host(lib.spmv_gen_cantlike(mode, copies, ctypes.byref(n), ctypes.byref(z), None, None, None), "gen_cantlike")
+    row = np.empty(z.value, np.int32)
+    col = np.empty(z.value, np.int32)
+    val = np.empty(z.value, np.float64)
+    _check_host(lib.spmv_gen_cantlike(mode, copies, ctypes.byref(n), ctypes.byref(z), _ptr(row), _ptr(col), _ptr(val)), "gen_cantlike")
+    label = f"cant-like stand-in (synthetic, mode {mode}, x{copies})"
+    return Coo(n.value, n.value, row, col, val, mode == 2, label)
+
+
+def gen_rmat(n: int = 10_000_000, nnz: int = 100_000_000, scale: int = 24, seed: int = 1) -> Coo:
+    lib = host_lib()
+    row = np.empty(nnz, np.int32)
+    col = np.empty(nnz, np.int32)
+    val = np.empty(nnz, np.float64)
+    _check_host(lib.spmv_gen_rmat(n, nnz, scale, seed, _ptr(row), _ptr(col), _ptr(val)), "gen_rmat")
+    return Coo(n, n, row, col, val, False, f"R-MAT {n} rows {nnz} entries (synthetic)")
+
+
+def gen_random(n_rows: int, n_cols: int, min_len: int, max_len: int, seed: int = 1) -> Coo:
+    lib = host_lib()
+    z = _c_i64()
+    _check_host(lib.spmv_gen_random(n_rows, n_cols, min_len, max_len, seed, ctypes.byref(z), None, None, None), "gen_random")
+    row = np.empty(z.value, np.int32)
+    col = np.empty(z.value, np.int32)
+    val = np.empty(z.value, np.float64)
+    _check_host(lib.spmv_gen_random(n_rows, n_cols, min_len, max_len, seed, ctypes.byref(z), _ptr(row), _ptr(col), _ptr(val)), "gen_random")
+    return Coo(n_rows, n_cols, row, col, val, False, f"random {n_rows}x{n_cols} len {min_len}..{max_len}")
+
+
+def gen_banded_csr(n: int, row_begin: int = 0, row_end: int | None = None, seed: int = 2):
+    """Banded rows [row_begin,row_end) in CSR form (local row_ptr)."""
+    row_end = n if row_end is None else row_end
+    m = row_end - row_begin
+    ptr = np.empty(m + 1, np.int64)
+    col = np.empty(16 * m, np.int32)
+    val = np.empty(16 * m, np.float64)
+    _check_host(host_lib().spmv_gen_banded_csr(n, seed, row_begin, row_end, _ptr(ptr), _ptr(col), _ptr(val)), "gen_banded")
+    return ptr, col, val
+
+
+def ramp_x(n_cols: int) -> np.ndarray:
+    """x[j] = j, the reference's input vector (reference csr.c:95-99)."""
+    return np.arange(n_cols, dtype=np.float64)
+
+
+# ------------------------------------------------------- host: formats
+def csr_from_coo(m: Coo):
+    ptr = np.empty(m.n_rows + 1, np.int64)
+    col = np.empty(m.nnz, np.int32)
+    val = np.empty(m.nnz, np.float64)
+    _check_host(host_lib().spmv_csr_from_coo(m.n_rows, m.nnz, _ptr(m.row), _ptr(m.col), _ptr(m.val),
+                                             _ptr(ptr), _ptr(col), _ptr(val)), "csr_from_coo")
+    return ptr, col, val
+
+
+def coo_sort_by_row(m: Coo):
+    row = np.empty(m.nnz, np.int32)
+    col = np.empty(m.nnz, np.int32)
+    val = np.empty(m.nnz, np.float64)
+    _check_host(host_lib().spmv_coo_sort_by_row(m.n_rows, m.nnz, _ptr(m.row), _ptr(m.col), _ptr(m.val),
+                                                _ptr(row), _ptr(col), _ptr(val)), "coo_sort_by_row")
+    return row, col, val
+
+
+def row_stats(n_rows: int, ptr: np.ndarray):
+    mn, mx, mean = _c_i64(), _c_i64(), ctypes.c_double()
+    host_lib().spmv_csr_row_stats(n_rows, _ptr(ptr), ctypes.byref(mn), ctypes.byref(mx), ctypes.byref(mean))
+    return mn.value, mx.value, mean.value
+
+
+def ell_build(n_rows: int, ptr, col, val, ki: int = 2, max_padding: float | None = None):
+    lib = host_lib()
+    K, ld = _c_i32(), _c_i64()
+    _check_host(lib.spmv_ell_plan(n_rows, _ptr(ptr), ki, ctypes.byref(K), ctypes.byref(ld)), "ell_plan")
+    stored = K.value * ld.value
+    nnz = int(ptr[-1]) if n_rows > 0 else 0
+    if max_padding is not None and nnz > 0 and stored / nnz > max_padding:
+        raise SpmvError(OTHER_ERROR, "ell_build", f"padding factor {stored / nnz:.1f} > {max_padding}")
+    ecol = np.empty(max(stored, 1), np.int32)
+    evalv = np.empty(max(stored, 1), np.float64)
+    _check_host(lib.spmv_ell_fill(n_rows, _ptr(ptr), _ptr(col), _ptr(val), K.value, ld.value, ki,
+                                  _ptr(ecol), _ptr(evalv)), "ell_fill")
+    return dict(K=K.value, ld=ld.value, ki=ki, col=ecol, val=evalv, stored=stored)
+
+
+def sell_build(n_rows: int, ptr, col, val, C: int = 64, sigma: int = 1024, ki: int = 2):
+    lib = host_lib()
+    ns, stored = _c_i64(), _c_i64()
+    _check_host(lib.spmv_sell_plan(n_rows, _ptr(ptr), C, sigma, ki, ctypes.byref(ns), ctypes.byref(stored)), "sell_plan")
+    sp = np.empty(ns.value + 1, np.int64)
+    perm = np.empty(max(ns.value * C, 1), np.int32)
+    scol = np.empty(max(stored.value, 1), np.int32)
+    sval = np.empty(max(stored.value, 1), np.float64)
+    _check_host(lib.spmv_sell_fill(n_rows, _ptr(ptr), _ptr(col), _ptr(val), C, sigma, ki, ns.value,
+                                   _ptr(sp), _ptr(perm), _ptr(scol), _ptr(sval)), "sell_fill")
+    return dict(C=C, sigma=sigma, ki=ki, n_slices=ns.value, slice_ptr=sp, perm=perm, col=scol,
+                val=sval, stored=stored.value)
+
+
+def cmrs_build(n_rows: int, ptr, h: int = 8):
+    ns = (n_rows + h - 1) // h
+    sp = np.empty(ns + 1, np.int64)
+    rin = np.empty(max(int(ptr[-1]), 1), np.uint8)
+    _check_host(host_lib().spmv_cmrs_build(n_rows, _ptr(ptr), h, _ptr(sp), _ptr(rin)), "cmrs_build")
+    return dict(h=h, n_strips=ns, strip_ptr=sp, row_in_strip=rin)
+
+
+def bytes_alg(n_rows: int, n_cols: int, nnz: int) -> int:
+    """Algorithmic bytes of one SpMV: fp64 values + int32
+    columns + int32 row offsets + x read once + y written once."""
+    return 12 * nnz + 4 * (n_rows + 1) + 8 * n_cols + 8 * n_rows
+
+
+def check(m: Coo, x: np.ndarray, y: np.ndarray, rel_tol: float = 1e-6, abs_tol: float = 0.0):
+    """Host check_result (reference inc/helper_functions.h:184-236)
+    -> (bad_rows, first_bad)."""
+    first = _c_i64()
+    ref = ctypes.c_double()
+    bad = host_lib().spmv_check(m.n_rows, m.nnz, _ptr(m.row), _ptr(m.col), _ptr(m.val), _ptr(x), _ptr(y),
+                                abs_tol, rel_tol, ctypes.byref(first), ctypes.byref(ref))
+    return int(bad), int(first.value)
+
+
+# ------------------------------------------------------------- device
+def _torch():
+    import torch
+
+    return torch
+
+
+def _dev_tensor(arr: np.ndarray, device):
+    torch = _torch()
+    return torch.from_numpy(np.ascontiguousarray(arr)).to(device)
+
+
+@dataclass
+class DeviceMatrix:
+    """One format resident in HBM, ready for repeated SpMV launches."""
+
+    fmt: str
+    n_rows: int
+    n_cols: int
+    nnz: int
+    device: object
+    arrays: dict = field(default_factory=dict)
+    params: dict = field(default_factory=dict)
+    stored_bytes: int = 0
+
+    @property
+    def bytes_alg(self) -> int:
+        return bytes_alg(self.n_rows, self.n_cols, self.nnz)
+
+    def dims(self, stream=None) -> Dims:
+        torch = _torch()
+        dev = torch.device(self.device)
+        if stream is None:
+            stream = torch.cuda.current_stream(dev)
+        return Dims(self.n_rows, self.n_cols, self.nnz, dev.index or 0, stream.cuda_stream)
+
+    def run(self, x, y, stream=None) -> None:
+        """y = A x on `stream` (default: torch's current stream)."""
+        lib = hip_lib()
+        d = self.dims(stream)
+        a = self.arrays
+        p = self.params
+        if x.dtype != _torch().float64 or y.dtype != _torch().float64:
+            raise SpmvError(OTHER_ERROR, "run", "x and y must be float64")
+        if x.numel() < self.n_cols or y.numel() < self.n_rows:
+            raise SpmvError(OTHER_ERROR, "run", "x or y too short")
+        if self.fmt == "coo":
+            rc = lib.spmv_coo_run(d, _ptr(a["row"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
+                                  _ptr(a["ws"]), a["ws"].numel())
+        elif self.fmt == "csr":
+            rc = lib.spmv_csr_run(d, _ptr(a["row_ptr"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
+                                  p["lanes"])
+        elif self.fmt == "ell":
+            rc = lib.spmv_ell_run(d, p["K"], p["ld"], p["ki"], _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y))
+        elif self.fmt == "sell":
+            rc = lib.spmv_sell_run(d, p["C"], p["ki"], p["n_slices"], _ptr(a["slice_ptr"]), _ptr(a["perm"]),
+                                   _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y))
+        elif self.fmt == "cmrs":
+            rc = lib.spmv_cmrs_run(d, p["h"], p["n_strips"], _ptr(a["strip_ptr"]), _ptr(a["row_in_strip"]),
+                                   _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y))
+        else:
+            raise SpmvError(OTHER_ERROR, "run", f"unknown format {self.fmt}")
+        _check(rc, f"spmv_{self.fmt}_run")
+
+
+def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, ki: int = 2, C: int = 64,
+              sigma: int = 1024, h: int = 8, ell_max_padding: float | None = 64.0) -> DeviceMatrix:
+    """Build `fmt` on the host (libspmv_host.so) and upload it."""
+    torch = _torch()
+    device = torch.device(device)
+    dm = DeviceMatrix(fmt, m.n_rows, m.n_cols, m.nnz, device)
+    if fmt == "coo":
+        row, col, val = coo_sort_by_row(m)
+        ws_bytes = hip_lib().spmv_coo_ws_bytes(m.nnz)
+        dm.arrays = dict(row=_dev_tensor(row, device), col=_dev_tensor(col, device),
+                         val=_dev_tensor(val, device),
+                         ws=torch.empty(ws_bytes, dtype=torch.uint8, device=device))
+        dm.stored_bytes = 16 * m.nnz
+        return dm
+    ptr, col, val = csr_from_coo(m)
+    if fmt == "csr":
+        L = lanes or hip_lib().spmv_csr_auto_lanes(m.n_rows, m.nnz)
+        dm.params = dict(lanes=L)
+        dm.arrays = dict(row_ptr=_dev_tensor(ptr, device), col=_dev_tensor(col, device),
+                         val=_dev_tensor(val, device))
+        dm.stored_bytes = 12 * m.nnz + 8 * (m.n_rows + 1)
+    elif fmt == "ell":
+        e = ell_build(m.n_rows, ptr, col, val, ki=ki, max_padding=ell_max_padding)
+        dm.params = dict(K=e["K"], ld=e["ld"], ki=ki, stored=e["stored"])
+        dm.arrays = dict(col=_dev_tensor(e["col"], device), val=_dev_tensor(e["val"], device))
+        dm.stored_bytes = 12 * e["stored"]
+    elif fmt == "sell":
+        s = sell_build(m.n_rows, ptr, col, val, C=C, sigma=sigma, ki=ki)
+        dm.params = dict(C=C, sigma=sigma, ki=ki, n_slices=s["n_slices"], stored=s["stored"])
+        dm.arrays = dict(slice_ptr=_dev_tensor(s["slice_ptr"], device), perm=_dev_tensor(s["perm"], device),
+                         col=_dev_tensor(s["col"], device), val=_dev_tensor(s["val"], device))
+        dm.stored_bytes = 12 * s["stored"] + 8 * (s["n_slices"] + 1) + 4 * s["n_slices"] * C
+    elif fmt == "cmrs":
+        c = cmrs_build(m.n_rows, ptr, h=h)
+        dm.params = dict(h=h, n_strips=c["n_strips"])
+        dm.arrays = dict(strip_ptr=_dev_tensor(c["strip_ptr"], device),
+                         row_in_strip=_dev_tensor(c["row_in_strip"], device),
+                         col=_dev_tensor(col, device), val=_dev_tensor(val, device))
+        dm.stored_bytes = 13 * m.nnz + 8 * (c["n_strips"] + 1)
+    else:
+        raise SpmvError(OTHER_ERROR, "to_device", f"unknown format {fmt}")
+    return dm
+
+
+def flush_cache(stream=None, nbytes: int = 0) -> None:
+    """Evict the 256 MiB Infinity Cache + L2s (512 MiB scratch write)."""
+    torch = _torch()
+    s = stream if stream is not None else torch.cuda.current_stream()
+    _check(hip_lib().spmv_flush_cache(s.cuda_stream, nbytes), "spmv_flush_cache")
+
+
+def device_name(device: int = 0) -> str:
+    buf = ctypes.create_string_buffer(256)
+    _check(hip_lib().spmv_device_name(device, buf, 256), "spmv_device_name")
+    return buf.value.decode()

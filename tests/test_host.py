@@ -1,0 +1,216 @@
+"""Host side of the product (libspmv_host.so) on a CPU-only machine.
+
+The reader must accept/reject exactly like the oracle (the reference's
+rules), every builder must lay the matrix out so that its CPU loop gives
+the oracle's y, and the generators must be deterministic with the
+documented sizes.  The HIP kernels read the same arrays (tests/test_gpu_*).
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import spmv_amd as sa
+from conftest import GOLDEN, golden_cases
+from oracle import oracle
+
+CASES = [c["name"] for c in golden_cases()]
+
+
+def _both(name):
+    m = sa.read_mtx(GOLDEN / f"{name}.mtx")
+    n, mc, r, c, v, sym = oracle.read_mtx(GOLDEN / f"{name}.mtx")
+    return m, (n, mc, r, c, v, sym)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_reader_matches_oracle_bit_exact(name):
+    m, (n, mc, r, c, v, sym) = _both(name)
+    assert (m.n_rows, m.n_cols, m.symmetric) == (n, mc, sym)
+    assert np.array_equal(m.row, r) and np.array_equal(m.col, c)
+    assert np.array_equal(m.val.view(np.uint64), v.view(np.uint64))  # same strtod rounding
+
+
+def test_reader_rejections(tmp_path):
+    bad = {
+        "complex.mtx": "%%MatrixMarket matrix coordinate complex general\n2 2 1\n1 1 1.0 0.0\n",
+        "array.mtx": "%%MatrixMarket matrix array real general\n2 2\n1\n2\n3\n4\n",
+        "nobanner.mtx": "2 2 1\n1 1 1.0\n",
+        "short.mtx": "%%MatrixMarket matrix coordinate real general\n2 2 3\n1 1 1.0\n",
+        "range.mtx": "%%MatrixMarket matrix coordinate real general\n2 2 1\n3 1 1.0\n",
+        "zero_index.mtx": "%%MatrixMarket matrix coordinate real general\n2 2 1\n0 1 1.0\n",
+        "badtype.mtx": "%%MatrixMarket matrix coordinate quaternion general\n2 2 1\n1 1 1.0\n",
+    }
+    for name, text in bad.items():
+        p = tmp_path / name
+        p.write_text(text)
+        with pytest.raises(sa.SpmvError) as e:
+            sa.read_mtx(p)
+        assert e.value.rc == sa.FILE_ERROR, name
+    with pytest.raises(sa.SpmvError) as e:
+        sa.read_mtx(tmp_path / "missing.mtx")
+    assert e.value.rc == sa.FILE_ERROR
+
+
+def test_reader_case_insensitive_banner(tmp_path):
+    p = tmp_path / "upper.mtx"
+    p.write_text("%%MatrixMarket MATRIX Coordinate REAL General\n2 2 2\n1 1 1.5\n2 2 -2e3\n")
+    m = sa.read_mtx(p)
+    assert m.val.tolist() == [1.5, -2000.0]
+
+
+def test_write_read_roundtrip(tmp_path):
+    m = sa.gen_random(300, 200, 0, 9, seed=11)
+    sa.write_mtx(tmp_path / "rt.mtx", m)
+    m2 = sa.read_mtx(tmp_path / "rt.mtx")
+    assert np.array_equal(m.row, m2.row) and np.array_equal(m.col, m2.col)
+    assert np.array_equal(m.val, m2.val)  # %.17g is exact
+
+
+def _y_gold(name):
+    return np.load(GOLDEN / f"{name}.y.npy")
+
+
+def _cpu_fmt(m, fmt, **kw):
+    """Build `fmt` with the product builders and run the product CPU loop."""
+    L = sa.host_lib()
+    x = sa.ramp_x(m.n_cols)
+    y = np.full(max(m.n_rows, 1), np.nan)
+    ptr, col, val = sa.csr_from_coo(m)
+    if fmt == "coo":
+        r, c, v = sa.coo_sort_by_row(m)
+        L.spmv_cpu_coo(m.n_rows, m.nnz, sa._ptr(r), sa._ptr(c), sa._ptr(v), sa._ptr(x), sa._ptr(y), 2)
+    elif fmt == "csr":
+        L.spmv_cpu_csr(m.n_rows, sa._ptr(ptr), sa._ptr(col), sa._ptr(val), sa._ptr(x), sa._ptr(y), 2)
+    elif fmt == "ell":
+        e = sa.ell_build(m.n_rows, ptr, col, val, ki=kw.get("ki", 2))
+        L.spmv_cpu_ell(m.n_rows, e["K"], e["ld"], e["ki"], sa._ptr(e["col"]), sa._ptr(e["val"]), sa._ptr(x),
+                       sa._ptr(y), 2)
+    elif fmt == "sell":
+        s = sa.sell_build(m.n_rows, ptr, col, val, C=kw.get("C", 64), sigma=kw.get("sigma", 1024),
+                          ki=kw.get("ki", 2))
+        L.spmv_cpu_sell(m.n_rows, s["C"], s["ki"], s["n_slices"], sa._ptr(s["slice_ptr"]), sa._ptr(s["perm"]),
+                        sa._ptr(s["col"]), sa._ptr(s["val"]), sa._ptr(x), sa._ptr(y), 2)
+    elif fmt == "cmrs":
+        c = sa.cmrs_build(m.n_rows, ptr, h=kw.get("h", 8))
+        L.spmv_cpu_cmrs(m.n_rows, c["h"], c["n_strips"], sa._ptr(c["strip_ptr"]), sa._ptr(c["row_in_strip"]),
+                        sa._ptr(col), sa._ptr(val), sa._ptr(x), sa._ptr(y), 2)
+    return y[: m.n_rows], x
+
+
+FMT_PARAMS = [
+    ("coo", {}),
+    ("csr", {}),
+    ("ell", {"ki": 1}),
+    ("ell", {"ki": 2}),
+    ("sell", {"C": 64, "sigma": 1024, "ki": 2}),
+    ("sell", {"C": 64, "sigma": 1, "ki": 1}),
+    ("sell", {"C": 32, "sigma": 1, "ki": 1}),  # the reference's configuration
+    ("sell", {"C": 128, "sigma": 256, "ki": 2}),
+    ("cmrs", {"h": 8}),
+    ("cmrs", {"h": 1}),
+    ("cmrs", {"h": 64}),
+]
+
+
+@pytest.mark.parametrize("fmt,kw", FMT_PARAMS, ids=[f"{f}-{'-'.join(f'{k}{v}' for k, v in kw.items())}" for f, kw in FMT_PARAMS])
+@pytest.mark.parametrize("name", CASES)
+def test_builders_cpu_loops_match_oracle(name, fmt, kw):
+    m = sa.read_mtx(GOLDEN / f"{name}.mtx")
+    y, x = _cpu_fmt(m, fmt, **kw)
+    y_ref = oracle.file_order_spmv(m.n_rows, m.row, m.col, m.val, x)
+    assert oracle.parity(y, y_ref, m.row, m.col, m.val, x, m.n_rows).size == 0
+    assert oracle.parity(y, _y_gold(name), m.row, m.col, m.val, x, m.n_rows).size == 0
+
+
+def test_sell_layout_properties():
+    m = sa.gen_random(1000, 1000, 0, 40, seed=5)
+    ptr, col, val = sa.csr_from_coo(m)
+    s = sa.sell_build(m.n_rows, ptr, col, val, C=64, sigma=256, ki=2)
+    perm = s["perm"][: s["n_slices"] * 64]
+    real = perm[perm >= 0]
+    assert np.array_equal(np.sort(real), np.arange(m.n_rows))  # a permutation
+    lens = np.diff(ptr)
+    for w in range(0, m.n_rows, 256):  # sorted by length, descending, per window
+        win = perm[w: w + 256]
+        win = win[win >= 0]
+        assert np.all(np.diff(lens[win]) <= 0)
+        assert set(win.tolist()) == set(range(w, min(w + 256, m.n_rows)))
+    widths = np.diff(s["slice_ptr"]) // 64
+    assert np.all(widths % 2 == 0)
+    assert s["slice_ptr"][-1] == s["stored"]
+
+
+def test_padding_reuses_row_column():
+    m = sa.gen_random(200, 500, 1, 20, seed=9)
+    ptr, col, val = sa.csr_from_coo(m)
+    e = sa.ell_build(m.n_rows, ptr, col, val, ki=2)
+    K, ld = e["K"], e["ld"]
+    for i in range(m.n_rows):
+        cols_i = set(col[ptr[i]:ptr[i + 1]].tolist())
+        for k in range(K):
+            pos = (k // 2) * ld * 2 + i * 2 + (k % 2)
+            if k >= ptr[i + 1] - ptr[i]:
+                assert e["val"][pos] == 0.0
+                assert e["col"][pos] in cols_i
+
+
+def test_cmrs_row_in_strip():
+    m = sa.gen_random(103, 50, 0, 7, seed=4)
+    ptr, col, val = sa.csr_from_coo(m)
+    c = sa.cmrs_build(m.n_rows, ptr, h=8)
+    assert c["n_strips"] == 13
+    for s in range(c["n_strips"]):
+        b, e = c["strip_ptr"][s], c["strip_ptr"][s + 1]
+        rin = c["row_in_strip"][b:e]
+        assert np.all(np.diff(rin.astype(int)) >= 0) and (rin.size == 0 or rin.max() < 8)
+
+
+def test_coo_sort_is_stable():
+    m = sa.read_mtx(GOLDEN / "colmajor.mtx")
+    r, c, v = sa.coo_sort_by_row(m)
+    order = np.argsort(m.row, kind="stable")
+    assert np.array_equal(r, m.row[order]) and np.array_equal(c, m.col[order])
+    assert np.array_equal(v, m.val[order])
+
+
+def test_cantlike_counts_and_symmetry():
+    m = sa.gen_cantlike(0)
+    assert (m.n_rows, m.nnz) == (62451, 4007383)  # SuiteSparse cant's N and nnz
+    assert np.all(np.diff(m.row) >= 0)
+    lo = sa.gen_cantlike(2)
+    assert lo.nnz == 2034917 and lo.symmetric and np.all(lo.row >= lo.col)
+    t = sa.gen_cantlike(1)
+    assert np.all(np.diff(t.col) >= 0)  # column-major order
+    # symmetric pattern + values: A == A^T
+    import scipy.sparse as sp
+
+    A = sp.coo_matrix((m.val, (m.row, m.col)), shape=(m.n_rows, m.n_rows)).tocsr()
+    assert abs(A - A.T).max() == 0.0
+    two = sa.gen_cantlike(0, copies=2)
+    assert two.n_rows == 2 * 62451 and two.nnz == 2 * 4007383
+    assert np.array_equal(two.row[m.nnz:] - 62451, m.row)
+
+
+def test_generators_deterministic():
+    a = sa.gen_rmat(100_000, 1_000_000, scale=17, seed=1)
+    b = sa.gen_rmat(100_000, 1_000_000, scale=17, seed=1)
+    assert np.array_equal(a.row, b.row) and np.array_equal(a.col, b.col) and np.array_equal(a.val, b.val)
+    assert a.row.max() < 100_000 and a.col.max() < 100_000 and a.row.min() >= 0
+    deg = np.bincount(a.row, minlength=100_000)
+    assert deg.max() > 20 * deg.mean()  # R-MAT skew
+    assert np.all((a.val >= -1) & (a.val < 1))
+    ptr, col, val = sa.gen_banded_csr(1000, 10, 20)
+    assert ptr.tolist() == list(range(0, 161, 16))
+    assert col[:16].tolist() == [(10 + o) % 1000 for o in range(-8, 8)]
+    p2, c2, v2 = sa.gen_banded_csr(1000)
+    assert np.array_equal(v2[160:320], val)  # row-range generation = slice of the whole
+
+
+def test_check_function():
+    m = sa.read_mtx(GOLDEN / "hand3.mtx")
+    x = sa.ramp_x(3)
+    assert sa.check(m, x, np.array([4.0, 3.0, 17.0])) == (0, -1)
+    bad, first = sa.check(m, x, np.array([4.0, 3.1, 17.0]))
+    assert bad == 1 and first == 1
+    assert sa.check(m, x, np.array([4.0, 3.0, np.nan]))[0] == 1

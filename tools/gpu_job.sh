@@ -1,0 +1,33 @@
+#!/usr/bin/env bash
+# GPU-box job: smoke, GPU parity tests, bench, rocprofv3 kernel-trace.
+# Each GPU step has its own time limit; a crash/timeout/abort stops the job
+# (exit codes 124/137 timeout, 134 abort, 139 segfault), plain test
+# failures (exit 1) do not stop the later measurement steps.
+# usage: tools/gpu_job.sh [steps...]   steps: smoke tests bench prof pmc
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+steps=("$@")
+[ ${#steps[@]} -eq 0 ] && steps=(smoke tests bench prof)
+fatal() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
+run() { # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  echo "=== $name: $*" | tee -a gpurun_out/job.log
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name exit $rc" | tee -a gpurun_out/job.log
+  tail -5 "gpurun_out/$name.log"
+  if fatal $rc; then echo "fatal exit $rc in $name: stopping"; exit $rc; fi
+  return 0
+}
+for s in "${steps[@]}"; do
+  case $s in
+    smoke) run smoke 400 python -c "import __graft_entry__ as g; g.smoke()";;
+    tests) run gpu_tests 1500 python -m pytest tests -m gpu -x -q;;
+    testsq) run gpu_tests 1500 python -m pytest tests -m gpu -q;;
+    bench) run bench 900 python bench.py;;
+    prof) run prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --profile --steps 200;;
+    *) echo "unknown step $s";;
+  esac
+done

@@ -96,6 +96,15 @@ int spmv_sell_fill(int64_t n_rows, const int64_t *row_ptr, const int32_t *col,
 int spmv_cmrs_build(int64_t n_rows, const int64_t *row_ptr, int32_t h,
                     int64_t *strip_ptr, uint8_t *row_in_strip);
 
+/* ----------------------------------------------------- multi-GPU shard ---
+ * Row-range partition for one process per GPU: `parts`
+ * contiguous ranges [bounds[p], bounds[p+1]) holding about nnz/parts
+ * entries each; every inner boundary is a multiple of `align` (use the
+ * SELL sigma, 1024, so sorting windows never straddle two GPUs).
+ * bounds has parts+1 entries, bounds[0] = 0, bounds[parts] = n_rows.    */
+int spmv_partition_rows(int64_t n_rows, const int64_t *row_ptr, int parts,
+                        int64_t align, int64_t *bounds);
+
 /* ---------------------------------------------------------- CPU loops ---
  * OpenMP restatements of the reference's compute_using_cpu loops, with
  * zero-initialised output (the reference accumulated into malloc'd

@@ -312,3 +312,36 @@ int spmv_cmrs_build(int64_t n_rows, const int64_t *row_ptr, int32_t h,
             row_in_strip[j] = (uint8_t)(r % h);
     return SPMV_SUCCESS;
 }
+
+/* ------------------------------------------------------------ sharding */
+
+int spmv_partition_rows(int64_t n_rows, const int64_t *row_ptr, int parts,
+                        int64_t align, int64_t *bounds)
+{
+    if (parts < 1 || n_rows < 0 || align < 1)
+        return SPMV_OTHER_ERROR;
+    const int64_t nnz = row_ptr[n_rows];
+    bounds[0] = 0;
+    for (int p = 1; p < parts; ++p) {
+        /* first row whose start offset reaches p/parts of the entries */
+        int64_t target = (int64_t)((double)nnz * p / parts);
+        int64_t lo = 0, hi = n_rows;
+        while (lo < hi) {
+            int64_t mid = lo + (hi - lo) / 2;
+            if (row_ptr[mid] < target)
+                lo = mid + 1;
+            else
+                hi = mid;
+        }
+        int64_t b = (lo + align / 2) / align * align;
+        if (nnz == 0)
+            b = (n_rows * p / parts) / align * align;
+        if (b < bounds[p - 1])
+            b = bounds[p - 1];
+        if (b > n_rows)
+            b = n_rows;
+        bounds[p] = b;
+    }
+    bounds[parts] = n_rows;
+    return SPMV_SUCCESS;
+}

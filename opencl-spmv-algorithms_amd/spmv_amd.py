@@ -112,6 +112,7 @@ HOST_SYMBOLS = {
     "spmv_sell_plan": (ctypes.c_int, [_c_i64, _vp, _c_i32, _c_i32, _c_i32, ctypes.POINTER(_c_i64), ctypes.POINTER(_c_i64)]),
     "spmv_sell_fill": (ctypes.c_int, [_c_i64, _vp, _vp, _vp, _c_i32, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, _vp]),
     "spmv_cmrs_build": (ctypes.c_int, [_c_i64, _vp, _c_i32, _vp, _vp]),
+    "spmv_partition_rows": (ctypes.c_int, [_c_i64, _vp, ctypes.c_int, _c_i64, _vp]),
     "spmv_cpu_coo": (ctypes.c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, ctypes.c_int]),
     "spmv_cpu_csr": (ctypes.c_int, [_c_i64, _vp, _vp, _vp, _vp, _vp, ctypes.c_int]),
     "spmv_cpu_ell": (ctypes.c_int, [_c_i64, _c_i32, _c_i64, _c_i32, _vp, _vp, _vp, _vp, ctypes.c_int]),
@@ -332,6 +333,21 @@ def cmrs_build(n_rows: int, ptr, h: int = 8):
     rin = np.empty(max(int(ptr[-1]), 1), np.uint8)
     _check_host(host_lib().spmv_cmrs_build(n_rows, _ptr(ptr), h, _ptr(sp), _ptr(rin)), "cmrs_build")
     return dict(h=h, n_strips=ns, strip_ptr=sp, row_in_strip=rin)
+
+
+def partition_rows(n_rows: int, ptr: np.ndarray, parts: int, align: int = 1024) -> np.ndarray:
+    """Contiguous row ranges with ~nnz/parts entries each."""
+    bounds = np.empty(parts + 1, np.int64)
+    _check_host(host_lib().spmv_partition_rows(n_rows, _ptr(ptr), parts, align, _ptr(bounds)), "partition_rows")
+    return bounds
+
+
+def shard(m: Coo, lo: int, hi: int) -> Coo:
+    """Rows [lo, hi) of m as a local matrix (row ids rebased, columns kept:
+    x stays replicated)."""
+    sel = (m.row >= lo) & (m.row < hi)
+    return Coo(hi - lo, m.n_cols, (m.row[sel] - lo).astype(np.int32), m.col[sel], m.val[sel], m.symmetric,
+               f"{m.label} rows [{lo},{hi})")
 
 
 def bytes_alg(n_rows: int, n_cols: int, nnz: int) -> int:

@@ -1,0 +1,106 @@
+"""Multi-process row sharding on CPU with gloo, world 2.
+
+Each rank takes its contiguous row range from spmv_partition_rows, builds
+its shard, computes y_shard with the product's CPU loop (the device
+kernel reads the same arrays; on the GPU box bench.py runs the same
+split over RCCL), and the shards are concatenated with an all-gather
+padded to the largest shard — the exchange step of the path.  The
+gathered y must equal the oracle's y for the whole matrix.
+"""
+from __future__ import annotations
+
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+import spmv_amd as sa
+from conftest import GOLDEN, PKG, REPO
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, case, fmt, q):
+    sys.path[:0] = [str(PKG), str(REPO)]
+    import torch
+    import torch.distributed as dist
+
+    import spmv_amd as sa
+    from oracle import oracle
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        if case == "cantlike":
+            m = sa.gen_cantlike(0)
+        elif case == "rmat":
+            m = sa.gen_rmat(200_000, 2_000_000, scale=18, seed=3)
+        else:
+            m = sa.read_mtx(GOLDEN / f"{case}.mtx")
+        ptr, _, _ = sa.csr_from_coo(m)
+        bounds = sa.partition_rows(m.n_rows, ptr, world, align=64)
+        lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+        loc = sa.shard(m, lo, hi)
+        x = sa.ramp_x(m.n_cols)  # replicated
+        y = np.zeros(max(loc.n_rows, 1))
+        L = sa.host_lib()
+        lptr, lcol, lval = sa.csr_from_coo(loc)
+        if fmt == "csr":
+            L.spmv_cpu_csr(loc.n_rows, sa._ptr(lptr), sa._ptr(lcol), sa._ptr(lval), sa._ptr(x), sa._ptr(y), 1)
+        else:
+            s = sa.sell_build(loc.n_rows, lptr, lcol, lval, C=64, sigma=1024 if loc.n_rows >= 1024 else 64, ki=2)
+            L.spmv_cpu_sell(loc.n_rows, 64, 2, s["n_slices"], sa._ptr(s["slice_ptr"]), sa._ptr(s["perm"]),
+                            sa._ptr(s["col"]), sa._ptr(s["val"]), sa._ptr(x), sa._ptr(y), 1)
+        # all-gather of y shards, padded to the largest shard
+        sizes = np.diff(bounds)
+        pad = int(sizes.max()) if sizes.size else 0
+        buf = torch.zeros(max(pad, 1), dtype=torch.float64)
+        buf[: loc.n_rows] = torch.from_numpy(y[: loc.n_rows])
+        out = [torch.zeros_like(buf) for _ in range(world)]
+        dist.all_gather(out, buf)
+        y_full = np.concatenate([out[r][: sizes[r]].numpy() for r in range(world)])
+        y_ref = oracle.file_order_spmv(m.n_rows, m.row, m.col, m.val, x)
+        bad = oracle.parity(y_full, y_ref, m.row, m.col, m.val, x, m.n_rows)
+        q.put((rank, int(bad.size), lo, hi, int(loc.nnz)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case,fmt", [("cantlike", "csr"), ("cantlike", "sell"), ("rmat", "csr"),
+                                      ("empty_rows", "csr"), ("n67", "sell"), ("all_empty", "csr")])
+def test_two_rank_shard_allgather(case, fmt):
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, case, fmt, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(180)
+        assert p.exitcode == 0
+    res = sorted(q.get() for _ in range(2))
+    assert all(bad == 0 for _, bad, *_ in res)
+    assert res[0][3] == res[1][2]  # contiguous ranges
+
+
+def test_partition_balances_entries():
+    m = sa.gen_rmat(100_000, 1_000_000, scale=17, seed=2)
+    ptr, _, _ = sa.csr_from_coo(m)
+    for parts in (1, 2, 4, 8):
+        b = sa.partition_rows(m.n_rows, ptr, parts, align=1024)
+        assert b[0] == 0 and b[-1] == m.n_rows and np.all(np.diff(b) >= 0)
+        assert np.all(b[1:-1] % 1024 == 0)
+        nnz = np.diff(ptr[b])
+        assert nnz.max() <= 1.1 * m.nnz / parts + 1024 * 200
+    b = sa.partition_rows(10, np.zeros(11, np.int64), 4, align=1)
+    assert b.tolist() == [0, 2, 5, 7, 10]

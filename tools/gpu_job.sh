@@ -28,6 +28,10 @@ for s in "${steps[@]}"; do
     testsq) run gpu_tests 1500 python -m pytest tests -m gpu -q;;
     bench) run bench 900 python bench.py;;
     prof) run prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --profile --steps 200;;
+    sweep) run sweep 600 python tools/sweep.py;;
+    sweep0) SPMV_XCD_REMAP=0 run sweep_noremap 600 python tools/sweep.py --rounds 2;;
+    sweeprmat) run sweep_rmat 600 python tools/sweep.py --matrix rmat --rounds 2 --reps 20;;
+    counters) run counters 120 rocprofv3 -L;;
     *) echo "unknown step $s";;
   esac
 done

@@ -1,0 +1,85 @@
+#!/usr/bin/env python3
+"""Kernel-variant sweep on the bench workload (B cant-like copies).
+
+Prints one line per variant: mean kernel ms over back-to-back launches
+(HIP events on the launch stream), effective GB/s of algorithmic bytes,
+and GB/s of stored bytes.  Variants are interleaved over rounds in ONE
+process (cdna_hip_programming.md §5.4 rule 24).
+    python tools/sweep.py [--copies 32] [--rounds 3] [--matrix cantlike|rmat]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+from pathlib import Path
+
+import numpy as np
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(REPO / "opencl-spmv-algorithms_amd"), str(REPO)]
+import spmv_amd as sa  # noqa: E402
+
+VARIANTS = [
+    ("csr", {"lanes": 4}), ("csr", {"lanes": 8}), ("csr", {"lanes": 16}), ("csr", {"lanes": 32}),
+    ("csr", {"lanes": 64}),
+    ("ell", {"ki": 1}), ("ell", {"ki": 2}),
+    ("sell", {"C": 64, "sigma": 1, "ki": 2}), ("sell", {"C": 64, "sigma": 256, "ki": 2}),
+    ("sell", {"C": 64, "sigma": 1024, "ki": 2}), ("sell", {"C": 64, "sigma": 1024, "ki": 1}),
+    ("sell", {"C": 128, "sigma": 1024, "ki": 2}), ("sell", {"C": 32, "sigma": 1, "ki": 1}),
+    ("cmrs", {"h": 4}), ("cmrs", {"h": 8}), ("cmrs", {"h": 16}), ("cmrs", {"h": 32}),
+    ("coo", {}),
+]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--copies", type=int, default=32)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--matrix", default="cantlike")
+    ap.add_argument("--only", default="")
+    a = ap.parse_args()
+    import torch
+
+    dev = torch.device("cuda:0")
+    m = sa.gen_cantlike(0, a.copies) if a.matrix == "cantlike" else sa.gen_rmat()
+    b = sa.bytes_alg(m.n_rows, m.n_cols, m.nnz)
+    x = torch.from_numpy(sa.ramp_x(m.n_cols)).to(dev)
+    y = torch.empty(m.n_rows, dtype=torch.float64, device=dev)
+    variants = [v for v in VARIANTS if not a.only or v[0] in a.only.split(",")]
+    if a.matrix != "cantlike":
+        variants = [v for v in variants if v[0] != "ell"]
+    res = {i: [] for i in range(len(variants))}
+    stored = {}
+    for r in range(a.rounds):
+        for i, (fmt, kw) in enumerate(variants):
+            dm = sa.to_device(m, fmt, dev, **kw)
+            stored[i] = dm.stored_bytes
+            s = torch.cuda.current_stream()
+            for _ in range(5):
+                dm.run(x, y, s)
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(a.reps + 1)]
+            ev[0].record(s)
+            for k in range(a.reps):
+                dm.run(x, y, s)
+                ev[k + 1].record(s)
+            torch.cuda.synchronize()
+            res[i].append(float(np.mean([ev[k].elapsed_time(ev[k + 1]) for k in range(a.reps)])))
+            del dm
+            torch.cuda.empty_cache()
+    out = []
+    for i, (fmt, kw) in enumerate(variants):
+        ms = float(np.median(res[i]))
+        row = dict(fmt=fmt, **kw, ms=round(ms, 5), GBs_alg=round(b / ms * 1e-6, 1),
+                   GBs_stored=round(stored[i] / ms * 1e-6, 1), frac=round(b / ms * 1e-6 / 8000, 4),
+                   spread=round((max(res[i]) - min(res[i])) / ms, 4))
+        out.append(row)
+        print(json.dumps(row), flush=True)
+    print(json.dumps({"matrix": a.matrix, "copies": a.copies, "bytes_alg": b,
+                      "xcd_remap": os.environ.get("SPMV_XCD_REMAP", "1")}))
+
+
+if __name__ == "__main__":
+    main()

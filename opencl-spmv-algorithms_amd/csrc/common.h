@@ -29,7 +29,7 @@ class DeviceGuard {
     int rc_ = SPMV_SUCCESS;
 };
 
-// Blocks per XCD remap switch (SPMV_XCD_REMAP=0 disables; read once).
+// XCD-contiguous blockIdx remap switch (SPMV_XCD_REMAP=1 enables; read once).
 bool xcd_remap_enabled();
 
 // ------------------------------------------------------- device helpers

@@ -11,11 +11,13 @@
 //   * the L partial sums are combined with cross-lane shuffles
 //     (__shfl_xor butterflies inside the L-lane group).
 // Bytes per row: 12·len + 8 (row_ptr) + 8 (y), plus x gathers.
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace spmv {
 
-template <int L>
+template <int L, bool PAIR>
 __global__ __launch_bounds__(kBlock) void csr_vector_kernel(
     int64_t n_rows, const int64_t *__restrict__ row_ptr,
     const int32_t *__restrict__ col, const double *__restrict__ val,
@@ -37,6 +39,38 @@ __global__ __launch_bounds__(kBlock) void csr_vector_kernel(
     const int64_t beg = s_ptr[g], end = s_ptr[g + 1];  // empty past n_rows
 
     double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    if constexpr (PAIR) {
+        // 16-byte loads: lane reads the aligned pair (p, p+1); entries of
+        // the pair outside [beg, end) are zeroed by value (their column is
+        // a valid neighbour column, so the gather stays in bounds).  The
+        // last pair of the row is loaded as a scalar when p+1 == end, so
+        // nothing past val[nnz-1] is ever read.
+        int64_t p = (beg & ~(int64_t)1) + 2 * lane;
+        for (; p + 1 + 2 * L < end; p += 4 * L) {
+            const double2 va = *reinterpret_cast<const double2 *>(val + p);
+            const int2 ca = *reinterpret_cast<const int2 *>(col + p);
+            const double2 vb = *reinterpret_cast<const double2 *>(val + p + 2 * L);
+            const int2 cb = *reinterpret_cast<const int2 *>(col + p + 2 * L);
+            s0 += (p >= beg ? va.x : 0.0) * x[ca.x];
+            s1 += va.y * x[ca.y];
+            s2 += vb.x * x[cb.x];
+            s3 += vb.y * x[cb.y];
+        }
+        for (; p < end; p += 2 * L) {
+            if (p + 1 < end) {
+                const double2 va = *reinterpret_cast<const double2 *>(val + p);
+                const int2 ca = *reinterpret_cast<const int2 *>(col + p);
+                s0 += (p >= beg ? va.x : 0.0) * x[ca.x];
+                s1 += va.y * x[ca.y];
+            } else if (p >= beg) {
+                s0 += val[p] * x[col[p]];
+            }
+        }
+        double sum = group_sum<L>((s0 + s1) + (s2 + s3));
+        if (lane == 0 && row < n_rows)
+            y[row] = sum;
+        return;
+    }
     int64_t j = beg + lane;
     for (; j + 3 * L < end; j += 4 * L) {
         const int32_t c0 = col[j], c1 = col[j + L], c2 = col[j + 2 * L],
@@ -55,6 +89,16 @@ __global__ __launch_bounds__(kBlock) void csr_vector_kernel(
         y[row] = sum;
 }
 
+static bool csr_pair_loads()
+{
+    static int cached = -1;
+    if (cached < 0) {
+        const char *s = getenv("SPMV_CSR_PAIR");
+        cached = (s && s[0] == '0') ? 0 : 1;
+    }
+    return cached == 1;
+}
+
 template <int L>
 static void launch_csr(const spmv_dims &d, const int64_t *row_ptr,
                        const int32_t *col, const double *val, const double *x,
@@ -62,9 +106,15 @@ static void launch_csr(const spmv_dims &d, const int64_t *row_ptr,
 {
     constexpr int RPB = kBlock / L;
     const int64_t blocks = (d.n_rows + RPB - 1) / RPB;
-    hipLaunchKernelGGL(csr_vector_kernel<L>, dim3((unsigned)blocks),
-                       dim3(kBlock), 0, (hipStream_t)d.stream, d.n_rows,
-                       row_ptr, col, val, x, y, xcd_remap_enabled() ? 1 : 0);
+    const int remap = xcd_remap_enabled() ? 1 : 0;
+    if (csr_pair_loads())
+        hipLaunchKernelGGL((csr_vector_kernel<L, true>), dim3((unsigned)blocks),
+                           dim3(kBlock), 0, (hipStream_t)d.stream, d.n_rows,
+                           row_ptr, col, val, x, y, remap);
+    else
+        hipLaunchKernelGGL((csr_vector_kernel<L, false>), dim3((unsigned)blocks),
+                           dim3(kBlock), 0, (hipStream_t)d.stream, d.n_rows,
+                           row_ptr, col, val, x, y, remap);
 }
 
 }  // namespace spmv
@@ -73,11 +123,14 @@ using namespace spmv;
 
 extern "C" int spmv_csr_auto_lanes(int64_t n_rows, int64_t nnz)
 {
-    // One lane per ~4 entries keeps the 4-deep unroll busy on the common
-    // row; rounded to a power of two in [2, 64].
+    // About one lane per 8 entries of the mean row: every lane then runs
+    // ~2 iterations of its 4-deep unrolled body, and the group is small
+    // enough that short rows waste few lanes (mean 64 -> L = 8 measured
+    // best on the cant-like batch, profiles/round1_sweep.md); rounded to a
+    // power of two in [2, 64].
     double mean = n_rows > 0 ? (double)nnz / (double)n_rows : 0.0;
     int L = 2;
-    while (L < 64 && (double)(2 * L) * 4.0 <= mean * 1.5)
+    while (L < 64 && (double)(2 * L) * 8.0 <= mean * 1.5)
         L *= 2;
     return L;
 }

@@ -52,8 +52,11 @@ bool xcd_remap_enabled()
 {
     static int cached = -1;
     if (cached < 0) {
+        // Off by default: on the cant-like batch the round-robin placement
+        // measured 1-2 % faster than the contiguous-per-XCD remap
+        // (profiles/round1_sweep.md).  SPMV_XCD_REMAP=1 turns it on.
         const char *s = getenv("SPMV_XCD_REMAP");
-        cached = (s && s[0] == '0') ? 0 : 1;
+        cached = (s && s[0] == '1') ? 1 : 0;
     }
     return cached == 1;
 }

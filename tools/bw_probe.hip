@@ -1,0 +1,107 @@
+// bw_probe.hip — achievable HBM bandwidth on this MI355X, for the roofline
+// next to the 8 TB/s spec (MI355X_MICROARCH.md quotes 6.29 TB/s for a
+// float4 copy).  Streams a 2 GiB buffer (8x the Infinity Cache) with the
+// access widths the SpMV kernels use and prints one JSON line per kernel.
+// Also the calibration workload for FETCH_SIZE (known bytes per launch).
+//   hipcc --offload-arch=gfx950 -O3 tools/bw_probe.hip -o tools/bw_probe
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#define CHECK(x)                                                              \
+    do {                                                                      \
+        hipError_t e_ = (x);                                                  \
+        if (e_ != hipSuccess) {                                               \
+            fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));          \
+            exit(2);                                                          \
+        }                                                                     \
+    } while (0)
+
+template <typename T>
+__device__ __forceinline__ double fold(T v);
+template <>
+__device__ __forceinline__ double fold(double v) { return v; }
+template <>
+__device__ __forceinline__ double fold(double2 v) { return v.x + v.y; }
+
+// Grid-stride read; one store per thread keeps the loads alive.
+template <typename T, int UNROLL>
+__global__ __launch_bounds__(256) void read_kernel(const T *__restrict__ a, size_t n,
+                                                   double *__restrict__ out)
+{
+    size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const size_t stride = (size_t)gridDim.x * 256;
+    double s = 0.0;
+    for (; i + (UNROLL - 1) * stride < n; i += UNROLL * stride) {
+        T v[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u)
+            v[u] = a[i + u * stride];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u)
+            s += fold(v[u]);
+    }
+    for (; i < n; i += stride)
+        s += fold(a[i]);
+    out[(size_t)blockIdx.x * 256 + threadIdx.x] = s;
+}
+
+__global__ __launch_bounds__(256) void copy_kernel(const double2 *__restrict__ a,
+                                                   double2 *__restrict__ b, size_t n)
+{
+    size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const size_t stride = (size_t)gridDim.x * 256;
+    for (; i < n; i += stride)
+        b[i] = a[i];
+}
+
+template <typename K>
+static double time_ms(K launch, int reps)
+{
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    for (int i = 0; i < 3; ++i)
+        launch();
+    CHECK(hipDeviceSynchronize());
+    CHECK(hipEventRecord(e0));
+    for (int i = 0; i < reps; ++i)
+        launch();
+    CHECK(hipEventRecord(e1));
+    CHECK(hipEventSynchronize(e1));
+    float ms = 0;
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    return ms / reps;
+}
+
+int main(int argc, char **argv)
+{
+    const size_t bytes = (argc > 1 ? (size_t)atoll(argv[1]) : (size_t)2 << 30);
+    const int reps = argc > 2 ? atoi(argv[2]) : 20;
+    void *a, *b;
+    double *out;
+    CHECK(hipMalloc(&a, bytes));
+    CHECK(hipMalloc(&b, bytes));
+    CHECK(hipMemset(a, 1, bytes));
+    const int grid = 256 * 16;  // 16 workgroups per CU, grid-stride
+    CHECK(hipMalloc(&out, (size_t)grid * 256 * sizeof(double)));
+    const size_t n8 = bytes / 8, n16 = bytes / 16;
+
+    double t;
+    t = time_ms([&] { hipLaunchKernelGGL((read_kernel<double2, 4>), dim3(grid), dim3(256), 0, 0,
+                                         (const double2 *)a, n16, out); }, reps);
+    printf("{\"probe\": \"read_dwordx4\", \"bytes\": %zu, \"ms\": %.4f, \"GBs\": %.1f}\n", bytes, t,
+           bytes / t * 1e-6);
+    t = time_ms([&] { hipLaunchKernelGGL((read_kernel<double, 4>), dim3(grid), dim3(256), 0, 0,
+                                         (const double *)a, n8, out); }, reps);
+    printf("{\"probe\": \"read_dwordx2\", \"bytes\": %zu, \"ms\": %.4f, \"GBs\": %.1f}\n", bytes, t,
+           bytes / t * 1e-6);
+    t = time_ms([&] { hipLaunchKernelGGL(copy_kernel, dim3(grid), dim3(256), 0, 0,
+                                         (const double2 *)a, (double2 *)b, n16); }, reps);
+    printf("{\"probe\": \"copy_dwordx4\", \"bytes\": %zu, \"ms\": %.4f, \"GBs\": %.1f}\n", 2 * bytes, t,
+           2 * bytes / t * 1e-6);
+    CHECK(hipFree(a));
+    CHECK(hipFree(b));
+    CHECK(hipFree(out));
+    return 0;
+}

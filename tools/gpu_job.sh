@@ -32,6 +32,10 @@ for s in "${steps[@]}"; do
     sweep0) SPMV_XCD_REMAP=0 run sweep_noremap 600 python tools/sweep.py --rounds 2;;
     sweeprmat) run sweep_rmat 600 python tools/sweep.py --matrix rmat --rounds 2 --reps 20;;
     counters) run counters 120 rocprofv3 -L;;
+    probe) [ -x tools/bw_probe ] || hipcc --offload-arch=gfx950 -O3 tools/bw_probe.hip -o tools/bw_probe; run bw_probe 300 tools/bw_probe;;
+    sweepfast) run sweep_fast 600 python tools/sweep.py --only csr,sell,ell --rounds 2;;
+    sweepnopair) SPMV_CSR_PAIR=0 run sweep_nopair 300 python tools/sweep.py --only csr --rounds 2;;
+    pmc) run pmc 1100 python tools/pmc_traffic.py;;
     *) echo "unknown step $s";;
   esac
 done

@@ -93,8 +93,11 @@ int spmv_ell_run(spmv_dims d, int32_t K, int64_t ld, int32_t ki,
  * occupies [slice_ptr[s], slice_ptr[s+1]) with entry (slot r, k) at
  *     slice_ptr[s] + (k / ki) * C * ki + r * ki + (k % ki)
  * perm[s*C + r] is the original row of slot r of slice s (-1 = padding
- * slot); y[perm[.]] is written directly, no un-permute pass.             */
-int spmv_sell_run(spmv_dims d, int32_t C, int32_t ki, int64_t n_slices,
+ * slot); y[perm[.]] is written directly, no un-permute pass.  `sigma` is
+ * the sorting window the builder used (1 = none; else a multiple of C):
+ * one workgroup covers one window so its scattered y stores merge in one
+ * L2.                                                                    */
+int spmv_sell_run(spmv_dims d, int32_t C, int32_t sigma, int32_t ki, int64_t n_slices,
                   const int64_t *slice_ptr, const int32_t *perm,
                   const int32_t *col, const double *val, const double *x,
                   double *y);

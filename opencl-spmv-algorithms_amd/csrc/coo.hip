@@ -33,6 +33,7 @@
 namespace spmv {
 
 constexpr int kCooIter = 16;                  // 64-entry steps per tile
+constexpr int kCooU = 4;                      // steps loaded ahead
 constexpr int64_t kTile = kWave * kCooIter;  // entries per wave
 
 // Inclusive segmented scan over one wave; `key` is non-decreasing across
@@ -70,46 +71,63 @@ __global__ __launch_bounds__(kBlock) void coo_tile_kernel(
 
     double run = 0.0;      // wave-uniform running sum of row `run_row`
     int32_t run_row = -1;
+    int32_t prev_r = before;  // row of the entry just before the step
     double pref = 0.0;     // this lane's share of a continued first row
 
-    for (int it = 0; it < kCooIter; ++it) {
-        const int64_t j0 = t0 + (int64_t)it * kWave;
-        if (j0 >= t1)
+    // kCooU steps are loaded before any is reduced, so each lane keeps
+    // 3·kCooU loads (+ kCooU x gathers) in flight instead of one step's.
+    for (int it0 = 0; it0 < kCooIter; it0 += kCooU) {
+        if (t0 + (int64_t)it0 * kWave >= t1)
             break;
-        const int64_t j = j0 + lane;
-        const int nvalid = (int)(t1 - j0 < kWave ? t1 - j0 : kWave);
-        const bool valid = lane < nvalid;
-        const int32_t r = valid ? row[j] : INT_MAX;
-        double p = valid ? val[j] * x[col[j]] : 0.0;
-
-        // The row carried from the previous step is finished unless this
-        // step starts with the same row.
-        const int32_t r0 = __shfl(r, 0, kWave);
-        if (lane == 0 && run_row >= 0 && r0 != run_row &&
-            !(first_continues && run_row == first_row))
-            y[run_row] = run;
-
-        // Rows strictly between the previous entry's row and r are empty.
-        int32_t rp = __shfl_up(r, 1, kWave);
-        if (lane == 0)
-            rp = j0 > 0 ? row[j0 - 1] : -1;
-        if (valid)
-            for (int32_t g = rp + 1; g < r; ++g)
-                y[g] = 0.0;
-
-        if (first_continues && r == first_row) {
-            pref += p;  // goes to the carry, not through the scan
-            p = 0.0;
+        int32_t rs[kCooU];
+        double ps[kCooU];
+#pragma unroll
+        for (int u = 0; u < kCooU; ++u) {
+            const int64_t j = t0 + (int64_t)(it0 + u) * kWave + lane;
+            const bool valid = j < t1;
+            rs[u] = valid ? row[j] : INT_MAX;
+            ps[u] = valid ? val[j] * x[col[j]] : 0.0;
         }
-        p = seg_scan(p, r, lane);
-        if (r == run_row)
-            p += run;
-        const int32_t rn = __shfl_down(r, 1, kWave);
-        const bool tail = valid && lane < nvalid - 1 && rn != r;
-        if (tail && !(first_continues && r == first_row))
-            y[r] = p;
-        run_row = __shfl(r, nvalid - 1, kWave);
-        run = __shfl(p, nvalid - 1, kWave);
+#pragma unroll
+        for (int u = 0; u < kCooU; ++u) {
+            const int64_t j0 = t0 + (int64_t)(it0 + u) * kWave;
+            if (j0 >= t1)
+                break;
+            const int nvalid = (int)(t1 - j0 < kWave ? t1 - j0 : kWave);
+            const bool valid = lane < nvalid;
+            const int32_t r = rs[u];
+            double p = ps[u];
+
+            // The row carried from the previous step is finished unless
+            // this step starts with the same row.
+            const int32_t r0 = __shfl(r, 0, kWave);
+            if (lane == 0 && run_row >= 0 && r0 != run_row &&
+                !(first_continues && run_row == first_row))
+                y[run_row] = run;
+
+            // Rows strictly between the previous entry's row and r are empty.
+            int32_t rp = __shfl_up(r, 1, kWave);
+            if (lane == 0)
+                rp = prev_r;
+            if (valid)
+                for (int32_t g = rp + 1; g < r; ++g)
+                    y[g] = 0.0;
+
+            if (first_continues && r == first_row) {
+                pref += p;  // goes to the carry, not through the scan
+                p = 0.0;
+            }
+            p = seg_scan(p, r, lane);
+            if (r == run_row)
+                p += run;
+            const int32_t rn = __shfl_down(r, 1, kWave);
+            const bool tail = valid && lane < nvalid - 1 && rn != r;
+            if (tail && !(first_continues && r == first_row))
+                y[r] = p;
+            run_row = __shfl(r, nvalid - 1, kWave);
+            run = __shfl(p, nvalid - 1, kWave);
+            prev_r = run_row;
+        }
     }
     if (lane == 0 && run_row >= 0 && !(first_continues && run_row == first_row))
         y[run_row] = run;
@@ -163,18 +181,31 @@ __global__ __launch_bounds__(kBlock) void cmrs_kernel(
     __builtin_amdgcn_wave_barrier();
 
     const int64_t beg = strip_ptr[s], end = strip_ptr[s + 1];
-    for (int64_t j0 = beg; j0 < end; j0 += kWave) {
-        const int64_t j = j0 + lane;
-        const int nvalid = (int)(end - j0 < kWave ? end - j0 : kWave);
-        const bool valid = lane < nvalid;
-        const int key = valid ? (int)row_in_strip[j] : INT_MAX;
-        double p = valid ? val[j] * x[col[j]] : 0.0;
-        p = seg_scan(p, key, lane);
-        const int kn = __shfl_down(key, 1, kWave);
-        const bool tail = valid && (lane == nvalid - 1 || kn != key);
-        if (tail)
-            acc[key] += p;  // distinct keys per step: no two tails collide
-        __builtin_amdgcn_wave_barrier();
+    for (int64_t b0 = beg; b0 < end; b0 += kCooU * kWave) {
+        int keys[kCooU];
+        double ps[kCooU];
+#pragma unroll
+        for (int u = 0; u < kCooU; ++u) {  // loads of kCooU steps in flight
+            const int64_t j = b0 + u * kWave + lane;
+            const bool valid = j < end;
+            keys[u] = valid ? (int)row_in_strip[j] : INT_MAX;
+            ps[u] = valid ? val[j] * x[col[j]] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < kCooU; ++u) {
+            const int64_t j0 = b0 + u * kWave;
+            if (j0 >= end)
+                break;
+            const int nvalid = (int)(end - j0 < kWave ? end - j0 : kWave);
+            const bool valid = lane < nvalid;
+            const int key = keys[u];
+            const double p = seg_scan(ps[u], key, lane);
+            const int kn = __shfl_down(key, 1, kWave);
+            const bool tail = valid && (lane == nvalid - 1 || kn != key);
+            if (tail)
+                acc[key] += p;  // distinct keys per step: no two tails collide
+            __builtin_amdgcn_wave_barrier();
+        }
     }
     __builtin_amdgcn_wave_barrier();
     if (lane < h) {

@@ -67,14 +67,20 @@ __device__ __forceinline__ double slot_dot(const double *__restrict__ vp,
     return (a0 + a1) + (a2 + a3);
 }
 
+// One workgroup covers one sigma window (up to 1024 slots): every y[perm]
+// store of a window then comes from ONE CU, so its L2 merges the window's
+// scattered 8-byte stores into whole lines.  With 256-slot workgroups a
+// 1024-row window was written from four XCDs and each partially written
+// line left the chip up to four times (WRITE_SIZE 2.9x the y bytes,
+// profiles/traffic.json), which cost ~10 % of the kernel.
 template <int KI>
-__global__ __launch_bounds__(kBlock) void sell_kernel(
+__global__ __launch_bounds__(1024) void sell_kernel(
     int32_t C, int64_t n_slices, const int64_t *__restrict__ slice_ptr,
     const int32_t *__restrict__ perm, const int32_t *__restrict__ col,
     const double *__restrict__ val, const double *__restrict__ x,
     double *__restrict__ y, int remap)
 {
-    const int64_t slot = xcd_block(remap) * kBlock + threadIdx.x;
+    const int64_t slot = xcd_block(remap) * (int64_t)blockDim.x + threadIdx.x;
     const int64_t s = slot / C;
     if (s >= n_slices)
         return;
@@ -105,7 +111,7 @@ __global__ __launch_bounds__(kBlock) void ell_kernel(
 
 using namespace spmv;
 
-extern "C" int spmv_sell_run(spmv_dims d, int32_t C, int32_t ki,
+extern "C" int spmv_sell_run(spmv_dims d, int32_t C, int32_t sigma, int32_t ki,
                              int64_t n_slices, const int64_t *slice_ptr,
                              const int32_t *perm, const int32_t *col,
                              const double *val, const double *x, double *y)
@@ -114,22 +120,27 @@ extern "C" int spmv_sell_run(spmv_dims d, int32_t C, int32_t ki,
         return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_run: bad C / sizes");
     if (ki != 1 && ki != 2)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_run: ki must be 1 or 2");
+    if (sigma < 1 || (sigma > 1 && sigma % C != 0))
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_run: sigma must be 1 or a multiple of C");
     if (n_slices * C < d.n_rows)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_run: n_slices*C < n_rows");
     if (d.n_rows == 0 || n_slices == 0)
         return SPMV_SUCCESS;
     SPMV_GUARD(d);
     const int64_t slots = n_slices * C;
-    const int64_t blocks = (slots + kBlock - 1) / kBlock;
+    // workgroup = one sigma window when it fits (256..1024 slots, a
+    // multiple of the wave), else 256 slots
+    const int bt = (sigma >= kBlock && sigma <= 1024 && sigma % kWave == 0) ? sigma : kBlock;
+    const int64_t blocks = (slots + bt - 1) / bt;
     if (blocks > INT32_MAX)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_run: grid too large");
     const int remap = xcd_remap_enabled() ? 1 : 0;
     if (ki == 2)
-        hipLaunchKernelGGL(sell_kernel<2>, dim3((unsigned)blocks), dim3(kBlock), 0,
+        hipLaunchKernelGGL(sell_kernel<2>, dim3((unsigned)blocks), dim3(bt), 0,
                            (hipStream_t)d.stream, C, n_slices, slice_ptr, perm,
                            col, val, x, y, remap);
     else
-        hipLaunchKernelGGL(sell_kernel<1>, dim3((unsigned)blocks), dim3(kBlock), 0,
+        hipLaunchKernelGGL(sell_kernel<1>, dim3((unsigned)blocks), dim3(bt), 0,
                            (hipStream_t)d.stream, C, n_slices, slice_ptr, perm,
                            col, val, x, y, remap);
     SPMV_CHECK_LAUNCH("sell_kernel");

@@ -198,7 +198,7 @@ typedef struct {
     double *d_val, *d_x, *d_y;
     void *d_ws;
     size_t ws_bytes;
-    int32_t K, C, ki, h, lanes;
+    int32_t K, C, sigma, ki, h, lanes;
     int64_t ld, n_slices, n_strips;
     /* host copies for the CPU loop */
     int64_t *h_ptr;
@@ -305,6 +305,7 @@ static int build_format(const opts_t *o, spmv_format fmt, const coo_t *m, dev_fm
         f->stored_bytes = (size_t)f->stored * 12;
     } else { /* SELL */
         f->C = o->C;
+        f->sigma = o->sigma;
         f->ki = o->ki;
         if ((rc = spmv_sell_plan(N, ptr, o->C, o->sigma, o->ki, &f->n_slices, &f->stored)))
             return rc;
@@ -342,7 +343,7 @@ static int launch(void *arg)
     case FMT_ELL:
         return spmv_ell_run(f->d, f->K, f->ld, f->ki, f->d_col, f->d_val, f->d_x, f->d_y);
     case FMT_SELL:
-        return spmv_sell_run(f->d, f->C, f->ki, f->n_slices, f->d_ptr, f->d_perm, f->d_col,
+        return spmv_sell_run(f->d, f->C, f->sigma, f->ki, f->n_slices, f->d_ptr, f->d_perm, f->d_col,
                              f->d_val, f->d_x, f->d_y);
     case FMT_CMRS:
         return spmv_cmrs_run(f->d, f->h, f->n_strips, f->d_ptr, f->d_rin, f->d_col, f->d_val,

@@ -79,7 +79,7 @@ HIP_SYMBOLS = {
     "spmv_csr_auto_lanes": (ctypes.c_int, [_c_i64, _c_i64]),
     "spmv_csr_run": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, ctypes.c_int]),
     "spmv_ell_run": (ctypes.c_int, [Dims, _c_i32, _c_i64, _c_i32, _vp, _vp, _vp, _vp]),
-    "spmv_sell_run": (ctypes.c_int, [Dims, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "spmv_sell_run": (ctypes.c_int, [Dims, _c_i32, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "spmv_cmrs_run": (ctypes.c_int, [Dims, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "spmv_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     "spmv_set_device": (ctypes.c_int, [ctypes.c_int]),
@@ -421,7 +421,7 @@ class DeviceMatrix:
         elif self.fmt == "ell":
             rc = lib.spmv_ell_run(d, p["K"], p["ld"], p["ki"], _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y))
         elif self.fmt == "sell":
-            rc = lib.spmv_sell_run(d, p["C"], p["ki"], p["n_slices"], _ptr(a["slice_ptr"]), _ptr(a["perm"]),
+            rc = lib.spmv_sell_run(d, p["C"], p["sigma"], p["ki"], p["n_slices"], _ptr(a["slice_ptr"]), _ptr(a["perm"]),
                                    _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y))
         elif self.fmt == "cmrs":
             rc = lib.spmv_cmrs_run(d, p["h"], p["n_strips"], _ptr(a["strip_ptr"]), _ptr(a["row_in_strip"]),

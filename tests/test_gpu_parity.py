@@ -225,8 +225,9 @@ def test_bad_arguments_rejected(torch_dev):
     d = sa.Dims(10, 10, 5, 0, None)
     assert L.spmv_csr_run(d, None, None, None, None, None, 3) == sa.OTHER_ERROR
     assert L.spmv_ell_run(d, 4, 63, 1, None, None, None, None) == sa.OTHER_ERROR
-    assert L.spmv_sell_run(d, 0, 1, 1, None, None, None, None, None, None) == sa.OTHER_ERROR
-    assert L.spmv_sell_run(d, 64, 3, 1, None, None, None, None, None, None) == sa.OTHER_ERROR
+    assert L.spmv_sell_run(d, 0, 1, 1, 1, None, None, None, None, None, None) == sa.OTHER_ERROR
+    assert L.spmv_sell_run(d, 64, 1, 3, 1, None, None, None, None, None, None) == sa.OTHER_ERROR
+    assert L.spmv_sell_run(d, 64, 100, 1, 1, None, None, None, None, None, None) == sa.OTHER_ERROR
     assert L.spmv_cmrs_run(d, 8, 7, None, None, None, None, None, None) == sa.OTHER_ERROR
     assert L.spmv_cmrs_run(d, 65, 1, None, None, None, None, None, None) == sa.OTHER_ERROR
     assert L.spmv_coo_run(d, None, None, None, None, None, None, 0) == sa.OTHER_ERROR

@@ -36,6 +36,7 @@ for s in "${steps[@]}"; do
     sweepfast) run sweep_fast 600 python tools/sweep.py --only csr,sell,ell --rounds 2;;
     sweepnopair) SPMV_CSR_PAIR=0 run sweep_nopair 300 python tools/sweep.py --only csr --rounds 2;;
     pmc) run pmc 1100 python tools/pmc_traffic.py;;
+    pmcvar) run pmc_var 1100 python tools/pmc_traffic.py --out traffic_variants.json --formats "csr,csr@SPMV_XCD_REMAP=1,csr:lanes=16,sell:sigma=256,sell,ell@SPMV_XCD_REMAP=1";;
     *) echo "unknown step $s";;
   esac
 done

@@ -81,6 +81,7 @@ def main():
     ap.add_argument("--formats", default="csr,sell,ell,coo,cmrs")
     ap.add_argument("--copies", type=int, default=32)
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--out", default=None, help="file name under profiles/ (default traffic.json)")
     a = ap.parse_args()
     probe = REPO / "tools" / "bw_probe"
     if not probe.exists():
@@ -103,12 +104,26 @@ def main():
                                "RDREQ_sized_bytes_over_known": cal_rdreq, "raw": cal}}
     print(json.dumps(result["_calibration"]), flush=True)
 
-    for fmt in a.formats.split(","):
+    for spec in a.formats.split(","):
+        # spec: fmt[:key=val;key=val][@ENV=val]  e.g. sell:sigma=256  csr@SPMV_XCD_REMAP=1
+        env_kv = {}
+        if "@" in spec:
+            spec_main, env_s = spec.split("@", 1)
+            k, v = env_s.split("=", 1)
+            env_kv[k] = v
+        else:
+            spec_main = spec
+        fmt, _, params = spec_main.partition(":")
         cmd = ["python3", "bench.py", "--profile", "--format", fmt, "--steps", str(a.steps), "--warmup", "2",
                "--copies", str(a.copies)]
+        for kv in filter(None, params.split(";")):
+            k, v = kv.split("=")
+            cmd += [f"--{k}", v]
+        os.environ.update(env_kv)
+        tag0 = spec.replace(":", "_").replace(";", "_").replace("=", "").replace("@", "_")
         counters, n = {}, 0
         for tag, cs in PASSES.items():
-            f = run_pass(f"{fmt}_{tag}", cs, cmd)
+            f = run_pass(f"{tag0}_{tag}", cs, cmd)
             if f:
                 c, n = mean_per_dispatch(f, KERNELS[fmt])
                 counters.update(c)
@@ -128,14 +143,17 @@ def main():
             how = "FETCH_SIZE*1024*2 (guide's gfx950 correction, uncalibrated)"
         write = counters.get("WRITE_SIZE", 0.0) * 1024
         hits, miss = counters.get("TCC_HIT_sum", 0.0), counters.get("TCC_MISS_sum", 0.0)
-        result[fmt] = {"kernel": KERNELS[fmt], "bytes_alg": b_alg, "dispatches": n,
+        for k in env_kv:
+            os.environ.pop(k, None)
+        result[spec] = {"kernel": KERNELS[fmt], "bytes_alg": b_alg, "dispatches": n, "cmd": " ".join(cmd[1:]),
+                        "env": env_kv or None,
                        "hbm_read_bytes_per_launch": round(read), "hbm_write_bytes_per_launch": round(write),
                        "hbm_bytes_per_launch": round(read + write),
                        "traffic_over_alg": round((read + write) / b_alg, 4), "method": how,
                        "l2_hit_rate": round(hits / (hits + miss), 4) if hits + miss else None,
                        "counters": {k: round(v, 1) for k, v in counters.items()}}
-        print(json.dumps({fmt: result[fmt]}), flush=True)
-    dst = REPO / "profiles" / "traffic.json"
+        print(json.dumps({spec: result[spec]}), flush=True)
+    dst = REPO / "profiles" / ("traffic.json" if a.out is None else a.out)
     dst.write_text(json.dumps(result, indent=1) + "\n")
     print(f"wrote {dst}")
 

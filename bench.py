@@ -64,6 +64,7 @@ def parse():
                    help="also measure the other formats (default: at N=1 only)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0: skip)")
     p.add_argument("--lanes", type=int, default=0)
+    p.add_argument("--variant", type=int, default=0, help="CSR kernel variant (0 auto, 1 direct, 2 staged)")
     p.add_argument("--ki", type=int, default=2)
     p.add_argument("--C", type=int, default=64)
     p.add_argument("--sigma", type=int, default=1024)
@@ -74,7 +75,7 @@ def parse():
 
 def fmt_kwargs(args, fmt):
     if fmt == "csr":
-        return {"lanes": args.lanes}
+        return {"lanes": args.lanes, "variant": args.variant}
     if fmt == "ell":
         return {"ki": args.ki}
     if fmt == "sell":

@@ -71,6 +71,14 @@ int spmv_csr_auto_lanes(int64_t n_rows, int64_t nnz);
 int spmv_csr_run(spmv_dims d, const int64_t *row_ptr, const int32_t *col,
                  const double *val, const double *x, double *y,
                  int lanes_per_row);
+/* Same, with the kernel variant explicit: 0 = library default,
+ * 1 = direct (each lane group streams its own row's entries),
+ * 2 = staged (all 256 lanes of a workgroup stream the workgroup's entry
+ *     range through LDS, then each lane group reduces its row from LDS). */
+int spmv_csr_run_variant(spmv_dims d, const int64_t *row_ptr,
+                         const int32_t *col, const double *val,
+                         const double *x, double *y, int lanes_per_row,
+                         int variant);
 
 /* ---------------------------------------------------------------- ELL ---
  * Replaces kernel `ell(val,idx,x,y,int N,int K,__local)` (reference

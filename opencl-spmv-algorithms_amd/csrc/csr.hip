@@ -89,6 +89,76 @@ __global__ __launch_bounds__(kBlock) void csr_vector_kernel(
         y[row] = sum;
 }
 
+// CSR-vector with the entry stream staged through LDS ("staged" variant).
+// The workgroup's rows occupy one contiguous range of entries
+// [ptr[row0], ptr[row0+RPB]).  Instead of every L-lane group walking its
+// own row (ragged trip counts, loads that straddle row ends), all 256
+// lanes stream that range like a copy kernel — aligned 16-byte value
+// pairs + 8-byte column pairs, kStageRounds pairs per lane in flight —
+// and store the products a·x in LDS.  After one barrier each L-lane group
+// sums its row's slice of the products (conflict-free ds_read_b64, stride
+// 1 across lanes) and reduces with the same shuffle butterfly.  Ranges
+// longer than the LDS chunk are processed in chunks; a row's partial sum
+// stays in its lanes' registers across chunks.
+constexpr int kStageRounds = 5;                           // pairs per lane per chunk
+constexpr int kStageEntries = 2 * kBlock * kStageRounds;  // 2560 products, 20 KiB
+
+template <int L>
+__global__ __launch_bounds__(kBlock) void csr_staged_kernel(
+    int64_t n_rows, const int64_t *__restrict__ row_ptr,
+    const int32_t *__restrict__ col, const double *__restrict__ val,
+    const double *__restrict__ x, double *__restrict__ y, int remap)
+{
+    constexpr int RPB = kBlock / L;
+    __shared__ int64_t s_ptr[RPB + 1];
+    __shared__ double2 s_prod[kStageEntries / 2];
+
+    const int64_t row0 = xcd_block(remap) * RPB;
+    if (threadIdx.x <= RPB) {
+        int64_t r = row0 + threadIdx.x;
+        s_ptr[threadIdx.x] = row_ptr[r < n_rows ? r : n_rows];
+    }
+    __syncthreads();
+
+    const int g = threadIdx.x / L;
+    const int lane = threadIdx.x % L;
+    const int64_t row = row0 + g;
+    const int64_t beg = s_ptr[g], end = s_ptr[g + 1];
+    const int64_t blk_end = s_ptr[RPB];
+    const double *prod = reinterpret_cast<const double *>(s_prod);
+
+    double acc = 0.0;
+    // chunks start on an even entry so value pairs stay 16-byte aligned;
+    // an entry before the block's range is loaded but never summed.
+    for (int64_t cb = s_ptr[0] & ~(int64_t)1; cb < blk_end; cb += kStageEntries) {
+        const int64_t ce = cb + kStageEntries < blk_end ? cb + kStageEntries : blk_end;
+#pragma unroll
+        for (int k = 0; k < kStageRounds; ++k) {
+            const int t = threadIdx.x + k * kBlock;
+            const int64_t p = cb + 2 * (int64_t)t;
+            double2 pr = {0.0, 0.0};
+            if (p + 1 < ce) {
+                const double2 v = *reinterpret_cast<const double2 *>(val + p);
+                const int2 c = *reinterpret_cast<const int2 *>(col + p);
+                pr.x = v.x * x[c.x];
+                pr.y = v.y * x[c.y];
+            } else if (p < ce) {  // odd tail: never read past the range
+                pr.x = val[p] * x[col[p]];
+            }
+            s_prod[t] = pr;
+        }
+        __syncthreads();
+        const int64_t lo = beg > cb ? beg : cb;
+        const int64_t hi = end < ce ? end : ce;
+        for (int64_t j = lo + lane; j < hi; j += L)
+            acc += prod[j - cb];
+        __syncthreads();
+    }
+    acc = group_sum<L>(acc);
+    if (lane == 0 && row < n_rows)
+        y[row] = acc;
+}
+
 static bool csr_pair_loads()
 {
     static int cached = -1;
@@ -99,22 +169,36 @@ static bool csr_pair_loads()
     return cached == 1;
 }
 
+// variant: 1 = direct (each L-lane group streams its own row),
+//          2 = staged (the block's entry range streamed through LDS)
+static int csr_default_variant()
+{
+    static int cached = -1;
+    if (cached < 0) {
+        const char *s = getenv("SPMV_CSR_VARIANT");
+        cached = (s && (s[0] == '1' || s[0] == '2')) ? s[0] - '0' : 1;
+    }
+    return cached;
+}
+
 template <int L>
 static void launch_csr(const spmv_dims &d, const int64_t *row_ptr,
                        const int32_t *col, const double *val, const double *x,
-                       double *y)
+                       double *y, int variant)
 {
     constexpr int RPB = kBlock / L;
     const int64_t blocks = (d.n_rows + RPB - 1) / RPB;
     const int remap = xcd_remap_enabled() ? 1 : 0;
-    if (csr_pair_loads())
+    const hipStream_t st = (hipStream_t)d.stream;
+    if (variant == 2)
+        hipLaunchKernelGGL((csr_staged_kernel<L>), dim3((unsigned)blocks), dim3(kBlock), 0, st,
+                           d.n_rows, row_ptr, col, val, x, y, remap);
+    else if (csr_pair_loads())
         hipLaunchKernelGGL((csr_vector_kernel<L, true>), dim3((unsigned)blocks),
-                           dim3(kBlock), 0, (hipStream_t)d.stream, d.n_rows,
-                           row_ptr, col, val, x, y, remap);
+                           dim3(kBlock), 0, st, d.n_rows, row_ptr, col, val, x, y, remap);
     else
         hipLaunchKernelGGL((csr_vector_kernel<L, false>), dim3((unsigned)blocks),
-                           dim3(kBlock), 0, (hipStream_t)d.stream, d.n_rows,
-                           row_ptr, col, val, x, y, remap);
+                           dim3(kBlock), 0, st, d.n_rows, row_ptr, col, val, x, y, remap);
 }
 
 }  // namespace spmv
@@ -135,29 +219,40 @@ extern "C" int spmv_csr_auto_lanes(int64_t n_rows, int64_t nnz)
     return L;
 }
 
-extern "C" int spmv_csr_run(spmv_dims d, const int64_t *row_ptr,
-                            const int32_t *col, const double *val,
-                            const double *x, double *y, int lanes_per_row)
+extern "C" int spmv_csr_run_variant(spmv_dims d, const int64_t *row_ptr,
+                                    const int32_t *col, const double *val,
+                                    const double *x, double *y, int lanes_per_row,
+                                    int variant)
 {
     if (d.n_rows < 0 || d.n_cols < 0 || d.nnz < 0)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_run: negative size");
+    if (variant < 0 || variant > 2)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_run: variant must be 0, 1 or 2");
     if (d.n_rows == 0)
         return SPMV_SUCCESS;
     if ((d.n_rows + 1) / 2 > (int64_t)INT32_MAX * 64)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_run: too many rows");
     SPMV_GUARD(d);
-    int L = lanes_per_row > 0 ? lanes_per_row : spmv_csr_auto_lanes(d.n_rows, d.nnz);
+    const int L = lanes_per_row > 0 ? lanes_per_row : spmv_csr_auto_lanes(d.n_rows, d.nnz);
+    const int v = variant ? variant : csr_default_variant();
     switch (L) {
-    case 2: launch_csr<2>(d, row_ptr, col, val, x, y); break;
-    case 4: launch_csr<4>(d, row_ptr, col, val, x, y); break;
-    case 8: launch_csr<8>(d, row_ptr, col, val, x, y); break;
-    case 16: launch_csr<16>(d, row_ptr, col, val, x, y); break;
-    case 32: launch_csr<32>(d, row_ptr, col, val, x, y); break;
-    case 64: launch_csr<64>(d, row_ptr, col, val, x, y); break;
+    case 2: launch_csr<2>(d, row_ptr, col, val, x, y, v); break;
+    case 4: launch_csr<4>(d, row_ptr, col, val, x, y, v); break;
+    case 8: launch_csr<8>(d, row_ptr, col, val, x, y, v); break;
+    case 16: launch_csr<16>(d, row_ptr, col, val, x, y, v); break;
+    case 32: launch_csr<32>(d, row_ptr, col, val, x, y, v); break;
+    case 64: launch_csr<64>(d, row_ptr, col, val, x, y, v); break;
     default:
         return fail_msg(SPMV_OTHER_ERROR,
                         "spmv_csr_run: lanes_per_row must be 0 or a power of two in [2,64]");
     }
-    SPMV_CHECK_LAUNCH("csr_vector_kernel");
+    SPMV_CHECK_LAUNCH("csr kernel");
     return SPMV_SUCCESS;
+}
+
+extern "C" int spmv_csr_run(spmv_dims d, const int64_t *row_ptr,
+                            const int32_t *col, const double *val,
+                            const double *x, double *y, int lanes_per_row)
+{
+    return spmv_csr_run_variant(d, row_ptr, col, val, x, y, lanes_per_row, 0);
 }

@@ -78,6 +78,7 @@ HIP_SYMBOLS = {
     "spmv_coo_run": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t]),
     "spmv_csr_auto_lanes": (ctypes.c_int, [_c_i64, _c_i64]),
     "spmv_csr_run": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, ctypes.c_int]),
+    "spmv_csr_run_variant": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, ctypes.c_int, ctypes.c_int]),
     "spmv_ell_run": (ctypes.c_int, [Dims, _c_i32, _c_i64, _c_i32, _vp, _vp, _vp, _vp]),
     "spmv_sell_run": (ctypes.c_int, [Dims, _c_i32, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "spmv_cmrs_run": (ctypes.c_int, [Dims, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
@@ -416,8 +417,8 @@ class DeviceMatrix:
             rc = lib.spmv_coo_run(d, _ptr(a["row"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
                                   _ptr(a["ws"]), a["ws"].numel())
         elif self.fmt == "csr":
-            rc = lib.spmv_csr_run(d, _ptr(a["row_ptr"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
-                                  p["lanes"])
+            rc = lib.spmv_csr_run_variant(d, _ptr(a["row_ptr"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x),
+                                          _ptr(y), p["lanes"], p.get("variant", 0))
         elif self.fmt == "ell":
             rc = lib.spmv_ell_run(d, p["K"], p["ld"], p["ki"], _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y))
         elif self.fmt == "sell":
@@ -431,7 +432,7 @@ class DeviceMatrix:
         _check(rc, f"spmv_{self.fmt}_run")
 
 
-def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, ki: int = 2, C: int = 64,
+def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int = 0, ki: int = 2, C: int = 64,
               sigma: int = 1024, h: int = 8, ell_max_padding: float | None = 64.0) -> DeviceMatrix:
     """Build `fmt` on the host (libspmv_host.so) and upload it."""
     torch = _torch()
@@ -448,7 +449,7 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, ki: int = 2,
     ptr, col, val = csr_from_coo(m)
     if fmt == "csr":
         L = lanes or hip_lib().spmv_csr_auto_lanes(m.n_rows, m.nnz)
-        dm.params = dict(lanes=L)
+        dm.params = dict(lanes=L, variant=variant)
         dm.arrays = dict(row_ptr=_dev_tensor(ptr, device), col=_dev_tensor(col, device),
                          val=_dev_tensor(val, device))
         dm.stored_bytes = 12 * m.nnz + 8 * (m.n_rows + 1)

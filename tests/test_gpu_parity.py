@@ -28,6 +28,9 @@ FMT_PARAMS = [
     ("csr", {"lanes": 8}),
     ("csr", {"lanes": 32}),
     ("csr", {"lanes": 64}),
+    ("csr", {"variant": 2}),
+    ("csr", {"lanes": 2, "variant": 2}),
+    ("csr", {"lanes": 64, "variant": 2}),
     ("ell", {"ki": 1}),
     ("ell", {"ki": 2}),
     ("sell", {"C": 64, "sigma": 1024, "ki": 2}),
@@ -100,12 +103,13 @@ def test_cantlike_batch_random_x(torch_dev, fmt):
     assert_parity(m, y, x)
 
 
-@pytest.mark.parametrize("fmt", ["coo", "csr", "sell", "cmrs"])
-def test_rmat_skewed(torch_dev, fmt):
+@pytest.mark.parametrize("fmt,kw", [("coo", {}), ("csr", {}), ("csr", {"variant": 2}), ("sell", {}),
+                                    ("cmrs", {})])
+def test_rmat_skewed(torch_dev, fmt, kw):
     """R-MAT 1e6 rows / 1e7 entries: empty rows, rows of thousands of entries."""
     torch, dev = torch_dev
     m = sa.gen_rmat(1_000_000, 10_000_000, scale=20, seed=1)
-    y, x, _ = run_fmt(torch, dev, m, fmt)
+    y, x, _ = run_fmt(torch, dev, m, fmt, **kw)
     assert_parity(m, y, x)
 
 
@@ -117,7 +121,8 @@ def test_ell_refuses_rmat_padding(torch_dev):
 
 
 @pytest.mark.parametrize("fmt,kw", [("coo", {}), ("csr", {}), ("sell", {}), ("cmrs", {"h": 8}),
-                                    ("cmrs", {"h": 32}), ("csr", {"lanes": 64})])
+                                    ("cmrs", {"h": 32}), ("csr", {"lanes": 64}), ("csr", {"variant": 2}),
+                                    ("csr", {"lanes": 2, "variant": 2})])
 def test_ragged_long_rows(torch_dev, fmt, kw):
     torch, dev = torch_dev
     m = sa.gen_random(20_000, 50_000, 0, 2_000, seed=21)

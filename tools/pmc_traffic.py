@@ -25,7 +25,7 @@ from pathlib import Path
 
 REPO = Path(__file__).resolve().parents[1]
 OUT = REPO / "gpurun_out" / "pmc"
-KERNELS = {"csr": "csr_vector_kernel", "sell": "sell_kernel", "ell": "ell_kernel",
+KERNELS = {"csr": "csr_", "sell": "sell_kernel", "ell": "ell_kernel",
            "coo": "coo_tile_kernel", "cmrs": "cmrs_kernel"}
 PASSES = {
     "fetch": ["FETCH_SIZE"],
@@ -155,6 +155,8 @@ def main():
         print(json.dumps({spec: result[spec]}), flush=True)
     dst = REPO / "profiles" / ("traffic.json" if a.out is None else a.out)
     dst.write_text(json.dumps(result, indent=1) + "\n")
+    # only gpurun_out/ travels back from the GPU box
+    (REPO / "gpurun_out" / dst.name).write_text(json.dumps(result, indent=1) + "\n")
     print(f"wrote {dst}")
 
 

@@ -23,7 +23,8 @@ import spmv_amd as sa  # noqa: E402
 
 VARIANTS = [
     ("csr", {"lanes": 4}), ("csr", {"lanes": 8}), ("csr", {"lanes": 16}), ("csr", {"lanes": 32}),
-    ("csr", {"lanes": 64}),
+    ("csr", {"lanes": 4, "variant": 2}), ("csr", {"lanes": 8, "variant": 2}), ("csr", {"lanes": 16, "variant": 2}),
+    ("csr", {"lanes": 64}), ("csr", {"lanes": 2, "variant": 2}),
     ("ell", {"ki": 1}), ("ell", {"ki": 2}),
     ("sell", {"C": 64, "sigma": 1, "ki": 2}), ("sell", {"C": 64, "sigma": 256, "ki": 2}),
     ("sell", {"C": 64, "sigma": 1024, "ki": 2}), ("sell", {"C": 64, "sigma": 1024, "ki": 1}),

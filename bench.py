@@ -51,6 +51,7 @@ KERNEL_NAMES = {  # dominant kernel per format (as rocprofv3 names it)
     "coo": "coo_tile_kernel",
     "cmrs": "cmrs_kernel",
 }
+CSR_DEFAULT_VARIANT = 2  # must match csr_default_variant() in csrc/csr.hip
 
 
 def parse():
@@ -70,7 +71,18 @@ def parse():
     p.add_argument("--sigma", type=int, default=1024)
     p.add_argument("--h", type=int, default=8)
     p.add_argument("--profile", action="store_true", help="only the timed loop (for rocprofv3 passes)")
+    p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                   help="collective backend for N>1 (nccl = RCCL; gloo only to rehearse on one GPU)")
+    p.add_argument("--share-gpu", action="store_true", help="all ranks on cuda:0 (rehearsal only)")
     return p.parse_args()
+
+
+def kernel_name(args):
+    """The dominant kernel as rocprofv3 names it (for profiles/)."""
+    if args.format == "csr":
+        v = args.variant or int(os.environ.get("SPMV_CSR_VARIANT", "0") or 0) or CSR_DEFAULT_VARIANT
+        return {2: "csr_staged_kernel", 3: "csr_staged_persistent_kernel"}.get(v, "csr_vector_kernel")
+    return KERNEL_NAMES[args.format]
 
 
 def fmt_kwargs(args, fmt):
@@ -180,14 +192,19 @@ def main():
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     dist = None
+    gpu = 0 if args.share_gpu else local
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
+    # collectives run on the GPU over RCCL (backend "nccl" on ROCm); the
+    # gloo backend (CPU tensors) exists only to rehearse N>1 on one GPU
+    cdev = dev if args.backend == "nccl" else torch.device("cpu")
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     # ---- the batch: B cant-like copies, this rank's row shard
     B = args.copies
@@ -212,9 +229,9 @@ def main():
     if bad:
         raise SystemExit(f"rank {rank}: parity failure at row {first}")
 
-    wall_t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    wall_t = torch.tensor([wall], dtype=torch.float64, device=cdev)
     kern_mean = float(np.mean(kern))
-    kern_t = torch.tensor([kern_mean], dtype=torch.float64, device=dev)
+    kern_t = torch.tensor([kern_mean], dtype=torch.float64, device=cdev)
     if dist is not None:
         dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
         dist.all_reduce(kern_t, op=dist.ReduceOp.MAX)
@@ -227,20 +244,24 @@ def main():
     # ---- y all-gather over RCCL (timed separately, not in `value`)
     allgather = None
     if dist is not None:
-        y_all = torch.empty(n_rows * world, dtype=torch.float64, device=dev)
+        y_loc = y if cdev.type == "cuda" else y.cpu()
+        y_all = torch.empty(n_rows * world, dtype=torch.float64, device=cdev)
         for _ in range(3):
-            dist.all_gather_into_tensor(y_all, y)
+            dist.all_gather_into_tensor(y_all, y_loc)
         torch.cuda.synchronize()
+        # the gathered vector must hold every rank's shard in rank order
+        if not torch.equal(y_all[rank * n_rows:(rank + 1) * n_rows], y_loc):
+            raise SystemExit(f"rank {rank}: all-gathered y does not match the local shard")
         dist.barrier()
         t0 = time.perf_counter()
         reps = 20
         for _ in range(reps):
-            dist.all_gather_into_tensor(y_all, y)
+            dist.all_gather_into_tensor(y_all, y_loc)
         torch.cuda.synchronize()
-        ag = torch.tensor([(time.perf_counter() - t0) / reps], dtype=torch.float64, device=dev)
+        ag = torch.tensor([(time.perf_counter() - t0) / reps], dtype=torch.float64, device=cdev)
         dist.all_reduce(ag, op=dist.ReduceOp.MAX)
         ag_ms = float(ag.item()) * 1e3
-        allgather = {"ms": round(ag_ms, 4), "bytes_per_rank": 8 * n_rows,
+        allgather = {"ms": round(ag_ms, 4), "bytes_per_rank": 8 * n_rows, "backend": args.backend,
                      "value_with_allgather_GBs": round(total_bytes / ((ms_per_step + ag_ms) * 1e-3) * 1e-9, 1)}
 
     kern_ms = float(kern_t.item())
@@ -248,7 +269,7 @@ def main():
     traffic = traffic_for(args.format, bytes_step)
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": sa.HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / sa.HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": KERNEL_NAMES[args.format], "kernel_ms": round(kern_ms, 5),
+                "kernel": kernel_name(args), "kernel_ms": round(kern_ms, 5),
                 "bytes_alg_per_launch": bytes_step}
 
     per_format = None
@@ -312,7 +333,7 @@ def main():
             "per_format": per_format,
             "cant_single": cant_single,
             "allgather": allgather,
-            "device": sa.device_name(local),
+            "device": sa.device_name(gpu),
         }
         print(json.dumps(line), flush=True)
     if dist is not None:

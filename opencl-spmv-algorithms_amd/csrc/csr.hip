@@ -100,40 +100,32 @@ __global__ __launch_bounds__(kBlock) void csr_vector_kernel(
 // 1 across lanes) and reduces with the same shuffle butterfly.  Ranges
 // longer than the LDS chunk are processed in chunks; a row's partial sum
 // stays in its lanes' registers across chunks.
-constexpr int kStageRounds = 5;                           // pairs per lane per chunk
-constexpr int kStageEntries = 2 * kBlock * kStageRounds;  // 2560 products, 20 KiB
+constexpr int kStageRoundsDefault = 5;  // pairs per lane per chunk: 2560 products, 20 KiB
 
-template <int L>
-__global__ __launch_bounds__(kBlock) void csr_staged_kernel(
-    int64_t n_rows, const int64_t *__restrict__ row_ptr,
+// One row group (RPB = 256/L rows) of the staged scheme; s_ptr holds the
+// group's RPB+1 row offsets.  Ends with a barrier, so the caller may
+// overwrite s_ptr / s_prod afterwards.
+template <int L, int R>
+__device__ __forceinline__ void staged_group(
+    int64_t row, const int64_t *s_ptr, double2 *s_prod,
     const int32_t *__restrict__ col, const double *__restrict__ val,
-    const double *__restrict__ x, double *__restrict__ y, int remap)
+    const double *__restrict__ x, double *__restrict__ y, int64_t n_rows)
 {
     constexpr int RPB = kBlock / L;
-    __shared__ int64_t s_ptr[RPB + 1];
-    __shared__ double2 s_prod[kStageEntries / 2];
-
-    const int64_t row0 = xcd_block(remap) * RPB;
-    if (threadIdx.x <= RPB) {
-        int64_t r = row0 + threadIdx.x;
-        s_ptr[threadIdx.x] = row_ptr[r < n_rows ? r : n_rows];
-    }
-    __syncthreads();
-
+    constexpr int CH = 2 * kBlock * R;  // products per chunk
     const int g = threadIdx.x / L;
     const int lane = threadIdx.x % L;
-    const int64_t row = row0 + g;
     const int64_t beg = s_ptr[g], end = s_ptr[g + 1];
     const int64_t blk_end = s_ptr[RPB];
     const double *prod = reinterpret_cast<const double *>(s_prod);
 
     double acc = 0.0;
     // chunks start on an even entry so value pairs stay 16-byte aligned;
-    // an entry before the block's range is loaded but never summed.
-    for (int64_t cb = s_ptr[0] & ~(int64_t)1; cb < blk_end; cb += kStageEntries) {
-        const int64_t ce = cb + kStageEntries < blk_end ? cb + kStageEntries : blk_end;
+    // an entry before the group's range is loaded but never summed.
+    for (int64_t cb = s_ptr[0] & ~(int64_t)1; cb < blk_end; cb += CH) {
+        const int64_t ce = cb + CH < blk_end ? cb + CH : blk_end;
 #pragma unroll
-        for (int k = 0; k < kStageRounds; ++k) {
+        for (int k = 0; k < R; ++k) {
             const int t = threadIdx.x + k * kBlock;
             const int64_t p = cb + 2 * (int64_t)t;
             double2 pr = {0.0, 0.0};
@@ -157,6 +149,58 @@ __global__ __launch_bounds__(kBlock) void csr_staged_kernel(
     acc = group_sum<L>(acc);
     if (lane == 0 && row < n_rows)
         y[row] = acc;
+    __syncthreads();
+}
+
+// Variant 2: one workgroup per row group.
+template <int L, int R>
+__global__ __launch_bounds__(kBlock) void csr_staged_kernel(
+    int64_t n_rows, const int64_t *__restrict__ row_ptr,
+    const int32_t *__restrict__ col, const double *__restrict__ val,
+    const double *__restrict__ x, double *__restrict__ y, int remap)
+{
+    constexpr int RPB = kBlock / L;
+    __shared__ int64_t s_ptr[RPB + 1];
+    __shared__ double2 s_prod[kBlock * R];
+    const int64_t row0 = xcd_block(remap) * RPB;
+    if (threadIdx.x <= RPB) {
+        int64_t r = row0 + threadIdx.x;
+        s_ptr[threadIdx.x] = row_ptr[r < n_rows ? r : n_rows];
+    }
+    __syncthreads();
+    staged_group<L, R>(row0 + threadIdx.x / L, s_ptr, s_prod, col, val, x, y, n_rows);
+}
+
+// Variant 3: persistent workgroups (a few per CU) walk the row groups
+// grid-stride and PREFETCH the next group's row offsets into registers
+// while the current group streams, so a group no longer starts with a
+// dependent round trip for its offsets.
+template <int L, int R>
+__global__ __launch_bounds__(kBlock) void csr_staged_persistent_kernel(
+    int64_t n_rows, int64_t n_groups, const int64_t *__restrict__ row_ptr,
+    const int32_t *__restrict__ col, const double *__restrict__ val,
+    const double *__restrict__ x, double *__restrict__ y)
+{
+    constexpr int RPB = kBlock / L;
+    __shared__ int64_t s_ptr[RPB + 1];
+    __shared__ double2 s_prod[kBlock * R];
+    int64_t grp = blockIdx.x;
+    int64_t next = 0;
+    if (threadIdx.x <= RPB) {
+        int64_t r = grp * RPB + threadIdx.x;
+        next = row_ptr[r < n_rows ? r : n_rows];
+    }
+    for (; grp < n_groups; grp += gridDim.x) {
+        if (threadIdx.x <= RPB)
+            s_ptr[threadIdx.x] = next;
+        __syncthreads();
+        const int64_t g2 = grp + gridDim.x;
+        if (threadIdx.x <= RPB && g2 < n_groups) {
+            int64_t r = g2 * RPB + threadIdx.x;
+            next = row_ptr[r < n_rows ? r : n_rows];
+        }
+        staged_group<L, R>(grp * RPB + threadIdx.x / L, s_ptr, s_prod, col, val, x, y, n_rows);
+    }
 }
 
 static bool csr_pair_loads()
@@ -170,15 +214,60 @@ static bool csr_pair_loads()
 }
 
 // variant: 1 = direct (each L-lane group streams its own row),
-//          2 = staged (the block's entry range streamed through LDS)
+//          2 = staged (the group's entry range streamed through LDS),
+//          3 = staged, persistent workgroups with offset prefetch
 static int csr_default_variant()
 {
     static int cached = -1;
     if (cached < 0) {
         const char *s = getenv("SPMV_CSR_VARIANT");
-        cached = (s && (s[0] == '1' || s[0] == '2')) ? s[0] - '0' : 1;
+        cached = (s && s[0] >= '1' && s[0] <= '3') ? s[0] - '0' : 2;
     }
     return cached;
+}
+
+// SPMV_CSR_STAGE_ROUNDS in {3,5,8}: chunk = 2*256*R products (tuning knob)
+static int csr_stage_rounds()
+{
+    static int cached = -1;
+    if (cached < 0) {
+        const char *s = getenv("SPMV_CSR_STAGE_ROUNDS");
+        int r = s ? atoi(s) : kStageRoundsDefault;
+        cached = (r == 3 || r == 5 || r == 8) ? r : kStageRoundsDefault;
+    }
+    return cached;
+}
+
+static int cu_count()
+{
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+        n = 256;
+    return n;
+}
+
+template <int L, int R>
+static void launch_staged(const spmv_dims &d, const int64_t *row_ptr, const int32_t *col,
+                          const double *val, const double *x, double *y, int variant)
+{
+    constexpr int RPB = kBlock / L;
+    const int64_t groups = (d.n_rows + RPB - 1) / RPB;
+    const hipStream_t st = (hipStream_t)d.stream;
+    if (variant == 3) {
+        // LDS per workgroup = 16·256·R bytes: as many per CU as fit in
+        // 160 KiB, at most 8 (32 waves)
+        const int per_cu = (160 * 1024) / (16 * kBlock * R + 8 * (RPB + 1)) < 8
+                               ? (160 * 1024) / (16 * kBlock * R + 8 * (RPB + 1)) : 8;
+        int64_t grid = (int64_t)cu_count() * per_cu;
+        if (grid > groups)
+            grid = groups;
+        hipLaunchKernelGGL((csr_staged_persistent_kernel<L, R>), dim3((unsigned)grid), dim3(kBlock), 0,
+                           st, d.n_rows, groups, row_ptr, col, val, x, y);
+    } else {
+        hipLaunchKernelGGL((csr_staged_kernel<L, R>), dim3((unsigned)groups), dim3(kBlock), 0, st,
+                           d.n_rows, row_ptr, col, val, x, y, xcd_remap_enabled() ? 1 : 0);
+    }
 }
 
 template <int L>
@@ -190,15 +279,19 @@ static void launch_csr(const spmv_dims &d, const int64_t *row_ptr,
     const int64_t blocks = (d.n_rows + RPB - 1) / RPB;
     const int remap = xcd_remap_enabled() ? 1 : 0;
     const hipStream_t st = (hipStream_t)d.stream;
-    if (variant == 2)
-        hipLaunchKernelGGL((csr_staged_kernel<L>), dim3((unsigned)blocks), dim3(kBlock), 0, st,
-                           d.n_rows, row_ptr, col, val, x, y, remap);
-    else if (csr_pair_loads())
+    if (variant >= 2) {
+        switch (csr_stage_rounds()) {
+        case 3: launch_staged<L, 3>(d, row_ptr, col, val, x, y, variant); break;
+        case 8: launch_staged<L, 8>(d, row_ptr, col, val, x, y, variant); break;
+        default: launch_staged<L, 5>(d, row_ptr, col, val, x, y, variant); break;
+        }
+    } else if (csr_pair_loads()) {
         hipLaunchKernelGGL((csr_vector_kernel<L, true>), dim3((unsigned)blocks),
                            dim3(kBlock), 0, st, d.n_rows, row_ptr, col, val, x, y, remap);
-    else
+    } else {
         hipLaunchKernelGGL((csr_vector_kernel<L, false>), dim3((unsigned)blocks),
                            dim3(kBlock), 0, st, d.n_rows, row_ptr, col, val, x, y, remap);
+    }
 }
 
 }  // namespace spmv
@@ -207,14 +300,15 @@ using namespace spmv;
 
 extern "C" int spmv_csr_auto_lanes(int64_t n_rows, int64_t nnz)
 {
-    // About one lane per 8 entries of the mean row: every lane then runs
-    // ~2 iterations of its 4-deep unrolled body, and the group is small
-    // enough that short rows waste few lanes (mean 64 -> L = 8 measured
-    // best on the cant-like batch, profiles/round1_sweep.md); rounded to a
-    // power of two in [2, 64].
+    // Lanes per row for the default (staged) variant: about one lane per 16
+    // entries of the mean row, a power of two in [2, 64].  The reduction
+    // reads LDS, so a few lanes per row suffice, and more rows per group
+    // amortise the group's offset fetch (mean 64 -> L = 4: 0.320 ms vs
+    // 0.328 ms at L = 8 on the cant-like batch, profiles/round1_sweep.md).
+    // The direct variant uses twice this (L = 8: 0.353 ms vs 0.383 at 16).
     double mean = n_rows > 0 ? (double)nnz / (double)n_rows : 0.0;
     int L = 2;
-    while (L < 64 && (double)(2 * L) * 8.0 <= mean * 1.5)
+    while (L < 64 && (double)(2 * L) * 16.0 <= mean * 1.5)
         L *= 2;
     return L;
 }
@@ -226,15 +320,20 @@ extern "C" int spmv_csr_run_variant(spmv_dims d, const int64_t *row_ptr,
 {
     if (d.n_rows < 0 || d.n_cols < 0 || d.nnz < 0)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_run: negative size");
-    if (variant < 0 || variant > 2)
-        return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_run: variant must be 0, 1 or 2");
+    if (variant < 0 || variant > 3)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_run: variant must be 0..3");
     if (d.n_rows == 0)
         return SPMV_SUCCESS;
     if ((d.n_rows + 1) / 2 > (int64_t)INT32_MAX * 64)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_run: too many rows");
     SPMV_GUARD(d);
-    const int L = lanes_per_row > 0 ? lanes_per_row : spmv_csr_auto_lanes(d.n_rows, d.nnz);
     const int v = variant ? variant : csr_default_variant();
+    int L = lanes_per_row;
+    if (L <= 0) {
+        L = spmv_csr_auto_lanes(d.n_rows, d.nnz);
+        if (v == 1 && L < 64)
+            L *= 2;
+    }
     switch (L) {
     case 2: launch_csr<2>(d, row_ptr, col, val, x, y, v); break;
     case 4: launch_csr<4>(d, row_ptr, col, val, x, y, v); break;

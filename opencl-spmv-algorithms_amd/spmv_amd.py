@@ -448,8 +448,7 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
         return dm
     ptr, col, val = csr_from_coo(m)
     if fmt == "csr":
-        L = lanes or hip_lib().spmv_csr_auto_lanes(m.n_rows, m.nnz)
-        dm.params = dict(lanes=L, variant=variant)
+        dm.params = dict(lanes=lanes, variant=variant)  # 0 = library picks
         dm.arrays = dict(row_ptr=_dev_tensor(ptr, device), col=_dev_tensor(col, device),
                          val=_dev_tensor(val, device))
         dm.stored_bytes = 12 * m.nnz + 8 * (m.n_rows + 1)

@@ -1,0 +1,78 @@
+"""The five drop-in programs ./bin/{coo,csr,ell,sigma_c,cmrs} on a GPU.
+
+Each reads a Matrix Market file (the reference's only input path, reference
+csr.c:43-91), prints the reference's lines (reference
+inc/helper_functions.h:167-182, coo.c:201, ell.c:104, csr.c:229-255) and
+checks its own result against the file-order sum; the parity verdict is
+read from the output and double-checked with the oracle by re-running the
+same file through the C-ABI in tests/test_gpu_parity.py.
+"""
+from __future__ import annotations
+
+import re
+import shutil
+import subprocess
+
+import pytest
+
+from conftest import GOLDEN, REPO
+
+pytestmark = pytest.mark.gpu
+
+PROGS = ["coo", "csr", "ell", "sigma_c", "cmrs"]
+
+
+def run(prog, *args, cwd=None, timeout=300):
+    exe = REPO / "bin" / prog
+    if not exe.exists():
+        subprocess.run(["make", "-C", str(REPO), prog], check=True, capture_output=True)
+    return subprocess.run([str(exe), *args], cwd=cwd, capture_output=True, text=True, timeout=timeout)
+
+
+@pytest.mark.parametrize("prog", PROGS)
+@pytest.mark.parametrize("case", ["ragged_shuffled", "empty_rows", "n67", "long_rows", "colmajor"])
+def test_program_on_fixture(prog, case):
+    r = run(prog, "--matrix", str(GOLDEN / f"{case}.mtx"), "--reps", "3", "--warmup", "1", "--strict",
+            "--cpu")
+    assert r.returncode == 0, r.stdout + r.stderr
+    out = r.stdout
+    assert re.search(r"^Your calculations took [0-9.]+ ms to run\.$", out, re.M)
+    assert re.search(r"^Number of operations \d+, PERFORMANCE [0-9.]+ GFlops$", out, re.M)
+    assert re.search(r"^GBytes transferred to processor [0-9.]+ - [0-9.]+, speed [0-9.]+ - [0-9.]+ GB/s$", out, re.M)
+    assert "\nresult is ok\n" in "\n" + out
+    assert "\ncpu result is ok\n" in out
+    if prog == "coo":
+        assert out.startswith("GPU calculations\n")
+    if prog == "ell":
+        assert out.startswith("average column length ")
+
+
+def test_default_paths_and_file_error(tmp_path):
+    """No arguments: the reference's default paths; missing file -> exit 3."""
+    for prog in PROGS:
+        r = run(prog, cwd=tmp_path)
+        assert r.returncode == 3, (prog, r.stdout, r.stderr)
+    # with databases/ present the programs read them (cant-like stand-in here)
+    db = tmp_path / "databases"
+    db.mkdir()
+    shutil.copy(GOLDEN / "colmajor.mtx", db / "cant.mtx")
+    shutil.copy(GOLDEN / "ragged_shuffled.mtx", db / "cant-sorted.mtx")
+    for prog in PROGS:
+        r = run(prog, "--reps", "2", cwd=tmp_path)
+        assert r.returncode == 0 and "result is ok" in r.stdout, (prog, r.stdout, r.stderr)
+
+
+def test_generated_cantlike_and_roundtrip(tmp_path):
+    """--gen cantlike --write-mtx, then the written file read back."""
+    path = tmp_path / "cantlike.mtx"
+    r = run("csr", "--gen", "cantlike", "--write-mtx", str(path), "--reps", "5", "--strict")
+    assert r.returncode == 0 and "result is ok" in r.stdout, r.stdout
+    for prog in ("sigma_c", "ell", "cmrs"):
+        r = run(prog, "--matrix", str(path), "--reps", "5", "--strict")
+        assert r.returncode == 0 and "result is ok" in r.stdout, (prog, r.stdout)
+    assert "Number of operations 8014766," in r.stdout  # 2 * 4,007,383
+
+
+def test_bad_option_exit_code():
+    r = run("csr", "--no-such-option")
+    assert r.returncode == 4

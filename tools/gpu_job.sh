@@ -30,6 +30,9 @@ for s in "${steps[@]}"; do
     prof) run prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --profile --steps 200;;
     sweep) run sweep 600 python tools/sweep.py;;
     sweep0) SPMV_XCD_REMAP=0 run sweep_noremap 600 python tools/sweep.py --rounds 2;;
+    sweepr3) SPMV_CSR_STAGE_ROUNDS=3 run sweep_r3 300 python tools/sweep.py --rounds 2 --only csr;;
+    sweepr8) SPMV_CSR_STAGE_ROUNDS=8 run sweep_r8 300 python tools/sweep.py --rounds 2 --only csr;;
+    drivers) run drivers 600 python -m pytest tests/test_drivers_gpu.py -q;;
     sweepremap) SPMV_XCD_REMAP=1 run sweep_remap 600 python tools/sweep.py --rounds 2 --only csr,sell,ell;;
     sweeprmat) run sweep_rmat 600 python tools/sweep.py --matrix rmat --rounds 2 --reps 20;;
     counters) run counters 120 rocprofv3 -L;;

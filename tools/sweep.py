@@ -22,14 +22,14 @@ sys.path[:0] = [str(REPO / "opencl-spmv-algorithms_amd"), str(REPO)]
 import spmv_amd as sa  # noqa: E402
 
 VARIANTS = [
-    ("csr", {"lanes": 4}), ("csr", {"lanes": 8}), ("csr", {"lanes": 16}), ("csr", {"lanes": 32}),
-    ("csr", {"lanes": 4, "variant": 2}), ("csr", {"lanes": 8, "variant": 2}), ("csr", {"lanes": 16, "variant": 2}),
-    ("csr", {"lanes": 64}), ("csr", {"lanes": 2, "variant": 2}),
+    ("csr", {"lanes": 8, "variant": 1}), ("csr", {"lanes": 16, "variant": 1}),
+    ("csr", {"lanes": 2, "variant": 2}), ("csr", {"lanes": 4, "variant": 2}), ("csr", {"lanes": 8, "variant": 2}),
+    ("csr", {"lanes": 2, "variant": 3}), ("csr", {"lanes": 4, "variant": 3}), ("csr", {"lanes": 8, "variant": 3}),
     ("ell", {"ki": 1}), ("ell", {"ki": 2}),
     ("sell", {"C": 64, "sigma": 1, "ki": 2}), ("sell", {"C": 64, "sigma": 256, "ki": 2}),
     ("sell", {"C": 64, "sigma": 1024, "ki": 2}), ("sell", {"C": 64, "sigma": 1024, "ki": 1}),
-    ("sell", {"C": 128, "sigma": 1024, "ki": 2}), ("sell", {"C": 32, "sigma": 1, "ki": 1}),
-    ("cmrs", {"h": 4}), ("cmrs", {"h": 8}), ("cmrs", {"h": 16}), ("cmrs", {"h": 32}),
+    ("sell", {"C": 64, "sigma": 512, "ki": 1}),
+    ("cmrs", {"h": 8}), ("cmrs", {"h": 16}), ("cmrs", {"h": 32}),
     ("coo", {}),
 ]
 

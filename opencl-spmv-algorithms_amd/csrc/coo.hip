@@ -27,13 +27,25 @@
 // slots), and lanes 0..h-1 store the strip's h contiguous y values,
 // bounds-checked.  No barrier: each wave only touches its own LDS slots.
 #include <limits.h>
+#include <stdlib.h>
 
 #include "common.h"
 
 namespace spmv {
 
 constexpr int kCooIter = 16;                  // 64-entry steps per tile
-constexpr int kCooU = 4;                      // steps loaded ahead
+constexpr int kCooUDefault = 4;               // steps loaded ahead (SPMV_COO_U: 4, 8, 16)
+
+static int coo_lookahead()
+{
+    static int cached = -1;
+    if (cached < 0) {
+        const char *s = getenv("SPMV_COO_U");
+        const int u = s ? atoi(s) : kCooUDefault;
+        cached = (u == 4 || u == 8 || u == 16) ? u : kCooUDefault;
+    }
+    return cached;
+}
 constexpr int64_t kTile = kWave * kCooIter;  // entries per wave
 
 // Inclusive segmented scan over one wave; `key` is non-decreasing across
@@ -52,6 +64,7 @@ __device__ __forceinline__ double seg_scan(double p, K key, int lane)
     return p;
 }
 
+template <int U>
 __global__ __launch_bounds__(kBlock) void coo_tile_kernel(
     int64_t n_rows, int64_t nnz, int64_t n_tiles,
     const int32_t *__restrict__ row, const int32_t *__restrict__ col,
@@ -74,22 +87,22 @@ __global__ __launch_bounds__(kBlock) void coo_tile_kernel(
     int32_t prev_r = before;  // row of the entry just before the step
     double pref = 0.0;     // this lane's share of a continued first row
 
-    // kCooU steps are loaded before any is reduced, so each lane keeps
-    // 3·kCooU loads (+ kCooU x gathers) in flight instead of one step's.
-    for (int it0 = 0; it0 < kCooIter; it0 += kCooU) {
+    // U steps are loaded before any is reduced, so each lane keeps 3·U
+    // loads (+ U x gathers) in flight instead of one step's.
+    for (int it0 = 0; it0 < kCooIter; it0 += U) {
         if (t0 + (int64_t)it0 * kWave >= t1)
             break;
-        int32_t rs[kCooU];
-        double ps[kCooU];
+        int32_t rs[U];
+        double ps[U];
 #pragma unroll
-        for (int u = 0; u < kCooU; ++u) {
+        for (int u = 0; u < U; ++u) {
             const int64_t j = t0 + (int64_t)(it0 + u) * kWave + lane;
             const bool valid = j < t1;
             rs[u] = valid ? row[j] : INT_MAX;
             ps[u] = valid ? val[j] * x[col[j]] : 0.0;
         }
 #pragma unroll
-        for (int u = 0; u < kCooU; ++u) {
+        for (int u = 0; u < U; ++u) {
             const int64_t j0 = t0 + (int64_t)(it0 + u) * kWave;
             if (j0 >= t1)
                 break;
@@ -163,6 +176,7 @@ __global__ __launch_bounds__(kBlock) void coo_carry_kernel(
 }
 
 // ------------------------------------------------------------------ CMRS
+template <int U>
 __global__ __launch_bounds__(kBlock) void cmrs_kernel(
     int64_t n_rows, int32_t h, int64_t n_strips,
     const int64_t *__restrict__ strip_ptr,
@@ -181,18 +195,18 @@ __global__ __launch_bounds__(kBlock) void cmrs_kernel(
     __builtin_amdgcn_wave_barrier();
 
     const int64_t beg = strip_ptr[s], end = strip_ptr[s + 1];
-    for (int64_t b0 = beg; b0 < end; b0 += kCooU * kWave) {
-        int keys[kCooU];
-        double ps[kCooU];
+    for (int64_t b0 = beg; b0 < end; b0 += U * kWave) {
+        int keys[U];
+        double ps[U];
 #pragma unroll
-        for (int u = 0; u < kCooU; ++u) {  // loads of kCooU steps in flight
+        for (int u = 0; u < U; ++u) {  // loads of U steps in flight
             const int64_t j = b0 + u * kWave + lane;
             const bool valid = j < end;
             keys[u] = valid ? (int)row_in_strip[j] : INT_MAX;
             ps[u] = valid ? val[j] * x[col[j]] : 0.0;
         }
 #pragma unroll
-        for (int u = 0; u < kCooU; ++u) {
+        for (int u = 0; u < U; ++u) {
             const int64_t j0 = b0 + u * kWave;
             if (j0 >= end)
                 break;
@@ -249,10 +263,17 @@ extern "C" int spmv_coo_run(spmv_dims d, const int32_t *row,
     const int64_t blocks = (tiles + (kBlock / kWave) - 1) / (kBlock / kWave);
     if (blocks > INT32_MAX)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_coo_run: grid too large");
-    hipLaunchKernelGGL(coo_tile_kernel, dim3((unsigned)blocks), dim3(kBlock), 0,
-                       (hipStream_t)d.stream, d.n_rows, d.nnz, tiles, row, col,
-                       val, x, y, carry_row, carry_val,
-                       xcd_remap_enabled() ? 1 : 0);
+    const int remap = xcd_remap_enabled() ? 1 : 0;
+#define SPMV_COO_LAUNCH(UU)                                                     \
+    hipLaunchKernelGGL(coo_tile_kernel<UU>, dim3((unsigned)blocks), dim3(kBlock), 0, \
+                       (hipStream_t)d.stream, d.n_rows, d.nnz, tiles, row, col,   \
+                       val, x, y, carry_row, carry_val, remap)
+    switch (coo_lookahead()) {
+    case 8: SPMV_COO_LAUNCH(8); break;
+    case 16: SPMV_COO_LAUNCH(16); break;
+    default: SPMV_COO_LAUNCH(4); break;
+    }
+#undef SPMV_COO_LAUNCH
     SPMV_CHECK_LAUNCH("coo_tile_kernel");
     const int64_t cblocks = (tiles + kBlock - 1) / kBlock;
     hipLaunchKernelGGL(coo_carry_kernel, dim3((unsigned)cblocks), dim3(kBlock), 0,
@@ -276,9 +297,17 @@ extern "C" int spmv_cmrs_run(spmv_dims d, int32_t h, int64_t n_strips,
     const int64_t blocks = (n_strips + (kBlock / kWave) - 1) / (kBlock / kWave);
     if (blocks > INT32_MAX)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_cmrs_run: grid too large");
-    hipLaunchKernelGGL(cmrs_kernel, dim3((unsigned)blocks), dim3(kBlock), 0,
-                       (hipStream_t)d.stream, d.n_rows, h, n_strips, strip_ptr,
-                       row_in_strip, col, val, x, y, xcd_remap_enabled() ? 1 : 0);
+    const int remap = xcd_remap_enabled() ? 1 : 0;
+#define SPMV_CMRS_LAUNCH(UU)                                                    \
+    hipLaunchKernelGGL(cmrs_kernel<UU>, dim3((unsigned)blocks), dim3(kBlock), 0,    \
+                       (hipStream_t)d.stream, d.n_rows, h, n_strips, strip_ptr,   \
+                       row_in_strip, col, val, x, y, remap)
+    switch (coo_lookahead()) {
+    case 8: SPMV_CMRS_LAUNCH(8); break;
+    case 16: SPMV_CMRS_LAUNCH(16); break;
+    default: SPMV_CMRS_LAUNCH(4); break;
+    }
+#undef SPMV_CMRS_LAUNCH
     SPMV_CHECK_LAUNCH("cmrs_kernel");
     return SPMV_SUCCESS;
 }

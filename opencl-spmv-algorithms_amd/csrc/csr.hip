@@ -100,7 +100,9 @@ __global__ __launch_bounds__(kBlock) void csr_vector_kernel(
 // 1 across lanes) and reduces with the same shuffle butterfly.  Ranges
 // longer than the LDS chunk are processed in chunks; a row's partial sum
 // stays in its lanes' registers across chunks.
-constexpr int kStageRoundsDefault = 5;  // pairs per lane per chunk: 2560 products, 20 KiB
+constexpr int kStageRoundsDefault = 4;  // pairs per lane per chunk: 2048 products, 16 KiB
+// (16 KiB keeps 8 workgroups = 32 waves per CU; 20 KiB (R = 5) capped the
+// CU at 7 and measured slower, R = 8 at 4 and much slower)
 
 // One row group (RPB = 256/L rows) of the staged scheme; s_ptr holds the
 // group's RPB+1 row offsets.  Ends with a barrier, so the caller may
@@ -226,14 +228,14 @@ static int csr_default_variant()
     return cached;
 }
 
-// SPMV_CSR_STAGE_ROUNDS in {3,5,8}: chunk = 2*256*R products (tuning knob)
+// SPMV_CSR_STAGE_ROUNDS in {3,4,5,8}: chunk = 2*256*R products (tuning knob)
 static int csr_stage_rounds()
 {
     static int cached = -1;
     if (cached < 0) {
         const char *s = getenv("SPMV_CSR_STAGE_ROUNDS");
         int r = s ? atoi(s) : kStageRoundsDefault;
-        cached = (r == 3 || r == 5 || r == 8) ? r : kStageRoundsDefault;
+        cached = (r == 3 || r == 4 || r == 5 || r == 8) ? r : kStageRoundsDefault;
     }
     return cached;
 }
@@ -282,8 +284,10 @@ static void launch_csr(const spmv_dims &d, const int64_t *row_ptr,
     if (variant >= 2) {
         switch (csr_stage_rounds()) {
         case 3: launch_staged<L, 3>(d, row_ptr, col, val, x, y, variant); break;
+        case 4: launch_staged<L, 4>(d, row_ptr, col, val, x, y, variant); break;
+        case 5: launch_staged<L, 5>(d, row_ptr, col, val, x, y, variant); break;
         case 8: launch_staged<L, 8>(d, row_ptr, col, val, x, y, variant); break;
-        default: launch_staged<L, 5>(d, row_ptr, col, val, x, y, variant); break;
+        default: launch_staged<L, 4>(d, row_ptr, col, val, x, y, variant); break;
         }
     } else if (csr_pair_loads()) {
         hipLaunchKernelGGL((csr_vector_kernel<L, true>), dim3((unsigned)blocks),

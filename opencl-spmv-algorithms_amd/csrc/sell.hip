@@ -130,7 +130,11 @@ extern "C" int spmv_sell_run(spmv_dims d, int32_t C, int32_t sigma, int32_t ki,
     const int64_t slots = n_slices * C;
     // workgroup = one sigma window when it fits (256..1024 slots, a
     // multiple of the wave), else 256 slots
-    const int bt = (sigma >= kBlock && sigma <= 1024 && sigma % kWave == 0) ? sigma : kBlock;
+    static const int force256 = [] {
+        const char *s = getenv("SPMV_SELL_BT");  // tuning knob: "256" forces 256-slot groups
+        return s && atoi(s) == 256;
+    }();
+    const int bt = (!force256 && sigma >= kBlock && sigma <= 1024 && sigma % kWave == 0) ? sigma : kBlock;
     const int64_t blocks = (slots + bt - 1) / bt;
     if (blocks > INT32_MAX)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_run: grid too large");

@@ -32,6 +32,9 @@ for s in "${steps[@]}"; do
     sweep0) SPMV_XCD_REMAP=0 run sweep_noremap 600 python tools/sweep.py --rounds 2;;
     sweepr3) SPMV_CSR_STAGE_ROUNDS=3 run sweep_r3 300 python tools/sweep.py --rounds 2 --only csr;;
     sweepr8) SPMV_CSR_STAGE_ROUNDS=8 run sweep_r8 300 python tools/sweep.py --rounds 2 --only csr;;
+    sweepbt) SPMV_SELL_BT=256 run sweep_bt256 300 python tools/sweep.py --rounds 2 --only sell;;
+    sweepu8) SPMV_COO_U=8 run sweep_u8 300 python tools/sweep.py --rounds 2 --only coo,cmrs;;
+    sweepu16) SPMV_COO_U=16 run sweep_u16 300 python tools/sweep.py --rounds 2 --only coo,cmrs;;
     drivers) run drivers 600 python -m pytest tests/test_drivers_gpu.py -q;;
     sweepremap) SPMV_XCD_REMAP=1 run sweep_remap 600 python tools/sweep.py --rounds 2 --only csr,sell,ell;;
     sweeprmat) run sweep_rmat 600 python tools/sweep.py --matrix rmat --rounds 2 --reps 20;;

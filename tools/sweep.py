@@ -28,7 +28,8 @@ VARIANTS = [
     ("ell", {"ki": 1}), ("ell", {"ki": 2}),
     ("sell", {"C": 64, "sigma": 1, "ki": 2}), ("sell", {"C": 64, "sigma": 256, "ki": 2}),
     ("sell", {"C": 64, "sigma": 1024, "ki": 2}), ("sell", {"C": 64, "sigma": 1024, "ki": 1}),
-    ("sell", {"C": 64, "sigma": 512, "ki": 1}),
+    ("sell", {"C": 64, "sigma": 512, "ki": 1}), ("sell", {"C": 64, "sigma": 256, "ki": 1}),
+    ("sell", {"C": 64, "sigma": 512, "ki": 2}),
     ("cmrs", {"h": 8}), ("cmrs", {"h": 16}), ("cmrs", {"h": 32}),
     ("coo", {}),
 ]

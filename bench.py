@@ -51,7 +51,7 @@ KERNEL_NAMES = {  # dominant kernel per format (as rocprofv3 names it)
     "coo": "coo_tile_kernel",
     "cmrs": "cmrs_kernel",
 }
-CSR_DEFAULT_VARIANT = 2  # must match csr_default_variant() in csrc/csr.hip
+CSR_DEFAULT_VARIANT = 3  # must match csr_default_variant() in csrc/csr.hip
 
 
 def parse():
@@ -66,7 +66,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0: skip)")
     p.add_argument("--lanes", type=int, default=0)
     p.add_argument("--variant", type=int, default=0, help="CSR kernel variant (0 auto, 1 direct, 2 staged)")
-    p.add_argument("--ki", type=int, default=2)
+    p.add_argument("--ki", type=int, default=0, help="k-interleave (0: format default, ELL 2, SELL 1)")
     p.add_argument("--C", type=int, default=64)
     p.add_argument("--sigma", type=int, default=1024)
     p.add_argument("--h", type=int, default=8)

@@ -124,6 +124,19 @@ int spmv_cmrs_run(spmv_dims d, int32_t h, int64_t n_strips,
                   const int32_t *col, const double *val, const double *x,
                   double *y);
 
+/* ------------------------------------------------- device generator ---
+ * Rows [row_begin, row_end) of the banded matrix of BASELINE.json
+ * configs[4] (row i: 16 entries at columns (i + o) mod n, o = -8..7),
+ * written straight into HBM — values bit-identical to the host's
+ * spmv_gen_banded_csr.  layout 0 = CSR: ptr[m+1] (local offsets),
+ * col/val[16m]; layout 1 = SELL-C with k-interleave ki (every row has 16
+ * entries, so any sigma sort is the identity): ptr = slice_ptr[ns+1],
+ * perm[ns*C], col/val[ns*C*16], ns = ceil(m/C).  m = row_end-row_begin. */
+int spmv_gen_banded_device(int64_t n, uint64_t seed, int64_t row_begin,
+                           int64_t row_end, int layout, int32_t C, int32_t ki,
+                           int64_t *ptr, int32_t *perm, int32_t *col, double *val,
+                           int device, void *stream);
+
 /* ------------------------------------------------------------ helpers ---
  * Device discovery (replaces reference inc/helper_functions.h:76-129),
  * memory (replaces clCreateBuffer / clEnqueueWriteBuffer /

@@ -54,6 +54,15 @@ int spmv_mtx_write(const char *path, int64_t n_rows, int64_t n_cols,
                    int64_t nnz, const int32_t *row, const int32_t *col,
                    const double *val, int symmetric);
 
+/* Binary cache of a parsed file: header + row, col,
+ * val arrays in file order.  The drivers' --cache option keeps PATH.bin
+ * next to PATH and reads it instead of the text when it is newer.       */
+int spmv_bin_write(const char *path, const spmv_mtx_info *info,
+                   const int32_t *row, const int32_t *col, const double *val);
+int spmv_bin_read_info(const char *path, spmv_mtx_info *info);
+int spmv_bin_read(const char *path, spmv_mtx_info *info, int32_t *row,
+                  int32_t *col, double *val);
+
 /* ------------------------------------------------------------ formats ---*/
 /* COO sorted by row, stable (file order kept inside a row).             */
 int spmv_coo_sort_by_row(int64_t n_rows, int64_t nnz, const int32_t *row,

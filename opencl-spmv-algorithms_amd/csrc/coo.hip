@@ -34,7 +34,7 @@
 namespace spmv {
 
 constexpr int kCooIter = 16;                  // 64-entry steps per tile
-constexpr int kCooUDefault = 4;               // steps loaded ahead (SPMV_COO_U: 4, 8, 16)
+constexpr int kCooUDefault = 8;               // steps loaded ahead (SPMV_COO_U: 4, 8, 16)
 
 static int coo_lookahead()
 {

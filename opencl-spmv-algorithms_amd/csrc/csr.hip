@@ -223,7 +223,7 @@ static int csr_default_variant()
     static int cached = -1;
     if (cached < 0) {
         const char *s = getenv("SPMV_CSR_VARIANT");
-        cached = (s && s[0] >= '1' && s[0] <= '3') ? s[0] - '0' : 2;
+        cached = (s && s[0] >= '1' && s[0] <= '3') ? s[0] - '0' : 3;
     }
     return cached;
 }

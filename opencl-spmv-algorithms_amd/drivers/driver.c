@@ -69,7 +69,7 @@ static int parse_opts(int argc, char **argv, spmv_format fmt, opts_t *o)
     o->warmup = 5;
     o->C = 64;
     o->sigma = 1024;
-    o->ki = 2;
+    o->ki = 0; /* 0: format default (ELL 2, SELL 1) */
     o->h = 8;
     o->cpu = fmt != FMT_SELL;
     for (int i = 1; i < argc; ++i) {
@@ -108,7 +108,7 @@ static int parse_opts(int argc, char **argv, spmv_format fmt, opts_t *o)
         }
 #undef NEEDV
     }
-    if (o->reps < 1 || o->warmup < 0 || o->copies < 1 || (o->ki != 1 && o->ki != 2) ||
+    if (o->reps < 1 || o->warmup < 0 || o->copies < 1 || (o->ki < 0 || o->ki > 2) ||
         o->h < 1 || o->h > 64 || o->C < 1 || o->C > 1024)
         return SPMV_OTHER_ERROR;
     return SPMV_SUCCESS;
@@ -289,8 +289,8 @@ static int build_format(const opts_t *o, spmv_format fmt, const coo_t *m, dev_fm
         /* reference ell.c:104 */
         printf("average column length %lf, shortest col %lld, longest col %lld\n", mean,
                (long long)mn, (long long)mx);
-        f->ki = o->ki;
-        if ((rc = spmv_ell_plan(N, ptr, o->ki, &f->K, &f->ld)))
+        f->ki = o->ki ? o->ki : 2;
+        if ((rc = spmv_ell_plan(N, ptr, f->ki, &f->K, &f->ld)))
             return rc;
         f->stored = f->ld * f->K;
         if (Z > 0 && (double)f->stored / (double)Z > 64.0) {
@@ -306,14 +306,14 @@ static int build_format(const opts_t *o, spmv_format fmt, const coo_t *m, dev_fm
     } else { /* SELL */
         f->C = o->C;
         f->sigma = o->sigma;
-        f->ki = o->ki;
-        if ((rc = spmv_sell_plan(N, ptr, o->C, o->sigma, o->ki, &f->n_slices, &f->stored)))
+        f->ki = o->ki ? o->ki : 1;
+        if ((rc = spmv_sell_plan(N, ptr, o->C, o->sigma, f->ki, &f->n_slices, &f->stored)))
             return rc;
         f->h_ptr = malloc((size_t)(f->n_slices + 1) * sizeof(int64_t));
         f->h_perm = malloc((size_t)(f->n_slices * o->C + 1) * sizeof(int32_t));
         f->h_col = malloc((size_t)(f->stored + 1) * sizeof(int32_t));
         f->h_val = malloc((size_t)(f->stored + 1) * sizeof(double));
-        if ((rc = spmv_sell_fill(N, ptr, col, val, o->C, o->sigma, o->ki, f->n_slices, f->h_ptr,
+        if ((rc = spmv_sell_fill(N, ptr, col, val, o->C, o->sigma, f->ki, f->n_slices, f->h_ptr,
                                  f->h_perm, f->h_col, f->h_val)))
             return rc;
         f->stored_bytes = (size_t)f->stored * 12 + (size_t)(f->n_slices + 1) * 8 +

@@ -82,6 +82,8 @@ HIP_SYMBOLS = {
     "spmv_ell_run": (ctypes.c_int, [Dims, _c_i32, _c_i64, _c_i32, _vp, _vp, _vp, _vp]),
     "spmv_sell_run": (ctypes.c_int, [Dims, _c_i32, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "spmv_cmrs_run": (ctypes.c_int, [Dims, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "spmv_gen_banded_device": (ctypes.c_int, [_c_i64, ctypes.c_uint64, _c_i64, _c_i64, ctypes.c_int, _c_i32,
+                                              _c_i32, _vp, _vp, _vp, _vp, ctypes.c_int, _vp]),
     "spmv_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     "spmv_set_device": (ctypes.c_int, [ctypes.c_int]),
     "spmv_device_name": (ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t]),
@@ -105,6 +107,9 @@ HOST_SYMBOLS = {
     "spmv_mtx_read_info": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(MtxInfo)]),
     "spmv_mtx_read": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(MtxInfo), _vp, _vp, _vp]),
     "spmv_mtx_write": (ctypes.c_int, [ctypes.c_char_p, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, ctypes.c_int]),
+    "spmv_bin_write": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(MtxInfo), _vp, _vp, _vp]),
+    "spmv_bin_read_info": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(MtxInfo)]),
+    "spmv_bin_read": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(MtxInfo), _vp, _vp, _vp]),
     "spmv_coo_sort_by_row": (ctypes.c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "spmv_csr_from_coo": (ctypes.c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "spmv_csr_row_stats": (ctypes.c_int, [_c_i64, _vp, ctypes.POINTER(_c_i64), ctypes.POINTER(_c_i64), ctypes.POINTER(ctypes.c_double)]),
@@ -432,7 +437,7 @@ class DeviceMatrix:
         _check(rc, f"spmv_{self.fmt}_run")
 
 
-def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int = 0, ki: int = 2, C: int = 64,
+def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int = 0, ki: int = 0, C: int = 64,
               sigma: int = 1024, h: int = 8, ell_max_padding: float | None = 64.0) -> DeviceMatrix:
     """Build `fmt` on the host (libspmv_host.so) and upload it."""
     torch = _torch()
@@ -453,11 +458,13 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
                          val=_dev_tensor(val, device))
         dm.stored_bytes = 12 * m.nnz + 8 * (m.n_rows + 1)
     elif fmt == "ell":
+        ki = ki or 2  # measured best for ELL (profiles/round1_sweep.md)
         e = ell_build(m.n_rows, ptr, col, val, ki=ki, max_padding=ell_max_padding)
         dm.params = dict(K=e["K"], ld=e["ld"], ki=ki, stored=e["stored"])
         dm.arrays = dict(col=_dev_tensor(e["col"], device), val=_dev_tensor(e["val"], device))
         dm.stored_bytes = 12 * e["stored"]
     elif fmt == "sell":
+        ki = ki or 1  # measured best for SELL-64-1024 (profiles/round1_sweep.md)
         s = sell_build(m.n_rows, ptr, col, val, C=C, sigma=sigma, ki=ki)
         dm.params = dict(C=C, sigma=sigma, ki=ki, n_slices=s["n_slices"], stored=s["stored"])
         dm.arrays = dict(slice_ptr=_dev_tensor(s["slice_ptr"], device), perm=_dev_tensor(s["perm"], device),
@@ -473,6 +480,64 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
     else:
         raise SpmvError(OTHER_ERROR, "to_device", f"unknown format {fmt}")
     return dm
+
+
+def banded_to_device(n: int, fmt: str, device="cuda:0", row_begin: int = 0, row_end: int | None = None,
+                     seed: int = 2, C: int = 64, sigma: int = 1024, ki: int = 2, lanes: int = 0,
+                     variant: int = 0) -> DeviceMatrix:
+    """Rows [row_begin, row_end) of the banded matrix (BASELINE.json
+    configs[4]) generated directly in HBM by spmv_gen_banded_device, as CSR
+    or SELL.  Row ids are local to the shard; columns are global (x is the
+    full, replicated vector)."""
+    torch = _torch()
+    device = torch.device(device)
+    row_end = n if row_end is None else row_end
+    m = row_end - row_begin
+    dm = DeviceMatrix(fmt, m, n, 16 * m, device)
+    stream = torch.cuda.current_stream(device)
+    if fmt == "csr":
+        ptr = torch.empty(m + 1, dtype=torch.int64, device=device)
+        col = torch.empty(16 * m, dtype=torch.int32, device=device)
+        val = torch.empty(16 * m, dtype=torch.float64, device=device)
+        rc = hip_lib().spmv_gen_banded_device(n, seed, row_begin, row_end, 0, 0, 0, _ptr(ptr), None, _ptr(col),
+                                              _ptr(val), device.index or 0, stream.cuda_stream)
+        dm.params = dict(lanes=lanes, variant=variant)
+        dm.arrays = dict(row_ptr=ptr, col=col, val=val)
+        dm.stored_bytes = 12 * 16 * m + 8 * (m + 1)
+    elif fmt == "sell":
+        ns = (m + C - 1) // C
+        sp = torch.empty(ns + 1, dtype=torch.int64, device=device)
+        perm = torch.empty(ns * C, dtype=torch.int32, device=device)
+        col = torch.empty(ns * C * 16, dtype=torch.int32, device=device)
+        val = torch.empty(ns * C * 16, dtype=torch.float64, device=device)
+        rc = hip_lib().spmv_gen_banded_device(n, seed, row_begin, row_end, 1, C, ki, _ptr(sp), _ptr(perm),
+                                              _ptr(col), _ptr(val), device.index or 0, stream.cuda_stream)
+        dm.params = dict(C=C, sigma=sigma, ki=ki, n_slices=ns, stored=ns * C * 16)
+        dm.arrays = dict(slice_ptr=sp, perm=perm, col=col, val=val)
+        dm.stored_bytes = 12 * ns * C * 16 + 8 * (ns + 1) + 4 * ns * C
+    else:
+        raise SpmvError(OTHER_ERROR, "banded_to_device", "format must be csr or sell")
+    _check(rc, "spmv_gen_banded_device")
+    return dm
+
+
+def read_bin(path) -> Coo:
+    """Binary cache written by write_bin / the drivers' --cache."""
+    lib = host_lib()
+    info = MtxInfo()
+    p = str(path).encode()
+    _check_host(lib.spmv_bin_read_info(p, ctypes.byref(info)), f"read {path}")
+    row = np.empty(info.nnz, np.int32)
+    col = np.empty(info.nnz, np.int32)
+    val = np.empty(info.nnz, np.float64)
+    _check_host(lib.spmv_bin_read(p, ctypes.byref(info), _ptr(row), _ptr(col), _ptr(val)), f"read {path}")
+    return Coo(info.n_rows, info.n_cols, row, col, val, bool(info.symmetric), str(path))
+
+
+def write_bin(path, m: Coo) -> None:
+    info = MtxInfo(m.n_rows, m.n_cols, m.nnz, int(m.symmetric), 0, 0)
+    _check_host(host_lib().spmv_bin_write(str(path).encode(), ctypes.byref(info), _ptr(m.row), _ptr(m.col),
+                                          _ptr(m.val)), f"write {path}")
 
 
 def flush_cache(stream=None, nbytes: int = 0) -> None:

@@ -32,6 +32,15 @@ class DeviceGuard {
 // XCD-contiguous blockIdx remap switch (SPMV_XCD_REMAP=1 enables; read once).
 bool xcd_remap_enabled();
 
+// LDS-staged CMRS / COO launchers (staged.hip)
+int launch_cmrs_staged(const spmv_dims &d, int32_t h, int64_t n_strips,
+                       const int64_t *strip_ptr, const uint8_t *rin, const int32_t *col,
+                       const double *val, const double *x, double *y);
+int launch_coo_staged(const spmv_dims &d, const int32_t *row, const int32_t *col,
+                      const double *val, const double *x, double *y, int32_t *carry_row,
+                      double *carry_val);
+int64_t coo_staged_tile();
+
 // ------------------------------------------------------- device helpers
 // Bijective blockIdx remap: blocks b and b+8 are dealt to the same XCD
 // (MI355X_MICROARCH.md §Workgroup dispatch), so give each such group a

@@ -36,6 +36,14 @@ namespace spmv {
 constexpr int kCooIter = 16;                  // 64-entry steps per tile
 constexpr int kCooUDefault = 8;               // steps loaded ahead (SPMV_COO_U: 4, 8, 16)
 
+// Kernel choice: "1" = wave segmented scan (this file), "2" = LDS-staged
+// (staged.hip, default).  Read once per variable.
+static bool staged_variant(const char *env)
+{
+    const char *s = getenv(env);
+    return !(s && s[0] == '1');
+}
+
 static int coo_lookahead()
 {
     static int cached = -1;
@@ -257,6 +265,19 @@ extern "C" int spmv_coo_run(spmv_dims d, const int32_t *row,
     }
     if (!ws || ws_bytes < spmv_coo_ws_bytes(d.nnz))
         return fail_msg(SPMV_OTHER_ERROR, "spmv_coo_run: workspace too small");
+    if (staged_variant("SPMV_COO_VARIANT")) {
+        // staged tiles are larger than kTile, so the workspace suffices
+        const int64_t st_tiles = (d.nnz + coo_staged_tile() - 1) / coo_staged_tile();
+        double *cv = (double *)ws;
+        int32_t *cr = (int32_t *)(cv + st_tiles);
+        int rc = launch_coo_staged(d, row, col, val, x, y, cr, cv);
+        if (rc != SPMV_SUCCESS)
+            return rc;
+        hipLaunchKernelGGL(coo_carry_kernel, dim3((unsigned)((st_tiles + kBlock - 1) / kBlock)),
+                           dim3(kBlock), 0, (hipStream_t)d.stream, st_tiles, cr, cv, y);
+        SPMV_CHECK_LAUNCH("coo_carry_kernel");
+        return SPMV_SUCCESS;
+    }
     const int64_t tiles = (d.nnz + kTile - 1) / kTile;
     double *carry_val = (double *)ws;
     int32_t *carry_row = (int32_t *)(carry_val + tiles);
@@ -294,6 +315,8 @@ extern "C" int spmv_cmrs_run(spmv_dims d, int32_t h, int64_t n_strips,
     if (d.n_rows == 0)
         return SPMV_SUCCESS;
     SPMV_GUARD(d);
+    if (staged_variant("SPMV_CMRS_VARIANT"))
+        return launch_cmrs_staged(d, h, n_strips, strip_ptr, row_in_strip, col, val, x, y);
     const int64_t blocks = (n_strips + (kBlock / kWave) - 1) / (kBlock / kWave);
     if (blocks > INT32_MAX)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_cmrs_run: grid too large");

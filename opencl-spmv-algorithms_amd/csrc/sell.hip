@@ -134,7 +134,13 @@ extern "C" int spmv_sell_run(spmv_dims d, int32_t C, int32_t sigma, int32_t ki,
         const char *s = getenv("SPMV_SELL_BT");  // tuning knob: "256" forces 256-slot groups
         return s && atoi(s) == 256;
     }();
-    const int bt = (!force256 && sigma >= kBlock && sigma <= 1024 && sigma % kWave == 0) ? sigma : kBlock;
+    // A small matrix (fewer than ~2 windows per CU) needs the parallelism of
+    // 256-slot groups more than merged stores: one cant-like copy has only
+    // 61 windows of 1024 rows for 256 CUs.
+    const int64_t windows = sigma > 1 ? (slots + sigma - 1) / sigma : 0;
+    const bool wide = !force256 && windows >= 512 && sigma >= kBlock && sigma <= 1024 &&
+                      sigma % kWave == 0;
+    const int bt = wide ? sigma : kBlock;
     const int64_t blocks = (slots + bt - 1) / bt;
     if (blocks > INT32_MAX)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_run: grid too large");

@@ -35,6 +35,9 @@ for s in "${steps[@]}"; do
     sweepbt) SPMV_SELL_BT=256 run sweep_bt256 300 python tools/sweep.py --rounds 2 --only sell;;
     sweepu8) SPMV_COO_U=8 run sweep_u8 300 python tools/sweep.py --rounds 2 --only coo,cmrs;;
     sweepu16) SPMV_COO_U=16 run sweep_u16 300 python tools/sweep.py --rounds 2 --only coo,cmrs;;
+    sweepcoo) run sweep_coo 300 python tools/sweep.py --rounds 2 --only coo,cmrs;;
+    sweepcoo1) SPMV_COO_VARIANT=1 SPMV_CMRS_VARIANT=1 run sweep_coo1 300 python tools/sweep.py --rounds 2 --only coo,cmrs;;
+    sweeprmat2) run sweep_rmat 900 python tools/sweep.py --matrix rmat --rounds 1 --reps 20;;
     drivers) run drivers 600 python -m pytest tests/test_drivers_gpu.py -q;;
     sweepremap) SPMV_XCD_REMAP=1 run sweep_remap 600 python tools/sweep.py --rounds 2 --only csr,sell,ell;;
     sweeprmat) run sweep_rmat 600 python tools/sweep.py --matrix rmat --rounds 2 --reps 20;;

@@ -61,6 +61,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--format", default="csr", choices=sa.FORMATS)
     p.add_argument("--copies", type=int, default=32, help="cant-like copies per GPU (batch)")
+    p.add_argument("--workload", default="cantlike", choices=["cantlike", "rmat", "banded"],
+                   help="cantlike (default, configs[1]/[2]); rmat (configs[3]); banded (configs[4])")
+    p.add_argument("--banded-rows", type=int, default=100_000_000)
     p.add_argument("--per-format", default="auto", choices=["auto", "yes", "no"],
                    help="also measure the other formats (default: at N=1 only)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0: skip)")
@@ -153,6 +156,94 @@ def traffic_for(fmt, workload_bytes):
     return t.get("hbm_bytes_per_launch")
 
 
+def build_workload(args, torch, dev, rank, world):
+    """This rank's share of the workload, resident in HBM.
+
+    cantlike (default, weak scaling): rank r owns copies [r·B, (r+1)·B) of
+        a block-diagonal stack of cant-like matrices; its x block is local.
+    rmat (strong scaling, BASELINE.json configs[3] / north-star sweep): the
+        1e7 x 1e7 / 1e8-entry R-MAT, rows cut by spmv_partition_rows into
+        nnz-balanced ranges aligned to 1024; x replicated.
+    banded (strong scaling, configs[4]): the 1e8-row / 1.6e9-entry banded
+        matrix, equal row ranges, each shard generated on its GPU.
+    """
+    fk = fmt_kwargs(args, args.format)
+    if args.workload == "cantlike":
+        B = args.copies
+        m = sa.gen_cantlike(0, B)
+        x = torch.from_numpy(sa.ramp_x(m.n_cols) + rank * m.n_cols).to(dev)  # this shard's x block
+        y = torch.empty(m.n_rows, dtype=torch.float64, device=dev)
+        dm = sa.to_device(m, args.format, dev, **fk)
+        b = sa.bytes_alg(m.n_rows, m.n_cols, m.nnz)
+        single = sa.gen_cantlike(0, 1)
+
+        def check():
+            bad, first = sa.check(single, x[:single.n_cols].cpu().numpy(), y[:single.n_rows].cpu().numpy())
+            return f"row {first}" if bad else None
+
+        return dict(dm=dm, x=x, y=y, m=m, rows=m.n_rows, nnz=m.nnz, bytes_rank=b, bytes_total=b * world,
+                    nnz_total=m.nnz * world, max_rows=m.n_rows, check=check, scaling="weak",
+                    data="synthetic: cant-like stand-in (62,451 rows, 4,007,383 entries = SuiteSparse cant's "
+                         "counts; the reference's cant.mtx is an unfetched Git-LFS pointer), x[j] = j",
+                    config={"workload": f"{args.format} SpMV on a block-diagonal batch of {B} cant-like copies "
+                                        "per GPU (BASELINE.json configs[1]"
+                                        + (")" if args.format == "csr" else "-style)"),
+                            "copies_per_gpu": B})
+    if args.workload == "rmat":
+        full = sa.gen_rmat()  # deterministic: every rank builds the same matrix
+        ptr, col, val = sa.csr_from_coo(full)
+        bounds = sa.partition_rows(full.n_rows, ptr, world, align=1024)
+        lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+        lptr = ptr[lo:hi + 1] - ptr[lo]
+        loc = sa.Coo(hi - lo, full.n_cols, np.repeat(np.arange(hi - lo, dtype=np.int32), np.diff(lptr)),
+                     col[ptr[lo]:ptr[hi]], val[ptr[lo]:ptr[hi]])
+        del full
+        x = torch.from_numpy(sa.ramp_x(loc.n_cols)).to(dev)
+        y = torch.empty(max(loc.n_rows, 1), dtype=torch.float64, device=dev)
+        dm = sa.to_device(loc, args.format, dev, **fk)
+        n, z = 10_000_000, 100_000_000
+        max_rows = int(np.max(np.diff(bounds)))
+
+        def check():
+            bad, first = sa.check(loc, sa.ramp_x(loc.n_cols), y[:loc.n_rows].cpu().numpy())
+            return f"row {first}" if bad else None
+
+        return dict(dm=dm, x=x, y=y, rows=loc.n_rows, nnz=loc.nnz,
+                    bytes_rank=sa.bytes_alg(loc.n_rows, loc.n_cols, loc.nnz), bytes_total=sa.bytes_alg(n, n, z),
+                    nnz_total=z, max_rows=max_rows, check=check, scaling="strong",
+                    data="synthetic: R-MAT (a,b,c,d)=(.57,.19,.19,.05), 1e7 rows, 1e8 entries, seed 1, x[j] = j",
+                    config={"workload": f"{args.format} SpMV on R-MAT 1e7/1e8 row-sharded over {world} GPU(s) "
+                                        "(BASELINE.json configs[3])"})
+    # banded
+    n = args.banded_rows
+    step = (n // world + 1023) // 1024 * 1024
+    lo, hi = min(rank * step, n), min((rank + 1) * step, n)
+    ksell = {k: v for k, v in fk.items() if k in ("C", "sigma", "ki")}
+    if args.format == "sell":
+        ksell["ki"] = ksell.get("ki") or 1
+        dm = sa.banded_to_device(n, "sell", dev, lo, hi, **ksell)
+    elif args.format == "csr":
+        dm = sa.banded_to_device(n, "csr", dev, lo, hi, lanes=args.lanes, variant=args.variant)
+    else:
+        raise SystemExit("--workload banded supports --format csr or sell")
+    x = torch.ones(n, dtype=torch.float64, device=dev)
+    y = torch.empty(max(hi - lo, 1), dtype=torch.float64, device=dev)
+
+    def check():  # x = 1: y_i is the sum of row i's 16 values (host generator)
+        k = min(hi - lo, 4096)
+        _, _, v = sa.gen_banded_csr(n, lo, lo + k)
+        ok = np.allclose(y[:k].cpu().numpy(), v.reshape(-1, 16).sum(axis=1), rtol=1e-12, atol=1e-12)
+        return None if ok else "banded row sums"
+
+    return dict(dm=dm, x=x, y=y, rows=hi - lo, nnz=16 * (hi - lo),
+                bytes_rank=sa.bytes_alg(hi - lo, n, 16 * (hi - lo)) - 8 * n + 8 * (hi - lo),
+                bytes_total=sa.bytes_alg(n, n, 16 * n), nnz_total=16 * n, max_rows=step, check=check,
+                scaling="strong",
+                data=f"synthetic: banded, {n} rows x 16 entries at offsets -8..7 (mod n), generated on device, x = 1",
+                config={"workload": f"{args.format} SpMV on the banded {n}-row / {16 * n}-entry matrix "
+                                    f"row-sharded over {world} GPU(s) (BASELINE.json configs[4])"})
+
+
 def cpu_baseline(m_single_csr, copies, budget_s):
     """The oracle's restatement of the reference's OpenMP CSR loop
     (reference csr.c:285-309) on the same batch, bounded to ~budget_s."""
@@ -206,28 +297,20 @@ def main():
         else:
             dist.init_process_group("gloo")
 
-    # ---- the batch: B cant-like copies, this rank's row shard
-    B = args.copies
-    single = sa.gen_cantlike(0, 1)
-    m = sa.gen_cantlike(0, B)
-    n_rows, n_cols, nnz = m.n_rows, m.n_cols, m.nnz
-    bytes_step = sa.bytes_alg(n_rows, n_cols, nnz)
-    x = torch.from_numpy(sa.ramp_x(n_cols) + rank * n_cols).to(dev)  # this shard's block of x
-    y = torch.empty(n_rows, dtype=torch.float64, device=dev)
-
-    dm = sa.to_device(m, args.format, dev, **fmt_kwargs(args, args.format))
+    w = build_workload(args, torch, dev, rank, world)
+    dm, x, y = w["dm"], w["x"], w["y"]
+    n_rows, nnz, bytes_step = w["rows"], w["nnz"], w["bytes_rank"]
     wall, kern = time_steps(torch, dm, x, y, args.steps, args.warmup, dist)
     if args.profile:
         if rank == 0:
             print(json.dumps({"profile_run": args.format, "ms_per_launch": float(np.mean(kern))}))
         return
 
-    # parity spot check of this step's output against the host check
-    yh = y.cpu().numpy()
-    xh = x.cpu().numpy()
-    bad, first = sa.check(single, xh[:single.n_cols], yh[:single.n_rows])
+    # parity spot check of this step's output (host check_result rule)
+    bad = w["check"]()
     if bad:
-        raise SystemExit(f"rank {rank}: parity failure at row {first}")
+        raise SystemExit(f"rank {rank}: parity failure ({bad})")
+    single = sa.gen_cantlike(0, 1)
 
     wall_t = torch.tensor([wall], dtype=torch.float64, device=cdev)
     kern_mean = float(np.mean(kern))
@@ -237,20 +320,24 @@ def main():
         dist.all_reduce(kern_t, op=dist.ReduceOp.MAX)
     wall_max = float(wall_t.item())
     ms_per_step = wall_max / args.steps * 1e3
-    total_bytes = bytes_step * world
+    total_bytes = w["bytes_total"]
     value = total_bytes / (ms_per_step * 1e-3) * 1e-9
-    gflops = 2.0 * nnz * world / (ms_per_step * 1e-3) * 1e-9
+    gflops = 2.0 * w["nnz_total"] / (ms_per_step * 1e-3) * 1e-9
 
-    # ---- y all-gather over RCCL (timed separately, not in `value`)
+    # ---- y all-gather over RCCL (timed separately, not in `value`);
+    # shards are padded to the largest one (all_gather_into_tensor needs
+    # equal sizes), then the real rows are the concatenation of the shards
     allgather = None
     if dist is not None:
-        y_loc = y if cdev.type == "cuda" else y.cpu()
-        y_all = torch.empty(n_rows * world, dtype=torch.float64, device=cdev)
+        pad = w["max_rows"]
+        y_loc = torch.zeros(pad, dtype=torch.float64, device=cdev)
+        y_loc[:n_rows] = y if cdev.type == "cuda" else y.cpu()
+        y_all = torch.empty(pad * world, dtype=torch.float64, device=cdev)
         for _ in range(3):
             dist.all_gather_into_tensor(y_all, y_loc)
         torch.cuda.synchronize()
         # the gathered vector must hold every rank's shard in rank order
-        if not torch.equal(y_all[rank * n_rows:(rank + 1) * n_rows], y_loc):
+        if not torch.equal(y_all[rank * pad:(rank + 1) * pad], y_loc):
             raise SystemExit(f"rank {rank}: all-gathered y does not match the local shard")
         dist.barrier()
         t0 = time.perf_counter()
@@ -276,8 +363,10 @@ def main():
     cant_single = None
     cpu = None
     do_pf = args.per_format == "yes" or (args.per_format == "auto" and world == 1)
+    do_pf = do_pf and args.workload == "cantlike"
     if rank == 0 and do_pf:
-        del dm
+        m, B = w["m"], args.copies
+        del dm, w["dm"]
         torch.cuda.empty_cache()
         per_format = {}
         cant_single = {}
@@ -317,16 +406,13 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 5),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": w["scaling"],
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic: cant-like stand-in (62,451 rows, 4,007,383 entries = SuiteSparse cant's counts; "
-                    "the reference's cant.mtx is an unfetched Git-LFS pointer), x[j] = j",
-            "config": {"workload": f"{args.format} SpMV on a block-diagonal batch of {B} cant-like copies per GPU "
-                                   f"(BASELINE.json configs[1]" + (")" if args.format == "csr" else "-style)"),
-                       "format": args.format, "params": fmt_kwargs(args, args.format) or None,
-                       "copies_per_gpu": B, "rows_per_gpu": n_rows, "nnz_per_gpu": nnz,
-                       "bytes_alg_per_gpu_step": bytes_step, "parallelism": f"row-shard x{world}"},
+            "data": w["data"],
+            "config": dict(w["config"], format=args.format, params=fmt_kwargs(args, args.format) or None,
+                           rows_rank0=n_rows, nnz_rank0=nnz, bytes_alg_rank0_step=bytes_step,
+                           bytes_alg_all_ranks_step=total_bytes, parallelism=f"row-shard x{world}"),
             "gflops": round(gflops, 1),
             "roofline": roofline,
             "cpu_baseline": cpu,

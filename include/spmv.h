@@ -79,6 +79,14 @@ int spmv_csr_run_variant(spmv_dims d, const int64_t *row_ptr,
                          const int32_t *col, const double *val,
                          const double *x, double *y, int lanes_per_row,
                          int variant);
+/* Entry-balanced CSR for skewed row lengths (power-law / R-MAT hubs):
+ * every workgroup takes the same number of ENTRIES, whatever the rows; a
+ * row that spans workgroups is finished by a deterministic carry pass (as
+ * COO).  `ws` is device scratch of spmv_csr_tiled_ws_bytes() bytes.      */
+size_t spmv_csr_tiled_ws_bytes(int64_t n_rows, int64_t nnz);
+int spmv_csr_run_tiled(spmv_dims d, const int64_t *row_ptr, const int32_t *col,
+                       const double *val, const double *x, double *y, void *ws,
+                       size_t ws_bytes);
 
 /* ---------------------------------------------------------------- ELL ---
  * Replaces kernel `ell(val,idx,x,y,int N,int K,__local)` (reference

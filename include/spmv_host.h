@@ -76,6 +76,11 @@ int spmv_csr_from_coo(int64_t n_rows, int64_t nnz, const int32_t *row,
 /* Row-length statistics of a CSR matrix. */
 int spmv_csr_row_stats(int64_t n_rows, const int64_t *row_ptr,
                        int64_t *min_len, int64_t *max_len, double *mean_len);
+/* CSR kernel variant for this matrix (include/spmv.h): 4 = entry-balanced
+ * tiled (spmv_csr_run_tiled) when the longest row exceeds both 4,096
+ * entries and 64x the mean (a row-per-group kernel would then wait on one
+ * group), else 0 (the library's row-group default).                    */
+int spmv_csr_pick_variant(int64_t n_rows, const int64_t *row_ptr);
 
 /* ELL, column-major with leading dimension ld = round_up(N, 64) and
  * k-interleave ki (spmv.h).  K = round_up(max row length, ki).

@@ -40,6 +40,13 @@ int launch_coo_staged(const spmv_dims &d, const int32_t *row, const int32_t *col
                       const double *val, const double *x, double *y, int32_t *carry_row,
                       double *carry_val);
 int64_t coo_staged_tile();
+int launch_csr_tiled(const spmv_dims &d, const int64_t *row_ptr, const int32_t *col,
+                     const double *val, const double *x, double *y, int32_t *own_lo,
+                     int32_t *carry_row, double *carry_val);
+int64_t csr_tiled_tile();
+// the deterministic carry pass shared by COO and tiled CSR (coo.hip)
+int launch_carry(int64_t tiles, const int32_t *carry_row, const double *carry_val, double *y,
+                 hipStream_t stream);
 
 // ------------------------------------------------------- device helpers
 // Bijective blockIdx remap: blocks b and b+8 are dealt to the same XCD

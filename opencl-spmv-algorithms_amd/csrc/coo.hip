@@ -183,6 +183,17 @@ __global__ __launch_bounds__(kBlock) void coo_carry_kernel(
     y[r] += s;
 }
 
+int launch_carry(int64_t tiles, const int32_t *carry_row, const double *carry_val, double *y,
+                 hipStream_t stream)
+{
+    if (tiles <= 0)
+        return SPMV_SUCCESS;
+    hipLaunchKernelGGL(coo_carry_kernel, dim3((unsigned)((tiles + kBlock - 1) / kBlock)),
+                       dim3(kBlock), 0, stream, tiles, carry_row, carry_val, y);
+    SPMV_CHECK_LAUNCH("coo_carry_kernel");
+    return SPMV_SUCCESS;
+}
+
 // ------------------------------------------------------------------ CMRS
 template <int U>
 __global__ __launch_bounds__(kBlock) void cmrs_kernel(

@@ -359,3 +359,38 @@ extern "C" int spmv_csr_run(spmv_dims d, const int64_t *row_ptr,
 {
     return spmv_csr_run_variant(d, row_ptr, col, val, x, y, lanes_per_row, 0);
 }
+
+extern "C" size_t spmv_csr_tiled_ws_bytes(int64_t n_rows, int64_t nnz)
+{
+    (void)n_rows;
+    const int64_t tiles = nnz > 0 ? (nnz + csr_tiled_tile() - 1) / csr_tiled_tile() : 0;
+    // carry_val[tiles] f64, own_lo[tiles+1] i32, carry_row[tiles] i32
+    return (size_t)(8 * tiles + 4 * (tiles + 1) + 4 * tiles + 16);
+}
+
+extern "C" int spmv_csr_run_tiled(spmv_dims d, const int64_t *row_ptr, const int32_t *col,
+                                  const double *val, const double *x, double *y, void *ws,
+                                  size_t ws_bytes)
+{
+    if (d.n_rows < 0 || d.n_cols < 0 || d.nnz < 0 || d.n_rows > INT32_MAX)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_run_tiled: bad sizes");
+    if (d.n_rows == 0)
+        return SPMV_SUCCESS;
+    SPMV_GUARD(d);
+    if (d.nnz == 0) {
+        hipError_t e = hipMemsetAsync(y, 0, (size_t)d.n_rows * sizeof(double), (hipStream_t)d.stream);
+        return e == hipSuccess ? SPMV_SUCCESS : fail(SPMV_PROGRAM_ERROR, "memset y", e);
+    }
+    if (!ws || ws_bytes < spmv_csr_tiled_ws_bytes(d.n_rows, d.nnz))
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_run_tiled: workspace too small");
+    const int64_t tiles = (d.nnz + csr_tiled_tile() - 1) / csr_tiled_tile();
+    if (tiles > INT32_MAX)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_run_tiled: grid too large");
+    double *carry_val = (double *)ws;
+    int32_t *own_lo = (int32_t *)(carry_val + tiles);
+    int32_t *carry_row = own_lo + tiles + 1;
+    int rc = launch_csr_tiled(d, row_ptr, col, val, x, y, own_lo, carry_row, carry_val);
+    if (rc != SPMV_SUCCESS)
+        return rc;
+    return launch_carry(tiles, carry_row, carry_val, y, (hipStream_t)d.stream);
+}

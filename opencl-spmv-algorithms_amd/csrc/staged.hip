@@ -165,8 +165,9 @@ __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
             carry_val[tile] = c;
         }
     }
-    // owned rows: (prev, last], plus the trailing empty rows in the last tile
-    const int64_t r_lo = (int64_t)prev + 1 + (first_continues ? 1 : 0);
+    // owned rows: (prev, last], plus the trailing empty rows in the last
+    // tile; a continued first row equals prev, so it is excluded here
+    const int64_t r_lo = (int64_t)prev + 1;
     const int64_t r_hi = t1 == nnz ? n_rows - 1 : (int64_t)last;
     for (int64_t r = r_lo + g; r <= r_hi; r += GROUPS) {
         double s = 0.0;
@@ -180,6 +181,112 @@ __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
         if (lane == 0)
             y[r] = s;
     }
+}
+
+// ------------------------------------------------------------ CSR tiled
+// Entry-balanced CSR for skewed row lengths (R-MAT hubs of ~1e5 entries):
+// a workgroup owns a fixed tile of CH entries, never a fixed row count, so
+// no workgroup streams more than CH entries.  A row is OWNED by the tile
+// holding its first offset row_ptr[r] (trailing empty rows: the last
+// tile); the owner writes y[r] = its partial sum, later tiles that the row
+// runs into write carry[tile], finished by coo_carry_kernel.
+// own_lo[t] = first row with row_ptr >= t·CH (pre-pass, one binary search
+// per tile over row_ptr).
+__global__ __launch_bounds__(kBlock) void csr_tile_rows_kernel(int64_t n_rows, int64_t nnz,
+                                                               int64_t tiles, int64_t ch,
+                                                               const int64_t *__restrict__ row_ptr,
+                                                               int32_t *__restrict__ own_lo)
+{
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (t > tiles)
+        return;
+    const int64_t off = t * ch < nnz ? t * ch : nnz + 1;  // t = tiles: past every row
+    int64_t lo = 0, hi = n_rows;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (row_ptr[mid] < off)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    own_lo[t] = (int32_t)lo;
+}
+
+template <int L, int R>
+__global__ __launch_bounds__(kBlock) void csr_tiled_kernel(
+    int64_t n_rows, int64_t nnz, const int64_t *__restrict__ row_ptr,
+    const int32_t *__restrict__ col, const double *__restrict__ val,
+    const double *__restrict__ x, double *__restrict__ y,
+    const int32_t *__restrict__ own_lo, int32_t *__restrict__ carry_row,
+    double *__restrict__ carry_val)
+{
+    constexpr int CH = 2 * kBlock * R;
+    constexpr int GROUPS = kBlock / L;
+    __shared__ double2 s_prod[kBlock * R];
+    const double *prod = reinterpret_cast<const double *>(s_prod);
+    const int64_t tile = blockIdx.x;
+    const int64_t t0 = tile * CH;
+    const int64_t t1 = t0 + CH < nnz ? t0 + CH : nnz;
+    const int64_t r_lo = own_lo[tile];
+    const int64_t r_hi = t1 == nnz ? n_rows - 1 : (int64_t)own_lo[tile + 1] - 1;
+    stage_chunk<R>(t0, t1, col, val, x, s_prod, [](int, int64_t, int) {});
+    __syncthreads();
+    const int g = threadIdx.x / L, lane = threadIdx.x % L;
+
+    // carry: entry t0 lies in row r_lo-1 when no row starts exactly at t0
+    if (g == 0) {
+        double c = 0.0;
+        int32_t cr = -1;
+        if (r_lo > 0 && (r_lo == n_rows || row_ptr[r_lo] > t0)) {
+            cr = (int32_t)(r_lo - 1);
+            const int64_t e = row_ptr[r_lo - 1 + 1] < t1 ? row_ptr[r_lo] : t1;
+            for (int64_t j = t0 + lane; j < e; j += L)
+                c += prod[j - t0];
+        }
+        c = group_sum<L>(c);
+        if (lane == 0) {
+            carry_row[tile] = cr;
+            carry_val[tile] = c;
+        }
+    }
+    for (int64_t r = r_lo + g; r <= r_hi; r += GROUPS) {
+        const int64_t a = row_ptr[r];
+        int64_t b = row_ptr[r + 1];
+        b = b < t1 ? b : t1;
+        double s = 0.0;
+        for (int64_t j = a + lane; j < b; j += L)
+            s += prod[j - t0];
+        s = group_sum<L>(s);
+        if (lane == 0)
+            y[r] = s;
+    }
+}
+
+int64_t csr_tiled_tile() { return 2 * kBlock * 3; }
+
+int launch_csr_tiled(const spmv_dims &d, const int64_t *row_ptr, const int32_t *col,
+                     const double *val, const double *x, double *y, int32_t *own_lo,
+                     int32_t *carry_row, double *carry_val)
+{
+    constexpr int R = 3;
+    const int64_t ch = csr_tiled_tile();
+    const int64_t tiles = (d.nnz + ch - 1) / ch;
+    const hipStream_t st = (hipStream_t)d.stream;
+    hipLaunchKernelGGL(csr_tile_rows_kernel, dim3((unsigned)((tiles + 1 + kBlock - 1) / kBlock)),
+                       dim3(kBlock), 0, st, d.n_rows, d.nnz, tiles, ch, row_ptr, own_lo);
+    SPMV_CHECK_LAUNCH("csr_tile_rows_kernel");
+    const double mean = d.n_rows > 0 ? (double)d.nnz / (double)d.n_rows : 0.0;
+    if (mean >= 48.0)
+        hipLaunchKernelGGL((csr_tiled_kernel<8, R>), dim3((unsigned)tiles), dim3(kBlock), 0, st,
+                           d.n_rows, d.nnz, row_ptr, col, val, x, y, own_lo, carry_row, carry_val);
+    else if (mean >= 12.0)
+        hipLaunchKernelGGL((csr_tiled_kernel<4, R>), dim3((unsigned)tiles), dim3(kBlock), 0, st,
+                           d.n_rows, d.nnz, row_ptr, col, val, x, y, own_lo, carry_row, carry_val);
+    else
+        hipLaunchKernelGGL((csr_tiled_kernel<2, R>), dim3((unsigned)tiles), dim3(kBlock), 0, st,
+                           d.n_rows, d.nnz, row_ptr, col, val, x, y, own_lo, carry_row, carry_val);
+    SPMV_CHECK_LAUNCH("csr_tiled_kernel");
+    return SPMV_SUCCESS;
 }
 
 // ----------------------------------------------------------- launchers

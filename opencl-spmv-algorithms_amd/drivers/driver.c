@@ -198,7 +198,7 @@ typedef struct {
     double *d_val, *d_x, *d_y;
     void *d_ws;
     size_t ws_bytes;
-    int32_t K, C, sigma, ki, h, lanes;
+    int32_t K, C, sigma, ki, h, lanes, variant;
     int64_t ld, n_slices, n_strips;
     /* host copies for the CPU loop */
     int64_t *h_ptr;
@@ -260,9 +260,15 @@ static int build_format(const opts_t *o, spmv_format fmt, const coo_t *m, dev_fm
         f->stored = Z;
         if (fmt == FMT_CSR) {
             f->lanes = o->lanes > 0 ? o->lanes : spmv_csr_auto_lanes(N, Z);
+            f->variant = spmv_csr_pick_variant(N, ptr); /* 4: entry-balanced (skewed rows) */
             f->stored_bytes = (size_t)Z * 12 + (size_t)(N + 1) * 8;
             if ((rc = upload((void **)&f->d_ptr, ptr, (size_t)(N + 1) * 8, NULL)))
                 return rc;
+            if (f->variant == 4) {
+                f->ws_bytes = spmv_csr_tiled_ws_bytes(N, Z);
+                if ((rc = spmv_malloc(&f->d_ws, f->ws_bytes)))
+                    return rc;
+            }
         } else {
             f->h = o->h;
             f->n_strips = (N + o->h - 1) / o->h;
@@ -339,6 +345,9 @@ static int launch(void *arg)
         return spmv_coo_run(f->d, f->d_row, f->d_col, f->d_val, f->d_x, f->d_y, f->d_ws,
                             f->ws_bytes);
     case FMT_CSR:
+        if (f->variant == 4)
+            return spmv_csr_run_tiled(f->d, f->d_ptr, f->d_col, f->d_val, f->d_x, f->d_y, f->d_ws,
+                                      f->ws_bytes);
         return spmv_csr_run(f->d, f->d_ptr, f->d_col, f->d_val, f->d_x, f->d_y, f->lanes);
     case FMT_ELL:
         return spmv_ell_run(f->d, f->K, f->ld, f->ki, f->d_col, f->d_val, f->d_x, f->d_y);

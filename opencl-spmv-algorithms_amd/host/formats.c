@@ -101,6 +101,14 @@ int spmv_csr_row_stats(int64_t n_rows, const int64_t *row_ptr,
     return SPMV_SUCCESS;
 }
 
+int spmv_csr_pick_variant(int64_t n_rows, const int64_t *row_ptr)
+{
+    int64_t mx = 0;
+    double mean = 0.0;
+    spmv_csr_row_stats(n_rows, row_ptr, NULL, &mx, &mean);
+    return (mx > 4096 && (double)mx > 64.0 * mean) ? 4 : 0;
+}
+
 /* ------------------------------------------------------------------ ELL */
 
 int spmv_ell_plan(int64_t n_rows, const int64_t *row_ptr, int32_t ki,

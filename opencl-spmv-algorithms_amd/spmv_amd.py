@@ -79,6 +79,8 @@ HIP_SYMBOLS = {
     "spmv_csr_auto_lanes": (ctypes.c_int, [_c_i64, _c_i64]),
     "spmv_csr_run": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, ctypes.c_int]),
     "spmv_csr_run_variant": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, ctypes.c_int, ctypes.c_int]),
+    "spmv_csr_tiled_ws_bytes": (ctypes.c_size_t, [_c_i64, _c_i64]),
+    "spmv_csr_run_tiled": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t]),
     "spmv_ell_run": (ctypes.c_int, [Dims, _c_i32, _c_i64, _c_i32, _vp, _vp, _vp, _vp]),
     "spmv_sell_run": (ctypes.c_int, [Dims, _c_i32, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "spmv_cmrs_run": (ctypes.c_int, [Dims, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
@@ -113,6 +115,7 @@ HOST_SYMBOLS = {
     "spmv_coo_sort_by_row": (ctypes.c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "spmv_csr_from_coo": (ctypes.c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "spmv_csr_row_stats": (ctypes.c_int, [_c_i64, _vp, ctypes.POINTER(_c_i64), ctypes.POINTER(_c_i64), ctypes.POINTER(ctypes.c_double)]),
+    "spmv_csr_pick_variant": (ctypes.c_int, [_c_i64, _vp]),
     "spmv_ell_plan": (ctypes.c_int, [_c_i64, _vp, _c_i32, ctypes.POINTER(_c_i32), ctypes.POINTER(_c_i64)]),
     "spmv_ell_fill": (ctypes.c_int, [_c_i64, _vp, _vp, _vp, _c_i32, _c_i64, _c_i32, _vp, _vp]),
     "spmv_sell_plan": (ctypes.c_int, [_c_i64, _vp, _c_i32, _c_i32, _c_i32, ctypes.POINTER(_c_i64), ctypes.POINTER(_c_i64)]),
@@ -422,8 +425,12 @@ class DeviceMatrix:
             rc = lib.spmv_coo_run(d, _ptr(a["row"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
                                   _ptr(a["ws"]), a["ws"].numel())
         elif self.fmt == "csr":
-            rc = lib.spmv_csr_run_variant(d, _ptr(a["row_ptr"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x),
-                                          _ptr(y), p["lanes"], p.get("variant", 0))
+            if p.get("variant", 0) == 4:
+                rc = lib.spmv_csr_run_tiled(d, _ptr(a["row_ptr"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x),
+                                            _ptr(y), _ptr(a["ws"]), a["ws"].numel())
+            else:
+                rc = lib.spmv_csr_run_variant(d, _ptr(a["row_ptr"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x),
+                                              _ptr(y), p["lanes"], p.get("variant", 0))
         elif self.fmt == "ell":
             rc = lib.spmv_ell_run(d, p["K"], p["ld"], p["ki"], _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y))
         elif self.fmt == "sell":
@@ -453,9 +460,14 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
         return dm
     ptr, col, val = csr_from_coo(m)
     if fmt == "csr":
+        if variant == 0:  # host-side choice from the row-length skew
+            variant = host_lib().spmv_csr_pick_variant(m.n_rows, _ptr(ptr))
         dm.params = dict(lanes=lanes, variant=variant)  # 0 = library picks
         dm.arrays = dict(row_ptr=_dev_tensor(ptr, device), col=_dev_tensor(col, device),
                          val=_dev_tensor(val, device))
+        if variant == 4:
+            ws = hip_lib().spmv_csr_tiled_ws_bytes(m.n_rows, m.nnz)
+            dm.arrays["ws"] = torch.empty(ws, dtype=torch.uint8, device=device)
         dm.stored_bytes = 12 * m.nnz + 8 * (m.n_rows + 1)
     elif fmt == "ell":
         ki = ki or 2  # measured best for ELL (profiles/round1_sweep.md)

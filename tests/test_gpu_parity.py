@@ -31,6 +31,8 @@ FMT_PARAMS = [
     ("csr", {"variant": 2}),
     ("csr", {"lanes": 2, "variant": 2}),
     ("csr", {"lanes": 64, "variant": 2}),
+    ("csr", {"variant": 3}),
+    ("csr", {"variant": 4}),
     ("ell", {"ki": 1}),
     ("ell", {"ki": 2}),
     ("sell", {"C": 64, "sigma": 1024, "ki": 2}),
@@ -103,8 +105,8 @@ def test_cantlike_batch_random_x(torch_dev, fmt):
     assert_parity(m, y, x)
 
 
-@pytest.mark.parametrize("fmt,kw", [("coo", {}), ("csr", {}), ("csr", {"variant": 2}), ("sell", {}),
-                                    ("cmrs", {})])
+@pytest.mark.parametrize("fmt,kw", [("coo", {}), ("csr", {}), ("csr", {"variant": 2}), ("csr", {"variant": 4}),
+                                    ("sell", {}), ("cmrs", {})])
 def test_rmat_skewed(torch_dev, fmt, kw):
     """R-MAT 1e6 rows / 1e7 entries: empty rows, rows of thousands of entries."""
     torch, dev = torch_dev
@@ -130,13 +132,13 @@ def test_ragged_long_rows(torch_dev, fmt, kw):
     assert_parity(m, y, x)
 
 
-@pytest.mark.parametrize("fmt", sa.FORMATS)
-def test_bitwise_reproducible(torch_dev, fmt):
+@pytest.mark.parametrize("fmt,kw", [(f, {}) for f in sa.FORMATS] + [("csr", {"variant": 4})])
+def test_bitwise_reproducible(torch_dev, fmt, kw):
     """No atomics anywhere: two launches give identical bits (the reference
     COO's CAS-atomic order is nondeterministic)."""
     torch, dev = torch_dev
     m = sa.gen_random(30_000, 30_000, 0, 300, seed=5)
-    dm = sa.to_device(m, fmt, dev)
+    dm = sa.to_device(m, fmt, dev, **kw)
     x = torch.from_numpy(np.random.default_rng(2).uniform(-1, 1, m.n_cols)).to(dev)
     y1 = torch.empty(m.n_rows, dtype=torch.float64, device=dev)
     y2 = torch.full_like(y1, float("nan"))

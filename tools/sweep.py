@@ -25,6 +25,7 @@ VARIANTS = [
     ("csr", {"lanes": 8, "variant": 1}), ("csr", {"lanes": 16, "variant": 1}),
     ("csr", {"lanes": 2, "variant": 2}), ("csr", {"lanes": 4, "variant": 2}), ("csr", {"lanes": 8, "variant": 2}),
     ("csr", {"lanes": 2, "variant": 3}), ("csr", {"lanes": 4, "variant": 3}), ("csr", {"lanes": 8, "variant": 3}),
+    ("csr", {"variant": 4}),
     ("ell", {"ki": 1}), ("ell", {"ki": 2}),
     ("sell", {"C": 64, "sigma": 1, "ki": 2}), ("sell", {"C": 64, "sigma": 256, "ki": 2}),
     ("sell", {"C": 64, "sigma": 1024, "ki": 2}), ("sell", {"C": 64, "sigma": 1024, "ki": 1}),

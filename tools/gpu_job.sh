@@ -38,6 +38,9 @@ for s in "${steps[@]}"; do
     sweepcoo) run sweep_coo 300 python tools/sweep.py --rounds 2 --only coo,cmrs;;
     sweepcoo1) SPMV_COO_VARIANT=1 SPMV_CMRS_VARIANT=1 run sweep_coo1 300 python tools/sweep.py --rounds 2 --only coo,cmrs;;
     sweeprmat2) run sweep_rmat 900 python tools/sweep.py --matrix rmat --rounds 1 --reps 20;;
+    benchrmat) run bench_rmat 600 python bench.py --workload rmat --steps 20;;
+    benchbanded) run bench_banded_sell 600 python bench.py --workload banded --format sell --steps 20 && run bench_banded_csr 600 python bench.py --workload banded --format csr --steps 20;;
+    rehearse2) run rehearse2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --backend gloo --share-gpu --steps 20;;
     drivers) run drivers 600 python -m pytest tests/test_drivers_gpu.py -q;;
     sweepremap) SPMV_XCD_REMAP=1 run sweep_remap 600 python tools/sweep.py --rounds 2 --only csr,sell,ell;;
     sweeprmat) run sweep_rmat 600 python tools/sweep.py --matrix rmat --rounds 2 --reps 20;;

@@ -80,11 +80,15 @@ def parse():
     return p.parse_args()
 
 
-def kernel_name(args):
+def kernel_name(args, dm=None):
     """The dominant kernel as rocprofv3 names it (for profiles/)."""
     if args.format == "csr":
-        v = args.variant or int(os.environ.get("SPMV_CSR_VARIANT", "0") or 0) or CSR_DEFAULT_VARIANT
-        return {2: "csr_staged_kernel", 3: "csr_staged_persistent_kernel"}.get(v, "csr_vector_kernel")
+        v = (getattr(dm, "params", {}) or {}).get("variant", 0) or args.variant
+        v = v or int(os.environ.get("SPMV_CSR_VARIANT", "0") or 0) or CSR_DEFAULT_VARIANT
+        return {2: "csr_staged_kernel", 3: "csr_staged_persistent_kernel",
+                4: "csr_tiled_kernel"}.get(v, "csr_vector_kernel")
+    if args.format in ("coo", "cmrs") and os.environ.get(f"SPMV_{args.format.upper()}_VARIANT", "2") != "1":
+        return f"{args.format}_staged_kernel"
     return KERNEL_NAMES[args.format]
 
 
@@ -356,7 +360,7 @@ def main():
     traffic = traffic_for(args.format, bytes_step)
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": sa.HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / sa.HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": kernel_name(args), "kernel_ms": round(kern_ms, 5),
+                "kernel": kernel_name(args, dm), "kernel_ms": round(kern_ms, 5),
                 "bytes_alg_per_launch": bytes_step}
 
     per_format = None

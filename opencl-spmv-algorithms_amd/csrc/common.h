@@ -65,6 +65,40 @@ __device__ __forceinline__ int64_t xcd_block(int remap)
     return xcd < r ? xcd * (q + 1) + idx : r * (q + 1) + (xcd - r) * q + idx;
 }
 
+// Streamed-once loads of the matrix arrays.  NT = true issues them
+// non-temporal (`global_load … nt`), so the values and columns, each read
+// exactly once, do not displace x from L2 / the Infinity Cache.
+typedef double v2f64 __attribute__((ext_vector_type(2)));
+typedef int32_t v2i32 __attribute__((ext_vector_type(2)));
+
+template <bool NT, typename T>
+__device__ __forceinline__ T stream_load(const T *p)
+{
+    if constexpr (NT)
+        return __builtin_nontemporal_load(p);
+    else
+        return *p;
+}
+
+template <bool NT>
+__device__ __forceinline__ double2 stream_load2(const double *p)
+{
+    const v2f64 v = stream_load<NT>(reinterpret_cast<const v2f64 *>(p));
+    return double2{v.x, v.y};
+}
+
+template <bool NT>
+__device__ __forceinline__ int2 stream_load2(const int32_t *p)
+{
+    const v2i32 v = stream_load<NT>(reinterpret_cast<const v2i32 *>(p));
+    return int2{v.x, v.y};
+}
+
+// Load-policy switch for the streamed arrays: SPMV_STREAM_NT=1 / 0 forces
+// it, otherwise `dflt` (each kernel's measured best).  Read on every call
+// so a sweep can flip it inside one process.
+bool stream_nt(bool dflt);
+
 template <int W>
 __device__ __forceinline__ double group_sum(double v)
 {

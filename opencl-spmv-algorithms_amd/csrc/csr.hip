@@ -103,11 +103,12 @@ __global__ __launch_bounds__(kBlock) void csr_vector_kernel(
 constexpr int kStageRoundsDefault = 4;  // pairs per lane per chunk: 2048 products, 16 KiB
 // (16 KiB keeps 8 workgroups = 32 waves per CU; 20 KiB (R = 5) capped the
 // CU at 7 and measured slower, R = 8 at 4 and much slower)
+constexpr bool kCsrStreamNtDefault = false;  // SPMV_STREAM_NT overrides
 
 // One row group (RPB = 256/L rows) of the staged scheme; s_ptr holds the
 // group's RPB+1 row offsets.  Ends with a barrier, so the caller may
 // overwrite s_ptr / s_prod afterwards.
-template <int L, int R>
+template <int L, int R, bool NT>
 __device__ __forceinline__ void staged_group(
     int64_t row, const int64_t *s_ptr, double2 *s_prod,
     const int32_t *__restrict__ col, const double *__restrict__ val,
@@ -132,12 +133,12 @@ __device__ __forceinline__ void staged_group(
             const int64_t p = cb + 2 * (int64_t)t;
             double2 pr = {0.0, 0.0};
             if (p + 1 < ce) {
-                const double2 v = *reinterpret_cast<const double2 *>(val + p);
-                const int2 c = *reinterpret_cast<const int2 *>(col + p);
+                const double2 v = stream_load2<NT>(val + p);
+                const int2 c = stream_load2<NT>(col + p);
                 pr.x = v.x * x[c.x];
                 pr.y = v.y * x[c.y];
             } else if (p < ce) {  // odd tail: never read past the range
-                pr.x = val[p] * x[col[p]];
+                pr.x = stream_load<NT>(val + p) * x[stream_load<NT>(col + p)];
             }
             s_prod[t] = pr;
         }
@@ -170,14 +171,14 @@ __global__ __launch_bounds__(kBlock) void csr_staged_kernel(
         s_ptr[threadIdx.x] = row_ptr[r < n_rows ? r : n_rows];
     }
     __syncthreads();
-    staged_group<L, R>(row0 + threadIdx.x / L, s_ptr, s_prod, col, val, x, y, n_rows);
+    staged_group<L, R, false>(row0 + threadIdx.x / L, s_ptr, s_prod, col, val, x, y, n_rows);
 }
 
 // Variant 3: persistent workgroups (a few per CU) walk the row groups
 // grid-stride and PREFETCH the next group's row offsets into registers
 // while the current group streams, so a group no longer starts with a
 // dependent round trip for its offsets.
-template <int L, int R>
+template <int L, int R, bool NT>
 __global__ __launch_bounds__(kBlock) void csr_staged_persistent_kernel(
     int64_t n_rows, int64_t n_groups, const int64_t *__restrict__ row_ptr,
     const int32_t *__restrict__ col, const double *__restrict__ val,
@@ -201,7 +202,149 @@ __global__ __launch_bounds__(kBlock) void csr_staged_persistent_kernel(
             int64_t r = g2 * RPB + threadIdx.x;
             next = row_ptr[r < n_rows ? r : n_rows];
         }
-        staged_group<L, R>(grp * RPB + threadIdx.x / L, s_ptr, s_prod, col, val, x, y, n_rows);
+        staged_group<L, R, NT>(grp * RPB + threadIdx.x / L, s_ptr, s_prod, col, val, x, y, n_rows);
+    }
+}
+
+// One lane's share of a staged chunk held in registers: R value pairs,
+// R column pairs and how many entries of each pair are inside the chunk.
+template <int R, bool NT>
+struct ChunkRegs {
+    double2 v[R];
+    int2 c[R];
+    uint32_t live;  // bit 2k: entry 2k+... of pair k inside the chunk; bit 2k+1: its partner
+
+    __device__ __forceinline__ void issue(const int32_t *__restrict__ col,
+                                          const double *__restrict__ val, int64_t cb, int64_t ce)
+    {
+        // one 64-bit base, 32-bit per-pair offsets (a chunk is < 2^31 entries)
+        const int32_t left = (int32_t)(ce - cb);
+        const double *vb = val + cb;
+        const int32_t *cbp = col + cb;
+        live = 0;
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const int32_t q = 2 * (int32_t)(threadIdx.x + k * kBlock);
+            if (q + 1 < left) {
+                v[k] = stream_load2<NT>(vb + q);
+                c[k] = stream_load2<NT>(cbp + q);
+                live |= 3u << (2 * k);
+            } else if (q < left) {  // odd tail: never read past the range
+                v[k] = double2{stream_load<NT>(vb + q), 0.0};
+                c[k] = int2{stream_load<NT>(cbp + q), 0};
+                live |= 1u << (2 * k);
+            }
+        }
+    }
+
+    __device__ __forceinline__ void products(const double *__restrict__ x, double2 *s_prod) const
+    {
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            double2 pr = {0.0, 0.0};
+            if (live & (1u << (2 * k)))
+                pr.x = v[k].x * x[c[k].x];
+            if (live & (2u << (2 * k)))
+                pr.y = v[k].y * x[c[k].y];
+            s_prod[threadIdx.x + k * kBlock] = pr;
+        }
+    }
+};
+
+// Variant 5: the persistent staged scheme, software-pipelined.  The value
+// and column loads of the NEXT chunk (of this row group or of the block's
+// next group) are issued right after the barrier that publishes the
+// current chunk's products, so HBM keeps streaming while the L-lane
+// groups reduce from LDS; variant 3 issued them only after its second
+// barrier.  Row offsets are double-buffered in LDS and fetched two groups
+// ahead.  Same products, same per-row summation order as variants 2/3,
+// so the results are bit-identical to them.
+template <int L, int R, bool NT>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void csr_pipelined_kernel(
+    int64_t n_rows, int64_t n_groups, const int64_t *__restrict__ row_ptr,
+    const int32_t *__restrict__ col, const double *__restrict__ val,
+    const double *__restrict__ x, double *__restrict__ y)
+{
+    constexpr int RPB = kBlock / L;
+    constexpr int CH = 2 * kBlock * R;
+    __shared__ int64_t s_ptr[2][RPB + 1];
+    __shared__ double2 s_prod[kBlock * R];
+    const double *prod = reinterpret_cast<const double *>(s_prod);
+    const int g = threadIdx.x / L;
+    const int lane = threadIdx.x % L;
+    const int64_t grid = gridDim.x;
+    int64_t grp = blockIdx.x;
+    if (grp >= n_groups)
+        return;  // whole workgroup
+    auto offsets = [&](int64_t gg) {
+        const int64_t r = gg * RPB + threadIdx.x;
+        return row_ptr[r < n_rows ? r : n_rows];
+    };
+    int64_t next = 0;  // offsets of group grp + grid, two groups ahead of use
+    if (threadIdx.x <= RPB) {
+        s_ptr[0][threadIdx.x] = offsets(grp);
+        if (grp + grid < n_groups)
+            next = offsets(grp + grid);
+    }
+    __syncthreads();
+    int b = 0;
+    int64_t beg, end, blk_end;
+    auto start_group = [&]() {
+        // the other buffer was last read before the previous barrier
+        if (threadIdx.x <= RPB) {
+            s_ptr[1 - b][threadIdx.x] = next;
+            if (grp + 2 * grid < n_groups)
+                next = offsets(grp + 2 * grid);
+        }
+        beg = s_ptr[b][g];
+        end = s_ptr[b][g + 1];
+        blk_end = s_ptr[b][RPB];
+    };
+    start_group();
+    int64_t cb = s_ptr[b][0] & ~(int64_t)1;
+    int64_t ce = cb + CH < blk_end ? cb + CH : blk_end;
+    ChunkRegs<R, NT> regs;
+    regs.issue(col, val, cb, ce);
+    double acc = 0.0;
+    for (;;) {
+        regs.products(x, s_prod);
+        __syncthreads();  // products (and the next group's offsets) visible
+        const bool last = ce >= blk_end;
+        int64_t ngrp = grp, ncb = 0, nce = 0;
+        if (!last) {
+            ncb = ce;
+            nce = ncb + CH < blk_end ? ncb + CH : blk_end;
+        } else {
+            ngrp = grp + grid;
+            if (ngrp < n_groups) {
+                const int64_t nend = s_ptr[1 - b][RPB];
+                ncb = s_ptr[1 - b][0] & ~(int64_t)1;
+                nce = ncb + CH < nend ? ncb + CH : nend;
+            }
+        }
+        if (ngrp < n_groups)
+            regs.issue(col, val, ncb, nce);
+        const int64_t lo = beg > cb ? beg : cb;
+        const int64_t hi = end < ce ? end : ce;
+        for (int64_t j = lo + lane; j < hi; j += L)
+            acc += prod[j - cb];
+        if (last) {
+            acc = group_sum<L>(acc);
+            const int64_t row = grp * RPB + g;
+            if (lane == 0 && row < n_rows)
+                y[row] = acc;
+            acc = 0.0;
+        }
+        __syncthreads();  // s_prod free again
+        if (ngrp >= n_groups)
+            break;
+        if (last) {
+            grp = ngrp;
+            b = 1 - b;
+            start_group();
+        }
+        cb = ncb;
+        ce = nce;
     }
 }
 
@@ -223,21 +366,18 @@ static int csr_default_variant()
     static int cached = -1;
     if (cached < 0) {
         const char *s = getenv("SPMV_CSR_VARIANT");
-        cached = (s && s[0] >= '1' && s[0] <= '3') ? s[0] - '0' : 3;
+        cached = (s && ((s[0] >= '1' && s[0] <= '3') || s[0] == '5')) ? s[0] - '0' : 3;
     }
     return cached;
 }
 
-// SPMV_CSR_STAGE_ROUNDS in {3,4,5,8}: chunk = 2*256*R products (tuning knob)
+// SPMV_CSR_STAGE_ROUNDS in {3,4,5,8}: chunk = 2*256*R products (tuning
+// knob, read per call so a sweep can change it inside one process)
 static int csr_stage_rounds()
 {
-    static int cached = -1;
-    if (cached < 0) {
-        const char *s = getenv("SPMV_CSR_STAGE_ROUNDS");
-        int r = s ? atoi(s) : kStageRoundsDefault;
-        cached = (r == 3 || r == 4 || r == 5 || r == 8) ? r : kStageRoundsDefault;
-    }
-    return cached;
+    const char *s = getenv("SPMV_CSR_STAGE_ROUNDS");
+    const int r = s ? atoi(s) : kStageRoundsDefault;
+    return (r == 3 || r == 4 || r == 5 || r == 8) ? r : kStageRoundsDefault;
 }
 
 static int cu_count()
@@ -249,26 +389,57 @@ static int cu_count()
     return n;
 }
 
+// Resident workgroups per CU for a persistent kernel, from the occupancy
+// calculator (VGPRs, LDS and the wave limit together), at most 8.  Sizing
+// the grid by hand once launched 8 per CU of a kernel that fit only 7,
+// and the 256 stragglers ran as a second wave.
+template <typename K>
+static int64_t persistent_grid(K kernel, int64_t groups)
+{
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, 0) != hipSuccess ||
+        per_cu <= 0)
+        per_cu = 1;
+    if (per_cu > 8)
+        per_cu = 8;
+    const int64_t grid = (int64_t)cu_count() * per_cu;
+    return grid < groups ? grid : groups;
+}
+
+template <int L, int R, bool NT>
+static void launch_persistent(const spmv_dims &d, const int64_t *row_ptr, const int32_t *col,
+                              const double *val, const double *x, double *y, int variant,
+                              int64_t groups)
+{
+    const hipStream_t st = (hipStream_t)d.stream;
+    if (variant == 5) {
+        static const int64_t per = persistent_grid(csr_pipelined_kernel<L, R, NT>, INT64_MAX);
+        const int64_t grid = per < groups ? per : groups;
+        hipLaunchKernelGGL((csr_pipelined_kernel<L, R, NT>), dim3((unsigned)grid), dim3(kBlock), 0, st,
+                           d.n_rows, groups, row_ptr, col, val, x, y);
+    } else {
+        static const int64_t per = persistent_grid(csr_staged_persistent_kernel<L, R, NT>, INT64_MAX);
+        const int64_t grid = per < groups ? per : groups;
+        hipLaunchKernelGGL((csr_staged_persistent_kernel<L, R, NT>), dim3((unsigned)grid), dim3(kBlock),
+                           0, st, d.n_rows, groups, row_ptr, col, val, x, y);
+    }
+}
+
 template <int L, int R>
 static void launch_staged(const spmv_dims &d, const int64_t *row_ptr, const int32_t *col,
                           const double *val, const double *x, double *y, int variant)
 {
     constexpr int RPB = kBlock / L;
     const int64_t groups = (d.n_rows + RPB - 1) / RPB;
-    const hipStream_t st = (hipStream_t)d.stream;
-    if (variant == 3) {
-        // LDS per workgroup = 16·256·R bytes: as many per CU as fit in
-        // 160 KiB, at most 8 (32 waves)
-        const int per_cu = (160 * 1024) / (16 * kBlock * R + 8 * (RPB + 1)) < 8
-                               ? (160 * 1024) / (16 * kBlock * R + 8 * (RPB + 1)) : 8;
-        int64_t grid = (int64_t)cu_count() * per_cu;
-        if (grid > groups)
-            grid = groups;
-        hipLaunchKernelGGL((csr_staged_persistent_kernel<L, R>), dim3((unsigned)grid), dim3(kBlock), 0,
-                           st, d.n_rows, groups, row_ptr, col, val, x, y);
+    if (variant == 3 || variant == 5) {
+        if (stream_nt(kCsrStreamNtDefault))
+            launch_persistent<L, R, true>(d, row_ptr, col, val, x, y, variant, groups);
+        else
+            launch_persistent<L, R, false>(d, row_ptr, col, val, x, y, variant, groups);
     } else {
-        hipLaunchKernelGGL((csr_staged_kernel<L, R>), dim3((unsigned)groups), dim3(kBlock), 0, st,
-                           d.n_rows, row_ptr, col, val, x, y, xcd_remap_enabled() ? 1 : 0);
+        hipLaunchKernelGGL((csr_staged_kernel<L, R>), dim3((unsigned)groups), dim3(kBlock), 0,
+                           (hipStream_t)d.stream, d.n_rows, row_ptr, col, val, x, y,
+                           xcd_remap_enabled() ? 1 : 0);
     }
 }
 
@@ -324,8 +495,8 @@ extern "C" int spmv_csr_run_variant(spmv_dims d, const int64_t *row_ptr,
 {
     if (d.n_rows < 0 || d.n_cols < 0 || d.nnz < 0)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_run: negative size");
-    if (variant < 0 || variant > 3)
-        return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_run: variant must be 0..3");
+    if (variant < 0 || variant > 5 || variant == 4)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_run: variant must be 0..3 or 5 (4 = spmv_csr_run_tiled)");
     if (d.n_rows == 0)
         return SPMV_SUCCESS;
     if ((d.n_rows + 1) / 2 > (int64_t)INT32_MAX * 64)

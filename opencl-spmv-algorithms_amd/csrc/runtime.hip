@@ -61,6 +61,14 @@ bool xcd_remap_enabled()
     return cached == 1;
 }
 
+bool stream_nt(bool dflt)
+{
+    const char *s = getenv("SPMV_STREAM_NT");
+    if (s && (s[0] == '0' || s[0] == '1'))
+        return s[0] == '1';
+    return dflt;
+}
+
 // One flush buffer per device, allocated on first use, freed by
 // spmv_release().
 static void *g_flush[64];

@@ -18,53 +18,74 @@
 
 namespace spmv {
 
-template <int KI>
+// Non-temporal matrix loads: SELL-64-1024 0.2955 vs 0.3130 ms and ELL
+// 0.3343 vs 0.3429 ms on the 32-copy cant-like batch, one process,
+// interleaved (profiles/round1/sweeps.md).  SPMV_STREAM_NT overrides.
+constexpr bool kSellStreamNtDefault = true;
+
+// slot groups in flight per lane: SPMV_SLOT_UNROLL = 4 (default) or 8
+static int slot_unroll()
+{
+    const char *s = getenv("SPMV_SLOT_UNROLL");
+    return (s && s[0] == '8') ? 8 : 4;
+}
+
+template <int KI, bool NT>
 struct Step;
 
-template <>
-struct Step<1> {
+template <bool NT>
+struct Step<1, NT> {
     static __device__ __forceinline__ double fma(const double *vp,
                                                  const int32_t *cp,
                                                  const double *__restrict__ x,
                                                  double acc)
     {
-        return acc + vp[0] * x[cp[0]];
+        return acc + stream_load<NT>(vp) * x[stream_load<NT>(cp)];
     }
 };
 
-template <>
-struct Step<2> {
+template <bool NT>
+struct Step<2, NT> {
     static __device__ __forceinline__ double fma(const double *vp,
                                                  const int32_t *cp,
                                                  const double *__restrict__ x,
                                                  double acc)
     {
-        const double2 v = *reinterpret_cast<const double2 *>(vp);
-        const int2 c = *reinterpret_cast<const int2 *>(cp);
+        const double2 v = stream_load2<NT>(vp);
+        const int2 c = stream_load2<NT>(cp);
         return acc + v.x * x[c.x] + v.y * x[c.y];
     }
 };
 
 // Slot-per-lane loop over `w` slots (a multiple of KI) with stride
-// `step` elements between consecutive KI-groups; 4 groups in flight.
-template <int KI>
+// `step` elements between consecutive KI-groups; U groups in flight
+// (U independent accumulators, combined as a pairwise tree).
+template <int KI, bool NT, int U>
 __device__ __forceinline__ double slot_dot(const double *__restrict__ vp,
                                            const int32_t *__restrict__ cp,
                                            int64_t w, int64_t step,
                                            const double *__restrict__ x)
 {
-    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    double a[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        a[u] = 0.0;
     const int64_t groups = w / KI;
     int64_t g = 0;
-    for (; g + 4 <= groups; g += 4) {
-        a0 = Step<KI>::fma(vp + (g + 0) * step, cp + (g + 0) * step, x, a0);
-        a1 = Step<KI>::fma(vp + (g + 1) * step, cp + (g + 1) * step, x, a1);
-        a2 = Step<KI>::fma(vp + (g + 2) * step, cp + (g + 2) * step, x, a2);
-        a3 = Step<KI>::fma(vp + (g + 3) * step, cp + (g + 3) * step, x, a3);
+    for (; g + U <= groups; g += U) {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            a[u] = Step<KI, NT>::fma(vp + (g + u) * step, cp + (g + u) * step, x, a[u]);
     }
     for (; g < groups; ++g)
-        a0 = Step<KI>::fma(vp + g * step, cp + g * step, x, a0);
-    return (a0 + a1) + (a2 + a3);
+        a[0] = Step<KI, NT>::fma(vp + g * step, cp + g * step, x, a[0]);
+#pragma unroll
+    for (int h = U / 2; h > 0; h /= 2) {
+#pragma unroll
+        for (int u = 0; u < h; ++u)
+            a[u] += a[u + h];
+    }
+    return a[0];
 }
 
 // One workgroup covers one sigma window (up to 1024 slots): every y[perm]
@@ -73,7 +94,7 @@ __device__ __forceinline__ double slot_dot(const double *__restrict__ vp,
 // 1024-row window was written from four XCDs and each partially written
 // line left the chip up to four times (WRITE_SIZE 2.9x the y bytes,
 // profiles/traffic.json), which cost ~10 % of the kernel.
-template <int KI>
+template <int KI, bool NT, int U>
 __global__ __launch_bounds__(1024) void sell_kernel(
     int32_t C, int64_t n_slices, const int64_t *__restrict__ slice_ptr,
     const int32_t *__restrict__ perm, const int32_t *__restrict__ col,
@@ -88,13 +109,13 @@ __global__ __launch_bounds__(1024) void sell_kernel(
     const int64_t base = slice_ptr[s];
     const int64_t w = (slice_ptr[s + 1] - base) / C;
     const int64_t off = base + r * KI;
-    const double sum = slot_dot<KI>(val + off, col + off, w, (int64_t)C * KI, x);
+    const double sum = slot_dot<KI, NT, U>(val + off, col + off, w, (int64_t)C * KI, x);
     const int32_t row = perm[slot];
     if (row >= 0)
         y[row] = sum;
 }
 
-template <int KI>
+template <int KI, bool NT, int U>
 __global__ __launch_bounds__(kBlock) void ell_kernel(
     int64_t n_rows, int32_t K, int64_t ld, const int32_t *__restrict__ col,
     const double *__restrict__ val, const double *__restrict__ x,
@@ -104,7 +125,7 @@ __global__ __launch_bounds__(kBlock) void ell_kernel(
     if (i >= n_rows)
         return;
     const int64_t off = i * KI;
-    y[i] = slot_dot<KI>(val + off, col + off, K, ld * KI, x);
+    y[i] = slot_dot<KI, NT, U>(val + off, col + off, K, ld * KI, x);
 }
 
 }  // namespace spmv
@@ -145,14 +166,14 @@ extern "C" int spmv_sell_run(spmv_dims d, int32_t C, int32_t sigma, int32_t ki,
     if (blocks > INT32_MAX)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_run: grid too large");
     const int remap = xcd_remap_enabled() ? 1 : 0;
-    if (ki == 2)
-        hipLaunchKernelGGL(sell_kernel<2>, dim3((unsigned)blocks), dim3(bt), 0,
-                           (hipStream_t)d.stream, C, n_slices, slice_ptr, perm,
-                           col, val, x, y, remap);
-    else
-        hipLaunchKernelGGL(sell_kernel<1>, dim3((unsigned)blocks), dim3(bt), 0,
-                           (hipStream_t)d.stream, C, n_slices, slice_ptr, perm,
-                           col, val, x, y, remap);
+    const bool nt = stream_nt(kSellStreamNtDefault);
+    const bool u8 = slot_unroll() == 8;
+    auto kern = ki == 2 ? (nt ? (u8 ? sell_kernel<2, true, 8> : sell_kernel<2, true, 4>)
+                              : (u8 ? sell_kernel<2, false, 8> : sell_kernel<2, false, 4>))
+                        : (nt ? (u8 ? sell_kernel<1, true, 8> : sell_kernel<1, true, 4>)
+                              : (u8 ? sell_kernel<1, false, 8> : sell_kernel<1, false, 4>));
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(bt), 0, (hipStream_t)d.stream, C,
+                       n_slices, slice_ptr, perm, col, val, x, y, remap);
     SPMV_CHECK_LAUNCH("sell_kernel");
     return SPMV_SUCCESS;
 }
@@ -170,14 +191,14 @@ extern "C" int spmv_ell_run(spmv_dims d, int32_t K, int64_t ld, int32_t ki,
     SPMV_GUARD(d);
     const int64_t blocks = (d.n_rows + kBlock - 1) / kBlock;
     const int remap = xcd_remap_enabled() ? 1 : 0;
-    if (ki == 2)
-        hipLaunchKernelGGL(ell_kernel<2>, dim3((unsigned)blocks), dim3(kBlock), 0,
-                           (hipStream_t)d.stream, d.n_rows, K, ld, col, val, x, y,
-                           remap);
-    else
-        hipLaunchKernelGGL(ell_kernel<1>, dim3((unsigned)blocks), dim3(kBlock), 0,
-                           (hipStream_t)d.stream, d.n_rows, K, ld, col, val, x, y,
-                           remap);
+    const bool nt = stream_nt(kSellStreamNtDefault);
+    const bool u8 = slot_unroll() == 8;
+    auto kern = ki == 2 ? (nt ? (u8 ? ell_kernel<2, true, 8> : ell_kernel<2, true, 4>)
+                              : (u8 ? ell_kernel<2, false, 8> : ell_kernel<2, false, 4>))
+                        : (nt ? (u8 ? ell_kernel<1, true, 8> : ell_kernel<1, true, 4>)
+                              : (u8 ? ell_kernel<1, false, 8> : ell_kernel<1, false, 4>));
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock), 0, (hipStream_t)d.stream,
+                       d.n_rows, K, ld, col, val, x, y, remap);
     SPMV_CHECK_LAUNCH("ell_kernel");
     return SPMV_SUCCESS;
 }

@@ -33,6 +33,9 @@ FMT_PARAMS = [
     ("csr", {"lanes": 64, "variant": 2}),
     ("csr", {"variant": 3}),
     ("csr", {"variant": 4}),
+    ("csr", {"variant": 5}),
+    ("csr", {"lanes": 2, "variant": 5}),
+    ("csr", {"lanes": 64, "variant": 5}),
     ("ell", {"ki": 1}),
     ("ell", {"ki": 2}),
     ("sell", {"C": 64, "sigma": 1024, "ki": 2}),
@@ -106,7 +109,7 @@ def test_cantlike_batch_random_x(torch_dev, fmt):
 
 
 @pytest.mark.parametrize("fmt,kw", [("coo", {}), ("csr", {}), ("csr", {"variant": 2}), ("csr", {"variant": 4}),
-                                    ("sell", {}), ("cmrs", {})])
+                                    ("csr", {"variant": 5}), ("sell", {}), ("cmrs", {})])
 def test_rmat_skewed(torch_dev, fmt, kw):
     """R-MAT 1e6 rows / 1e7 entries: empty rows, rows of thousands of entries."""
     torch, dev = torch_dev
@@ -124,7 +127,8 @@ def test_ell_refuses_rmat_padding(torch_dev):
 
 @pytest.mark.parametrize("fmt,kw", [("coo", {}), ("csr", {}), ("sell", {}), ("cmrs", {"h": 8}),
                                     ("cmrs", {"h": 32}), ("csr", {"lanes": 64}), ("csr", {"variant": 2}),
-                                    ("csr", {"lanes": 2, "variant": 2})])
+                                    ("csr", {"lanes": 2, "variant": 2}), ("csr", {"variant": 5}),
+                                    ("csr", {"lanes": 2, "variant": 5})])
 def test_ragged_long_rows(torch_dev, fmt, kw):
     torch, dev = torch_dev
     m = sa.gen_random(20_000, 50_000, 0, 2_000, seed=21)
@@ -132,7 +136,7 @@ def test_ragged_long_rows(torch_dev, fmt, kw):
     assert_parity(m, y, x)
 
 
-@pytest.mark.parametrize("fmt,kw", [(f, {}) for f in sa.FORMATS] + [("csr", {"variant": 4})])
+@pytest.mark.parametrize("fmt,kw", [(f, {}) for f in sa.FORMATS] + [("csr", {"variant": 4}), ("csr", {"variant": 5})])
 def test_bitwise_reproducible(torch_dev, fmt, kw):
     """No atomics anywhere: two launches give identical bits (the reference
     COO's CAS-atomic order is nondeterministic)."""
@@ -146,6 +150,43 @@ def test_bitwise_reproducible(torch_dev, fmt, kw):
     dm.run(x, y2)
     torch.cuda.synchronize()
     assert torch.equal(y1.view(torch.int64), y2.view(torch.int64))
+
+
+@pytest.mark.parametrize("lanes", [2, 4, 16])
+def test_csr_staged_variants_bit_identical(torch_dev, lanes):
+    """Variants 2, 3 and 5 form the same products and sum each row in the
+    same order, so their y agree bit for bit."""
+    torch, dev = torch_dev
+    m = sa.gen_random(40_000, 40_000, 0, 700, seed=9)
+    x = torch.from_numpy(np.random.default_rng(4).uniform(-1, 1, m.n_cols)).to(dev)
+    ys = []
+    for v in (2, 3, 5):
+        dm = sa.to_device(m, "csr", dev, lanes=lanes, variant=v)
+        y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
+        dm.run(x, y)
+        ys.append(y)
+    torch.cuda.synchronize()
+    assert torch.equal(ys[0].view(torch.int64), ys[1].view(torch.int64))
+    assert torch.equal(ys[0].view(torch.int64), ys[2].view(torch.int64))
+
+
+@pytest.mark.parametrize("fmt,kw", [("csr", {"variant": 3}), ("csr", {"variant": 5}), ("csr", {"variant": 2}),
+                                    ("sell", {"ki": 1}), ("sell", {"ki": 2}), ("ell", {"ki": 1}), ("ell", {"ki": 2})])
+def test_stream_load_policy_same_bits(torch_dev, monkeypatch, fmt, kw):
+    """SPMV_STREAM_NT only changes the cache policy of the matrix loads."""
+    torch, dev = torch_dev
+    m = sa.gen_cantlike(0, copies=2)
+    x = torch.from_numpy(np.random.default_rng(3).uniform(-1, 1, m.n_cols)).to(dev)
+    dm = sa.to_device(m, fmt, dev, **kw)
+    out = []
+    for nt in ("0", "1"):
+        monkeypatch.setenv("SPMV_STREAM_NT", nt)
+        y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
+        dm.run(x, y)
+        torch.cuda.synchronize()
+        out.append(y)
+    assert torch.equal(out[0].view(torch.int64), out[1].view(torch.int64))
+    assert_parity(m, out[1].cpu().numpy(), x.cpu().numpy())
 
 
 @pytest.fixture(scope="module")

@@ -46,6 +46,33 @@ __global__ __launch_bounds__(256) void read_kernel(const T *__restrict__ a, size
     out[(size_t)blockIdx.x * 256 + threadIdx.x] = s;
 }
 
+// One-shot grid, each workgroup reads U·4 KiB contiguous (the SpMV
+// kernels' shape: no grid stride, every block streams its own tile).
+// NT = non-temporal loads.  The store never happens; it keeps the loads.
+template <bool NT, int U>
+__global__ __launch_bounds__(256) void tile_read_kernel(const double2 *__restrict__ a, size_t n,
+                                                        double *__restrict__ out)
+{
+    typedef double v2 __attribute__((ext_vector_type(2)));
+    const size_t base = (size_t)blockIdx.x * U * 256 + threadIdx.x;
+    double s = 0.0;
+    v2 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const size_t i = base + (size_t)u * 256;
+        const v2 *p = reinterpret_cast<const v2 *>(a + (i < n ? i : 0));
+        if constexpr (NT)
+            v[u] = __builtin_nontemporal_load(p);
+        else
+            v[u] = *p;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        s += v[u].x + v[u].y;
+    if (s == 123.456)
+        out[0] = s;
+}
+
 __global__ __launch_bounds__(256) void copy_kernel(const double2 *__restrict__ a,
                                                    double2 *__restrict__ b, size_t n)
 {
@@ -95,6 +122,29 @@ int main(int argc, char **argv)
     t = time_ms([&] { hipLaunchKernelGGL((read_kernel<double, 4>), dim3(grid), dim3(256), 0, 0,
                                          (const double *)a, n8, out); }, reps);
     printf("{\"probe\": \"read_dwordx2\", \"bytes\": %zu, \"ms\": %.4f, \"GBs\": %.1f}\n", bytes, t,
+           bytes / t * 1e-6);
+    const unsigned g4 = (unsigned)((n16 + 4 * 256 - 1) / (4 * 256));
+    const unsigned g8 = (unsigned)((n16 + 8 * 256 - 1) / (8 * 256));
+    const unsigned g16 = (unsigned)((n16 + 16 * 256 - 1) / (16 * 256));
+    t = time_ms([&] { hipLaunchKernelGGL((tile_read_kernel<false, 4>), dim3(g4), dim3(256), 0, 0,
+                                         (const double2 *)a, n16, out); }, reps);
+    printf("{\"probe\": \"tile_read_dwordx4_u4\", \"bytes\": %zu, \"ms\": %.4f, \"GBs\": %.1f}\n", bytes, t,
+           bytes / t * 1e-6);
+    t = time_ms([&] { hipLaunchKernelGGL((tile_read_kernel<false, 8>), dim3(g8), dim3(256), 0, 0,
+                                         (const double2 *)a, n16, out); }, reps);
+    printf("{\"probe\": \"tile_read_dwordx4_u8\", \"bytes\": %zu, \"ms\": %.4f, \"GBs\": %.1f}\n", bytes, t,
+           bytes / t * 1e-6);
+    t = time_ms([&] { hipLaunchKernelGGL((tile_read_kernel<false, 16>), dim3(g16), dim3(256), 0, 0,
+                                         (const double2 *)a, n16, out); }, reps);
+    printf("{\"probe\": \"tile_read_dwordx4_u16\", \"bytes\": %zu, \"ms\": %.4f, \"GBs\": %.1f}\n", bytes, t,
+           bytes / t * 1e-6);
+    t = time_ms([&] { hipLaunchKernelGGL((tile_read_kernel<true, 8>), dim3(g8), dim3(256), 0, 0,
+                                         (const double2 *)a, n16, out); }, reps);
+    printf("{\"probe\": \"tile_read_dwordx4_u8_nt\", \"bytes\": %zu, \"ms\": %.4f, \"GBs\": %.1f}\n", bytes, t,
+           bytes / t * 1e-6);
+    t = time_ms([&] { hipLaunchKernelGGL((tile_read_kernel<true, 16>), dim3(g16), dim3(256), 0, 0,
+                                         (const double2 *)a, n16, out); }, reps);
+    printf("{\"probe\": \"tile_read_dwordx4_u16_nt\", \"bytes\": %zu, \"ms\": %.4f, \"GBs\": %.1f}\n", bytes, t,
            bytes / t * 1e-6);
     t = time_ms([&] { hipLaunchKernelGGL(copy_kernel, dim3(grid), dim3(256), 0, 0,
                                          (const double2 *)a, (double2 *)b, n16); }, reps);

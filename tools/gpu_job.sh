@@ -50,6 +50,9 @@ for s in "${steps[@]}"; do
     sweepnopair) SPMV_CSR_PAIR=0 run sweep_nopair 300 python tools/sweep.py --only csr --rounds 2;;
     pmc) run pmc 1100 python tools/pmc_traffic.py;;
     pmcvar) run pmc_var 1100 python tools/pmc_traffic.py --out traffic_variants.json --formats "csr,csr@SPMV_XCD_REMAP=1,csr:lanes=16,sell:sigma=256,sell,ell@SPMV_XCD_REMAP=1";;
+    sweepnt) run sweep_nt 600 python tools/sweep.py --env-only --rounds 3;;
+    pmcnt) run pmc_nt 1100 python tools/pmc_traffic.py --out traffic_nt.json --formats "csr@SPMV_STREAM_NT=1,sell@SPMV_STREAM_NT=1,ell@SPMV_STREAM_NT=1,coo,cmrs";;
+    stalls) run pmc_stalls 1150 python tools/pmc_stalls.py --formats csr,sell;;
     *) echo "unknown step $s";;
   esac
 done

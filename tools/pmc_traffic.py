@@ -26,7 +26,14 @@ from pathlib import Path
 REPO = Path(__file__).resolve().parents[1]
 OUT = REPO / "gpurun_out" / "pmc"
 KERNELS = {"csr": "csr_", "sell": "sell_kernel", "ell": "ell_kernel",
-           "coo": "coo_tile_kernel", "cmrs": "cmrs_kernel"}
+           "coo": "coo_staged_kernel", "cmrs": "cmrs_staged_kernel"}
+
+
+def kernel_for(fmt, env):
+    """The dominant kernel's name (substring) for `fmt` under `env`."""
+    if fmt in ("coo", "cmrs") and env.get(f"SPMV_{fmt.upper()}_VARIANT") == "1":
+        return {"coo": "coo_tile_kernel", "cmrs": "cmrs_kernel"}[fmt]
+    return KERNELS[fmt]
 PASSES = {
     "fetch": ["FETCH_SIZE"],
     "write": ["WRITE_SIZE"],
@@ -106,13 +113,8 @@ def main():
 
     for spec in a.formats.split(","):
         # spec: fmt[:key=val;key=val][@ENV=val]  e.g. sell:sigma=256  csr@SPMV_XCD_REMAP=1
-        env_kv = {}
-        if "@" in spec:
-            spec_main, env_s = spec.split("@", 1)
-            k, v = env_s.split("=", 1)
-            env_kv[k] = v
-        else:
-            spec_main = spec
+        spec_main, *env_parts = spec.split("@")
+        env_kv = dict(e.split("=", 1) for e in env_parts)
         fmt, _, params = spec_main.partition(":")
         cmd = ["python3", "bench.py", "--profile", "--format", fmt, "--steps", str(a.steps), "--warmup", "2",
                "--copies", str(a.copies)]
@@ -125,7 +127,7 @@ def main():
         for tag, cs in PASSES.items():
             f = run_pass(f"{tag0}_{tag}", cs, cmd)
             if f:
-                c, n = mean_per_dispatch(f, KERNELS[fmt])
+                c, n = mean_per_dispatch(f, kernel_for(fmt, env_kv))
                 counters.update(c)
         if not counters:
             continue
@@ -145,7 +147,7 @@ def main():
         hits, miss = counters.get("TCC_HIT_sum", 0.0), counters.get("TCC_MISS_sum", 0.0)
         for k in env_kv:
             os.environ.pop(k, None)
-        result[spec] = {"kernel": KERNELS[fmt], "bytes_alg": b_alg, "dispatches": n, "cmd": " ".join(cmd[1:]),
+        result[spec] = {"kernel": kernel_for(fmt, env_kv), "bytes_alg": b_alg, "dispatches": n, "cmd": " ".join(cmd[1:]),
                         "env": env_kv or None,
                        "hbm_read_bytes_per_launch": round(read), "hbm_write_bytes_per_launch": round(write),
                        "hbm_bytes_per_launch": round(read + write),

@@ -33,6 +33,19 @@ VARIANTS = [
     ("sell", {"C": 64, "sigma": 512, "ki": 2}),
     ("cmrs", {"h": 8}), ("cmrs", {"h": 16}), ("cmrs", {"h": 32}),
     ("coo", {}),
+    # load policy of the streamed arrays (SPMV_STREAM_NT), groups in flight (SPMV_SLOT_UNROLL)
+    ("csr", {"lanes": 4, "variant": 3, "env": {"SPMV_STREAM_NT": "0"}}),
+    ("csr", {"lanes": 4, "variant": 3, "env": {"SPMV_STREAM_NT": "1"}}),
+    ("csr", {"lanes": 4, "variant": 5, "env": {"SPMV_STREAM_NT": "1"}}),
+    ("sell", {"C": 64, "sigma": 1024, "ki": 1, "env": {"SPMV_STREAM_NT": "0"}}),
+    ("sell", {"C": 64, "sigma": 1024, "ki": 1, "env": {"SPMV_STREAM_NT": "1"}}),
+    ("sell", {"C": 64, "sigma": 1024, "ki": 1, "env": {"SPMV_STREAM_NT": "1", "SPMV_SLOT_UNROLL": "8"}}),
+    ("sell", {"C": 64, "sigma": 1024, "ki": 2, "env": {"SPMV_STREAM_NT": "1"}}),
+    ("sell", {"C": 64, "sigma": 1024, "ki": 2, "env": {"SPMV_STREAM_NT": "1", "SPMV_SLOT_UNROLL": "8"}}),
+    ("ell", {"ki": 2, "env": {"SPMV_STREAM_NT": "0"}}),
+    ("ell", {"ki": 2, "env": {"SPMV_STREAM_NT": "1"}}),
+    ("ell", {"ki": 2, "env": {"SPMV_STREAM_NT": "1", "SPMV_SLOT_UNROLL": "8"}}),
+    ("ell", {"ki": 1, "env": {"SPMV_STREAM_NT": "1", "SPMV_SLOT_UNROLL": "8"}}),
 ]
 
 
@@ -42,7 +55,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--matrix", default="cantlike")
-    ap.add_argument("--only", default="")
+    ap.add_argument("--only", default="", help="comma list of formats")
+    ap.add_argument("--env-only", action="store_true", help="only the variants that set env knobs")
     a = ap.parse_args()
     import torch
 
@@ -52,12 +66,18 @@ def main():
     x = torch.from_numpy(sa.ramp_x(m.n_cols)).to(dev)
     y = torch.empty(m.n_rows, dtype=torch.float64, device=dev)
     variants = [v for v in VARIANTS if not a.only or v[0] in a.only.split(",")]
+    if a.env_only:
+        variants = [v for v in variants if "env" in v[1]]
     if a.matrix != "cantlike":
         variants = [v for v in variants if v[0] != "ell"]
     res = {i: [] for i in range(len(variants))}
     stored = {}
     for r in range(a.rounds):
         for i, (fmt, kw) in enumerate(variants):
+            kw = dict(kw)
+            env = kw.pop("env", {})
+            saved = {k: os.environ.get(k) for k in env}
+            os.environ.update(env)
             dm = sa.to_device(m, fmt, dev, **kw)
             stored[i] = dm.stored_bytes
             s = torch.cuda.current_stream()
@@ -72,6 +92,11 @@ def main():
             res[i].append(float(np.mean([ev[k].elapsed_time(ev[k + 1]) for k in range(a.reps)])))
             del dm
             torch.cuda.empty_cache()
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
     out = []
     for i, (fmt, kw) in enumerate(variants):
         ms = float(np.median(res[i]))

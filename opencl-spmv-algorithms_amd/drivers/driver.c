@@ -27,7 +27,10 @@
  * Options: --matrix PATH  --gen cantlike[0|1|2]|rmat|banded|random
  *          --copies B  --reps N  --warmup W  --warm  --device D
  *          --C C --sigma S --ki K --h H --lanes L  --threads T
- *          --cpu / --no-cpu  --strict  --write-mtx PATH  --help
+ *          --cpu / --no-cpu  --strict  --write-mtx PATH  --cache  --help
+ *   --cache keeps a binary copy of the parsed file at PATH.bin (SURVEY.md
+ *   §8f row 1) and reads it instead of the text whenever it is at least as
+ *   new as PATH; the entries, their order and the result are unchanged.
  */
 #define _POSIX_C_SOURCE 200809L
 #include <errno.h>
@@ -35,6 +38,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/stat.h>
 #include <time.h>
 
 #include "driver.h"
@@ -48,7 +52,7 @@ typedef struct {
     const char *gen;
     const char *write_mtx;
     int64_t copies;
-    int reps, warmup, warm, device, C, sigma, ki, h, lanes, threads, cpu, strict;
+    int reps, warmup, warm, device, C, sigma, ki, h, lanes, threads, cpu, strict, cache;
 } opts_t;
 
 static void usage(const char *prog)
@@ -56,7 +60,7 @@ static void usage(const char *prog)
     printf("usage: %s [--matrix PATH | --gen cantlike[0|1|2]|rmat|banded|random]\n"
            "          [--copies B] [--reps N] [--warmup W] [--warm] [--device D]\n"
            "          [--C C] [--sigma S] [--ki 1|2] [--h H] [--lanes L]\n"
-           "          [--threads T] [--cpu|--no-cpu] [--strict] [--write-mtx PATH]\n",
+           "          [--threads T] [--cpu|--no-cpu] [--strict] [--write-mtx PATH] [--cache]\n",
            prog);
 }
 
@@ -100,6 +104,7 @@ static int parse_opts(int argc, char **argv, spmv_format fmt, opts_t *o)
         else if (!strcmp(a, "--cpu")) o->cpu = 1;
         else if (!strcmp(a, "--no-cpu")) o->cpu = 0;
         else if (!strcmp(a, "--strict")) o->strict = 1;
+        else if (!strcmp(a, "--cache")) o->cache = 1;
         else if (!strcmp(a, "--help") || !strcmp(a, "-h")) { usage(argv[0]); exit(0); }
         else {
             fprintf(stderr, "unknown option %s\n", a);
@@ -123,9 +128,49 @@ typedef struct {
     const char *label;
 } coo_t;
 
+/* PATH.bin when --cache is on and it is at least as new as PATH */
+static int cache_fresh(const char *mtx, const char *bin)
+{
+    struct stat sm, sb;
+    return stat(mtx, &sm) == 0 && stat(bin, &sb) == 0 && sb.st_mtime >= sm.st_mtime;
+}
+
+static int load_cached(const opts_t *o, const char *bin, coo_t *m)
+{
+    spmv_mtx_info info;
+    if (spmv_bin_read_info(bin, &info) != SPMV_SUCCESS)
+        return SPMV_FILE_ERROR;
+    m->n_rows = info.n_rows;
+    m->n_cols = info.n_cols;
+    m->nnz = info.nnz;
+    m->row = malloc((size_t)(m->nnz + 1) * sizeof(int32_t));
+    m->col = malloc((size_t)(m->nnz + 1) * sizeof(int32_t));
+    m->val = malloc((size_t)(m->nnz + 1) * sizeof(double));
+    if (!m->row || !m->col || !m->val)
+        return SPMV_OTHER_ERROR;
+    if (spmv_bin_read(bin, &info, m->row, m->col, m->val) != SPMV_SUCCESS)
+        return SPMV_FILE_ERROR;
+    m->label = o->matrix;
+    return SPMV_SUCCESS;
+}
+
 static int load_input(const opts_t *o, spmv_format fmt, coo_t *m)
 {
     memset(m, 0, sizeof *m);
+    char bin[4096] = "";
+    if (!o->gen && o->cache) {
+        snprintf(bin, sizeof bin, "%s.bin", o->matrix);
+        if (cache_fresh(o->matrix, bin)) {
+            if (load_cached(o, bin, m) == SPMV_SUCCESS) {
+                printf("  [cache] read %s\n", bin);
+                return SPMV_SUCCESS;
+            }
+            free(m->row);
+            free(m->col);
+            free(m->val);
+            memset(m, 0, sizeof *m);
+        }
+    }
     if (!o->gen) {
         spmv_mtx_info info;
         int rc = spmv_mtx_read_info(o->matrix, &info);
@@ -149,6 +194,12 @@ static int load_input(const opts_t *o, spmv_format fmt, coo_t *m)
             return SPMV_FILE_ERROR;
         }
         m->label = o->matrix;
+        if (bin[0]) {
+            if (spmv_bin_write(bin, &info, m->row, m->col, m->val) == SPMV_SUCCESS)
+                printf("  [cache] wrote %s\n", bin);
+            else
+                printf("  [cache] could not write %s (continuing)\n", bin);
+        }
         return SPMV_SUCCESS;
     }
     int rc = SPMV_OTHER_ERROR;

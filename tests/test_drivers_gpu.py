@@ -76,3 +76,24 @@ def test_generated_cantlike_and_roundtrip(tmp_path):
 def test_bad_option_exit_code():
     r = run("csr", "--no-such-option")
     assert r.returncode == 4
+
+
+@pytest.mark.parametrize("prog", ["csr", "sigma_c"])
+def test_binary_cache(tmp_path, prog):
+    """--cache writes PATH.bin on the first run and reads it on the next;
+    the verdict is the same, and a newer text file invalidates it."""
+    src = tmp_path / "m.mtx"
+    shutil.copy(GOLDEN / "ragged_shuffled.mtx", src)
+    args = ("--matrix", str(src), "--reps", "2", "--warmup", "0", "--strict", "--cache")
+    r1 = run(prog, *args)
+    assert r1.returncode == 0, r1.stdout + r1.stderr
+    assert "[cache] wrote" in r1.stdout and (tmp_path / "m.mtx.bin").exists()
+    r2 = run(prog, *args)
+    assert r2.returncode == 0, r2.stdout + r2.stderr
+    assert "[cache] read" in r2.stdout and "\nresult is ok\n" in "\n" + r2.stdout
+    # a newer text file is parsed again
+    import os
+    st = (tmp_path / "m.mtx.bin").stat()
+    os.utime(src, (st.st_atime + 10, st.st_mtime + 10))
+    r3 = run(prog, *args)
+    assert "[cache] wrote" in r3.stdout, r3.stdout

@@ -20,7 +20,9 @@ sys.path.insert(0, str(REPO / "tools"))
 from pmc_traffic import kernel_for, mean_per_dispatch, run_pass  # noqa: E402
 
 PASSES = {
-    "ta": ["TA_BUSY_avr", "TA_ADDR_STALLED_BY_TC_CYCLES_sum", "TA_DATA_STALLED_BY_TC_CYCLES_sum", "GRBM_GUI_ACTIVE"],
+    "ta": ["TA_BUSY_avr", "GRBM_GUI_ACTIVE"],
+    "ta2": ["TA_ADDR_STALLED_BY_TC_CYCLES_sum"],
+    "ta3": ["TA_DATA_STALLED_BY_TC_CYCLES_sum"],
     "tcp": ["TCP_PENDING_STALL_CYCLES_sum", "TCP_TCR_TCP_STALL_CYCLES_sum", "TCP_READ_TAGCONFLICT_STALL_CYCLES_sum",
             "TCP_TCC_READ_REQ_sum"],
     "td": ["TD_TD_BUSY_sum", "TD_TC_STALL_sum", "TD_SPI_STALL_sum", "TCP_TOTAL_CACHE_ACCESSES_sum"],
@@ -50,7 +52,7 @@ def main():
         counters = {}
         for tag, cs in PASSES.items():
             tagdir = f"stall_{name}_{tag}".replace(":", "_").replace("=", "").replace("@", "_")
-            f = run_pass(tagdir, cs, cmd)
+            f = run_pass(tagdir, cs, cmd, timeout=150)
             if f:
                 c, _ = mean_per_dispatch(f, kern)
                 counters.update(c)

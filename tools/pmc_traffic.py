@@ -43,19 +43,25 @@ PASSES = {
 CANT_N, CANT_Z = 62451, 4007383
 
 
-def run_pass(tag, counters, cmd):
+def run_pass(tag, counters, cmd, timeout=600):
     d = OUT / tag
     d.mkdir(parents=True, exist_ok=True)
     full = ["rocprofv3", "--pmc", *counters, "--output-format", "csv", "-d", str(d), "-o", "run", "--", *cmd]
     env = dict(os.environ, TMPDIR="/tmp")
-    r = subprocess.run(full, cwd=REPO, env=env, capture_output=True, text=True, timeout=600)
+    print(f"pass {tag}: {' '.join(counters)}", flush=True)
+    try:
+        r = subprocess.run(full, cwd=REPO, env=env, capture_output=True, text=True, timeout=timeout)
+    except subprocess.TimeoutExpired as e:
+        (d / "stdout.log").write_text(f"timed out after {timeout} s\n{e.stdout or ''}\n--- stderr ---\n{e.stderr or ''}")
+        print(f"pass {tag} timed out after {timeout} s", file=sys.stderr, flush=True)
+        return None
     (d / "stdout.log").write_text(r.stdout[-20000:] + "\n--- stderr ---\n" + r.stderr[-20000:])
     if r.returncode != 0:
-        print(f"pass {tag} failed rc={r.returncode}", file=sys.stderr)
+        print(f"pass {tag} failed rc={r.returncode}", file=sys.stderr, flush=True)
         return None
     files = list(d.rglob("*counter_collection.csv"))
     if not files:
-        print(f"pass {tag}: no counter_collection.csv", file=sys.stderr)
+        print(f"pass {tag}: no counter_collection.csv", file=sys.stderr, flush=True)
         return None
     return files[0]
 

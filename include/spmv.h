@@ -149,6 +149,26 @@ int spmv_gen_banded_device(int64_t n, uint64_t seed, int64_t row_begin,
                            int64_t *ptr, int32_t *perm, int32_t *col, double *val,
                            int device, void *stream);
 
+/* ------------------------------------------------- iterated SpMV -------
+ * Vector kernels for power iteration / CG over row shards (SURVEY.md §8f
+ * row 3).  The reference stops after one SpMV (reference csr.c:198-236),
+ * so nothing here replaces a reference call.  Scalars live in DEVICE
+ * memory (num, den, s, out) so an iteration needs no host round trip; the
+ * dot product is a fixed two-stage tree: same n and data, same bits.    */
+size_t spmv_dot_ws_bytes(int64_t n);
+/* *out = sum_i a[i]*b[i]; ws holds spmv_dot_ws_bytes(n) bytes.          */
+int spmv_dot(int64_t n, const double *a, const double *b, double *out, void *ws,
+             size_t ws_bytes, int device, void *stream);
+/* y += sign * (*num / *den) * x   (CG: x += a p, r -= a Ap)             */
+int spmv_axpy_ratio(int64_t n, const double *num, const double *den, double sign,
+                    const double *x, double *y, int device, void *stream);
+/* y = x + (*num / *den) * y       (CG: p = r + b p)                     */
+int spmv_xpay_ratio(int64_t n, const double *num, const double *den, const double *x,
+                    double *y, int device, void *stream);
+/* y = x / sqrt(*s)                (power iteration: normalise)          */
+int spmv_scale_rsqrt(int64_t n, const double *s, const double *x, double *y, int device,
+                     void *stream);
+
 /* ------------------------------------------------------------ helpers ---
  * Device discovery (replaces reference inc/helper_functions.h:76-129),
  * memory (replaces clCreateBuffer / clEnqueueWriteBuffer /

@@ -260,7 +260,7 @@ struct ChunkRegs {
 // ahead.  Same products, same per-row summation order as variants 2/3,
 // so the results are bit-identical to them.
 template <int L, int R, bool NT>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void csr_pipelined_kernel(
+__global__ __launch_bounds__(kBlock) void csr_pipelined_kernel(
     int64_t n_rows, int64_t n_groups, const int64_t *__restrict__ row_ptr,
     const int32_t *__restrict__ col, const double *__restrict__ val,
     const double *__restrict__ x, double *__restrict__ y)

@@ -25,7 +25,7 @@ __device__ __forceinline__ double block_sum(double v, double *s_warp)
     double t = 0.0;
     if (threadIdx.x < kWave) {
         const int nw = blockDim.x / kWave;
-        t = threadIdx.x < nw ? s_warp[threadIdx.x] : 0.0;
+        t = (int)threadIdx.x < nw ? s_warp[threadIdx.x] : 0.0;
         t = group_sum<kWave>(t);
     }
     return t;  // valid in thread 0
@@ -56,7 +56,7 @@ __global__ __launch_bounds__(1024) void dot_final_kernel(int g, const double *__
                                                          double *__restrict__ out)
 {
     __shared__ double s_warp[1024 / kWave];
-    const double v = threadIdx.x < g ? partial[threadIdx.x] : 0.0;
+    const double v = (int)threadIdx.x < g ? partial[threadIdx.x] : 0.0;
     const double t = block_sum(v, s_warp);
     if (threadIdx.x == 0)
         *out = t;

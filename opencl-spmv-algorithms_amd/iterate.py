@@ -1,0 +1,298 @@
+"""iterate.py — iterated SpMV over row shards: power iteration and CG.
+
+SURVEY.md §8f row 3: "Iterated SpMV (power iteration / CG) reusing the y
+all-gather as the next x".  The reference stops after one SpMV (reference
+csr.c:198-236: launch, read y back, check), so this module has no reference
+counterpart; it is the natural consumer of the row-sharded design of §8e.
+
+Layout.  Rank r owns rows [bounds[r], bounds[r+1]) (spmv_partition_rows,
+nnz-balanced).  The vector that multiplies A is kept in the GATHERED layout:
+`world` blocks of `pad` entries, block r = rank r's rows followed by zeros.
+The shard's column indices are renumbered into that layout once, at build
+time, so `all_gather_into_tensor` of each rank's padded block IS the next
+x — no reorder pass, and the y all-gather becomes the input
+of the next SpMV directly.
+
+Per iteration everything stays on the device: SpMV (libspmv_hip), the
+deterministic dot product, and the vector updates read their scalars
+(norms, CG's alpha = rr/pAp and beta = rr'/rr) from device memory; the
+scalars are all-reduced in place over RCCL (`torch.distributed`, backend
+nccl) and never visit the host except for CG's convergence test every
+`check_every` iterations.  With one rank the loop can be captured into a
+HIP graph (`graph=True`).
+
+The device work goes through a `kernels` object (HipKernels by default).
+Tests substitute a numpy double to exercise the multi-rank orchestration on
+CPU ranks (gloo); the product path only ever builds HipKernels.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+import spmv_amd as sa
+
+
+# ------------------------------------------------------------------ layout
+@dataclass
+class ShardLayout:
+    """Row ownership and the gathered vector layout for `world` ranks."""
+
+    bounds: np.ndarray  # int64[world + 1]
+    pad: int  # entries per rank in the gathered vector
+
+    @property
+    def world(self) -> int:
+        return len(self.bounds) - 1
+
+    def positions(self, idx: np.ndarray) -> np.ndarray:
+        """Gathered-layout position of global row/column indices."""
+        idx = np.asarray(idx, np.int64)
+        owner = np.searchsorted(self.bounds, idx, side="right") - 1
+        return (owner * self.pad + (idx - self.bounds[owner])).astype(np.int64)
+
+    def to_gathered(self, v: np.ndarray) -> np.ndarray:
+        out = np.zeros(self.world * self.pad, dtype=v.dtype)
+        out[self.positions(np.arange(len(v)))] = v
+        return out
+
+    def from_gathered(self, g: np.ndarray, n: int) -> np.ndarray:
+        return np.asarray(g)[self.positions(np.arange(n))]
+
+
+def layout_for(n_rows: int, row_counts: np.ndarray, world: int, align: int = 1024) -> ShardLayout:
+    """nnz-balanced row ranges (spmv_partition_rows) and a pad rounded up to
+    64 entries (one wave of x per block)."""
+    ptr = np.zeros(n_rows + 1, np.int64)
+    np.cumsum(row_counts, out=ptr[1:])
+    bounds = sa.partition_rows(n_rows, ptr, world, align)
+    pad = int(np.max(np.diff(bounds))) if world > 0 else 0
+    pad = max(64, (pad + 63) // 64 * 64)
+    return ShardLayout(bounds, pad)
+
+
+def local_shard(m: sa.Coo, layout: ShardLayout, rank: int) -> sa.Coo:
+    """Rank `rank`'s rows with columns renumbered into the gathered layout
+    (square matrices: x and y share the row partition)."""
+    if m.n_rows != m.n_cols:
+        raise sa.SpmvError(sa.OTHER_ERROR, "local_shard", "iterated SpMV needs a square matrix")
+    lo, hi = int(layout.bounds[rank]), int(layout.bounds[rank + 1])
+    loc = sa.shard(m, lo, hi)
+    col = layout.positions(loc.col)
+    if col.size and col.max() > np.iinfo(np.int32).max:
+        raise sa.SpmvError(sa.OTHER_ERROR, "local_shard", "gathered layout exceeds int32 columns")
+    return sa.Coo(hi - lo, layout.world * layout.pad, loc.row, col.astype(np.int32), loc.val, m.symmetric,
+                  f"{m.label} rank {rank}/{layout.world}")
+
+
+# ------------------------------------------------------------- collectives
+class Comm:
+    """In-place collectives over torch.distributed (nccl = RCCL on ROCm);
+    with one rank they are no-ops and the gathered vector aliases the local
+    block."""
+
+    def __init__(self, dist=None):
+        self.dist = dist if dist is not None and dist.is_available() and dist.is_initialized() else None
+        self.rank = self.dist.get_rank() if self.dist else 0
+        self.world = self.dist.get_world_size() if self.dist else 1
+
+    def allreduce(self, t) -> None:
+        if self.dist is not None and self.world > 1:
+            self.dist.all_reduce(t)
+
+    def allgather(self, out, inp) -> None:
+        if self.dist is not None and self.world > 1:
+            self.dist.all_gather_into_tensor(out, inp)
+        elif out.data_ptr() != inp.data_ptr():
+            out[: inp.numel()].copy_(inp)
+
+
+# ---------------------------------------------------------------- kernels
+class HipKernels:
+    """The device kernels of one iteration, all on one stream."""
+
+    def __init__(self, dm: sa.DeviceMatrix, stream=None):
+        torch = sa._torch()
+        self.dm = dm
+        self.dev = torch.device(dm.device)
+        self.lib = sa.hip_lib()
+        self.stream = stream
+
+    def _s(self):
+        torch = sa._torch()
+        st = self.stream if self.stream is not None else torch.cuda.current_stream(self.dev)
+        return st.cuda_stream
+
+    def spmv(self, x_full, y) -> None:
+        self.dm.run(x_full, y, self.stream)
+
+    def dot(self, n, a, b, out, ws) -> None:
+        sa._check(self.lib.spmv_dot(n, sa._ptr(a), sa._ptr(b), sa._ptr(out), sa._ptr(ws), ws.numel(),
+                                    self.dev.index or 0, self._s()), "spmv_dot")
+
+    def axpy_ratio(self, n, num, den, sign, x, y) -> None:
+        sa._check(self.lib.spmv_axpy_ratio(n, sa._ptr(num), sa._ptr(den), float(sign), sa._ptr(x), sa._ptr(y),
+                                           self.dev.index or 0, self._s()), "spmv_axpy_ratio")
+
+    def xpay_ratio(self, n, num, den, x, y) -> None:
+        sa._check(self.lib.spmv_xpay_ratio(n, sa._ptr(num), sa._ptr(den), sa._ptr(x), sa._ptr(y),
+                                           self.dev.index or 0, self._s()), "spmv_xpay_ratio")
+
+    def scale_rsqrt(self, n, s, x, y) -> None:
+        sa._check(self.lib.spmv_scale_rsqrt(n, sa._ptr(s), sa._ptr(x), sa._ptr(y), self.dev.index or 0,
+                                            self._s()), "spmv_scale_rsqrt")
+
+    def dot_ws(self, n):
+        torch = sa._torch()
+        nbytes = self.lib.spmv_dot_ws_bytes(n)
+        return torch.empty(nbytes, dtype=torch.uint8, device=self.dev)
+
+
+# --------------------------------------------------------------- operator
+@dataclass
+class DistOperator:
+    """One rank's share of a square matrix in the gathered layout."""
+
+    layout: ShardLayout
+    rank: int
+    n: int  # global rows
+    kernels: object  # HipKernels (or a test double)
+    device: object = None
+
+    @property
+    def world(self) -> int:
+        return self.layout.world
+
+    @property
+    def lo(self) -> int:
+        return int(self.layout.bounds[self.rank])
+
+    @property
+    def rows(self) -> int:
+        return int(self.layout.bounds[self.rank + 1] - self.layout.bounds[self.rank])
+
+    @property
+    def pad(self) -> int:
+        return self.layout.pad
+
+
+def build_operator(m: sa.Coo, rank: int = 0, world: int = 1, fmt: str = "csr", device="cuda:0", align: int = 1024,
+                   **fmt_kw) -> DistOperator:
+    """Partition, renumber and upload this rank's shard (HIP kernels)."""
+    counts = np.bincount(m.row, minlength=m.n_rows).astype(np.int64)
+    layout = layout_for(m.n_rows, counts, world, align)
+    loc = local_shard(m, layout, rank)
+    dm = sa.to_device(loc, fmt, device, **fmt_kw)
+    return DistOperator(layout, rank, m.n_rows, HipKernels(dm), device)
+
+
+def _zeros(op, n):
+    torch = sa._torch()
+    return torch.zeros(n, dtype=torch.float64, device=op.device)
+
+
+def _gathered_pair(op, comm):
+    """(full gathered vector, this rank's send block); one tensor when alone."""
+    if comm.world > 1:
+        return _zeros(op, op.world * op.pad), _zeros(op, op.pad)
+    full = _zeros(op, op.pad)
+    return full, full
+
+
+# -------------------------------------------------------- power iteration
+def power_iteration(op: DistOperator, iters: int, comm: Comm | None = None, x0=None, graph: bool = False,
+                    block: int = 16):
+    """x <- A x / ||A x||, `iters` times.  Returns (hist, x_local): hist is a
+    host array [iters, 2] of (x·Ax, ||Ax||²) per iteration — x·Ax converges
+    to the dominant eigenvalue of a symmetric A — and x_local is this
+    rank's block of the final normalised x (device).  graph=True (one rank)
+    replays `block` iterations per HIP graph launch; same kernels, same
+    bits."""
+    torch = sa._torch()
+    comm = comm or Comm()
+    k = op.kernels
+    rows = op.rows
+    full, send = _gathered_pair(op, comm)
+    x_loc = send[:rows]
+    if x0 is None:  # deterministic start, no zero entries, not orthogonal to much
+        gidx = np.arange(op.lo, op.lo + rows)
+        x_loc.copy_(torch.from_numpy(1.0 + (gidx % 7) / 7.0))
+    else:
+        x_loc.copy_(x0)
+    ws = k.dot_ws(rows)
+    s0 = _zeros(op, 1)
+    k.dot(rows, x_loc, x_loc, s0, ws)
+    comm.allreduce(s0)
+    k.scale_rsqrt(rows, s0, x_loc, x_loc)
+    comm.allgather(full, send)
+    y = _zeros(op, max(rows, 1))
+    hist = _zeros(op, 2 * max(iters, 1)).view(-1, 2)
+
+    def step(h):
+        k.spmv(full, y)
+        k.dot(rows, x_loc, y, h[0:1], ws)
+        k.dot(rows, y, y, h[1:2], ws)
+        comm.allreduce(h)  # both scalars in one collective
+        k.scale_rsqrt(rows, h[1:2], y, x_loc)
+        comm.allgather(full, send)
+
+    done = 0
+    if graph and comm.world == 1 and iters > block:
+        # one eager step (first-call setup), then `block` steps per graph
+        # replay: 7 launches per step become one graph launch per block
+        step(hist[0])
+        done = 1
+        blk = _zeros(op, 2 * block).view(-1, 2)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for j in range(block):
+                step(blk[j])
+        while done + block <= iters:
+            g.replay()
+            hist[done:done + block].copy_(blk)
+            done += block
+    for it in range(done, iters):
+        step(hist[it])
+    return hist[:iters].cpu().numpy(), x_loc
+
+
+# ---------------------------------------------------------------------- CG
+def cg(op: DistOperator, b_loc, comm: Comm | None = None, tol: float = 1e-10, maxit: int = 1000,
+       check_every: int = 10):
+    """Conjugate gradients for a symmetric positive definite A, x0 = 0.
+    Returns (x_local, iterations, relative residual ||r||/||b||)."""
+    comm = comm or Comm()
+    k = op.kernels
+    rows = op.rows
+    full, send = _gathered_pair(op, comm)
+    p = send[:rows]
+    x = _zeros(op, rows)
+    r = b_loc.clone()
+    p.copy_(b_loc)
+    comm.allgather(full, send)
+    Ap = _zeros(op, max(rows, 1))
+    ws = k.dot_ws(rows)
+    rr, rr_new, pAp = _zeros(op, 1), _zeros(op, 1), _zeros(op, 1)
+    k.dot(rows, r, r, rr, ws)
+    comm.allreduce(rr)
+    bb = float(rr.item())
+    if bb == 0.0:
+        return x, 0, 0.0
+    it = 0
+    while it < maxit:
+        k.spmv(full, Ap)
+        k.dot(rows, p, Ap, pAp, ws)
+        comm.allreduce(pAp)
+        k.axpy_ratio(rows, rr, pAp, 1.0, p, x)  # x += alpha p
+        k.axpy_ratio(rows, rr, pAp, -1.0, Ap, r)  # r -= alpha Ap
+        k.dot(rows, r, r, rr_new, ws)
+        comm.allreduce(rr_new)
+        k.xpay_ratio(rows, rr_new, rr, r, p)  # p = r + beta p
+        comm.allgather(full, send)
+        rr, rr_new = rr_new, rr
+        it += 1
+        if it % check_every == 0 or it == maxit:
+            if float(rr.item()) <= tol * tol * bb:
+                break
+    return x, it, float(np.sqrt(max(float(rr.item()), 0.0) / bb))

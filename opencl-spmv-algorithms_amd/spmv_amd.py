@@ -86,6 +86,11 @@ HIP_SYMBOLS = {
     "spmv_cmrs_run": (ctypes.c_int, [Dims, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "spmv_gen_banded_device": (ctypes.c_int, [_c_i64, ctypes.c_uint64, _c_i64, _c_i64, ctypes.c_int, _c_i32,
                                               _c_i32, _vp, _vp, _vp, _vp, ctypes.c_int, _vp]),
+    "spmv_dot_ws_bytes": (ctypes.c_size_t, [_c_i64]),
+    "spmv_dot": (ctypes.c_int, [_c_i64, _vp, _vp, _vp, _vp, ctypes.c_size_t, ctypes.c_int, _vp]),
+    "spmv_axpy_ratio": (ctypes.c_int, [_c_i64, _vp, _vp, ctypes.c_double, _vp, _vp, ctypes.c_int, _vp]),
+    "spmv_xpay_ratio": (ctypes.c_int, [_c_i64, _vp, _vp, _vp, _vp, ctypes.c_int, _vp]),
+    "spmv_scale_rsqrt": (ctypes.c_int, [_c_i64, _vp, _vp, _vp, ctypes.c_int, _vp]),
     "spmv_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     "spmv_set_device": (ctypes.c_int, [ctypes.c_int]),
     "spmv_device_name": (ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t]),

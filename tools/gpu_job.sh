@@ -53,6 +53,10 @@ for s in "${steps[@]}"; do
     sweepnt) run sweep_nt 600 python tools/sweep.py --env-only --rounds 3;;
     pmcnt) run pmc_nt 1100 python tools/pmc_traffic.py --out traffic_nt.json --formats "csr@SPMV_STREAM_NT=1,sell@SPMV_STREAM_NT=1,ell@SPMV_STREAM_NT=1,coo,cmrs";;
     stalls) run pmc_stalls 1150 python tools/pmc_stalls.py --formats csr,sell;;
+    iterbench) run iter_power 300 python tools/iterate_bench.py --what power --matrix cantlike --iters 200 &&
+               run iter_power_graph 300 python tools/iterate_bench.py --what power --matrix cantlike --iters 200 --graph &&
+               run iter_power_sell 300 python tools/iterate_bench.py --what power --matrix cantlike --iters 200 --format sell --graph &&
+               run iter_cg 600 python tools/iterate_bench.py --what cg --matrix laplacian --k 2000 --iters 500;;
     *) echo "unknown step $s";;
   esac
 done

@@ -59,7 +59,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=10)
-    p.add_argument("--format", default="csr", choices=sa.FORMATS)
+    p.add_argument("--format", default="csr", choices=sa.ALL_FORMATS)
     p.add_argument("--copies", type=int, default=32, help="cant-like copies per GPU (batch)")
     p.add_argument("--workload", default="cantlike", choices=["cantlike", "rmat", "banded"],
                    help="cantlike (default, configs[1]/[2]); rmat (configs[3]); banded (configs[4])")
@@ -87,6 +87,8 @@ def kernel_name(args, dm=None):
         v = v or int(os.environ.get("SPMV_CSR_VARIANT", "0") or 0) or CSR_DEFAULT_VARIANT
         return {2: "csr_staged_kernel", 3: "csr_staged_persistent_kernel",
                 4: "csr_tiled_kernel"}.get(v, "csr_vector_kernel")
+    if args.format == "csr16":
+        return "csr_staged_persistent_kernel"
     if args.format in ("coo", "cmrs") and os.environ.get(f"SPMV_{args.format.upper()}_VARIANT", "2") != "1":
         return f"{args.format}_staged_kernel"
     return KERNEL_NAMES[args.format]
@@ -95,6 +97,8 @@ def kernel_name(args, dm=None):
 def fmt_kwargs(args, fmt):
     if fmt == "csr":
         return {"lanes": args.lanes, "variant": args.variant}
+    if fmt == "csr16":
+        return {"lanes": args.lanes}
     if fmt == "ell":
         return {"ki": args.ki}
     if fmt == "sell":
@@ -377,7 +381,7 @@ def main():
         xs = torch.from_numpy(sa.ramp_x(single.n_cols)).to(dev)
         ys = torch.empty(single.n_rows, dtype=torch.float64, device=dev)
         bs = sa.bytes_alg(single.n_rows, single.n_cols, single.nnz)
-        for fmt in sa.FORMATS:
+        for fmt in sa.ALL_FORMATS:
             kw = fmt_kwargs(args, fmt)
             d2 = sa.to_device(m, fmt, dev, **kw)
             w2, k2 = time_steps(torch, d2, x, y, max(20, args.steps // 2), 5)

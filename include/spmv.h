@@ -83,6 +83,14 @@ int spmv_csr_run_variant(spmv_dims d, const int64_t *row_ptr,
                          const int32_t *col, const double *val,
                          const double *x, double *y, int lanes_per_row,
                          int variant);
+/* CSR with compressed 16-bit column indices (arrays
+ * from spmv_csr16_plan/fill in spmv_host.h): 10.06 instead of 12 bytes per
+ * entry when 64-entry blocks of columns span < 65536 (banded / FEM
+ * matrices).  Same kernel as CSR variant 3 with the column source swapped,
+ * so y is bit-identical to spmv_csr_run_variant(..., 3).                 */
+int spmv_csr16_run(spmv_dims d, const int64_t *row_ptr, const int32_t *blk_base,
+                   const uint16_t *col_off, const int32_t *col_esc, const double *val,
+                   const double *x, double *y, int lanes_per_row);
 /* Entry-balanced CSR for skewed row lengths (power-law / R-MAT hubs):
  * every workgroup takes the same number of ENTRIES, whatever the rows; a
  * row that spans workgroups is finished by a deterministic carry pass (as

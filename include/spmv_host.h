@@ -110,6 +110,17 @@ int spmv_sell_fill(int64_t n_rows, const int64_t *row_ptr, const int32_t *col,
 int spmv_cmrs_build(int64_t n_rows, const int64_t *row_ptr, int32_t h,
                     int64_t *strip_ptr, uint8_t *row_in_strip);
 
+/* CSR with compressed 16-bit column indices: the
+ * CSR entries are cut into 64-entry blocks (entry p in block p/64).  A
+ * block whose columns span < 65536 stores blk_base = its smallest column
+ * and col_off[p] = col[p] - blk_base; any other block stores its columns
+ * whole in col_esc[slot*64 .. +64) and blk_base = -1 - slot.  row_ptr and
+ * val are CSR's.  Plan: n_blocks = ceil(nnz/64), n_esc escaped blocks.
+ * Fill: blk_base[n_blocks], col_off[nnz], col_esc[n_esc*64].            */
+int spmv_csr16_plan(int64_t nnz, const int32_t *col, int64_t *n_blocks, int64_t *n_esc);
+int spmv_csr16_fill(int64_t nnz, const int32_t *col, int32_t *blk_base, uint16_t *col_off,
+                    int32_t *col_esc);
+
 /* ----------------------------------------------------- multi-GPU shard ---
  * Row-range partition for one process per GPU: `parts`
  * contiguous ranges [bounds[p], bounds[p+1]) holding about nnz/parts

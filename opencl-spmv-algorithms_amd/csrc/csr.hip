@@ -108,10 +108,45 @@ constexpr bool kCsrStreamNtDefault = false;  // SPMV_STREAM_NT overrides
 // One row group (RPB = 256/L rows) of the staged scheme; s_ptr holds the
 // group's RPB+1 row offsets.  Ends with a barrier, so the caller may
 // overwrite s_ptr / s_prod afterwards.
-template <int L, int R, bool NT>
+// Column sources of the staged kernels: where the column of entry p comes
+// from.  Col32 = the CSR int32 array.  Col16 = compressed 16-bit indices
+// (SURVEY.md §8f row 4): entry p's column is base[p/64] + off[p] when the
+// 64-entry block's columns span < 65536, else the block is stored whole in
+// esc (base = -1 - slot).  10.06 instead of 12 bytes per entry; the
+// columns, hence products and sums, are exactly CSR's.
+template <bool NT>
+struct Col32 {
+    const int32_t *__restrict__ col;
+    __device__ __forceinline__ int2 pair(int64_t p) const { return stream_load2<NT>(col + p); }
+    __device__ __forceinline__ int32_t one(int64_t p) const { return stream_load<NT>(col + p); }
+};
+
+template <bool NT>
+struct Col16 {
+    const int32_t *__restrict__ base;
+    const uint16_t *__restrict__ off;
+    const int32_t *__restrict__ esc;
+    // p even: entries p, p+1 share a 64-entry block and a 4-byte word
+    __device__ __forceinline__ int2 pair(int64_t p) const
+    {
+        const int32_t b = base[p >> 6];
+        if (b >= 0) {
+            const uint32_t w = stream_load<NT>(reinterpret_cast<const uint32_t *>(off + p));
+            return int2{b + (int32_t)(w & 0xffffu), b + (int32_t)(w >> 16)};
+        }
+        return stream_load2<NT>(esc + (int64_t)(-1 - b) * 64 + (p & 63));
+    }
+    __device__ __forceinline__ int32_t one(int64_t p) const
+    {
+        const int32_t b = base[p >> 6];
+        return b >= 0 ? b + (int32_t)stream_load<NT>(off + p) : esc[(int64_t)(-1 - b) * 64 + (p & 63)];
+    }
+};
+
+template <int L, int R, bool NT, typename Cols = Col32<NT>>
 __device__ __forceinline__ void staged_group(
     int64_t row, const int64_t *s_ptr, double2 *s_prod,
-    const int32_t *__restrict__ col, const double *__restrict__ val,
+    const Cols cols, const double *__restrict__ val,
     const double *__restrict__ x, double *__restrict__ y, int64_t n_rows)
 {
     constexpr int RPB = kBlock / L;
@@ -134,11 +169,11 @@ __device__ __forceinline__ void staged_group(
             double2 pr = {0.0, 0.0};
             if (p + 1 < ce) {
                 const double2 v = stream_load2<NT>(val + p);
-                const int2 c = stream_load2<NT>(col + p);
+                const int2 c = cols.pair(p);
                 pr.x = v.x * x[c.x];
                 pr.y = v.y * x[c.y];
             } else if (p < ce) {  // odd tail: never read past the range
-                pr.x = stream_load<NT>(val + p) * x[stream_load<NT>(col + p)];
+                pr.x = stream_load<NT>(val + p) * x[cols.one(p)];
             }
             s_prod[t] = pr;
         }
@@ -171,17 +206,18 @@ __global__ __launch_bounds__(kBlock) void csr_staged_kernel(
         s_ptr[threadIdx.x] = row_ptr[r < n_rows ? r : n_rows];
     }
     __syncthreads();
-    staged_group<L, R, false>(row0 + threadIdx.x / L, s_ptr, s_prod, col, val, x, y, n_rows);
+    staged_group<L, R, false>(row0 + threadIdx.x / L, s_ptr, s_prod, Col32<false>{col}, val, x, y, n_rows);
 }
 
 // Variant 3: persistent workgroups (a few per CU) walk the row groups
 // grid-stride and PREFETCH the next group's row offsets into registers
 // while the current group streams, so a group no longer starts with a
-// dependent round trip for its offsets.
-template <int L, int R, bool NT>
+// dependent round trip for its offsets.  Cols = Col32 (CSR) or Col16
+// (compressed column indices, spmv_csr16_run).
+template <int L, int R, bool NT, typename Cols>
 __global__ __launch_bounds__(kBlock) void csr_staged_persistent_kernel(
     int64_t n_rows, int64_t n_groups, const int64_t *__restrict__ row_ptr,
-    const int32_t *__restrict__ col, const double *__restrict__ val,
+    const Cols cols, const double *__restrict__ val,
     const double *__restrict__ x, double *__restrict__ y)
 {
     constexpr int RPB = kBlock / L;
@@ -202,7 +238,7 @@ __global__ __launch_bounds__(kBlock) void csr_staged_persistent_kernel(
             int64_t r = g2 * RPB + threadIdx.x;
             next = row_ptr[r < n_rows ? r : n_rows];
         }
-        staged_group<L, R, NT>(grp * RPB + threadIdx.x / L, s_ptr, s_prod, col, val, x, y, n_rows);
+        staged_group<L, R, NT, Cols>(grp * RPB + threadIdx.x / L, s_ptr, s_prod, cols, val, x, y, n_rows);
     }
 }
 
@@ -418,11 +454,27 @@ static void launch_persistent(const spmv_dims &d, const int64_t *row_ptr, const 
         hipLaunchKernelGGL((csr_pipelined_kernel<L, R, NT>), dim3((unsigned)grid), dim3(kBlock), 0, st,
                            d.n_rows, groups, row_ptr, col, val, x, y);
     } else {
-        static const int64_t per = persistent_grid(csr_staged_persistent_kernel<L, R, NT>, INT64_MAX);
+        using K = Col32<NT>;
+        static const int64_t per = persistent_grid(csr_staged_persistent_kernel<L, R, NT, K>, INT64_MAX);
         const int64_t grid = per < groups ? per : groups;
-        hipLaunchKernelGGL((csr_staged_persistent_kernel<L, R, NT>), dim3((unsigned)grid), dim3(kBlock),
-                           0, st, d.n_rows, groups, row_ptr, col, val, x, y);
+        hipLaunchKernelGGL((csr_staged_persistent_kernel<L, R, NT, K>), dim3((unsigned)grid), dim3(kBlock),
+                           0, st, d.n_rows, groups, row_ptr, K{col}, val, x, y);
     }
+}
+
+// compressed-index CSR: the persistent staged kernel with Col16 columns
+template <int L, bool NT>
+static void launch_csr16(const spmv_dims &d, const int64_t *row_ptr, const Col16<NT> cols,
+                         const double *val, const double *x, double *y)
+{
+    constexpr int RPB = kBlock / L;
+    constexpr int R = kStageRoundsDefault;
+    const int64_t groups = (d.n_rows + RPB - 1) / RPB;
+    static const int64_t per =
+        persistent_grid(csr_staged_persistent_kernel<L, R, NT, Col16<NT>>, INT64_MAX);
+    const int64_t grid = per < groups ? per : groups;
+    hipLaunchKernelGGL((csr_staged_persistent_kernel<L, R, NT, Col16<NT>>), dim3((unsigned)grid),
+                       dim3(kBlock), 0, (hipStream_t)d.stream, d.n_rows, groups, row_ptr, cols, val, x, y);
 }
 
 template <int L, int R>
@@ -529,6 +581,38 @@ extern "C" int spmv_csr_run(spmv_dims d, const int64_t *row_ptr,
                             const double *x, double *y, int lanes_per_row)
 {
     return spmv_csr_run_variant(d, row_ptr, col, val, x, y, lanes_per_row, 0);
+}
+
+extern "C" int spmv_csr16_run(spmv_dims d, const int64_t *row_ptr, const int32_t *blk_base,
+                              const uint16_t *col_off, const int32_t *col_esc, const double *val,
+                              const double *x, double *y, int lanes_per_row)
+{
+    if (d.n_rows < 0 || d.n_cols < 0 || d.nnz < 0)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_csr16_run: negative size");
+    if (d.n_rows == 0)
+        return SPMV_SUCCESS;
+    if (d.nnz > 0 && (!blk_base || !col_off))
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_csr16_run: missing index arrays");
+    SPMV_GUARD(d);
+    const int L = lanes_per_row > 0 ? lanes_per_row : spmv_csr_auto_lanes(d.n_rows, d.nnz);
+    const bool nt = stream_nt(kCsrStreamNtDefault);
+#define SPMV_CSR16(LL)                                                                          \
+    (nt ? launch_csr16<LL, true>(d, row_ptr, Col16<true>{blk_base, col_off, col_esc}, val, x, y) \
+        : launch_csr16<LL, false>(d, row_ptr, Col16<false>{blk_base, col_off, col_esc}, val, x, y))
+    switch (L) {
+    case 2: SPMV_CSR16(2); break;
+    case 4: SPMV_CSR16(4); break;
+    case 8: SPMV_CSR16(8); break;
+    case 16: SPMV_CSR16(16); break;
+    case 32: SPMV_CSR16(32); break;
+    case 64: SPMV_CSR16(64); break;
+    default:
+        return fail_msg(SPMV_OTHER_ERROR,
+                        "spmv_csr16_run: lanes_per_row must be 0 or a power of two in [2,64]");
+    }
+#undef SPMV_CSR16
+    SPMV_CHECK_LAUNCH("csr16 kernel");
+    return SPMV_SUCCESS;
 }
 
 extern "C" size_t spmv_csr_tiled_ws_bytes(int64_t n_rows, int64_t nnz)

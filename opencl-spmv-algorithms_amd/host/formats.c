@@ -321,6 +321,66 @@ int spmv_cmrs_build(int64_t n_rows, const int64_t *row_ptr, int32_t h,
     return SPMV_SUCCESS;
 }
 
+/* ------------------------------------------- CSR, 16-bit column offsets */
+
+/* smallest column of block b and whether the block's span fits 16 bits */
+static int csr16_block(int64_t nnz, const int32_t *col, int64_t b, int32_t *lo)
+{
+    const int64_t p0 = b * 64, p1 = p0 + 64 < nnz ? p0 + 64 : nnz;
+    int32_t mn = col[p0], mx = col[p0];
+    for (int64_t p = p0 + 1; p < p1; ++p) {
+        mn = col[p] < mn ? col[p] : mn;
+        mx = col[p] > mx ? col[p] : mx;
+    }
+    *lo = mn;
+    return (int64_t)mx - (int64_t)mn <= 65535;
+}
+
+int spmv_csr16_plan(int64_t nnz, const int32_t *col, int64_t *n_blocks, int64_t *n_esc)
+{
+    if (nnz < 0 || !n_blocks || !n_esc)
+        return SPMV_OTHER_ERROR;
+    const int64_t nb = (nnz + 63) / 64;
+    int64_t esc = 0;
+#pragma omp parallel for schedule(static) reduction(+ : esc)
+    for (int64_t b = 0; b < nb; ++b) {
+        int32_t lo;
+        esc += !csr16_block(nnz, col, b, &lo);
+    }
+    if (esc > (int64_t)INT32_MAX)
+        return SPMV_OTHER_ERROR;
+    *n_blocks = nb;
+    *n_esc = esc;
+    return SPMV_SUCCESS;
+}
+
+int spmv_csr16_fill(int64_t nnz, const int32_t *col, int32_t *blk_base, uint16_t *col_off,
+                    int32_t *col_esc)
+{
+    if (nnz < 0)
+        return SPMV_OTHER_ERROR;
+    const int64_t nb = (nnz + 63) / 64;
+    int64_t slot = 0;
+    /* serial: escape slots are numbered in block order */
+    for (int64_t b = 0; b < nb; ++b) {
+        const int64_t p0 = b * 64, p1 = p0 + 64 < nnz ? p0 + 64 : nnz;
+        int32_t lo;
+        if (csr16_block(nnz, col, b, &lo)) {
+            blk_base[b] = lo;
+            for (int64_t p = p0; p < p1; ++p)
+                col_off[p] = (uint16_t)(col[p] - lo);
+        } else {
+            blk_base[b] = (int32_t)(-1 - slot);
+            for (int64_t p = p0; p < p0 + 64; ++p)
+                col_esc[slot * 64 + (p - p0)] = col[p < p1 ? p : p1 - 1];
+            for (int64_t p = p0; p < p1; ++p)
+                col_off[p] = 0;
+            ++slot;
+        }
+    }
+    return SPMV_SUCCESS;
+}
+
 /* ------------------------------------------------------------ sharding */
 
 int spmv_partition_rows(int64_t n_rows, const int64_t *row_ptr, int parts,

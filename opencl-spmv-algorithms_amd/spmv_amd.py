@@ -26,7 +26,9 @@ PKG_DIR = Path(__file__).resolve().parent
 LIB_DIR = PKG_DIR / "lib"
 REPO_DIR = PKG_DIR.parent
 
-FORMATS = ("coo", "csr", "ell", "sell", "cmrs")
+FORMATS = ("coo", "csr", "ell", "sell", "cmrs")  # the reference's five
+EXTRA_FORMATS = ("csr16",)  # CSR with 16-bit column offsets
+ALL_FORMATS = FORMATS + EXTRA_FORMATS
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 # The reference's ReturnCode values (reference inc/enums.h:4-11).
@@ -81,6 +83,7 @@ HIP_SYMBOLS = {
     "spmv_csr_run_variant": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, ctypes.c_int, ctypes.c_int]),
     "spmv_csr_tiled_ws_bytes": (ctypes.c_size_t, [_c_i64, _c_i64]),
     "spmv_csr_run_tiled": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t]),
+    "spmv_csr16_run": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_int]),
     "spmv_ell_run": (ctypes.c_int, [Dims, _c_i32, _c_i64, _c_i32, _vp, _vp, _vp, _vp]),
     "spmv_sell_run": (ctypes.c_int, [Dims, _c_i32, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "spmv_cmrs_run": (ctypes.c_int, [Dims, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
@@ -127,6 +130,8 @@ HOST_SYMBOLS = {
     "spmv_sell_fill": (ctypes.c_int, [_c_i64, _vp, _vp, _vp, _c_i32, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, _vp]),
     "spmv_cmrs_build": (ctypes.c_int, [_c_i64, _vp, _c_i32, _vp, _vp]),
     "spmv_partition_rows": (ctypes.c_int, [_c_i64, _vp, ctypes.c_int, _c_i64, _vp]),
+    "spmv_csr16_plan": (ctypes.c_int, [_c_i64, _vp, ctypes.POINTER(_c_i64), ctypes.POINTER(_c_i64)]),
+    "spmv_csr16_fill": (ctypes.c_int, [_c_i64, _vp, _vp, _vp, _vp]),
     "spmv_cpu_coo": (ctypes.c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, ctypes.c_int]),
     "spmv_cpu_csr": (ctypes.c_int, [_c_i64, _vp, _vp, _vp, _vp, _vp, ctypes.c_int]),
     "spmv_cpu_ell": (ctypes.c_int, [_c_i64, _c_i32, _c_i64, _c_i32, _vp, _vp, _vp, _vp, ctypes.c_int]),
@@ -349,6 +354,18 @@ def cmrs_build(n_rows: int, ptr, h: int = 8):
     return dict(h=h, n_strips=ns, strip_ptr=sp, row_in_strip=rin)
 
 
+def csr16_build(col: np.ndarray):
+    """16-bit column offsets per 64-entry block."""
+    nnz = int(col.shape[0])
+    nb, ne = _c_i64(0), _c_i64(0)
+    _check_host(host_lib().spmv_csr16_plan(nnz, _ptr(col), ctypes.byref(nb), ctypes.byref(ne)), "csr16_plan")
+    base = np.empty(max(nb.value, 1), np.int32)
+    off = np.empty(max(nnz, 2), np.uint16)
+    esc = np.empty(max(ne.value * 64, 1), np.int32)
+    _check_host(host_lib().spmv_csr16_fill(nnz, _ptr(col), _ptr(base), _ptr(off), _ptr(esc)), "csr16_fill")
+    return dict(n_blocks=nb.value, n_esc=ne.value, blk_base=base, col_off=off, col_esc=esc)
+
+
 def partition_rows(n_rows: int, ptr: np.ndarray, parts: int, align: int = 1024) -> np.ndarray:
     """Contiguous row ranges with ~nnz/parts entries each."""
     bounds = np.empty(parts + 1, np.int64)
@@ -436,6 +453,9 @@ class DeviceMatrix:
             else:
                 rc = lib.spmv_csr_run_variant(d, _ptr(a["row_ptr"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x),
                                               _ptr(y), p["lanes"], p.get("variant", 0))
+        elif self.fmt == "csr16":
+            rc = lib.spmv_csr16_run(d, _ptr(a["row_ptr"]), _ptr(a["blk_base"]), _ptr(a["col_off"]),
+                                    _ptr(a["col_esc"]), _ptr(a["val"]), _ptr(x), _ptr(y), p["lanes"])
         elif self.fmt == "ell":
             rc = lib.spmv_ell_run(d, p["K"], p["ld"], p["ki"], _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y))
         elif self.fmt == "sell":
@@ -474,6 +494,13 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
             ws = hip_lib().spmv_csr_tiled_ws_bytes(m.n_rows, m.nnz)
             dm.arrays["ws"] = torch.empty(ws, dtype=torch.uint8, device=device)
         dm.stored_bytes = 12 * m.nnz + 8 * (m.n_rows + 1)
+    elif fmt == "csr16":
+        c = csr16_build(col)
+        dm.params = dict(lanes=lanes, n_blocks=c["n_blocks"], n_esc=c["n_esc"])
+        dm.arrays = dict(row_ptr=_dev_tensor(ptr, device), blk_base=_dev_tensor(c["blk_base"], device),
+                         col_off=_dev_tensor(c["col_off"], device), col_esc=_dev_tensor(c["col_esc"], device),
+                         val=_dev_tensor(val, device))
+        dm.stored_bytes = 10 * m.nnz + 4 * c["n_blocks"] + 256 * c["n_esc"] + 8 * (m.n_rows + 1)
     elif fmt == "ell":
         ki = ki or 2  # measured best for ELL (profiles/round1_sweep.md)
         e = ell_build(m.n_rows, ptr, col, val, ki=ki, max_padding=ell_max_padding)

@@ -36,6 +36,9 @@ FMT_PARAMS = [
     ("csr", {"variant": 5}),
     ("csr", {"lanes": 2, "variant": 5}),
     ("csr", {"lanes": 64, "variant": 5}),
+    ("csr16", {}),
+    ("csr16", {"lanes": 2}),
+    ("csr16", {"lanes": 64}),
     ("ell", {"ki": 1}),
     ("ell", {"ki": 2}),
     ("sell", {"C": 64, "sigma": 1024, "ki": 2}),
@@ -168,6 +171,29 @@ def test_csr_staged_variants_bit_identical(torch_dev, lanes):
     torch.cuda.synchronize()
     assert torch.equal(ys[0].view(torch.int64), ys[1].view(torch.int64))
     assert torch.equal(ys[0].view(torch.int64), ys[2].view(torch.int64))
+
+
+@pytest.mark.parametrize("case", ["cantlike", "rmat", "ragged"])
+def test_csr16_bit_identical_to_csr(torch_dev, case):
+    """Compressed 16-bit column indices decode to CSR's columns, so the
+    staged kernel gives CSR variant 3's bits (escaped blocks included)."""
+    torch, dev = torch_dev
+    if case == "cantlike":
+        m = sa.gen_cantlike(1, copies=2)
+    elif case == "rmat":
+        m = sa.gen_rmat(1_000_000, 10_000_000, scale=20, seed=1)
+    else:
+        m = sa.gen_random(20_000, 300_000, 0, 2_000, seed=21)
+    x = torch.from_numpy(np.random.default_rng(6).uniform(-1, 1, m.n_cols)).to(dev)
+    ys = []
+    for fmt, kw in (("csr", {"variant": 3, "lanes": 4}), ("csr16", {"lanes": 4})):
+        dm = sa.to_device(m, fmt, dev, **kw)
+        y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
+        dm.run(x, y)
+        ys.append(y)
+    torch.cuda.synchronize()
+    assert torch.equal(ys[0].view(torch.int64), ys[1].view(torch.int64))
+    assert_parity(m, ys[1].cpu().numpy(), x.cpu().numpy())
 
 
 @pytest.mark.parametrize("fmt,kw", [("csr", {"variant": 3}), ("csr", {"variant": 5}), ("csr", {"variant": 2}),

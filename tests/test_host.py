@@ -243,3 +243,33 @@ def test_parallel_parse_matches_serial_semantics(tmp_path):
         f.write("1 1 5.0\n")
     r2 = sa.read_mtx(p)
     assert r2.nnz == m.nnz and np.array_equal(r2.val, r.val)
+
+
+@pytest.mark.parametrize("kind", ["cantlike", "rmat", "mixed", "tiny"])
+def test_csr16_round_trip(kind):
+    """Compressed 16-bit column offsets decode to the
+    CSR columns exactly; wide blocks go through the escape array."""
+    if kind == "cantlike":
+        m = sa.gen_cantlike(0)
+    elif kind == "rmat":
+        m = sa.gen_rmat(100_000, 1_000_000, scale=17, seed=2)
+    elif kind == "mixed":
+        m = sa.gen_random(70_000, 200_000, 0, 40, seed=11)
+    else:
+        m = sa.read_mtx(GOLDEN / "n67.mtx")
+    ptr, col, val = sa.csr_from_coo(m)
+    c = sa.csr16_build(col)
+    nnz = len(col)
+    assert c["n_blocks"] == (nnz + 63) // 64
+    p = np.arange(nnz)
+    base = c["blk_base"][p // 64].astype(np.int64)
+    esc_slot = -1 - base
+    esc = np.concatenate([c["col_esc"], np.zeros(64, np.int32)])  # np.where evaluates both sides
+    dec = np.where(base >= 0, base + c["col_off"][:nnz].astype(np.int64),
+                   esc[np.maximum(esc_slot, 0) * 64 + (p % 64)])
+    assert np.array_equal(dec, col.astype(np.int64))
+    assert c["n_esc"] == int(np.sum(c["blk_base"][: c["n_blocks"]] < 0))
+    if kind == "cantlike":
+        assert c["n_esc"] == 0
+    if kind == "rmat":
+        assert c["n_esc"] > 0.9 * c["n_blocks"]

@@ -26,7 +26,7 @@ from pathlib import Path
 REPO = Path(__file__).resolve().parents[1]
 OUT = REPO / "gpurun_out" / "pmc"
 KERNELS = {"csr": "csr_", "sell": "sell_kernel", "ell": "ell_kernel",
-           "coo": "coo_staged_kernel", "cmrs": "cmrs_staged_kernel"}
+           "coo": "coo_staged_kernel", "cmrs": "cmrs_staged_kernel", "csr16": "Col16"}
 
 
 def kernel_for(fmt, env):

@@ -33,6 +33,7 @@ VARIANTS = [
     ("sell", {"C": 64, "sigma": 512, "ki": 2}),
     ("cmrs", {"h": 8}), ("cmrs", {"h": 16}), ("cmrs", {"h": 32}),
     ("coo", {}),
+    ("csr16", {"lanes": 4}), ("csr16", {"lanes": 2}), ("csr16", {"lanes": 8}),
     # load policy of the streamed arrays (SPMV_STREAM_NT), groups in flight (SPMV_SLOT_UNROLL)
     ("csr", {"lanes": 4, "variant": 3, "env": {"SPMV_STREAM_NT": "0"}}),
     ("csr", {"lanes": 4, "variant": 3, "env": {"SPMV_STREAM_NT": "1"}}),

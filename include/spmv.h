@@ -129,6 +129,21 @@ int spmv_sell_run(spmv_dims d, int32_t C, int32_t sigma, int32_t ki, int64_t n_s
                   const int64_t *slice_ptr, const int32_t *perm,
                   const int32_t *col, const double *val, const double *x,
                   double *y);
+/* SELL with each workgroup's x window staged in LDS (MI355X: 160 KiB LDS
+ * per CU).  Build once: spmv_sell_xwin_build scans col (device) for every
+ * workgroup's column range into `win` (spmv_sell_xwin_bytes bytes) and
+ * returns in *xcap the LDS entries the run needs (0: no window fits, the
+ * run gathers from global memory).  spmv_sell_run_xwin copies x[lo..hi]
+ * into LDS per workgroup and gathers from there; y is bit-identical to
+ * spmv_sell_run's.                                                       */
+size_t spmv_sell_xwin_bytes(int64_t n_slices, int32_t C, int32_t sigma);
+int spmv_sell_xwin_build(spmv_dims d, int32_t C, int32_t sigma, int64_t n_slices,
+                         const int64_t *slice_ptr, const int32_t *col, void *win,
+                         size_t win_bytes, int32_t *xcap);
+int spmv_sell_run_xwin(spmv_dims d, int32_t C, int32_t sigma, int32_t ki, int64_t n_slices,
+                       const int64_t *slice_ptr, const int32_t *perm, const int32_t *col,
+                       const double *val, const double *x, double *y, const void *win,
+                       int32_t xcap);
 
 /* --------------------------------------------------------------- CMRS ---
  * Replaces kernel `cmrs(val,idx,strip_ptr,row_in_strip,x,y,N,h,__local)`

@@ -104,6 +104,10 @@ constexpr int kStageRoundsDefault = 4;  // pairs per lane per chunk: 2048 produc
 // (16 KiB keeps 8 workgroups = 32 waves per CU; 20 KiB (R = 5) capped the
 // CU at 7 and measured slower, R = 8 at 4 and much slower)
 constexpr bool kCsrStreamNtDefault = false;  // SPMV_STREAM_NT overrides
+// Stage load schedule (SPMV_CSR_BATCH overrides): 0 = per-round guarded
+// loads measured 0.313 ms against 0.350 ms for loads + gathers batched
+// (mode 2: 76 VGPRs, 6 waves/SIMD) on the cant-like batch.
+constexpr int kCsrBatchDefault = 0;
 
 // One row group (RPB = 256/L rows) of the staged scheme; s_ptr holds the
 // group's RPB+1 row offsets.  Ends with a barrier, so the caller may
@@ -143,11 +147,69 @@ struct Col16 {
     }
 };
 
-template <int L, int R, bool NT, typename Cols = Col32<NT>>
+// One chunk of a staged range, [cb, ce), cb even: every lane loads its R
+// value/column pairs FIRST (branch-free, so all 2R loads are in flight
+// together), then gathers x and stores the products in LDS.  A lane whose
+// pair starts at or past ce, or would reach past the array (nz entries),
+// loads pair 0 instead — always valid memory, one cached line — and its
+// products are never read: the reductions only read [cb, ce).  The one
+// entry that can need more is the array's last entry when nz is odd; it
+// is loaded singly in a branch almost every wave skips.  (With the guarded
+// loads inside per-round branches the compiler serialised the rounds:
+// one round's loads in flight at a time.)
+// GATHERS_TOGETHER: also issue all 2R x gathers before the first product
+// (more loads in flight per wave, more VGPRs, lower occupancy) instead of
+// gathering round by round.
+template <int R, bool NT, bool GATHERS_TOGETHER, typename Cols>
+__device__ __forceinline__ void stage_products(int64_t cb, int64_t ce, int64_t nz, const Cols &cols,
+                                               const double *__restrict__ val,
+                                               const double *__restrict__ x, double2 *s_prod)
+{
+    double2 v[R];
+    int2 c[R];
+    if (nz >= 2) {  // uniform; a 1-entry array has no pair 0
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const int64_t p = cb + 2 * (int64_t)(threadIdx.x + k * kBlock);
+            const int64_t q = (p < ce && p + 1 < nz) ? p : 0;
+            v[k] = stream_load2<NT>(val + q);
+            c[k] = cols.pair(q);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            v[k] = double2{0.0, 0.0};
+            c[k] = int2{0, 0};
+        }
+    }
+    if constexpr (GATHERS_TOGETHER) {
+        double2 xv[R];
+#pragma unroll
+        for (int k = 0; k < R; ++k)  // all 2R gathers in flight together
+            xv[k] = double2{x[c[k].x], x[c[k].y]};
+#pragma unroll
+        for (int k = 0; k < R; ++k)
+            s_prod[threadIdx.x + k * kBlock] = double2{v[k].x * xv[k].x, v[k].y * xv[k].y};
+    } else {
+#pragma unroll
+        for (int k = 0; k < R; ++k)
+            s_prod[threadIdx.x + k * kBlock] = double2{v[k].x * x[c[k].x], v[k].y * x[c[k].y]};
+    }
+    // the array's odd last entry (at most one lane of one chunk)
+    const int64_t tail = nz - 1 - cb;
+    if ((nz & 1) && nz - 1 < ce && tail >= 0 && tail < 2 * R * kBlock && (tail >> 1) % kBlock == threadIdx.x) {
+        const int64_t p = nz - 1;
+        s_prod[tail >> 1].x = stream_load<NT>(val + p) * x[cols.one(p)];
+    }
+}
+
+// BATCH: 0 = per-round guarded loads, 1 = stream loads batched (gathers
+// per round), 2 = stream loads and gathers batched (stage_products)
+template <int L, int R, bool NT, typename Cols = Col32<NT>, int BATCH = 0>
 __device__ __forceinline__ void staged_group(
     int64_t row, const int64_t *s_ptr, double2 *s_prod,
     const Cols cols, const double *__restrict__ val,
-    const double *__restrict__ x, double *__restrict__ y, int64_t n_rows)
+    const double *__restrict__ x, double *__restrict__ y, int64_t n_rows, int64_t nz)
 {
     constexpr int RPB = kBlock / L;
     constexpr int CH = 2 * kBlock * R;  // products per chunk
@@ -162,20 +224,24 @@ __device__ __forceinline__ void staged_group(
     // an entry before the group's range is loaded but never summed.
     for (int64_t cb = s_ptr[0] & ~(int64_t)1; cb < blk_end; cb += CH) {
         const int64_t ce = cb + CH < blk_end ? cb + CH : blk_end;
+        if constexpr (BATCH > 0) {
+            stage_products<R, NT, BATCH == 2>(cb, ce, nz, cols, val, x, s_prod);
+        } else {  // per-round guarded loads
 #pragma unroll
-        for (int k = 0; k < R; ++k) {
-            const int t = threadIdx.x + k * kBlock;
-            const int64_t p = cb + 2 * (int64_t)t;
-            double2 pr = {0.0, 0.0};
-            if (p + 1 < ce) {
-                const double2 v = stream_load2<NT>(val + p);
-                const int2 c = cols.pair(p);
-                pr.x = v.x * x[c.x];
-                pr.y = v.y * x[c.y];
-            } else if (p < ce) {  // odd tail: never read past the range
-                pr.x = stream_load<NT>(val + p) * x[cols.one(p)];
+            for (int k = 0; k < R; ++k) {
+                const int t = threadIdx.x + k * kBlock;
+                const int64_t p = cb + 2 * (int64_t)t;
+                double2 pr = {0.0, 0.0};
+                if (p + 1 < ce) {
+                    const double2 v = stream_load2<NT>(val + p);
+                    const int2 c = cols.pair(p);
+                    pr.x = v.x * x[c.x];
+                    pr.y = v.y * x[c.y];
+                } else if (p < ce) {
+                    pr.x = stream_load<NT>(val + p) * x[cols.one(p)];
+                }
+                s_prod[t] = pr;
             }
-            s_prod[t] = pr;
         }
         __syncthreads();
         const int64_t lo = beg > cb ? beg : cb;
@@ -206,7 +272,8 @@ __global__ __launch_bounds__(kBlock) void csr_staged_kernel(
         s_ptr[threadIdx.x] = row_ptr[r < n_rows ? r : n_rows];
     }
     __syncthreads();
-    staged_group<L, R, false>(row0 + threadIdx.x / L, s_ptr, s_prod, Col32<false>{col}, val, x, y, n_rows);
+    staged_group<L, R, false>(row0 + threadIdx.x / L, s_ptr, s_prod, Col32<false>{col}, val, x, y, n_rows,
+                              row_ptr[n_rows]);
 }
 
 // Variant 3: persistent workgroups (a few per CU) walk the row groups
@@ -214,7 +281,7 @@ __global__ __launch_bounds__(kBlock) void csr_staged_kernel(
 // while the current group streams, so a group no longer starts with a
 // dependent round trip for its offsets.  Cols = Col32 (CSR) or Col16
 // (compressed column indices, spmv_csr16_run).
-template <int L, int R, bool NT, typename Cols>
+template <int L, int R, bool NT, typename Cols, int BATCH = 0>
 __global__ __launch_bounds__(kBlock) void csr_staged_persistent_kernel(
     int64_t n_rows, int64_t n_groups, const int64_t *__restrict__ row_ptr,
     const Cols cols, const double *__restrict__ val,
@@ -223,6 +290,7 @@ __global__ __launch_bounds__(kBlock) void csr_staged_persistent_kernel(
     constexpr int RPB = kBlock / L;
     __shared__ int64_t s_ptr[RPB + 1];
     __shared__ double2 s_prod[kBlock * R];
+    const int64_t nz = row_ptr[n_rows];
     int64_t grp = blockIdx.x;
     int64_t next = 0;
     if (threadIdx.x <= RPB) {
@@ -238,7 +306,8 @@ __global__ __launch_bounds__(kBlock) void csr_staged_persistent_kernel(
             int64_t r = g2 * RPB + threadIdx.x;
             next = row_ptr[r < n_rows ? r : n_rows];
         }
-        staged_group<L, R, NT, Cols>(grp * RPB + threadIdx.x / L, s_ptr, s_prod, cols, val, x, y, n_rows);
+        staged_group<L, R, NT, Cols, BATCH>(grp * RPB + threadIdx.x / L, s_ptr, s_prod, cols, val, x, y, n_rows,
+                                            nz);
     }
 }
 
@@ -413,7 +482,7 @@ static int csr_stage_rounds()
 {
     const char *s = getenv("SPMV_CSR_STAGE_ROUNDS");
     const int r = s ? atoi(s) : kStageRoundsDefault;
-    return (r == 3 || r == 4 || r == 5 || r == 8) ? r : kStageRoundsDefault;
+    return (r == 2 || r == 3 || r == 4 || r == 5 || r == 8) ? r : kStageRoundsDefault;
 }
 
 static int cu_count()
@@ -442,23 +511,42 @@ static int64_t persistent_grid(K kernel, int64_t groups)
     return grid < groups ? grid : groups;
 }
 
+// SPMV_CSR_BATCH = 0 / 1 / 2 selects the stage's load schedule (see
+// staged_group); read per call so a sweep can flip it in-process
+static int csr_batch_mode(int dflt)
+{
+    const char *s = getenv("SPMV_CSR_BATCH");
+    return (s && s[0] >= '0' && s[0] <= '2') ? s[0] - '0' : dflt;
+}
+
+template <int L, int R, bool NT, typename Cols, int BATCH>
+static void launch_persistent_cols(const spmv_dims &d, const int64_t *row_ptr, const Cols cols,
+                                   const double *val, const double *x, double *y, int64_t groups)
+{
+    static const int64_t per = persistent_grid(csr_staged_persistent_kernel<L, R, NT, Cols, BATCH>, INT64_MAX);
+    const int64_t grid = per < groups ? per : groups;
+    hipLaunchKernelGGL((csr_staged_persistent_kernel<L, R, NT, Cols, BATCH>), dim3((unsigned)grid),
+                       dim3(kBlock), 0, (hipStream_t)d.stream, d.n_rows, groups, row_ptr, cols, val, x, y);
+}
+
 template <int L, int R, bool NT>
 static void launch_persistent(const spmv_dims &d, const int64_t *row_ptr, const int32_t *col,
                               const double *val, const double *x, double *y, int variant,
                               int64_t groups)
 {
     const hipStream_t st = (hipStream_t)d.stream;
+    using K = Col32<NT>;
     if (variant == 5) {
         static const int64_t per = persistent_grid(csr_pipelined_kernel<L, R, NT>, INT64_MAX);
         const int64_t grid = per < groups ? per : groups;
         hipLaunchKernelGGL((csr_pipelined_kernel<L, R, NT>), dim3((unsigned)grid), dim3(kBlock), 0, st,
                            d.n_rows, groups, row_ptr, col, val, x, y);
-    } else {
-        using K = Col32<NT>;
-        static const int64_t per = persistent_grid(csr_staged_persistent_kernel<L, R, NT, K>, INT64_MAX);
-        const int64_t grid = per < groups ? per : groups;
-        hipLaunchKernelGGL((csr_staged_persistent_kernel<L, R, NT, K>), dim3((unsigned)grid), dim3(kBlock),
-                           0, st, d.n_rows, groups, row_ptr, K{col}, val, x, y);
+        return;
+    }
+    switch (csr_batch_mode(kCsrBatchDefault)) {
+    case 1: launch_persistent_cols<L, R, NT, K, 1>(d, row_ptr, K{col}, val, x, y, groups); break;
+    case 2: launch_persistent_cols<L, R, NT, K, 2>(d, row_ptr, K{col}, val, x, y, groups); break;
+    default: launch_persistent_cols<L, R, NT, K, 0>(d, row_ptr, K{col}, val, x, y, groups); break;
     }
 }
 
@@ -470,11 +558,11 @@ static void launch_csr16(const spmv_dims &d, const int64_t *row_ptr, const Col16
     constexpr int RPB = kBlock / L;
     constexpr int R = kStageRoundsDefault;
     const int64_t groups = (d.n_rows + RPB - 1) / RPB;
-    static const int64_t per =
-        persistent_grid(csr_staged_persistent_kernel<L, R, NT, Col16<NT>>, INT64_MAX);
-    const int64_t grid = per < groups ? per : groups;
-    hipLaunchKernelGGL((csr_staged_persistent_kernel<L, R, NT, Col16<NT>>), dim3((unsigned)grid),
-                       dim3(kBlock), 0, (hipStream_t)d.stream, d.n_rows, groups, row_ptr, cols, val, x, y);
+    switch (csr_batch_mode(kCsrBatchDefault)) {
+    case 1: launch_persistent_cols<L, R, NT, Col16<NT>, 1>(d, row_ptr, cols, val, x, y, groups); break;
+    case 2: launch_persistent_cols<L, R, NT, Col16<NT>, 2>(d, row_ptr, cols, val, x, y, groups); break;
+    default: launch_persistent_cols<L, R, NT, Col16<NT>, 0>(d, row_ptr, cols, val, x, y, groups); break;
+    }
 }
 
 template <int L, int R>
@@ -506,6 +594,7 @@ static void launch_csr(const spmv_dims &d, const int64_t *row_ptr,
     const hipStream_t st = (hipStream_t)d.stream;
     if (variant >= 2) {
         switch (csr_stage_rounds()) {
+        case 2: launch_staged<L, 2>(d, row_ptr, col, val, x, y, variant); break;
         case 3: launch_staged<L, 3>(d, row_ptr, col, val, x, y, variant); break;
         case 4: launch_staged<L, 4>(d, row_ptr, col, val, x, y, variant); break;
         case 5: launch_staged<L, 5>(d, row_ptr, col, val, x, y, variant); break;

@@ -14,6 +14,9 @@
 // undone in the store, not in an extra pass).
 // Bytes per slice step: C·ki·(8 + 4) + x gathers; padding slots are
 // loaded (that is the format's cost) but re-use the row's own column.
+#include <stdio.h>
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace spmv {
@@ -30,41 +33,51 @@ static int slot_unroll()
     return (s && s[0] == '8') ? 8 : 4;
 }
 
+// Where x[c] comes from: global memory (XGlobal) or the workgroup's
+// window x[lo..hi] staged in LDS (XWindow, see sell_xwin_kernel).
+struct XGlobal {
+    const double *__restrict__ x;
+    __device__ __forceinline__ double operator()(int32_t c) const { return x[c]; }
+};
+
+struct XWindow {
+    const double *s;  // LDS
+    int32_t lo;
+    __device__ __forceinline__ double operator()(int32_t c) const { return s[c - lo]; }
+};
+
 template <int KI, bool NT>
 struct Step;
 
 template <bool NT>
 struct Step<1, NT> {
-    static __device__ __forceinline__ double fma(const double *vp,
-                                                 const int32_t *cp,
-                                                 const double *__restrict__ x,
+    template <typename XS>
+    static __device__ __forceinline__ double fma(const double *vp, const int32_t *cp, const XS &xs,
                                                  double acc)
     {
-        return acc + stream_load<NT>(vp) * x[stream_load<NT>(cp)];
+        return acc + stream_load<NT>(vp) * xs(stream_load<NT>(cp));
     }
 };
 
 template <bool NT>
 struct Step<2, NT> {
-    static __device__ __forceinline__ double fma(const double *vp,
-                                                 const int32_t *cp,
-                                                 const double *__restrict__ x,
+    template <typename XS>
+    static __device__ __forceinline__ double fma(const double *vp, const int32_t *cp, const XS &xs,
                                                  double acc)
     {
         const double2 v = stream_load2<NT>(vp);
         const int2 c = stream_load2<NT>(cp);
-        return acc + v.x * x[c.x] + v.y * x[c.y];
+        return acc + v.x * xs(c.x) + v.y * xs(c.y);
     }
 };
 
 // Slot-per-lane loop over `w` slots (a multiple of KI) with stride
 // `step` elements between consecutive KI-groups; U groups in flight
 // (U independent accumulators, combined as a pairwise tree).
-template <int KI, bool NT, int U>
+template <int KI, bool NT, int U, typename XS>
 __device__ __forceinline__ double slot_dot(const double *__restrict__ vp,
                                            const int32_t *__restrict__ cp,
-                                           int64_t w, int64_t step,
-                                           const double *__restrict__ x)
+                                           int64_t w, int64_t step, const XS &xs)
 {
     double a[U];
 #pragma unroll
@@ -75,10 +88,10 @@ __device__ __forceinline__ double slot_dot(const double *__restrict__ vp,
     for (; g + U <= groups; g += U) {
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            a[u] = Step<KI, NT>::fma(vp + (g + u) * step, cp + (g + u) * step, x, a[u]);
+            a[u] = Step<KI, NT>::fma(vp + (g + u) * step, cp + (g + u) * step, xs, a[u]);
     }
     for (; g < groups; ++g)
-        a[0] = Step<KI, NT>::fma(vp + g * step, cp + g * step, x, a[0]);
+        a[0] = Step<KI, NT>::fma(vp + g * step, cp + g * step, xs, a[0]);
 #pragma unroll
     for (int h = U / 2; h > 0; h /= 2) {
 #pragma unroll
@@ -109,7 +122,7 @@ __global__ __launch_bounds__(1024) void sell_kernel(
     const int64_t base = slice_ptr[s];
     const int64_t w = (slice_ptr[s + 1] - base) / C;
     const int64_t off = base + r * KI;
-    const double sum = slot_dot<KI, NT, U>(val + off, col + off, w, (int64_t)C * KI, x);
+    const double sum = slot_dot<KI, NT, U>(val + off, col + off, w, (int64_t)C * KI, XGlobal{x});
     const int32_t row = perm[slot];
     if (row >= 0)
         y[row] = sum;
@@ -125,44 +138,153 @@ __global__ __launch_bounds__(kBlock) void ell_kernel(
     if (i >= n_rows)
         return;
     const int64_t off = i * KI;
-    y[i] = slot_dot<KI, NT, U>(val + off, col + off, K, ld * KI, x);
+    y[i] = slot_dot<KI, NT, U>(val + off, col + off, K, ld * KI, XGlobal{x});
 }
 
 }  // namespace spmv
 
 using namespace spmv;
 
+namespace spmv {
+
+// Workgroup geometry of the SELL kernels: one workgroup per sigma window
+// when it fits (256..1024 slots, a multiple of the wave), else 256 slots.
+// A small matrix (fewer than ~2 windows per CU) needs the parallelism of
+// 256-slot groups more than merged stores: one cant-like copy has only 61
+// windows of 1024 rows for 256 CUs.
+static void sell_geometry(int32_t C, int32_t sigma, int64_t n_slices, int *bt, int64_t *blocks)
+{
+    static const int force256 = [] {
+        const char *s = getenv("SPMV_SELL_BT");  // tuning knob: "256" forces 256-slot groups
+        return s && atoi(s) == 256;
+    }();
+    const int64_t slots = n_slices * C;
+    const int64_t windows = sigma > 1 ? (slots + sigma - 1) / sigma : 0;
+    const bool wide = !force256 && windows >= 512 && sigma >= kBlock && sigma <= 1024 &&
+                      sigma % kWave == 0;
+    *bt = wide ? sigma : kBlock;
+    *blocks = (slots + *bt - 1) / *bt;
+}
+
+static int sell_check_args(const spmv_dims &d, int32_t C, int32_t sigma, int32_t ki, int64_t n_slices,
+                           const char *who)
+{
+    static thread_local char msg[160];
+    if (d.n_rows < 0 || C <= 0 || C > 1024 || n_slices < 0) {
+        snprintf(msg, sizeof msg, "%s: bad C / sizes", who);
+        return fail_msg(SPMV_OTHER_ERROR, msg);
+    }
+    if (ki != 1 && ki != 2) {
+        snprintf(msg, sizeof msg, "%s: ki must be 1 or 2", who);
+        return fail_msg(SPMV_OTHER_ERROR, msg);
+    }
+    if (sigma < 1 || (sigma > 1 && sigma % C != 0)) {
+        snprintf(msg, sizeof msg, "%s: sigma must be 1 or a multiple of C", who);
+        return fail_msg(SPMV_OTHER_ERROR, msg);
+    }
+    if (n_slices * C < d.n_rows) {
+        snprintf(msg, sizeof msg, "%s: n_slices*C < n_rows", who);
+        return fail_msg(SPMV_OTHER_ERROR, msg);
+    }
+    return SPMV_SUCCESS;
+}
+
+// Column window [lo, hi] of every SELL workgroup: min/max column over the
+// contiguous entries of the slices it covers (one pass over col, build time).
+__global__ __launch_bounds__(kBlock) void sell_window_kernel(int32_t C, int bt, int64_t n_slices,
+                                                             const int64_t *__restrict__ slice_ptr,
+                                                             const int32_t *__restrict__ col,
+                                                             int2 *__restrict__ win)
+{
+    __shared__ int s_lo[kBlock / kWave], s_hi[kBlock / kWave];
+    const int64_t b = blockIdx.x;
+    const int64_t s0 = b * bt / C;
+    int64_t s1 = ((b + 1) * bt + C - 1) / C;
+    s1 = s1 < n_slices ? s1 : n_slices;
+    const int64_t e0 = slice_ptr[s0], e1 = slice_ptr[s1];
+    int lo = INT32_MAX, hi = INT32_MIN;
+    for (int64_t e = e0 + threadIdx.x; e < e1; e += kBlock) {
+        const int c = col[e];
+        lo = c < lo ? c : lo;
+        hi = c > hi ? c : hi;
+    }
+#pragma unroll
+    for (int off = kWave / 2; off > 0; off >>= 1) {
+        const int l2 = __shfl_xor(lo, off), h2 = __shfl_xor(hi, off);
+        lo = l2 < lo ? l2 : lo;
+        hi = h2 > hi ? h2 : hi;
+    }
+    if (threadIdx.x % kWave == 0) {
+        s_lo[threadIdx.x / kWave] = lo;
+        s_hi[threadIdx.x / kWave] = hi;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kBlock / kWave; ++w) {
+            lo = s_lo[w] < lo ? s_lo[w] : lo;
+            hi = s_hi[w] > hi ? s_hi[w] : hi;
+        }
+        win[b] = lo <= hi ? int2{lo, hi} : int2{0, -1};
+    }
+}
+
+// SELL with the workgroup's x window staged in LDS.  Cant-like rows of a
+// 1024-row sigma window read ~1,600 distinct columns; gathering them from
+// global memory costs one TA/TCP address per lane per step (the kernels'
+// limiter: TA busy 80 %, requests far below the DRAM credit limit,
+// profiles/round1/pmc_stalls.json).  Here the window is copied into LDS
+// once with coalesced loads and every gather is a ds_read_b64.  A
+// workgroup whose window exceeds xcap entries gathers from global memory.
+template <int KI, bool NT, int U>
+__global__ __launch_bounds__(1024) void sell_xwin_kernel(
+    int32_t C, int64_t n_slices, const int64_t *__restrict__ slice_ptr,
+    const int32_t *__restrict__ perm, const int32_t *__restrict__ col,
+    const double *__restrict__ val, const double *__restrict__ x,
+    double *__restrict__ y, const int2 *__restrict__ win, int32_t xcap)
+{
+    extern __shared__ double s_x[];
+    const int2 wnd = win[blockIdx.x];
+    const int32_t span = wnd.y - wnd.x + 1;
+    const bool staged = span > 0 && span <= xcap;  // uniform per workgroup
+    if (staged) {
+        for (int32_t i = threadIdx.x; i < span; i += blockDim.x)
+            s_x[i] = x[wnd.x + i];
+        __syncthreads();
+    }
+    const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t s = slot / C;
+    if (s >= n_slices)
+        return;
+    const int64_t r = slot - s * C;
+    const int64_t base = slice_ptr[s];
+    const int64_t w = (slice_ptr[s + 1] - base) / C;
+    const int64_t off = base + r * KI;
+    const double sum = staged ? slot_dot<KI, NT, U>(val + off, col + off, w, (int64_t)C * KI, XWindow{s_x, wnd.x})
+                              : slot_dot<KI, NT, U>(val + off, col + off, w, (int64_t)C * KI, XGlobal{x});
+    const int32_t row = perm[slot];
+    if (row >= 0)
+        y[row] = sum;
+}
+
+constexpr int32_t kXwinCapWide = 8192;   // 64 KiB of LDS per 1024-slot workgroup (2 per CU)
+constexpr int32_t kXwinCapNarrow = 2048; // 16 KiB per 256-slot workgroup
+
+}  // namespace spmv
+
 extern "C" int spmv_sell_run(spmv_dims d, int32_t C, int32_t sigma, int32_t ki,
                              int64_t n_slices, const int64_t *slice_ptr,
                              const int32_t *perm, const int32_t *col,
                              const double *val, const double *x, double *y)
 {
-    if (d.n_rows < 0 || C <= 0 || C > 1024 || n_slices < 0)
-        return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_run: bad C / sizes");
-    if (ki != 1 && ki != 2)
-        return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_run: ki must be 1 or 2");
-    if (sigma < 1 || (sigma > 1 && sigma % C != 0))
-        return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_run: sigma must be 1 or a multiple of C");
-    if (n_slices * C < d.n_rows)
-        return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_run: n_slices*C < n_rows");
+    int rc = sell_check_args(d, C, sigma, ki, n_slices, "spmv_sell_run");
+    if (rc != SPMV_SUCCESS)
+        return rc;
     if (d.n_rows == 0 || n_slices == 0)
         return SPMV_SUCCESS;
     SPMV_GUARD(d);
-    const int64_t slots = n_slices * C;
-    // workgroup = one sigma window when it fits (256..1024 slots, a
-    // multiple of the wave), else 256 slots
-    static const int force256 = [] {
-        const char *s = getenv("SPMV_SELL_BT");  // tuning knob: "256" forces 256-slot groups
-        return s && atoi(s) == 256;
-    }();
-    // A small matrix (fewer than ~2 windows per CU) needs the parallelism of
-    // 256-slot groups more than merged stores: one cant-like copy has only
-    // 61 windows of 1024 rows for 256 CUs.
-    const int64_t windows = sigma > 1 ? (slots + sigma - 1) / sigma : 0;
-    const bool wide = !force256 && windows >= 512 && sigma >= kBlock && sigma <= 1024 &&
-                      sigma % kWave == 0;
-    const int bt = wide ? sigma : kBlock;
-    const int64_t blocks = (slots + bt - 1) / bt;
+    int bt;
+    int64_t blocks;
+    sell_geometry(C, sigma, n_slices, &bt, &blocks);
     if (blocks > INT32_MAX)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_run: grid too large");
     const int remap = xcd_remap_enabled() ? 1 : 0;
@@ -175,6 +297,90 @@ extern "C" int spmv_sell_run(spmv_dims d, int32_t C, int32_t sigma, int32_t ki,
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(bt), 0, (hipStream_t)d.stream, C,
                        n_slices, slice_ptr, perm, col, val, x, y, remap);
     SPMV_CHECK_LAUNCH("sell_kernel");
+    return SPMV_SUCCESS;
+}
+
+extern "C" size_t spmv_sell_xwin_bytes(int64_t n_slices, int32_t C, int32_t sigma)
+{
+    if (n_slices <= 0 || C <= 0)
+        return 0;
+    int bt;
+    int64_t blocks;
+    sell_geometry(C, sigma, n_slices, &bt, &blocks);
+    return (size_t)blocks * sizeof(int2);
+}
+
+extern "C" int spmv_sell_xwin_build(spmv_dims d, int32_t C, int32_t sigma, int64_t n_slices,
+                                    const int64_t *slice_ptr, const int32_t *col, void *win,
+                                    size_t win_bytes, int32_t *xcap)
+{
+    int rc = sell_check_args(d, C, sigma, 1, n_slices, "spmv_sell_xwin_build");
+    if (rc != SPMV_SUCCESS)
+        return rc;
+    if (!xcap)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_xwin_build: xcap is NULL");
+    *xcap = 0;
+    if (d.n_rows == 0 || n_slices == 0)
+        return SPMV_SUCCESS;
+    if (!win || win_bytes < spmv_sell_xwin_bytes(n_slices, C, sigma))
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_xwin_build: window buffer too small");
+    SPMV_GUARD(d);
+    int bt;
+    int64_t blocks;
+    sell_geometry(C, sigma, n_slices, &bt, &blocks);
+    const hipStream_t st = (hipStream_t)d.stream;
+    hipLaunchKernelGGL(sell_window_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, st, C, bt, n_slices,
+                       slice_ptr, col, (int2 *)win);
+    SPMV_CHECK_LAUNCH("sell_window_kernel");
+    // the LDS size of the run: the widest window, up to the cap (build time,
+    // so the one synchronising copy is off the SpMV path)
+    int2 *h = (int2 *)malloc((size_t)blocks * sizeof(int2));
+    if (!h)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_xwin_build: out of host memory");
+    hipError_t e = hipMemcpyAsync(h, win, (size_t)blocks * sizeof(int2), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess)
+        e = hipStreamSynchronize(st);
+    if (e != hipSuccess) {
+        free(h);
+        return fail(SPMV_PROGRAM_ERROR, "spmv_sell_xwin_build: copy windows", e);
+    }
+    const int32_t cap = bt >= 1024 ? kXwinCapWide : kXwinCapNarrow;
+    int32_t need = 0;
+    for (int64_t b = 0; b < blocks; ++b) {
+        const int64_t span = (int64_t)h[b].y - h[b].x + 1;
+        if (span <= cap && span > need)
+            need = (int32_t)span;
+    }
+    free(h);
+    *xcap = need;
+    return SPMV_SUCCESS;
+}
+
+extern "C" int spmv_sell_run_xwin(spmv_dims d, int32_t C, int32_t sigma, int32_t ki, int64_t n_slices,
+                                  const int64_t *slice_ptr, const int32_t *perm, const int32_t *col,
+                                  const double *val, const double *x, double *y, const void *win,
+                                  int32_t xcap)
+{
+    int rc = sell_check_args(d, C, sigma, ki, n_slices, "spmv_sell_run_xwin");
+    if (rc != SPMV_SUCCESS)
+        return rc;
+    if (d.n_rows == 0 || n_slices == 0)
+        return SPMV_SUCCESS;
+    if (!win || xcap < 0 || xcap > kXwinCapWide)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_run_xwin: bad window arguments");
+    SPMV_GUARD(d);
+    int bt;
+    int64_t blocks;
+    sell_geometry(C, sigma, n_slices, &bt, &blocks);
+    if (blocks > INT32_MAX)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_run_xwin: grid too large");
+    const bool nt = stream_nt(kSellStreamNtDefault);
+    auto kern = ki == 2 ? (nt ? sell_xwin_kernel<2, true, 4> : sell_xwin_kernel<2, false, 4>)
+                        : (nt ? sell_xwin_kernel<1, true, 4> : sell_xwin_kernel<1, false, 4>);
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(bt), (size_t)xcap * sizeof(double),
+                       (hipStream_t)d.stream, C, n_slices, slice_ptr, perm, col, val, x, y,
+                       (const int2 *)win, xcap);
+    SPMV_CHECK_LAUNCH("sell_xwin_kernel");
     return SPMV_SUCCESS;
 }
 

@@ -279,6 +279,17 @@ int spmv_sell_fill(int64_t n_rows, const int64_t *row_ptr, const int32_t *col,
     for (int64_t s = 0; s < n_slices; ++s) {
         int64_t base = slice_ptr[s];
         int64_t w = (slice_ptr[s + 1] - base) / C;
+        /* padding of an empty (or missing) row points at a column some row
+         * of this slice really reads, so a slice's columns stay a tight
+         * window (the x-window kernels stage that window in LDS) */
+        int32_t slice_col = 0;
+        for (int64_t r = 0; r < C; ++r) {
+            int32_t row = perm[s * C + r];
+            if (row >= 0 && row_ptr[row + 1] > row_ptr[row]) {
+                slice_col = col[row_ptr[row]];
+                break;
+            }
+        }
         for (int64_t r = 0; r < C; ++r) {
             int32_t row = perm[s * C + r];
             int64_t b = 0, e = 0;
@@ -286,7 +297,7 @@ int spmv_sell_fill(int64_t n_rows, const int64_t *row_ptr, const int32_t *col,
                 b = row_ptr[row];
                 e = row_ptr[row + 1];
             }
-            int32_t pad_col = e > b ? col[e - 1] : 0;
+            int32_t pad_col = e > b ? col[e - 1] : slice_col;
             for (int64_t k = 0; k < w; ++k) {
                 int64_t pos = base + (k / ki) * (int64_t)C * ki + r * ki + (k % ki);
                 if (b + k < e) {

@@ -85,6 +85,11 @@ HIP_SYMBOLS = {
     "spmv_csr_run_tiled": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t]),
     "spmv_csr16_run": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_int]),
     "spmv_ell_run": (ctypes.c_int, [Dims, _c_i32, _c_i64, _c_i32, _vp, _vp, _vp, _vp]),
+    "spmv_sell_xwin_bytes": (ctypes.c_size_t, [_c_i64, _c_i32, _c_i32]),
+    "spmv_sell_xwin_build": (ctypes.c_int, [Dims, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, ctypes.c_size_t,
+                                            ctypes.POINTER(_c_i32)]),
+    "spmv_sell_run_xwin": (ctypes.c_int, [Dims, _c_i32, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp,
+                                          _vp, _c_i32]),
     "spmv_sell_run": (ctypes.c_int, [Dims, _c_i32, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "spmv_cmrs_run": (ctypes.c_int, [Dims, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "spmv_gen_banded_device": (ctypes.c_int, [_c_i64, ctypes.c_uint64, _c_i64, _c_i64, ctypes.c_int, _c_i32,
@@ -458,6 +463,10 @@ class DeviceMatrix:
                                     _ptr(a["col_esc"]), _ptr(a["val"]), _ptr(x), _ptr(y), p["lanes"])
         elif self.fmt == "ell":
             rc = lib.spmv_ell_run(d, p["K"], p["ld"], p["ki"], _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y))
+        elif self.fmt == "sell" and "win" in a:
+            rc = lib.spmv_sell_run_xwin(d, p["C"], p["sigma"], p["ki"], p["n_slices"], _ptr(a["slice_ptr"]),
+                                        _ptr(a["perm"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
+                                        _ptr(a["win"]), p["xcap"])
         elif self.fmt == "sell":
             rc = lib.spmv_sell_run(d, p["C"], p["sigma"], p["ki"], p["n_slices"], _ptr(a["slice_ptr"]), _ptr(a["perm"]),
                                    _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y))
@@ -469,9 +478,25 @@ class DeviceMatrix:
         _check(rc, f"spmv_{self.fmt}_run")
 
 
+def _sell_xwin(dm: DeviceMatrix) -> None:
+    """Per-workgroup column windows for the x-window SELL kernel (device
+    pass over col; xcap = LDS entries the run stages, 0 = none fits)."""
+    torch = _torch()
+    p, a = dm.params, dm.arrays
+    nbytes = hip_lib().spmv_sell_xwin_bytes(p["n_slices"], p["C"], p["sigma"])
+    a["win"] = torch.empty(max(nbytes, 8), dtype=torch.uint8, device=dm.device)
+    cap = _c_i32(0)
+    _check(hip_lib().spmv_sell_xwin_build(dm.dims(), p["C"], p["sigma"], p["n_slices"], _ptr(a["slice_ptr"]),
+                                          _ptr(a["col"]), _ptr(a["win"]), a["win"].numel(), ctypes.byref(cap)),
+           "spmv_sell_xwin_build")
+    p["xcap"] = cap.value
+
+
 def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int = 0, ki: int = 0, C: int = 64,
-              sigma: int = 1024, h: int = 8, ell_max_padding: float | None = 64.0) -> DeviceMatrix:
-    """Build `fmt` on the host (libspmv_host.so) and upload it."""
+              sigma: int = 1024, h: int = 8, ell_max_padding: float | None = 64.0,
+              xwin: bool = False) -> DeviceMatrix:
+    """Build `fmt` on the host (libspmv_host.so) and upload it.  xwin (SELL):
+    also build the per-workgroup x windows and run the LDS-window kernel."""
     torch = _torch()
     device = torch.device(device)
     dm = DeviceMatrix(fmt, m.n_rows, m.n_cols, m.nnz, device)
@@ -514,6 +539,8 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
         dm.arrays = dict(slice_ptr=_dev_tensor(s["slice_ptr"], device), perm=_dev_tensor(s["perm"], device),
                          col=_dev_tensor(s["col"], device), val=_dev_tensor(s["val"], device))
         dm.stored_bytes = 12 * s["stored"] + 8 * (s["n_slices"] + 1) + 4 * s["n_slices"] * C
+        if xwin:
+            _sell_xwin(dm)
     elif fmt == "cmrs":
         c = cmrs_build(m.n_rows, ptr, h=h)
         dm.params = dict(h=h, n_strips=c["n_strips"])

@@ -42,6 +42,8 @@ FMT_PARAMS = [
     ("ell", {"ki": 1}),
     ("ell", {"ki": 2}),
     ("sell", {"C": 64, "sigma": 1024, "ki": 2}),
+    ("sell", {"C": 64, "sigma": 1024, "ki": 1, "xwin": True}),
+    ("sell", {"C": 32, "sigma": 64, "ki": 2, "xwin": True}),
     ("sell", {"C": 64, "sigma": 1, "ki": 1}),
     ("sell", {"C": 32, "sigma": 1, "ki": 1}),
     ("sell", {"C": 128, "sigma": 256, "ki": 2}),
@@ -344,3 +346,35 @@ def test_device_banded_generator_matches_host(torch_dev, layout):
     torch.cuda.synchronize()
     m = sa.Coo(hi - lo, n, np.repeat(np.arange(hi - lo, dtype=np.int32), 16), col, val)
     assert_parity(m, y.cpu().numpy(), np.arange(n, dtype=np.float64))
+
+
+@pytest.mark.parametrize("case", ["cantlike", "rmat", "ragged", "banded"])
+@pytest.mark.parametrize("ki", [1, 2])
+def test_sell_xwin_bit_identical(torch_dev, case, ki):
+    """The LDS x-window kernel reads the same x values in the same order as
+    the global-gather kernel; workgroups whose window does not fit fall back
+    to global gathers (R-MAT: all of them)."""
+    torch, dev = torch_dev
+    if case == "cantlike":
+        m = sa.gen_cantlike(0, copies=16)  # >= 512 windows: 1024-slot workgroups
+    elif case == "rmat":
+        m = sa.gen_rmat(1_000_000, 10_000_000, scale=20, seed=1)
+    elif case == "ragged":
+        m = sa.gen_random(20_000, 20_000, 0, 700, seed=21)
+    else:
+        n = 600_000
+        ptr, col, val = sa.gen_banded_csr(n, 0, n)
+        row = np.repeat(np.arange(n, dtype=np.int32), np.diff(ptr))
+        m = sa.Coo(n, n, row, col, val, False, "banded")
+    x = torch.from_numpy(np.random.default_rng(8).uniform(-1, 1, m.n_cols)).to(dev)
+    ys = []
+    for xw in (False, True):
+        dm = sa.to_device(m, "sell", dev, C=64, sigma=1024, ki=ki, xwin=xw)
+        y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
+        dm.run(x, y)
+        ys.append(y)
+        if xw and case in ("cantlike", "banded"):
+            assert dm.params["xcap"] > 0
+    torch.cuda.synchronize()
+    assert torch.equal(ys[0].view(torch.int64), ys[1].view(torch.int64))
+    assert_parity(m, ys[1].cpu().numpy(), x.cpu().numpy())

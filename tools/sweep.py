@@ -34,19 +34,14 @@ VARIANTS = [
     ("cmrs", {"h": 8}), ("cmrs", {"h": 16}), ("cmrs", {"h": 32}),
     ("coo", {}),
     ("csr16", {"lanes": 4}), ("csr16", {"lanes": 2}), ("csr16", {"lanes": 8}),
-    # load policy of the streamed arrays (SPMV_STREAM_NT), groups in flight (SPMV_SLOT_UNROLL)
-    ("csr", {"lanes": 4, "variant": 3, "env": {"SPMV_STREAM_NT": "0"}}),
-    ("csr", {"lanes": 4, "variant": 3, "env": {"SPMV_STREAM_NT": "1"}}),
-    ("csr", {"lanes": 4, "variant": 5, "env": {"SPMV_STREAM_NT": "1"}}),
-    ("sell", {"C": 64, "sigma": 1024, "ki": 1, "env": {"SPMV_STREAM_NT": "0"}}),
+    # SELL x window in LDS (xwin) vs global gathers
     ("sell", {"C": 64, "sigma": 1024, "ki": 1, "env": {"SPMV_STREAM_NT": "1"}}),
-    ("sell", {"C": 64, "sigma": 1024, "ki": 1, "env": {"SPMV_STREAM_NT": "1", "SPMV_SLOT_UNROLL": "8"}}),
-    ("sell", {"C": 64, "sigma": 1024, "ki": 2, "env": {"SPMV_STREAM_NT": "1"}}),
-    ("sell", {"C": 64, "sigma": 1024, "ki": 2, "env": {"SPMV_STREAM_NT": "1", "SPMV_SLOT_UNROLL": "8"}}),
-    ("ell", {"ki": 2, "env": {"SPMV_STREAM_NT": "0"}}),
-    ("ell", {"ki": 2, "env": {"SPMV_STREAM_NT": "1"}}),
-    ("ell", {"ki": 2, "env": {"SPMV_STREAM_NT": "1", "SPMV_SLOT_UNROLL": "8"}}),
-    ("ell", {"ki": 1, "env": {"SPMV_STREAM_NT": "1", "SPMV_SLOT_UNROLL": "8"}}),
+    ("sell", {"C": 64, "sigma": 1024, "ki": 1, "xwin": True, "env": {"SPMV_STREAM_NT": "1"}}),
+    ("sell", {"C": 64, "sigma": 1024, "ki": 1, "xwin": True, "env": {"SPMV_STREAM_NT": "0"}}),
+    ("sell", {"C": 64, "sigma": 1024, "ki": 2, "xwin": True, "env": {"SPMV_STREAM_NT": "1"}}),
+    ("sell", {"C": 64, "sigma": 512, "ki": 1, "xwin": True, "env": {"SPMV_STREAM_NT": "1"}}),
+    ("sell", {"C": 64, "sigma": 256, "ki": 1, "xwin": True, "env": {"SPMV_STREAM_NT": "1"}}),
+    ("csr", {"lanes": 4, "variant": 3, "env": {"SPMV_CSR_BATCH": "0"}}),
 ]
 
 

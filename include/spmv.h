@@ -83,6 +83,18 @@ int spmv_csr_run_variant(spmv_dims d, const int64_t *row_ptr,
                          const int32_t *col, const double *val,
                          const double *x, double *y, int lanes_per_row,
                          int variant);
+/* CSR with each row group's x window staged in LDS (the default staged
+ * kernel, variant 3, whose gathers read LDS instead of global memory).
+ * Build once: spmv_csr_xwin_build scans col (device) for the column range
+ * of every group of 256/L rows (L = lanes_per_row, 0 = auto; the run must
+ * use the same L) into `win` (spmv_csr_xwin_bytes bytes) and returns in
+ * *xcap the LDS entries the run stages (0: no window fits).  y is
+ * bit-identical to spmv_csr_run_variant(..., L, 3).                     */
+size_t spmv_csr_xwin_bytes(int64_t n_rows, int64_t nnz, int lanes_per_row);
+int spmv_csr_xwin_build(spmv_dims d, const int64_t *row_ptr, const int32_t *col, int lanes_per_row,
+                        void *win, size_t win_bytes, int32_t *xcap);
+int spmv_csr_run_xwin(spmv_dims d, const int64_t *row_ptr, const int32_t *col, const double *val,
+                      const double *x, double *y, int lanes_per_row, const void *win, int32_t xcap);
 /* CSR with compressed 16-bit column indices (arrays
  * from spmv_csr16_plan/fill in spmv_host.h): 10.06 instead of 12 bytes per
  * entry when 64-entry blocks of columns span < 65536 (banded / FEM
@@ -112,6 +124,13 @@ int spmv_csr_run_tiled(spmv_dims d, const int64_t *row_ptr, const int32_t *col,
 int spmv_ell_run(spmv_dims d, int32_t K, int64_t ld, int32_t ki,
                  const int32_t *col, const double *val, const double *x,
                  double *y);
+/* ELL with each 256-row workgroup's x window staged in LDS (see
+ * spmv_sell_xwin_build for the protocol); y bit-identical to spmv_ell_run. */
+size_t spmv_ell_xwin_bytes(int64_t n_rows);
+int spmv_ell_xwin_build(spmv_dims d, int32_t K, int64_t ld, int32_t ki, const int32_t *col,
+                        void *win, size_t win_bytes, int32_t *xcap);
+int spmv_ell_run_xwin(spmv_dims d, int32_t K, int64_t ld, int32_t ki, const int32_t *col,
+                      const double *val, const double *x, double *y, const void *win, int32_t xcap);
 
 /* -------------------------------------------------------- SELL-C-sigma ---
  * Replaces kernel `sigma_c(val,idx,x,y,slice_ptr,int C)` (reference

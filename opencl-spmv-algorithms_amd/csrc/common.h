@@ -99,6 +99,59 @@ __device__ __forceinline__ int2 stream_load2(const int32_t *p)
 // so a sweep can flip it inside one process.
 bool stream_nt(bool dflt);
 
+// Where x[c] comes from: global memory (XGlobal) or the workgroup's
+// window x[lo..hi] staged in LDS (XWindow: the x-window kernels).
+struct XGlobal {
+    const double *__restrict__ x;
+    __device__ __forceinline__ double operator()(int32_t c) const { return x[c]; }
+};
+
+struct XWindow {
+    const double *s;  // LDS
+    int32_t lo;
+    __device__ __forceinline__ double operator()(int32_t c) const { return s[c - lo]; }
+};
+
+// [min, max] of col[e0..e1) over one 256-thread workgroup ({0, -1} when
+// empty); the result is valid in thread 0.  Build-time pass of the
+// x-window kernels.
+__device__ __forceinline__ int2 block_minmax(int lo, int hi);
+
+__device__ __forceinline__ int2 block_col_range(const int32_t *__restrict__ col, int64_t e0, int64_t e1)
+{
+    int lo = INT32_MAX, hi = INT32_MIN;
+    for (int64_t e = e0 + threadIdx.x; e < e1; e += kBlock) {
+        const int c = col[e];
+        lo = c < lo ? c : lo;
+        hi = c > hi ? c : hi;
+    }
+    return block_minmax(lo, hi);
+}
+
+// workgroup-wide [min lo, max hi] of per-thread partials (valid in thread 0)
+__device__ __forceinline__ int2 block_minmax(int lo, int hi)
+{
+    __shared__ int s_lo[kBlock / kWave], s_hi[kBlock / kWave];
+#pragma unroll
+    for (int off = kWave / 2; off > 0; off >>= 1) {
+        const int l2 = __shfl_xor(lo, off), h2 = __shfl_xor(hi, off);
+        lo = l2 < lo ? l2 : lo;
+        hi = h2 > hi ? h2 : hi;
+    }
+    if (threadIdx.x % kWave == 0) {
+        s_lo[threadIdx.x / kWave] = lo;
+        s_hi[threadIdx.x / kWave] = hi;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kBlock / kWave; ++w) {
+            lo = s_lo[w] < lo ? s_lo[w] : lo;
+            hi = s_hi[w] > hi ? s_hi[w] : hi;
+        }
+    }
+    return lo <= hi ? int2{lo, hi} : int2{0, -1};
+}
+
 template <int W>
 __device__ __forceinline__ double group_sum(double v)
 {

@@ -17,6 +17,41 @@
 
 namespace spmv {
 
+// One L-lane group's row [beg, end) with 16-byte pair loads: the lane
+// reads the aligned pair (p, p+1); entries of the pair outside [beg, end)
+// are zeroed by value (their column is a valid neighbour column, so the
+// gather stays in bounds).  The last pair of the row is loaded as a
+// scalar when p+1 == end, so nothing past val[nnz-1] is ever read.
+template <int L, typename XS>
+__device__ __forceinline__ double row_dot_pairs(int64_t beg, int64_t end, int lane,
+                                                const int32_t *__restrict__ col,
+                                                const double *__restrict__ val, const XS &xs)
+{
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    int64_t p = (beg & ~(int64_t)1) + 2 * lane;
+    for (; p + 1 + 2 * L < end; p += 4 * L) {
+        const double2 va = *reinterpret_cast<const double2 *>(val + p);
+        const int2 ca = *reinterpret_cast<const int2 *>(col + p);
+        const double2 vb = *reinterpret_cast<const double2 *>(val + p + 2 * L);
+        const int2 cb = *reinterpret_cast<const int2 *>(col + p + 2 * L);
+        s0 += (p >= beg ? va.x : 0.0) * xs(ca.x);
+        s1 += va.y * xs(ca.y);
+        s2 += vb.x * xs(cb.x);
+        s3 += vb.y * xs(cb.y);
+    }
+    for (; p < end; p += 2 * L) {
+        if (p + 1 < end) {
+            const double2 va = *reinterpret_cast<const double2 *>(val + p);
+            const int2 ca = *reinterpret_cast<const int2 *>(col + p);
+            s0 += (p >= beg ? va.x : 0.0) * xs(ca.x);
+            s1 += va.y * xs(ca.y);
+        } else if (p >= beg) {
+            s0 += val[p] * xs(col[p]);
+        }
+    }
+    return group_sum<L>((s0 + s1) + (s2 + s3));
+}
+
 template <int L, bool PAIR>
 __global__ __launch_bounds__(kBlock) void csr_vector_kernel(
     int64_t n_rows, const int64_t *__restrict__ row_ptr,
@@ -38,39 +73,13 @@ __global__ __launch_bounds__(kBlock) void csr_vector_kernel(
     const int64_t row = row0 + g;
     const int64_t beg = s_ptr[g], end = s_ptr[g + 1];  // empty past n_rows
 
-    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
     if constexpr (PAIR) {
-        // 16-byte loads: lane reads the aligned pair (p, p+1); entries of
-        // the pair outside [beg, end) are zeroed by value (their column is
-        // a valid neighbour column, so the gather stays in bounds).  The
-        // last pair of the row is loaded as a scalar when p+1 == end, so
-        // nothing past val[nnz-1] is ever read.
-        int64_t p = (beg & ~(int64_t)1) + 2 * lane;
-        for (; p + 1 + 2 * L < end; p += 4 * L) {
-            const double2 va = *reinterpret_cast<const double2 *>(val + p);
-            const int2 ca = *reinterpret_cast<const int2 *>(col + p);
-            const double2 vb = *reinterpret_cast<const double2 *>(val + p + 2 * L);
-            const int2 cb = *reinterpret_cast<const int2 *>(col + p + 2 * L);
-            s0 += (p >= beg ? va.x : 0.0) * x[ca.x];
-            s1 += va.y * x[ca.y];
-            s2 += vb.x * x[cb.x];
-            s3 += vb.y * x[cb.y];
-        }
-        for (; p < end; p += 2 * L) {
-            if (p + 1 < end) {
-                const double2 va = *reinterpret_cast<const double2 *>(val + p);
-                const int2 ca = *reinterpret_cast<const int2 *>(col + p);
-                s0 += (p >= beg ? va.x : 0.0) * x[ca.x];
-                s1 += va.y * x[ca.y];
-            } else if (p >= beg) {
-                s0 += val[p] * x[col[p]];
-            }
-        }
-        double sum = group_sum<L>((s0 + s1) + (s2 + s3));
+        const double sum = row_dot_pairs<L>(beg, end, lane, col, val, XGlobal{x});
         if (lane == 0 && row < n_rows)
             y[row] = sum;
         return;
     }
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
     int64_t j = beg + lane;
     for (; j + 3 * L < end; j += 4 * L) {
         const int32_t c0 = col[j], c1 = col[j + L], c2 = col[j + 2 * L],
@@ -85,6 +94,40 @@ __global__ __launch_bounds__(kBlock) void csr_vector_kernel(
     for (; j < end; j += L)
         s0 += val[j] * x[col[j]];
     double sum = group_sum<L>((s0 + s1) + (s2 + s3));
+    if (lane == 0 && row < n_rows)
+        y[row] = sum;
+}
+
+// CSR-vector (direct: every L-lane group walks its own row) with the
+// workgroup's x window staged in LDS first; windows from
+// spmv_csr_xwin_build (one per 256/L rows = one per workgroup here).
+template <int L>
+__global__ __launch_bounds__(kBlock) void csr_vector_xwin_kernel(
+    int64_t n_rows, const int64_t *__restrict__ row_ptr,
+    const int32_t *__restrict__ col, const double *__restrict__ val,
+    const double *__restrict__ x, double *__restrict__ y, const int2 *__restrict__ win, int32_t xcap)
+{
+    constexpr int RPB = kBlock / L;
+    extern __shared__ double s_x[];
+    __shared__ int64_t s_ptr[RPB + 1];
+    const int64_t row0 = (int64_t)blockIdx.x * RPB;
+    if (threadIdx.x <= RPB) {
+        const int64_t r = row0 + threadIdx.x;
+        s_ptr[threadIdx.x] = row_ptr[r < n_rows ? r : n_rows];
+    }
+    const int2 wnd = win[blockIdx.x];
+    const int32_t span = wnd.y - wnd.x + 1;
+    const bool staged = span > 0 && span <= xcap;  // uniform per workgroup
+    if (staged)
+        for (int32_t i = threadIdx.x; i < span; i += kBlock)
+            s_x[i] = x[wnd.x + i];
+    __syncthreads();
+    const int g = threadIdx.x / L;
+    const int lane = threadIdx.x % L;
+    const int64_t row = row0 + g;
+    const int64_t beg = s_ptr[g], end = s_ptr[g + 1];
+    const double sum = staged ? row_dot_pairs<L>(beg, end, lane, col, val, XWindow{s_x, wnd.x})
+                              : row_dot_pairs<L>(beg, end, lane, col, val, XGlobal{x});
     if (lane == 0 && row < n_rows)
         y[row] = sum;
 }
@@ -104,6 +147,9 @@ constexpr int kStageRoundsDefault = 4;  // pairs per lane per chunk: 2048 produc
 // (16 KiB keeps 8 workgroups = 32 waves per CU; 20 KiB (R = 5) capped the
 // CU at 7 and measured slower, R = 8 at 4 and much slower)
 constexpr bool kCsrStreamNtDefault = false;  // SPMV_STREAM_NT overrides
+// the x-window kernel (x gathers from LDS) streams faster non-temporal:
+// 0.2991 vs 0.3077 ms on the cant-like batch
+constexpr bool kCsrXwinNtDefault = true;
 // Stage load schedule (SPMV_CSR_BATCH overrides): 0 = per-round guarded
 // loads measured 0.313 ms against 0.350 ms for loads + gathers batched
 // (mode 2: 76 VGPRs, 6 waves/SIMD) on the cant-like batch.
@@ -160,10 +206,10 @@ struct Col16 {
 // GATHERS_TOGETHER: also issue all 2R x gathers before the first product
 // (more loads in flight per wave, more VGPRs, lower occupancy) instead of
 // gathering round by round.
-template <int R, bool NT, bool GATHERS_TOGETHER, typename Cols>
+template <int R, bool NT, bool GATHERS_TOGETHER, typename Cols, typename XS>
 __device__ __forceinline__ void stage_products(int64_t cb, int64_t ce, int64_t nz, const Cols &cols,
-                                               const double *__restrict__ val,
-                                               const double *__restrict__ x, double2 *s_prod)
+                                               const double *__restrict__ val, const XS &xs,
+                                               double2 *s_prod)
 {
     double2 v[R];
     int2 c[R];
@@ -186,30 +232,48 @@ __device__ __forceinline__ void stage_products(int64_t cb, int64_t ce, int64_t n
         double2 xv[R];
 #pragma unroll
         for (int k = 0; k < R; ++k)  // all 2R gathers in flight together
-            xv[k] = double2{x[c[k].x], x[c[k].y]};
+            xv[k] = double2{xs(c[k].x), xs(c[k].y)};
 #pragma unroll
         for (int k = 0; k < R; ++k)
             s_prod[threadIdx.x + k * kBlock] = double2{v[k].x * xv[k].x, v[k].y * xv[k].y};
     } else {
 #pragma unroll
         for (int k = 0; k < R; ++k)
-            s_prod[threadIdx.x + k * kBlock] = double2{v[k].x * x[c[k].x], v[k].y * x[c[k].y]};
+            s_prod[threadIdx.x + k * kBlock] = double2{v[k].x * xs(c[k].x), v[k].y * xs(c[k].y)};
     }
     // the array's odd last entry (at most one lane of one chunk)
     const int64_t tail = nz - 1 - cb;
     if ((nz & 1) && nz - 1 < ce && tail >= 0 && tail < 2 * R * kBlock && (tail >> 1) % kBlock == threadIdx.x) {
         const int64_t p = nz - 1;
-        s_prod[tail >> 1].x = stream_load<NT>(val + p) * x[cols.one(p)];
+        s_prod[tail >> 1].x = stream_load<NT>(val + p) * xs(cols.one(p));
     }
 }
 
 // BATCH: 0 = per-round guarded loads, 1 = stream loads batched (gathers
 // per round), 2 = stream loads and gathers batched (stage_products)
-template <int L, int R, bool NT, typename Cols = Col32<NT>, int BATCH = 0>
+// One lane's share of a row's products in the staged chunk: entries
+// [lo, hi) of the chunk (chunk-relative, < 2^31), every L-th from lo+lane,
+// two partial sums so consecutive LDS reads do not wait on each other.
+template <int L>
+__device__ __forceinline__ double slice_sum(const double *prod, int64_t lo64, int64_t hi64, int lane)
+{
+    const int lo = (int)lo64, hi = (int)hi64;
+    double a0 = 0.0, a1 = 0.0;
+    int j = lo + lane;
+    for (; j + L < hi; j += 2 * L) {
+        a0 += prod[j];
+        a1 += prod[j + L];
+    }
+    if (j < hi)
+        a0 += prod[j];
+    return a0 + a1;
+}
+
+template <int L, int R, bool NT, typename Cols = Col32<NT>, int BATCH = 0, typename XS = XGlobal>
 __device__ __forceinline__ void staged_group(
     int64_t row, const int64_t *s_ptr, double2 *s_prod,
     const Cols cols, const double *__restrict__ val,
-    const double *__restrict__ x, double *__restrict__ y, int64_t n_rows, int64_t nz)
+    const XS xs, double *__restrict__ y, int64_t n_rows, int64_t nz)
 {
     constexpr int RPB = kBlock / L;
     constexpr int CH = 2 * kBlock * R;  // products per chunk
@@ -225,7 +289,7 @@ __device__ __forceinline__ void staged_group(
     for (int64_t cb = s_ptr[0] & ~(int64_t)1; cb < blk_end; cb += CH) {
         const int64_t ce = cb + CH < blk_end ? cb + CH : blk_end;
         if constexpr (BATCH > 0) {
-            stage_products<R, NT, BATCH == 2>(cb, ce, nz, cols, val, x, s_prod);
+            stage_products<R, NT, BATCH == 2>(cb, ce, nz, cols, val, xs, s_prod);
         } else {  // per-round guarded loads
 #pragma unroll
             for (int k = 0; k < R; ++k) {
@@ -235,19 +299,16 @@ __device__ __forceinline__ void staged_group(
                 if (p + 1 < ce) {
                     const double2 v = stream_load2<NT>(val + p);
                     const int2 c = cols.pair(p);
-                    pr.x = v.x * x[c.x];
-                    pr.y = v.y * x[c.y];
+                    pr.x = v.x * xs(c.x);
+                    pr.y = v.y * xs(c.y);
                 } else if (p < ce) {
-                    pr.x = stream_load<NT>(val + p) * x[cols.one(p)];
+                    pr.x = stream_load<NT>(val + p) * xs(cols.one(p));
                 }
                 s_prod[t] = pr;
             }
         }
         __syncthreads();
-        const int64_t lo = beg > cb ? beg : cb;
-        const int64_t hi = end < ce ? end : ce;
-        for (int64_t j = lo + lane; j < hi; j += L)
-            acc += prod[j - cb];
+        acc += slice_sum<L>(prod, beg > cb ? beg - cb : 0, (end < ce ? end : ce) - cb, lane);
         __syncthreads();
     }
     acc = group_sum<L>(acc);
@@ -272,7 +333,7 @@ __global__ __launch_bounds__(kBlock) void csr_staged_kernel(
         s_ptr[threadIdx.x] = row_ptr[r < n_rows ? r : n_rows];
     }
     __syncthreads();
-    staged_group<L, R, false>(row0 + threadIdx.x / L, s_ptr, s_prod, Col32<false>{col}, val, x, y, n_rows,
+    staged_group<L, R, false>(row0 + threadIdx.x / L, s_ptr, s_prod, Col32<false>{col}, val, XGlobal{x}, y, n_rows,
                               row_ptr[n_rows]);
 }
 
@@ -306,8 +367,75 @@ __global__ __launch_bounds__(kBlock) void csr_staged_persistent_kernel(
             int64_t r = g2 * RPB + threadIdx.x;
             next = row_ptr[r < n_rows ? r : n_rows];
         }
-        staged_group<L, R, NT, Cols, BATCH>(grp * RPB + threadIdx.x / L, s_ptr, s_prod, cols, val, x, y, n_rows,
+        staged_group<L, R, NT, Cols, BATCH>(grp * RPB + threadIdx.x / L, s_ptr, s_prod, cols, val, XGlobal{x}, y, n_rows,
                                             nz);
+    }
+}
+
+// Column window of every row group (RPB rows): [min, max] column of its
+// entry range (one pass over col, build time).
+__global__ __launch_bounds__(kBlock) void csr_window_kernel(int64_t n_rows, int64_t rpb,
+                                                            const int64_t *__restrict__ row_ptr,
+                                                            const int32_t *__restrict__ col,
+                                                            int2 *__restrict__ win)
+{
+    const int64_t g = blockIdx.x;
+    const int64_t r1 = (g + 1) * rpb < n_rows ? (g + 1) * rpb : n_rows;
+    const int2 r = block_col_range(col, row_ptr[g * rpb], row_ptr[r1]);
+    if (threadIdx.x == 0)
+        win[g] = r;
+}
+
+// The persistent staged kernel with each row group's x window
+// x[win.x .. win.y] copied into LDS (dynamic, xcap entries) when the group
+// starts: the products then gather from LDS instead of global memory, the
+// limiter of the staged kernel (TA busy, requests well below the DRAM
+// credit limit: profiles/round1/pmc_stalls.json).  A group whose window
+// exceeds xcap gathers from global memory.  Same products, same order:
+// y is bit-identical to variant 3.
+template <int L, int R, bool NT>
+__global__ __launch_bounds__(kBlock) void csr_xwin_kernel(
+    int64_t n_rows, int64_t n_groups, const int64_t *__restrict__ row_ptr,
+    const int32_t *__restrict__ col, const double *__restrict__ val,
+    const double *__restrict__ x, double *__restrict__ y, const int2 *__restrict__ win, int32_t xcap)
+{
+    constexpr int RPB = kBlock / L;
+    extern __shared__ double s_x[];
+    __shared__ int64_t s_ptr[RPB + 1];
+    __shared__ double2 s_prod[kBlock * R];
+    const int64_t nz = row_ptr[n_rows];
+    int64_t grp = blockIdx.x;
+    int64_t next = 0;
+    if (threadIdx.x <= RPB) {
+        const int64_t r = grp * RPB + threadIdx.x;
+        next = row_ptr[r < n_rows ? r : n_rows];
+    }
+    int2 wnext = grp < n_groups ? win[grp] : int2{0, -1};
+    for (; grp < n_groups; grp += gridDim.x) {
+        if (threadIdx.x <= RPB)
+            s_ptr[threadIdx.x] = next;
+        const int2 wnd = wnext;
+        const int32_t span = wnd.y - wnd.x + 1;
+        const bool staged = span > 0 && span <= xcap;  // uniform per workgroup
+        if (staged)
+            for (int32_t i = threadIdx.x; i < span; i += kBlock)
+                s_x[i] = x[wnd.x + i];
+        __syncthreads();
+        const int64_t g2 = grp + gridDim.x;
+        if (g2 < n_groups) {
+            if (threadIdx.x <= RPB) {
+                const int64_t r = g2 * RPB + threadIdx.x;
+                next = row_ptr[r < n_rows ? r : n_rows];
+            }
+            wnext = win[g2];
+        }
+        const int64_t row = grp * RPB + threadIdx.x / L;
+        if (staged)
+            staged_group<L, R, NT, Col32<NT>, 0, XWindow>(row, s_ptr, s_prod, Col32<NT>{col}, val,
+                                                          XWindow{s_x, wnd.x}, y, n_rows, nz);
+        else
+            staged_group<L, R, NT, Col32<NT>, 0, XGlobal>(row, s_ptr, s_prod, Col32<NT>{col}, val, XGlobal{x},
+                                                          y, n_rows, nz);
     }
 }
 
@@ -429,10 +557,7 @@ __global__ __launch_bounds__(kBlock) void csr_pipelined_kernel(
         }
         if (ngrp < n_groups)
             regs.issue(col, val, ncb, nce);
-        const int64_t lo = beg > cb ? beg : cb;
-        const int64_t hi = end < ce ? end : ce;
-        for (int64_t j = lo + lane; j < hi; j += L)
-            acc += prod[j - cb];
+        acc += slice_sum<L>(prod, beg > cb ? beg - cb : 0, (end < ce ? end : ce) - cb, lane);
         if (last) {
             acc = group_sum<L>(acc);
             const int64_t row = grp * RPB + g;
@@ -499,10 +624,10 @@ static int cu_count()
 // the grid by hand once launched 8 per CU of a kernel that fit only 7,
 // and the 256 stragglers ran as a second wave.
 template <typename K>
-static int64_t persistent_grid(K kernel, int64_t groups)
+static int64_t persistent_grid(K kernel, int64_t groups, size_t dyn_lds = 0)
 {
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, dyn_lds) != hipSuccess ||
         per_cu <= 0)
         per_cu = 1;
     if (per_cu > 8)
@@ -670,6 +795,129 @@ extern "C" int spmv_csr_run(spmv_dims d, const int64_t *row_ptr,
                             const double *x, double *y, int lanes_per_row)
 {
     return spmv_csr_run_variant(d, row_ptr, col, val, x, y, lanes_per_row, 0);
+}
+
+namespace spmv {
+
+constexpr int32_t kCsrXwinCap = 2048;  // 16 KiB of LDS: 32 KiB per workgroup with the stage
+
+template <int L, int R, bool NT>
+static void launch_csr_xwin(const spmv_dims &d, const int64_t *row_ptr, const int32_t *col,
+                            const double *val, const double *x, double *y, const int2 *win, int32_t xcap)
+{
+    constexpr int RPB = kBlock / L;
+    const int64_t groups = (d.n_rows + RPB - 1) / RPB;
+    const size_t lds = (size_t)xcap * sizeof(double);
+    const int64_t grid = persistent_grid(csr_xwin_kernel<L, R, NT>, groups, lds);
+    hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT>), dim3((unsigned)grid), dim3(kBlock), lds,
+                       (hipStream_t)d.stream, d.n_rows, groups, row_ptr, col, val, x, y, win, xcap);
+}
+
+template <int L>
+static void launch_csr_vector_xwin(const spmv_dims &d, const int64_t *row_ptr, const int32_t *col,
+                                   const double *val, const double *x, double *y, const int2 *win,
+                                   int32_t xcap)
+{
+    constexpr int RPB = kBlock / L;
+    const int64_t blocks = (d.n_rows + RPB - 1) / RPB;
+    hipLaunchKernelGGL((csr_vector_xwin_kernel<L>), dim3((unsigned)blocks), dim3(kBlock),
+                       (size_t)xcap * sizeof(double), (hipStream_t)d.stream, d.n_rows, row_ptr, col, val, x, y,
+                       win, xcap);
+}
+
+// SPMV_CSR_XWIN_DIRECT=1: the x-window run uses the direct (row-walking)
+// kernel instead of the staged one (read per call: sweep knob)
+static bool csr_xwin_direct()
+{
+    const char *s = getenv("SPMV_CSR_XWIN_DIRECT");
+    return s && s[0] == '1';
+}
+
+}  // namespace spmv
+
+extern "C" size_t spmv_csr_xwin_bytes(int64_t n_rows, int64_t nnz, int lanes_per_row)
+{
+    const int L = lanes_per_row > 0 ? lanes_per_row : spmv_csr_auto_lanes(n_rows, nnz);
+    if (L < 2 || L > 64 || (L & (L - 1)) || n_rows <= 0)
+        return 0;
+    const int64_t rpb = kBlock / L;
+    return (size_t)((n_rows + rpb - 1) / rpb) * sizeof(int2);
+}
+
+extern "C" int spmv_csr_xwin_build(spmv_dims d, const int64_t *row_ptr, const int32_t *col,
+                                   int lanes_per_row, void *win, size_t win_bytes, int32_t *xcap)
+{
+    if (d.n_rows < 0 || d.nnz < 0 || !xcap)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_xwin_build: bad arguments");
+    *xcap = 0;
+    if (d.n_rows == 0)
+        return SPMV_SUCCESS;
+    const int L = lanes_per_row > 0 ? lanes_per_row : spmv_csr_auto_lanes(d.n_rows, d.nnz);
+    const size_t need = spmv_csr_xwin_bytes(d.n_rows, d.nnz, L);
+    if (need == 0)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_xwin_build: lanes_per_row must be 0 or a power of two in [2,64]");
+    if (!win || win_bytes < need)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_xwin_build: window buffer too small");
+    SPMV_GUARD(d);
+    const int64_t rpb = kBlock / L;
+    const int64_t groups = (d.n_rows + rpb - 1) / rpb;
+    const hipStream_t st = (hipStream_t)d.stream;
+    hipLaunchKernelGGL(csr_window_kernel, dim3((unsigned)groups), dim3(kBlock), 0, st, d.n_rows, rpb, row_ptr,
+                       col, (int2 *)win);
+    SPMV_CHECK_LAUNCH("csr_window_kernel");
+    int2 *h = (int2 *)malloc(need);
+    if (!h)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_xwin_build: out of host memory");
+    hipError_t e = hipMemcpyAsync(h, win, need, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess)
+        e = hipStreamSynchronize(st);
+    if (e != hipSuccess) {
+        free(h);
+        return fail(SPMV_PROGRAM_ERROR, "spmv_csr_xwin_build: copy windows", e);
+    }
+    int32_t best = 0;
+    for (int64_t g = 0; g < groups; ++g) {
+        const int64_t span = (int64_t)h[g].y - h[g].x + 1;
+        if (span <= kCsrXwinCap && span > best)
+            best = (int32_t)span;
+    }
+    free(h);
+    *xcap = best;
+    return SPMV_SUCCESS;
+}
+
+extern "C" int spmv_csr_run_xwin(spmv_dims d, const int64_t *row_ptr, const int32_t *col, const double *val,
+                                 const double *x, double *y, int lanes_per_row, const void *win, int32_t xcap)
+{
+    if (d.n_rows < 0 || d.n_cols < 0 || d.nnz < 0)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_run_xwin: negative size");
+    if (d.n_rows == 0)
+        return SPMV_SUCCESS;
+    if (!win || xcap < 0 || xcap > kCsrXwinCap)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_run_xwin: bad window arguments");
+    SPMV_GUARD(d);
+    const int L = lanes_per_row > 0 ? lanes_per_row : spmv_csr_auto_lanes(d.n_rows, d.nnz);
+    const bool nt = stream_nt(kCsrXwinNtDefault);
+    constexpr int R = kStageRoundsDefault;
+    const int2 *w = (const int2 *)win;
+    const bool direct = csr_xwin_direct();
+#define SPMV_XWIN(LL)                                                                  \
+    (direct ? launch_csr_vector_xwin<LL>(d, row_ptr, col, val, x, y, w, xcap)          \
+     : nt   ? launch_csr_xwin<LL, R, true>(d, row_ptr, col, val, x, y, w, xcap)        \
+            : launch_csr_xwin<LL, R, false>(d, row_ptr, col, val, x, y, w, xcap))
+    switch (L) {
+    case 2: SPMV_XWIN(2); break;
+    case 4: SPMV_XWIN(4); break;
+    case 8: SPMV_XWIN(8); break;
+    case 16: SPMV_XWIN(16); break;
+    case 32: SPMV_XWIN(32); break;
+    case 64: SPMV_XWIN(64); break;
+    default:
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_run_xwin: lanes_per_row must be 0 or a power of two in [2,64]");
+    }
+#undef SPMV_XWIN
+    SPMV_CHECK_LAUNCH("csr_xwin_kernel");
+    return SPMV_SUCCESS;
 }
 
 extern "C" int spmv_csr16_run(spmv_dims d, const int64_t *row_ptr, const int32_t *blk_base,

@@ -33,19 +33,6 @@ static int slot_unroll()
     return (s && s[0] == '8') ? 8 : 4;
 }
 
-// Where x[c] comes from: global memory (XGlobal) or the workgroup's
-// window x[lo..hi] staged in LDS (XWindow, see sell_xwin_kernel).
-struct XGlobal {
-    const double *__restrict__ x;
-    __device__ __forceinline__ double operator()(int32_t c) const { return x[c]; }
-};
-
-struct XWindow {
-    const double *s;  // LDS
-    int32_t lo;
-    __device__ __forceinline__ double operator()(int32_t c) const { return s[c - lo]; }
-};
-
 template <int KI, bool NT>
 struct Step;
 
@@ -141,6 +128,54 @@ __global__ __launch_bounds__(kBlock) void ell_kernel(
     y[i] = slot_dot<KI, NT, U>(val + off, col + off, K, ld * KI, XGlobal{x});
 }
 
+// Column window of every 256-row ELL workgroup: its rows' entries of
+// k-group g are the contiguous run [g*ld*ki + b*256*ki, ... + rows*ki).
+__global__ __launch_bounds__(kBlock) void ell_window_kernel(int64_t n_rows, int32_t K, int64_t ld, int32_t ki,
+                                                            const int32_t *__restrict__ col,
+                                                            int2 *__restrict__ win)
+{
+    const int64_t r0 = (int64_t)blockIdx.x * kBlock;
+    const int64_t r1 = r0 + kBlock < n_rows ? r0 + kBlock : n_rows;
+    int lo = INT32_MAX, hi = INT32_MIN;
+    for (int32_t g = 0; g < K / ki; ++g) {
+        const int64_t base = (int64_t)g * ld * ki;
+        for (int64_t e = base + r0 * ki + threadIdx.x; e < base + r1 * ki; e += kBlock) {
+            const int c = col[e];
+            lo = c < lo ? c : lo;
+            hi = c > hi ? c : hi;
+        }
+    }
+    const int2 r = block_minmax(lo, hi);
+    if (threadIdx.x == 0)
+        win[blockIdx.x] = r;
+}
+
+// ELL with the workgroup's x window staged in LDS (as sell_xwin_kernel).
+template <int KI, bool NT, int U>
+__global__ __launch_bounds__(kBlock) void ell_xwin_kernel(
+    int64_t n_rows, int32_t K, int64_t ld, const int32_t *__restrict__ col,
+    const double *__restrict__ val, const double *__restrict__ x,
+    double *__restrict__ y, const int2 *__restrict__ win, int32_t xcap)
+{
+    extern __shared__ double s_x[];
+    const int2 wnd = win[blockIdx.x];
+    const int32_t span = wnd.y - wnd.x + 1;
+    const bool staged = span > 0 && span <= xcap;  // uniform per workgroup
+    if (staged) {
+        for (int32_t j = threadIdx.x; j < span; j += kBlock)
+            s_x[j] = x[wnd.x + j];
+        __syncthreads();
+    }
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n_rows)
+        return;
+    const int64_t off = i * KI;
+    y[i] = staged ? slot_dot<KI, NT, U>(val + off, col + off, K, ld * KI, XWindow{s_x, wnd.x})
+                  : slot_dot<KI, NT, U>(val + off, col + off, K, ld * KI, XGlobal{x});
+}
+
+constexpr int32_t kEllXwinCap = 2048;  // 16 KiB per 256-row workgroup
+
 }  // namespace spmv
 
 using namespace spmv;
@@ -196,36 +231,13 @@ __global__ __launch_bounds__(kBlock) void sell_window_kernel(int32_t C, int bt, 
                                                              const int32_t *__restrict__ col,
                                                              int2 *__restrict__ win)
 {
-    __shared__ int s_lo[kBlock / kWave], s_hi[kBlock / kWave];
     const int64_t b = blockIdx.x;
     const int64_t s0 = b * bt / C;
     int64_t s1 = ((b + 1) * bt + C - 1) / C;
     s1 = s1 < n_slices ? s1 : n_slices;
-    const int64_t e0 = slice_ptr[s0], e1 = slice_ptr[s1];
-    int lo = INT32_MAX, hi = INT32_MIN;
-    for (int64_t e = e0 + threadIdx.x; e < e1; e += kBlock) {
-        const int c = col[e];
-        lo = c < lo ? c : lo;
-        hi = c > hi ? c : hi;
-    }
-#pragma unroll
-    for (int off = kWave / 2; off > 0; off >>= 1) {
-        const int l2 = __shfl_xor(lo, off), h2 = __shfl_xor(hi, off);
-        lo = l2 < lo ? l2 : lo;
-        hi = h2 > hi ? h2 : hi;
-    }
-    if (threadIdx.x % kWave == 0) {
-        s_lo[threadIdx.x / kWave] = lo;
-        s_hi[threadIdx.x / kWave] = hi;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int w = 1; w < kBlock / kWave; ++w) {
-            lo = s_lo[w] < lo ? s_lo[w] : lo;
-            hi = s_hi[w] > hi ? s_hi[w] : hi;
-        }
-        win[b] = lo <= hi ? int2{lo, hi} : int2{0, -1};
-    }
+    const int2 r = block_col_range(col, slice_ptr[s0], slice_ptr[s1]);
+    if (threadIdx.x == 0)
+        win[b] = r;
 }
 
 // SELL with the workgroup's x window staged in LDS.  Cant-like rows of a
@@ -406,5 +418,70 @@ extern "C" int spmv_ell_run(spmv_dims d, int32_t K, int64_t ld, int32_t ki,
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock), 0, (hipStream_t)d.stream,
                        d.n_rows, K, ld, col, val, x, y, remap);
     SPMV_CHECK_LAUNCH("ell_kernel");
+    return SPMV_SUCCESS;
+}
+
+extern "C" size_t spmv_ell_xwin_bytes(int64_t n_rows)
+{
+    return n_rows > 0 ? (size_t)((n_rows + kBlock - 1) / kBlock) * sizeof(int2) : 0;
+}
+
+extern "C" int spmv_ell_xwin_build(spmv_dims d, int32_t K, int64_t ld, int32_t ki, const int32_t *col,
+                                   void *win, size_t win_bytes, int32_t *xcap)
+{
+    if (d.n_rows < 0 || K < 0 || ld < d.n_rows || ld % 64 != 0 || (ki != 1 && ki != 2) || K % ki != 0 || !xcap)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_ell_xwin_build: bad arguments");
+    *xcap = 0;
+    if (d.n_rows == 0)
+        return SPMV_SUCCESS;
+    const size_t need = spmv_ell_xwin_bytes(d.n_rows);
+    if (!win || win_bytes < need)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_ell_xwin_build: window buffer too small");
+    SPMV_GUARD(d);
+    const int64_t blocks = (d.n_rows + kBlock - 1) / kBlock;
+    const hipStream_t st = (hipStream_t)d.stream;
+    hipLaunchKernelGGL(ell_window_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, st, d.n_rows, K, ld, ki, col,
+                       (int2 *)win);
+    SPMV_CHECK_LAUNCH("ell_window_kernel");
+    int2 *h = (int2 *)malloc(need);
+    if (!h)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_ell_xwin_build: out of host memory");
+    hipError_t e = hipMemcpyAsync(h, win, need, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess)
+        e = hipStreamSynchronize(st);
+    if (e != hipSuccess) {
+        free(h);
+        return fail(SPMV_PROGRAM_ERROR, "spmv_ell_xwin_build: copy windows", e);
+    }
+    int32_t best = 0;
+    for (int64_t b = 0; b < blocks; ++b) {
+        const int64_t span = (int64_t)h[b].y - h[b].x + 1;
+        if (span <= kEllXwinCap && span > best)
+            best = (int32_t)span;
+    }
+    free(h);
+    *xcap = best;
+    return SPMV_SUCCESS;
+}
+
+extern "C" int spmv_ell_run_xwin(spmv_dims d, int32_t K, int64_t ld, int32_t ki, const int32_t *col,
+                                 const double *val, const double *x, double *y, const void *win, int32_t xcap)
+{
+    if (d.n_rows < 0 || K < 0 || ld < d.n_rows || ld % 64 != 0)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_ell_run_xwin: bad K / ld");
+    if ((ki != 1 && ki != 2) || K % ki != 0)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_ell_run_xwin: ki must be 1 or 2 and divide K");
+    if (d.n_rows == 0)
+        return SPMV_SUCCESS;
+    if (!win || xcap < 0 || xcap > kEllXwinCap)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_ell_run_xwin: bad window arguments");
+    SPMV_GUARD(d);
+    const int64_t blocks = (d.n_rows + kBlock - 1) / kBlock;
+    const bool nt = stream_nt(kSellStreamNtDefault);
+    auto kern = ki == 2 ? (nt ? ell_xwin_kernel<2, true, 4> : ell_xwin_kernel<2, false, 4>)
+                        : (nt ? ell_xwin_kernel<1, true, 4> : ell_xwin_kernel<1, false, 4>);
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock), (size_t)xcap * sizeof(double),
+                       (hipStream_t)d.stream, d.n_rows, K, ld, col, val, x, y, (const int2 *)win, xcap);
+    SPMV_CHECK_LAUNCH("ell_xwin_kernel");
     return SPMV_SUCCESS;
 }

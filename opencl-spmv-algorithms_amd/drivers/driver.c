@@ -27,10 +27,13 @@
  * Options: --matrix PATH  --gen cantlike[0|1|2]|rmat|banded|random
  *          --copies B  --reps N  --warmup W  --warm  --device D
  *          --C C --sigma S --ki K --h H --lanes L  --threads T
- *          --cpu / --no-cpu  --strict  --write-mtx PATH  --cache  --help
+ *          --cpu / --no-cpu  --strict  --write-mtx PATH  --cache  --no-xwin  --help
  *   --cache keeps a binary copy of the parsed file at PATH.bin (SURVEY.md
  *   §8f row 1) and reads it instead of the text whenever it is at least as
  *   new as PATH; the entries, their order and the result are unchanged.
+ *   CSR, ELL and SELL run the x-window kernels (each workgroup's x range
+ *   staged in LDS, include/spmv.h); --no-xwin runs the global-gather ones.
+ *   Device buffers are released by spmv_release() / process exit.
  */
 #define _POSIX_C_SOURCE 200809L
 #include <errno.h>
@@ -52,7 +55,7 @@ typedef struct {
     const char *gen;
     const char *write_mtx;
     int64_t copies;
-    int reps, warmup, warm, device, C, sigma, ki, h, lanes, threads, cpu, strict, cache;
+    int reps, warmup, warm, device, C, sigma, ki, h, lanes, threads, cpu, strict, cache, xwin;
 } opts_t;
 
 static void usage(const char *prog)
@@ -60,7 +63,8 @@ static void usage(const char *prog)
     printf("usage: %s [--matrix PATH | --gen cantlike[0|1|2]|rmat|banded|random]\n"
            "          [--copies B] [--reps N] [--warmup W] [--warm] [--device D]\n"
            "          [--C C] [--sigma S] [--ki 1|2] [--h H] [--lanes L]\n"
-           "          [--threads T] [--cpu|--no-cpu] [--strict] [--write-mtx PATH] [--cache]\n",
+           "          [--threads T] [--cpu|--no-cpu] [--strict] [--write-mtx PATH] [--cache]\n"
+           "          [--no-xwin]\n",
            prog);
 }
 
@@ -76,6 +80,7 @@ static int parse_opts(int argc, char **argv, spmv_format fmt, opts_t *o)
     o->ki = 0; /* 0: format default (ELL 2, SELL 1) */
     o->h = 8;
     o->cpu = fmt != FMT_SELL;
+    o->xwin = 1;
     for (int i = 1; i < argc; ++i) {
         const char *a = argv[i];
         const char *v = i + 1 < argc ? argv[i + 1] : NULL;
@@ -105,6 +110,7 @@ static int parse_opts(int argc, char **argv, spmv_format fmt, opts_t *o)
         else if (!strcmp(a, "--no-cpu")) o->cpu = 0;
         else if (!strcmp(a, "--strict")) o->strict = 1;
         else if (!strcmp(a, "--cache")) o->cache = 1;
+        else if (!strcmp(a, "--no-xwin")) o->xwin = 0;
         else if (!strcmp(a, "--help") || !strcmp(a, "-h")) { usage(argv[0]); exit(0); }
         else {
             fprintf(stderr, "unknown option %s\n", a);
@@ -249,6 +255,8 @@ typedef struct {
     double *d_val, *d_x, *d_y;
     void *d_ws;
     size_t ws_bytes;
+    void *d_win; /* x-window kernels: per-workgroup column ranges */
+    int32_t xcap;
     int32_t K, C, sigma, ki, h, lanes, variant;
     int64_t ld, n_slices, n_strips;
     /* host copies for the CPU loop */
@@ -388,9 +396,47 @@ static int build_format(const opts_t *o, spmv_format fmt, const coo_t *m, dev_fm
     return SPMV_SUCCESS;
 }
 
+/* CSR (not the entry-balanced variant), ELL and SELL run the x-window
+ * kernels: each workgroup's x range is staged in LDS (include/spmv.h).
+ * The windows are built once on the device, outside the timed launches. */
+static int build_windows(dev_fmt_t *f)
+{
+    size_t bytes = 0;
+    if (f->fmt == FMT_CSR && f->variant != 4)
+        bytes = spmv_csr_xwin_bytes(f->d.n_rows, f->d.nnz, f->lanes);
+    else if (f->fmt == FMT_ELL)
+        bytes = spmv_ell_xwin_bytes(f->d.n_rows);
+    else if (f->fmt == FMT_SELL)
+        bytes = spmv_sell_xwin_bytes(f->n_slices, f->C, f->sigma);
+    if (bytes == 0)
+        return SPMV_SUCCESS;
+    int rc = spmv_malloc(&f->d_win, bytes);
+    if (rc)
+        return rc;
+    if (f->fmt == FMT_CSR)
+        rc = spmv_csr_xwin_build(f->d, f->d_ptr, f->d_col, f->lanes, f->d_win, bytes, &f->xcap);
+    else if (f->fmt == FMT_ELL)
+        rc = spmv_ell_xwin_build(f->d, f->K, f->ld, f->ki, f->d_col, f->d_win, bytes, &f->xcap);
+    else
+        rc = spmv_sell_xwin_build(f->d, f->C, f->sigma, f->n_slices, f->d_ptr, f->d_col, f->d_win, bytes,
+                                  &f->xcap);
+    return rc;
+}
+
 static int launch(void *arg)
 {
     dev_fmt_t *f = (dev_fmt_t *)arg;
+    if (f->d_win) {
+        if (f->fmt == FMT_CSR)
+            return spmv_csr_run_xwin(f->d, f->d_ptr, f->d_col, f->d_val, f->d_x, f->d_y, f->lanes, f->d_win,
+                                     f->xcap);
+        if (f->fmt == FMT_ELL)
+            return spmv_ell_run_xwin(f->d, f->K, f->ld, f->ki, f->d_col, f->d_val, f->d_x, f->d_y, f->d_win,
+                                     f->xcap);
+        if (f->fmt == FMT_SELL)
+            return spmv_sell_run_xwin(f->d, f->C, f->sigma, f->ki, f->n_slices, f->d_ptr, f->d_perm, f->d_col,
+                                      f->d_val, f->d_x, f->d_y, f->d_win, f->xcap);
+    }
     switch (f->fmt) {
     case FMT_COO:
         return spmv_coo_run(f->d, f->d_row, f->d_col, f->d_val, f->d_x, f->d_y, f->d_ws,
@@ -520,6 +566,8 @@ int spmv_driver_main(int argc, char **argv, spmv_format fmt)
 
     dev_fmt_t f;
     rc = build_format(&o, fmt, &m, &f);
+    if (rc == SPMV_SUCCESS && o.xwin)
+        rc = build_windows(&f);
     if (rc != SPMV_SUCCESS) {
         printf("format build/upload failed: %s %s\n", spmv_strerror(rc), spmv_last_error());
         return rc == SPMV_OTHER_ERROR ? SPMV_OTHER_ERROR : SPMV_PROGRAM_ERROR;

@@ -84,7 +84,15 @@ HIP_SYMBOLS = {
     "spmv_csr_tiled_ws_bytes": (ctypes.c_size_t, [_c_i64, _c_i64]),
     "spmv_csr_run_tiled": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t]),
     "spmv_csr16_run": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_int]),
+    "spmv_csr_xwin_bytes": (ctypes.c_size_t, [_c_i64, _c_i64, ctypes.c_int]),
+    "spmv_csr_xwin_build": (ctypes.c_int, [Dims, _vp, _vp, ctypes.c_int, _vp, ctypes.c_size_t,
+                                           ctypes.POINTER(_c_i32)]),
+    "spmv_csr_run_xwin": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, ctypes.c_int, _vp, _c_i32]),
     "spmv_ell_run": (ctypes.c_int, [Dims, _c_i32, _c_i64, _c_i32, _vp, _vp, _vp, _vp]),
+    "spmv_ell_xwin_bytes": (ctypes.c_size_t, [_c_i64]),
+    "spmv_ell_xwin_build": (ctypes.c_int, [Dims, _c_i32, _c_i64, _c_i32, _vp, _vp, ctypes.c_size_t,
+                                           ctypes.POINTER(_c_i32)]),
+    "spmv_ell_run_xwin": (ctypes.c_int, [Dims, _c_i32, _c_i64, _c_i32, _vp, _vp, _vp, _vp, _vp, _c_i32]),
     "spmv_sell_xwin_bytes": (ctypes.c_size_t, [_c_i64, _c_i32, _c_i32]),
     "spmv_sell_xwin_build": (ctypes.c_int, [Dims, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, ctypes.c_size_t,
                                             ctypes.POINTER(_c_i32)]),
@@ -451,6 +459,9 @@ class DeviceMatrix:
         if self.fmt == "coo":
             rc = lib.spmv_coo_run(d, _ptr(a["row"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
                                   _ptr(a["ws"]), a["ws"].numel())
+        elif self.fmt == "csr" and "win" in a:
+            rc = lib.spmv_csr_run_xwin(d, _ptr(a["row_ptr"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
+                                       p["lanes"], _ptr(a["win"]), p["xcap"])
         elif self.fmt == "csr":
             if p.get("variant", 0) == 4:
                 rc = lib.spmv_csr_run_tiled(d, _ptr(a["row_ptr"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x),
@@ -461,6 +472,9 @@ class DeviceMatrix:
         elif self.fmt == "csr16":
             rc = lib.spmv_csr16_run(d, _ptr(a["row_ptr"]), _ptr(a["blk_base"]), _ptr(a["col_off"]),
                                     _ptr(a["col_esc"]), _ptr(a["val"]), _ptr(x), _ptr(y), p["lanes"])
+        elif self.fmt == "ell" and "win" in a:
+            rc = lib.spmv_ell_run_xwin(d, p["K"], p["ld"], p["ki"], _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
+                                       _ptr(a["win"]), p["xcap"])
         elif self.fmt == "ell":
             rc = lib.spmv_ell_run(d, p["K"], p["ld"], p["ki"], _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y))
         elif self.fmt == "sell" and "win" in a:
@@ -492,12 +506,40 @@ def _sell_xwin(dm: DeviceMatrix) -> None:
     p["xcap"] = cap.value
 
 
+def _ell_xwin(dm: DeviceMatrix) -> None:
+    """Per-256-row column windows for the x-window ELL kernel."""
+    torch = _torch()
+    p, a = dm.params, dm.arrays
+    nbytes = hip_lib().spmv_ell_xwin_bytes(dm.n_rows)
+    a["win"] = torch.empty(max(nbytes, 8), dtype=torch.uint8, device=dm.device)
+    cap = _c_i32(0)
+    _check(hip_lib().spmv_ell_xwin_build(dm.dims(), p["K"], p["ld"], p["ki"], _ptr(a["col"]), _ptr(a["win"]),
+                                         a["win"].numel(), ctypes.byref(cap)), "spmv_ell_xwin_build")
+    p["xcap"] = cap.value
+
+
+def _csr_xwin(dm: DeviceMatrix) -> None:
+    """Per-row-group column windows for the x-window CSR kernel."""
+    torch = _torch()
+    p, a = dm.params, dm.arrays
+    nbytes = hip_lib().spmv_csr_xwin_bytes(dm.n_rows, dm.nnz, p["lanes"])
+    a["win"] = torch.empty(max(nbytes, 8), dtype=torch.uint8, device=dm.device)
+    cap = _c_i32(0)
+    _check(hip_lib().spmv_csr_xwin_build(dm.dims(), _ptr(a["row_ptr"]), _ptr(a["col"]), p["lanes"], _ptr(a["win"]),
+                                         a["win"].numel(), ctypes.byref(cap)), "spmv_csr_xwin_build")
+    p["xcap"] = cap.value
+    p["variant"] = 3
+
+
 def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int = 0, ki: int = 0, C: int = 64,
               sigma: int = 1024, h: int = 8, ell_max_padding: float | None = 64.0,
-              xwin: bool = False) -> DeviceMatrix:
-    """Build `fmt` on the host (libspmv_host.so) and upload it.  xwin (SELL):
-    also build the per-workgroup x windows and run the LDS-window kernel."""
+              xwin: bool | None = None) -> DeviceMatrix:
+    """Build `fmt` on the host (libspmv_host.so) and upload it.  xwin (CSR,
+    ELL, SELL; default on): also build the per-workgroup x windows on the
+    device and run the LDS x-window kernels (same bits as without)."""
     torch = _torch()
+    if xwin is None:
+        xwin = fmt in ("csr", "ell", "sell")
     device = torch.device(device)
     dm = DeviceMatrix(fmt, m.n_rows, m.n_cols, m.nnz, device)
     if fmt == "coo":
@@ -518,6 +560,8 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
         if variant == 4:
             ws = hip_lib().spmv_csr_tiled_ws_bytes(m.n_rows, m.nnz)
             dm.arrays["ws"] = torch.empty(ws, dtype=torch.uint8, device=device)
+        elif xwin and variant in (0, 3):
+            _csr_xwin(dm)
         dm.stored_bytes = 12 * m.nnz + 8 * (m.n_rows + 1)
     elif fmt == "csr16":
         c = csr16_build(col)
@@ -532,6 +576,8 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
         dm.params = dict(K=e["K"], ld=e["ld"], ki=ki, stored=e["stored"])
         dm.arrays = dict(col=_dev_tensor(e["col"], device), val=_dev_tensor(e["val"], device))
         dm.stored_bytes = 12 * e["stored"]
+        if xwin:
+            _ell_xwin(dm)
     elif fmt == "sell":
         ki = ki or 1  # measured best for SELL-64-1024 (profiles/round1_sweep.md)
         s = sell_build(m.n_rows, ptr, col, val, C=C, sigma=sigma, ki=ki)

@@ -97,3 +97,13 @@ def test_binary_cache(tmp_path, prog):
     os.utime(src, (st.st_atime + 10, st.st_mtime + 10))
     r3 = run(prog, *args)
     assert "[cache] wrote" in r3.stdout, r3.stdout
+
+
+@pytest.mark.parametrize("prog", ["csr", "ell", "sigma_c"])
+def test_xwin_and_global_paths_agree(prog):
+    """Default (x window in LDS) and --no-xwin both pass the check."""
+    for extra in ([], ["--no-xwin"]):
+        r = run(prog, "--gen", "cantlike", "--copies", "2", "--reps", "3", "--warmup", "1", "--strict",
+                "--no-cpu", *extra)
+        assert r.returncode == 0, r.stdout + r.stderr
+        assert "\nresult is ok\n" in "\n" + r.stdout

@@ -44,6 +44,9 @@ FMT_PARAMS = [
     ("sell", {"C": 64, "sigma": 1024, "ki": 2}),
     ("sell", {"C": 64, "sigma": 1024, "ki": 1, "xwin": True}),
     ("sell", {"C": 32, "sigma": 64, "ki": 2, "xwin": True}),
+    ("ell", {"ki": 2, "xwin": True}),
+    ("csr", {"xwin": True}),
+    ("csr", {"lanes": 2, "xwin": True}),
     ("sell", {"C": 64, "sigma": 1, "ki": 1}),
     ("sell", {"C": 32, "sigma": 1, "ki": 1}),
     ("sell", {"C": 128, "sigma": 256, "ki": 2}),
@@ -378,3 +381,69 @@ def test_sell_xwin_bit_identical(torch_dev, case, ki):
     torch.cuda.synchronize()
     assert torch.equal(ys[0].view(torch.int64), ys[1].view(torch.int64))
     assert_parity(m, ys[1].cpu().numpy(), x.cpu().numpy())
+
+
+@pytest.mark.parametrize("case", ["cantlike", "rmat", "ragged", "fixtures"])
+@pytest.mark.parametrize("lanes", [0, 2, 16])
+def test_csr_xwin_bit_identical(torch_dev, case, lanes):
+    """The LDS x-window CSR kernel gives variant 3's bits (row groups whose
+    window does not fit gather from global memory)."""
+    torch, dev = torch_dev
+    if case == "cantlike":
+        ms = [sa.gen_cantlike(2, copies=4)]
+    elif case == "rmat":
+        ms = [sa.gen_rmat(1_000_000, 10_000_000, scale=20, seed=1)]
+    elif case == "ragged":
+        ms = [sa.gen_random(20_000, 20_000, 0, 700, seed=21)]
+    else:
+        ms = [sa.read_mtx(GOLDEN / f"{c}.mtx") for c in CASES]
+    for m in ms:
+        if m.n_rows == 0:
+            continue
+        x = torch.from_numpy(np.random.default_rng(8).uniform(-1, 1, max(m.n_cols, 1))).to(dev)
+        ys = []
+        for xw in (False, True):
+            dm = sa.to_device(m, "csr", dev, lanes=lanes, variant=3, xwin=xw)
+            y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
+            dm.run(x, y)
+            ys.append(y)
+            if xw and case == "cantlike":
+                assert dm.params["xcap"] > 0
+        torch.cuda.synchronize()
+        assert torch.equal(ys[0].view(torch.int64), ys[1].view(torch.int64)), m.label
+        assert_parity(m, ys[1].cpu().numpy(), x.cpu().numpy()[: m.n_cols])
+
+
+@pytest.mark.parametrize("lanes", [4, 8, 32])
+def test_csr_xwin_direct_bit_identical(torch_dev, monkeypatch, lanes):
+    """SPMV_CSR_XWIN_DIRECT=1: the row-walking kernel with LDS x windows
+    gives variant 1's bits."""
+    torch, dev = torch_dev
+    for m in (sa.gen_cantlike(0, copies=2), sa.gen_random(20_000, 20_000, 0, 700, seed=21)):
+        x = torch.from_numpy(np.random.default_rng(8).uniform(-1, 1, m.n_cols)).to(dev)
+        ref = sa.to_device(m, "csr", dev, lanes=lanes, variant=1)
+        y0 = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
+        ref.run(x, y0)
+        monkeypatch.setenv("SPMV_CSR_XWIN_DIRECT", "1")
+        dm = sa.to_device(m, "csr", dev, lanes=lanes, variant=3, xwin=True)
+        y1 = torch.full_like(y0, float("nan"))
+        dm.run(x, y1)
+        monkeypatch.delenv("SPMV_CSR_XWIN_DIRECT")
+        torch.cuda.synchronize()
+        assert torch.equal(y0.view(torch.int64), y1.view(torch.int64))
+
+
+@pytest.mark.parametrize("ki", [1, 2])
+def test_ell_xwin_bit_identical(torch_dev, ki):
+    torch, dev = torch_dev
+    for m in (sa.gen_cantlike(0, copies=2), sa.gen_random(20_000, 20_000, 0, 70, seed=21)):
+        x = torch.from_numpy(np.random.default_rng(8).uniform(-1, 1, m.n_cols)).to(dev)
+        ys = []
+        for xw in (False, True):
+            dm = sa.to_device(m, "ell", dev, ki=ki, xwin=xw, ell_max_padding=None)
+            y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
+            dm.run(x, y)
+            ys.append(y)
+        torch.cuda.synchronize()
+        assert torch.equal(ys[0].view(torch.int64), ys[1].view(torch.int64))
+        assert_parity(m, ys[1].cpu().numpy(), x.cpu().numpy())

@@ -34,14 +34,18 @@ VARIANTS = [
     ("cmrs", {"h": 8}), ("cmrs", {"h": 16}), ("cmrs", {"h": 32}),
     ("coo", {}),
     ("csr16", {"lanes": 4}), ("csr16", {"lanes": 2}), ("csr16", {"lanes": 8}),
-    # SELL x window in LDS (xwin) vs global gathers
-    ("sell", {"C": 64, "sigma": 1024, "ki": 1, "env": {"SPMV_STREAM_NT": "1"}}),
-    ("sell", {"C": 64, "sigma": 1024, "ki": 1, "xwin": True, "env": {"SPMV_STREAM_NT": "1"}}),
-    ("sell", {"C": 64, "sigma": 1024, "ki": 1, "xwin": True, "env": {"SPMV_STREAM_NT": "0"}}),
-    ("sell", {"C": 64, "sigma": 1024, "ki": 2, "xwin": True, "env": {"SPMV_STREAM_NT": "1"}}),
-    ("sell", {"C": 64, "sigma": 512, "ki": 1, "xwin": True, "env": {"SPMV_STREAM_NT": "1"}}),
-    ("sell", {"C": 64, "sigma": 256, "ki": 1, "xwin": True, "env": {"SPMV_STREAM_NT": "1"}}),
-    ("csr", {"lanes": 4, "variant": 3, "env": {"SPMV_CSR_BATCH": "0"}}),
+    # x window in LDS (xwin) vs global gathers
+    ("sell", {"C": 64, "sigma": 1024, "ki": 1, "env": {}}),
+    ("sell", {"C": 64, "sigma": 1024, "ki": 1, "xwin": True}),
+    ("csr", {"lanes": 4, "variant": 3, "env": {}}),
+    ("csr", {"lanes": 4, "variant": 3, "xwin": True}),
+    ("csr", {"lanes": 2, "variant": 3, "xwin": True}),
+    ("csr", {"lanes": 4, "variant": 3, "xwin": True, "env": {"SPMV_STREAM_NT": "1"}}),
+    ("csr", {"lanes": 4, "variant": 3, "xwin": True, "env": {"SPMV_CSR_STAGE_ROUNDS": "3"}}),
+    ("ell", {"ki": 2, "env": {}}),
+    ("ell", {"ki": 2, "xwin": True}),
+    ("ell", {"ki": 1, "xwin": True}),
+    ("csr", {"lanes": 8, "variant": 3, "xwin": True, "env": {"SPMV_CSR_XWIN_DIRECT": "1"}}),
 ]
 
 
@@ -63,7 +67,7 @@ def main():
     y = torch.empty(m.n_rows, dtype=torch.float64, device=dev)
     variants = [v for v in VARIANTS if not a.only or v[0] in a.only.split(",")]
     if a.env_only:
-        variants = [v for v in variants if "env" in v[1]]
+        variants = [v for v in variants if "env" in v[1] or v[1].get("xwin")]
     if a.matrix != "cantlike":
         variants = [v for v in variants if v[0] != "ell"]
     res = {i: [] for i in range(len(variants))}

@@ -82,6 +82,10 @@ def parse():
 
 def kernel_name(args, dm=None):
     """The dominant kernel as rocprofv3 names it (for profiles/)."""
+    if dm is not None and "win" in getattr(dm, "arrays", {}):
+        if args.format == "csr" and os.environ.get("SPMV_CSR_XWIN_DIRECT") == "1":
+            return "csr_vector_xwin_kernel"
+        return f"{args.format}_xwin_kernel"
     if args.format == "csr":
         v = (getattr(dm, "params", {}) or {}).get("variant", 0) or args.variant
         v = v or int(os.environ.get("SPMV_CSR_VARIANT", "0") or 0) or CSR_DEFAULT_VARIANT
@@ -150,8 +154,9 @@ def cold_single(torch, dm, x, y, reps=30):
     return float(np.median(cold)), float(np.median(warm))
 
 
-def traffic_for(fmt, workload_bytes):
-    """HBM bytes per launch from the committed PMC passes, if they match."""
+def traffic_for(fmt, workload_bytes, kernel=None):
+    """HBM bytes per launch from the committed PMC passes, if they were
+    measured on this workload and this kernel."""
     f = REPO / "profiles" / "traffic.json"
     if not f.exists():
         return None
@@ -160,6 +165,8 @@ def traffic_for(fmt, workload_bytes):
     except (ValueError, AttributeError):
         return None
     if not t or int(t.get("bytes_alg", -1)) != int(workload_bytes):
+        return None
+    if kernel is not None and t.get("kernel") != kernel:
         return None
     return t.get("hbm_bytes_per_launch")
 
@@ -361,7 +368,7 @@ def main():
 
     kern_ms = float(kern_t.item())
     achieved = bytes_step / (kern_ms * 1e-3) * 1e-9
-    traffic = traffic_for(args.format, bytes_step)
+    traffic = traffic_for(args.format, bytes_step, kernel_name(args, dm))
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": sa.HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / sa.HBM_PEAK_GBS, 4), "traffic": traffic,
                 "kernel": kernel_name(args, dm), "kernel_ms": round(kern_ms, 5),

@@ -601,7 +601,7 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
 
 def banded_to_device(n: int, fmt: str, device="cuda:0", row_begin: int = 0, row_end: int | None = None,
                      seed: int = 2, C: int = 64, sigma: int = 1024, ki: int = 2, lanes: int = 0,
-                     variant: int = 0) -> DeviceMatrix:
+                     variant: int = 0, xwin: bool = True) -> DeviceMatrix:
     """Rows [row_begin, row_end) of the banded matrix (BASELINE.json
     configs[4]) generated directly in HBM by spmv_gen_banded_device, as CSR
     or SELL.  Row ids are local to the shard; columns are global (x is the
@@ -635,6 +635,10 @@ def banded_to_device(n: int, fmt: str, device="cuda:0", row_begin: int = 0, row_
     else:
         raise SpmvError(OTHER_ERROR, "banded_to_device", "format must be csr or sell")
     _check(rc, "spmv_gen_banded_device")
+    if xwin and fmt == "csr":
+        _csr_xwin(dm)
+    elif xwin:
+        _sell_xwin(dm)
     return dm
 
 

@@ -25,7 +25,7 @@ from pathlib import Path
 
 REPO = Path(__file__).resolve().parents[1]
 OUT = REPO / "gpurun_out" / "pmc"
-KERNELS = {"csr": "csr_", "sell": "sell_kernel", "ell": "ell_kernel",
+KERNELS = {"csr": "csr_xwin_kernel", "sell": "sell_xwin_kernel", "ell": "ell_xwin_kernel",
            "coo": "coo_staged_kernel", "cmrs": "cmrs_staged_kernel", "csr16": "Col16"}
 
 

@@ -86,15 +86,18 @@ int spmv_csr_run_variant(spmv_dims d, const int64_t *row_ptr,
 /* CSR with each row group's x window staged in LDS (the default staged
  * kernel, variant 3, whose gathers read LDS instead of global memory).
  * Build once: spmv_csr_xwin_build scans col (device) for the column range
- * of every group of 256/L rows (L = lanes_per_row, 0 = auto; the run must
- * use the same L) into `win` (spmv_csr_xwin_bytes bytes) and returns in
- * *xcap the LDS entries the run stages (0: no window fits).  y is
- * bit-identical to spmv_csr_run_variant(..., L, 3).                     */
-size_t spmv_csr_xwin_bytes(int64_t n_rows, int64_t nnz, int lanes_per_row);
+ * of every window of rows_per_window rows (0 = library default, 256;
+ * rounded up to whole groups of 256/L rows, L = lanes_per_row, 0 = auto)
+ * into `win` (spmv_csr_xwin_bytes bytes) and returns in *xcap the LDS
+ * entries the run stages (0: no window fits).  The run must pass the same
+ * lanes_per_row and rows_per_window.  y is bit-identical to
+ * spmv_csr_run_variant(..., L, 3).                                       */
+size_t spmv_csr_xwin_bytes(int64_t n_rows, int64_t nnz, int lanes_per_row, int32_t rows_per_window);
 int spmv_csr_xwin_build(spmv_dims d, const int64_t *row_ptr, const int32_t *col, int lanes_per_row,
-                        void *win, size_t win_bytes, int32_t *xcap);
+                        int32_t rows_per_window, void *win, size_t win_bytes, int32_t *xcap);
 int spmv_csr_run_xwin(spmv_dims d, const int64_t *row_ptr, const int32_t *col, const double *val,
-                      const double *x, double *y, int lanes_per_row, const void *win, int32_t xcap);
+                      const double *x, double *y, int lanes_per_row, int32_t rows_per_window,
+                      const void *win, int32_t xcap);
 /* CSR with compressed 16-bit column indices (arrays
  * from spmv_csr16_plan/fill in spmv_host.h): 10.06 instead of 12 bytes per
  * entry when 64-entry blocks of columns span < 65536 (banded / FEM

@@ -100,10 +100,10 @@ __global__ __launch_bounds__(kBlock) void csr_vector_kernel(
 
 // CSR-vector (direct: every L-lane group walks its own row) with the
 // workgroup's x window staged in LDS first; windows from
-// spmv_csr_xwin_build (one per 256/L rows = one per workgroup here).
+// spmv_csr_xwin_build (one per gpw workgroups of 256/L rows).
 template <int L>
 __global__ __launch_bounds__(kBlock) void csr_vector_xwin_kernel(
-    int64_t n_rows, const int64_t *__restrict__ row_ptr,
+    int64_t n_rows, int64_t gpw, const int64_t *__restrict__ row_ptr,
     const int32_t *__restrict__ col, const double *__restrict__ val,
     const double *__restrict__ x, double *__restrict__ y, const int2 *__restrict__ win, int32_t xcap)
 {
@@ -115,7 +115,7 @@ __global__ __launch_bounds__(kBlock) void csr_vector_xwin_kernel(
         const int64_t r = row0 + threadIdx.x;
         s_ptr[threadIdx.x] = row_ptr[r < n_rows ? r : n_rows];
     }
-    const int2 wnd = win[blockIdx.x];
+    const int2 wnd = win[blockIdx.x / gpw];  // the window covering this workgroup's rows
     const int32_t span = wnd.y - wnd.x + 1;
     const bool staged = span > 0 && span <= xcap;  // uniform per workgroup
     if (staged)
@@ -386,16 +386,18 @@ __global__ __launch_bounds__(kBlock) void csr_window_kernel(int64_t n_rows, int6
         win[g] = r;
 }
 
-// The persistent staged kernel with each row group's x window
-// x[win.x .. win.y] copied into LDS (dynamic, xcap entries) when the group
-// starts: the products then gather from LDS instead of global memory, the
-// limiter of the staged kernel (TA busy, requests well below the DRAM
-// credit limit: profiles/round1/pmc_stalls.json).  A group whose window
-// exceeds xcap gathers from global memory.  Same products, same order:
-// y is bit-identical to variant 3.
+// The persistent staged kernel with x windows in LDS.  A window covers
+// gpw consecutive row groups (rows_per_window = gpw * 256/L rows): the
+// workgroup copies x[win.x .. win.y] into LDS (dynamic, xcap entries) once
+// and then streams the gpw groups, whose products gather from LDS instead
+// of global memory — the limiter of the staged kernel (TA busy, requests
+// well below the DRAM credit limit: profiles/round1/pmc_stalls.json).
+// Windows of several groups overlap less than per-group windows, so less
+// x is re-read.  A window wider than xcap gathers from global memory.
+// Same products, same order: y is bit-identical to variant 3.
 template <int L, int R, bool NT>
 __global__ __launch_bounds__(kBlock) void csr_xwin_kernel(
-    int64_t n_rows, int64_t n_groups, const int64_t *__restrict__ row_ptr,
+    int64_t n_rows, int64_t n_groups, int64_t gpw, const int64_t *__restrict__ row_ptr,
     const int32_t *__restrict__ col, const double *__restrict__ val,
     const double *__restrict__ x, double *__restrict__ y, const int2 *__restrict__ win, int32_t xcap)
 {
@@ -404,38 +406,29 @@ __global__ __launch_bounds__(kBlock) void csr_xwin_kernel(
     __shared__ int64_t s_ptr[RPB + 1];
     __shared__ double2 s_prod[kBlock * R];
     const int64_t nz = row_ptr[n_rows];
-    int64_t grp = blockIdx.x;
-    int64_t next = 0;
-    if (threadIdx.x <= RPB) {
-        const int64_t r = grp * RPB + threadIdx.x;
-        next = row_ptr[r < n_rows ? r : n_rows];
-    }
-    int2 wnext = grp < n_groups ? win[grp] : int2{0, -1};
-    for (; grp < n_groups; grp += gridDim.x) {
-        if (threadIdx.x <= RPB)
-            s_ptr[threadIdx.x] = next;
-        const int2 wnd = wnext;
+    const int64_t n_win = (n_groups + gpw - 1) / gpw;
+    for (int64_t wi = blockIdx.x; wi < n_win; wi += gridDim.x) {
+        const int2 wnd = win[wi];
         const int32_t span = wnd.y - wnd.x + 1;
         const bool staged = span > 0 && span <= xcap;  // uniform per workgroup
         if (staged)
             for (int32_t i = threadIdx.x; i < span; i += kBlock)
                 s_x[i] = x[wnd.x + i];
-        __syncthreads();
-        const int64_t g2 = grp + gridDim.x;
-        if (g2 < n_groups) {
+        const int64_t g_end = (wi + 1) * gpw < n_groups ? (wi + 1) * gpw : n_groups;
+        for (int64_t grp = wi * gpw; grp < g_end; ++grp) {
             if (threadIdx.x <= RPB) {
-                const int64_t r = g2 * RPB + threadIdx.x;
-                next = row_ptr[r < n_rows ? r : n_rows];
+                const int64_t r = grp * RPB + threadIdx.x;
+                s_ptr[threadIdx.x] = row_ptr[r < n_rows ? r : n_rows];
             }
-            wnext = win[g2];
+            __syncthreads();  // offsets (and, for the first group, the window) visible
+            const int64_t row = grp * RPB + threadIdx.x / L;
+            if (staged)
+                staged_group<L, R, NT, Col32<NT>, 0, XWindow>(row, s_ptr, s_prod, Col32<NT>{col}, val,
+                                                              XWindow{s_x, wnd.x}, y, n_rows, nz);
+            else
+                staged_group<L, R, NT, Col32<NT>, 0, XGlobal>(row, s_ptr, s_prod, Col32<NT>{col}, val,
+                                                              XGlobal{x}, y, n_rows, nz);
         }
-        const int64_t row = grp * RPB + threadIdx.x / L;
-        if (staged)
-            staged_group<L, R, NT, Col32<NT>, 0, XWindow>(row, s_ptr, s_prod, Col32<NT>{col}, val,
-                                                          XWindow{s_x, wnd.x}, y, n_rows, nz);
-        else
-            staged_group<L, R, NT, Col32<NT>, 0, XGlobal>(row, s_ptr, s_prod, Col32<NT>{col}, val, XGlobal{x},
-                                                          y, n_rows, nz);
     }
 }
 
@@ -800,29 +793,42 @@ extern "C" int spmv_csr_run(spmv_dims d, const int64_t *row_ptr,
 namespace spmv {
 
 constexpr int32_t kCsrXwinCap = 2048;  // 16 KiB of LDS: 32 KiB per workgroup with the stage
+constexpr int32_t kCsrXwinRows = 256;  // rows per x window (SPMV API rows_per_window = 0)
+
+// rows per x window: a multiple of the row group (256/L rows), default
+// kCsrXwinRows, at least one group
+static int64_t csr_xwin_gpw(int L, int32_t rows_per_window)
+{
+    const int64_t rpb = kBlock / L;
+    const int64_t rows = rows_per_window > 0 ? rows_per_window : kCsrXwinRows;
+    const int64_t g = (rows + rpb - 1) / rpb;
+    return g < 1 ? 1 : g;
+}
 
 template <int L, int R, bool NT>
 static void launch_csr_xwin(const spmv_dims &d, const int64_t *row_ptr, const int32_t *col,
-                            const double *val, const double *x, double *y, const int2 *win, int32_t xcap)
+                            const double *val, const double *x, double *y, const int2 *win, int32_t xcap,
+                            int64_t gpw)
 {
     constexpr int RPB = kBlock / L;
     const int64_t groups = (d.n_rows + RPB - 1) / RPB;
+    const int64_t n_win = (groups + gpw - 1) / gpw;
     const size_t lds = (size_t)xcap * sizeof(double);
-    const int64_t grid = persistent_grid(csr_xwin_kernel<L, R, NT>, groups, lds);
+    const int64_t grid = persistent_grid(csr_xwin_kernel<L, R, NT>, n_win, lds);
     hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT>), dim3((unsigned)grid), dim3(kBlock), lds,
-                       (hipStream_t)d.stream, d.n_rows, groups, row_ptr, col, val, x, y, win, xcap);
+                       (hipStream_t)d.stream, d.n_rows, groups, gpw, row_ptr, col, val, x, y, win, xcap);
 }
 
 template <int L>
 static void launch_csr_vector_xwin(const spmv_dims &d, const int64_t *row_ptr, const int32_t *col,
                                    const double *val, const double *x, double *y, const int2 *win,
-                                   int32_t xcap)
+                                   int32_t xcap, int64_t gpw)
 {
     constexpr int RPB = kBlock / L;
     const int64_t blocks = (d.n_rows + RPB - 1) / RPB;
     hipLaunchKernelGGL((csr_vector_xwin_kernel<L>), dim3((unsigned)blocks), dim3(kBlock),
-                       (size_t)xcap * sizeof(double), (hipStream_t)d.stream, d.n_rows, row_ptr, col, val, x, y,
-                       win, xcap);
+                       (size_t)xcap * sizeof(double), (hipStream_t)d.stream, d.n_rows, gpw, row_ptr, col, val, x,
+                       y, win, xcap);
 }
 
 // SPMV_CSR_XWIN_DIRECT=1: the x-window run uses the direct (row-walking)
@@ -835,34 +841,35 @@ static bool csr_xwin_direct()
 
 }  // namespace spmv
 
-extern "C" size_t spmv_csr_xwin_bytes(int64_t n_rows, int64_t nnz, int lanes_per_row)
+extern "C" size_t spmv_csr_xwin_bytes(int64_t n_rows, int64_t nnz, int lanes_per_row, int32_t rows_per_window)
 {
     const int L = lanes_per_row > 0 ? lanes_per_row : spmv_csr_auto_lanes(n_rows, nnz);
-    if (L < 2 || L > 64 || (L & (L - 1)) || n_rows <= 0)
+    if (L < 2 || L > 64 || (L & (L - 1)) || n_rows <= 0 || rows_per_window < 0)
         return 0;
-    const int64_t rpb = kBlock / L;
-    return (size_t)((n_rows + rpb - 1) / rpb) * sizeof(int2);
+    const int64_t rpw = csr_xwin_gpw(L, rows_per_window) * (kBlock / L);
+    return (size_t)((n_rows + rpw - 1) / rpw) * sizeof(int2);
 }
 
 extern "C" int spmv_csr_xwin_build(spmv_dims d, const int64_t *row_ptr, const int32_t *col,
-                                   int lanes_per_row, void *win, size_t win_bytes, int32_t *xcap)
+                                   int lanes_per_row, int32_t rows_per_window, void *win, size_t win_bytes,
+                                   int32_t *xcap)
 {
-    if (d.n_rows < 0 || d.nnz < 0 || !xcap)
+    if (d.n_rows < 0 || d.nnz < 0 || !xcap || rows_per_window < 0)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_xwin_build: bad arguments");
     *xcap = 0;
     if (d.n_rows == 0)
         return SPMV_SUCCESS;
     const int L = lanes_per_row > 0 ? lanes_per_row : spmv_csr_auto_lanes(d.n_rows, d.nnz);
-    const size_t need = spmv_csr_xwin_bytes(d.n_rows, d.nnz, L);
+    const size_t need = spmv_csr_xwin_bytes(d.n_rows, d.nnz, L, rows_per_window);
     if (need == 0)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_xwin_build: lanes_per_row must be 0 or a power of two in [2,64]");
     if (!win || win_bytes < need)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_xwin_build: window buffer too small");
     SPMV_GUARD(d);
-    const int64_t rpb = kBlock / L;
-    const int64_t groups = (d.n_rows + rpb - 1) / rpb;
+    const int64_t rpw = csr_xwin_gpw(L, rows_per_window) * (kBlock / L);
+    const int64_t n_win = (d.n_rows + rpw - 1) / rpw;
     const hipStream_t st = (hipStream_t)d.stream;
-    hipLaunchKernelGGL(csr_window_kernel, dim3((unsigned)groups), dim3(kBlock), 0, st, d.n_rows, rpb, row_ptr,
+    hipLaunchKernelGGL(csr_window_kernel, dim3((unsigned)n_win), dim3(kBlock), 0, st, d.n_rows, rpw, row_ptr,
                        col, (int2 *)win);
     SPMV_CHECK_LAUNCH("csr_window_kernel");
     int2 *h = (int2 *)malloc(need);
@@ -876,7 +883,7 @@ extern "C" int spmv_csr_xwin_build(spmv_dims d, const int64_t *row_ptr, const in
         return fail(SPMV_PROGRAM_ERROR, "spmv_csr_xwin_build: copy windows", e);
     }
     int32_t best = 0;
-    for (int64_t g = 0; g < groups; ++g) {
+    for (int64_t g = 0; g < n_win; ++g) {
         const int64_t span = (int64_t)h[g].y - h[g].x + 1;
         if (span <= kCsrXwinCap && span > best)
             best = (int32_t)span;
@@ -887,33 +894,35 @@ extern "C" int spmv_csr_xwin_build(spmv_dims d, const int64_t *row_ptr, const in
 }
 
 extern "C" int spmv_csr_run_xwin(spmv_dims d, const int64_t *row_ptr, const int32_t *col, const double *val,
-                                 const double *x, double *y, int lanes_per_row, const void *win, int32_t xcap)
+                                 const double *x, double *y, int lanes_per_row, int32_t rows_per_window,
+                                 const void *win, int32_t xcap)
 {
-    if (d.n_rows < 0 || d.n_cols < 0 || d.nnz < 0)
-        return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_run_xwin: negative size");
+    if (d.n_rows < 0 || d.n_cols < 0 || d.nnz < 0 || rows_per_window < 0)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_run_xwin: bad sizes");
     if (d.n_rows == 0)
         return SPMV_SUCCESS;
     if (!win || xcap < 0 || xcap > kCsrXwinCap)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_run_xwin: bad window arguments");
     SPMV_GUARD(d);
     const int L = lanes_per_row > 0 ? lanes_per_row : spmv_csr_auto_lanes(d.n_rows, d.nnz);
+    if (L < 2 || L > 64 || (L & (L - 1)))
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_run_xwin: lanes_per_row must be 0 or a power of two in [2,64]");
+    const int64_t gpw = csr_xwin_gpw(L, rows_per_window);
     const bool nt = stream_nt(kCsrXwinNtDefault);
     constexpr int R = kStageRoundsDefault;
     const int2 *w = (const int2 *)win;
     const bool direct = csr_xwin_direct();
 #define SPMV_XWIN(LL)                                                                  \
-    (direct ? launch_csr_vector_xwin<LL>(d, row_ptr, col, val, x, y, w, xcap)          \
-     : nt   ? launch_csr_xwin<LL, R, true>(d, row_ptr, col, val, x, y, w, xcap)        \
-            : launch_csr_xwin<LL, R, false>(d, row_ptr, col, val, x, y, w, xcap))
+    (direct ? launch_csr_vector_xwin<LL>(d, row_ptr, col, val, x, y, w, xcap, gpw)     \
+     : nt   ? launch_csr_xwin<LL, R, true>(d, row_ptr, col, val, x, y, w, xcap, gpw)   \
+            : launch_csr_xwin<LL, R, false>(d, row_ptr, col, val, x, y, w, xcap, gpw))
     switch (L) {
     case 2: SPMV_XWIN(2); break;
     case 4: SPMV_XWIN(4); break;
     case 8: SPMV_XWIN(8); break;
     case 16: SPMV_XWIN(16); break;
     case 32: SPMV_XWIN(32); break;
-    case 64: SPMV_XWIN(64); break;
-    default:
-        return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_run_xwin: lanes_per_row must be 0 or a power of two in [2,64]");
+    default: SPMV_XWIN(64); break;
     }
 #undef SPMV_XWIN
     SPMV_CHECK_LAUNCH("csr_xwin_kernel");

@@ -403,7 +403,7 @@ static int build_windows(dev_fmt_t *f)
 {
     size_t bytes = 0;
     if (f->fmt == FMT_CSR && f->variant != 4)
-        bytes = spmv_csr_xwin_bytes(f->d.n_rows, f->d.nnz, f->lanes);
+        bytes = spmv_csr_xwin_bytes(f->d.n_rows, f->d.nnz, f->lanes, 0);
     else if (f->fmt == FMT_ELL)
         bytes = spmv_ell_xwin_bytes(f->d.n_rows);
     else if (f->fmt == FMT_SELL)
@@ -414,7 +414,7 @@ static int build_windows(dev_fmt_t *f)
     if (rc)
         return rc;
     if (f->fmt == FMT_CSR)
-        rc = spmv_csr_xwin_build(f->d, f->d_ptr, f->d_col, f->lanes, f->d_win, bytes, &f->xcap);
+        rc = spmv_csr_xwin_build(f->d, f->d_ptr, f->d_col, f->lanes, 0, f->d_win, bytes, &f->xcap);
     else if (f->fmt == FMT_ELL)
         rc = spmv_ell_xwin_build(f->d, f->K, f->ld, f->ki, f->d_col, f->d_win, bytes, &f->xcap);
     else
@@ -428,8 +428,8 @@ static int launch(void *arg)
     dev_fmt_t *f = (dev_fmt_t *)arg;
     if (f->d_win) {
         if (f->fmt == FMT_CSR)
-            return spmv_csr_run_xwin(f->d, f->d_ptr, f->d_col, f->d_val, f->d_x, f->d_y, f->lanes, f->d_win,
-                                     f->xcap);
+            return spmv_csr_run_xwin(f->d, f->d_ptr, f->d_col, f->d_val, f->d_x, f->d_y, f->lanes, 0,
+                                     f->d_win, f->xcap);
         if (f->fmt == FMT_ELL)
             return spmv_ell_run_xwin(f->d, f->K, f->ld, f->ki, f->d_col, f->d_val, f->d_x, f->d_y, f->d_win,
                                      f->xcap);

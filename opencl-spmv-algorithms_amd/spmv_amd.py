@@ -84,10 +84,10 @@ HIP_SYMBOLS = {
     "spmv_csr_tiled_ws_bytes": (ctypes.c_size_t, [_c_i64, _c_i64]),
     "spmv_csr_run_tiled": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t]),
     "spmv_csr16_run": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_int]),
-    "spmv_csr_xwin_bytes": (ctypes.c_size_t, [_c_i64, _c_i64, ctypes.c_int]),
-    "spmv_csr_xwin_build": (ctypes.c_int, [Dims, _vp, _vp, ctypes.c_int, _vp, ctypes.c_size_t,
+    "spmv_csr_xwin_bytes": (ctypes.c_size_t, [_c_i64, _c_i64, ctypes.c_int, _c_i32]),
+    "spmv_csr_xwin_build": (ctypes.c_int, [Dims, _vp, _vp, ctypes.c_int, _c_i32, _vp, ctypes.c_size_t,
                                            ctypes.POINTER(_c_i32)]),
-    "spmv_csr_run_xwin": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, ctypes.c_int, _vp, _c_i32]),
+    "spmv_csr_run_xwin": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, ctypes.c_int, _c_i32, _vp, _c_i32]),
     "spmv_ell_run": (ctypes.c_int, [Dims, _c_i32, _c_i64, _c_i32, _vp, _vp, _vp, _vp]),
     "spmv_ell_xwin_bytes": (ctypes.c_size_t, [_c_i64]),
     "spmv_ell_xwin_build": (ctypes.c_int, [Dims, _c_i32, _c_i64, _c_i32, _vp, _vp, ctypes.c_size_t,
@@ -461,7 +461,7 @@ class DeviceMatrix:
                                   _ptr(a["ws"]), a["ws"].numel())
         elif self.fmt == "csr" and "win" in a:
             rc = lib.spmv_csr_run_xwin(d, _ptr(a["row_ptr"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
-                                       p["lanes"], _ptr(a["win"]), p["xcap"])
+                                       p["lanes"], p.get("xwin_rows", 0), _ptr(a["win"]), p["xcap"])
         elif self.fmt == "csr":
             if p.get("variant", 0) == 4:
                 rc = lib.spmv_csr_run_tiled(d, _ptr(a["row_ptr"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x),
@@ -522,18 +522,19 @@ def _csr_xwin(dm: DeviceMatrix) -> None:
     """Per-row-group column windows for the x-window CSR kernel."""
     torch = _torch()
     p, a = dm.params, dm.arrays
-    nbytes = hip_lib().spmv_csr_xwin_bytes(dm.n_rows, dm.nnz, p["lanes"])
+    rows = p.setdefault("xwin_rows", 0)
+    nbytes = hip_lib().spmv_csr_xwin_bytes(dm.n_rows, dm.nnz, p["lanes"], rows)
     a["win"] = torch.empty(max(nbytes, 8), dtype=torch.uint8, device=dm.device)
     cap = _c_i32(0)
-    _check(hip_lib().spmv_csr_xwin_build(dm.dims(), _ptr(a["row_ptr"]), _ptr(a["col"]), p["lanes"], _ptr(a["win"]),
-                                         a["win"].numel(), ctypes.byref(cap)), "spmv_csr_xwin_build")
+    _check(hip_lib().spmv_csr_xwin_build(dm.dims(), _ptr(a["row_ptr"]), _ptr(a["col"]), p["lanes"], rows,
+                                         _ptr(a["win"]), a["win"].numel(), ctypes.byref(cap)), "spmv_csr_xwin_build")
     p["xcap"] = cap.value
     p["variant"] = 3
 
 
 def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int = 0, ki: int = 0, C: int = 64,
               sigma: int = 1024, h: int = 8, ell_max_padding: float | None = 64.0,
-              xwin: bool | None = None) -> DeviceMatrix:
+              xwin: bool | None = None, xwin_rows: int = 0) -> DeviceMatrix:
     """Build `fmt` on the host (libspmv_host.so) and upload it.  xwin (CSR,
     ELL, SELL; default on): also build the per-workgroup x windows on the
     device and run the LDS x-window kernels (same bits as without)."""
@@ -554,7 +555,7 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
     if fmt == "csr":
         if variant == 0:  # host-side choice from the row-length skew
             variant = host_lib().spmv_csr_pick_variant(m.n_rows, _ptr(ptr))
-        dm.params = dict(lanes=lanes, variant=variant)  # 0 = library picks
+        dm.params = dict(lanes=lanes, variant=variant, xwin_rows=xwin_rows)  # 0 = library picks
         dm.arrays = dict(row_ptr=_dev_tensor(ptr, device), col=_dev_tensor(col, device),
                          val=_dev_tensor(val, device))
         if variant == 4:

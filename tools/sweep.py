@@ -34,18 +34,17 @@ VARIANTS = [
     ("cmrs", {"h": 8}), ("cmrs", {"h": 16}), ("cmrs", {"h": 32}),
     ("coo", {}),
     ("csr16", {"lanes": 4}), ("csr16", {"lanes": 2}), ("csr16", {"lanes": 8}),
-    # x window in LDS (xwin) vs global gathers
+    # x window in LDS (xwin) vs global gathers; CSR rows per window
     ("sell", {"C": 64, "sigma": 1024, "ki": 1, "env": {}}),
     ("sell", {"C": 64, "sigma": 1024, "ki": 1, "xwin": True}),
-    ("csr", {"lanes": 4, "variant": 3, "env": {}}),
-    ("csr", {"lanes": 4, "variant": 3, "xwin": True}),
-    ("csr", {"lanes": 2, "variant": 3, "xwin": True}),
-    ("csr", {"lanes": 4, "variant": 3, "xwin": True, "env": {"SPMV_STREAM_NT": "1"}}),
-    ("csr", {"lanes": 4, "variant": 3, "xwin": True, "env": {"SPMV_CSR_STAGE_ROUNDS": "3"}}),
-    ("ell", {"ki": 2, "env": {}}),
+    ("csr", {"lanes": 4, "variant": 3, "xwin": False, "env": {}}),
+    ("csr", {"lanes": 4, "variant": 3, "xwin": True, "xwin_rows": 64}),
+    ("csr", {"lanes": 4, "variant": 3, "xwin": True, "xwin_rows": 256}),
+    ("csr", {"lanes": 4, "variant": 3, "xwin": True, "xwin_rows": 512}),
+    ("csr", {"lanes": 4, "variant": 3, "xwin": True, "xwin_rows": 1024}),
+    ("csr", {"lanes": 2, "variant": 3, "xwin": True, "xwin_rows": 512}),
+    ("csr", {"lanes": 8, "variant": 3, "xwin": True, "xwin_rows": 512, "env": {"SPMV_CSR_XWIN_DIRECT": "1"}}),
     ("ell", {"ki": 2, "xwin": True}),
-    ("ell", {"ki": 1, "xwin": True}),
-    ("csr", {"lanes": 8, "variant": 3, "xwin": True, "env": {"SPMV_CSR_XWIN_DIRECT": "1"}}),
 ]
 
 

@@ -86,7 +86,7 @@ int spmv_csr_run_variant(spmv_dims d, const int64_t *row_ptr,
 /* CSR with each row group's x window staged in LDS (the default staged
  * kernel, variant 3, whose gathers read LDS instead of global memory).
  * Build once: spmv_csr_xwin_build scans col (device) for the column range
- * of every window of rows_per_window rows (0 = library default, 256;
+ * of every window of rows_per_window rows (0 = library default, 128;
  * rounded up to whole groups of 256/L rows, L = lanes_per_row, 0 = auto)
  * into `win` (spmv_csr_xwin_bytes bytes) and returns in *xcap the LDS
  * entries the run stages (0: no window fits).  The run must pass the same

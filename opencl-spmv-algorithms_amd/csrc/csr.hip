@@ -793,7 +793,7 @@ extern "C" int spmv_csr_run(spmv_dims d, const int64_t *row_ptr,
 namespace spmv {
 
 constexpr int32_t kCsrXwinCap = 2048;  // 16 KiB of LDS: 32 KiB per workgroup with the stage
-constexpr int32_t kCsrXwinRows = 256;  // rows per x window (SPMV API rows_per_window = 0)
+constexpr int32_t kCsrXwinRows = 128;  // rows per x window (rows_per_window = 0): 0.2836 ms vs 0.2907 (64), 0.2938 (256), 0.2964 (512), 0.3397 (1024)
 
 // rows per x window: a multiple of the row group (256/L rows), default
 // kCsrXwinRows, at least one group
@@ -814,7 +814,12 @@ static void launch_csr_xwin(const spmv_dims &d, const int64_t *row_ptr, const in
     const int64_t groups = (d.n_rows + RPB - 1) / RPB;
     const int64_t n_win = (groups + gpw - 1) / gpw;
     const size_t lds = (size_t)xcap * sizeof(double);
-    const int64_t grid = persistent_grid(csr_xwin_kernel<L, R, NT>, n_win, lds);
+    // one workgroup per window (the dispatcher balances) unless
+    // SPMV_CSR_XWIN_PERSISTENT=1 (resident workgroups walk the windows)
+    const char *ps = getenv("SPMV_CSR_XWIN_PERSISTENT");
+    const int64_t grid = (ps && ps[0] == '1') ? persistent_grid(csr_xwin_kernel<L, R, NT>, n_win, lds) : n_win;
+    if (grid > INT32_MAX)
+        return;
     hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT>), dim3((unsigned)grid), dim3(kBlock), lds,
                        (hipStream_t)d.stream, d.n_rows, groups, gpw, row_ptr, col, val, x, y, win, xcap);
 }

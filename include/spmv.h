@@ -194,6 +194,33 @@ int spmv_gen_banded_device(int64_t n, uint64_t seed, int64_t row_begin,
                            int64_t *ptr, int32_t *perm, int32_t *col, double *val,
                            int device, void *stream);
 
+/* ------------------------------------------- device format builders ---
+ * build the formats from a COO (entries in any order,
+ * file order kept inside a row) that is already in HBM, without a host
+ * round trip.  Every output array equals the host builder's of
+ * spmv_host.h element for element (CSR: spmv_csr_from_coo; ELL:
+ * spmv_ell_plan/fill; SELL: spmv_sell_plan/fill; CMRS: spmv_cmrs_build).
+ * Builders allocate their own scratch, run on d.stream and synchronise it
+ * before returning; they are build-time calls, not SpMV-path calls.
+ * Sizes: row_ptr[N+1], col_out/val_out[Z]; SELL perm[n_slices*C],
+ * slice_ptr[n_slices+1], slice_col[n_slices] (scratch for the fill),
+ * n_slices = ceil(N/C), sigma <= 4096; *stored (host) = entries incl.
+ * padding, the size of the SELL col/val arrays.                          */
+int spmv_dev_csr_from_coo(spmv_dims d, const int32_t *row, const int32_t *col, const double *val,
+                          int64_t *row_ptr, int32_t *col_out, double *val_out);
+int spmv_dev_ell_plan(spmv_dims d, const int64_t *row_ptr, int32_t ki, int32_t *K, int64_t *ld);
+int spmv_dev_ell_fill(spmv_dims d, const int64_t *row_ptr, const int32_t *col, const double *val,
+                      int32_t K, int64_t ld, int32_t ki, int32_t *col_out, double *val_out);
+int spmv_dev_sell_plan(spmv_dims d, const int64_t *row_ptr, const int32_t *col, int32_t C,
+                       int32_t sigma, int32_t ki, int64_t n_slices, int32_t *perm, int64_t *slice_ptr,
+                       int32_t *slice_col, int64_t *stored);
+int spmv_dev_sell_fill(spmv_dims d, const int64_t *row_ptr, const int32_t *col, const double *val,
+                       int32_t C, int32_t ki, int64_t n_slices, const int64_t *slice_ptr,
+                       const int32_t *perm, const int32_t *slice_col, int32_t *col_out,
+                       double *val_out);
+int spmv_dev_cmrs_build(spmv_dims d, const int64_t *row_ptr, int32_t h, int64_t *strip_ptr,
+                        uint8_t *row_in_strip);
+
 /* ------------------------------------------------- iterated SpMV -------
  * Vector kernels for power iteration / CG over row shards (SURVEY.md §8f
  * row 3).  The reference stops after one SpMV (reference csr.c:198-236),

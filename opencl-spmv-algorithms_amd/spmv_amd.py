@@ -102,6 +102,13 @@ HIP_SYMBOLS = {
     "spmv_cmrs_run": (ctypes.c_int, [Dims, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "spmv_gen_banded_device": (ctypes.c_int, [_c_i64, ctypes.c_uint64, _c_i64, _c_i64, ctypes.c_int, _c_i32,
                                               _c_i32, _vp, _vp, _vp, _vp, ctypes.c_int, _vp]),
+    "spmv_dev_csr_from_coo": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "spmv_dev_ell_plan": (ctypes.c_int, [Dims, _vp, _c_i32, ctypes.POINTER(_c_i32), ctypes.POINTER(_c_i64)]),
+    "spmv_dev_ell_fill": (ctypes.c_int, [Dims, _vp, _vp, _vp, _c_i32, _c_i64, _c_i32, _vp, _vp]),
+    "spmv_dev_sell_plan": (ctypes.c_int, [Dims, _vp, _vp, _c_i32, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp,
+                                          ctypes.POINTER(_c_i64)]),
+    "spmv_dev_sell_fill": (ctypes.c_int, [Dims, _vp, _vp, _vp, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp]),
+    "spmv_dev_cmrs_build": (ctypes.c_int, [Dims, _vp, _c_i32, _vp, _vp]),
     "spmv_dot_ws_bytes": (ctypes.c_size_t, [_c_i64]),
     "spmv_dot": (ctypes.c_int, [_c_i64, _vp, _vp, _vp, _vp, ctypes.c_size_t, ctypes.c_int, _vp]),
     "spmv_axpy_ratio": (ctypes.c_int, [_c_i64, _vp, _vp, ctypes.c_double, _vp, _vp, ctypes.c_int, _vp]),
@@ -597,6 +604,78 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
         dm.stored_bytes = 13 * m.nnz + 8 * (c["n_strips"] + 1)
     else:
         raise SpmvError(OTHER_ERROR, "to_device", f"unknown format {fmt}")
+    return dm
+
+
+def device_build(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, ki: int = 0, C: int = 64,
+                 sigma: int = 1024, h: int = 8, xwin: bool | None = None) -> DeviceMatrix:
+    """Like to_device, but only the raw COO (file order) crosses PCIe: CSR,
+    ELL, SELL and CMRS are built on the device by the spmv_dev_* builders
+    (SURVEY.md §8f row 2); the arrays equal the host builders'."""
+    torch = _torch()
+    device = torch.device(device)
+    if fmt not in ("csr", "ell", "sell", "cmrs"):
+        raise SpmvError(OTHER_ERROR, "device_build", "format must be csr, ell, sell or cmrs")
+    if xwin is None:
+        xwin = fmt in ("csr", "ell", "sell")
+    lib = hip_lib()
+    N, Z = m.n_rows, m.nnz
+    d_row, d_col, d_val = (_dev_tensor(a, device) for a in (m.row, m.col, m.val))
+    ptr = torch.empty(N + 1, dtype=torch.int64, device=device)
+    col = torch.empty(max(Z, 1), dtype=torch.int32, device=device)
+    val = torch.empty(max(Z, 1), dtype=torch.float64, device=device)
+    dm = DeviceMatrix(fmt, N, m.n_cols, Z, device)
+    d = dm.dims()
+    _check(lib.spmv_dev_csr_from_coo(d, _ptr(d_row), _ptr(d_col), _ptr(d_val), _ptr(ptr), _ptr(col), _ptr(val)),
+           "spmv_dev_csr_from_coo")
+    del d_row, d_col, d_val
+    if fmt == "csr":
+        dm.params = dict(lanes=lanes, variant=3, xwin_rows=0)
+        dm.arrays = dict(row_ptr=ptr, col=col, val=val)
+        dm.stored_bytes = 12 * Z + 8 * (N + 1)
+        if xwin:
+            _csr_xwin(dm)
+    elif fmt == "ell":
+        ki = ki or 2
+        K, ld = _c_i32(0), _c_i64(0)
+        _check(lib.spmv_dev_ell_plan(d, _ptr(ptr), ki, ctypes.byref(K), ctypes.byref(ld)), "spmv_dev_ell_plan")
+        stored = K.value * ld.value
+        ec = torch.empty(max(stored, 1), dtype=torch.int32, device=device)
+        ev = torch.empty(max(stored, 1), dtype=torch.float64, device=device)
+        _check(lib.spmv_dev_ell_fill(d, _ptr(ptr), _ptr(col), _ptr(val), K.value, ld.value, ki, _ptr(ec), _ptr(ev)),
+               "spmv_dev_ell_fill")
+        dm.params = dict(K=K.value, ld=ld.value, ki=ki, stored=stored)
+        dm.arrays = dict(col=ec, val=ev)
+        dm.stored_bytes = 12 * stored
+        if xwin:
+            _ell_xwin(dm)
+    elif fmt == "sell":
+        ki = ki or 1
+        ns = (N + C - 1) // C
+        perm = torch.empty(max(ns * C, 1), dtype=torch.int32, device=device)
+        sp = torch.empty(ns + 1, dtype=torch.int64, device=device)
+        scol = torch.empty(max(ns, 1), dtype=torch.int32, device=device)
+        stored = _c_i64(0)
+        _check(lib.spmv_dev_sell_plan(d, _ptr(ptr), _ptr(col), C, sigma, ki, ns, _ptr(perm), _ptr(sp), _ptr(scol),
+                                      ctypes.byref(stored)), "spmv_dev_sell_plan")
+        sc = torch.empty(max(stored.value, 1), dtype=torch.int32, device=device)
+        sv = torch.empty(max(stored.value, 1), dtype=torch.float64, device=device)
+        _check(lib.spmv_dev_sell_fill(d, _ptr(ptr), _ptr(col), _ptr(val), C, ki, ns, _ptr(sp), _ptr(perm), _ptr(scol),
+                                      _ptr(sc), _ptr(sv)), "spmv_dev_sell_fill")
+        dm.params = dict(C=C, sigma=sigma, ki=ki, n_slices=ns, stored=stored.value)
+        dm.arrays = dict(slice_ptr=sp, perm=perm, col=sc, val=sv)
+        dm.stored_bytes = 12 * stored.value + 8 * (ns + 1) + 4 * ns * C
+        if xwin:
+            _sell_xwin(dm)
+    else:
+        ns = (N + h - 1) // h
+        stp = torch.empty(ns + 1, dtype=torch.int64, device=device)
+        rin = torch.empty(max(Z, 1), dtype=torch.uint8, device=device)
+        _check(lib.spmv_dev_cmrs_build(d, _ptr(ptr), h, _ptr(stp), _ptr(rin)), "spmv_dev_cmrs_build")
+        dm.params = dict(h=h, n_strips=ns)
+        dm.arrays = dict(strip_ptr=stp, row_in_strip=rin, col=col, val=val)
+        dm.stored_bytes = 13 * Z + 8 * (ns + 1)
+    dm.arrays["row_ptr_csr"] = ptr
     return dm
 
 

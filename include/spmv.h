@@ -135,6 +135,16 @@ int spmv_ell_xwin_build(spmv_dims d, int32_t K, int64_t ld, int32_t ki, const in
 int spmv_ell_run_xwin(spmv_dims d, int32_t K, int64_t ld, int32_t ki, const int32_t *col,
                       const double *val, const double *x, double *y, const void *win, int32_t xcap);
 
+/* HYB (arrays from spmv_hyb_plan/fill in spmv_host.h):
+ * the ELL part writes y, the row-sorted COO tail of the long rows is added
+ * by the staged COO kernel in accumulate mode and the deterministic carry
+ * pass.  `ws` holds spmv_hyb_ws_bytes(tail_nnz) bytes.                    */
+size_t spmv_hyb_ws_bytes(int64_t tail_nnz);
+int spmv_hyb_run(spmv_dims d, int32_t K, int64_t ld, int32_t ki, const int32_t *ell_col,
+                 const double *ell_val, int64_t tail_nnz, const int32_t *tail_row,
+                 const int32_t *tail_col, const double *tail_val, const double *x, double *y,
+                 void *ws, size_t ws_bytes);
+
 /* -------------------------------------------------------- SELL-C-sigma ---
  * Replaces kernel `sigma_c(val,idx,x,y,slice_ptr,int C)` (reference
  * kernels/Sigma_C.cl:1) and its launch (reference sigma_c.c:50-51,71-72,

@@ -110,6 +110,17 @@ int spmv_sell_fill(int64_t n_rows, const int64_t *row_ptr, const int32_t *col,
 int spmv_cmrs_build(int64_t n_rows, const int64_t *row_ptr, int32_t h,
                     int64_t *strip_ptr, uint8_t *row_in_strip);
 
+/* HYB = ELL + COO tail: the first K entries of every
+ * row in the column-major ELL layout of spmv_ell_fill (ld, ki), the rest
+ * as a row-sorted COO tail.  K_req > 0 forces K (rounded up to ki); 0
+ * picks the K that minimises stored bytes (12 per ELL slot, 16 per tail
+ * entry).  Fill: ell_col/ell_val[K*ld], tail_row/col/val[tail_nnz].     */
+int spmv_hyb_plan(int64_t n_rows, const int64_t *row_ptr, int32_t ki, int32_t K_req, int32_t *K,
+                  int64_t *ld, int64_t *tail_nnz);
+int spmv_hyb_fill(int64_t n_rows, const int64_t *row_ptr, const int32_t *col, const double *val,
+                  int32_t K, int64_t ld, int32_t ki, int32_t *ell_col, double *ell_val,
+                  int32_t *tail_row, int32_t *tail_col, double *tail_val);
+
 /* CSR with compressed 16-bit column indices: the
  * CSR entries are cut into 64-entry blocks (entry p in block p/64).  A
  * block whose columns span < 65536 stores blk_base = its smallest column

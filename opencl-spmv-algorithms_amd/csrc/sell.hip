@@ -485,3 +485,36 @@ extern "C" int spmv_ell_run_xwin(spmv_dims d, int32_t K, int64_t ld, int32_t ki,
     SPMV_CHECK_LAUNCH("ell_xwin_kernel");
     return SPMV_SUCCESS;
 }
+
+extern "C" size_t spmv_hyb_ws_bytes(int64_t tail_nnz)
+{
+    return spmv_coo_ws_bytes(tail_nnz);
+}
+
+// HYB: the ELL part (first K entries of every row)
+// writes y, then the row-sorted COO tail ADDS the remaining entries of the
+// long rows (staged COO kernel in accumulate mode + the deterministic carry
+// pass).  No atomics: bitwise reproducible.
+extern "C" int spmv_hyb_run(spmv_dims d, int32_t K, int64_t ld, int32_t ki, const int32_t *ell_col,
+                            const double *ell_val, int64_t tail_nnz, const int32_t *tail_row,
+                            const int32_t *tail_col, const double *tail_val, const double *x, double *y,
+                            void *ws, size_t ws_bytes)
+{
+    if (tail_nnz < 0)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_hyb_run: negative tail size");
+    int rc = spmv_ell_run(d, K, ld, ki, ell_col, ell_val, x, y);
+    if (rc != SPMV_SUCCESS || tail_nnz == 0 || d.n_rows == 0)
+        return rc;
+    if (!ws || ws_bytes < spmv_hyb_ws_bytes(tail_nnz))
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_hyb_run: workspace too small");
+    SPMV_GUARD(d);
+    const int64_t tiles = (tail_nnz + coo_staged_tile() - 1) / coo_staged_tile();
+    double *carry_val = (double *)ws;
+    int32_t *carry_row = (int32_t *)(carry_val + tiles);
+    spmv_dims dt = d;
+    dt.nnz = tail_nnz;
+    rc = launch_coo_staged_acc(dt, tail_row, tail_col, tail_val, x, y, carry_row, carry_val);
+    if (rc != SPMV_SUCCESS)
+        return rc;
+    return launch_carry(tiles, carry_row, carry_val, y, (hipStream_t)d.stream);
+}

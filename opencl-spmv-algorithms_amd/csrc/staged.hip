@@ -120,7 +120,7 @@ __global__ __launch_bounds__(kBlock) void cmrs_staged_kernel(
 // writes y for rows (row[t0-1], row[t1-1]] (rows without entries get 0;
 // the last tile also covers the trailing rows).  A first row that began
 // in an earlier tile goes to carry[tile] for coo_carry_kernel (coo.hip).
-template <int L, int R>
+template <int L, int R, bool ACC = false>
 __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
     int64_t n_rows, int64_t nnz, const int32_t *__restrict__ row,
     const int32_t *__restrict__ col, const double *__restrict__ val,
@@ -164,6 +164,24 @@ __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
             carry_row[tile] = first_continues ? first : -1;
             carry_val[tile] = c;
         }
+    }
+    if constexpr (ACC) {
+        // accumulate mode (HYB tail): y[r] += the tile's entries of every row
+        // that begins here; rows without entries are left untouched, so only
+        // the row keys present are visited: one thread per run of equal keys,
+        // summed in entry order
+        for (int j = threadIdx.x; j < n; j += kBlock) {
+            const int32_t r = s_row[j];
+            const bool head = j == 0 ? r != prev : r != s_row[j - 1];
+            if (!head || (j == 0 && first_continues))
+                continue;
+            double s = 0.0;
+            int k = j;
+            for (; k < n && s_row[k] == r; ++k)
+                s += prod[k];
+            y[r] += s;
+        }
+        return;
     }
     // owned rows: (prev, last], plus the trailing empty rows in the last
     // tile; a continued first row equals prev, so it is excluded here
@@ -323,6 +341,22 @@ int launch_cmrs_staged(const spmv_dims &d, int32_t h, int64_t n_strips,
 }
 
 int64_t coo_staged_tile() { return 2 * kBlock * 3; }
+
+int launch_coo_staged_acc(const spmv_dims &d, const int32_t *row, const int32_t *col,
+                          const double *val, const double *x, double *y, int32_t *carry_row,
+                          double *carry_val)
+{
+    constexpr int R = 3;
+    const int64_t tiles = (d.nnz + coo_staged_tile() - 1) / coo_staged_tile();
+    if (tiles > INT32_MAX)
+        return fail_msg(SPMV_OTHER_ERROR, "coo tail: grid too large");
+    if (tiles == 0)
+        return SPMV_SUCCESS;
+    hipLaunchKernelGGL((coo_staged_kernel<4, R, true>), dim3((unsigned)tiles), dim3(kBlock), 0,
+                       (hipStream_t)d.stream, d.n_rows, d.nnz, row, col, val, x, y, carry_row, carry_val);
+    SPMV_CHECK_LAUNCH("coo_staged_kernel (accumulate)");
+    return SPMV_SUCCESS;
+}
 
 int launch_coo_staged(const spmv_dims &d, const int32_t *row, const int32_t *col,
                       const double *val, const double *x, double *y, int32_t *carry_row,

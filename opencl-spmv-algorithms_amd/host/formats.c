@@ -332,6 +332,94 @@ int spmv_cmrs_build(int64_t n_rows, const int64_t *row_ptr, int32_t h,
     return SPMV_SUCCESS;
 }
 
+/* ------------------------------------------------------------------ HYB */
+
+int spmv_hyb_plan(int64_t n_rows, const int64_t *row_ptr, int32_t ki, int32_t K_req, int32_t *K,
+                  int64_t *ld, int64_t *tail_nnz)
+{
+    if ((ki != 1 && ki != 2) || n_rows < 0 || !K || !ld || !tail_nnz)
+        return SPMV_OTHER_ERROR;
+    const int64_t ldv = round_up(n_rows, 64);
+    int64_t mx = 0, nnz = n_rows > 0 ? row_ptr[n_rows] - row_ptr[0] : 0;
+    spmv_csr_row_stats(n_rows, row_ptr, NULL, &mx, NULL);
+    int64_t k = K_req;
+    if (k <= 0) {
+        /* width that minimises stored bytes: 12 per ELL slot (all ld rows),
+         * 16 per tail entry (row, col, val) */
+        const int64_t cap = mx < 65536 ? mx : 65536;
+        int64_t *cnt = (int64_t *)calloc((size_t)cap + 2, sizeof(int64_t));
+        if (!cnt)
+            return SPMV_OTHER_ERROR;
+        for (int64_t r = 0; r < n_rows; ++r) {
+            const int64_t l = row_ptr[r + 1] - row_ptr[r];
+            cnt[l < cap ? l : cap]++;
+        }
+        int64_t gt = n_rows - cnt[0]; /* rows longer than kk */
+        int64_t tail = nnz, best_k = 0;
+        double best = 16.0 * (double)tail;
+        for (int64_t kk = 1; kk <= cap; ++kk) {
+            tail -= gt;           /* every row longer than kk-1 moves one entry */
+            gt -= cnt[kk];        /* rows longer than kk */
+            const double cost = 12.0 * (double)ldv * (double)kk + 16.0 * (double)tail;
+            if (cost < best) {
+                best = cost;
+                best_k = kk;
+            }
+        }
+        free(cnt);
+        k = best_k;
+    }
+    k = round_up(k, ki);
+    if (k > INT32_MAX)
+        return SPMV_OTHER_ERROR;
+    int64_t tail = 0;
+    for (int64_t r = 0; r < n_rows; ++r) {
+        const int64_t l = row_ptr[r + 1] - row_ptr[r];
+        tail += l > k ? l - k : 0;
+    }
+    *K = (int32_t)k;
+    *ld = ldv;
+    *tail_nnz = tail;
+    return SPMV_SUCCESS;
+}
+
+int spmv_hyb_fill(int64_t n_rows, const int64_t *row_ptr, const int32_t *col, const double *val,
+                  int32_t K, int64_t ld, int32_t ki, int32_t *ell_col, double *ell_val,
+                  int32_t *tail_row, int32_t *tail_col, double *tail_val)
+{
+    if ((ki != 1 && ki != 2) || K < 0 || K % ki != 0 || ld < n_rows || ld % 64 != 0)
+        return SPMV_OTHER_ERROR;
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < ld; ++i) {
+        int64_t b = 0, e = 0;
+        if (i < n_rows) {
+            b = row_ptr[i];
+            e = row_ptr[i + 1];
+        }
+        const int32_t pad_col = e > b ? col[(e - b > K ? b + K : e) - 1] : 0;
+        for (int64_t k = 0; k < K; ++k) {
+            const int64_t pos = (k / ki) * ld * ki + i * ki + (k % ki);
+            if (b + k < e) {
+                ell_col[pos] = col[b + k];
+                ell_val[pos] = val[b + k];
+            } else {
+                ell_col[pos] = pad_col;
+                ell_val[pos] = 0.0;
+            }
+        }
+    }
+    /* tail: entries past the first K of each row, in CSR (row-sorted) order */
+    int64_t t = 0;
+    for (int64_t r = 0; r < n_rows; ++r)
+        for (int64_t j = row_ptr[r] + K; j < row_ptr[r + 1]; ++j) {
+            tail_row[t] = (int32_t)r;
+            tail_col[t] = col[j];
+            tail_val[t] = val[j];
+            ++t;
+        }
+    return SPMV_SUCCESS;
+}
+
 /* ------------------------------------------- CSR, 16-bit column offsets */
 
 /* smallest column of block b and whether the block's span fits 16 bits */

@@ -27,7 +27,7 @@ LIB_DIR = PKG_DIR / "lib"
 REPO_DIR = PKG_DIR.parent
 
 FORMATS = ("coo", "csr", "ell", "sell", "cmrs")  # the reference's five
-EXTRA_FORMATS = ("csr16",)  # CSR with 16-bit column offsets
+EXTRA_FORMATS = ("csr16", "hyb")  # §8f row 4: CSR with 16-bit column offsets; ELL + COO tail
 ALL_FORMATS = FORMATS + EXTRA_FORMATS
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
@@ -84,6 +84,9 @@ HIP_SYMBOLS = {
     "spmv_csr_tiled_ws_bytes": (ctypes.c_size_t, [_c_i64, _c_i64]),
     "spmv_csr_run_tiled": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t]),
     "spmv_csr16_run": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_int]),
+    "spmv_hyb_ws_bytes": (ctypes.c_size_t, [_c_i64]),
+    "spmv_hyb_run": (ctypes.c_int, [Dims, _c_i32, _c_i64, _c_i32, _vp, _vp, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp,
+                                    ctypes.c_size_t]),
     "spmv_csr_xwin_bytes": (ctypes.c_size_t, [_c_i64, _c_i64, ctypes.c_int, _c_i32]),
     "spmv_csr_xwin_build": (ctypes.c_int, [Dims, _vp, _vp, ctypes.c_int, _c_i32, _vp, ctypes.c_size_t,
                                            ctypes.POINTER(_c_i32)]),
@@ -151,6 +154,9 @@ HOST_SYMBOLS = {
     "spmv_cmrs_build": (ctypes.c_int, [_c_i64, _vp, _c_i32, _vp, _vp]),
     "spmv_partition_rows": (ctypes.c_int, [_c_i64, _vp, ctypes.c_int, _c_i64, _vp]),
     "spmv_csr16_plan": (ctypes.c_int, [_c_i64, _vp, ctypes.POINTER(_c_i64), ctypes.POINTER(_c_i64)]),
+    "spmv_hyb_plan": (ctypes.c_int, [_c_i64, _vp, _c_i32, _c_i32, ctypes.POINTER(_c_i32), ctypes.POINTER(_c_i64),
+                                     ctypes.POINTER(_c_i64)]),
+    "spmv_hyb_fill": (ctypes.c_int, [_c_i64, _vp, _vp, _vp, _c_i32, _c_i64, _c_i32, _vp, _vp, _vp, _vp, _vp]),
     "spmv_csr16_fill": (ctypes.c_int, [_c_i64, _vp, _vp, _vp, _vp]),
     "spmv_cpu_coo": (ctypes.c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, ctypes.c_int]),
     "spmv_cpu_csr": (ctypes.c_int, [_c_i64, _vp, _vp, _vp, _vp, _vp, ctypes.c_int]),
@@ -374,6 +380,21 @@ def cmrs_build(n_rows: int, ptr, h: int = 8):
     return dict(h=h, n_strips=ns, strip_ptr=sp, row_in_strip=rin)
 
 
+def hyb_build(n_rows: int, ptr, col, val, ki: int = 2, K: int = 0):
+    """ELL part (first K entries per row) + row-sorted COO tail (§8f row 4)."""
+    Kc, ld, tail = _c_i32(0), _c_i64(0), _c_i64(0)
+    _check_host(host_lib().spmv_hyb_plan(n_rows, _ptr(ptr), ki, K, ctypes.byref(Kc), ctypes.byref(ld),
+                                         ctypes.byref(tail)), "hyb_plan")
+    stored = Kc.value * ld.value
+    ec, ev = np.empty(max(stored, 1), np.int32), np.empty(max(stored, 1), np.float64)
+    tr, tc = np.empty(max(tail.value, 1), np.int32), np.empty(max(tail.value, 1), np.int32)
+    tv = np.empty(max(tail.value, 1), np.float64)
+    _check_host(host_lib().spmv_hyb_fill(n_rows, _ptr(ptr), _ptr(col), _ptr(val), Kc.value, ld.value, ki, _ptr(ec),
+                                         _ptr(ev), _ptr(tr), _ptr(tc), _ptr(tv)), "hyb_fill")
+    return dict(K=Kc.value, ld=ld.value, ki=ki, stored=stored, tail_nnz=tail.value, ell_col=ec, ell_val=ev,
+                tail_row=tr, tail_col=tc, tail_val=tv)
+
+
 def csr16_build(col: np.ndarray):
     """16-bit column offsets per 64-entry block."""
     nnz = int(col.shape[0])
@@ -479,6 +500,10 @@ class DeviceMatrix:
         elif self.fmt == "csr16":
             rc = lib.spmv_csr16_run(d, _ptr(a["row_ptr"]), _ptr(a["blk_base"]), _ptr(a["col_off"]),
                                     _ptr(a["col_esc"]), _ptr(a["val"]), _ptr(x), _ptr(y), p["lanes"])
+        elif self.fmt == "hyb":
+            rc = lib.spmv_hyb_run(d, p["K"], p["ld"], p["ki"], _ptr(a["ell_col"]), _ptr(a["ell_val"]), p["tail_nnz"],
+                                  _ptr(a["tail_row"]), _ptr(a["tail_col"]), _ptr(a["tail_val"]), _ptr(x), _ptr(y),
+                                  _ptr(a["ws"]), a["ws"].numel())
         elif self.fmt == "ell" and "win" in a:
             rc = lib.spmv_ell_run_xwin(d, p["K"], p["ld"], p["ki"], _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
                                        _ptr(a["win"]), p["xcap"])
@@ -595,6 +620,13 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
         dm.stored_bytes = 12 * s["stored"] + 8 * (s["n_slices"] + 1) + 4 * s["n_slices"] * C
         if xwin:
             _sell_xwin(dm)
+    elif fmt == "hyb":
+        hb = hyb_build(m.n_rows, ptr, col, val, ki=ki or 2)
+        dm.params = dict(K=hb["K"], ld=hb["ld"], ki=hb["ki"], tail_nnz=hb["tail_nnz"], stored=hb["stored"])
+        ws = hip_lib().spmv_hyb_ws_bytes(hb["tail_nnz"])
+        dm.arrays = {k: _dev_tensor(hb[k], device) for k in ("ell_col", "ell_val", "tail_row", "tail_col", "tail_val")}
+        dm.arrays["ws"] = torch.empty(max(ws, 16), dtype=torch.uint8, device=device)
+        dm.stored_bytes = 12 * hb["stored"] + 16 * hb["tail_nnz"]
     elif fmt == "cmrs":
         c = cmrs_build(m.n_rows, ptr, h=h)
         dm.params = dict(h=h, n_strips=c["n_strips"])

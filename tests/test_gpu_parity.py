@@ -45,6 +45,8 @@ FMT_PARAMS = [
     ("sell", {"C": 64, "sigma": 1024, "ki": 1, "xwin": True}),
     ("sell", {"C": 32, "sigma": 64, "ki": 2, "xwin": True}),
     ("ell", {"ki": 2, "xwin": True}),
+    ("hyb", {}),
+    ("hyb", {"ki": 1}),
     ("csr", {"xwin": True}),
     ("csr", {"lanes": 2, "xwin": True}),
     ("sell", {"C": 64, "sigma": 1, "ki": 1}),
@@ -117,7 +119,7 @@ def test_cantlike_batch_random_x(torch_dev, fmt):
 
 
 @pytest.mark.parametrize("fmt,kw", [("coo", {}), ("csr", {}), ("csr", {"variant": 2}), ("csr", {"variant": 4}),
-                                    ("csr", {"variant": 5}), ("sell", {}), ("cmrs", {})])
+                                    ("csr", {"variant": 5}), ("sell", {}), ("cmrs", {}), ("hyb", {})])
 def test_rmat_skewed(torch_dev, fmt, kw):
     """R-MAT 1e6 rows / 1e7 entries: empty rows, rows of thousands of entries."""
     torch, dev = torch_dev
@@ -144,7 +146,7 @@ def test_ragged_long_rows(torch_dev, fmt, kw):
     assert_parity(m, y, x)
 
 
-@pytest.mark.parametrize("fmt,kw", [(f, {}) for f in sa.FORMATS] + [("csr", {"variant": 4}), ("csr", {"variant": 5})])
+@pytest.mark.parametrize("fmt,kw", [(f, {}) for f in sa.ALL_FORMATS] + [("csr", {"variant": 4}), ("csr", {"variant": 5})])
 def test_bitwise_reproducible(torch_dev, fmt, kw):
     """No atomics anywhere: two launches give identical bits (the reference
     COO's CAS-atomic order is nondeterministic)."""

@@ -273,3 +273,35 @@ def test_csr16_round_trip(kind):
         assert c["n_esc"] == 0
     if kind == "rmat":
         assert c["n_esc"] > 0.9 * c["n_blocks"]
+
+
+@pytest.mark.parametrize("kind,K", [("rmat", 0), ("rmat", 3), ("ragged", 0), ("cantlike", 0), ("tiny", 0)])
+def test_hyb_split_round_trip(kind, K):
+    """HYB (§8f row 4): ELL part + COO tail hold exactly the CSR entries,
+    each row's first K in the ELL slots, the rest row-sorted in the tail."""
+    if kind == "rmat":
+        m = sa.gen_rmat(100_000, 1_000_000, scale=17, seed=2)
+    elif kind == "ragged":
+        m = sa.gen_random(5_000, 5_000, 0, 300, seed=4)
+    elif kind == "cantlike":
+        m = sa.gen_cantlike(0)
+    else:
+        m = sa.read_mtx(GOLDEN / "empty_rows.mtx")
+    ptr, col, val = sa.csr_from_coo(m)
+    h = sa.hyb_build(m.n_rows, ptr, col, val, ki=2, K=K)
+    Kh, ld = h["K"], h["ld"]
+    if K:
+        assert Kh == K + (K % 2)
+    lens = np.diff(ptr)
+    assert h["tail_nnz"] == int(np.maximum(lens - Kh, 0).sum())
+    for i in range(0, m.n_rows, max(1, m.n_rows // 500)):
+        n_e = min(int(lens[i]), Kh)
+        for k in range(n_e):
+            pos = (k // 2) * ld * 2 + i * 2 + (k % 2)
+            assert h["ell_col"][pos] == col[ptr[i] + k] and h["ell_val"][pos] == val[ptr[i] + k]
+    t = h["tail_nnz"]
+    assert np.all(np.diff(h["tail_row"][:t].astype(np.int64)) >= 0)
+    if t:
+        # the tail is the CSR entries past K, in order
+        exp = np.concatenate([col[ptr[r] + Kh:ptr[r + 1]] for r in range(m.n_rows) if lens[r] > Kh])
+        assert np.array_equal(h["tail_col"][:t], exp)

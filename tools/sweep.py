@@ -34,20 +34,10 @@ VARIANTS = [
     ("cmrs", {"h": 8}), ("cmrs", {"h": 16}), ("cmrs", {"h": 32}),
     ("coo", {}),
     ("csr16", {"lanes": 4}), ("csr16", {"lanes": 2}), ("csr16", {"lanes": 8}),
-    # CSR x windows: rows per window x grid (one workgroup per window vs persistent)
-    ("sell", {"C": 64, "sigma": 1024, "ki": 1, "xwin": True}),
-    ("csr", {"lanes": 4, "variant": 3, "xwin": False, "env": {}}),
-    ("csr", {"lanes": 4, "variant": 3, "xwin": True, "xwin_rows": 64}),
-    ("csr", {"lanes": 4, "variant": 3, "xwin": True, "xwin_rows": 64, "env": {"SPMV_CSR_XWIN_PERSISTENT": "1"}}),
-    ("csr", {"lanes": 4, "variant": 3, "xwin": True, "xwin_rows": 128}),
-    ("csr", {"lanes": 4, "variant": 3, "xwin": True, "xwin_rows": 128, "env": {"SPMV_CSR_XWIN_PERSISTENT": "1"}}),
-    ("csr", {"lanes": 4, "variant": 3, "xwin": True, "xwin_rows": 256}),
-    ("csr", {"lanes": 4, "variant": 3, "xwin": True, "xwin_rows": 256, "env": {"SPMV_CSR_XWIN_PERSISTENT": "1"}}),
-    ("csr", {"lanes": 4, "variant": 3, "xwin": True, "xwin_rows": 512}),
-    ("csr", {"lanes": 4, "variant": 3, "xwin": True, "xwin_rows": 512, "env": {"SPMV_CSR_XWIN_PERSISTENT": "1"}}),
-    ("csr", {"lanes": 4, "variant": 3, "xwin": True, "xwin_rows": 1024}),
-    ("csr", {"lanes": 4, "variant": 3, "xwin": True, "xwin_rows": 1024, "env": {"SPMV_CSR_XWIN_PERSISTENT": "1"}}),
-    ("csr", {"lanes": 2, "variant": 3, "xwin": True, "xwin_rows": 256}),
+    # skewed matrices (--matrix rmat): HYB vs tiled CSR
+    ("hyb", {"env": {}}),
+    ("hyb", {"ki": 1, "env": {}}),
+    ("csr", {"variant": 4, "env": {}}),
 ]
 
 

@@ -82,6 +82,9 @@ def parse():
 
 def kernel_name(args, dm=None):
     """The dominant kernel as rocprofv3 names it (for profiles/)."""
+    params = (getattr(dm, "params", {}) or {}) if dm is not None else {}
+    if args.format == "cmrs" and params.get("variant") == 1:
+        return "cmrs_tiled_kernel"
     if dm is not None and "win" in getattr(dm, "arrays", {}):
         if args.format == "csr" and os.environ.get("SPMV_CSR_XWIN_DIRECT") == "1":
             return "csr_vector_xwin_kernel"
@@ -223,7 +226,7 @@ def build_workload(args, torch, dev, rank, world):
             bad, first = sa.check(loc, sa.ramp_x(loc.n_cols), y[:loc.n_rows].cpu().numpy())
             return f"row {first}" if bad else None
 
-        return dict(dm=dm, x=x, y=y, rows=loc.n_rows, nnz=loc.nnz,
+        return dict(dm=dm, x=x, y=y, loc=loc, rows=loc.n_rows, nnz=loc.nnz,
                     bytes_rank=sa.bytes_alg(loc.n_rows, loc.n_cols, loc.nnz), bytes_total=sa.bytes_alg(n, n, z),
                     nnz_total=z, max_rows=max_rows, check=check, scaling="strong",
                     data="synthetic: R-MAT (a,b,c,d)=(.57,.19,.19,.05), 1e7 rows, 1e8 entries, seed 1, x[j] = j",
@@ -378,6 +381,35 @@ def main():
     cant_single = None
     cpu = None
     do_pf = args.per_format == "yes" or (args.per_format == "auto" and world == 1)
+    if rank == 0 and do_pf and args.workload == "rmat":
+        # configs[3]: every format on the same R-MAT (ELL: N/A, padding)
+        m = w["loc"]
+        del dm, w["dm"]
+        torch.cuda.empty_cache()
+        per_format = {}
+        for fmt in sa.ALL_FORMATS:
+            kw = fmt_kwargs(args, fmt)
+            try:
+                d2 = sa.to_device(m, fmt, dev, **kw)
+            except sa.SpmvError as e:
+                per_format[fmt] = {"na": str(e)}
+                continue
+            _, k2 = time_steps(torch, d2, x, y, max(10, args.steps // 2), 3)
+            km = float(np.mean(k2))
+            bad2, _ = sa.check(m, sa.ramp_x(m.n_cols), y[:m.n_rows].cpu().numpy())
+            per_format[fmt] = {"GBs": round(bytes_step / (km * 1e-3) * 1e-9, 1),
+                               "GFLOPs": round(2 * nnz / (km * 1e-3) * 1e-9, 1),
+                               "frac": round(bytes_step / (km * 1e-3) * 1e-9 / sa.HBM_PEAK_GBS, 4),
+                               "kernel_ms": round(km, 5), "stored_MB": round(d2.stored_bytes * 1e-6, 1),
+                               "params": dict(kw, **{k: v for k, v in d2.params.items()
+                                                     if k in ("variant", "split_T", "n_chunks")}) or None,
+                               "parity_ok": bad2 == 0}
+            del d2
+            torch.cuda.empty_cache()
+        if args.cpu_seconds > 0:
+            ptr, col, val = sa.csr_from_coo(m)
+            cpu = cpu_baseline((ptr, col, val, m.n_rows, m.n_cols), 1, args.cpu_seconds)
+            cpu["sample"] = cpu["sample"].replace("the same 1-copy batch", "the same R-MAT")
     do_pf = do_pf and args.workload == "cantlike"
     if rank == 0 and do_pf:
         m, B = w["m"], args.copies

@@ -168,6 +168,19 @@ int spmv_sell_run(spmv_dims d, int32_t C, int32_t sigma, int32_t ki, int64_t n_s
  * run gathers from global memory).  spmv_sell_run_xwin copies x[lo..hi]
  * into LDS per workgroup and gathers from there; y is bit-identical to
  * spmv_sell_run's.                                                       */
+/* SELL with wide slices split (power-law matrices; plan from
+ * spmv_sell_split_plan in spmv_host.h, uploaded): the main kernel covers
+ * the first T slot columns of every slice (win = NULL: global x gathers,
+ * else the x-window kernel with win/xcap from spmv_sell_xwin_build); chunk
+ * c covers columns [chunk_k0[c], +T) of slice chunk_slice[c], one lane per
+ * slot, and the chunks of a slice are added to y[perm] in chunk order.
+ * `ws` holds spmv_sell_split_ws_bytes(n_chunks, C) bytes.               */
+size_t spmv_sell_split_ws_bytes(int64_t n_chunks, int32_t C);
+int spmv_sell_run_split(spmv_dims d, int32_t C, int32_t sigma, int32_t ki, int64_t n_slices,
+                        const int64_t *slice_ptr, const int32_t *perm, const int32_t *col,
+                        const double *val, const double *x, double *y, const void *win,
+                        int32_t xcap, int32_t T, int64_t n_chunks, const int32_t *chunk_slice,
+                        const int32_t *chunk_k0, void *ws, size_t ws_bytes);
 size_t spmv_sell_xwin_bytes(int64_t n_slices, int32_t C, int32_t sigma);
 int spmv_sell_xwin_build(spmv_dims d, int32_t C, int32_t sigma, int64_t n_slices,
                          const int64_t *slice_ptr, const int32_t *col, void *win,
@@ -190,6 +203,33 @@ int spmv_cmrs_run(spmv_dims d, int32_t h, int64_t n_strips,
                   const int64_t *strip_ptr, const uint8_t *row_in_strip,
                   const int32_t *col, const double *val, const double *x,
                   double *y);
+/* COO and CMRS with x windows in LDS (the protocol of the CSR/ELL/SELL
+ * x-window entry points): *_xwin_bytes sizes the window buffer,
+ * *_xwin_build fills it on the device (column range of every COO tile of
+ * the staged kernel / every CMRS strip run) and returns xcap, the LDS
+ * entries a workgroup stages (<= 2,048; 0 = none fits); *_run_xwin is the
+ * plain run with win/xcap appended.  A window wider than xcap gathers
+ * from global memory: y is bit-identical to the plain run.  The CMRS
+ * windows depend on d (n_rows and nnz pick the lanes per row).          */
+size_t spmv_coo_xwin_bytes(int64_t nnz);
+int spmv_coo_xwin_build(spmv_dims d, const int32_t *col, void *win, size_t win_bytes, int32_t *xcap);
+int spmv_coo_run_xwin(spmv_dims d, const int32_t *row, const int32_t *col, const double *val,
+                      const double *x, double *y, void *ws, size_t ws_bytes, const void *win,
+                      int32_t xcap);
+size_t spmv_cmrs_xwin_bytes(spmv_dims d, int32_t h, int64_t n_strips);
+int spmv_cmrs_xwin_build(spmv_dims d, int32_t h, int64_t n_strips, const int64_t *strip_ptr,
+                         const int32_t *col, void *win, size_t win_bytes, int32_t *xcap);
+int spmv_cmrs_run_xwin(spmv_dims d, int32_t h, int64_t n_strips, const int64_t *strip_ptr,
+                       const uint8_t *row_in_strip, const int32_t *col, const double *val,
+                       const double *x, double *y, const void *win, int32_t xcap);
+/* Entry-balanced CMRS for skewed strips (spmv_cmrs_pick_variant): every
+ * workgroup takes a fixed tile of entries; a strip spanning tiles leaves
+ * per-row partials for the deterministic carry pass.  `ws` holds
+ * spmv_cmrs_tiled_ws_bytes() bytes.  Same arrays as spmv_cmrs_run.      */
+size_t spmv_cmrs_tiled_ws_bytes(int64_t n_strips, int64_t nnz, int32_t h);
+int spmv_cmrs_run_tiled(spmv_dims d, int32_t h, int64_t n_strips, const int64_t *strip_ptr,
+                        const uint8_t *row_in_strip, const int32_t *col, const double *val,
+                        const double *x, double *y, void *ws, size_t ws_bytes);
 
 /* ------------------------------------------------- device generator ---
  * Rows [row_begin, row_end) of the banded matrix of BASELINE.json

@@ -109,6 +109,19 @@ int spmv_sell_fill(int64_t n_rows, const int64_t *row_ptr, const int32_t *col,
  * row_in_strip[nnz].                                                    */
 int spmv_cmrs_build(int64_t n_rows, const int64_t *row_ptr, int32_t h,
                     int64_t *strip_ptr, uint8_t *row_in_strip);
+/* 1 = entry-balanced (spmv_cmrs_run_tiled) when the longest strip exceeds
+ * both 4,096 entries and 64x the mean strip, else 0 (spmv_cmrs_run).    */
+int spmv_cmrs_pick_variant(int64_t n_strips, const int64_t *strip_ptr);
+
+/* SELL split plan for wide slices (spmv_sell_run_split).  _auto gives T
+ * (slot columns kept by the main kernel, a multiple of ki) or 0 when no
+ * slice is wider than both 1,024 and 16x the mean width.  _plan lists the
+ * chunks [k0, k0+T) beyond the first T columns of every slice, in slice
+ * order, and returns their count (arrays may be NULL: count only); -1 on
+ * bad arguments.                                                        */
+int32_t spmv_sell_split_auto(int64_t n_slices, const int64_t *slice_ptr, int32_t C, int32_t ki);
+int64_t spmv_sell_split_plan(int64_t n_slices, const int64_t *slice_ptr, int32_t C, int32_t T,
+                             int32_t *chunk_slice, int32_t *chunk_k0);
 
 /* HYB = ELL + COO tail: the first K entries of every
  * row in the column-major ELL layout of spmv_ell_fill (ld, ki), the rest

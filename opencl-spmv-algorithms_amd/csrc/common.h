@@ -33,12 +33,17 @@ class DeviceGuard {
 bool xcd_remap_enabled();
 
 // LDS-staged CMRS / COO launchers (staged.hip)
+// win != nullptr: the x-window kernels (win/xcap from *_xwin_build)
 int launch_cmrs_staged(const spmv_dims &d, int32_t h, int64_t n_strips,
                        const int64_t *strip_ptr, const uint8_t *rin, const int32_t *col,
-                       const double *val, const double *x, double *y);
+                       const double *val, const double *x, double *y, const int2 *win = nullptr,
+                       int32_t xcap = 0);
+void cmrs_geometry(const spmv_dims &d, int32_t h, int64_t n_strips, int *L, int *G, int64_t *blocks);
 int launch_coo_staged(const spmv_dims &d, const int32_t *row, const int32_t *col,
                       const double *val, const double *x, double *y, int32_t *carry_row,
-                      double *carry_val);
+                      double *carry_val, const int2 *win = nullptr, int32_t xcap = 0);
+// LDS entries of x a staged COO tile / CMRS strip run may stage (16 KiB)
+constexpr int32_t kStagedXwinCap = 2048;
 int64_t coo_staged_tile();
 // accumulate mode: y[r] += entries of the rows present (HYB tail)
 int launch_coo_staged_acc(const spmv_dims &d, const int32_t *row, const int32_t *col,
@@ -48,6 +53,10 @@ int launch_csr_tiled(const spmv_dims &d, const int64_t *row_ptr, const int32_t *
                      const double *val, const double *x, double *y, int32_t *own_lo,
                      int32_t *carry_row, double *carry_val);
 int64_t csr_tiled_tile();
+int launch_cmrs_tiled(const spmv_dims &d, int32_t h, int64_t n_strips, const int64_t *strip_ptr,
+                      const uint8_t *rin, const int32_t *col, const double *val, const double *x,
+                      double *y, int32_t *own_lo, int32_t *carry_row, double *carry_val);
+int64_t cmrs_tiled_tile();
 // the deterministic carry pass shared by COO and tiled CSR (coo.hip)
 int launch_carry(int64_t tiles, const int32_t *carry_row, const double *carry_val, double *y,
                  hipStream_t stream);

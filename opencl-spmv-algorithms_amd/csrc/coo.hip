@@ -345,3 +345,84 @@ extern "C" int spmv_cmrs_run(spmv_dims d, int32_t h, int64_t n_strips,
     SPMV_CHECK_LAUNCH("cmrs_kernel");
     return SPMV_SUCCESS;
 }
+
+extern "C" size_t spmv_cmrs_tiled_ws_bytes(int64_t n_strips, int64_t nnz, int32_t h)
+{
+    (void)n_strips;
+    if (h < 1)
+        return 0;
+    const int64_t tiles = nnz > 0 ? (nnz + cmrs_tiled_tile() - 1) / cmrs_tiled_tile() : 0;
+    // carry_val[h·tiles] f64, own_lo[tiles+1] i32, carry_row[h·tiles] i32
+    return (size_t)(8 * h * tiles + 4 * (tiles + 1) + 4 * h * tiles + 16);
+}
+
+// Entry-balanced CMRS (staged.hip cmrs_tiled_kernel): every workgroup
+// takes the same number of entries whatever the strips, for skewed
+// matrices (spmv_cmrs_pick_variant).  Same y as spmv_cmrs_run up to the
+// order of the fp64 sums of strips that span tiles.
+extern "C" int spmv_cmrs_run_tiled(spmv_dims d, int32_t h, int64_t n_strips, const int64_t *strip_ptr,
+                                   const uint8_t *row_in_strip, const int32_t *col, const double *val,
+                                   const double *x, double *y, void *ws, size_t ws_bytes)
+{
+    if (d.n_rows < 0 || d.nnz < 0 || h < 1 || h > 64)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_cmrs_run_tiled: h must be in [1,64]");
+    if (n_strips != (d.n_rows + h - 1) / h || d.n_rows > INT32_MAX)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_cmrs_run_tiled: n_strips != ceil(N/h)");
+    if (d.n_rows == 0)
+        return SPMV_SUCCESS;
+    SPMV_GUARD(d);
+    if (d.nnz == 0) {
+        hipError_t e = hipMemsetAsync(y, 0, (size_t)d.n_rows * sizeof(double), (hipStream_t)d.stream);
+        return e == hipSuccess ? SPMV_SUCCESS : fail(SPMV_PROGRAM_ERROR, "memset y", e);
+    }
+    if (!ws || ws_bytes < spmv_cmrs_tiled_ws_bytes(n_strips, d.nnz, h))
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_cmrs_run_tiled: workspace too small");
+    const int64_t tiles = (d.nnz + cmrs_tiled_tile() - 1) / cmrs_tiled_tile();
+    if (tiles * h > INT32_MAX)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_cmrs_run_tiled: grid too large");
+    double *carry_val = (double *)ws;
+    int32_t *own_lo = (int32_t *)(carry_val + (int64_t)h * tiles);
+    int32_t *carry_row = own_lo + tiles + 1;
+    return launch_cmrs_tiled(d, h, n_strips, strip_ptr, row_in_strip, col, val, x, y, own_lo, carry_row,
+                             carry_val);
+}
+
+extern "C" int spmv_coo_run_xwin(spmv_dims d, const int32_t *row, const int32_t *col, const double *val,
+                                 const double *x, double *y, void *ws, size_t ws_bytes, const void *win,
+                                 int32_t xcap)
+{
+    if (d.n_rows < 0 || d.nnz < 0 || d.n_rows > INT32_MAX)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_coo_run_xwin: bad sizes");
+    if (d.n_rows == 0 || d.nnz == 0)
+        return spmv_coo_run(d, row, col, val, x, y, ws, ws_bytes);
+    if (!win || xcap < 0 || xcap > kStagedXwinCap)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_coo_run_xwin: bad window arguments");
+    if (!ws || ws_bytes < spmv_coo_ws_bytes(d.nnz))
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_coo_run_xwin: workspace too small");
+    SPMV_GUARD(d);
+    const int64_t st_tiles = (d.nnz + coo_staged_tile() - 1) / coo_staged_tile();
+    double *cv = (double *)ws;
+    int32_t *cr = (int32_t *)(cv + st_tiles);
+    int rc = launch_coo_staged(d, row, col, val, x, y, cr, cv, (const int2 *)win, xcap);
+    if (rc != SPMV_SUCCESS)
+        return rc;
+    return launch_carry(st_tiles, cr, cv, y, (hipStream_t)d.stream);
+}
+
+extern "C" int spmv_cmrs_run_xwin(spmv_dims d, int32_t h, int64_t n_strips, const int64_t *strip_ptr,
+                                  const uint8_t *row_in_strip, const int32_t *col, const double *val,
+                                  const double *x, double *y, const void *win, int32_t xcap)
+{
+    if (d.n_rows < 0 || h < 1 || h > 64)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_cmrs_run_xwin: h must be in [1,64]");
+    if (n_strips != (d.n_rows + h - 1) / h)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_cmrs_run_xwin: n_strips != ceil(N/h)");
+    if (d.n_rows == 0)
+        return SPMV_SUCCESS;
+    if (d.nnz == 0)  // no windows were built
+        return spmv_cmrs_run(d, h, n_strips, strip_ptr, row_in_strip, col, val, x, y);
+    if (!win || xcap < 0 || xcap > kStagedXwinCap)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_cmrs_run_xwin: bad window arguments");
+    SPMV_GUARD(d);
+    return launch_cmrs_staged(d, h, n_strips, strip_ptr, row_in_strip, col, val, x, y, (const int2 *)win, xcap);
+}

@@ -99,7 +99,7 @@ __global__ __launch_bounds__(1024) void sell_kernel(
     int32_t C, int64_t n_slices, const int64_t *__restrict__ slice_ptr,
     const int32_t *__restrict__ perm, const int32_t *__restrict__ col,
     const double *__restrict__ val, const double *__restrict__ x,
-    double *__restrict__ y, int remap)
+    double *__restrict__ y, int remap, int64_t wcap)
 {
     const int64_t slot = xcd_block(remap) * (int64_t)blockDim.x + threadIdx.x;
     const int64_t s = slot / C;
@@ -107,7 +107,8 @@ __global__ __launch_bounds__(1024) void sell_kernel(
         return;
     const int64_t r = slot - s * C;
     const int64_t base = slice_ptr[s];
-    const int64_t w = (slice_ptr[s + 1] - base) / C;
+    int64_t w = (slice_ptr[s + 1] - base) / C;
+    w = w < wcap ? w : wcap;  // split plan: the rest of a wide slice is sell_split_kernel's
     const int64_t off = base + r * KI;
     const double sum = slot_dot<KI, NT, U>(val + off, col + off, w, (int64_t)C * KI, XGlobal{x});
     const int32_t row = perm[slot];
@@ -252,7 +253,7 @@ __global__ __launch_bounds__(1024) void sell_xwin_kernel(
     int32_t C, int64_t n_slices, const int64_t *__restrict__ slice_ptr,
     const int32_t *__restrict__ perm, const int32_t *__restrict__ col,
     const double *__restrict__ val, const double *__restrict__ x,
-    double *__restrict__ y, const int2 *__restrict__ win, int32_t xcap)
+    double *__restrict__ y, const int2 *__restrict__ win, int32_t xcap, int64_t wcap)
 {
     extern __shared__ double s_x[];
     const int2 wnd = win[blockIdx.x];
@@ -269,13 +270,64 @@ __global__ __launch_bounds__(1024) void sell_xwin_kernel(
         return;
     const int64_t r = slot - s * C;
     const int64_t base = slice_ptr[s];
-    const int64_t w = (slice_ptr[s + 1] - base) / C;
+    int64_t w = (slice_ptr[s + 1] - base) / C;
+    w = w < wcap ? w : wcap;
     const int64_t off = base + r * KI;
     const double sum = staged ? slot_dot<KI, NT, U>(val + off, col + off, w, (int64_t)C * KI, XWindow{s_x, wnd.x})
                               : slot_dot<KI, NT, U>(val + off, col + off, w, (int64_t)C * KI, XGlobal{x});
     const int32_t row = perm[slot];
     if (row >= 0)
         y[row] = sum;
+}
+
+// Wide slices (SELL split plan, spmv_sell_split_plan): a slice wider than
+// T slot columns keeps its first T in the main kernel; chunk c covers slot
+// columns [k0_c, k0_c + T) of slice s_c, one lane per slot, and leaves the
+// slot's partial sum in part[c·C + r].  sell_split_fix_kernel adds each
+// slice's chunks in chunk order to y[perm] (deterministic, no atomics).
+// An R-MAT hub slice (~1.4e5 slot columns) otherwise keeps one wave busy
+// for the whole kernel.
+template <int KI, bool NT, int U>
+__global__ __launch_bounds__(kBlock) void sell_split_kernel(
+    int32_t C, int64_t n_chunks, int32_t T, const int64_t *__restrict__ slice_ptr,
+    const int32_t *__restrict__ chunk_slice, const int32_t *__restrict__ chunk_k0,
+    const int32_t *__restrict__ col, const double *__restrict__ val, const double *__restrict__ x,
+    double *__restrict__ part)
+{
+    const int64_t gid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t c = gid / C;
+    if (c >= n_chunks)
+        return;
+    const int64_t r = gid - c * C;
+    const int64_t s = chunk_slice[c];
+    const int64_t k0 = chunk_k0[c];
+    const int64_t base = slice_ptr[s];
+    const int64_t w = (slice_ptr[s + 1] - base) / C;
+    const int64_t n = w - k0 < T ? w - k0 : T;
+    const int64_t off = base + k0 * C + r * KI;
+    part[gid] = slot_dot<KI, NT, U>(val + off, col + off, n, (int64_t)C * KI, XGlobal{x});
+}
+
+__global__ __launch_bounds__(kBlock) void sell_split_fix_kernel(int32_t C, int64_t n_chunks,
+                                                                const int32_t *__restrict__ chunk_slice,
+                                                                const int32_t *__restrict__ perm,
+                                                                const double *__restrict__ part,
+                                                                double *__restrict__ y)
+{
+    const int64_t gid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t c = gid / C;
+    if (c >= n_chunks)
+        return;
+    const int32_t s = chunk_slice[c];
+    if (c > 0 && chunk_slice[c - 1] == s)
+        return;  // not the first chunk of its slice
+    const int64_t r = gid - c * C;
+    double acc = 0.0;
+    for (int64_t u = c; u < n_chunks && chunk_slice[u] == s; ++u)
+        acc += part[u * C + r];
+    const int32_t row = perm[(int64_t)s * C + r];
+    if (row >= 0)
+        y[row] += acc;
 }
 
 constexpr int32_t kXwinCapWide = 8192;   // 64 KiB of LDS per 1024-slot workgroup (2 per CU)
@@ -307,7 +359,7 @@ extern "C" int spmv_sell_run(spmv_dims d, int32_t C, int32_t sigma, int32_t ki,
                         : (nt ? (u8 ? sell_kernel<1, true, 8> : sell_kernel<1, true, 4>)
                               : (u8 ? sell_kernel<1, false, 8> : sell_kernel<1, false, 4>));
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(bt), 0, (hipStream_t)d.stream, C,
-                       n_slices, slice_ptr, perm, col, val, x, y, remap);
+                       n_slices, slice_ptr, perm, col, val, x, y, remap, (int64_t)INT64_MAX);
     SPMV_CHECK_LAUNCH("sell_kernel");
     return SPMV_SUCCESS;
 }
@@ -391,7 +443,7 @@ extern "C" int spmv_sell_run_xwin(spmv_dims d, int32_t C, int32_t sigma, int32_t
                         : (nt ? sell_xwin_kernel<1, true, 4> : sell_xwin_kernel<1, false, 4>);
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(bt), (size_t)xcap * sizeof(double),
                        (hipStream_t)d.stream, C, n_slices, slice_ptr, perm, col, val, x, y,
-                       (const int2 *)win, xcap);
+                       (const int2 *)win, xcap, (int64_t)INT64_MAX);
     SPMV_CHECK_LAUNCH("sell_xwin_kernel");
     return SPMV_SUCCESS;
 }
@@ -517,4 +569,65 @@ extern "C" int spmv_hyb_run(spmv_dims d, int32_t K, int64_t ld, int32_t ki, cons
     if (rc != SPMV_SUCCESS)
         return rc;
     return launch_carry(tiles, carry_row, carry_val, y, (hipStream_t)d.stream);
+}
+
+extern "C" size_t spmv_sell_split_ws_bytes(int64_t n_chunks, int32_t C)
+{
+    return n_chunks > 0 && C > 0 ? (size_t)n_chunks * C * sizeof(double) : 0;
+}
+
+// SELL with the wide slices split (plan from spmv_sell_split_plan): the
+// main kernel covers the first T slot columns of every slice and writes y;
+// the chunks beyond go to sell_split_kernel, then sell_split_fix_kernel
+// adds them.  win = NULL runs the plain main kernel, else the x-window one.
+extern "C" int spmv_sell_run_split(spmv_dims d, int32_t C, int32_t sigma, int32_t ki, int64_t n_slices,
+                                   const int64_t *slice_ptr, const int32_t *perm, const int32_t *col,
+                                   const double *val, const double *x, double *y, const void *win,
+                                   int32_t xcap, int32_t T, int64_t n_chunks, const int32_t *chunk_slice,
+                                   const int32_t *chunk_k0, void *ws, size_t ws_bytes)
+{
+    int rc = sell_check_args(d, C, sigma, ki, n_slices, "spmv_sell_run_split");
+    if (rc != SPMV_SUCCESS)
+        return rc;
+    if (T <= 0 || T % ki != 0 || n_chunks < 0)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_run_split: T must be a positive multiple of ki");
+    if (d.n_rows == 0 || n_slices == 0)
+        return SPMV_SUCCESS;
+    if (n_chunks > 0 && (!chunk_slice || !chunk_k0 || !ws || ws_bytes < spmv_sell_split_ws_bytes(n_chunks, C)))
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_run_split: chunk plan or workspace missing");
+    if (win && (xcap < 0 || xcap > kXwinCapWide))
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_run_split: bad window arguments");
+    SPMV_GUARD(d);
+    int bt;
+    int64_t blocks;
+    sell_geometry(C, sigma, n_slices, &bt, &blocks);
+    const int64_t cblocks = (n_chunks * C + kBlock - 1) / kBlock;
+    if (blocks > INT32_MAX || cblocks > INT32_MAX)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_run_split: grid too large");
+    const hipStream_t st = (hipStream_t)d.stream;
+    const bool nt = stream_nt(kSellStreamNtDefault);
+    if (win) {
+        auto kern = ki == 2 ? (nt ? sell_xwin_kernel<2, true, 4> : sell_xwin_kernel<2, false, 4>)
+                            : (nt ? sell_xwin_kernel<1, true, 4> : sell_xwin_kernel<1, false, 4>);
+        hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(bt), (size_t)xcap * sizeof(double), st, C, n_slices,
+                           slice_ptr, perm, col, val, x, y, (const int2 *)win, xcap, (int64_t)T);
+    } else {
+        auto kern = ki == 2 ? (nt ? sell_kernel<2, true, 4> : sell_kernel<2, false, 4>)
+                            : (nt ? sell_kernel<1, true, 4> : sell_kernel<1, false, 4>);
+        hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(bt), 0, st, C, n_slices, slice_ptr, perm, col, val, x,
+                           y, 0, (int64_t)T);
+    }
+    SPMV_CHECK_LAUNCH("sell kernel (split main)");
+    if (n_chunks == 0)
+        return SPMV_SUCCESS;
+    double *part = (double *)ws;
+    auto sk = ki == 2 ? (nt ? sell_split_kernel<2, true, 4> : sell_split_kernel<2, false, 4>)
+                      : (nt ? sell_split_kernel<1, true, 4> : sell_split_kernel<1, false, 4>);
+    hipLaunchKernelGGL(sk, dim3((unsigned)cblocks), dim3(kBlock), 0, st, C, n_chunks, T, slice_ptr, chunk_slice,
+                       chunk_k0, col, val, x, part);
+    SPMV_CHECK_LAUNCH("sell_split_kernel");
+    hipLaunchKernelGGL(sell_split_fix_kernel, dim3((unsigned)cblocks), dim3(kBlock), 0, st, C, n_chunks,
+                       chunk_slice, perm, part, y);
+    SPMV_CHECK_LAUNCH("sell_split_fix_kernel");
+    return SPMV_SUCCESS;
 }

@@ -16,6 +16,8 @@
 // out-of-bounds tail store); COO replaces the reference's CAS-atomic coo
 // kernel (reference kernels/Coo.cl:4-32) — rows that start in an earlier
 // tile go through the same deterministic carry pass as coo.hip.
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace spmv {
@@ -37,11 +39,10 @@ __device__ __forceinline__ int lower_bound_lds(const K *keys, int lo, int hi, in
 // Streams entries [cb, ce) into LDS: products in s_prod, keys via `key`.
 // cb is even, so value pairs are 16-byte aligned; nothing at or past ce
 // is read.
-template <int R, typename KeyFn>
+template <int R, typename XS, typename KeyFn>
 __device__ __forceinline__ void stage_chunk(int64_t cb, int64_t ce, const int32_t *__restrict__ col,
-                                            const double *__restrict__ val,
-                                            const double *__restrict__ x, double2 *s_prod,
-                                            KeyFn key)
+                                            const double *__restrict__ val, const XS &xs,
+                                            double2 *s_prod, KeyFn key)
 {
 #pragma unroll
     for (int k = 0; k < R; ++k) {
@@ -51,11 +52,11 @@ __device__ __forceinline__ void stage_chunk(int64_t cb, int64_t ce, const int32_
         if (p + 1 < ce) {
             const double2 v = *reinterpret_cast<const double2 *>(val + p);
             const int2 c = *reinterpret_cast<const int2 *>(col + p);
-            pr.x = v.x * x[c.x];
-            pr.y = v.y * x[c.y];
+            pr.x = v.x * xs(c.x);
+            pr.y = v.y * xs(c.y);
             key(t, p, 2);
         } else if (p < ce) {
-            pr.x = val[p] * x[col[p]];
+            pr.x = val[p] * xs(col[p]);
             key(t, p, 1);
         }
         s_prod[t] = pr;
@@ -64,14 +65,20 @@ __device__ __forceinline__ void stage_chunk(int64_t cb, int64_t ce, const int32_
 
 // ------------------------------------------------------------------ CMRS
 // A workgroup owns G consecutive strips (G·h rows, L lanes per row).
-template <int L, int R>
+// XW: the workgroup's x window x[win.x .. win.y] (the column range of its
+// entry run, spmv_cmrs_xwin_build) is copied into LDS first and the
+// products gather from LDS; a window wider than xcap gathers from global
+// memory.  Same products, same order: y is bit-identical either way.
+template <int L, int R, bool XW>
 __global__ __launch_bounds__(kBlock) void cmrs_staged_kernel(
     int64_t n_rows, int32_t h, int32_t G, int64_t n_strips,
     const int64_t *__restrict__ strip_ptr, const uint8_t *__restrict__ rin,
     const int32_t *__restrict__ col, const double *__restrict__ val,
-    const double *__restrict__ x, double *__restrict__ y)
+    const double *__restrict__ x, double *__restrict__ y,
+    const int2 *__restrict__ win, int32_t xcap)
 {
     constexpr int CH = 2 * kBlock * R;
+    extern __shared__ double s_x[];
     __shared__ int64_t s_sp[kBlock + 1];
     __shared__ double2 s_prod[kBlock * R];
     __shared__ uint16_t s_key2[kBlock * R];  // keys of entry pairs
@@ -83,6 +90,17 @@ __global__ __launch_bounds__(kBlock) void cmrs_staged_kernel(
         const int64_t s = s0 + threadIdx.x;
         s_sp[threadIdx.x] = strip_ptr[s < n_strips ? s : n_strips];
     }
+    bool staged = false;  // uniform per workgroup
+    int32_t wlo = 0;
+    if constexpr (XW) {
+        const int2 wnd = win[blockIdx.x];
+        const int32_t span = wnd.y - wnd.x + 1;
+        staged = span > 0 && span <= xcap;
+        wlo = wnd.x;
+        if (staged)
+            for (int32_t i = threadIdx.x; i < span; i += kBlock)
+                s_x[i] = x[wlo + i];
+    }
     __syncthreads();
 
     const int rl = threadIdx.x / L, lane = threadIdx.x % L;
@@ -92,13 +110,17 @@ __global__ __launch_bounds__(kBlock) void cmrs_staged_kernel(
     const int64_t sb = s_sp[si], se = active ? s_sp[si + 1] : s_sp[si];
     const int64_t row = (s0 + si) * h + key;
     const int64_t blk_end = s_sp[G];
+    auto keys = [&](int t, int64_t p, int n) {
+        s_key2[t] = n == 2 ? *reinterpret_cast<const uint16_t *>(rin + p) : (uint16_t)rin[p];
+    };
 
     double acc = 0.0;
     for (int64_t cb = s_sp[0] & ~(int64_t)1; cb < blk_end; cb += CH) {
         const int64_t ce = cb + CH < blk_end ? cb + CH : blk_end;
-        stage_chunk<R>(cb, ce, col, val, x, s_prod, [&](int t, int64_t p, int n) {
-            s_key2[t] = n == 2 ? *reinterpret_cast<const uint16_t *>(rin + p) : (uint16_t)rin[p];
-        });
+        if (staged)
+            stage_chunk<R>(cb, ce, col, val, XWindow{s_x, wlo}, s_prod, keys);
+        else
+            stage_chunk<R>(cb, ce, col, val, XGlobal{x}, s_prod, keys);
         __syncthreads();
         const int64_t lo = sb > cb ? sb : cb;
         const int64_t hi = se < ce ? se : ce;
@@ -120,14 +142,16 @@ __global__ __launch_bounds__(kBlock) void cmrs_staged_kernel(
 // writes y for rows (row[t0-1], row[t1-1]] (rows without entries get 0;
 // the last tile also covers the trailing rows).  A first row that began
 // in an earlier tile goes to carry[tile] for coo_carry_kernel (coo.hip).
-template <int L, int R, bool ACC = false>
+// XW: the tile's x window in LDS (as cmrs_staged_kernel), bit-identical.
+template <int L, int R, bool ACC, bool XW>
 __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
     int64_t n_rows, int64_t nnz, const int32_t *__restrict__ row,
     const int32_t *__restrict__ col, const double *__restrict__ val,
     const double *__restrict__ x, double *__restrict__ y, int32_t *__restrict__ carry_row,
-    double *__restrict__ carry_val)
+    double *__restrict__ carry_val, const int2 *__restrict__ win, int32_t xcap)
 {
     constexpr int CH = 2 * kBlock * R;
+    extern __shared__ double s_x[];
     constexpr int GROUPS = kBlock / L;
     __shared__ double2 s_prod[kBlock * R];
     __shared__ int2 s_row2[kBlock * R];
@@ -141,9 +165,26 @@ __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
     const int n = (int)(t1 - t0);
     if (threadIdx.x == 0)
         s_prev = t0 > 0 ? row[t0 - 1] : -1;
-    stage_chunk<R>(t0, t1, col, val, x, s_prod, [&](int t, int64_t p, int cnt) {
+    auto keys = [&](int t, int64_t p, int cnt) {
         s_row2[t] = cnt == 2 ? *reinterpret_cast<const int2 *>(row + p) : make_int2(row[p], 0);
-    });
+    };
+    bool staged = false;  // uniform per workgroup
+    int32_t wlo = 0;
+    if constexpr (XW) {
+        const int2 wnd = win[tile];
+        const int32_t span = wnd.y - wnd.x + 1;
+        staged = span > 0 && span <= xcap;
+        wlo = wnd.x;
+        if (staged) {
+            for (int32_t i = threadIdx.x; i < span; i += kBlock)
+                s_x[i] = x[wlo + i];
+            __syncthreads();
+        }
+    }
+    if (staged)
+        stage_chunk<R>(t0, t1, col, val, XWindow{s_x, wlo}, s_prod, keys);
+    else
+        stage_chunk<R>(t0, t1, col, val, XGlobal{x}, s_prod, keys);
     __syncthreads();
 
     const int32_t prev = s_prev;
@@ -247,7 +288,7 @@ __global__ __launch_bounds__(kBlock) void csr_tiled_kernel(
     const int64_t t1 = t0 + CH < nnz ? t0 + CH : nnz;
     const int64_t r_lo = own_lo[tile];
     const int64_t r_hi = t1 == nnz ? n_rows - 1 : (int64_t)own_lo[tile + 1] - 1;
-    stage_chunk<R>(t0, t1, col, val, x, s_prod, [](int, int64_t, int) {});
+    stage_chunk<R>(t0, t1, col, val, XGlobal{x}, s_prod, [](int, int64_t, int) {});
     __syncthreads();
     const int g = threadIdx.x / L, lane = threadIdx.x % L;
 
@@ -280,6 +321,121 @@ __global__ __launch_bounds__(kBlock) void csr_tiled_kernel(
     }
 }
 
+// ------------------------------------------------------------ CMRS tiled
+// Entry-balanced CMRS for skewed strips (the R-MAT strip of rows 0-7 holds
+// ~3e5 entries; with one workgroup per run of strips that workgroup
+// streams it alone).  As csr_tiled_kernel: a workgroup owns a fixed tile of
+// CH entries; strip s is OWNED by the tile holding strip_ptr[s] (own_lo
+// from csr_tile_rows_kernel over strip_ptr), which writes all h rows of it
+// from its part of the strip.  The strip running into a tile from an
+// earlier one leaves up to h partial rows: carry[k·tiles + tile] for row
+// key k (k-major, so each row's continuation tiles are consecutive and
+// coo_carry_kernel adds them in tile order).  Needs kBlock / L >= h.
+template <int L, int R>
+__global__ __launch_bounds__(kBlock) void cmrs_tiled_kernel(
+    int64_t n_rows, int32_t h, int64_t n_strips, int64_t nnz, int64_t tiles,
+    const int64_t *__restrict__ strip_ptr, const uint8_t *__restrict__ rin,
+    const int32_t *__restrict__ col, const double *__restrict__ val,
+    const double *__restrict__ x, double *__restrict__ y,
+    const int32_t *__restrict__ own_lo, int32_t *__restrict__ carry_row,
+    double *__restrict__ carry_val)
+{
+    constexpr int CH = 2 * kBlock * R;
+    constexpr int GROUPS = kBlock / L;
+    __shared__ double2 s_prod[kBlock * R];
+    __shared__ uint16_t s_key2[kBlock * R];  // row keys of entry pairs
+    const uint8_t *s_key = reinterpret_cast<const uint8_t *>(s_key2);
+    const double *prod = reinterpret_cast<const double *>(s_prod);
+    const int64_t tile = blockIdx.x;
+    const int64_t t0 = tile * CH;
+    const int64_t t1 = t0 + CH < nnz ? t0 + CH : nnz;
+    const int64_t s_lo = own_lo[tile];
+    const int64_t s_hi = t1 == nnz ? n_strips - 1 : (int64_t)own_lo[tile + 1] - 1;
+    stage_chunk<R>(t0, t1, col, val, XGlobal{x}, s_prod, [&](int t, int64_t p, int n) {
+        s_key2[t] = n == 2 ? *reinterpret_cast<const uint16_t *>(rin + p) : (uint16_t)rin[p];
+    });
+    __syncthreads();
+    const int g = threadIdx.x / L, lane = threadIdx.x % L;
+
+    // carried strip: entry t0 lies in strip s_lo-1 when no strip starts at t0
+    if (g < h) {
+        double c = 0.0;
+        int32_t cr = -1;
+        if (s_lo > 0 && (s_lo == n_strips || strip_ptr[s_lo] > t0)) {
+            const int64_t e64 = s_lo < n_strips && strip_ptr[s_lo] < t1 ? strip_ptr[s_lo] : t1;
+            const int e = (int)(e64 - t0);
+            const int a = lower_bound_lds(s_key, 0, e, g);
+            const int b = lower_bound_lds(s_key, a, e, g + 1);
+            for (int j = a + lane; j < b; j += L)
+                c += prod[j];
+            const int64_t r = (s_lo - 1) * h + g;
+            if (b > a && r < n_rows)
+                cr = (int32_t)r;
+        }
+        c = group_sum<L>(c);
+        if (lane == 0) {
+            carry_row[(int64_t)g * tiles + tile] = cr;
+            carry_val[(int64_t)g * tiles + tile] = c;
+        }
+    }
+    // owned strips, one L-lane group per row
+    const int64_t items = (s_hi - s_lo + 1) * h;
+    for (int64_t it = g; it < items; it += GROUPS) {
+        const int64_t s = s_lo + it / h;
+        const int k = (int)(it % h);
+        const int64_t sa = strip_ptr[s];
+        int64_t sb = strip_ptr[s + 1];
+        sb = sb < t1 ? sb : t1;
+        double acc = 0.0;
+        if (sa < sb) {
+            const int a = lower_bound_lds(s_key, (int)(sa - t0), (int)(sb - t0), k);
+            const int b = lower_bound_lds(s_key, a, (int)(sb - t0), k + 1);
+            for (int j = a + lane; j < b; j += L)
+                acc += prod[j];
+        }
+        acc = group_sum<L>(acc);
+        const int64_t r = s * h + k;
+        if (lane == 0 && r < n_rows)
+            y[r] = acc;
+    }
+}
+
+int64_t cmrs_tiled_tile() { return 2 * kBlock * 3; }
+
+int launch_cmrs_tiled(const spmv_dims &d, int32_t h, int64_t n_strips, const int64_t *strip_ptr,
+                      const uint8_t *rin, const int32_t *col, const double *val, const double *x,
+                      double *y, int32_t *own_lo, int32_t *carry_row, double *carry_val)
+{
+    constexpr int R = 3;
+    const int64_t ch = cmrs_tiled_tile();
+    const int64_t tiles = (d.nnz + ch - 1) / ch;
+    const hipStream_t st = (hipStream_t)d.stream;
+    hipLaunchKernelGGL(csr_tile_rows_kernel, dim3((unsigned)((tiles + 1 + kBlock - 1) / kBlock)),
+                       dim3(kBlock), 0, st, n_strips, d.nnz, tiles, ch, strip_ptr, own_lo);
+    SPMV_CHECK_LAUNCH("csr_tile_rows_kernel (strips)");
+    // lanes per row as the staged kernels (one per ~16 entries of the mean
+    // row), at most kBlock / h so every carried row key has its group
+    int L = spmv_csr_auto_lanes(d.n_rows, d.nnz);
+    while (L > 1 && L * h > kBlock)
+        L >>= 1;
+#define SPMV_CMRS_TILED(LL)                                                                        \
+    hipLaunchKernelGGL((cmrs_tiled_kernel<LL, R>), dim3((unsigned)tiles), dim3(kBlock), 0, st,     \
+                       d.n_rows, h, n_strips, d.nnz, tiles, strip_ptr, rin, col, val, x, y, own_lo, \
+                       carry_row, carry_val)
+    switch (L) {
+    case 1: SPMV_CMRS_TILED(1); break;
+    case 2: SPMV_CMRS_TILED(2); break;
+    case 4: SPMV_CMRS_TILED(4); break;
+    case 8: SPMV_CMRS_TILED(8); break;
+    case 16: SPMV_CMRS_TILED(16); break;
+    case 32: SPMV_CMRS_TILED(32); break;
+    default: SPMV_CMRS_TILED(64); break;
+    }
+#undef SPMV_CMRS_TILED
+    SPMV_CHECK_LAUNCH("cmrs_tiled_kernel");
+    return launch_carry((int64_t)h * tiles, carry_row, carry_val, y, st);
+}
+
 int64_t csr_tiled_tile() { return 2 * kBlock * 3; }
 
 int launch_csr_tiled(const spmv_dims &d, const int64_t *row_ptr, const int32_t *col,
@@ -308,24 +464,42 @@ int launch_csr_tiled(const spmv_dims &d, const int64_t *row_ptr, const int32_t *
 }
 
 // ----------------------------------------------------------- launchers
+// Geometry of the strip-run CMRS kernel: lanes per row as the staged CSR
+// (one per ~16 entries of the mean row), at most 256/h so one strip fits a
+// workgroup; G strips per workgroup.  The x windows use the same G.
+void cmrs_geometry(const spmv_dims &d, int32_t h, int64_t n_strips, int *L, int *G, int64_t *blocks)
+{
+    int l = spmv_csr_auto_lanes(d.n_rows, d.nnz);
+    while (l > 1 && l * h > kBlock)
+        l >>= 1;
+    *L = l;
+    *G = kBlock / (l * h) > 0 ? kBlock / (l * h) : 1;
+    *blocks = (n_strips + *G - 1) / *G;
+}
+
 int launch_cmrs_staged(const spmv_dims &d, int32_t h, int64_t n_strips,
                        const int64_t *strip_ptr, const uint8_t *rin, const int32_t *col,
-                       const double *val, const double *x, double *y)
+                       const double *val, const double *x, double *y, const int2 *win, int32_t xcap)
 {
-    // lanes per row: one per ~16 entries of the mean row (as staged CSR),
-    // at most 256/h so one strip fits a workgroup
-    int L = spmv_csr_auto_lanes(d.n_rows, d.nnz);
-    while (L > 1 && L * h > kBlock)
-        L >>= 1;
-    const int G = kBlock / (L * h) > 0 ? kBlock / (L * h) : 1;
-    const int64_t blocks = (n_strips + G - 1) / G;
+    int L, G;
+    int64_t blocks;
+    cmrs_geometry(d, h, n_strips, &L, &G, &blocks);
     if (blocks > INT32_MAX)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_cmrs_run: grid too large");
     const hipStream_t st = (hipStream_t)d.stream;
     constexpr int R = 3;
-#define SPMV_CMRS_STAGED(LL)                                                                    \
-    hipLaunchKernelGGL((cmrs_staged_kernel<LL, R>), dim3((unsigned)blocks), dim3(kBlock), 0, st, \
-                       d.n_rows, h, G, n_strips, strip_ptr, rin, col, val, x, y)
+    const size_t lds = win ? (size_t)xcap * sizeof(double) : 0;
+#define SPMV_CMRS_STAGED(LL)                                                                            \
+    do {                                                                                                \
+        if (win)                                                                                        \
+            hipLaunchKernelGGL((cmrs_staged_kernel<LL, R, true>), dim3((unsigned)blocks), dim3(kBlock),  \
+                               lds, st, d.n_rows, h, G, n_strips, strip_ptr, rin, col, val, x, y, win,   \
+                               xcap);                                                                   \
+        else                                                                                            \
+            hipLaunchKernelGGL((cmrs_staged_kernel<LL, R, false>), dim3((unsigned)blocks), dim3(kBlock), \
+                               0, st, d.n_rows, h, G, n_strips, strip_ptr, rin, col, val, x, y,          \
+                               (const int2 *)nullptr, 0);                                               \
+    } while (0)
     switch (L) {
     case 1: SPMV_CMRS_STAGED(1); break;
     case 2: SPMV_CMRS_STAGED(2); break;
@@ -352,34 +526,155 @@ int launch_coo_staged_acc(const spmv_dims &d, const int32_t *row, const int32_t 
         return fail_msg(SPMV_OTHER_ERROR, "coo tail: grid too large");
     if (tiles == 0)
         return SPMV_SUCCESS;
-    hipLaunchKernelGGL((coo_staged_kernel<4, R, true>), dim3((unsigned)tiles), dim3(kBlock), 0,
-                       (hipStream_t)d.stream, d.n_rows, d.nnz, row, col, val, x, y, carry_row, carry_val);
+    hipLaunchKernelGGL((coo_staged_kernel<4, R, true, false>), dim3((unsigned)tiles), dim3(kBlock), 0,
+                       (hipStream_t)d.stream, d.n_rows, d.nnz, row, col, val, x, y, carry_row, carry_val,
+                       (const int2 *)nullptr, 0);
     SPMV_CHECK_LAUNCH("coo_staged_kernel (accumulate)");
     return SPMV_SUCCESS;
 }
 
 int launch_coo_staged(const spmv_dims &d, const int32_t *row, const int32_t *col,
                       const double *val, const double *x, double *y, int32_t *carry_row,
-                      double *carry_val)
+                      double *carry_val, const int2 *win, int32_t xcap)
 {
     constexpr int R = 3;
     const int64_t tiles = (d.nnz + coo_staged_tile() - 1) / coo_staged_tile();
     if (tiles > INT32_MAX)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_coo_run: grid too large");
     const hipStream_t st = (hipStream_t)d.stream;
+    const size_t lds = win ? (size_t)xcap * sizeof(double) : 0;
     // rows per tile ~ tile / mean row length; 4 lanes per row unless rows are long
     const double mean = d.n_rows > 0 ? (double)d.nnz / (double)d.n_rows : 0.0;
+#define SPMV_COO_STAGED(LL)                                                                              \
+    do {                                                                                                 \
+        if (win)                                                                                         \
+            hipLaunchKernelGGL((coo_staged_kernel<LL, R, false, true>), dim3((unsigned)tiles),            \
+                               dim3(kBlock), lds, st, d.n_rows, d.nnz, row, col, val, x, y, carry_row,    \
+                               carry_val, win, xcap);                                                    \
+        else                                                                                             \
+            hipLaunchKernelGGL((coo_staged_kernel<LL, R, false, false>), dim3((unsigned)tiles),           \
+                               dim3(kBlock), 0, st, d.n_rows, d.nnz, row, col, val, x, y, carry_row,      \
+                               carry_val, (const int2 *)nullptr, 0);                                     \
+    } while (0)
     if (mean >= 48.0)
-        hipLaunchKernelGGL((coo_staged_kernel<8, R>), dim3((unsigned)tiles), dim3(kBlock), 0, st,
-                           d.n_rows, d.nnz, row, col, val, x, y, carry_row, carry_val);
+        SPMV_COO_STAGED(8);
     else if (mean >= 12.0)
-        hipLaunchKernelGGL((coo_staged_kernel<4, R>), dim3((unsigned)tiles), dim3(kBlock), 0, st,
-                           d.n_rows, d.nnz, row, col, val, x, y, carry_row, carry_val);
+        SPMV_COO_STAGED(4);
     else
-        hipLaunchKernelGGL((coo_staged_kernel<2, R>), dim3((unsigned)tiles), dim3(kBlock), 0, st,
-                           d.n_rows, d.nnz, row, col, val, x, y, carry_row, carry_val);
+        SPMV_COO_STAGED(2);
+#undef SPMV_COO_STAGED
     SPMV_CHECK_LAUNCH("coo_staged_kernel");
     return SPMV_SUCCESS;
 }
 
+// ------------------------------------------------------------ x windows
+// Column range of every COO tile / CMRS strip run (build time, one pass
+// over col), and the LDS size of a run: the widest window up to the cap.
+__global__ __launch_bounds__(kBlock) void tile_window_kernel(int64_t nnz, int64_t per,
+                                                             const int32_t *__restrict__ col,
+                                                             int2 *__restrict__ win)
+{
+    const int64_t e0 = (int64_t)blockIdx.x * per;
+    const int64_t e1 = e0 + per < nnz ? e0 + per : nnz;
+    const int2 r = block_col_range(col, e0, e1);
+    if (threadIdx.x == 0)
+        win[blockIdx.x] = r;
+}
+
+__global__ __launch_bounds__(kBlock) void cmrs_window_kernel(int64_t n_strips, int32_t G,
+                                                             const int64_t *__restrict__ strip_ptr,
+                                                             const int32_t *__restrict__ col,
+                                                             int2 *__restrict__ win)
+{
+    const int64_t s0 = (int64_t)blockIdx.x * G;
+    const int64_t s1 = s0 + G < n_strips ? s0 + G : n_strips;
+    const int2 r = block_col_range(col, strip_ptr[s0], strip_ptr[s1]);
+    if (threadIdx.x == 0)
+        win[blockIdx.x] = r;
+}
+
+static int windows_xcap(const int2 *win, int64_t n, int32_t cap, hipStream_t st, int32_t *xcap,
+                        const char *who)
+{
+    int2 *h = (int2 *)malloc((size_t)n * sizeof(int2));
+    if (!h)
+        return fail_msg(SPMV_OTHER_ERROR, who);
+    hipError_t e = hipMemcpyAsync(h, win, (size_t)n * sizeof(int2), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess)
+        e = hipStreamSynchronize(st);
+    if (e != hipSuccess) {
+        free(h);
+        return fail(SPMV_PROGRAM_ERROR, who, e);
+    }
+    int32_t best = 0;
+    for (int64_t b = 0; b < n; ++b) {
+        const int64_t span = (int64_t)h[b].y - h[b].x + 1;
+        if (span <= cap && span > best)
+            best = (int32_t)span;
+    }
+    free(h);
+    *xcap = best;
+    return SPMV_SUCCESS;
+}
+
 }  // namespace spmv
+
+using namespace spmv;
+
+extern "C" size_t spmv_coo_xwin_bytes(int64_t nnz)
+{
+    return nnz > 0 ? (size_t)((nnz + coo_staged_tile() - 1) / coo_staged_tile()) * sizeof(int2) : 0;
+}
+
+extern "C" int spmv_coo_xwin_build(spmv_dims d, const int32_t *col, void *win, size_t win_bytes, int32_t *xcap)
+{
+    if (d.nnz < 0 || !xcap)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_coo_xwin_build: bad arguments");
+    *xcap = 0;
+    if (d.nnz == 0 || d.n_rows == 0)
+        return SPMV_SUCCESS;
+    if (!win || win_bytes < spmv_coo_xwin_bytes(d.nnz))
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_coo_xwin_build: window buffer too small");
+    SPMV_GUARD(d);
+    const int64_t tiles = (d.nnz + coo_staged_tile() - 1) / coo_staged_tile();
+    if (tiles > INT32_MAX)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_coo_xwin_build: grid too large");
+    const hipStream_t st = (hipStream_t)d.stream;
+    hipLaunchKernelGGL(tile_window_kernel, dim3((unsigned)tiles), dim3(kBlock), 0, st, d.nnz, coo_staged_tile(), col,
+                       (int2 *)win);
+    SPMV_CHECK_LAUNCH("tile_window_kernel");
+    return windows_xcap((const int2 *)win, tiles, kStagedXwinCap, st, xcap, "spmv_coo_xwin_build: copy windows");
+}
+
+extern "C" size_t spmv_cmrs_xwin_bytes(spmv_dims d, int32_t h, int64_t n_strips)
+{
+    if (h < 1 || h > 64 || n_strips <= 0 || d.nnz <= 0)
+        return 0;
+    int L, G;
+    int64_t blocks;
+    cmrs_geometry(d, h, n_strips, &L, &G, &blocks);
+    return (size_t)blocks * sizeof(int2);
+}
+
+extern "C" int spmv_cmrs_xwin_build(spmv_dims d, int32_t h, int64_t n_strips, const int64_t *strip_ptr,
+                                    const int32_t *col, void *win, size_t win_bytes, int32_t *xcap)
+{
+    if (d.n_rows < 0 || d.nnz < 0 || h < 1 || h > 64 || !xcap || n_strips != (d.n_rows + h - 1) / h)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_cmrs_xwin_build: bad arguments");
+    *xcap = 0;
+    if (d.n_rows == 0 || d.nnz == 0)
+        return SPMV_SUCCESS;
+    if (!win || win_bytes < spmv_cmrs_xwin_bytes(d, h, n_strips))
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_cmrs_xwin_build: window buffer too small");
+    SPMV_GUARD(d);
+    int L, G;
+    int64_t blocks;
+    cmrs_geometry(d, h, n_strips, &L, &G, &blocks);
+    if (blocks > INT32_MAX)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_cmrs_xwin_build: grid too large");
+    const hipStream_t st = (hipStream_t)d.stream;
+    hipLaunchKernelGGL(cmrs_window_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, st, n_strips, G, strip_ptr, col,
+                       (int2 *)win);
+    SPMV_CHECK_LAUNCH("cmrs_window_kernel");
+    return windows_xcap((const int2 *)win, blocks, kStagedXwinCap, st, xcap, "spmv_cmrs_xwin_build: copy windows");
+}

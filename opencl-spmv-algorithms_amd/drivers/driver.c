@@ -259,6 +259,10 @@ typedef struct {
     int32_t xcap;
     int32_t K, C, sigma, ki, h, lanes, variant;
     int64_t ld, n_slices, n_strips;
+    /* SELL wide-slice split plan (power-law rows; spmv_sell_run_split) */
+    int32_t split_T;
+    int64_t n_chunks;
+    int32_t *d_chunk_slice, *d_chunk_k0;
     /* host copies for the CPU loop */
     int64_t *h_ptr;
     int32_t *h_row, *h_col, *h_perm;
@@ -341,6 +345,12 @@ static int build_format(const opts_t *o, spmv_format fmt, const coo_t *m, dev_fm
             if ((rc = upload((void **)&f->d_ptr, sp, (size_t)(f->n_strips + 1) * 8, NULL)) ||
                 (rc = upload((void **)&f->d_rin, f->h_rin, (size_t)Z, NULL)))
                 return rc;
+            f->variant = spmv_cmrs_pick_variant(f->n_strips, sp); /* 1: entry-balanced (skewed strips) */
+            if (f->variant == 1) {
+                f->ws_bytes = spmv_cmrs_tiled_ws_bytes(f->n_strips, Z, f->h);
+                if ((rc = spmv_malloc(&f->d_ws, f->ws_bytes)))
+                    return rc;
+            }
         }
         if ((rc = upload((void **)&f->d_col, col, (size_t)Z * 4, NULL)) ||
             (rc = upload((void **)&f->d_val, val, (size_t)Z * 8, NULL)))
@@ -386,6 +396,30 @@ static int build_format(const opts_t *o, spmv_format fmt, const coo_t *m, dev_fm
         if ((rc = upload((void **)&f->d_ptr, f->h_ptr, (size_t)(f->n_slices + 1) * 8, NULL)) ||
             (rc = upload((void **)&f->d_perm, f->h_perm, (size_t)f->n_slices * o->C * 4, NULL)))
             return rc;
+        /* wide slices (power-law rows) split into chunks of T slot columns */
+        f->split_T = spmv_sell_split_auto(f->n_slices, f->h_ptr, f->C, f->ki);
+        if (f->split_T > 0) {
+            f->n_chunks = spmv_sell_split_plan(f->n_slices, f->h_ptr, f->C, f->split_T, NULL, NULL);
+            if (f->n_chunks < 0)
+                return SPMV_OTHER_ERROR;
+            int32_t *cs = malloc((size_t)(f->n_chunks + 1) * sizeof(int32_t));
+            int32_t *ck = malloc((size_t)(f->n_chunks + 1) * sizeof(int32_t));
+            if (!cs || !ck)
+                return SPMV_OTHER_ERROR;
+            spmv_sell_split_plan(f->n_slices, f->h_ptr, f->C, f->split_T, cs, ck);
+            f->ws_bytes = spmv_sell_split_ws_bytes(f->n_chunks, f->C);
+            rc = upload((void **)&f->d_chunk_slice, cs, (size_t)(f->n_chunks + 1) * 4, NULL);
+            if (!rc)
+                rc = upload((void **)&f->d_chunk_k0, ck, (size_t)(f->n_chunks + 1) * 4, NULL);
+            if (!rc && f->ws_bytes)
+                rc = spmv_malloc(&f->d_ws, f->ws_bytes);
+            free(cs);
+            free(ck);
+            if (rc)
+                return rc;
+            printf("SELL split: %lld chunks of %d slot columns beyond the first %d of the wide slices\n",
+                   (long long)f->n_chunks, f->split_T, f->split_T);
+        }
     }
     free(ptr);
     free(col);
@@ -408,6 +442,10 @@ static int build_windows(dev_fmt_t *f)
         bytes = spmv_ell_xwin_bytes(f->d.n_rows);
     else if (f->fmt == FMT_SELL)
         bytes = spmv_sell_xwin_bytes(f->n_slices, f->C, f->sigma);
+    else if (f->fmt == FMT_COO)
+        bytes = spmv_coo_xwin_bytes(f->d.nnz);
+    else if (f->fmt == FMT_CMRS && f->variant == 0)
+        bytes = spmv_cmrs_xwin_bytes(f->d, f->h, f->n_strips);
     if (bytes == 0)
         return SPMV_SUCCESS;
     int rc = spmv_malloc(&f->d_win, bytes);
@@ -417,6 +455,10 @@ static int build_windows(dev_fmt_t *f)
         rc = spmv_csr_xwin_build(f->d, f->d_ptr, f->d_col, f->lanes, 0, f->d_win, bytes, &f->xcap);
     else if (f->fmt == FMT_ELL)
         rc = spmv_ell_xwin_build(f->d, f->K, f->ld, f->ki, f->d_col, f->d_win, bytes, &f->xcap);
+    else if (f->fmt == FMT_COO)
+        rc = spmv_coo_xwin_build(f->d, f->d_col, f->d_win, bytes, &f->xcap);
+    else if (f->fmt == FMT_CMRS)
+        rc = spmv_cmrs_xwin_build(f->d, f->h, f->n_strips, f->d_ptr, f->d_col, f->d_win, bytes, &f->xcap);
     else
         rc = spmv_sell_xwin_build(f->d, f->C, f->sigma, f->n_slices, f->d_ptr, f->d_col, f->d_win, bytes,
                                   &f->xcap);
@@ -426,6 +468,10 @@ static int build_windows(dev_fmt_t *f)
 static int launch(void *arg)
 {
     dev_fmt_t *f = (dev_fmt_t *)arg;
+    if (f->fmt == FMT_SELL && f->split_T > 0)
+        return spmv_sell_run_split(f->d, f->C, f->sigma, f->ki, f->n_slices, f->d_ptr, f->d_perm, f->d_col,
+                                   f->d_val, f->d_x, f->d_y, f->d_win, f->xcap, f->split_T, f->n_chunks,
+                                   f->d_chunk_slice, f->d_chunk_k0, f->d_ws, f->ws_bytes);
     if (f->d_win) {
         if (f->fmt == FMT_CSR)
             return spmv_csr_run_xwin(f->d, f->d_ptr, f->d_col, f->d_val, f->d_x, f->d_y, f->lanes, 0,
@@ -433,6 +479,12 @@ static int launch(void *arg)
         if (f->fmt == FMT_ELL)
             return spmv_ell_run_xwin(f->d, f->K, f->ld, f->ki, f->d_col, f->d_val, f->d_x, f->d_y, f->d_win,
                                      f->xcap);
+        if (f->fmt == FMT_COO)
+            return spmv_coo_run_xwin(f->d, f->d_row, f->d_col, f->d_val, f->d_x, f->d_y, f->d_ws, f->ws_bytes,
+                                     f->d_win, f->xcap);
+        if (f->fmt == FMT_CMRS)
+            return spmv_cmrs_run_xwin(f->d, f->h, f->n_strips, f->d_ptr, f->d_rin, f->d_col, f->d_val, f->d_x,
+                                      f->d_y, f->d_win, f->xcap);
         if (f->fmt == FMT_SELL)
             return spmv_sell_run_xwin(f->d, f->C, f->sigma, f->ki, f->n_slices, f->d_ptr, f->d_perm, f->d_col,
                                       f->d_val, f->d_x, f->d_y, f->d_win, f->xcap);
@@ -452,6 +504,9 @@ static int launch(void *arg)
         return spmv_sell_run(f->d, f->C, f->sigma, f->ki, f->n_slices, f->d_ptr, f->d_perm, f->d_col,
                              f->d_val, f->d_x, f->d_y);
     case FMT_CMRS:
+        if (f->variant == 1)
+            return spmv_cmrs_run_tiled(f->d, f->h, f->n_strips, f->d_ptr, f->d_rin, f->d_col, f->d_val, f->d_x,
+                                       f->d_y, f->d_ws, f->ws_bytes);
         return spmv_cmrs_run(f->d, f->h, f->n_strips, f->d_ptr, f->d_rin, f->d_col, f->d_val,
                              f->d_x, f->d_y);
     }

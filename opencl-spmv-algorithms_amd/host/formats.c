@@ -332,6 +332,58 @@ int spmv_cmrs_build(int64_t n_rows, const int64_t *row_ptr, int32_t h,
     return SPMV_SUCCESS;
 }
 
+int spmv_cmrs_pick_variant(int64_t n_strips, const int64_t *strip_ptr)
+{
+    if (n_strips <= 0)
+        return 0;
+    int64_t mx = 0;
+    for (int64_t s = 0; s < n_strips; ++s) {
+        const int64_t l = strip_ptr[s + 1] - strip_ptr[s];
+        mx = l > mx ? l : mx;
+    }
+    const double mean = (double)(strip_ptr[n_strips] - strip_ptr[0]) / (double)n_strips;
+    return (mx > 4096 && (double)mx > 64.0 * mean) ? 1 : 0;
+}
+
+/* ------------------------------------------------------------ SELL split */
+
+int32_t spmv_sell_split_auto(int64_t n_slices, const int64_t *slice_ptr, int32_t C, int32_t ki)
+{
+    if (n_slices <= 0 || C <= 0 || (ki != 1 && ki != 2))
+        return 0;
+    int64_t mx = 0;
+    for (int64_t s = 0; s < n_slices; ++s) {
+        const int64_t w = (slice_ptr[s + 1] - slice_ptr[s]) / C;
+        mx = w > mx ? w : mx;
+    }
+    const double mean = (double)(slice_ptr[n_slices] - slice_ptr[0]) / (double)C / (double)n_slices;
+    if (mx <= 1024 || (double)mx <= 16.0 * mean)
+        return 0;
+    int64_t t = (int64_t)(4.0 * mean);
+    t = t < 256 ? 256 : t;
+    return (int32_t)round_up(t, ki);
+}
+
+int64_t spmv_sell_split_plan(int64_t n_slices, const int64_t *slice_ptr, int32_t C, int32_t T,
+                             int32_t *chunk_slice, int32_t *chunk_k0)
+{
+    if (n_slices < 0 || C <= 0 || T <= 0 || n_slices > INT32_MAX)
+        return -1;
+    int64_t n = 0;
+    for (int64_t s = 0; s < n_slices; ++s) {
+        const int64_t w = (slice_ptr[s + 1] - slice_ptr[s]) / C;
+        for (int64_t k0 = T; k0 < w; k0 += T, ++n) {
+            if (k0 > INT32_MAX)
+                return -1;
+            if (chunk_slice) {
+                chunk_slice[n] = (int32_t)s;
+                chunk_k0[n] = (int32_t)k0;
+            }
+        }
+    }
+    return n;
+}
+
 /* ------------------------------------------------------------------ HYB */
 
 int spmv_hyb_plan(int64_t n_rows, const int64_t *row_ptr, int32_t ki, int32_t K_req, int32_t *K,

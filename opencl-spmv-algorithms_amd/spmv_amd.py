@@ -103,6 +103,18 @@ HIP_SYMBOLS = {
                                           _vp, _c_i32]),
     "spmv_sell_run": (ctypes.c_int, [Dims, _c_i32, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "spmv_cmrs_run": (ctypes.c_int, [Dims, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "spmv_coo_xwin_bytes": (ctypes.c_size_t, [_c_i64]),
+    "spmv_coo_xwin_build": (ctypes.c_int, [Dims, _vp, _vp, ctypes.c_size_t, ctypes.POINTER(_c_i32)]),
+    "spmv_coo_run_xwin": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t, _vp, _c_i32]),
+    "spmv_cmrs_xwin_bytes": (ctypes.c_size_t, [Dims, _c_i32, _c_i64]),
+    "spmv_cmrs_xwin_build": (ctypes.c_int, [Dims, _c_i32, _c_i64, _vp, _vp, _vp, ctypes.c_size_t,
+                                            ctypes.POINTER(_c_i32)]),
+    "spmv_cmrs_run_xwin": (ctypes.c_int, [Dims, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_i32]),
+    "spmv_cmrs_tiled_ws_bytes": (ctypes.c_size_t, [_c_i64, _c_i64, _c_i32]),
+    "spmv_cmrs_run_tiled": (ctypes.c_int, [Dims, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t]),
+    "spmv_sell_split_ws_bytes": (ctypes.c_size_t, [_c_i64, _c_i32]),
+    "spmv_sell_run_split": (ctypes.c_int, [Dims, _c_i32, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                           _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, ctypes.c_size_t]),
     "spmv_gen_banded_device": (ctypes.c_int, [_c_i64, ctypes.c_uint64, _c_i64, _c_i64, ctypes.c_int, _c_i32,
                                               _c_i32, _vp, _vp, _vp, _vp, ctypes.c_int, _vp]),
     "spmv_dev_csr_from_coo": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, _vp]),
@@ -152,6 +164,9 @@ HOST_SYMBOLS = {
     "spmv_sell_plan": (ctypes.c_int, [_c_i64, _vp, _c_i32, _c_i32, _c_i32, ctypes.POINTER(_c_i64), ctypes.POINTER(_c_i64)]),
     "spmv_sell_fill": (ctypes.c_int, [_c_i64, _vp, _vp, _vp, _c_i32, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, _vp]),
     "spmv_cmrs_build": (ctypes.c_int, [_c_i64, _vp, _c_i32, _vp, _vp]),
+    "spmv_cmrs_pick_variant": (ctypes.c_int, [_c_i64, _vp]),
+    "spmv_sell_split_auto": (_c_i32, [_c_i64, _vp, _c_i32, _c_i32]),
+    "spmv_sell_split_plan": (_c_i64, [_c_i64, _vp, _c_i32, _c_i32, _vp, _vp]),
     "spmv_partition_rows": (ctypes.c_int, [_c_i64, _vp, ctypes.c_int, _c_i64, _vp]),
     "spmv_csr16_plan": (ctypes.c_int, [_c_i64, _vp, ctypes.POINTER(_c_i64), ctypes.POINTER(_c_i64)]),
     "spmv_hyb_plan": (ctypes.c_int, [_c_i64, _vp, _c_i32, _c_i32, ctypes.POINTER(_c_i32), ctypes.POINTER(_c_i64),
@@ -372,6 +387,23 @@ def sell_build(n_rows: int, ptr, col, val, C: int = 64, sigma: int = 1024, ki: i
                 val=sval, stored=stored.value)
 
 
+def sell_split_plan(s: dict, T: int | None = None):
+    """Wide-slice split plan of a sell_build result: (T, chunk_slice,
+    chunk_k0); T None = the library rule (0: no split)."""
+    hl = host_lib()
+    sp = np.ascontiguousarray(s["slice_ptr"], dtype=np.int64)
+    if T is None:
+        T = hl.spmv_sell_split_auto(s["n_slices"], _ptr(sp), s["C"], s["ki"])
+    if T <= 0:
+        return 0, np.zeros(0, np.int32), np.zeros(0, np.int32)
+    n = hl.spmv_sell_split_plan(s["n_slices"], _ptr(sp), s["C"], T, None, None)
+    if n < 0:
+        raise SpmvError(OTHER_ERROR, "spmv_sell_split_plan", "bad plan arguments")
+    cs, ck = np.zeros(max(n, 1), np.int32), np.zeros(max(n, 1), np.int32)
+    hl.spmv_sell_split_plan(s["n_slices"], _ptr(sp), s["C"], T, _ptr(cs), _ptr(ck))
+    return T, cs[:n], ck[:n]
+
+
 def cmrs_build(n_rows: int, ptr, h: int = 8):
     ns = (n_rows + h - 1) // h
     sp = np.empty(ns + 1, np.int64)
@@ -484,7 +516,10 @@ class DeviceMatrix:
             raise SpmvError(OTHER_ERROR, "run", "x and y must be float64")
         if x.numel() < self.n_cols or y.numel() < self.n_rows:
             raise SpmvError(OTHER_ERROR, "run", "x or y too short")
-        if self.fmt == "coo":
+        if self.fmt == "coo" and "win" in a:
+            rc = lib.spmv_coo_run_xwin(d, _ptr(a["row"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
+                                       _ptr(a["ws"]), a["ws"].numel(), _ptr(a["win"]), p["xcap"])
+        elif self.fmt == "coo":
             rc = lib.spmv_coo_run(d, _ptr(a["row"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
                                   _ptr(a["ws"]), a["ws"].numel())
         elif self.fmt == "csr" and "win" in a:
@@ -509,6 +544,12 @@ class DeviceMatrix:
                                        _ptr(a["win"]), p["xcap"])
         elif self.fmt == "ell":
             rc = lib.spmv_ell_run(d, p["K"], p["ld"], p["ki"], _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y))
+        elif self.fmt == "sell" and p.get("split_T", 0) > 0:
+            rc = lib.spmv_sell_run_split(d, p["C"], p["sigma"], p["ki"], p["n_slices"], _ptr(a["slice_ptr"]),
+                                         _ptr(a["perm"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
+                                         _ptr(a.get("win")), p.get("xcap", 0), p["split_T"], p["n_chunks"],
+                                         _ptr(a["chunk_slice"]), _ptr(a["chunk_k0"]), _ptr(a["split_ws"]),
+                                         a["split_ws"].numel())
         elif self.fmt == "sell" and "win" in a:
             rc = lib.spmv_sell_run_xwin(d, p["C"], p["sigma"], p["ki"], p["n_slices"], _ptr(a["slice_ptr"]),
                                         _ptr(a["perm"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
@@ -516,6 +557,13 @@ class DeviceMatrix:
         elif self.fmt == "sell":
             rc = lib.spmv_sell_run(d, p["C"], p["sigma"], p["ki"], p["n_slices"], _ptr(a["slice_ptr"]), _ptr(a["perm"]),
                                    _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y))
+        elif self.fmt == "cmrs" and p.get("variant", 0) == 1:
+            rc = lib.spmv_cmrs_run_tiled(d, p["h"], p["n_strips"], _ptr(a["strip_ptr"]), _ptr(a["row_in_strip"]),
+                                         _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y), _ptr(a["ws"]),
+                                         a["ws"].numel())
+        elif self.fmt == "cmrs" and "win" in a:
+            rc = lib.spmv_cmrs_run_xwin(d, p["h"], p["n_strips"], _ptr(a["strip_ptr"]), _ptr(a["row_in_strip"]),
+                                        _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y), _ptr(a["win"]), p["xcap"])
         elif self.fmt == "cmrs":
             rc = lib.spmv_cmrs_run(d, p["h"], p["n_strips"], _ptr(a["strip_ptr"]), _ptr(a["row_in_strip"]),
                                    _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y))
@@ -535,6 +583,66 @@ def _sell_xwin(dm: DeviceMatrix) -> None:
     _check(hip_lib().spmv_sell_xwin_build(dm.dims(), p["C"], p["sigma"], p["n_slices"], _ptr(a["slice_ptr"]),
                                           _ptr(a["col"]), _ptr(a["win"]), a["win"].numel(), ctypes.byref(cap)),
            "spmv_sell_xwin_build")
+    p["xcap"] = cap.value
+
+
+def _sell_split(dm: DeviceMatrix, slice_ptr: np.ndarray, split: int | None) -> None:
+    """Wide-slice split plan (power-law rows): split None = library rule
+    (spmv_sell_split_auto), 0 = off, T > 0 = keep T slot columns per slice
+    in the main kernel and hand the rest to the chunk kernel."""
+    torch = _torch()
+    p, a = dm.params, dm.arrays
+    if split is not None and split > 0 and split % p["ki"]:
+        raise SpmvError(OTHER_ERROR, "sell split", "T must be a multiple of ki")
+    T, cs, ck = sell_split_plan(dict(slice_ptr=slice_ptr, n_slices=p["n_slices"], C=p["C"], ki=p["ki"]), split)
+    p["split_T"] = 0
+    if T <= 0:
+        return
+    n = len(cs)
+    if n == 0:
+        cs, ck = np.zeros(1, np.int32), np.zeros(1, np.int32)
+    p["split_T"], p["n_chunks"] = T, n
+    a["chunk_slice"] = _dev_tensor(cs, dm.device)
+    a["chunk_k0"] = _dev_tensor(ck, dm.device)
+    a["split_ws"] = torch.empty(max(hip_lib().spmv_sell_split_ws_bytes(n, p["C"]), 8), dtype=torch.uint8,
+                                device=dm.device)
+
+
+def _cmrs_variant(dm: DeviceMatrix, strip_ptr: np.ndarray, variant: int | None) -> None:
+    """variant None = library rule (spmv_cmrs_pick_variant), 0 = strip-run
+    kernel, 1 = entry-balanced tiles (+ workspace)."""
+    torch = _torch()
+    p = dm.params
+    sp = np.ascontiguousarray(strip_ptr, dtype=np.int64)
+    v = host_lib().spmv_cmrs_pick_variant(p["n_strips"], _ptr(sp)) if variant is None else int(variant)
+    p["variant"] = v
+    if v == 1:
+        ws = hip_lib().spmv_cmrs_tiled_ws_bytes(p["n_strips"], dm.nnz, p["h"])
+        dm.arrays["ws"] = torch.empty(max(ws, 16), dtype=torch.uint8, device=dm.device)
+
+
+def _coo_xwin(dm: DeviceMatrix) -> None:
+    """Per-tile column windows for the x-window COO kernel."""
+    torch = _torch()
+    p, a = dm.params, dm.arrays
+    nbytes = hip_lib().spmv_coo_xwin_bytes(dm.nnz)
+    a["win"] = torch.empty(max(nbytes, 8), dtype=torch.uint8, device=dm.device)
+    cap = _c_i32(0)
+    _check(hip_lib().spmv_coo_xwin_build(dm.dims(), _ptr(a["col"]), _ptr(a["win"]), a["win"].numel(),
+                                         ctypes.byref(cap)), "spmv_coo_xwin_build")
+    p["xcap"] = cap.value
+
+
+def _cmrs_xwin(dm: DeviceMatrix) -> None:
+    """Per-strip-run column windows for the x-window CMRS kernel."""
+    torch = _torch()
+    p, a = dm.params, dm.arrays
+    nbytes = hip_lib().spmv_cmrs_xwin_bytes(dm.dims(), p["h"], p["n_strips"])
+    a["win"] = torch.empty(max(nbytes, 8), dtype=torch.uint8, device=dm.device)
+    cap = _c_i32(0)
+    _check(hip_lib().spmv_cmrs_xwin_build(dm.dims(), p["h"], p["n_strips"], _ptr(a["strip_ptr"]), _ptr(a["col"]),
+                                          _ptr(a["win"]), a["win"].numel(), ctypes.byref(cap)),
+           "spmv_cmrs_xwin_build")
     p["xcap"] = cap.value
 
 
@@ -566,13 +674,15 @@ def _csr_xwin(dm: DeviceMatrix) -> None:
 
 def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int = 0, ki: int = 0, C: int = 64,
               sigma: int = 1024, h: int = 8, ell_max_padding: float | None = 64.0,
-              xwin: bool | None = None, xwin_rows: int = 0) -> DeviceMatrix:
+              xwin: bool | None = None, xwin_rows: int = 0, split: int | None = None,
+              cmrs_variant: int | None = None) -> DeviceMatrix:
     """Build `fmt` on the host (libspmv_host.so) and upload it.  xwin (CSR,
     ELL, SELL; default on): also build the per-workgroup x windows on the
-    device and run the LDS x-window kernels (same bits as without)."""
+    device and run the LDS x-window kernels (same bits as without).  split
+    (SELL) / cmrs_variant (CMRS): None = the library's skew rule."""
     torch = _torch()
     if xwin is None:
-        xwin = fmt in ("csr", "ell", "sell")
+        xwin = fmt in ("csr", "ell", "sell", "coo", "cmrs")
     device = torch.device(device)
     dm = DeviceMatrix(fmt, m.n_rows, m.n_cols, m.nnz, device)
     if fmt == "coo":
@@ -582,6 +692,8 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
                          val=_dev_tensor(val, device),
                          ws=torch.empty(ws_bytes, dtype=torch.uint8, device=device))
         dm.stored_bytes = 16 * m.nnz
+        if xwin:
+            _coo_xwin(dm)
         return dm
     ptr, col, val = csr_from_coo(m)
     if fmt == "csr":
@@ -620,6 +732,7 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
         dm.stored_bytes = 12 * s["stored"] + 8 * (s["n_slices"] + 1) + 4 * s["n_slices"] * C
         if xwin:
             _sell_xwin(dm)
+        _sell_split(dm, s["slice_ptr"], split)
     elif fmt == "hyb":
         hb = hyb_build(m.n_rows, ptr, col, val, ki=ki or 2)
         dm.params = dict(K=hb["K"], ld=hb["ld"], ki=hb["ki"], tail_nnz=hb["tail_nnz"], stored=hb["stored"])
@@ -634,13 +747,17 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
                          row_in_strip=_dev_tensor(c["row_in_strip"], device),
                          col=_dev_tensor(col, device), val=_dev_tensor(val, device))
         dm.stored_bytes = 13 * m.nnz + 8 * (c["n_strips"] + 1)
+        _cmrs_variant(dm, c["strip_ptr"], cmrs_variant)
+        if xwin and dm.params["variant"] == 0:
+            _cmrs_xwin(dm)
     else:
         raise SpmvError(OTHER_ERROR, "to_device", f"unknown format {fmt}")
     return dm
 
 
 def device_build(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, ki: int = 0, C: int = 64,
-                 sigma: int = 1024, h: int = 8, xwin: bool | None = None) -> DeviceMatrix:
+                 sigma: int = 1024, h: int = 8, xwin: bool | None = None, split: int | None = None,
+                 cmrs_variant: int | None = None) -> DeviceMatrix:
     """Like to_device, but only the raw COO (file order) crosses PCIe: CSR,
     ELL, SELL and CMRS are built on the device by the spmv_dev_* builders
     (SURVEY.md §8f row 2); the arrays equal the host builders'."""
@@ -649,7 +766,7 @@ def device_build(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, ki: int =
     if fmt not in ("csr", "ell", "sell", "cmrs"):
         raise SpmvError(OTHER_ERROR, "device_build", "format must be csr, ell, sell or cmrs")
     if xwin is None:
-        xwin = fmt in ("csr", "ell", "sell")
+        xwin = fmt in ("csr", "ell", "sell", "cmrs")
     lib = hip_lib()
     N, Z = m.n_rows, m.nnz
     d_row, d_col, d_val = (_dev_tensor(a, device) for a in (m.row, m.col, m.val))
@@ -699,6 +816,7 @@ def device_build(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, ki: int =
         dm.stored_bytes = 12 * stored.value + 8 * (ns + 1) + 4 * ns * C
         if xwin:
             _sell_xwin(dm)
+        _sell_split(dm, sp.cpu().numpy(), split)
     else:
         ns = (N + h - 1) // h
         stp = torch.empty(ns + 1, dtype=torch.int64, device=device)
@@ -707,6 +825,9 @@ def device_build(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, ki: int =
         dm.params = dict(h=h, n_strips=ns)
         dm.arrays = dict(strip_ptr=stp, row_in_strip=rin, col=col, val=val)
         dm.stored_bytes = 13 * Z + 8 * (ns + 1)
+        _cmrs_variant(dm, stp.cpu().numpy(), cmrs_variant)
+        if xwin and dm.params["variant"] == 0:
+            _cmrs_xwin(dm)
     dm.arrays["row_ptr_csr"] = ptr
     return dm
 

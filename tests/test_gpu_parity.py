@@ -55,6 +55,17 @@ FMT_PARAMS = [
     ("cmrs", {"h": 8}),
     ("cmrs", {"h": 1}),
     ("cmrs", {"h": 64}),
+    # wide-slice split / entry-balanced CMRS forced on ordinary matrices
+    # (tiny T: every slice wider than T is split; tiles cut strips anywhere)
+    ("sell", {"C": 64, "sigma": 1024, "ki": 2, "split": 2}),
+    ("sell", {"C": 32, "sigma": 64, "ki": 1, "split": 1, "xwin": True}),
+    ("sell", {"C": 64, "sigma": 1, "ki": 1, "split": 3, "xwin": False}),
+    ("cmrs", {"h": 8, "cmrs_variant": 1}),
+    ("cmrs", {"h": 1, "cmrs_variant": 1}),
+    ("cmrs", {"h": 64, "cmrs_variant": 1}),
+    # COO / CMRS with global x gathers (the defaults stage x windows in LDS)
+    ("coo", {"xwin": False}),
+    ("cmrs", {"h": 8, "xwin": False}),
 ]
 IDS = [f"{f}-{'-'.join(f'{k}{v}' for k, v in kw.items()) or 'default'}" for f, kw in FMT_PARAMS]
 
@@ -119,7 +130,12 @@ def test_cantlike_batch_random_x(torch_dev, fmt):
 
 
 @pytest.mark.parametrize("fmt,kw", [("coo", {}), ("csr", {}), ("csr", {"variant": 2}), ("csr", {"variant": 4}),
-                                    ("csr", {"variant": 5}), ("sell", {}), ("cmrs", {}), ("hyb", {})])
+                                    ("csr", {"variant": 5}), ("sell", {}), ("cmrs", {}), ("hyb", {}),
+                                    ("sell", {"split": 0}), ("sell", {"split": 256, "ki": 2}),
+                                    ("sell", {"split": 64, "ki": 1, "xwin": False}),
+                                    ("sell", {"sigma": 65536, "ki": 2}),
+                                    ("cmrs", {"cmrs_variant": 0}), ("cmrs", {"cmrs_variant": 1, "h": 1}),
+                                    ("cmrs", {"cmrs_variant": 1, "h": 64})])
 def test_rmat_skewed(torch_dev, fmt, kw):
     """R-MAT 1e6 rows / 1e7 entries: empty rows, rows of thousands of entries."""
     torch, dev = torch_dev
@@ -146,7 +162,8 @@ def test_ragged_long_rows(torch_dev, fmt, kw):
     assert_parity(m, y, x)
 
 
-@pytest.mark.parametrize("fmt,kw", [(f, {}) for f in sa.ALL_FORMATS] + [("csr", {"variant": 4}), ("csr", {"variant": 5})])
+@pytest.mark.parametrize("fmt,kw", [(f, {}) for f in sa.ALL_FORMATS] + [("csr", {"variant": 4}), ("csr", {"variant": 5}),
+                                                                     ("sell", {"split": 2}), ("cmrs", {"cmrs_variant": 1})])
 def test_bitwise_reproducible(torch_dev, fmt, kw):
     """No atomics anywhere: two launches give identical bits (the reference
     COO's CAS-atomic order is nondeterministic)."""
@@ -449,3 +466,34 @@ def test_ell_xwin_bit_identical(torch_dev, ki):
         torch.cuda.synchronize()
         assert torch.equal(ys[0].view(torch.int64), ys[1].view(torch.int64))
         assert_parity(m, ys[1].cpu().numpy(), x.cpu().numpy())
+
+
+@pytest.mark.parametrize("case", ["cantlike", "rmat", "ragged", "fixtures"])
+@pytest.mark.parametrize("fmt,kw", [("coo", {}), ("cmrs", {"h": 8, "cmrs_variant": 0}),
+                                    ("cmrs", {"h": 1, "cmrs_variant": 0}), ("cmrs", {"h": 64, "cmrs_variant": 0})])
+def test_coo_cmrs_xwin_bit_identical(torch_dev, case, fmt, kw):
+    """COO / CMRS x windows in LDS: same products, same order as the global
+    gathers, so y is bit-identical (windows too wide fall back per tile)."""
+    torch, dev = torch_dev
+    if case == "cantlike":
+        ms = [sa.gen_cantlike(0, copies=2)]
+    elif case == "rmat":
+        ms = [sa.gen_rmat(1_000_000, 10_000_000, scale=20, seed=1)]
+    elif case == "ragged":
+        ms = [sa.gen_random(20_000, 50_000, 0, 2_000, seed=21)]
+    else:
+        ms = [sa.read_mtx(GOLDEN / f"{n}.mtx") for n in CASES]
+    for m in ms:
+        a = sa.to_device(m, fmt, dev, xwin=True, **kw)
+        b = sa.to_device(m, fmt, dev, xwin=False, **kw)
+        assert "win" in a.arrays and "win" not in b.arrays
+        if case == "cantlike":
+            assert a.params["xcap"] > 0
+        x = torch.from_numpy(np.random.default_rng(4).uniform(-1, 1, m.n_cols)).to(dev)
+        ya = torch.full((max(m.n_rows, 1),), float("nan"), dtype=torch.float64, device=dev)
+        yb = torch.full_like(ya, float("nan"))
+        a.run(x, ya)
+        b.run(x, yb)
+        torch.cuda.synchronize()
+        assert torch.equal(ya.view(torch.int64), yb.view(torch.int64))
+        assert_parity(m, ya.cpu().numpy()[: m.n_rows], x.cpu().numpy())

@@ -305,3 +305,71 @@ def test_hyb_split_round_trip(kind, K):
         # the tail is the CSR entries past K, in order
         exp = np.concatenate([col[ptr[r] + Kh:ptr[r + 1]] for r in range(m.n_rows) if lens[r] > Kh])
         assert np.array_equal(h["tail_col"][:t], exp)
+
+
+def _sell_split_model(s, T, cs, ck, x):
+    """numpy model of spmv_sell_run_split: main part = first T slot columns
+    of every slice, chunks add the rest; y scattered through perm."""
+    C, ki = s["C"], s["ki"]
+    sp, perm, col, val = s["slice_ptr"], s["perm"], s["col"], s["val"]
+    acc = np.zeros(s["n_slices"] * C)
+    for sl in range(s["n_slices"]):
+        w = (sp[sl + 1] - sp[sl]) // C
+        blk_v = val[sp[sl]:sp[sl + 1]].reshape(w // ki, C, ki)
+        blk_c = col[sp[sl]:sp[sl + 1]].reshape(w // ki, C, ki)
+        n = min(w, T) if T else w
+        acc[sl * C:(sl + 1) * C] = (blk_v[: n // ki] * x[blk_c[: n // ki]]).sum(axis=(0, 2))
+    for c, k0 in zip(cs, ck):
+        sl = int(c)
+        w = (sp[sl + 1] - sp[sl]) // C
+        blk_v = val[sp[sl]:sp[sl + 1]].reshape(w // ki, C, ki)
+        blk_c = col[sp[sl]:sp[sl + 1]].reshape(w // ki, C, ki)
+        g0, g1 = k0 // ki, min(k0 + T, w) // ki
+        acc[sl * C:(sl + 1) * C] += (blk_v[g0:g1] * x[blk_c[g0:g1]]).sum(axis=(0, 2))
+    y = np.full(max(perm.max() + 1, 0) if perm.size else 0, np.nan)
+    ok = perm[: s["n_slices"] * C] >= 0
+    y[perm[: s["n_slices"] * C][ok]] = acc[ok]
+    return y
+
+
+@pytest.mark.parametrize("kind,T,ki", [("rmat", None, 1), ("rmat", None, 2), ("rmat", 64, 2), ("cantlike", 2, 1),
+                                       ("cantlike", None, 1), ("tiny", 1, 1)])
+def test_sell_split_plan_covers_every_slot(kind, T, ki):
+    """The split plan (§8 A6 on power-law rows): main kernel's first T slot
+    columns + chunks [k0, k0+T) tile every slice exactly once, so the model
+    of spmv_sell_run_split gives the oracle's y."""
+    if kind == "rmat":
+        m = sa.gen_rmat(100_000, 1_000_000, scale=17, seed=2)
+    elif kind == "cantlike":
+        m = sa.gen_cantlike(0)
+    else:
+        m = sa.read_mtx(GOLDEN / "empty_rows.mtx")
+    ptr, col, val = sa.csr_from_coo(m)
+    s = sa.sell_build(m.n_rows, ptr, col, val, C=64, sigma=1024, ki=ki)
+    Tp, cs, ck = sa.sell_split_plan(s, T)
+    if kind == "rmat" and T is None:
+        assert Tp >= 256 and Tp % ki == 0 and len(cs) > 0  # the rule fires on hubs
+    if kind == "cantlike" and T is None:
+        assert Tp == 0  # and stays off for ordinary matrices
+    widths = np.diff(s["slice_ptr"]) // 64
+    if Tp:
+        exp = sum(max(0, -(-int(w) // Tp) - 1) for w in widths)
+        assert len(cs) == exp and np.all(np.diff(cs) >= 0) and np.all(ck % Tp == 0) and np.all(ck > 0)
+        assert np.all(ck < widths[cs])
+    x = np.random.default_rng(3).uniform(-1, 1, m.n_cols)
+    y = _sell_split_model(s, Tp, cs, ck, x)[: m.n_rows]
+    y_ref = oracle.file_order_spmv(m.n_rows, m.row, m.col, m.val, x)
+    assert len(oracle.parity(y, y_ref, m.row, m.col, m.val, x, m.n_rows)) == 0
+
+
+@pytest.mark.parametrize("kind,exp", [("rmat", 1), ("cantlike", 0), ("ragged", 0)])
+def test_cmrs_pick_variant(kind, exp):
+    if kind == "rmat":
+        m = sa.gen_rmat(100_000, 1_000_000, scale=17, seed=2)
+    elif kind == "cantlike":
+        m = sa.gen_cantlike(0)
+    else:
+        m = sa.gen_random(5_000, 5_000, 0, 300, seed=4)
+    ptr, _, _ = sa.csr_from_coo(m)
+    c = sa.cmrs_build(m.n_rows, ptr, h=8)
+    assert sa.host_lib().spmv_cmrs_pick_variant(c["n_strips"], sa._ptr(c["strip_ptr"])) == exp

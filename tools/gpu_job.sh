@@ -48,6 +48,11 @@ for s in "${steps[@]}"; do
     probe) [ -x tools/bw_probe ] || hipcc --offload-arch=gfx950 -O3 tools/bw_probe.hip -o tools/bw_probe; run bw_probe 300 tools/bw_probe;;
     sweepfast) run sweep_fast 600 python tools/sweep.py --only csr,sell,ell --rounds 2;;
     sweepnopair) SPMV_CSR_PAIR=0 run sweep_nopair 300 python tools/sweep.py --only csr --rounds 2;;
+    pmcrmat) run pmc_rmat 1100 python tools/pmc_traffic.py --workload rmat --formats csr --kernel csr_tiled_kernel --out traffic_rmat.json --steps 5;;
+    rmatexp) run rmat_exp 600 python tools/rmat_exp.py;;
+    testsplit) run gpu_tests_split 900 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "split or cmrs_variant or rmat_skewed or h8-cmrs or bitwise";;
+    benchrmatpf) run bench_rmat_pf 900 python bench.py --workload rmat --steps 20 --per-format yes;;
+    sweeprmatfmt) run sweep_rmat_fmt 600 python tools/sweep.py --matrix rmat --rounds 1 --reps 10 --only sell,cmrs,coo,hyb;;
     pmc) run pmc 1100 python tools/pmc_traffic.py;;
     pmcvar) run pmc_var 1100 python tools/pmc_traffic.py --out traffic_variants.json --formats "csr,csr@SPMV_XCD_REMAP=1,csr:lanes=16,sell:sigma=256,sell,ell@SPMV_XCD_REMAP=1";;
     sweepnt) run sweep_nt 600 python tools/sweep.py --env-only --rounds 3;;

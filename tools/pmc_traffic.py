@@ -95,6 +95,8 @@ def main():
     ap.add_argument("--copies", type=int, default=32)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--out", default=None, help="file name under profiles/ (default traffic.json)")
+    ap.add_argument("--workload", default="cantlike", choices=["cantlike", "rmat"])
+    ap.add_argument("--kernel", default=None, help="kernel name substring (default: the format's)")
     a = ap.parse_args()
     probe = REPO / "tools" / "bw_probe"
     if not probe.exists():
@@ -123,7 +125,7 @@ def main():
         env_kv = dict(e.split("=", 1) for e in env_parts)
         fmt, _, params = spec_main.partition(":")
         cmd = ["python3", "bench.py", "--profile", "--format", fmt, "--steps", str(a.steps), "--warmup", "2",
-               "--copies", str(a.copies)]
+               "--copies", str(a.copies), "--workload", a.workload]
         for kv in filter(None, params.split(";")):
             k, v = kv.split("=")
             cmd += [f"--{k}", v]
@@ -133,11 +135,11 @@ def main():
         for tag, cs in PASSES.items():
             f = run_pass(f"{tag0}_{tag}", cs, cmd)
             if f:
-                c, n = mean_per_dispatch(f, kernel_for(fmt, env_kv))
+                c, n = mean_per_dispatch(f, a.kernel or kernel_for(fmt, env_kv))
                 counters.update(c)
         if not counters:
             continue
-        N, Z = CANT_N * a.copies, CANT_Z * a.copies
+        N, Z = (CANT_N * a.copies, CANT_Z * a.copies) if a.workload == "cantlike" else (10**7, 10**8)
         b_alg = 12 * Z + 4 * (N + 1) + 8 * N + 8 * N
         read_rdreq = bytes_from_rdreq(counters)
         if cal_rdreq and 0.8 < cal_rdreq < 1.25:
@@ -153,7 +155,7 @@ def main():
         hits, miss = counters.get("TCC_HIT_sum", 0.0), counters.get("TCC_MISS_sum", 0.0)
         for k in env_kv:
             os.environ.pop(k, None)
-        result[spec] = {"kernel": kernel_for(fmt, env_kv), "bytes_alg": b_alg, "dispatches": n, "cmd": " ".join(cmd[1:]),
+        result[spec] = {"kernel": a.kernel or kernel_for(fmt, env_kv), "workload": a.workload, "bytes_alg": b_alg, "dispatches": n, "cmd": " ".join(cmd[1:]),
                         "env": env_kv or None,
                        "hbm_read_bytes_per_launch": round(read), "hbm_write_bytes_per_launch": round(write),
                        "hbm_bytes_per_launch": round(read + write),

@@ -402,7 +402,7 @@ def main():
                                "frac": round(bytes_step / (km * 1e-3) * 1e-9 / sa.HBM_PEAK_GBS, 4),
                                "kernel_ms": round(km, 5), "stored_MB": round(d2.stored_bytes * 1e-6, 1),
                                "params": dict(kw, **{k: v for k, v in d2.params.items()
-                                                     if k in ("variant", "split_T", "n_chunks")}) or None,
+                                                     if k in ("variant", "split_T", "n_chunks", "H")}) or None,
                                "parity_ok": bad2 == 0}
             del d2
             torch.cuda.empty_cache()

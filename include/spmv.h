@@ -115,6 +115,19 @@ int spmv_csr_run_tiled(spmv_dims d, const int64_t *row_ptr, const int32_t *col,
                        const double *val, const double *x, double *y, void *ws,
                        size_t ws_bytes);
 
+/* Hot-column CSR for power-law columns (R-MAT: the 2^19 most frequent of
+ * 1e7 columns hold ~84 % of the entries): col_hot from spmv_hot_columns
+ * (spmv_host.h) names the H hottest columns n_cols + rank; the run gathers
+ * xh[rank] = x[hot[rank]] into the workspace and the tiled kernel reads
+ * those x values from the compact table, which stays in L2, instead of
+ * from one 128-B line each spread over the whole vector.  y is
+ * bit-identical to spmv_csr_run_tiled.  `ws` holds
+ * spmv_csr_hot_ws_bytes() bytes; H = 0 is spmv_csr_run_tiled.           */
+size_t spmv_csr_hot_ws_bytes(int64_t n_rows, int64_t nnz, int64_t H);
+int spmv_csr_run_tiled_hot(spmv_dims d, const int64_t *row_ptr, const int32_t *col_hot,
+                           const double *val, const double *x, double *y, int64_t H,
+                           const int32_t *hot, void *ws, size_t ws_bytes);
+
 /* ---------------------------------------------------------------- ELL ---
  * Replaces kernel `ell(val,idx,x,y,int N,int K,__local)` (reference
  * kernels/Ell.cl:1) and its launch (reference ell.c:47-48,242-248,273).

@@ -82,6 +82,17 @@ int spmv_csr_row_stats(int64_t n_rows, const int64_t *row_ptr,
  * group), else 0 (the library's row-group default).                    */
 int spmv_csr_pick_variant(int64_t n_rows, const int64_t *row_ptr);
 
+/* Hot columns for spmv_csr_run_tiled_hot: the H most frequent columns in
+ * decreasing count (ties: lower column first) into hot[], and col_out
+ * (may alias col) = col with every hot column c renumbered n_cols +
+ * rank(c).  H_req > 0 takes min(H_req, non-empty columns); H_req = 0 is
+ * the rule: 2^19 columns (4 MiB of x, one XCD's L2) when n_cols > 2^21,
+ * they hold at least half of the entries and at least 8 entries each on
+ * average (the table fill re-reads each once), else none (col_out = col).
+ * hot[] holds max(H_req, 2^19) entries.  Returns H, -1 on bad input.    */
+int64_t spmv_hot_columns(int64_t n_cols, int64_t nnz, const int32_t *col, int64_t H_req, int32_t *hot,
+                         int32_t *col_out);
+
 /* ELL, column-major with leading dimension ld = round_up(N, 64) and
  * k-interleave ki (spmv.h).  K = round_up(max row length, ki).
  * spmv_ell_plan gives K and ld; arrays are ld*K elements.               */

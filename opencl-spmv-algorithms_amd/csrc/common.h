@@ -53,6 +53,9 @@ int launch_csr_tiled(const spmv_dims &d, const int64_t *row_ptr, const int32_t *
                      const double *val, const double *x, double *y, int32_t *own_lo,
                      int32_t *carry_row, double *carry_val);
 int64_t csr_tiled_tile();
+int launch_csr_tiled_hot(const spmv_dims &d, const int64_t *row_ptr, const int32_t *col,
+                         const double *val, const double *x, double *y, int64_t H, const int32_t *hot,
+                         double *xh, int32_t *own_lo, int32_t *carry_row, double *carry_val);
 int launch_cmrs_tiled(const spmv_dims &d, int32_t h, int64_t n_strips, const int64_t *strip_ptr,
                       const uint8_t *rin, const int32_t *col, const double *val, const double *x,
                       double *y, int32_t *own_lo, int32_t *carry_row, double *carry_val);
@@ -123,6 +126,15 @@ struct XWindow {
     const double *s;  // LDS
     int32_t lo;
     __device__ __forceinline__ double operator()(int32_t c) const { return s[c - lo]; }
+};
+
+// Hot-column CSR (spmv_csr_run_tiled_hot): ids >= M name the compact table
+// xh of the most frequent columns, gathered from x at the start of the run.
+struct XHot {
+    const double *__restrict__ x;
+    const double *__restrict__ xh;
+    int32_t M;
+    __device__ __forceinline__ double operator()(int32_t c) const { return c >= M ? xh[c - M] : x[c]; }
 };
 
 // [min, max] of col[e0..e1) over one 256-thread workgroup ({0, -1} when

@@ -39,7 +39,9 @@ __device__ __forceinline__ int lower_bound_lds(const K *keys, int lo, int hi, in
 // Streams entries [cb, ce) into LDS: products in s_prod, keys via `key`.
 // cb is even, so value pairs are 16-byte aligned; nothing at or past ce
 // is read.
-template <int R, typename XS, typename KeyFn>
+// NT: non-temporal stream loads (the skewed-matrix kernels: x, gathered
+// from a vector far larger than L2, keeps the cache).
+template <int R, bool NT = false, typename XS, typename KeyFn>
 __device__ __forceinline__ void stage_chunk(int64_t cb, int64_t ce, const int32_t *__restrict__ col,
                                             const double *__restrict__ val, const XS &xs,
                                             double2 *s_prod, KeyFn key)
@@ -50,13 +52,13 @@ __device__ __forceinline__ void stage_chunk(int64_t cb, int64_t ce, const int32_
         const int64_t p = cb + 2 * (int64_t)t;
         double2 pr = {0.0, 0.0};
         if (p + 1 < ce) {
-            const double2 v = *reinterpret_cast<const double2 *>(val + p);
-            const int2 c = *reinterpret_cast<const int2 *>(col + p);
+            const double2 v = stream_load2<NT>(val + p);
+            const int2 c = stream_load2<NT>(col + p);
             pr.x = v.x * xs(c.x);
             pr.y = v.y * xs(c.y);
             key(t, p, 2);
         } else if (p < ce) {
-            pr.x = val[p] * xs(col[p]);
+            pr.x = stream_load<NT>(val + p) * xs(stream_load<NT>(col + p));
             key(t, p, 1);
         }
         s_prod[t] = pr;
@@ -271,24 +273,40 @@ __global__ __launch_bounds__(kBlock) void csr_tile_rows_kernel(int64_t n_rows, i
     own_lo[t] = (int32_t)lo;
 }
 
-template <int L, int R>
+// The tile's row offsets (rows r_lo..r_hi+1, clipped to the tile, relative
+// to t0) are staged in LDS together with the products, so the row phase
+// makes no dependent global loads; a tile spanning more than kTiledRowCap
+// rows (long runs of empty rows) reads them from global memory.  With a
+// stream-only x this phase, not the gathers, held the kernel to 2.6 TB/s
+// on R-MAT (tools/rmat_exp.hip mode 2).
+constexpr int kTiledRowCap = 1024;
+
+template <int L, int R, bool NT, typename XS>
 __global__ __launch_bounds__(kBlock) void csr_tiled_kernel(
     int64_t n_rows, int64_t nnz, const int64_t *__restrict__ row_ptr,
     const int32_t *__restrict__ col, const double *__restrict__ val,
-    const double *__restrict__ x, double *__restrict__ y,
+    const XS xs, double *__restrict__ y,
     const int32_t *__restrict__ own_lo, int32_t *__restrict__ carry_row,
     double *__restrict__ carry_val)
 {
     constexpr int CH = 2 * kBlock * R;
     constexpr int GROUPS = kBlock / L;
     __shared__ double2 s_prod[kBlock * R];
+    __shared__ int32_t s_rp[kTiledRowCap + 1];
     const double *prod = reinterpret_cast<const double *>(s_prod);
     const int64_t tile = blockIdx.x;
     const int64_t t0 = tile * CH;
     const int64_t t1 = t0 + CH < nnz ? t0 + CH : nnz;
     const int64_t r_lo = own_lo[tile];
     const int64_t r_hi = t1 == nnz ? n_rows - 1 : (int64_t)own_lo[tile + 1] - 1;
-    stage_chunk<R>(t0, t1, col, val, XGlobal{x}, s_prod, [](int, int64_t, int) {});
+    const int64_t nr = r_hi - r_lo + 1;  // owned rows (may be 0)
+    const bool rp_lds = nr >= 0 && nr <= kTiledRowCap;  // uniform
+    if (rp_lds)
+        for (int i = threadIdx.x; i <= nr; i += kBlock) {  // r_lo + nr <= n_rows
+            const int64_t o = row_ptr[r_lo + i];
+            s_rp[i] = (int32_t)((o < t1 ? o : t1) - t0);
+        }
+    stage_chunk<R, NT>(t0, t1, col, val, xs, s_prod, [](int, int64_t, int) {});
     __syncthreads();
     const int g = threadIdx.x / L, lane = threadIdx.x % L;
 
@@ -298,7 +316,7 @@ __global__ __launch_bounds__(kBlock) void csr_tiled_kernel(
         int32_t cr = -1;
         if (r_lo > 0 && (r_lo == n_rows || row_ptr[r_lo] > t0)) {
             cr = (int32_t)(r_lo - 1);
-            const int64_t e = row_ptr[r_lo - 1 + 1] < t1 ? row_ptr[r_lo] : t1;
+            const int64_t e = r_lo < n_rows && row_ptr[r_lo] < t1 ? row_ptr[r_lo] : t1;
             for (int64_t j = t0 + lane; j < e; j += L)
                 c += prod[j - t0];
         }
@@ -309,12 +327,18 @@ __global__ __launch_bounds__(kBlock) void csr_tiled_kernel(
         }
     }
     for (int64_t r = r_lo + g; r <= r_hi; r += GROUPS) {
-        const int64_t a = row_ptr[r];
-        int64_t b = row_ptr[r + 1];
-        b = b < t1 ? b : t1;
+        int a, b;
+        if (rp_lds) {
+            a = s_rp[r - r_lo];
+            b = s_rp[r - r_lo + 1];
+        } else {
+            const int64_t b64 = row_ptr[r + 1];
+            a = (int)(row_ptr[r] - t0);
+            b = (int)((b64 < t1 ? b64 : t1) - t0);
+        }
         double s = 0.0;
-        for (int64_t j = a + lane; j < b; j += L)
-            s += prod[j - t0];
+        for (int j = a + lane; j < b; j += L)
+            s += prod[j];
         s = group_sum<L>(s);
         if (lane == 0)
             y[r] = s;
@@ -351,7 +375,7 @@ __global__ __launch_bounds__(kBlock) void cmrs_tiled_kernel(
     const int64_t t1 = t0 + CH < nnz ? t0 + CH : nnz;
     const int64_t s_lo = own_lo[tile];
     const int64_t s_hi = t1 == nnz ? n_strips - 1 : (int64_t)own_lo[tile + 1] - 1;
-    stage_chunk<R>(t0, t1, col, val, XGlobal{x}, s_prod, [&](int t, int64_t p, int n) {
+    stage_chunk<R, true>(t0, t1, col, val, XGlobal{x}, s_prod, [&](int t, int64_t p, int n) {
         s_key2[t] = n == 2 ? *reinterpret_cast<const uint16_t *>(rin + p) : (uint16_t)rin[p];
     });
     __syncthreads();
@@ -438,28 +462,73 @@ int launch_cmrs_tiled(const spmv_dims &d, int32_t h, int64_t n_strips, const int
 
 int64_t csr_tiled_tile() { return 2 * kBlock * 3; }
 
+template <typename XS>
+static void launch_tiled_xs(const spmv_dims &d, int64_t tiles, const int64_t *row_ptr, const int32_t *col,
+                            const double *val, XS xs, double *y, int32_t *own_lo, int32_t *carry_row,
+                            double *carry_val)
+{
+    constexpr int R = 3;
+    const hipStream_t st = (hipStream_t)d.stream;
+    const double mean = d.n_rows > 0 ? (double)d.nnz / (double)d.n_rows : 0.0;
+    const bool nt = stream_nt(true);
+#define SPMV_TILED(LL)                                                                                    \
+    do {                                                                                                  \
+        if (nt)                                                                                           \
+            hipLaunchKernelGGL((csr_tiled_kernel<LL, R, true, XS>), dim3((unsigned)tiles), dim3(kBlock), 0, \
+                               st, d.n_rows, d.nnz, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val); \
+        else                                                                                              \
+            hipLaunchKernelGGL((csr_tiled_kernel<LL, R, false, XS>), dim3((unsigned)tiles), dim3(kBlock),  \
+                               0, st, d.n_rows, d.nnz, row_ptr, col, val, xs, y, own_lo, carry_row,        \
+                               carry_val);                                                                \
+    } while (0)
+    if (mean >= 48.0)
+        SPMV_TILED(8);
+    else if (mean >= 12.0)
+        SPMV_TILED(4);
+    else
+        SPMV_TILED(2);
+#undef SPMV_TILED
+}
+
 int launch_csr_tiled(const spmv_dims &d, const int64_t *row_ptr, const int32_t *col,
                      const double *val, const double *x, double *y, int32_t *own_lo,
                      int32_t *carry_row, double *carry_val)
 {
-    constexpr int R = 3;
     const int64_t ch = csr_tiled_tile();
     const int64_t tiles = (d.nnz + ch - 1) / ch;
     const hipStream_t st = (hipStream_t)d.stream;
     hipLaunchKernelGGL(csr_tile_rows_kernel, dim3((unsigned)((tiles + 1 + kBlock - 1) / kBlock)),
                        dim3(kBlock), 0, st, d.n_rows, d.nnz, tiles, ch, row_ptr, own_lo);
     SPMV_CHECK_LAUNCH("csr_tile_rows_kernel");
-    const double mean = d.n_rows > 0 ? (double)d.nnz / (double)d.n_rows : 0.0;
-    if (mean >= 48.0)
-        hipLaunchKernelGGL((csr_tiled_kernel<8, R>), dim3((unsigned)tiles), dim3(kBlock), 0, st,
-                           d.n_rows, d.nnz, row_ptr, col, val, x, y, own_lo, carry_row, carry_val);
-    else if (mean >= 12.0)
-        hipLaunchKernelGGL((csr_tiled_kernel<4, R>), dim3((unsigned)tiles), dim3(kBlock), 0, st,
-                           d.n_rows, d.nnz, row_ptr, col, val, x, y, own_lo, carry_row, carry_val);
-    else
-        hipLaunchKernelGGL((csr_tiled_kernel<2, R>), dim3((unsigned)tiles), dim3(kBlock), 0, st,
-                           d.n_rows, d.nnz, row_ptr, col, val, x, y, own_lo, carry_row, carry_val);
+    launch_tiled_xs(d, tiles, row_ptr, col, val, XGlobal{x}, y, own_lo, carry_row, carry_val);
     SPMV_CHECK_LAUNCH("csr_tiled_kernel");
+    return SPMV_SUCCESS;
+}
+
+__global__ __launch_bounds__(kBlock) void hot_gather_kernel(int64_t H, const int32_t *__restrict__ hot,
+                                                            const double *__restrict__ x,
+                                                            double *__restrict__ xh)
+{
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < H)
+        xh[i] = x[hot[i]];
+}
+
+int launch_csr_tiled_hot(const spmv_dims &d, const int64_t *row_ptr, const int32_t *col,
+                         const double *val, const double *x, double *y, int64_t H, const int32_t *hot,
+                         double *xh, int32_t *own_lo, int32_t *carry_row, double *carry_val)
+{
+    const int64_t ch = csr_tiled_tile();
+    const int64_t tiles = (d.nnz + ch - 1) / ch;
+    const hipStream_t st = (hipStream_t)d.stream;
+    if (H > 0)
+        hipLaunchKernelGGL(hot_gather_kernel, dim3((unsigned)((H + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, H,
+                           hot, x, xh);
+    hipLaunchKernelGGL(csr_tile_rows_kernel, dim3((unsigned)((tiles + 1 + kBlock - 1) / kBlock)),
+                       dim3(kBlock), 0, st, d.n_rows, d.nnz, tiles, ch, row_ptr, own_lo);
+    SPMV_CHECK_LAUNCH("csr_tile_rows_kernel");
+    launch_tiled_xs(d, tiles, row_ptr, col, val, XHot{x, xh, (int32_t)d.n_cols}, y, own_lo, carry_row, carry_val);
+    SPMV_CHECK_LAUNCH("csr_tiled_kernel (hot columns)");
     return SPMV_SUCCESS;
 }
 

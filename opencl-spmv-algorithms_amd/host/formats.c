@@ -101,6 +101,111 @@ int spmv_csr_row_stats(int64_t n_rows, const int64_t *row_ptr,
     return SPMV_SUCCESS;
 }
 
+typedef struct {
+    int64_t cnt;
+    int32_t col;
+} col_count_t;
+
+static int by_count_desc(const void *a, const void *b)
+{
+    const col_count_t *p = (const col_count_t *)a, *q = (const col_count_t *)b;
+    if (p->cnt != q->cnt)
+        return p->cnt > q->cnt ? -1 : 1;
+    return (p->col > q->col) - (p->col < q->col);
+}
+
+int64_t spmv_hot_columns(int64_t n_cols, int64_t nnz, const int32_t *col, int64_t H_req, int32_t *hot,
+                         int32_t *col_out)
+{
+    const int64_t kAutoH = (int64_t)1 << 19;
+    const int64_t cap = H_req > 0 ? H_req : kAutoH;
+    if (n_cols <= 0 || nnz < 0 || H_req < 0 || !hot || !col_out || (nnz > 0 && !col) ||
+        n_cols + cap > INT32_MAX)
+        return -1;
+    if (col_out != col)
+        memcpy(col_out, col, (size_t)nnz * sizeof(int32_t));
+    if (H_req == 0 && n_cols <= ((int64_t)1 << 21))
+        return 0;
+    int64_t *cnt = (int64_t *)calloc((size_t)n_cols, sizeof(int64_t));
+    if (!cnt)
+        return -1;
+    int64_t maxc = 0;
+    for (int64_t j = 0; j < nnz; ++j) {
+        if (col[j] < 0 || col[j] >= n_cols) {
+            free(cnt);
+            return -1;
+        }
+        const int64_t c = ++cnt[col[j]];
+        maxc = c > maxc ? c : maxc;
+    }
+    /* threshold count T: every column above T is hot, then columns equal
+     * to T in increasing id until cap */
+    int64_t *hist = (int64_t *)calloc((size_t)maxc + 2, sizeof(int64_t));
+    if (!hist) {
+        free(cnt);
+        return -1;
+    }
+    for (int64_t c = 0; c < n_cols; ++c)
+        hist[cnt[c]]++;
+    int64_t above = 0, T = maxc;
+    for (; T >= 1; --T) {
+        if (above + hist[T] >= cap)
+            break;
+        above += hist[T];
+    }
+    free(hist);
+    col_count_t *sel = (col_count_t *)malloc((size_t)cap * sizeof(col_count_t));
+    if (!sel) {
+        free(cnt);
+        return -1;
+    }
+    int64_t n = 0, eq = 0, mass = 0;
+    const int64_t eq_cap = T >= 1 ? cap - above : 0;
+    for (int64_t c = 0; c < n_cols; ++c) {
+        const int64_t k = cnt[c];
+        if (k <= 0 || (T >= 1 && k < T))
+            continue;
+        if (T >= 1 && k == T) {
+            if (eq >= eq_cap)
+                continue;
+            ++eq;
+        }
+        sel[n].cnt = k;
+        sel[n].col = (int32_t)c;
+        mass += k;
+        ++n;
+    }
+    free(cnt);
+    /* the rule: worth a table when the chosen columns take half of the
+     * gathers and each is re-read at least 8 times per SpMV (the table
+     * fill costs one scattered read per hot column) */
+    if (H_req == 0 && (2 * mass < nnz || mass < 8 * n)) {
+        free(sel);
+        return 0;
+    }
+    qsort(sel, (size_t)n, sizeof *sel, by_count_desc);
+    int32_t *rank = (int32_t *)malloc((size_t)n_cols * sizeof(int32_t));
+    if (!rank) {
+        free(sel);
+        return -1;
+    }
+    for (int64_t c = 0; c < n_cols; ++c)
+        rank[c] = -1;
+    for (int64_t i = 0; i < n; ++i) {
+        hot[i] = sel[i].col;
+        rank[sel[i].col] = (int32_t)i;
+    }
+    free(sel);
+#pragma omp parallel for schedule(static)
+    for (int64_t j = 0; j < nnz; ++j) {
+        const int32_t r = rank[col_out[j]];
+        if (r >= 0)
+            col_out[j] = (int32_t)(n_cols + r);
+    }
+    free(rank);
+    return n;
+}
+
 int spmv_csr_pick_variant(int64_t n_rows, const int64_t *row_ptr)
 {
     int64_t mx = 0;

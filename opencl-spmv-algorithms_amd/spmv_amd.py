@@ -83,6 +83,8 @@ HIP_SYMBOLS = {
     "spmv_csr_run_variant": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, ctypes.c_int, ctypes.c_int]),
     "spmv_csr_tiled_ws_bytes": (ctypes.c_size_t, [_c_i64, _c_i64]),
     "spmv_csr_run_tiled": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t]),
+    "spmv_csr_hot_ws_bytes": (ctypes.c_size_t, [_c_i64, _c_i64, _c_i64]),
+    "spmv_csr_run_tiled_hot": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, _c_i64, _vp, _vp, ctypes.c_size_t]),
     "spmv_csr16_run": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_int]),
     "spmv_hyb_ws_bytes": (ctypes.c_size_t, [_c_i64]),
     "spmv_hyb_run": (ctypes.c_int, [Dims, _c_i32, _c_i64, _c_i32, _vp, _vp, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp,
@@ -159,6 +161,7 @@ HOST_SYMBOLS = {
     "spmv_csr_from_coo": (ctypes.c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "spmv_csr_row_stats": (ctypes.c_int, [_c_i64, _vp, ctypes.POINTER(_c_i64), ctypes.POINTER(_c_i64), ctypes.POINTER(ctypes.c_double)]),
     "spmv_csr_pick_variant": (ctypes.c_int, [_c_i64, _vp]),
+    "spmv_hot_columns": (_c_i64, [_c_i64, _c_i64, _vp, _c_i64, _vp, _vp]),
     "spmv_ell_plan": (ctypes.c_int, [_c_i64, _vp, _c_i32, ctypes.POINTER(_c_i32), ctypes.POINTER(_c_i64)]),
     "spmv_ell_fill": (ctypes.c_int, [_c_i64, _vp, _vp, _vp, _c_i32, _c_i64, _c_i32, _vp, _vp]),
     "spmv_sell_plan": (ctypes.c_int, [_c_i64, _vp, _c_i32, _c_i32, _c_i32, ctypes.POINTER(_c_i64), ctypes.POINTER(_c_i64)]),
@@ -404,6 +407,18 @@ def sell_split_plan(s: dict, T: int | None = None):
     return T, cs[:n], ck[:n]
 
 
+def hot_columns(n_cols: int, col, H: int = 0):
+    """spmv_hot_columns: (H, hot[H], col_hot) — the H most frequent columns
+    and col with them renumbered n_cols + rank (H = 0: the library rule)."""
+    col = np.ascontiguousarray(col, dtype=np.int32)
+    hot = np.empty(max(H, 1 << 19), np.int32)
+    out = np.empty(max(col.size, 1), np.int32)
+    n = host_lib().spmv_hot_columns(n_cols, col.size, _ptr(col), H, _ptr(hot), _ptr(out))
+    if n < 0:
+        raise SpmvError(OTHER_ERROR, "spmv_hot_columns", "bad arguments")
+    return int(n), hot[:n].copy(), out[: col.size]
+
+
 def cmrs_build(n_rows: int, ptr, h: int = 8):
     ns = (n_rows + h - 1) // h
     sp = np.empty(ns + 1, np.int64)
@@ -526,7 +541,10 @@ class DeviceMatrix:
             rc = lib.spmv_csr_run_xwin(d, _ptr(a["row_ptr"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
                                        p["lanes"], p.get("xwin_rows", 0), _ptr(a["win"]), p["xcap"])
         elif self.fmt == "csr":
-            if p.get("variant", 0) == 4:
+            if p.get("variant", 0) == 4 and p.get("H", 0) > 0:
+                rc = lib.spmv_csr_run_tiled_hot(d, _ptr(a["row_ptr"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x),
+                                                _ptr(y), p["H"], _ptr(a["hot"]), _ptr(a["ws"]), a["ws"].numel())
+            elif p.get("variant", 0) == 4:
                 rc = lib.spmv_csr_run_tiled(d, _ptr(a["row_ptr"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x),
                                             _ptr(y), _ptr(a["ws"]), a["ws"].numel())
             else:
@@ -675,14 +693,17 @@ def _csr_xwin(dm: DeviceMatrix) -> None:
 def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int = 0, ki: int = 0, C: int = 64,
               sigma: int = 1024, h: int = 8, ell_max_padding: float | None = 64.0,
               xwin: bool | None = None, xwin_rows: int = 0, split: int | None = None,
-              cmrs_variant: int | None = None) -> DeviceMatrix:
+              cmrs_variant: int | None = None, hot: int | None = None,
+              csr16_max_escape: float | None = 0.5) -> DeviceMatrix:
     """Build `fmt` on the host (libspmv_host.so) and upload it.  xwin (CSR,
     ELL, SELL; default on): also build the per-workgroup x windows on the
     device and run the LDS x-window kernels (same bits as without).  split
     (SELL) / cmrs_variant (CMRS): None = the library's skew rule."""
     torch = _torch()
     if xwin is None:
-        xwin = fmt in ("csr", "ell", "sell", "coo", "cmrs")
+        # COO: per-tile windows measured slower (0.534 vs 0.491 ms on the
+        # cant-like batch), so they stay opt-in; CMRS 0.352 vs 0.404 ms
+        xwin = fmt in ("csr", "ell", "sell", "cmrs")
     device = torch.device(device)
     dm = DeviceMatrix(fmt, m.n_rows, m.n_cols, m.nnz, device)
     if fmt == "coo":
@@ -703,13 +724,24 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
         dm.arrays = dict(row_ptr=_dev_tensor(ptr, device), col=_dev_tensor(col, device),
                          val=_dev_tensor(val, device))
         if variant == 4:
-            ws = hip_lib().spmv_csr_tiled_ws_bytes(m.n_rows, m.nnz)
+            # hot-column table for power-law columns (None: library rule)
+            H, hot_cols, col_hot = hot_columns(m.n_cols, col, 0 if hot is None else hot) if hot != 0 else (0, None, col)
+            dm.params["H"] = H
+            if H > 0:
+                dm.arrays["col"] = _dev_tensor(col_hot, device)
+                dm.arrays["hot"] = _dev_tensor(hot_cols, device)
+            ws = hip_lib().spmv_csr_hot_ws_bytes(m.n_rows, m.nnz, H)
             dm.arrays["ws"] = torch.empty(ws, dtype=torch.uint8, device=device)
         elif xwin and variant in (0, 3):
             _csr_xwin(dm)
         dm.stored_bytes = 12 * m.nnz + 8 * (m.n_rows + 1)
     elif fmt == "csr16":
         c = csr16_build(col)
+        if csr16_max_escape is not None and c["n_esc"] > csr16_max_escape * max(c["n_blocks"], 1):
+            # columns spread wider than 16 bits in most blocks (R-MAT): the
+            # escapes store more than plain CSR; reported N/A like ELL padding
+            raise SpmvError(OTHER_ERROR, "csr16_build", f"{c['n_esc']} of {c['n_blocks']} 64-entry blocks "
+                            f"need 32-bit escapes (> {csr16_max_escape:.0%})")
         dm.params = dict(lanes=lanes, n_blocks=c["n_blocks"], n_esc=c["n_esc"])
         dm.arrays = dict(row_ptr=_dev_tensor(ptr, device), blk_base=_dev_tensor(c["blk_base"], device),
                          col_off=_dev_tensor(c["col_off"], device), col_esc=_dev_tensor(c["col_esc"], device),

@@ -63,8 +63,8 @@ FMT_PARAMS = [
     ("cmrs", {"h": 8, "cmrs_variant": 1}),
     ("cmrs", {"h": 1, "cmrs_variant": 1}),
     ("cmrs", {"h": 64, "cmrs_variant": 1}),
-    # COO / CMRS with global x gathers (the defaults stage x windows in LDS)
-    ("coo", {"xwin": False}),
+    # COO with x windows in LDS (opt-in), CMRS with global x gathers
+    ("coo", {"xwin": True}),
     ("cmrs", {"h": 8, "xwin": False}),
 ]
 IDS = [f"{f}-{'-'.join(f'{k}{v}' for k, v in kw.items()) or 'default'}" for f, kw in FMT_PARAMS]
@@ -134,6 +134,7 @@ def test_cantlike_batch_random_x(torch_dev, fmt):
                                     ("sell", {"split": 0}), ("sell", {"split": 256, "ki": 2}),
                                     ("sell", {"split": 64, "ki": 1, "xwin": False}),
                                     ("sell", {"sigma": 65536, "ki": 2}),
+                                    ("csr", {"variant": 4, "hot": 4096}), ("csr", {"variant": 4, "hot": 0}),
                                     ("cmrs", {"cmrs_variant": 0}), ("cmrs", {"cmrs_variant": 1, "h": 1}),
                                     ("cmrs", {"cmrs_variant": 1, "h": 64})])
 def test_rmat_skewed(torch_dev, fmt, kw):
@@ -210,7 +211,7 @@ def test_csr16_bit_identical_to_csr(torch_dev, case):
         m = sa.gen_random(20_000, 300_000, 0, 2_000, seed=21)
     x = torch.from_numpy(np.random.default_rng(6).uniform(-1, 1, m.n_cols)).to(dev)
     ys = []
-    for fmt, kw in (("csr", {"variant": 3, "lanes": 4}), ("csr16", {"lanes": 4})):
+    for fmt, kw in (("csr", {"variant": 3, "lanes": 4}), ("csr16", {"lanes": 4, "csr16_max_escape": None})):
         dm = sa.to_device(m, fmt, dev, **kw)
         y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
         dm.run(x, y)
@@ -497,3 +498,31 @@ def test_coo_cmrs_xwin_bit_identical(torch_dev, case, fmt, kw):
         torch.cuda.synchronize()
         assert torch.equal(ya.view(torch.int64), yb.view(torch.int64))
         assert_parity(m, ya.cpu().numpy()[: m.n_rows], x.cpu().numpy())
+
+
+@pytest.mark.parametrize("H", [1, 4096, 1 << 16])
+def test_csr_hot_bit_identical(torch_dev, H):
+    """Hot-column table (spmv_csr_run_tiled_hot): the same products in the
+    same order as the tiled kernel on the original columns."""
+    torch, dev = torch_dev
+    m = sa.gen_rmat(1_000_000, 10_000_000, scale=20, seed=1)
+    a = sa.to_device(m, "csr", dev, variant=4, hot=H)
+    b = sa.to_device(m, "csr", dev, variant=4, hot=0)
+    assert a.params["H"] == H and b.params["H"] == 0
+    x = torch.from_numpy(np.random.default_rng(6).uniform(-1, 1, m.n_cols)).to(dev)
+    ya = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
+    yb = torch.full_like(ya, float("nan"))
+    a.run(x, ya)
+    b.run(x, yb)
+    torch.cuda.synchronize()
+    assert torch.equal(ya.view(torch.int64), yb.view(torch.int64))
+    assert_parity(m, ya.cpu().numpy(), x.cpu().numpy())
+
+
+def test_csr16_refuses_escape_heavy_matrix(torch_dev):
+    """R-MAT columns spread over 1e6 ids: most 64-entry blocks need 32-bit
+    escapes, so CSR16 is reported not applicable (like ELL's padding cap)."""
+    torch, dev = torch_dev
+    m = sa.gen_rmat(1_000_000, 10_000_000, scale=20, seed=1)
+    with pytest.raises(sa.SpmvError):
+        sa.to_device(m, "csr16", dev)

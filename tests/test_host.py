@@ -373,3 +373,45 @@ def test_cmrs_pick_variant(kind, exp):
     ptr, _, _ = sa.csr_from_coo(m)
     c = sa.cmrs_build(m.n_rows, ptr, h=8)
     assert sa.host_lib().spmv_cmrs_pick_variant(c["n_strips"], sa._ptr(c["strip_ptr"])) == exp
+
+
+@pytest.mark.parametrize("H", [0, 1, 100, 5000])
+def test_hot_columns_selection_and_renumbering(H):
+    """spmv_hot_columns: the H most frequent columns in decreasing count,
+    renumbered n_cols + rank; every other column untouched (the inverse
+    map restores col exactly, so the hot-column CSR is the same matrix)."""
+    m = sa.gen_rmat(100_000, 1_000_000, scale=17, seed=2)
+    _, col, _ = sa.csr_from_coo(m)
+    n, hot, ch = sa.hot_columns(m.n_cols, col, H)
+    cnt = np.bincount(col, minlength=m.n_cols)
+    if H == 0:  # the rule: 1e5 columns (0.8 MB of x) need no table
+        assert n == 0 and np.array_equal(ch, col)
+        return
+    assert n == min(H, np.count_nonzero(cnt))
+    assert len(set(hot.tolist())) == n and np.all(np.diff(cnt[hot]) <= 0)
+    rest = np.delete(cnt, hot)
+    assert cnt[hot].min() >= rest.max()
+    is_hot = ch >= m.n_cols
+    back = ch.copy()
+    back[is_hot] = hot[ch[is_hot] - m.n_cols]
+    assert np.array_equal(back, col)
+    assert not np.isin(col[~is_hot], hot).any()
+
+
+@pytest.mark.parametrize("skewed", [True, False])
+def test_hot_columns_rule(skewed):
+    """H = 0 picks 2^19 columns when they hold at least half the entries of
+    a matrix with more than 2^21 columns, 8 or more each on average; a
+    uniform column spread (little reuse) gets none."""
+    rng = np.random.default_rng(9)
+    n_cols = 3_000_000
+    if skewed:
+        col = np.concatenate([rng.integers(0, 1000, 5_000_000), rng.integers(0, n_cols, 600_000)])
+    else:
+        col = rng.integers(0, n_cols, 2_000_000)
+    col = col.astype(np.int32)
+    n, hot, ch = sa.hot_columns(n_cols, col, 0)
+    if skewed:
+        assert n == 1 << 19 and np.all(hot[:1000] < 1000)
+    else:
+        assert n == 0 and np.array_equal(ch, col)

@@ -40,6 +40,8 @@ for s in "${steps[@]}"; do
     sweeprmat2) run sweep_rmat 900 python tools/sweep.py --matrix rmat --rounds 1 --reps 20;;
     benchrmat) run bench_rmat 600 python bench.py --workload rmat --steps 20;;
     benchbanded) run bench_banded_sell 600 python bench.py --workload banded --format sell --steps 20 && run bench_banded_csr 600 python bench.py --workload banded --format csr --steps 20;;
+    rehearse8) run shard_rehearse 900 python tools/shard_rehearse.py --gpus 1,2,4,8 &&
+               run shard_rehearse_sell 900 python tools/shard_rehearse.py --gpus 1,8 --format sell;;
     rehearse2) run rehearse2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --backend gloo --share-gpu --steps 20;;
     drivers) run drivers 600 python -m pytest tests/test_drivers_gpu.py -q;;
     sweepremap) SPMV_XCD_REMAP=1 run sweep_remap 600 python tools/sweep.py --rounds 2 --only csr,sell,ell;;
@@ -52,6 +54,8 @@ for s in "${steps[@]}"; do
     rmatexp) run rmat_exp 600 python tools/rmat_exp.py;;
     testsplit) run gpu_tests_split 900 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "split or cmrs_variant or rmat_skewed or h8-cmrs or bitwise";;
     benchrmatpf) run bench_rmat_pf 900 python bench.py --workload rmat --steps 20 --per-format yes;;
+    sweeprmatenv) run sweep_rmat_env 900 python tools/sweep.py --matrix rmat --rounds 2 --reps 10 --env-only --only csr,sell,coo;;
+    sweepcantenv) run sweep_cant_env 600 python tools/sweep.py --rounds 2 --env-only --only coo,cmrs,csr;;
     sweeprmatfmt) run sweep_rmat_fmt 600 python tools/sweep.py --matrix rmat --rounds 1 --reps 10 --only sell,cmrs,coo,hyb;;
     pmc) run pmc 1100 python tools/pmc_traffic.py;;
     pmcvar) run pmc_var 1100 python tools/pmc_traffic.py --out traffic_variants.json --formats "csr,csr@SPMV_XCD_REMAP=1,csr:lanes=16,sell:sigma=256,sell,ell@SPMV_XCD_REMAP=1";;

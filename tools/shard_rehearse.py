@@ -1,0 +1,94 @@
+#!/usr/bin/env python3
+"""Strong-scaling rehearsal of the row-sharded R-MAT on ONE GPU.
+
+bench.py --workload rmat --gpus G cuts the 1e7 x 1e7 / 1e8-entry R-MAT
+(BASELINE.json configs[3], the north-star scaling matrix) into G
+nnz-balanced row shards (spmv_partition_rows, aligned to 1024 rows), one
+per GPU, x replicated, and reports bytes_alg(whole) / max over ranks of the
+step time.  Here every shard of every G is built and timed ALONE on cuda:0
+(HIP events over back-to-back launches, as bench.py), so
+
+    aggregate_GBs(G) = bytes_alg(whole matrix) / max_g t_g
+
+is the SpMV-only figure a G-GPU run reports when every GPU runs its shard
+concurrently (the GPUs share nothing on the SpMV path).  Back-to-back
+launches keep part of a small shard and of x in the 256 MiB Infinity Cache,
+on every GPU alike, so the figure is labelled warm.  The y all-gather over
+RCCL is not included (bench.py times it separately).  A rehearsal on one
+card, not a substitute for the driver's 8-GPU run.
+
+    python tools/shard_rehearse.py [--gpus 1,2,4,8] [--format csr] [--reps 20]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(REPO / "opencl-spmv-algorithms_amd"), str(REPO)]
+import spmv_amd as sa  # noqa: E402
+
+
+def time_shard(torch, dm, x, y, reps):
+    s = torch.cuda.current_stream()
+    for _ in range(3):
+        dm.run(x, y, s)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
+    ev[0].record(s)
+    for k in range(reps):
+        dm.run(x, y, s)
+        ev[k + 1].record(s)
+    torch.cuda.synchronize()
+    return float(np.mean([ev[k].elapsed_time(ev[k + 1]) for k in range(reps)]))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", default="1,2,4,8")
+    ap.add_argument("--format", default="csr")
+    ap.add_argument("--reps", type=int, default=20)
+    a = ap.parse_args()
+    import torch
+
+    dev = torch.device("cuda:0")
+    full = sa.gen_rmat()
+    ptr, col, val = sa.csr_from_coo(full)
+    n, z = full.n_rows, full.nnz
+    del full
+    xh = sa.ramp_x(n)
+    x = torch.from_numpy(xh).to(dev)
+    b_total = sa.bytes_alg(n, n, z)
+    base = None
+    for G in [int(g) for g in a.gpus.split(",")]:
+        bounds = sa.partition_rows(n, ptr, G, align=1024)
+        times, nnzs, params = [], [], None
+        for r in range(G):
+            lo, hi = int(bounds[r]), int(bounds[r + 1])
+            lptr = ptr[lo:hi + 1] - ptr[lo]
+            loc = sa.Coo(hi - lo, n, np.repeat(np.arange(hi - lo, dtype=np.int32), np.diff(lptr)),
+                         col[ptr[lo]:ptr[hi]], val[ptr[lo]:ptr[hi]])
+            dm = sa.to_device(loc, a.format, dev)
+            params = params or {k: v for k, v in dm.params.items() if isinstance(v, (int, float, str))}
+            y = torch.empty(max(loc.n_rows, 1), dtype=torch.float64, device=dev)
+            times.append(time_shard(torch, dm, x, y, a.reps))
+            nnzs.append(loc.nnz)
+            bad, first = sa.check(loc, xh, y[:loc.n_rows].cpu().numpy())
+            if bad:
+                raise SystemExit(f"G={G} shard {r}: parity failure at row {first}")
+            del dm, y, loc
+            torch.cuda.empty_cache()
+        tmax = max(times)
+        agg = b_total / (tmax * 1e-3) * 1e-9
+        base = base or agg
+        print(json.dumps({"workload": "rmat 1e7/1e8", "format": a.format, "params_shard0": params, "gpus": G,
+                          "shard_nnz": nnzs, "shard_ms": [round(t, 4) for t in times], "max_ms": round(tmax, 4),
+                          "aggregate_GBs_warm": round(agg, 1), "speedup_vs_first": round(agg / base, 2)}),
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()

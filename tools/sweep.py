@@ -38,6 +38,15 @@ VARIANTS = [
     ("hyb", {"env": {}}),
     ("hyb", {"ki": 1, "env": {}}),
     ("csr", {"variant": 4, "env": {}}),
+    ("csr", {"variant": 4, "hot": 0, "env": {}}),
+    ("csr", {"variant": 4, "hot": 1 << 18, "env": {}}),
+    ("csr", {"variant": 4, "hot": 1 << 20, "env": {}}),
+    ("csr", {"variant": 4, "env": {"SPMV_STREAM_NT": "0"}}),
+    ("coo", {"xwin": True, "env": {}}),
+    ("sell", {"C": 64, "sigma": 65536, "ki": 1, "env": {}}),
+    ("sell", {"C": 64, "sigma": 1 << 20, "ki": 1, "env": {}}),
+    ("sell", {"C": 64, "sigma": 1 << 24, "ki": 1, "env": {}}),
+    ("sell", {"C": 64, "sigma": 1 << 24, "ki": 2, "env": {}}),
 ]
 
 

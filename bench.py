@@ -51,6 +51,9 @@ KERNEL_NAMES = {  # dominant kernel per format (as rocprofv3 names it)
     "coo": "coo_tile_kernel",
     "cmrs": "cmrs_kernel",
 }
+# R-MAT shards: a row costs the tiled kernel about as much as this many
+# entries (tools/shard_rehearse.py); shards balance entries + weight * rows
+RMAT_ROW_WEIGHT = 2.0
 CSR_DEFAULT_VARIANT = 3  # must match csr_default_variant() in csrc/csr.hip
 
 
@@ -71,7 +74,8 @@ def parse():
     p.add_argument("--variant", type=int, default=0, help="CSR kernel variant (0 auto, 1 direct, 2 staged)")
     p.add_argument("--ki", type=int, default=0, help="k-interleave (0: format default, ELL 2, SELL 1)")
     p.add_argument("--C", type=int, default=64)
-    p.add_argument("--sigma", type=int, default=1024)
+    p.add_argument("--sigma", type=int, default=0,
+                   help="SELL sigma (0: 1024 = configs[2]; whole-matrix sort, 2^24, on R-MAT)")
     p.add_argument("--h", type=int, default=8)
     p.add_argument("--profile", action="store_true", help="only the timed loop (for rocprofv3 passes)")
     p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -109,7 +113,8 @@ def fmt_kwargs(args, fmt):
     if fmt == "ell":
         return {"ki": args.ki}
     if fmt == "sell":
-        return {"C": args.C, "sigma": args.sigma, "ki": args.ki}
+        sigma = args.sigma or (1 << 24 if args.workload == "rmat" else 1024)
+        return {"C": args.C, "sigma": sigma, "ki": args.ki}
     if fmt == "cmrs":
         return {"h": args.h}
     return {}
@@ -210,7 +215,7 @@ def build_workload(args, torch, dev, rank, world):
     if args.workload == "rmat":
         full = sa.gen_rmat()  # deterministic: every rank builds the same matrix
         ptr, col, val = sa.csr_from_coo(full)
-        bounds = sa.partition_rows(full.n_rows, ptr, world, align=1024)
+        bounds = sa.partition_rows(full.n_rows, ptr, world, align=1024, row_weight=RMAT_ROW_WEIGHT)
         lo, hi = int(bounds[rank]), int(bounds[rank + 1])
         lptr = ptr[lo:hi + 1] - ptr[lo]
         loc = sa.Coo(hi - lo, full.n_cols, np.repeat(np.arange(hi - lo, dtype=np.int32), np.diff(lptr)),

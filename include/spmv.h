@@ -126,7 +126,13 @@ int spmv_csr_run_tiled(spmv_dims d, const int64_t *row_ptr, const int32_t *col,
 size_t spmv_csr_hot_ws_bytes(int64_t n_rows, int64_t nnz, int64_t H);
 int spmv_csr_run_tiled_hot(spmv_dims d, const int64_t *row_ptr, const int32_t *col_hot,
                            const double *val, const double *x, double *y, int64_t H,
-                           const int32_t *hot, void *ws, size_t ws_bytes);
+                           const int32_t *hot, const int32_t *own_lo_plan, void *ws,
+                           size_t ws_bytes);
+/* The tile -> first owned row table of the entry-balanced CSR (int32,
+ * spmv_csr_tiled_plan_len(nnz) entries) built once from row_ptr; passed as
+ * own_lo_plan it saves every run its pre-pass (NULL: built per run).    */
+int64_t spmv_csr_tiled_plan_len(int64_t nnz);
+int spmv_csr_tiled_plan(spmv_dims d, const int64_t *row_ptr, int32_t *own_lo);
 
 /* ---------------------------------------------------------------- ELL ---
  * Replaces kernel `ell(val,idx,x,y,int N,int K,__local)` (reference
@@ -216,6 +222,19 @@ int spmv_cmrs_run(spmv_dims d, int32_t h, int64_t n_strips,
                   const int64_t *strip_ptr, const uint8_t *row_in_strip,
                   const int32_t *col, const double *val, const double *x,
                   double *y);
+/* COO and entry-balanced CMRS over a hot-column table (col_hot / hot from
+ * spmv_hot_columns on the format's own column array), as
+ * spmv_csr_run_tiled_hot: bit-identical to spmv_coo_run /
+ * spmv_cmrs_run_tiled on the original columns; H = 0 is those runs.     */
+size_t spmv_coo_hot_ws_bytes(int64_t nnz, int64_t H);
+int spmv_coo_run_hot(spmv_dims d, const int32_t *row, const int32_t *col_hot, const double *val,
+                     const double *x, double *y, int64_t H, const int32_t *hot, void *ws, size_t ws_bytes);
+size_t spmv_cmrs_hot_ws_bytes(int64_t n_strips, int64_t nnz, int32_t h, int64_t H);
+int spmv_cmrs_run_tiled_hot(spmv_dims d, int32_t h, int64_t n_strips, const int64_t *strip_ptr,
+                            const uint8_t *row_in_strip, const int32_t *col_hot, const double *val,
+                            const double *x, double *y, int64_t H, const int32_t *hot, void *ws,
+                            size_t ws_bytes);
+
 /* COO and CMRS with x windows in LDS (the protocol of the CSR/ELL/SELL
  * x-window entry points): *_xwin_bytes sizes the window buffer,
  * *_xwin_build fills it on the device (column range of every COO tile of

@@ -164,6 +164,11 @@ int spmv_csr16_fill(int64_t nnz, const int32_t *col, int32_t *blk_base, uint16_t
  * bounds has parts+1 entries, bounds[0] = 0, bounds[parts] = n_rows.    */
 int spmv_partition_rows(int64_t n_rows, const int64_t *row_ptr, int parts,
                         int64_t align, int64_t *bounds);
+/* Same cut, balancing entries + row_weight per row (a row costs the
+ * kernels about as much as row_weight entries: its offset, its y store and
+ * its reduction; 0 = spmv_partition_rows).                              */
+int spmv_partition_rows_weighted(int64_t n_rows, const int64_t *row_ptr, int parts, int64_t align,
+                                 double row_weight, int64_t *bounds);
 
 /* ---------------------------------------------------------- CPU loops ---
  * OpenMP restatements of the reference's compute_using_cpu loops, with

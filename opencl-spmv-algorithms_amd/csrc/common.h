@@ -55,10 +55,15 @@ int launch_csr_tiled(const spmv_dims &d, const int64_t *row_ptr, const int32_t *
 int64_t csr_tiled_tile();
 int launch_csr_tiled_hot(const spmv_dims &d, const int64_t *row_ptr, const int32_t *col,
                          const double *val, const double *x, double *y, int64_t H, const int32_t *hot,
-                         double *xh, int32_t *own_lo, int32_t *carry_row, double *carry_val);
+                         double *xh, const int32_t *own_lo_plan, int32_t *own_lo, int32_t *carry_row,
+                         double *carry_val);
 int launch_cmrs_tiled(const spmv_dims &d, int32_t h, int64_t n_strips, const int64_t *strip_ptr,
                       const uint8_t *rin, const int32_t *col, const double *val, const double *x,
-                      double *y, int32_t *own_lo, int32_t *carry_row, double *carry_val);
+                      double *y, int32_t *own_lo, int32_t *carry_row, double *carry_val, int64_t H = 0,
+                      const int32_t *hot = nullptr, double *xh = nullptr);
+int launch_coo_staged_hot(const spmv_dims &d, const int32_t *row, const int32_t *col, const double *val,
+                          const double *x, double *y, int32_t *carry_row, double *carry_val, int64_t H,
+                          const int32_t *hot, double *xh);
 int64_t cmrs_tiled_tile();
 // the deterministic carry pass shared by COO and tiled CSR (coo.hip)
 int launch_carry(int64_t tiles, const int32_t *carry_row, const double *carry_val, double *y,

@@ -426,3 +426,63 @@ extern "C" int spmv_cmrs_run_xwin(spmv_dims d, int32_t h, int64_t n_strips, cons
     SPMV_GUARD(d);
     return launch_cmrs_staged(d, h, n_strips, strip_ptr, row_in_strip, col, val, x, y, (const int2 *)win, xcap);
 }
+
+extern "C" size_t spmv_coo_hot_ws_bytes(int64_t nnz, int64_t H)
+{
+    return (size_t)(H > 0 ? H : 0) * sizeof(double) + spmv_coo_ws_bytes(nnz);
+}
+
+// COO whose column ids >= n_cols name the hot-column table (host
+// spmv_hot_columns, applied to the row-sorted columns): bit-identical to
+// spmv_coo_run on the original columns.
+extern "C" int spmv_coo_run_hot(spmv_dims d, const int32_t *row, const int32_t *col_hot, const double *val,
+                                const double *x, double *y, int64_t H, const int32_t *hot, void *ws,
+                                size_t ws_bytes)
+{
+    if (d.n_rows < 0 || d.nnz < 0 || d.n_rows > INT32_MAX || H < 0 || d.n_cols + H > INT32_MAX)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_coo_run_hot: bad sizes");
+    if (H == 0 || d.n_rows == 0 || d.nnz == 0)
+        return spmv_coo_run(d, row, col_hot, val, x, y, ws, ws_bytes);
+    if (!hot || !ws || ws_bytes < spmv_coo_hot_ws_bytes(d.nnz, H))
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_coo_run_hot: hot list or workspace missing");
+    SPMV_GUARD(d);
+    const int64_t st_tiles = (d.nnz + coo_staged_tile() - 1) / coo_staged_tile();
+    double *xh = (double *)ws;
+    double *cv = xh + H;
+    int32_t *cr = (int32_t *)(cv + st_tiles);
+    int rc = launch_coo_staged_hot(d, row, col_hot, val, x, y, cr, cv, H, hot, xh);
+    if (rc != SPMV_SUCCESS)
+        return rc;
+    return launch_carry(st_tiles, cr, cv, y, (hipStream_t)d.stream);
+}
+
+extern "C" size_t spmv_cmrs_hot_ws_bytes(int64_t n_strips, int64_t nnz, int32_t h, int64_t H)
+{
+    return (size_t)(H > 0 ? H : 0) * sizeof(double) + spmv_cmrs_tiled_ws_bytes(n_strips, nnz, h);
+}
+
+// Entry-balanced CMRS over a hot-column table (as spmv_coo_run_hot).
+extern "C" int spmv_cmrs_run_tiled_hot(spmv_dims d, int32_t h, int64_t n_strips, const int64_t *strip_ptr,
+                                       const uint8_t *row_in_strip, const int32_t *col_hot, const double *val,
+                                       const double *x, double *y, int64_t H, const int32_t *hot, void *ws,
+                                       size_t ws_bytes)
+{
+    if (H < 0 || d.n_cols + H > INT32_MAX)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_cmrs_run_tiled_hot: bad sizes");
+    if (H == 0 || d.n_rows <= 0 || d.nnz <= 0)
+        return spmv_cmrs_run_tiled(d, h, n_strips, strip_ptr, row_in_strip, col_hot, val, x, y, ws, ws_bytes);
+    if (h < 1 || h > 64 || n_strips != (d.n_rows + h - 1) / h || d.n_rows > INT32_MAX)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_cmrs_run_tiled_hot: bad strips");
+    if (!hot || !ws || ws_bytes < spmv_cmrs_hot_ws_bytes(n_strips, d.nnz, h, H))
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_cmrs_run_tiled_hot: hot list or workspace missing");
+    SPMV_GUARD(d);
+    const int64_t tiles = (d.nnz + cmrs_tiled_tile() - 1) / cmrs_tiled_tile();
+    if (tiles * h > INT32_MAX)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_cmrs_run_tiled_hot: grid too large");
+    double *xh = (double *)ws;
+    double *carry_val = xh + H;
+    int32_t *own_lo = (int32_t *)(carry_val + (int64_t)h * tiles);
+    int32_t *carry_row = own_lo + tiles + 1;
+    return launch_cmrs_tiled(d, h, n_strips, strip_ptr, row_in_strip, col_hot, val, x, y, own_lo, carry_row,
+                             carry_val, H, hot, xh);
+}

@@ -1013,14 +1013,15 @@ extern "C" size_t spmv_csr_hot_ws_bytes(int64_t n_rows, int64_t nnz, int64_t H)
 // un-renumbered columns, so y is bit-identical to it.
 extern "C" int spmv_csr_run_tiled_hot(spmv_dims d, const int64_t *row_ptr, const int32_t *col_hot,
                                       const double *val, const double *x, double *y, int64_t H,
-                                      const int32_t *hot, void *ws, size_t ws_bytes)
+                                      const int32_t *hot, const int32_t *own_lo_plan, void *ws,
+                                      size_t ws_bytes)
 {
     if (d.n_rows < 0 || d.n_cols < 0 || d.nnz < 0 || d.n_rows > INT32_MAX || H < 0 ||
         d.n_cols + H > INT32_MAX)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_run_tiled_hot: bad sizes");
-    if (H == 0 || d.n_rows == 0 || d.nnz == 0)
+    if (d.n_rows == 0 || d.nnz == 0 || (H == 0 && !own_lo_plan))
         return spmv_csr_run_tiled(d, row_ptr, col_hot, val, x, y, ws, ws_bytes);
-    if (!hot || !ws || ws_bytes < spmv_csr_hot_ws_bytes(d.n_rows, d.nnz, H))
+    if ((H > 0 && !hot) || !ws || ws_bytes < spmv_csr_hot_ws_bytes(d.n_rows, d.nnz, H))
         return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_run_tiled_hot: hot list or workspace missing");
     SPMV_GUARD(d);
     const int64_t tiles = (d.nnz + csr_tiled_tile() - 1) / csr_tiled_tile();
@@ -1030,7 +1031,8 @@ extern "C" int spmv_csr_run_tiled_hot(spmv_dims d, const int64_t *row_ptr, const
     double *carry_val = xh + H;
     int32_t *own_lo = (int32_t *)(carry_val + tiles);
     int32_t *carry_row = own_lo + tiles + 1;
-    int rc = launch_csr_tiled_hot(d, row_ptr, col_hot, val, x, y, H, hot, xh, own_lo, carry_row, carry_val);
+    int rc = launch_csr_tiled_hot(d, row_ptr, col_hot, val, x, y, H, hot, xh, own_lo_plan, own_lo, carry_row,
+                                  carry_val);
     if (rc != SPMV_SUCCESS)
         return rc;
     return launch_carry(tiles, carry_row, carry_val, y, (hipStream_t)d.stream);

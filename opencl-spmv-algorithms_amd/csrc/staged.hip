@@ -145,12 +145,14 @@ __global__ __launch_bounds__(kBlock) void cmrs_staged_kernel(
 // the last tile also covers the trailing rows).  A first row that began
 // in an earlier tile goes to carry[tile] for coo_carry_kernel (coo.hip).
 // XW: the tile's x window in LDS (as cmrs_staged_kernel), bit-identical.
-template <int L, int R, bool ACC, bool XW>
+// XS/NT: x accessor of the global gathers (XHot: hot-column table) and the
+// stream load policy.
+template <int L, int R, bool ACC, bool XW, bool NT = false, typename XS = XGlobal>
 __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
     int64_t n_rows, int64_t nnz, const int32_t *__restrict__ row,
     const int32_t *__restrict__ col, const double *__restrict__ val,
     const double *__restrict__ x, double *__restrict__ y, int32_t *__restrict__ carry_row,
-    double *__restrict__ carry_val, const int2 *__restrict__ win, int32_t xcap)
+    double *__restrict__ carry_val, const int2 *__restrict__ win, int32_t xcap, const XS xs)
 {
     constexpr int CH = 2 * kBlock * R;
     extern __shared__ double s_x[];
@@ -184,9 +186,9 @@ __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
         }
     }
     if (staged)
-        stage_chunk<R>(t0, t1, col, val, XWindow{s_x, wlo}, s_prod, keys);
+        stage_chunk<R, NT>(t0, t1, col, val, XWindow{s_x, wlo}, s_prod, keys);
     else
-        stage_chunk<R>(t0, t1, col, val, XGlobal{x}, s_prod, keys);
+        stage_chunk<R, NT>(t0, t1, col, val, xs, s_prod, keys);
     __syncthreads();
 
     const int32_t prev = s_prev;
@@ -355,12 +357,12 @@ __global__ __launch_bounds__(kBlock) void csr_tiled_kernel(
 // earlier one leaves up to h partial rows: carry[k·tiles + tile] for row
 // key k (k-major, so each row's continuation tiles are consecutive and
 // coo_carry_kernel adds them in tile order).  Needs kBlock / L >= h.
-template <int L, int R>
+template <int L, int R, typename XS>
 __global__ __launch_bounds__(kBlock) void cmrs_tiled_kernel(
     int64_t n_rows, int32_t h, int64_t n_strips, int64_t nnz, int64_t tiles,
     const int64_t *__restrict__ strip_ptr, const uint8_t *__restrict__ rin,
     const int32_t *__restrict__ col, const double *__restrict__ val,
-    const double *__restrict__ x, double *__restrict__ y,
+    const XS xs, double *__restrict__ y,
     const int32_t *__restrict__ own_lo, int32_t *__restrict__ carry_row,
     double *__restrict__ carry_val)
 {
@@ -375,7 +377,7 @@ __global__ __launch_bounds__(kBlock) void cmrs_tiled_kernel(
     const int64_t t1 = t0 + CH < nnz ? t0 + CH : nnz;
     const int64_t s_lo = own_lo[tile];
     const int64_t s_hi = t1 == nnz ? n_strips - 1 : (int64_t)own_lo[tile + 1] - 1;
-    stage_chunk<R, true>(t0, t1, col, val, XGlobal{x}, s_prod, [&](int t, int64_t p, int n) {
+    stage_chunk<R, true>(t0, t1, col, val, xs, s_prod, [&](int t, int64_t p, int n) {
         s_key2[t] = n == 2 ? *reinterpret_cast<const uint16_t *>(rin + p) : (uint16_t)rin[p];
     });
     __syncthreads();
@@ -426,14 +428,32 @@ __global__ __launch_bounds__(kBlock) void cmrs_tiled_kernel(
 
 int64_t cmrs_tiled_tile() { return 2 * kBlock * 3; }
 
+__global__ __launch_bounds__(kBlock) void hot_gather_kernel(int64_t H, const int32_t *__restrict__ hot,
+                                                            const double *__restrict__ x,
+                                                            double *__restrict__ xh)
+{
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < H)
+        xh[i] = x[hot[i]];
+}
+
+static void launch_hot_gather(int64_t H, const int32_t *hot, const double *x, double *xh, hipStream_t st)
+{
+    if (H > 0)
+        hipLaunchKernelGGL(hot_gather_kernel, dim3((unsigned)((H + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, H,
+                           hot, x, xh);
+}
+
 int launch_cmrs_tiled(const spmv_dims &d, int32_t h, int64_t n_strips, const int64_t *strip_ptr,
                       const uint8_t *rin, const int32_t *col, const double *val, const double *x,
-                      double *y, int32_t *own_lo, int32_t *carry_row, double *carry_val)
+                      double *y, int32_t *own_lo, int32_t *carry_row, double *carry_val, int64_t H,
+                      const int32_t *hot, double *xh)
 {
     constexpr int R = 3;
     const int64_t ch = cmrs_tiled_tile();
     const int64_t tiles = (d.nnz + ch - 1) / ch;
     const hipStream_t st = (hipStream_t)d.stream;
+    launch_hot_gather(H, hot, x, xh, st);
     hipLaunchKernelGGL(csr_tile_rows_kernel, dim3((unsigned)((tiles + 1 + kBlock - 1) / kBlock)),
                        dim3(kBlock), 0, st, n_strips, d.nnz, tiles, ch, strip_ptr, own_lo);
     SPMV_CHECK_LAUNCH("csr_tile_rows_kernel (strips)");
@@ -442,10 +462,17 @@ int launch_cmrs_tiled(const spmv_dims &d, int32_t h, int64_t n_strips, const int
     int L = spmv_csr_auto_lanes(d.n_rows, d.nnz);
     while (L > 1 && L * h > kBlock)
         L >>= 1;
-#define SPMV_CMRS_TILED(LL)                                                                        \
-    hipLaunchKernelGGL((cmrs_tiled_kernel<LL, R>), dim3((unsigned)tiles), dim3(kBlock), 0, st,     \
-                       d.n_rows, h, n_strips, d.nnz, tiles, strip_ptr, rin, col, val, x, y, own_lo, \
-                       carry_row, carry_val)
+#define SPMV_CMRS_TILED(LL)                                                                          \
+    do {                                                                                             \
+        if (H > 0)                                                                                   \
+            hipLaunchKernelGGL((cmrs_tiled_kernel<LL, R, XHot>), dim3((unsigned)tiles), dim3(kBlock), 0, \
+                               st, d.n_rows, h, n_strips, d.nnz, tiles, strip_ptr, rin, col, val,       \
+                               XHot{x, xh, (int32_t)d.n_cols}, y, own_lo, carry_row, carry_val);       \
+        else                                                                                         \
+            hipLaunchKernelGGL((cmrs_tiled_kernel<LL, R, XGlobal>), dim3((unsigned)tiles), dim3(kBlock), \
+                               0, st, d.n_rows, h, n_strips, d.nnz, tiles, strip_ptr, rin, col, val,    \
+                               XGlobal{x}, y, own_lo, carry_row, carry_val);                            \
+    } while (0)
     switch (L) {
     case 1: SPMV_CMRS_TILED(1); break;
     case 2: SPMV_CMRS_TILED(2); break;
@@ -464,7 +491,7 @@ int64_t csr_tiled_tile() { return 2 * kBlock * 3; }
 
 template <typename XS>
 static void launch_tiled_xs(const spmv_dims &d, int64_t tiles, const int64_t *row_ptr, const int32_t *col,
-                            const double *val, XS xs, double *y, int32_t *own_lo, int32_t *carry_row,
+                            const double *val, XS xs, double *y, const int32_t *own_lo, int32_t *carry_row,
                             double *carry_val)
 {
     constexpr int R = 3;
@@ -485,8 +512,10 @@ static void launch_tiled_xs(const spmv_dims &d, int64_t tiles, const int64_t *ro
         SPMV_TILED(8);
     else if (mean >= 12.0)
         SPMV_TILED(4);
-    else
+    else if (mean >= 6.0)
         SPMV_TILED(2);
+    else  // mostly empty rows (an R-MAT shard of high row ids): one lane per row
+        SPMV_TILED(1);
 #undef SPMV_TILED
 }
 
@@ -505,29 +534,26 @@ int launch_csr_tiled(const spmv_dims &d, const int64_t *row_ptr, const int32_t *
     return SPMV_SUCCESS;
 }
 
-__global__ __launch_bounds__(kBlock) void hot_gather_kernel(int64_t H, const int32_t *__restrict__ hot,
-                                                            const double *__restrict__ x,
-                                                            double *__restrict__ xh)
-{
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i < H)
-        xh[i] = x[hot[i]];
-}
-
 int launch_csr_tiled_hot(const spmv_dims &d, const int64_t *row_ptr, const int32_t *col,
                          const double *val, const double *x, double *y, int64_t H, const int32_t *hot,
-                         double *xh, int32_t *own_lo, int32_t *carry_row, double *carry_val)
+                         double *xh, const int32_t *own_lo_plan, int32_t *own_lo, int32_t *carry_row,
+                         double *carry_val)
 {
     const int64_t ch = csr_tiled_tile();
     const int64_t tiles = (d.nnz + ch - 1) / ch;
     const hipStream_t st = (hipStream_t)d.stream;
+    launch_hot_gather(H, hot, x, xh, st);
+    if (!own_lo_plan) {
+        hipLaunchKernelGGL(csr_tile_rows_kernel, dim3((unsigned)((tiles + 1 + kBlock - 1) / kBlock)),
+                           dim3(kBlock), 0, st, d.n_rows, d.nnz, tiles, ch, row_ptr, own_lo);
+        SPMV_CHECK_LAUNCH("csr_tile_rows_kernel");
+        own_lo_plan = own_lo;
+    }
     if (H > 0)
-        hipLaunchKernelGGL(hot_gather_kernel, dim3((unsigned)((H + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, H,
-                           hot, x, xh);
-    hipLaunchKernelGGL(csr_tile_rows_kernel, dim3((unsigned)((tiles + 1 + kBlock - 1) / kBlock)),
-                       dim3(kBlock), 0, st, d.n_rows, d.nnz, tiles, ch, row_ptr, own_lo);
-    SPMV_CHECK_LAUNCH("csr_tile_rows_kernel");
-    launch_tiled_xs(d, tiles, row_ptr, col, val, XHot{x, xh, (int32_t)d.n_cols}, y, own_lo, carry_row, carry_val);
+        launch_tiled_xs(d, tiles, row_ptr, col, val, XHot{x, xh, (int32_t)d.n_cols}, y, own_lo_plan, carry_row,
+                        carry_val);
+    else
+        launch_tiled_xs(d, tiles, row_ptr, col, val, XGlobal{x}, y, own_lo_plan, carry_row, carry_val);
     SPMV_CHECK_LAUNCH("csr_tiled_kernel (hot columns)");
     return SPMV_SUCCESS;
 }
@@ -597,7 +623,7 @@ int launch_coo_staged_acc(const spmv_dims &d, const int32_t *row, const int32_t 
         return SPMV_SUCCESS;
     hipLaunchKernelGGL((coo_staged_kernel<4, R, true, false>), dim3((unsigned)tiles), dim3(kBlock), 0,
                        (hipStream_t)d.stream, d.n_rows, d.nnz, row, col, val, x, y, carry_row, carry_val,
-                       (const int2 *)nullptr, 0);
+                       (const int2 *)nullptr, 0, XGlobal{x});
     SPMV_CHECK_LAUNCH("coo_staged_kernel (accumulate)");
     return SPMV_SUCCESS;
 }
@@ -619,11 +645,11 @@ int launch_coo_staged(const spmv_dims &d, const int32_t *row, const int32_t *col
         if (win)                                                                                         \
             hipLaunchKernelGGL((coo_staged_kernel<LL, R, false, true>), dim3((unsigned)tiles),            \
                                dim3(kBlock), lds, st, d.n_rows, d.nnz, row, col, val, x, y, carry_row,    \
-                               carry_val, win, xcap);                                                    \
+                               carry_val, win, xcap, XGlobal{x});                                        \
         else                                                                                             \
             hipLaunchKernelGGL((coo_staged_kernel<LL, R, false, false>), dim3((unsigned)tiles),           \
                                dim3(kBlock), 0, st, d.n_rows, d.nnz, row, col, val, x, y, carry_row,      \
-                               carry_val, (const int2 *)nullptr, 0);                                     \
+                               carry_val, (const int2 *)nullptr, 0, XGlobal{x});                         \
     } while (0)
     if (mean >= 48.0)
         SPMV_COO_STAGED(8);
@@ -633,6 +659,35 @@ int launch_coo_staged(const spmv_dims &d, const int32_t *row, const int32_t *col
         SPMV_COO_STAGED(2);
 #undef SPMV_COO_STAGED
     SPMV_CHECK_LAUNCH("coo_staged_kernel");
+    return SPMV_SUCCESS;
+}
+
+// COO over a hot-column table (power-law columns): non-temporal stream
+// loads, the H hottest x values gathered into xh first (as the tiled CSR).
+int launch_coo_staged_hot(const spmv_dims &d, const int32_t *row, const int32_t *col, const double *val,
+                          const double *x, double *y, int32_t *carry_row, double *carry_val, int64_t H,
+                          const int32_t *hot, double *xh)
+{
+    constexpr int R = 3;
+    const int64_t tiles = (d.nnz + coo_staged_tile() - 1) / coo_staged_tile();
+    if (tiles > INT32_MAX)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_coo_run_hot: grid too large");
+    const hipStream_t st = (hipStream_t)d.stream;
+    launch_hot_gather(H, hot, x, xh, st);
+    const XHot xs{x, xh, (int32_t)d.n_cols};
+    const double mean = d.n_rows > 0 ? (double)d.nnz / (double)d.n_rows : 0.0;
+#define SPMV_COO_HOT(LL)                                                                                 \
+    hipLaunchKernelGGL((coo_staged_kernel<LL, R, false, false, true, XHot>), dim3((unsigned)tiles),       \
+                       dim3(kBlock), 0, st, d.n_rows, d.nnz, row, col, val, x, y, carry_row, carry_val,    \
+                       (const int2 *)nullptr, 0, xs)
+    if (mean >= 48.0)
+        SPMV_COO_HOT(8);
+    else if (mean >= 12.0)
+        SPMV_COO_HOT(4);
+    else
+        SPMV_COO_HOT(2);
+#undef SPMV_COO_HOT
+    SPMV_CHECK_LAUNCH("coo_staged_kernel (hot columns)");
     return SPMV_SUCCESS;
 }
 
@@ -746,4 +801,28 @@ extern "C" int spmv_cmrs_xwin_build(spmv_dims d, int32_t h, int64_t n_strips, co
                        (int2 *)win);
     SPMV_CHECK_LAUNCH("cmrs_window_kernel");
     return windows_xcap((const int2 *)win, blocks, kStagedXwinCap, st, xcap, "spmv_cmrs_xwin_build: copy windows");
+}
+
+// The tile -> first owned row table of the entry-balanced CSR depends on
+// row_ptr only: built once here, the runs skip their pre-pass.
+extern "C" int64_t spmv_csr_tiled_plan_len(int64_t nnz)
+{
+    return nnz > 0 ? (nnz + csr_tiled_tile() - 1) / csr_tiled_tile() + 1 : 0;
+}
+
+extern "C" int spmv_csr_tiled_plan(spmv_dims d, const int64_t *row_ptr, int32_t *own_lo)
+{
+    if (d.n_rows < 0 || d.nnz < 0 || d.n_rows > INT32_MAX || (d.nnz > 0 && !own_lo))
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_tiled_plan: bad arguments");
+    if (d.nnz == 0 || d.n_rows == 0)
+        return SPMV_SUCCESS;
+    SPMV_GUARD(d);
+    const int64_t ch = csr_tiled_tile();
+    const int64_t tiles = (d.nnz + ch - 1) / ch;
+    if (tiles > INT32_MAX)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_tiled_plan: grid too large");
+    hipLaunchKernelGGL(csr_tile_rows_kernel, dim3((unsigned)((tiles + 1 + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       (hipStream_t)d.stream, d.n_rows, d.nnz, tiles, ch, row_ptr, own_lo);
+    SPMV_CHECK_LAUNCH("csr_tile_rows_kernel (plan)");
+    return SPMV_SUCCESS;
 }

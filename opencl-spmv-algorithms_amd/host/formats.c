@@ -639,6 +639,38 @@ int spmv_csr16_fill(int64_t nnz, const int32_t *col, int32_t *blk_base, uint16_t
 
 /* ------------------------------------------------------------ sharding */
 
+int spmv_partition_rows_weighted(int64_t n_rows, const int64_t *row_ptr, int parts, int64_t align,
+                                 double row_weight, int64_t *bounds)
+{
+    if (parts < 1 || n_rows < 0 || align < 1 || !(row_weight >= 0.0))
+        return SPMV_OTHER_ERROR;
+    const double total = (double)row_ptr[n_rows] + row_weight * (double)n_rows;
+    bounds[0] = 0;
+    for (int p = 1; p < parts; ++p) {
+        /* first row whose cost prefix (entries + row_weight per row)
+         * reaches p/parts of the total */
+        const double target = total * p / parts;
+        int64_t lo = 0, hi = n_rows;
+        while (lo < hi) {
+            int64_t mid = lo + (hi - lo) / 2;
+            if ((double)row_ptr[mid] + row_weight * (double)mid < target)
+                lo = mid + 1;
+            else
+                hi = mid;
+        }
+        int64_t b = (lo + align / 2) / align * align;
+        if (total == 0.0)
+            b = (n_rows * p / parts) / align * align;
+        if (b < bounds[p - 1])
+            b = bounds[p - 1];
+        if (b > n_rows)
+            b = n_rows;
+        bounds[p] = b;
+    }
+    bounds[parts] = n_rows;
+    return SPMV_SUCCESS;
+}
+
 int spmv_partition_rows(int64_t n_rows, const int64_t *row_ptr, int parts,
                         int64_t align, int64_t *bounds)
 {

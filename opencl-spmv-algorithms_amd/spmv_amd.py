@@ -84,7 +84,10 @@ HIP_SYMBOLS = {
     "spmv_csr_tiled_ws_bytes": (ctypes.c_size_t, [_c_i64, _c_i64]),
     "spmv_csr_run_tiled": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t]),
     "spmv_csr_hot_ws_bytes": (ctypes.c_size_t, [_c_i64, _c_i64, _c_i64]),
-    "spmv_csr_run_tiled_hot": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, _c_i64, _vp, _vp, ctypes.c_size_t]),
+    "spmv_csr_run_tiled_hot": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, _c_i64, _vp, _vp, _vp,
+                                              ctypes.c_size_t]),
+    "spmv_csr_tiled_plan_len": (_c_i64, [_c_i64]),
+    "spmv_csr_tiled_plan": (ctypes.c_int, [Dims, _vp, _vp]),
     "spmv_csr16_run": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_int]),
     "spmv_hyb_ws_bytes": (ctypes.c_size_t, [_c_i64]),
     "spmv_hyb_run": (ctypes.c_int, [Dims, _c_i32, _c_i64, _c_i32, _vp, _vp, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp,
@@ -112,6 +115,11 @@ HIP_SYMBOLS = {
     "spmv_cmrs_xwin_build": (ctypes.c_int, [Dims, _c_i32, _c_i64, _vp, _vp, _vp, ctypes.c_size_t,
                                             ctypes.POINTER(_c_i32)]),
     "spmv_cmrs_run_xwin": (ctypes.c_int, [Dims, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_i32]),
+    "spmv_coo_hot_ws_bytes": (ctypes.c_size_t, [_c_i64, _c_i64]),
+    "spmv_coo_run_hot": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, _c_i64, _vp, _vp, ctypes.c_size_t]),
+    "spmv_cmrs_hot_ws_bytes": (ctypes.c_size_t, [_c_i64, _c_i64, _c_i32, _c_i64]),
+    "spmv_cmrs_run_tiled_hot": (ctypes.c_int, [Dims, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _c_i64, _vp, _vp,
+                                               ctypes.c_size_t]),
     "spmv_cmrs_tiled_ws_bytes": (ctypes.c_size_t, [_c_i64, _c_i64, _c_i32]),
     "spmv_cmrs_run_tiled": (ctypes.c_int, [Dims, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t]),
     "spmv_sell_split_ws_bytes": (ctypes.c_size_t, [_c_i64, _c_i32]),
@@ -171,6 +179,7 @@ HOST_SYMBOLS = {
     "spmv_sell_split_auto": (_c_i32, [_c_i64, _vp, _c_i32, _c_i32]),
     "spmv_sell_split_plan": (_c_i64, [_c_i64, _vp, _c_i32, _c_i32, _vp, _vp]),
     "spmv_partition_rows": (ctypes.c_int, [_c_i64, _vp, ctypes.c_int, _c_i64, _vp]),
+    "spmv_partition_rows_weighted": (ctypes.c_int, [_c_i64, _vp, ctypes.c_int, _c_i64, ctypes.c_double, _vp]),
     "spmv_csr16_plan": (ctypes.c_int, [_c_i64, _vp, ctypes.POINTER(_c_i64), ctypes.POINTER(_c_i64)]),
     "spmv_hyb_plan": (ctypes.c_int, [_c_i64, _vp, _c_i32, _c_i32, ctypes.POINTER(_c_i32), ctypes.POINTER(_c_i64),
                                      ctypes.POINTER(_c_i64)]),
@@ -454,10 +463,17 @@ def csr16_build(col: np.ndarray):
     return dict(n_blocks=nb.value, n_esc=ne.value, blk_base=base, col_off=off, col_esc=esc)
 
 
-def partition_rows(n_rows: int, ptr: np.ndarray, parts: int, align: int = 1024) -> np.ndarray:
-    """Contiguous row ranges with ~nnz/parts entries each."""
+def partition_rows(n_rows: int, ptr: np.ndarray, parts: int, align: int = 1024,
+                   row_weight: float = 0.0) -> np.ndarray:
+    """Contiguous row ranges with ~nnz/parts entries each (SURVEY.md §8e);
+    row_weight > 0 balances entries + row_weight per row instead."""
     bounds = np.empty(parts + 1, np.int64)
-    _check_host(host_lib().spmv_partition_rows(n_rows, _ptr(ptr), parts, align, _ptr(bounds)), "partition_rows")
+    ptr = np.ascontiguousarray(ptr, dtype=np.int64)
+    if row_weight:
+        rc = host_lib().spmv_partition_rows_weighted(n_rows, _ptr(ptr), parts, align, float(row_weight), _ptr(bounds))
+    else:
+        rc = host_lib().spmv_partition_rows(n_rows, _ptr(ptr), parts, align, _ptr(bounds))
+    _check_host(rc, "partition_rows")
     return bounds
 
 
@@ -531,7 +547,10 @@ class DeviceMatrix:
             raise SpmvError(OTHER_ERROR, "run", "x and y must be float64")
         if x.numel() < self.n_cols or y.numel() < self.n_rows:
             raise SpmvError(OTHER_ERROR, "run", "x or y too short")
-        if self.fmt == "coo" and "win" in a:
+        if self.fmt == "coo" and p.get("H", 0) > 0:
+            rc = lib.spmv_coo_run_hot(d, _ptr(a["row"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y), p["H"],
+                                      _ptr(a["hot"]), _ptr(a["ws"]), a["ws"].numel())
+        elif self.fmt == "coo" and "win" in a:
             rc = lib.spmv_coo_run_xwin(d, _ptr(a["row"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
                                        _ptr(a["ws"]), a["ws"].numel(), _ptr(a["win"]), p["xcap"])
         elif self.fmt == "coo":
@@ -541,9 +560,10 @@ class DeviceMatrix:
             rc = lib.spmv_csr_run_xwin(d, _ptr(a["row_ptr"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
                                        p["lanes"], p.get("xwin_rows", 0), _ptr(a["win"]), p["xcap"])
         elif self.fmt == "csr":
-            if p.get("variant", 0) == 4 and p.get("H", 0) > 0:
+            if p.get("variant", 0) == 4 and "own_lo" in a:
                 rc = lib.spmv_csr_run_tiled_hot(d, _ptr(a["row_ptr"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x),
-                                                _ptr(y), p["H"], _ptr(a["hot"]), _ptr(a["ws"]), a["ws"].numel())
+                                                _ptr(y), p["H"], _ptr(a.get("hot")), _ptr(a["own_lo"]), _ptr(a["ws"]),
+                                                a["ws"].numel())
             elif p.get("variant", 0) == 4:
                 rc = lib.spmv_csr_run_tiled(d, _ptr(a["row_ptr"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x),
                                             _ptr(y), _ptr(a["ws"]), a["ws"].numel())
@@ -575,6 +595,10 @@ class DeviceMatrix:
         elif self.fmt == "sell":
             rc = lib.spmv_sell_run(d, p["C"], p["sigma"], p["ki"], p["n_slices"], _ptr(a["slice_ptr"]), _ptr(a["perm"]),
                                    _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y))
+        elif self.fmt == "cmrs" and p.get("variant", 0) == 1 and p.get("H", 0) > 0:
+            rc = lib.spmv_cmrs_run_tiled_hot(d, p["h"], p["n_strips"], _ptr(a["strip_ptr"]), _ptr(a["row_in_strip"]),
+                                             _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y), p["H"], _ptr(a["hot"]),
+                                             _ptr(a["ws"]), a["ws"].numel())
         elif self.fmt == "cmrs" and p.get("variant", 0) == 1:
             rc = lib.spmv_cmrs_run_tiled(d, p["h"], p["n_strips"], _ptr(a["strip_ptr"]), _ptr(a["row_in_strip"]),
                                          _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y), _ptr(a["ws"]),
@@ -626,16 +650,25 @@ def _sell_split(dm: DeviceMatrix, slice_ptr: np.ndarray, split: int | None) -> N
                                 device=dm.device)
 
 
-def _cmrs_variant(dm: DeviceMatrix, strip_ptr: np.ndarray, variant: int | None) -> None:
+def _cmrs_variant(dm: DeviceMatrix, strip_ptr: np.ndarray, variant: int | None, col=None,
+                  hot: int | None = None) -> None:
     """variant None = library rule (spmv_cmrs_pick_variant), 0 = strip-run
-    kernel, 1 = entry-balanced tiles (+ workspace)."""
+    kernel, 1 = entry-balanced tiles (+ workspace, and the hot-column table
+    of `col` unless hot == 0)."""
     torch = _torch()
     p = dm.params
     sp = np.ascontiguousarray(strip_ptr, dtype=np.int64)
     v = host_lib().spmv_cmrs_pick_variant(p["n_strips"], _ptr(sp)) if variant is None else int(variant)
     p["variant"] = v
+    p["H"] = 0
     if v == 1:
-        ws = hip_lib().spmv_cmrs_tiled_ws_bytes(p["n_strips"], dm.nnz, p["h"])
+        if col is not None and hot != 0:
+            H, hot_cols, col_hot = hot_columns(dm.n_cols, col, hot or 0)
+            if H > 0:
+                p["H"] = H
+                dm.arrays["col"] = _dev_tensor(col_hot, dm.device)
+                dm.arrays["hot"] = _dev_tensor(hot_cols, dm.device)
+        ws = hip_lib().spmv_cmrs_hot_ws_bytes(p["n_strips"], dm.nnz, p["h"], p["H"])
         dm.arrays["ws"] = torch.empty(max(ws, 16), dtype=torch.uint8, device=dm.device)
 
 
@@ -708,12 +741,17 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
     dm = DeviceMatrix(fmt, m.n_rows, m.n_cols, m.nnz, device)
     if fmt == "coo":
         row, col, val = coo_sort_by_row(m)
-        ws_bytes = hip_lib().spmv_coo_ws_bytes(m.nnz)
-        dm.arrays = dict(row=_dev_tensor(row, device), col=_dev_tensor(col, device),
+        # hot-column table for power-law columns (None: library rule)
+        H, hot_cols, col_hot = hot_columns(m.n_cols, col, hot or 0) if hot != 0 else (0, None, col)
+        ws_bytes = hip_lib().spmv_coo_hot_ws_bytes(m.nnz, H)
+        dm.params["H"] = H
+        dm.arrays = dict(row=_dev_tensor(row, device), col=_dev_tensor(col_hot, device),
                          val=_dev_tensor(val, device),
                          ws=torch.empty(ws_bytes, dtype=torch.uint8, device=device))
+        if H > 0:
+            dm.arrays["hot"] = _dev_tensor(hot_cols, device)
         dm.stored_bytes = 16 * m.nnz
-        if xwin:
+        if xwin and H == 0:
             _coo_xwin(dm)
         return dm
     ptr, col, val = csr_from_coo(m)
@@ -732,6 +770,11 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
                 dm.arrays["hot"] = _dev_tensor(hot_cols, device)
             ws = hip_lib().spmv_csr_hot_ws_bytes(m.n_rows, m.nnz, H)
             dm.arrays["ws"] = torch.empty(ws, dtype=torch.uint8, device=device)
+            n_plan = hip_lib().spmv_csr_tiled_plan_len(m.nnz)
+            if n_plan > 0:  # tile -> first row table, built once (row_ptr only)
+                dm.arrays["own_lo"] = torch.empty(n_plan, dtype=torch.int32, device=device)
+                _check(hip_lib().spmv_csr_tiled_plan(dm.dims(), _ptr(dm.arrays["row_ptr"]), _ptr(dm.arrays["own_lo"])),
+                       "spmv_csr_tiled_plan")
         elif xwin and variant in (0, 3):
             _csr_xwin(dm)
         dm.stored_bytes = 12 * m.nnz + 8 * (m.n_rows + 1)
@@ -779,7 +822,7 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
                          row_in_strip=_dev_tensor(c["row_in_strip"], device),
                          col=_dev_tensor(col, device), val=_dev_tensor(val, device))
         dm.stored_bytes = 13 * m.nnz + 8 * (c["n_strips"] + 1)
-        _cmrs_variant(dm, c["strip_ptr"], cmrs_variant)
+        _cmrs_variant(dm, c["strip_ptr"], cmrs_variant, col, hot)
         if xwin and dm.params["variant"] == 0:
             _cmrs_xwin(dm)
     else:

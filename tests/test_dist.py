@@ -104,3 +104,22 @@ def test_partition_balances_entries():
         assert nnz.max() <= 1.1 * m.nnz / parts + 1024 * 200
     b = sa.partition_rows(10, np.zeros(11, np.int64), 4, align=1)
     assert b.tolist() == [0, 2, 5, 7, 10]
+
+
+@pytest.mark.parametrize("w", [0.0, 0.5, 2.0, 8.0])
+def test_weighted_partition_balances_cost(w):
+    """spmv_partition_rows_weighted: contiguous aligned ranges whose
+    entries + w * rows are balanced (w = 0 is the plain nnz partition)."""
+    m = sa.gen_rmat(200_000, 2_000_000, scale=18, seed=3)
+    ptr, _, _ = sa.csr_from_coo(m)
+    parts = 8
+    b = sa.partition_rows(m.n_rows, ptr, parts, align=64, row_weight=w)
+    assert b[0] == 0 and b[-1] == m.n_rows and np.all(np.diff(b) >= 0)
+    assert np.all(b[1:-1] % 64 == 0)
+    if w == 0.0:
+        assert np.array_equal(b, sa.partition_rows(m.n_rows, ptr, parts, align=64))
+    cost = ptr[b[1:]] - ptr[b[:-1]] + w * np.diff(b)
+    total = ptr[-1] + w * m.n_rows
+    # every cut is within one aligned block (+ its longest row) of its target
+    slack = 64 * (w + 1) + np.diff(ptr).max()
+    assert np.all(np.abs(cost - total / parts) <= 2 * slack)

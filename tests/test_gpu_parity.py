@@ -512,6 +512,33 @@ def test_csr_hot_bit_identical(torch_dev, H):
     x = torch.from_numpy(np.random.default_rng(6).uniform(-1, 1, m.n_cols)).to(dev)
     ya = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
     yb = torch.full_like(ya, float("nan"))
+    yc = torch.full_like(ya, float("nan"))
+    a.run(x, ya)
+    b.run(x, yb)
+    # and without the build-once tile plan (the per-run pre-pass)
+    bb = b.arrays
+    rc = sa.hip_lib().spmv_csr_run_tiled(b.dims(), sa._ptr(bb["row_ptr"]), sa._ptr(bb["col"]), sa._ptr(bb["val"]),
+                                         sa._ptr(x), sa._ptr(yc), sa._ptr(bb["ws"]), bb["ws"].numel())
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert torch.equal(ya.view(torch.int64), yb.view(torch.int64))
+    assert torch.equal(yc.view(torch.int64), yb.view(torch.int64))
+    assert_parity(m, ya.cpu().numpy(), x.cpu().numpy())
+
+
+@pytest.mark.parametrize("fmt,kw", [("coo", {}), ("cmrs", {"cmrs_variant": 1}), ("cmrs", {"cmrs_variant": 1, "h": 32})])
+@pytest.mark.parametrize("H", [1, 4096])
+def test_coo_cmrs_hot_bit_identical(torch_dev, fmt, kw, H):
+    """COO / tiled CMRS over the hot-column table: the same products in the
+    same order as over the original columns."""
+    torch, dev = torch_dev
+    m = sa.gen_rmat(1_000_000, 10_000_000, scale=20, seed=1)
+    a = sa.to_device(m, fmt, dev, hot=H, **kw)
+    b = sa.to_device(m, fmt, dev, hot=0, **kw)
+    assert a.params["H"] == H and b.params["H"] == 0
+    x = torch.from_numpy(np.random.default_rng(7).uniform(-1, 1, m.n_cols)).to(dev)
+    ya = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
+    yb = torch.full_like(ya, float("nan"))
     a.run(x, ya)
     b.run(x, yb)
     torch.cuda.synchronize()

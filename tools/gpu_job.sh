@@ -42,6 +42,10 @@ for s in "${steps[@]}"; do
     benchbanded) run bench_banded_sell 600 python bench.py --workload banded --format sell --steps 20 && run bench_banded_csr 600 python bench.py --workload banded --format csr --steps 20;;
     rehearse8) run shard_rehearse 900 python tools/shard_rehearse.py --gpus 1,2,4,8 &&
                run shard_rehearse_sell 900 python tools/shard_rehearse.py --gpus 1,8 --format sell;;
+    rehearsew) run shard_rehearse_w 900 python tools/shard_rehearse.py --gpus 1,8 --row-weights 0,2,4 &&
+               run shard_rehearse_nohot 600 python tools/shard_rehearse.py --gpus 8 --row-weights 2 --hot 0 &&
+               run prof_rehearse 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_rehearse -o run -- python3 tools/shard_rehearse.py --gpus 8 --row-weights 2;;
+    rehearsew2) run shard_rehearse_w2 900 python tools/shard_rehearse.py --gpus 8 --row-weights 4,6,8;;
     rehearse2) run rehearse2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --backend gloo --share-gpu --steps 20;;
     drivers) run drivers 600 python -m pytest tests/test_drivers_gpu.py -q;;
     sweepremap) SPMV_XCD_REMAP=1 run sweep_remap 600 python tools/sweep.py --rounds 2 --only csr,sell,ell;;
@@ -61,6 +65,7 @@ for s in "${steps[@]}"; do
     pmcvar) run pmc_var 1100 python tools/pmc_traffic.py --out traffic_variants.json --formats "csr,csr@SPMV_XCD_REMAP=1,csr:lanes=16,sell:sigma=256,sell,ell@SPMV_XCD_REMAP=1";;
     sweepnt) run sweep_nt 600 python tools/sweep.py --env-only --rounds 3;;
     pmcnt) run pmc_nt 1100 python tools/pmc_traffic.py --out traffic_nt.json --formats "csr@SPMV_STREAM_NT=1,sell@SPMV_STREAM_NT=1,ell@SPMV_STREAM_NT=1,coo,cmrs";;
+    ldsconf) run pmc_lds 600 python tools/pmc_stalls.py --formats csr,sell,cmrs --passes ta,sq,lds --out pmc_lds.json;;
     stalls) run pmc_stalls 1150 python tools/pmc_stalls.py --formats csr,sell;;
     iterbench) run iter_power 300 python tools/iterate_bench.py --what power --matrix cantlike --iters 200 &&
                run iter_power_graph 300 python tools/iterate_bench.py --what power --matrix cantlike --iters 200 --graph &&

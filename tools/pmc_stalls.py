@@ -31,6 +31,7 @@ PASSES = {
     "tcc": ["TCC_EA0_RDREQ_DRAM_sum", "TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum", "TCC_TAG_STALL_sum", "TCC_BUSY_avr"],
     "lat": ["TCP_TCC_READ_REQ_LATENCY_sum", "TA_FLAT_READ_WAVEFRONTS_sum", "TA_TOTAL_WAVEFRONTS_sum",
             "SQ_WAVES"],
+    "lds": ["SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE", "SQ_WAIT_INST_LDS", "SQ_ACTIVE_INST_LDS"],
 }
 
 
@@ -38,7 +39,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--formats", default="csr,sell,ell")
     ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--passes", default="", help="comma list of pass names (default all)")
+    ap.add_argument("--out", default="pmc_stalls.json")
     a = ap.parse_args()
+    passes = {k: v for k, v in PASSES.items() if not a.passes or k in a.passes.split(",")}
     probe = REPO / "tools" / "bw_probe"
     jobs = [("probe_tile_nt", [str(probe), str(2 << 30), "3"], "tile_read_kernel<true, 8>")]
     for spec in a.formats.split(","):
@@ -50,7 +54,7 @@ def main():
     out = {}
     for name, cmd, kern in jobs:
         counters = {}
-        for tag, cs in PASSES.items():
+        for tag, cs in passes.items():
             tagdir = f"stall_{name}_{tag}".replace(":", "_").replace("=", "").replace("@", "_")
             f = run_pass(tagdir, cs, cmd, timeout=150)
             if f:
@@ -65,7 +69,7 @@ def main():
         out[name] = {"kernel": kern, "counters": {k: round(v, 1) for k, v in counters.items()},
                      "per_gui_active": frac}
         print(json.dumps({name: out[name]}), flush=True)
-    (REPO / "gpurun_out" / "pmc_stalls.json").write_text(json.dumps(out, indent=1) + "\n")
+    (REPO / "gpurun_out" / a.out).write_text(json.dumps(out, indent=1) + "\n")
 
 
 if __name__ == "__main__":

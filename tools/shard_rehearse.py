@@ -51,6 +51,8 @@ def main():
     ap.add_argument("--gpus", default="1,2,4,8")
     ap.add_argument("--format", default="csr")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--row-weights", default="2", help="spmv_partition_rows_weighted weights to try")
+    ap.add_argument("--hot", type=int, default=-1, help="CSR hot-column table: -1 library rule, 0 off, H")
     a = ap.parse_args()
     import torch
 
@@ -63,15 +65,16 @@ def main():
     x = torch.from_numpy(xh).to(dev)
     b_total = sa.bytes_alg(n, n, z)
     base = None
-    for G in [int(g) for g in a.gpus.split(",")]:
-        bounds = sa.partition_rows(n, ptr, G, align=1024)
+    kw = {"hot": None if a.hot < 0 else a.hot} if a.format == "csr" else {}
+    for G, w in [(int(g), float(w)) for w in a.row_weights.split(",") for g in a.gpus.split(",")]:
+        bounds = sa.partition_rows(n, ptr, G, align=1024, row_weight=w)
         times, nnzs, params = [], [], None
         for r in range(G):
             lo, hi = int(bounds[r]), int(bounds[r + 1])
             lptr = ptr[lo:hi + 1] - ptr[lo]
             loc = sa.Coo(hi - lo, n, np.repeat(np.arange(hi - lo, dtype=np.int32), np.diff(lptr)),
                          col[ptr[lo]:ptr[hi]], val[ptr[lo]:ptr[hi]])
-            dm = sa.to_device(loc, a.format, dev)
+            dm = sa.to_device(loc, a.format, dev, **kw)
             params = params or {k: v for k, v in dm.params.items() if isinstance(v, (int, float, str))}
             y = torch.empty(max(loc.n_rows, 1), dtype=torch.float64, device=dev)
             times.append(time_shard(torch, dm, x, y, a.reps))
@@ -85,7 +88,7 @@ def main():
         agg = b_total / (tmax * 1e-3) * 1e-9
         base = base or agg
         print(json.dumps({"workload": "rmat 1e7/1e8", "format": a.format, "params_shard0": params, "gpus": G,
-                          "shard_nnz": nnzs, "shard_ms": [round(t, 4) for t in times], "max_ms": round(tmax, 4),
+                          "row_weight": w, "shard_rows": np.diff(bounds).tolist(), "shard_nnz": nnzs, "shard_ms": [round(t, 4) for t in times], "max_ms": round(tmax, 4),
                           "aggregate_GBs_warm": round(agg, 1), "speedup_vs_first": round(agg / base, 2)}),
               flush=True)
 

@@ -51,9 +51,10 @@ KERNEL_NAMES = {  # dominant kernel per format (as rocprofv3 names it)
     "coo": "coo_tile_kernel",
     "cmrs": "cmrs_kernel",
 }
-# R-MAT shards: a row costs the tiled kernel about as much as this many
-# entries (tools/shard_rehearse.py); shards balance entries + weight * rows
-RMAT_ROW_WEIGHT = 2.0
+# R-MAT shards balance entries + RMAT_ROW_WEIGHT * rows: at 8 shards the
+# slowest one took 0.2134 / 0.2023 / 0.1715 / 0.1767 / 0.1950 ms with
+# weights 0 / 2 / 4 / 6 / 8 (tools/shard_rehearse.py, one MI355X)
+RMAT_ROW_WEIGHT = 4.0
 CSR_DEFAULT_VARIANT = 3  # must match csr_default_variant() in csrc/csr.hip
 
 

@@ -140,6 +140,8 @@ __global__ __launch_bounds__(kBlock) void cmrs_staged_kernel(
 }
 
 // ------------------------------------------------------------------- COO
+constexpr int kCooRowCap = 1024;
+
 // A workgroup owns one tile of CH consecutive row-sorted entries and
 // writes y for rows (row[t0-1], row[t1-1]] (rows without entries get 0;
 // the last tile also covers the trailing rows).  A first row that began
@@ -160,6 +162,7 @@ __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
     __shared__ double2 s_prod[kBlock * R];
     __shared__ int2 s_row2[kBlock * R];
     __shared__ int32_t s_prev;
+    __shared__ int32_t s_start[kCooRowCap + 1];  // owned rows' first entries
     const int32_t *s_row = reinterpret_cast<const int32_t *>(s_row2);
     const double *prod = reinterpret_cast<const double *>(s_prod);
 
@@ -195,12 +198,33 @@ __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
     const int32_t first = s_row[0], last = s_row[n - 1];
     const bool first_continues = prev == first;
     const int g = threadIdx.x / L, lane = threadIdx.x % L;
+    // Row starts from the key changes (one pass over the staged keys, every
+    // row of (prev, last] written by exactly one thread) instead of two
+    // binary searches per row; a tile spanning more than kCooRowCap rows
+    // (long runs of empty rows) keeps the searches.
+    const int64_t r_lo = (int64_t)prev + 1;
+    const int64_t span = (int64_t)last - r_lo + 1;  // rows (prev, last]
+    bool heads = false;  // uniform per workgroup
+    if constexpr (!ACC) {
+        heads = span >= 0 && span <= kCooRowCap;
+        if (heads) {
+            for (int j = threadIdx.x; j < n; j += kBlock) {
+                const int32_t k = s_row[j];
+                const int32_t kp = j > 0 ? s_row[j - 1] : prev;
+                for (int32_t r = kp + 1; r <= k; ++r)
+                    s_start[r - r_lo] = j;
+            }
+            if (threadIdx.x == 0)
+                s_start[span] = n;
+            __syncthreads();
+        }
+    }
 
     // carry: the first row's entries when it began in an earlier tile
     if (g == 0) {
         double c = 0.0;
         if (first_continues) {
-            const int b = lower_bound_lds(s_row, 0, n, first + 1);
+            const int b = heads ? s_start[0] : lower_bound_lds(s_row, 0, n, first + 1);
             for (int j = lane; j < b; j += L)
                 c += prod[j];
         }
@@ -230,13 +254,18 @@ __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
     }
     // owned rows: (prev, last], plus the trailing empty rows in the last
     // tile; a continued first row equals prev, so it is excluded here
-    const int64_t r_lo = (int64_t)prev + 1;
     const int64_t r_hi = t1 == nnz ? n_rows - 1 : (int64_t)last;
     for (int64_t r = r_lo + g; r <= r_hi; r += GROUPS) {
         double s = 0.0;
         if (r <= last) {
-            const int a = lower_bound_lds(s_row, 0, n, (int)r);
-            const int b = lower_bound_lds(s_row, a, n, (int)r + 1);
+            int a, b;
+            if (heads) {
+                a = s_start[r - r_lo];
+                b = s_start[r - r_lo + 1];
+            } else {
+                a = lower_bound_lds(s_row, 0, n, (int)r);
+                b = lower_bound_lds(s_row, a, n, (int)r + 1);
+            }
             for (int j = a + lane; j < b; j += L)
                 s += prod[j];
         }

@@ -33,14 +33,26 @@ sys.path[:0] = [str(REPO / "opencl-spmv-algorithms_amd"), str(REPO)]
 import spmv_amd as sa  # noqa: E402
 
 
-def time_shard(torch, dm, x, y, reps):
+def time_shard(torch, dm, x, y, reps, graph=False):
+    """Mean ms per SpMV over back-to-back launches; graph=True captures one
+    SpMV (its 3-4 kernels) into a HIP graph and replays it."""
     s = torch.cuda.current_stream()
     for _ in range(3):
         dm.run(x, y, s)
+    step = lambda: dm.run(x, y, s)  # noqa: E731
+    if graph:
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            dm.run(x, y)
+        torch.cuda.synchronize()
+        step = g.replay
+        for _ in range(3):
+            step()
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
     ev[0].record(s)
     for k in range(reps):
-        dm.run(x, y, s)
+        step()
         ev[k + 1].record(s)
     torch.cuda.synchronize()
     return float(np.mean([ev[k].elapsed_time(ev[k + 1]) for k in range(reps)]))
@@ -53,6 +65,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--row-weights", default="2", help="spmv_partition_rows_weighted weights to try")
     ap.add_argument("--hot", type=int, default=-1, help="CSR hot-column table: -1 library rule, 0 off, H")
+    ap.add_argument("--graph", action="store_true", help="replay each SpMV as a captured HIP graph")
     a = ap.parse_args()
     import torch
 
@@ -77,7 +90,7 @@ def main():
             dm = sa.to_device(loc, a.format, dev, **kw)
             params = params or {k: v for k, v in dm.params.items() if isinstance(v, (int, float, str))}
             y = torch.empty(max(loc.n_rows, 1), dtype=torch.float64, device=dev)
-            times.append(time_shard(torch, dm, x, y, a.reps))
+            times.append(time_shard(torch, dm, x, y, a.reps, a.graph))
             nnzs.append(loc.nnz)
             bad, first = sa.check(loc, xh, y[:loc.n_rows].cpu().numpy())
             if bad:
@@ -88,7 +101,7 @@ def main():
         agg = b_total / (tmax * 1e-3) * 1e-9
         base = base or agg
         print(json.dumps({"workload": "rmat 1e7/1e8", "format": a.format, "params_shard0": params, "gpus": G,
-                          "row_weight": w, "shard_rows": np.diff(bounds).tolist(), "shard_nnz": nnzs, "shard_ms": [round(t, 4) for t in times], "max_ms": round(tmax, 4),
+                          "row_weight": w, "graph": a.graph, "shard_rows": np.diff(bounds).tolist(), "shard_nnz": nnzs, "shard_ms": [round(t, 4) for t in times], "max_ms": round(tmax, 4),
                           "aggregate_GBs_warm": round(agg, 1), "speedup_vs_first": round(agg / base, 2)}),
               flush=True)
 

@@ -166,18 +166,20 @@ def cold_single(torch, dm, x, y, reps=30):
 def traffic_for(fmt, workload_bytes, kernel=None):
     """HBM bytes per launch from the committed PMC passes, if they were
     measured on this workload and this kernel."""
-    f = REPO / "profiles" / "traffic.json"
-    if not f.exists():
-        return None
-    try:
-        t = json.loads(f.read_text()).get(fmt)
-    except (ValueError, AttributeError):
-        return None
-    if not t or int(t.get("bytes_alg", -1)) != int(workload_bytes):
-        return None
-    if kernel is not None and t.get("kernel") != kernel:
-        return None
-    return t.get("hbm_bytes_per_launch")
+    for name in ("traffic.json", "traffic_rmat.json"):
+        f = REPO / "profiles" / name
+        if not f.exists():
+            continue
+        try:
+            t = json.loads(f.read_text()).get(fmt)
+        except (ValueError, AttributeError):
+            continue
+        if not t or int(t.get("bytes_alg", -1)) != int(workload_bytes):
+            continue
+        if kernel is not None and t.get("kernel") != kernel:
+            continue
+        return t.get("hbm_bytes_per_launch")
+    return None
 
 
 def build_workload(args, torch, dev, rank, world):

@@ -200,6 +200,17 @@ int spmv_sell_run_split(spmv_dims d, int32_t C, int32_t sigma, int32_t ki, int64
                         const double *val, const double *x, double *y, const void *win,
                         int32_t xcap, int32_t T, int64_t n_chunks, const int32_t *chunk_slice,
                         const int32_t *chunk_k0, void *ws, size_t ws_bytes);
+/* SELL over a hot-column table (col_hot / hot from spmv_hot_columns on the
+ * stored SELL columns), global x gathers, with the split plan of
+ * spmv_sell_run_split (T = INT32_MAX and n_chunks = 0: no split).  `ws`
+ * holds spmv_sell_hot_ws_bytes(n_chunks, C, H) bytes; bit-identical to
+ * spmv_sell_run_split on the original columns.                          */
+size_t spmv_sell_hot_ws_bytes(int64_t n_chunks, int32_t C, int64_t H);
+int spmv_sell_run_hot(spmv_dims d, int32_t C, int32_t sigma, int32_t ki, int64_t n_slices,
+                      const int64_t *slice_ptr, const int32_t *perm, const int32_t *col_hot,
+                      const double *val, const double *x, double *y, int32_t T, int64_t n_chunks,
+                      const int32_t *chunk_slice, const int32_t *chunk_k0, int64_t H,
+                      const int32_t *hot, void *ws, size_t ws_bytes);
 size_t spmv_sell_xwin_bytes(int64_t n_slices, int32_t C, int32_t sigma);
 int spmv_sell_xwin_build(spmv_dims d, int32_t C, int32_t sigma, int64_t n_slices,
                          const int64_t *slice_ptr, const int32_t *col, void *win,

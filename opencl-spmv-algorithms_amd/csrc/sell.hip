@@ -94,11 +94,11 @@ __device__ __forceinline__ double slot_dot(const double *__restrict__ vp,
 // 1024-row window was written from four XCDs and each partially written
 // line left the chip up to four times (WRITE_SIZE 2.9x the y bytes,
 // profiles/traffic.json), which cost ~10 % of the kernel.
-template <int KI, bool NT, int U>
+template <int KI, bool NT, int U, typename XS = XGlobal>
 __global__ __launch_bounds__(1024) void sell_kernel(
     int32_t C, int64_t n_slices, const int64_t *__restrict__ slice_ptr,
     const int32_t *__restrict__ perm, const int32_t *__restrict__ col,
-    const double *__restrict__ val, const double *__restrict__ x,
+    const double *__restrict__ val, const XS xs,
     double *__restrict__ y, int remap, int64_t wcap)
 {
     const int64_t slot = xcd_block(remap) * (int64_t)blockDim.x + threadIdx.x;
@@ -110,7 +110,7 @@ __global__ __launch_bounds__(1024) void sell_kernel(
     int64_t w = (slice_ptr[s + 1] - base) / C;
     w = w < wcap ? w : wcap;  // split plan: the rest of a wide slice is sell_split_kernel's
     const int64_t off = base + r * KI;
-    const double sum = slot_dot<KI, NT, U>(val + off, col + off, w, (int64_t)C * KI, XGlobal{x});
+    const double sum = slot_dot<KI, NT, U>(val + off, col + off, w, (int64_t)C * KI, xs);
     const int32_t row = perm[slot];
     if (row >= 0)
         y[row] = sum;
@@ -287,11 +287,11 @@ __global__ __launch_bounds__(1024) void sell_xwin_kernel(
 // slice's chunks in chunk order to y[perm] (deterministic, no atomics).
 // An R-MAT hub slice (~1.4e5 slot columns) otherwise keeps one wave busy
 // for the whole kernel.
-template <int KI, bool NT, int U>
+template <int KI, bool NT, int U, typename XS = XGlobal>
 __global__ __launch_bounds__(kBlock) void sell_split_kernel(
     int32_t C, int64_t n_chunks, int32_t T, const int64_t *__restrict__ slice_ptr,
     const int32_t *__restrict__ chunk_slice, const int32_t *__restrict__ chunk_k0,
-    const int32_t *__restrict__ col, const double *__restrict__ val, const double *__restrict__ x,
+    const int32_t *__restrict__ col, const double *__restrict__ val, const XS xs,
     double *__restrict__ part)
 {
     const int64_t gid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -305,7 +305,7 @@ __global__ __launch_bounds__(kBlock) void sell_split_kernel(
     const int64_t w = (slice_ptr[s + 1] - base) / C;
     const int64_t n = w - k0 < T ? w - k0 : T;
     const int64_t off = base + k0 * C + r * KI;
-    part[gid] = slot_dot<KI, NT, U>(val + off, col + off, n, (int64_t)C * KI, XGlobal{x});
+    part[gid] = slot_dot<KI, NT, U>(val + off, col + off, n, (int64_t)C * KI, xs);
 }
 
 __global__ __launch_bounds__(kBlock) void sell_split_fix_kernel(int32_t C, int64_t n_chunks,
@@ -328,6 +328,15 @@ __global__ __launch_bounds__(kBlock) void sell_split_fix_kernel(int32_t C, int64
     const int32_t row = perm[(int64_t)s * C + r];
     if (row >= 0)
         y[row] += acc;
+}
+
+__global__ __launch_bounds__(kBlock) void sell_hot_gather_kernel(int64_t H, const int32_t *__restrict__ hot,
+                                                                 const double *__restrict__ x,
+                                                                 double *__restrict__ xh)
+{
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < H)
+        xh[i] = x[hot[i]];
 }
 
 constexpr int32_t kXwinCapWide = 8192;   // 64 KiB of LDS per 1024-slot workgroup (2 per CU)
@@ -359,7 +368,7 @@ extern "C" int spmv_sell_run(spmv_dims d, int32_t C, int32_t sigma, int32_t ki,
                         : (nt ? (u8 ? sell_kernel<1, true, 8> : sell_kernel<1, true, 4>)
                               : (u8 ? sell_kernel<1, false, 8> : sell_kernel<1, false, 4>));
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(bt), 0, (hipStream_t)d.stream, C,
-                       n_slices, slice_ptr, perm, col, val, x, y, remap, (int64_t)INT64_MAX);
+                       n_slices, slice_ptr, perm, col, val, XGlobal{x}, y, remap, (int64_t)INT64_MAX);
     SPMV_CHECK_LAUNCH("sell_kernel");
     return SPMV_SUCCESS;
 }
@@ -614,8 +623,8 @@ extern "C" int spmv_sell_run_split(spmv_dims d, int32_t C, int32_t sigma, int32_
     } else {
         auto kern = ki == 2 ? (nt ? sell_kernel<2, true, 4> : sell_kernel<2, false, 4>)
                             : (nt ? sell_kernel<1, true, 4> : sell_kernel<1, false, 4>);
-        hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(bt), 0, st, C, n_slices, slice_ptr, perm, col, val, x,
-                           y, 0, (int64_t)T);
+        hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(bt), 0, st, C, n_slices, slice_ptr, perm, col, val,
+                           XGlobal{x}, y, 0, (int64_t)T);
     }
     SPMV_CHECK_LAUNCH("sell kernel (split main)");
     if (n_chunks == 0)
@@ -624,8 +633,66 @@ extern "C" int spmv_sell_run_split(spmv_dims d, int32_t C, int32_t sigma, int32_
     auto sk = ki == 2 ? (nt ? sell_split_kernel<2, true, 4> : sell_split_kernel<2, false, 4>)
                       : (nt ? sell_split_kernel<1, true, 4> : sell_split_kernel<1, false, 4>);
     hipLaunchKernelGGL(sk, dim3((unsigned)cblocks), dim3(kBlock), 0, st, C, n_chunks, T, slice_ptr, chunk_slice,
-                       chunk_k0, col, val, x, part);
+                       chunk_k0, col, val, XGlobal{x}, part);
     SPMV_CHECK_LAUNCH("sell_split_kernel");
+    hipLaunchKernelGGL(sell_split_fix_kernel, dim3((unsigned)cblocks), dim3(kBlock), 0, st, C, n_chunks,
+                       chunk_slice, perm, part, y);
+    SPMV_CHECK_LAUNCH("sell_split_fix_kernel");
+    return SPMV_SUCCESS;
+}
+
+extern "C" size_t spmv_sell_hot_ws_bytes(int64_t n_chunks, int32_t C, int64_t H)
+{
+    return (size_t)(H > 0 ? H : 0) * sizeof(double) + spmv_sell_split_ws_bytes(n_chunks, C);
+}
+
+// SELL over a hot-column table (col_hot / hot from spmv_hot_columns on the
+// stored SELL columns), global gathers (no x windows: renumbered ids are
+// not x positions), optional split plan (T = INT32_MAX, n_chunks = 0: none).
+// Bit-identical to spmv_sell_run_split on the original columns.
+extern "C" int spmv_sell_run_hot(spmv_dims d, int32_t C, int32_t sigma, int32_t ki, int64_t n_slices,
+                                 const int64_t *slice_ptr, const int32_t *perm, const int32_t *col_hot,
+                                 const double *val, const double *x, double *y, int32_t T, int64_t n_chunks,
+                                 const int32_t *chunk_slice, const int32_t *chunk_k0, int64_t H,
+                                 const int32_t *hot, void *ws, size_t ws_bytes)
+{
+    int rc = sell_check_args(d, C, sigma, ki, n_slices, "spmv_sell_run_hot");
+    if (rc != SPMV_SUCCESS)
+        return rc;
+    if (T <= 0 || T % ki != 0 || n_chunks < 0 || H < 0 || d.n_cols + H > INT32_MAX)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_run_hot: bad T / H");
+    if (d.n_rows == 0 || n_slices == 0)
+        return SPMV_SUCCESS;
+    if ((n_chunks > 0 && (!chunk_slice || !chunk_k0)) || (H > 0 && !hot) || !ws ||
+        ws_bytes < spmv_sell_hot_ws_bytes(n_chunks, C, H))
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_run_hot: plan, hot list or workspace missing");
+    SPMV_GUARD(d);
+    int bt;
+    int64_t blocks;
+    sell_geometry(C, sigma, n_slices, &bt, &blocks);
+    const int64_t cblocks = (n_chunks * C + kBlock - 1) / kBlock;
+    if (blocks > INT32_MAX || cblocks > INT32_MAX)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_run_hot: grid too large");
+    const hipStream_t st = (hipStream_t)d.stream;
+    double *xh = (double *)ws;
+    double *part = xh + H;
+    if (H > 0)
+        hipLaunchKernelGGL(sell_hot_gather_kernel, dim3((unsigned)((H + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
+                           H, hot, x, xh);
+    const XHot xs{x, xh, (int32_t)d.n_cols};
+    const bool nt = stream_nt(kSellStreamNtDefault);
+    auto kern = ki == 2 ? (nt ? sell_kernel<2, true, 4, XHot> : sell_kernel<2, false, 4, XHot>)
+                        : (nt ? sell_kernel<1, true, 4, XHot> : sell_kernel<1, false, 4, XHot>);
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(bt), 0, st, C, n_slices, slice_ptr, perm, col_hot, val, xs,
+                       y, 0, (int64_t)T);
+    SPMV_CHECK_LAUNCH("sell kernel (hot columns)");
+    if (n_chunks == 0)
+        return SPMV_SUCCESS;
+    auto sk = ki == 2 ? (nt ? sell_split_kernel<2, true, 4, XHot> : sell_split_kernel<2, false, 4, XHot>)
+                      : (nt ? sell_split_kernel<1, true, 4, XHot> : sell_split_kernel<1, false, 4, XHot>);
+    hipLaunchKernelGGL(sk, dim3((unsigned)cblocks), dim3(kBlock), 0, st, C, n_chunks, T, slice_ptr, chunk_slice,
+                       chunk_k0, col_hot, val, xs, part);
+    SPMV_CHECK_LAUNCH("sell_split_kernel (hot columns)");
     hipLaunchKernelGGL(sell_split_fix_kernel, dim3((unsigned)cblocks), dim3(kBlock), 0, st, C, n_chunks,
                        chunk_slice, perm, part, y);
     SPMV_CHECK_LAUNCH("sell_split_fix_kernel");

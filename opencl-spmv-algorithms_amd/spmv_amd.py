@@ -123,6 +123,9 @@ HIP_SYMBOLS = {
     "spmv_cmrs_tiled_ws_bytes": (ctypes.c_size_t, [_c_i64, _c_i64, _c_i32]),
     "spmv_cmrs_run_tiled": (ctypes.c_int, [Dims, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t]),
     "spmv_sell_split_ws_bytes": (ctypes.c_size_t, [_c_i64, _c_i32]),
+    "spmv_sell_hot_ws_bytes": (ctypes.c_size_t, [_c_i64, _c_i32, _c_i64]),
+    "spmv_sell_run_hot": (ctypes.c_int, [Dims, _c_i32, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _c_i32,
+                                         _c_i64, _vp, _vp, _c_i64, _vp, _vp, ctypes.c_size_t]),
     "spmv_sell_run_split": (ctypes.c_int, [Dims, _c_i32, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                            _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, ctypes.c_size_t]),
     "spmv_gen_banded_device": (ctypes.c_int, [_c_i64, ctypes.c_uint64, _c_i64, _c_i64, ctypes.c_int, _c_i32,
@@ -582,6 +585,13 @@ class DeviceMatrix:
                                        _ptr(a["win"]), p["xcap"])
         elif self.fmt == "ell":
             rc = lib.spmv_ell_run(d, p["K"], p["ld"], p["ki"], _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y))
+        elif self.fmt == "sell" and p.get("H", 0) > 0:
+            split = p.get("split_T", 0) > 0
+            rc = lib.spmv_sell_run_hot(d, p["C"], p["sigma"], p["ki"], p["n_slices"], _ptr(a["slice_ptr"]),
+                                       _ptr(a["perm"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
+                                       p["split_T"] if split else 2**31 - 1, p["n_chunks"] if split else 0,
+                                       _ptr(a.get("chunk_slice")), _ptr(a.get("chunk_k0")), p["H"], _ptr(a["hot"]),
+                                       _ptr(a["hot_ws"]), a["hot_ws"].numel())
         elif self.fmt == "sell" and p.get("split_T", 0) > 0:
             rc = lib.spmv_sell_run_split(d, p["C"], p["sigma"], p["ki"], p["n_slices"], _ptr(a["slice_ptr"]),
                                          _ptr(a["perm"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
@@ -648,6 +658,27 @@ def _sell_split(dm: DeviceMatrix, slice_ptr: np.ndarray, split: int | None) -> N
     a["chunk_k0"] = _dev_tensor(ck, dm.device)
     a["split_ws"] = torch.empty(max(hip_lib().spmv_sell_split_ws_bytes(n, p["C"]), 8), dtype=torch.uint8,
                                 device=dm.device)
+
+
+def _sell_hot(dm: DeviceMatrix, col: np.ndarray, hot: int | None) -> None:
+    """Hot-column table over the stored SELL columns (None: library rule,
+    0: off).  The renumbered ids are not x positions, so the x windows are
+    dropped; the run gathers globally (spmv_sell_run_hot)."""
+    torch = _torch()
+    p, a = dm.params, dm.arrays
+    p["H"] = 0
+    if hot == 0:
+        return
+    H, hot_cols, col_hot = hot_columns(dm.n_cols, col, hot or 0)
+    if H == 0:
+        return
+    p["H"] = H
+    a["col"] = _dev_tensor(col_hot, dm.device)
+    a["hot"] = _dev_tensor(hot_cols, dm.device)
+    a.pop("win", None)
+    n_chunks = p.get("n_chunks", 0) if p.get("split_T", 0) > 0 else 0
+    a["hot_ws"] = torch.empty(max(hip_lib().spmv_sell_hot_ws_bytes(n_chunks, p["C"], H), 8), dtype=torch.uint8,
+                              device=dm.device)
 
 
 def _cmrs_variant(dm: DeviceMatrix, strip_ptr: np.ndarray, variant: int | None, col=None,
@@ -808,6 +839,7 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
         if xwin:
             _sell_xwin(dm)
         _sell_split(dm, s["slice_ptr"], split)
+        _sell_hot(dm, s["col"][: s["stored"]], hot)
     elif fmt == "hyb":
         hb = hyb_build(m.n_rows, ptr, col, val, ki=ki or 2)
         dm.params = dict(K=hb["K"], ld=hb["ld"], ki=hb["ki"], tail_nnz=hb["tail_nnz"], stored=hb["stored"])

@@ -177,9 +177,24 @@ __global__ __launch_bounds__(kBlock) void coo_carry_kernel(
     const int32_t r = carry_row[t];
     if (r < 0 || (t > 0 && carry_row[t - 1] == r))
         return;  // not a carry, or not the head of its run
+    // A hub row runs over ~100 tiles: 8 tiles' loads in flight per step
+    // instead of one dependent load per tile; still added in tile order.
     double s = 0.0;
-    for (int64_t u = t; u < n_tiles && carry_row[u] == r; ++u)
-        s += carry_val[u];
+    for (int64_t u = t;; u += 8) {
+        int32_t rr[8];
+        double vv[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const bool in = u + k < n_tiles;
+            rr[k] = in ? carry_row[u + k] : -2;
+            vv[k] = in ? carry_val[u + k] : 0.0;
+        }
+        int k = 0;
+        for (; k < 8 && rr[k] == r; ++k)
+            s += vv[k];
+        if (k < 8)
+            break;
+    }
     y[r] += s;
 }
 

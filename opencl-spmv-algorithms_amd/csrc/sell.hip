@@ -322,9 +322,22 @@ __global__ __launch_bounds__(kBlock) void sell_split_fix_kernel(int32_t C, int64
     if (c > 0 && chunk_slice[c - 1] == s)
         return;  // not the first chunk of its slice
     const int64_t r = gid - c * C;
-    double acc = 0.0;
-    for (int64_t u = c; u < n_chunks && chunk_slice[u] == s; ++u)
-        acc += part[u * C + r];
+    double acc = 0.0;  // 8 chunks' loads in flight per step, added in chunk order
+    for (int64_t u = c;; u += 8) {
+        int32_t ss[8];
+        double pp[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const bool in = u + k < n_chunks;
+            ss[k] = in ? chunk_slice[u + k] : -1;
+            pp[k] = in ? part[(u + k) * C + r] : 0.0;
+        }
+        int k = 0;
+        for (; k < 8 && ss[k] == s; ++k)
+            acc += pp[k];
+        if (k < 8)
+            break;
+    }
     const int32_t row = perm[(int64_t)s * C + r];
     if (row >= 0)
         y[row] += acc;

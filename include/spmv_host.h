@@ -127,7 +127,7 @@ int spmv_cmrs_pick_variant(int64_t n_strips, const int64_t *strip_ptr);
 /* SELL split plan for wide slices (spmv_sell_run_split).  _auto gives T
  * (slot columns kept by the main kernel, a multiple of ki) or 0 when no
  * slice is wider than both 1,024 and 16x the mean width.  _plan lists the
- * chunks [k0, k0+T) beyond the first T columns of every slice, in slice
+ * chunks [k0, k0+T) beyond the first T columns of every slice (T = 256), in slice
  * order, and returns their count (arrays may be NULL: count only); -1 on
  * bad arguments.                                                        */
 int32_t spmv_sell_split_auto(int64_t n_slices, const int64_t *slice_ptr, int32_t C, int32_t ki);

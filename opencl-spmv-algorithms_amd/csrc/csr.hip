@@ -463,6 +463,20 @@ struct ChunkRegs {
         }
     }
 
+    template <typename XS>
+    __device__ __forceinline__ void products_xs(const XS &xs, double2 *s_prod) const
+    {
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            double2 pr = {0.0, 0.0};
+            if (live & (1u << (2 * k)))
+                pr.x = v[k].x * xs(c[k].x);
+            if (live & (2u << (2 * k)))
+                pr.y = v[k].y * xs(c[k].y);
+            s_prod[threadIdx.x + k * kBlock] = pr;
+        }
+    }
+
     __device__ __forceinline__ void products(const double *__restrict__ x, double2 *s_prod) const
     {
 #pragma unroll
@@ -476,6 +490,111 @@ struct ChunkRegs {
         }
     }
 };
+
+// The x-window kernel with the first chunk of every window PREFETCHED: its
+// value/column loads are issued (into registers, ChunkRegs) before the
+// window's x range is copied into LDS, so the window copy and the first
+// barrier no longer sit in front of the stream.  Same products, same order:
+// bit-identical to csr_xwin_kernel.  SPMV_CSR_XWIN_PF=0 turns it off.
+template <int L, int R, bool NT, typename XS>
+__device__ __forceinline__ void staged_group_pf(int64_t row, const int64_t *s_ptr, double2 *s_prod,
+                                                const int32_t *__restrict__ col, const double *__restrict__ val,
+                                                const XS xs, double *__restrict__ y, int64_t n_rows,
+                                                const ChunkRegs<R, NT> &pre)
+{
+    constexpr int RPB = kBlock / L;
+    constexpr int CH = 2 * kBlock * R;
+    const int g = threadIdx.x / L;
+    const int lane = threadIdx.x % L;
+    const int64_t beg = s_ptr[g], end = s_ptr[g + 1];
+    const int64_t blk_end = s_ptr[RPB];
+    const double *prod = reinterpret_cast<const double *>(s_prod);
+    double acc = 0.0;
+    bool first = true;
+    for (int64_t cb = s_ptr[0] & ~(int64_t)1; cb < blk_end; cb += CH) {
+        const int64_t ce = cb + CH < blk_end ? cb + CH : blk_end;
+        if (first) {
+            pre.products_xs(xs, s_prod);
+            first = false;
+        } else {
+#pragma unroll
+            for (int k = 0; k < R; ++k) {
+                const int t = threadIdx.x + k * kBlock;
+                const int64_t p = cb + 2 * (int64_t)t;
+                double2 pr = {0.0, 0.0};
+                if (p + 1 < ce) {
+                    const double2 v = stream_load2<NT>(val + p);
+                    const int2 c = stream_load2<NT>(col + p);
+                    pr.x = v.x * xs(c.x);
+                    pr.y = v.y * xs(c.y);
+                } else if (p < ce) {
+                    pr.x = stream_load<NT>(val + p) * xs(stream_load<NT>(col + p));
+                }
+                s_prod[t] = pr;
+            }
+        }
+        __syncthreads();
+        acc += slice_sum<L>(prod, beg > cb ? beg - cb : 0, (end < ce ? end : ce) - cb, lane);
+        __syncthreads();
+    }
+    acc = group_sum<L>(acc);
+    if (lane == 0 && row < n_rows)
+        y[row] = acc;
+    __syncthreads();
+}
+
+template <int L, int R, bool NT>
+__global__ __launch_bounds__(kBlock) void csr_xwin_pf_kernel(
+    int64_t n_rows, int64_t n_groups, int64_t gpw, const int64_t *__restrict__ row_ptr,
+    const int32_t *__restrict__ col, const double *__restrict__ val,
+    const double *__restrict__ x, double *__restrict__ y, const int2 *__restrict__ win, int32_t xcap)
+{
+    constexpr int RPB = kBlock / L;
+    constexpr int CH = 2 * kBlock * R;
+    extern __shared__ double s_x[];
+    __shared__ int64_t s_ptr[RPB + 1];
+    __shared__ double2 s_prod[kBlock * R];
+    const int64_t nz = row_ptr[n_rows];
+    const int64_t n_win = (n_groups + gpw - 1) / gpw;
+    for (int64_t wi = blockIdx.x; wi < n_win; wi += gridDim.x) {
+        const int64_t g_beg = wi * gpw;
+        ChunkRegs<R, NT> pre;
+        {
+            const int64_t r0 = g_beg * RPB;
+            const int64_t r1 = r0 + RPB < n_rows ? r0 + RPB : n_rows;
+            const int64_t b0 = row_ptr[r0] & ~(int64_t)1;
+            const int64_t e0 = row_ptr[r1];
+            pre.issue(col, val, b0, b0 + CH < e0 ? b0 + CH : e0);
+        }
+        const int2 wnd = win[wi];
+        const int32_t span = wnd.y - wnd.x + 1;
+        const bool staged = span > 0 && span <= xcap;  // uniform per workgroup
+        if (staged)
+            for (int32_t i = threadIdx.x; i < span; i += kBlock)
+                s_x[i] = x[wnd.x + i];
+        const int64_t g_end = (wi + 1) * gpw < n_groups ? (wi + 1) * gpw : n_groups;
+        for (int64_t grp = g_beg; grp < g_end; ++grp) {
+            if (threadIdx.x <= RPB) {
+                const int64_t r = grp * RPB + threadIdx.x;
+                s_ptr[threadIdx.x] = row_ptr[r < n_rows ? r : n_rows];
+            }
+            __syncthreads();  // offsets (and, for the first group, the window) visible
+            const int64_t row = grp * RPB + threadIdx.x / L;
+            if (grp == g_beg) {
+                if (staged)
+                    staged_group_pf<L, R, NT>(row, s_ptr, s_prod, col, val, XWindow{s_x, wnd.x}, y, n_rows, pre);
+                else
+                    staged_group_pf<L, R, NT>(row, s_ptr, s_prod, col, val, XGlobal{x}, y, n_rows, pre);
+            } else if (staged) {
+                staged_group<L, R, NT, Col32<NT>, 0, XWindow>(row, s_ptr, s_prod, Col32<NT>{col}, val,
+                                                              XWindow{s_x, wnd.x}, y, n_rows, nz);
+            } else {
+                staged_group<L, R, NT, Col32<NT>, 0, XGlobal>(row, s_ptr, s_prod, Col32<NT>{col}, val,
+                                                              XGlobal{x}, y, n_rows, nz);
+            }
+        }
+    }
+}
 
 // Variant 5: the persistent staged scheme, software-pipelined.  The value
 // and column loads of the NEXT chunk (of this row group or of the block's
@@ -795,6 +914,14 @@ namespace spmv {
 constexpr int32_t kCsrXwinCap = 2048;  // 16 KiB of LDS: 32 KiB per workgroup with the stage
 constexpr int32_t kCsrXwinRows = 128;  // rows per x window (rows_per_window = 0): 0.2836 ms vs 0.2907 (64), 0.2938 (256), 0.2964 (512), 0.3397 (1024)
 
+// SPMV_CSR_XWIN_PF: 1 = csr_xwin_pf_kernel (first chunk prefetched before
+// the window copy), 0 = csr_xwin_kernel.  Read on every call (sweeps).
+static bool csr_xwin_prefetch()
+{
+    const char *s = getenv("SPMV_CSR_XWIN_PF");
+    return s && s[0] == '1';
+}
+
 // rows per x window: a multiple of the row group (256/L rows), default
 // kCsrXwinRows, at least one group
 static int64_t csr_xwin_gpw(int L, int32_t rows_per_window)
@@ -820,8 +947,12 @@ static void launch_csr_xwin(const spmv_dims &d, const int64_t *row_ptr, const in
     const int64_t grid = (ps && ps[0] == '1') ? persistent_grid(csr_xwin_kernel<L, R, NT>, n_win, lds) : n_win;
     if (grid > INT32_MAX)
         return;
-    hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT>), dim3((unsigned)grid), dim3(kBlock), lds,
-                       (hipStream_t)d.stream, d.n_rows, groups, gpw, row_ptr, col, val, x, y, win, xcap);
+    if (csr_xwin_prefetch())
+        hipLaunchKernelGGL((csr_xwin_pf_kernel<L, R, NT>), dim3((unsigned)grid), dim3(kBlock), lds,
+                           (hipStream_t)d.stream, d.n_rows, groups, gpw, row_ptr, col, val, x, y, win, xcap);
+    else
+        hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT>), dim3((unsigned)grid), dim3(kBlock), lds,
+                           (hipStream_t)d.stream, d.n_rows, groups, gpw, row_ptr, col, val, x, y, win, xcap);
 }
 
 template <int L>

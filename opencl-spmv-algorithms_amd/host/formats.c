@@ -464,9 +464,9 @@ int32_t spmv_sell_split_auto(int64_t n_slices, const int64_t *slice_ptr, int32_t
     const double mean = (double)(slice_ptr[n_slices] - slice_ptr[0]) / (double)C / (double)n_slices;
     if (mx <= 1024 || (double)mx <= 16.0 * mean)
         return 0;
-    int64_t t = (int64_t)(4.0 * mean);
-    t = t < 256 ? 256 : t;
-    return (int32_t)round_up(t, ki);
+    /* 256 columns per wave whatever the mean: a mean raised by a few hub
+     * slices (an R-MAT shard of low row ids) must not lengthen every chunk */
+    return (int32_t)round_up(256, ki);
 }
 
 int64_t spmv_sell_split_plan(int64_t n_slices, const int64_t *slice_ptr, int32_t C, int32_t T,

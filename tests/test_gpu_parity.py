@@ -555,3 +555,30 @@ def test_csr16_refuses_escape_heavy_matrix(torch_dev):
     m = sa.gen_rmat(1_000_000, 10_000_000, scale=20, seed=1)
     with pytest.raises(sa.SpmvError):
         sa.to_device(m, "csr16", dev)
+
+
+@pytest.mark.parametrize("case", ["cantlike", "ragged", "fixtures", "rmat"])
+def test_csr_xwin_prefetch_bit_identical(torch_dev, monkeypatch, case):
+    """csr_xwin_pf_kernel (first chunk's loads issued before the x-window
+    copy) gives csr_xwin_kernel's bits."""
+    torch, dev = torch_dev
+    if case == "cantlike":
+        ms = [sa.gen_cantlike(0, copies=2)]
+    elif case == "ragged":
+        ms = [sa.gen_random(20_000, 50_000, 0, 2_000, seed=21)]
+    elif case == "rmat":
+        ms = [sa.gen_rmat(100_000, 1_000_000, scale=17, seed=2)]
+    else:
+        ms = [sa.read_mtx(GOLDEN / f"{n}.mtx") for n in CASES]
+    for m in ms:
+        dm = sa.to_device(m, "csr", dev, variant=3, xwin=True)
+        x = torch.from_numpy(np.random.default_rng(8).uniform(-1, 1, m.n_cols)).to(dev)
+        ys = []
+        for pf in ("0", "1"):
+            monkeypatch.setenv("SPMV_CSR_XWIN_PF", pf)
+            y = torch.full((max(m.n_rows, 1),), float("nan"), dtype=torch.float64, device=dev)
+            dm.run(x, y)
+            ys.append(y)
+        torch.cuda.synchronize()
+        assert torch.equal(ys[0].view(torch.int64), ys[1].view(torch.int64))
+        assert_parity(m, ys[1].cpu().numpy()[: m.n_rows], x.cpu().numpy())

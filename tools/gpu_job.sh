@@ -51,6 +51,8 @@ for s in "${steps[@]}"; do
     rehearseg) run shard_rehearse_graph 900 python tools/shard_rehearse.py --gpus 1,8 --row-weights 4 --graph;;
     profrmat) run prof_rmat 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_rmat -o run -- python3 bench.py --workload rmat --profile --steps 50;;
     testhot) run gpu_tests_hot 900 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "hot or rmat_skewed or bitwise or split";;
+    testpf) run gpu_tests_pf 600 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "prefetch or xwin";;
+    sweeppf) run sweep_pf 600 python tools/sweep.py --rounds 3 --env-only --only csr;;
     rehearse2) run rehearse2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --backend gloo --share-gpu --steps 20;;
     drivers) run drivers 600 python -m pytest tests/test_drivers_gpu.py -q;;
     sweepremap) SPMV_XCD_REMAP=1 run sweep_remap 600 python tools/sweep.py --rounds 2 --only csr,sell,ell;;

@@ -63,7 +63,7 @@ def main():
     ap.add_argument("--gpus", default="1,2,4,8")
     ap.add_argument("--format", default="csr")
     ap.add_argument("--reps", type=int, default=20)
-    ap.add_argument("--row-weights", default="2", help="spmv_partition_rows_weighted weights to try")
+    ap.add_argument("--row-weights", default="4", help="spmv_partition_rows_weighted weights to try")
     ap.add_argument("--hot", type=int, default=-1, help="CSR hot-column table: -1 library rule, 0 off, H")
     ap.add_argument("--graph", action="store_true", help="replay each SpMV as a captured HIP graph")
     a = ap.parse_args()
@@ -78,7 +78,9 @@ def main():
     x = torch.from_numpy(xh).to(dev)
     b_total = sa.bytes_alg(n, n, z)
     base = None
-    kw = {"hot": None if a.hot < 0 else a.hot} if a.format == "csr" else {}
+    kw = {"hot": None if a.hot < 0 else a.hot} if a.format in ("csr", "coo", "cmrs", "sell") else {}
+    if a.format == "sell":
+        kw["sigma"] = 1 << 24  # whole-matrix sort on R-MAT (bench.py's R-MAT default)
     for G, w in [(int(g), float(w)) for w in a.row_weights.split(",") for g in a.gpus.split(",")]:
         bounds = sa.partition_rows(n, ptr, G, align=1024, row_weight=w)
         times, nnzs, params = [], [], None

@@ -263,6 +263,10 @@ typedef struct {
     int32_t split_T;
     int64_t n_chunks;
     int32_t *d_chunk_slice, *d_chunk_k0;
+    /* hot-column table (power-law columns; tiled CSR / CMRS): d_col holds
+     * the renumbered columns, h_col the original ones for the CPU loop */
+    int64_t H;
+    int32_t *d_hot, *d_own_lo;
     /* host copies for the CPU loop */
     int64_t *h_ptr;
     int32_t *h_row, *h_col, *h_perm;
@@ -277,6 +281,33 @@ static int upload(void **dst, const void *src, size_t bytes, void *stream)
     int rc = spmv_malloc(dst, bytes);
     if (rc == SPMV_SUCCESS)
         rc = spmv_upload(*dst, src, bytes, stream);
+    return rc;
+}
+
+/* Hot-column table of the skewed-matrix kernels (spmv_hot_columns' rule):
+ * *col_dev = a renumbered copy of col when it applies, else col. */
+static int hot_table(dev_fmt_t *f, int64_t n_cols, int64_t Z, const int32_t *col, int32_t **col_dev)
+{
+    const int64_t cap = (int64_t)1 << 19;
+    int32_t *hot = malloc((size_t)cap * sizeof(int32_t));
+    int32_t *out = malloc((size_t)(Z + 1) * sizeof(int32_t));
+    if (!hot || !out) {
+        free(hot);
+        free(out);
+        return SPMV_OTHER_ERROR;
+    }
+    const int64_t H = spmv_hot_columns(n_cols, Z, col, 0, hot, out);
+    int rc = H < 0 ? SPMV_OTHER_ERROR : SPMV_SUCCESS;
+    if (H > 0) {
+        f->H = H;
+        rc = upload((void **)&f->d_hot, hot, (size_t)H * 4, NULL);
+        *col_dev = out;
+        out = NULL;
+        if (!rc)
+            printf("hot-column table: %lld columns\n", (long long)H);
+    }
+    free(hot);
+    free(out);
     return rc;
 }
 
@@ -321,6 +352,7 @@ static int build_format(const opts_t *o, spmv_format fmt, const coo_t *m, dev_fm
         f->h_col = col;
         f->h_val = val;
         f->stored = Z;
+        int32_t *col_dev = col; /* what d_col gets: col, or col with hot ids */
         if (fmt == FMT_CSR) {
             f->lanes = o->lanes > 0 ? o->lanes : spmv_csr_auto_lanes(N, Z);
             f->variant = spmv_csr_pick_variant(N, ptr); /* 4: entry-balanced (skewed rows) */
@@ -328,8 +360,14 @@ static int build_format(const opts_t *o, spmv_format fmt, const coo_t *m, dev_fm
             if ((rc = upload((void **)&f->d_ptr, ptr, (size_t)(N + 1) * 8, NULL)))
                 return rc;
             if (f->variant == 4) {
-                f->ws_bytes = spmv_csr_tiled_ws_bytes(N, Z);
+                if ((rc = hot_table(f, m->n_cols, Z, col, &col_dev)))
+                    return rc;
+                f->ws_bytes = spmv_csr_hot_ws_bytes(N, Z, f->H);
+                const int64_t n_plan = spmv_csr_tiled_plan_len(Z);
                 if ((rc = spmv_malloc(&f->d_ws, f->ws_bytes)))
+                    return rc;
+                if (n_plan > 0 && ((rc = spmv_malloc((void **)&f->d_own_lo, (size_t)n_plan * 4)) ||
+                                   (rc = spmv_csr_tiled_plan(f->d, f->d_ptr, f->d_own_lo))))
                     return rc;
             }
         } else {
@@ -347,13 +385,17 @@ static int build_format(const opts_t *o, spmv_format fmt, const coo_t *m, dev_fm
                 return rc;
             f->variant = spmv_cmrs_pick_variant(f->n_strips, sp); /* 1: entry-balanced (skewed strips) */
             if (f->variant == 1) {
-                f->ws_bytes = spmv_cmrs_tiled_ws_bytes(f->n_strips, Z, f->h);
+                if ((rc = hot_table(f, m->n_cols, Z, col, &col_dev)))
+                    return rc;
+                f->ws_bytes = spmv_cmrs_hot_ws_bytes(f->n_strips, Z, f->h, f->H);
                 if ((rc = spmv_malloc(&f->d_ws, f->ws_bytes)))
                     return rc;
             }
         }
-        if ((rc = upload((void **)&f->d_col, col, (size_t)Z * 4, NULL)) ||
-            (rc = upload((void **)&f->d_val, val, (size_t)Z * 8, NULL)))
+        rc = upload((void **)&f->d_col, col_dev, (size_t)Z * 4, NULL);
+        if (col_dev != col)
+            free(col_dev);
+        if (rc || (rc = upload((void **)&f->d_val, val, (size_t)Z * 8, NULL)))
             return rc;
         return SPMV_SUCCESS;
     }
@@ -442,8 +484,6 @@ static int build_windows(dev_fmt_t *f)
         bytes = spmv_ell_xwin_bytes(f->d.n_rows);
     else if (f->fmt == FMT_SELL)
         bytes = spmv_sell_xwin_bytes(f->n_slices, f->C, f->sigma);
-    else if (f->fmt == FMT_COO)
-        bytes = spmv_coo_xwin_bytes(f->d.nnz);
     else if (f->fmt == FMT_CMRS && f->variant == 0)
         bytes = spmv_cmrs_xwin_bytes(f->d, f->h, f->n_strips);
     if (bytes == 0)
@@ -495,8 +535,8 @@ static int launch(void *arg)
                             f->ws_bytes);
     case FMT_CSR:
         if (f->variant == 4)
-            return spmv_csr_run_tiled(f->d, f->d_ptr, f->d_col, f->d_val, f->d_x, f->d_y, f->d_ws,
-                                      f->ws_bytes);
+            return spmv_csr_run_tiled_hot(f->d, f->d_ptr, f->d_col, f->d_val, f->d_x, f->d_y, f->H, f->d_hot,
+                                          f->d_own_lo, f->d_ws, f->ws_bytes);
         return spmv_csr_run(f->d, f->d_ptr, f->d_col, f->d_val, f->d_x, f->d_y, f->lanes);
     case FMT_ELL:
         return spmv_ell_run(f->d, f->K, f->ld, f->ki, f->d_col, f->d_val, f->d_x, f->d_y);
@@ -505,8 +545,8 @@ static int launch(void *arg)
                              f->d_val, f->d_x, f->d_y);
     case FMT_CMRS:
         if (f->variant == 1)
-            return spmv_cmrs_run_tiled(f->d, f->h, f->n_strips, f->d_ptr, f->d_rin, f->d_col, f->d_val, f->d_x,
-                                       f->d_y, f->d_ws, f->ws_bytes);
+            return spmv_cmrs_run_tiled_hot(f->d, f->h, f->n_strips, f->d_ptr, f->d_rin, f->d_col, f->d_val,
+                                           f->d_x, f->d_y, f->H, f->d_hot, f->d_ws, f->ws_bytes);
         return spmv_cmrs_run(f->d, f->h, f->n_strips, f->d_ptr, f->d_rin, f->d_col, f->d_val,
                              f->d_x, f->d_y);
     }

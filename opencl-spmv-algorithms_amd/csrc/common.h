@@ -31,6 +31,9 @@ class DeviceGuard {
 
 // XCD-contiguous blockIdx remap switch (SPMV_XCD_REMAP=1 enables; read once).
 bool xcd_remap_enabled();
+// XCD-contiguous window placement of the CSR / SELL x-window kernels:
+// SPMV_XWIN_REMAP=1 (read on every call, so a sweep can flip it).
+bool xwin_remap();
 
 // LDS-staged CMRS / COO launchers (staged.hip)
 // win != nullptr: the x-window kernels (win/xcap from *_xwin_build)

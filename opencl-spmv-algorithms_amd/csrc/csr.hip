@@ -399,7 +399,8 @@ template <int L, int R, bool NT>
 __global__ __launch_bounds__(kBlock) void csr_xwin_kernel(
     int64_t n_rows, int64_t n_groups, int64_t gpw, const int64_t *__restrict__ row_ptr,
     const int32_t *__restrict__ col, const double *__restrict__ val,
-    const double *__restrict__ x, double *__restrict__ y, const int2 *__restrict__ win, int32_t xcap)
+    const double *__restrict__ x, double *__restrict__ y, const int2 *__restrict__ win, int32_t xcap,
+    int remap)
 {
     constexpr int RPB = kBlock / L;
     extern __shared__ double s_x[];
@@ -407,7 +408,9 @@ __global__ __launch_bounds__(kBlock) void csr_xwin_kernel(
     __shared__ double2 s_prod[kBlock * R];
     const int64_t nz = row_ptr[n_rows];
     const int64_t n_win = (n_groups + gpw - 1) / gpw;
-    for (int64_t wi = blockIdx.x; wi < n_win; wi += gridDim.x) {
+    // remap: consecutive windows on one XCD, so the overlapping x ranges of
+    // neighbouring windows are copied from that XCD's L2
+    for (int64_t wi = xcd_block(remap); wi < n_win; wi += gridDim.x) {
         const int2 wnd = win[wi];
         const int32_t span = wnd.y - wnd.x + 1;
         const bool staged = span > 0 && span <= xcap;  // uniform per workgroup
@@ -952,7 +955,8 @@ static void launch_csr_xwin(const spmv_dims &d, const int64_t *row_ptr, const in
                            (hipStream_t)d.stream, d.n_rows, groups, gpw, row_ptr, col, val, x, y, win, xcap);
     else
         hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT>), dim3((unsigned)grid), dim3(kBlock), lds,
-                           (hipStream_t)d.stream, d.n_rows, groups, gpw, row_ptr, col, val, x, y, win, xcap);
+                           (hipStream_t)d.stream, d.n_rows, groups, gpw, row_ptr, col, val, x, y, win, xcap,
+                           xwin_remap() ? 1 : 0);
 }
 
 template <int L>

@@ -48,6 +48,12 @@ DeviceGuard::~DeviceGuard()
         (void)hipSetDevice(prev_);
 }
 
+bool xwin_remap()
+{
+    const char *s = getenv("SPMV_XWIN_REMAP");
+    return s && s[0] == '1';
+}
+
 bool xcd_remap_enabled()
 {
     static int cached = -1;

@@ -253,10 +253,11 @@ __global__ __launch_bounds__(1024) void sell_xwin_kernel(
     int32_t C, int64_t n_slices, const int64_t *__restrict__ slice_ptr,
     const int32_t *__restrict__ perm, const int32_t *__restrict__ col,
     const double *__restrict__ val, const double *__restrict__ x,
-    double *__restrict__ y, const int2 *__restrict__ win, int32_t xcap, int64_t wcap)
+    double *__restrict__ y, const int2 *__restrict__ win, int32_t xcap, int64_t wcap, int remap)
 {
     extern __shared__ double s_x[];
-    const int2 wnd = win[blockIdx.x];
+    const int64_t blk = xcd_block(remap);  // remap: neighbouring windows on one XCD (shared x lines in L2)
+    const int2 wnd = win[blk];
     const int32_t span = wnd.y - wnd.x + 1;
     const bool staged = span > 0 && span <= xcap;  // uniform per workgroup
     if (staged) {
@@ -264,7 +265,7 @@ __global__ __launch_bounds__(1024) void sell_xwin_kernel(
             s_x[i] = x[wnd.x + i];
         __syncthreads();
     }
-    const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t slot = blk * blockDim.x + threadIdx.x;
     const int64_t s = slot / C;
     if (s >= n_slices)
         return;
@@ -465,7 +466,7 @@ extern "C" int spmv_sell_run_xwin(spmv_dims d, int32_t C, int32_t sigma, int32_t
                         : (nt ? sell_xwin_kernel<1, true, 4> : sell_xwin_kernel<1, false, 4>);
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(bt), (size_t)xcap * sizeof(double),
                        (hipStream_t)d.stream, C, n_slices, slice_ptr, perm, col, val, x, y,
-                       (const int2 *)win, xcap, (int64_t)INT64_MAX);
+                       (const int2 *)win, xcap, (int64_t)INT64_MAX, xwin_remap() ? 1 : 0);
     SPMV_CHECK_LAUNCH("sell_xwin_kernel");
     return SPMV_SUCCESS;
 }
@@ -632,7 +633,8 @@ extern "C" int spmv_sell_run_split(spmv_dims d, int32_t C, int32_t sigma, int32_
         auto kern = ki == 2 ? (nt ? sell_xwin_kernel<2, true, 4> : sell_xwin_kernel<2, false, 4>)
                             : (nt ? sell_xwin_kernel<1, true, 4> : sell_xwin_kernel<1, false, 4>);
         hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(bt), (size_t)xcap * sizeof(double), st, C, n_slices,
-                           slice_ptr, perm, col, val, x, y, (const int2 *)win, xcap, (int64_t)T);
+                           slice_ptr, perm, col, val, x, y, (const int2 *)win, xcap, (int64_t)T,
+                           xwin_remap() ? 1 : 0);
     } else {
         auto kern = ki == 2 ? (nt ? sell_kernel<2, true, 4> : sell_kernel<2, false, 4>)
                             : (nt ? sell_kernel<1, true, 4> : sell_kernel<1, false, 4>);

@@ -43,8 +43,10 @@ VARIANTS = [
     ("csr", {"variant": 4, "hot": 1 << 20, "env": {}}),
     ("csr", {"variant": 4, "env": {"SPMV_STREAM_NT": "0"}}),
     ("coo", {"xwin": True, "env": {}}),
-    ("csr", {"env": {"SPMV_CSR_XWIN_PF": "1"}}),
-    ("csr", {"env": {"SPMV_CSR_XWIN_PF": "0"}}),
+    ("csr", {"env": {"SPMV_XWIN_REMAP": "1"}}),
+    ("csr", {"env": {"SPMV_XWIN_REMAP": "0"}}),
+    ("sell", {"env": {"SPMV_XWIN_REMAP": "1"}}),
+    ("sell", {"env": {"SPMV_XWIN_REMAP": "0"}}),
     ("sell", {"C": 64, "sigma": 65536, "ki": 1, "env": {}}),
     ("sell", {"C": 64, "sigma": 1 << 20, "ki": 1, "env": {}}),
     ("sell", {"C": 64, "sigma": 1 << 24, "ki": 1, "env": {}}),

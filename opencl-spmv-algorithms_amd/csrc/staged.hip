@@ -205,7 +205,7 @@ __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
     const int64_t r_lo = (int64_t)prev + 1;
     const int64_t span = (int64_t)last - r_lo + 1;  // rows (prev, last]
     bool heads = false;  // uniform per workgroup
-    if constexpr (!ACC) {
+    {
         heads = span >= 0 && span <= kCooRowCap;
         if (heads) {
             for (int j = threadIdx.x; j < n; j += kBlock) {
@@ -236,19 +236,26 @@ __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
     }
     if constexpr (ACC) {
         // accumulate mode (HYB tail): y[r] += the tile's entries of every row
-        // that begins here; rows without entries are left untouched, so only
-        // the row keys present are visited: one thread per run of equal keys,
-        // summed in entry order
-        for (int j = threadIdx.x; j < n; j += kBlock) {
-            const int32_t r = s_row[j];
-            const bool head = j == 0 ? r != prev : r != s_row[j - 1];
-            if (!head || (j == 0 && first_continues))
-                continue;
+        // that begins here; rows without entries in the tail are left
+        // untouched.  One L-lane group per row (a hub row's 1,536 tile
+        // entries no longer fall to one thread).
+        for (int64_t r = r_lo + g; r <= (int64_t)last; r += GROUPS) {
+            int a, b;
+            if (heads) {
+                a = s_start[r - r_lo];
+                b = s_start[r - r_lo + 1];
+            } else {
+                a = lower_bound_lds(s_row, 0, n, (int)r);
+                b = lower_bound_lds(s_row, a, n, (int)r + 1);
+            }
+            if (a == b)
+                continue;  // uniform over the group
             double s = 0.0;
-            int k = j;
-            for (; k < n && s_row[k] == r; ++k)
-                s += prod[k];
-            y[r] += s;
+            for (int j = a + lane; j < b; j += L)
+                s += prod[j];
+            s = group_sum<L>(s);
+            if (lane == 0)
+                y[r] += s;
         }
         return;
     }

@@ -159,6 +159,14 @@ int spmv_ell_run_xwin(spmv_dims d, int32_t K, int64_t ld, int32_t ki, const int3
  * by the staged COO kernel in accumulate mode and the deterministic carry
  * pass.  `ws` holds spmv_hyb_ws_bytes(tail_nnz) bytes.                    */
 size_t spmv_hyb_ws_bytes(int64_t tail_nnz);
+/* HYB over a hot-column table (spmv_hot_columns over the ELL and tail
+ * columns together): bit-identical to spmv_hyb_run on the original
+ * columns; `ws` holds spmv_hyb_hot_ws_bytes(tail_nnz, H) bytes.          */
+size_t spmv_hyb_hot_ws_bytes(int64_t tail_nnz, int64_t H);
+int spmv_hyb_run_hot(spmv_dims d, int32_t K, int64_t ld, int32_t ki, const int32_t *ell_col_hot,
+                     const double *ell_val, int64_t tail_nnz, const int32_t *tail_row,
+                     const int32_t *tail_col_hot, const double *tail_val, const double *x, double *y,
+                     int64_t H, const int32_t *hot, void *ws, size_t ws_bytes);
 int spmv_hyb_run(spmv_dims d, int32_t K, int64_t ld, int32_t ki, const int32_t *ell_col,
                  const double *ell_val, int64_t tail_nnz, const int32_t *tail_row,
                  const int32_t *tail_col, const double *tail_val, const double *x, double *y,

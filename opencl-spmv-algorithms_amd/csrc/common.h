@@ -64,6 +64,10 @@ int launch_cmrs_tiled(const spmv_dims &d, int32_t h, int64_t n_strips, const int
                       const uint8_t *rin, const int32_t *col, const double *val, const double *x,
                       double *y, int32_t *own_lo, int32_t *carry_row, double *carry_val, int64_t H = 0,
                       const int32_t *hot = nullptr, double *xh = nullptr);
+struct XHot;
+int launch_coo_staged_acc_hot(const spmv_dims &d, const int32_t *row, const int32_t *col,
+                              const double *val, const double *x, double *y, int32_t *carry_row,
+                              double *carry_val, const XHot xs);
 int launch_coo_staged_hot(const spmv_dims &d, const int32_t *row, const int32_t *col, const double *val,
                           const double *x, double *y, int32_t *carry_row, double *carry_val, int64_t H,
                           const int32_t *hot, double *xh);

@@ -116,17 +116,17 @@ __global__ __launch_bounds__(1024) void sell_kernel(
         y[row] = sum;
 }
 
-template <int KI, bool NT, int U>
+template <int KI, bool NT, int U, typename XS = XGlobal>
 __global__ __launch_bounds__(kBlock) void ell_kernel(
     int64_t n_rows, int32_t K, int64_t ld, const int32_t *__restrict__ col,
-    const double *__restrict__ val, const double *__restrict__ x,
+    const double *__restrict__ val, const XS xs,
     double *__restrict__ y, int remap)
 {
     const int64_t i = xcd_block(remap) * kBlock + threadIdx.x;
     if (i >= n_rows)
         return;
     const int64_t off = i * KI;
-    y[i] = slot_dot<KI, NT, U>(val + off, col + off, K, ld * KI, XGlobal{x});
+    y[i] = slot_dot<KI, NT, U>(val + off, col + off, K, ld * KI, xs);
 }
 
 // Column window of every 256-row ELL workgroup: its rows' entries of
@@ -491,7 +491,7 @@ extern "C" int spmv_ell_run(spmv_dims d, int32_t K, int64_t ld, int32_t ki,
                         : (nt ? (u8 ? ell_kernel<1, true, 8> : ell_kernel<1, true, 4>)
                               : (u8 ? ell_kernel<1, false, 8> : ell_kernel<1, false, 4>));
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock), 0, (hipStream_t)d.stream,
-                       d.n_rows, K, ld, col, val, x, y, remap);
+                       d.n_rows, K, ld, col, val, XGlobal{x}, y, remap);
     SPMV_CHECK_LAUNCH("ell_kernel");
     return SPMV_SUCCESS;
 }
@@ -712,4 +712,55 @@ extern "C" int spmv_sell_run_hot(spmv_dims d, int32_t C, int32_t sigma, int32_t 
                        chunk_slice, perm, part, y);
     SPMV_CHECK_LAUNCH("sell_split_fix_kernel");
     return SPMV_SUCCESS;
+}
+
+extern "C" size_t spmv_hyb_hot_ws_bytes(int64_t tail_nnz, int64_t H)
+{
+    return (size_t)(H > 0 ? H : 0) * sizeof(double) + spmv_hyb_ws_bytes(tail_nnz);
+}
+
+// HYB over a hot-column table (ell_col_hot / tail_col_hot renumbered by
+// spmv_hot_columns over both column arrays): the ELL part and the COO tail
+// read the hottest x values from xh.  Bit-identical to spmv_hyb_run on the
+// original columns.
+extern "C" int spmv_hyb_run_hot(spmv_dims d, int32_t K, int64_t ld, int32_t ki, const int32_t *ell_col_hot,
+                                const double *ell_val, int64_t tail_nnz, const int32_t *tail_row,
+                                const int32_t *tail_col_hot, const double *tail_val, const double *x, double *y,
+                                int64_t H, const int32_t *hot, void *ws, size_t ws_bytes)
+{
+    if (H < 0 || tail_nnz < 0 || d.n_cols + H > INT32_MAX)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_hyb_run_hot: bad sizes");
+    if (H == 0)
+        return spmv_hyb_run(d, K, ld, ki, ell_col_hot, ell_val, tail_nnz, tail_row, tail_col_hot, tail_val, x, y,
+                            ws, ws_bytes);
+    if (d.n_rows < 0 || K < 0 || ld < d.n_rows || ld % 64 != 0 || (ki != 1 && ki != 2) || K % ki != 0)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_hyb_run_hot: bad K / ld / ki");
+    if (d.n_rows == 0)
+        return SPMV_SUCCESS;
+    if (!hot || !ws || ws_bytes < spmv_hyb_hot_ws_bytes(tail_nnz, H))
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_hyb_run_hot: hot list or workspace missing");
+    SPMV_GUARD(d);
+    const hipStream_t st = (hipStream_t)d.stream;
+    double *xh = (double *)ws;
+    hipLaunchKernelGGL(sell_hot_gather_kernel, dim3((unsigned)((H + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, H,
+                       hot, x, xh);
+    const XHot xs{x, xh, (int32_t)d.n_cols};
+    const int64_t blocks = (d.n_rows + kBlock - 1) / kBlock;
+    const bool nt = stream_nt(kSellStreamNtDefault);
+    auto kern = ki == 2 ? (nt ? ell_kernel<2, true, 4, XHot> : ell_kernel<2, false, 4, XHot>)
+                        : (nt ? ell_kernel<1, true, 4, XHot> : ell_kernel<1, false, 4, XHot>);
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock), 0, st, d.n_rows, K, ld, ell_col_hot, ell_val, xs,
+                       y, 0);
+    SPMV_CHECK_LAUNCH("ell_kernel (hot columns)");
+    if (tail_nnz == 0)
+        return SPMV_SUCCESS;
+    const int64_t tiles = (tail_nnz + coo_staged_tile() - 1) / coo_staged_tile();
+    double *carry_val = xh + H;
+    int32_t *carry_row = (int32_t *)(carry_val + tiles);
+    spmv_dims dt = d;
+    dt.nnz = tail_nnz;
+    int rc = launch_coo_staged_acc_hot(dt, tail_row, tail_col_hot, tail_val, x, y, carry_row, carry_val, xs);
+    if (rc != SPMV_SUCCESS)
+        return rc;
+    return launch_carry(tiles, carry_row, carry_val, y, st);
 }

@@ -664,6 +664,23 @@ int launch_coo_staged_acc(const spmv_dims &d, const int32_t *row, const int32_t 
     return SPMV_SUCCESS;
 }
 
+int launch_coo_staged_acc_hot(const spmv_dims &d, const int32_t *row, const int32_t *col,
+                              const double *val, const double *x, double *y, int32_t *carry_row,
+                              double *carry_val, const XHot xs)
+{
+    constexpr int R = 3;
+    const int64_t tiles = (d.nnz + coo_staged_tile() - 1) / coo_staged_tile();
+    if (tiles > INT32_MAX)
+        return fail_msg(SPMV_OTHER_ERROR, "hyb tail: grid too large");
+    if (tiles == 0)
+        return SPMV_SUCCESS;
+    hipLaunchKernelGGL((coo_staged_kernel<4, R, true, false, true, XHot>), dim3((unsigned)tiles), dim3(kBlock), 0,
+                       (hipStream_t)d.stream, d.n_rows, d.nnz, row, col, val, x, y, carry_row, carry_val,
+                       (const int2 *)nullptr, 0, xs);
+    SPMV_CHECK_LAUNCH("coo_staged_kernel (accumulate, hot columns)");
+    return SPMV_SUCCESS;
+}
+
 int launch_coo_staged(const spmv_dims &d, const int32_t *row, const int32_t *col,
                       const double *val, const double *x, double *y, int32_t *carry_row,
                       double *carry_val, const int2 *win, int32_t xcap)

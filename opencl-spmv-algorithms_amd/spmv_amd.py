@@ -124,6 +124,9 @@ HIP_SYMBOLS = {
     "spmv_cmrs_run_tiled": (ctypes.c_int, [Dims, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t]),
     "spmv_sell_split_ws_bytes": (ctypes.c_size_t, [_c_i64, _c_i32]),
     "spmv_sell_hot_ws_bytes": (ctypes.c_size_t, [_c_i64, _c_i32, _c_i64]),
+    "spmv_hyb_hot_ws_bytes": (ctypes.c_size_t, [_c_i64, _c_i64]),
+    "spmv_hyb_run_hot": (ctypes.c_int, [Dims, _c_i32, _c_i64, _c_i32, _vp, _vp, _c_i64, _vp, _vp, _vp, _vp, _vp,
+                                        _c_i64, _vp, _vp, ctypes.c_size_t]),
     "spmv_sell_run_hot": (ctypes.c_int, [Dims, _c_i32, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _c_i32,
                                          _c_i64, _vp, _vp, _c_i64, _vp, _vp, ctypes.c_size_t]),
     "spmv_sell_run_split": (ctypes.c_int, [Dims, _c_i32, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
@@ -576,6 +579,10 @@ class DeviceMatrix:
         elif self.fmt == "csr16":
             rc = lib.spmv_csr16_run(d, _ptr(a["row_ptr"]), _ptr(a["blk_base"]), _ptr(a["col_off"]),
                                     _ptr(a["col_esc"]), _ptr(a["val"]), _ptr(x), _ptr(y), p["lanes"])
+        elif self.fmt == "hyb" and p.get("H", 0) > 0:
+            rc = lib.spmv_hyb_run_hot(d, p["K"], p["ld"], p["ki"], _ptr(a["ell_col"]), _ptr(a["ell_val"]),
+                                      p["tail_nnz"], _ptr(a["tail_row"]), _ptr(a["tail_col"]), _ptr(a["tail_val"]),
+                                      _ptr(x), _ptr(y), p["H"], _ptr(a["hot"]), _ptr(a["ws"]), a["ws"].numel())
         elif self.fmt == "hyb":
             rc = lib.spmv_hyb_run(d, p["K"], p["ld"], p["ki"], _ptr(a["ell_col"]), _ptr(a["ell_val"]), p["tail_nnz"],
                                   _ptr(a["tail_row"]), _ptr(a["tail_col"]), _ptr(a["tail_val"]), _ptr(x), _ptr(y),
@@ -842,10 +849,20 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
         _sell_hot(dm, s["col"][: s["stored"]], hot)
     elif fmt == "hyb":
         hb = hyb_build(m.n_rows, ptr, col, val, ki=ki or 2)
-        dm.params = dict(K=hb["K"], ld=hb["ld"], ki=hb["ki"], tail_nnz=hb["tail_nnz"], stored=hb["stored"])
-        ws = hip_lib().spmv_hyb_ws_bytes(hb["tail_nnz"])
+        dm.params = dict(K=hb["K"], ld=hb["ld"], ki=hb["ki"], tail_nnz=hb["tail_nnz"], stored=hb["stored"], H=0)
+        if hot != 0:  # one table over the ELL and tail columns together
+            ne, nt_ = hb["stored"], hb["tail_nnz"]
+            both = np.concatenate([hb["ell_col"][:ne], hb["tail_col"][:nt_]])
+            H, hot_cols, both_hot = hot_columns(m.n_cols, both, hot or 0)
+            if H > 0:
+                dm.params["H"] = H
+                hb["ell_col"] = both_hot[:ne]
+                hb["tail_col"] = np.concatenate([both_hot[ne:], np.zeros(max(1 - nt_, 0), np.int32)])
+        ws = hip_lib().spmv_hyb_hot_ws_bytes(hb["tail_nnz"], dm.params["H"])
         dm.arrays = {k: _dev_tensor(hb[k], device) for k in ("ell_col", "ell_val", "tail_row", "tail_col", "tail_val")}
         dm.arrays["ws"] = torch.empty(max(ws, 16), dtype=torch.uint8, device=device)
+        if dm.params["H"] > 0:
+            dm.arrays["hot"] = _dev_tensor(hot_cols, device)
         dm.stored_bytes = 12 * hb["stored"] + 16 * hb["tail_nnz"]
     elif fmt == "cmrs":
         c = cmrs_build(m.n_rows, ptr, h=h)

@@ -528,7 +528,7 @@ def test_csr_hot_bit_identical(torch_dev, H):
 
 @pytest.mark.parametrize("fmt,kw", [("coo", {}), ("cmrs", {"cmrs_variant": 1}), ("cmrs", {"cmrs_variant": 1, "h": 32}),
                                     ("sell", {"xwin": False}), ("sell", {"sigma": 1 << 24, "ki": 2, "xwin": False}),
-                                    ("sell", {"split": 0, "xwin": False})])
+                                    ("sell", {"split": 0, "xwin": False}), ("hyb", {}), ("hyb", {"ki": 1})])
 @pytest.mark.parametrize("H", [1, 4096])
 def test_coo_cmrs_hot_bit_identical(torch_dev, fmt, kw, H):
     """COO / tiled CMRS over the hot-column table: the same products in the

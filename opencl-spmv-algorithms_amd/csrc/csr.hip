@@ -269,10 +269,34 @@ __device__ __forceinline__ double slice_sum(const double *prod, int64_t lo64, in
     return a0 + a1;
 }
 
-template <int L, int R, bool NT, typename Cols = Col32<NT>, int BATCH = 0, typename XS = XGlobal>
+// Value loads of the staged kernels: fp64 values, or fp32 values (CSR-f32v,
+// SURVEY.md §8f row 4) widened to fp64 before the product.
+typedef float v2f32 __attribute__((ext_vector_type(2)));
+
+template <bool NT>
+__device__ __forceinline__ double2 vpair(const double *p)
+{
+    return stream_load2<NT>(p);
+}
+
+template <bool NT>
+__device__ __forceinline__ double2 vpair(const float *p)
+{
+    const v2f32 v = stream_load<NT>(reinterpret_cast<const v2f32 *>(p));
+    return double2{(double)v.x, (double)v.y};
+}
+
+template <bool NT, typename V>
+__device__ __forceinline__ double vone(const V *p)
+{
+    return (double)stream_load<NT>(p);
+}
+
+template <int L, int R, bool NT, typename Cols = Col32<NT>, int BATCH = 0, typename XS = XGlobal,
+          typename V = double>
 __device__ __forceinline__ void staged_group(
     int64_t row, const int64_t *s_ptr, double2 *s_prod,
-    const Cols cols, const double *__restrict__ val,
+    const Cols cols, const V *__restrict__ val,
     const XS xs, double *__restrict__ y, int64_t n_rows, int64_t nz)
 {
     constexpr int RPB = kBlock / L;
@@ -297,12 +321,12 @@ __device__ __forceinline__ void staged_group(
                 const int64_t p = cb + 2 * (int64_t)t;
                 double2 pr = {0.0, 0.0};
                 if (p + 1 < ce) {
-                    const double2 v = stream_load2<NT>(val + p);
+                    const double2 v = vpair<NT>(val + p);
                     const int2 c = cols.pair(p);
                     pr.x = v.x * xs(c.x);
                     pr.y = v.y * xs(c.y);
                 } else if (p < ce) {
-                    pr.x = stream_load<NT>(val + p) * xs(cols.one(p));
+                    pr.x = vone<NT>(val + p) * xs(cols.one(p));
                 }
                 s_prod[t] = pr;
             }
@@ -395,10 +419,10 @@ __global__ __launch_bounds__(kBlock) void csr_window_kernel(int64_t n_rows, int6
 // Windows of several groups overlap less than per-group windows, so less
 // x is re-read.  A window wider than xcap gathers from global memory.
 // Same products, same order: y is bit-identical to variant 3.
-template <int L, int R, bool NT>
+template <int L, int R, bool NT, typename V = double>
 __global__ __launch_bounds__(kBlock) void csr_xwin_kernel(
     int64_t n_rows, int64_t n_groups, int64_t gpw, const int64_t *__restrict__ row_ptr,
-    const int32_t *__restrict__ col, const double *__restrict__ val,
+    const int32_t *__restrict__ col, const V *__restrict__ val,
     const double *__restrict__ x, double *__restrict__ y, const int2 *__restrict__ win, int32_t xcap,
     int remap)
 {
@@ -426,11 +450,11 @@ __global__ __launch_bounds__(kBlock) void csr_xwin_kernel(
             __syncthreads();  // offsets (and, for the first group, the window) visible
             const int64_t row = grp * RPB + threadIdx.x / L;
             if (staged)
-                staged_group<L, R, NT, Col32<NT>, 0, XWindow>(row, s_ptr, s_prod, Col32<NT>{col}, val,
-                                                              XWindow{s_x, wnd.x}, y, n_rows, nz);
+                staged_group<L, R, NT, Col32<NT>, 0, XWindow, V>(row, s_ptr, s_prod, Col32<NT>{col}, val,
+                                                                 XWindow{s_x, wnd.x}, y, n_rows, nz);
             else
-                staged_group<L, R, NT, Col32<NT>, 0, XGlobal>(row, s_ptr, s_prod, Col32<NT>{col}, val,
-                                                              XGlobal{x}, y, n_rows, nz);
+                staged_group<L, R, NT, Col32<NT>, 0, XGlobal, V>(row, s_ptr, s_prod, Col32<NT>{col}, val,
+                                                                 XGlobal{x}, y, n_rows, nz);
         }
     }
 }
@@ -1171,4 +1195,57 @@ extern "C" int spmv_csr_run_tiled_hot(spmv_dims d, const int64_t *row_ptr, const
     if (rc != SPMV_SUCCESS)
         return rc;
     return launch_carry(tiles, carry_row, carry_val, y, (hipStream_t)d.stream);
+}
+
+// CSR with fp32 values (8 bytes per entry instead of
+// 12): the x-window kernel widens each value to fp64 before the product
+// and sums in fp64, so y equals spmv_csr_run_xwin's on the fp32-rounded
+// values bit for bit.  Windows from spmv_csr_xwin_build on the same
+// row_ptr/col with the same lanes_per_row and rows_per_window.
+extern "C" int spmv_csr_f32v_run_xwin(spmv_dims d, const int64_t *row_ptr, const int32_t *col, const float *val,
+                                      const double *x, double *y, int lanes_per_row, int32_t rows_per_window,
+                                      const void *win, int32_t xcap)
+{
+    if (d.n_rows < 0 || d.n_cols < 0 || d.nnz < 0 || rows_per_window < 0)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_f32v_run_xwin: bad sizes");
+    if (d.n_rows == 0)
+        return SPMV_SUCCESS;
+    if (!win || xcap < 0 || xcap > kCsrXwinCap)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_f32v_run_xwin: bad window arguments");
+    SPMV_GUARD(d);
+    const int L = lanes_per_row > 0 ? lanes_per_row : spmv_csr_auto_lanes(d.n_rows, d.nnz);
+    if (L < 2 || L > 64 || (L & (L - 1)))
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_f32v_run_xwin: lanes_per_row must be 0 or a power of two in [2,64]");
+    const int64_t gpw = csr_xwin_gpw(L, rows_per_window);
+    const bool nt = stream_nt(kCsrXwinNtDefault);
+    constexpr int R = kStageRoundsDefault;
+    const int2 *w = (const int2 *)win;
+    const int64_t groups_base = d.n_rows;
+#define SPMV_XWIN32(LL)                                                                                     \
+    do {                                                                                                    \
+        constexpr int RPB = kBlock / LL;                                                                    \
+        const int64_t groups = (groups_base + RPB - 1) / RPB;                                               \
+        const int64_t n_win = (groups + gpw - 1) / gpw;                                                     \
+        if (n_win > INT32_MAX)                                                                              \
+            return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_f32v_run_xwin: grid too large");                    \
+        if (nt)                                                                                             \
+            hipLaunchKernelGGL((csr_xwin_kernel<LL, R, true, float>), dim3((unsigned)n_win), dim3(kBlock),   \
+                               (size_t)xcap * sizeof(double), (hipStream_t)d.stream, d.n_rows, groups, gpw, \
+                               row_ptr, col, val, x, y, w, xcap, 0);                                        \
+        else                                                                                                \
+            hipLaunchKernelGGL((csr_xwin_kernel<LL, R, false, float>), dim3((unsigned)n_win), dim3(kBlock),  \
+                               (size_t)xcap * sizeof(double), (hipStream_t)d.stream, d.n_rows, groups, gpw, \
+                               row_ptr, col, val, x, y, w, xcap, 0);                                        \
+    } while (0)
+    switch (L) {
+    case 2: SPMV_XWIN32(2); break;
+    case 4: SPMV_XWIN32(4); break;
+    case 8: SPMV_XWIN32(8); break;
+    case 16: SPMV_XWIN32(16); break;
+    case 32: SPMV_XWIN32(32); break;
+    default: SPMV_XWIN32(64); break;
+    }
+#undef SPMV_XWIN32
+    SPMV_CHECK_LAUNCH("csr_xwin_kernel (fp32 values)");
+    return SPMV_SUCCESS;
 }

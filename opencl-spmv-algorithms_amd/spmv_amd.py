@@ -27,7 +27,8 @@ LIB_DIR = PKG_DIR / "lib"
 REPO_DIR = PKG_DIR.parent
 
 FORMATS = ("coo", "csr", "ell", "sell", "cmrs")  # the reference's five
-EXTRA_FORMATS = ("csr16", "hyb")  # §8f row 4: CSR with 16-bit column offsets; ELL + COO tail
+# §8f row 4: CSR with 16-bit column offsets; ELL + COO tail; CSR with fp32 values
+EXTRA_FORMATS = ("csr16", "hyb", "csrf32")
 ALL_FORMATS = FORMATS + EXTRA_FORMATS
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
@@ -84,6 +85,7 @@ HIP_SYMBOLS = {
     "spmv_csr_tiled_ws_bytes": (ctypes.c_size_t, [_c_i64, _c_i64]),
     "spmv_csr_run_tiled": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t]),
     "spmv_csr_hot_ws_bytes": (ctypes.c_size_t, [_c_i64, _c_i64, _c_i64]),
+    "spmv_csr_f32v_run_xwin": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, ctypes.c_int, _c_i32, _vp, _c_i32]),
     "spmv_csr_run_tiled_hot": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, _c_i64, _vp, _vp, _vp,
                                               ctypes.c_size_t]),
     "spmv_csr_tiled_plan_len": (_c_i64, [_c_i64]),
@@ -576,6 +578,9 @@ class DeviceMatrix:
             else:
                 rc = lib.spmv_csr_run_variant(d, _ptr(a["row_ptr"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x),
                                               _ptr(y), p["lanes"], p.get("variant", 0))
+        elif self.fmt == "csrf32":
+            rc = lib.spmv_csr_f32v_run_xwin(d, _ptr(a["row_ptr"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
+                                            p["lanes"], p.get("xwin_rows", 0), _ptr(a["win"]), p["xcap"])
         elif self.fmt == "csr16":
             rc = lib.spmv_csr16_run(d, _ptr(a["row_ptr"]), _ptr(a["blk_base"]), _ptr(a["col_off"]),
                                     _ptr(a["col_esc"]), _ptr(a["val"]), _ptr(x), _ptr(y), p["lanes"])
@@ -816,6 +821,16 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
         elif xwin and variant in (0, 3):
             _csr_xwin(dm)
         dm.stored_bytes = 12 * m.nnz + 8 * (m.n_rows + 1)
+    elif fmt == "csrf32":
+        # fp32 values, fp64 products and sums (§8f row 4); the row-group x-window
+        # kernel, so power-law rows (the tiled CSR's case) are not applicable
+        if host_lib().spmv_csr_pick_variant(m.n_rows, _ptr(ptr)) == 4:
+            raise SpmvError(OTHER_ERROR, "csrf32", "skewed rows: use the entry-balanced CSR (variant 4)")
+        dm.params = dict(lanes=lanes, xwin_rows=xwin_rows)
+        dm.arrays = dict(row_ptr=_dev_tensor(ptr, device), col=_dev_tensor(col, device),
+                         val=_dev_tensor(val.astype(np.float32), device))
+        dm.stored_bytes = 8 * m.nnz + 8 * (m.n_rows + 1)
+        _csr_xwin(dm)
     elif fmt == "csr16":
         c = csr16_build(col)
         if csr16_max_escape is not None and c["n_esc"] > csr16_max_escape * max(c["n_blocks"], 1):

@@ -37,6 +37,8 @@ FMT_PARAMS = [
     ("csr", {"lanes": 2, "variant": 5}),
     ("csr", {"lanes": 64, "variant": 5}),
     ("csr16", {}),
+    ("csrf32", {}),
+    ("csrf32", {"lanes": 2}),
     ("csr16", {"lanes": 2}),
     ("csr16", {"lanes": 64}),
     ("ell", {"ki": 1}),
@@ -582,3 +584,37 @@ def test_csr_xwin_prefetch_bit_identical(torch_dev, monkeypatch, case):
         torch.cuda.synchronize()
         assert torch.equal(ys[0].view(torch.int64), ys[1].view(torch.int64))
         assert_parity(m, ys[1].cpu().numpy()[: m.n_rows], x.cpu().numpy())
+
+
+@pytest.mark.parametrize("case", ["cantlike", "ragged", "fixtures"])
+def test_csrf32_equals_csr_on_rounded_values(torch_dev, case):
+    """CSR with fp32 values widens each value before the fp64 product: y is
+    bit-identical to the fp64 CSR x-window kernel on the fp32-rounded
+    matrix, and within the 1e-6 criterion of the exact one."""
+    torch, dev = torch_dev
+    if case == "cantlike":
+        ms = [sa.gen_cantlike(0, copies=2)]
+    elif case == "ragged":
+        ms = [sa.gen_random(20_000, 50_000, 0, 2_000, seed=21)]
+    else:
+        ms = [sa.read_mtx(GOLDEN / f"{n}.mtx") for n in CASES]
+    for m in ms:
+        m32 = sa.Coo(m.n_rows, m.n_cols, m.row, m.col, m.val.astype(np.float32).astype(np.float64))
+        a = sa.to_device(m, "csrf32", dev)
+        b = sa.to_device(m32, "csr", dev, variant=3, xwin=True)
+        assert a.stored_bytes < b.stored_bytes
+        x = torch.from_numpy(np.random.default_rng(9).uniform(-1, 1, m.n_cols)).to(dev)
+        ya = torch.full((max(m.n_rows, 1),), float("nan"), dtype=torch.float64, device=dev)
+        yb = torch.full_like(ya, float("nan"))
+        a.run(x, ya)
+        b.run(x, yb)
+        torch.cuda.synchronize()
+        assert torch.equal(ya.view(torch.int64), yb.view(torch.int64))
+        assert_parity(m, ya.cpu().numpy()[: m.n_rows], x.cpu().numpy())
+
+
+def test_csrf32_refuses_skewed_rows(torch_dev):
+    torch, dev = torch_dev
+    m = sa.gen_rmat(1_000_000, 10_000_000, scale=20, seed=1)
+    with pytest.raises(sa.SpmvError):
+        sa.to_device(m, "csrf32", dev)

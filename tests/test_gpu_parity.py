@@ -602,7 +602,7 @@ def test_csrf32_equals_csr_on_rounded_values(torch_dev, case):
         m32 = sa.Coo(m.n_rows, m.n_cols, m.row, m.col, m.val.astype(np.float32).astype(np.float64))
         a = sa.to_device(m, "csrf32", dev)
         b = sa.to_device(m32, "csr", dev, variant=3, xwin=True)
-        assert a.stored_bytes < b.stored_bytes
+        assert a.stored_bytes < b.stored_bytes or m.nnz == 0
         x = torch.from_numpy(np.random.default_rng(9).uniform(-1, 1, m.n_cols)).to(dev)
         ya = torch.full((max(m.n_rows, 1),), float("nan"), dtype=torch.float64, device=dev)
         yb = torch.full_like(ya, float("nan"))

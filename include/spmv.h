@@ -114,6 +114,12 @@ int spmv_csr16_run(spmv_dims d, const int64_t *row_ptr, const int32_t *blk_base,
 int spmv_csr_f32v_run_xwin(spmv_dims d, const int64_t *row_ptr, const int32_t *col, const float *val,
                            const double *x, double *y, int lanes_per_row, int32_t rows_per_window,
                            const void *win, int32_t xcap);
+/* fp32 values on the entry-balanced CSR (skewed rows), with the hot-column
+ * table and tile plan of spmv_csr_run_tiled_hot (H = 0: no table).     */
+int spmv_csr_f32v_run_tiled_hot(spmv_dims d, const int64_t *row_ptr, const int32_t *col_hot,
+                                const float *val, const double *x, double *y, int64_t H,
+                                const int32_t *hot, const int32_t *own_lo_plan, void *ws,
+                                size_t ws_bytes);
 /* Entry-balanced CSR for skewed row lengths (power-law / R-MAT hubs):
  * every workgroup takes the same number of ENTRIES, whatever the rows; a
  * row that spans workgroups is finished by a deterministic carry pass (as

@@ -56,8 +56,9 @@ int launch_csr_tiled(const spmv_dims &d, const int64_t *row_ptr, const int32_t *
                      const double *val, const double *x, double *y, int32_t *own_lo,
                      int32_t *carry_row, double *carry_val);
 int64_t csr_tiled_tile();
+template <typename V>  // double or float values (instantiated in staged.hip)
 int launch_csr_tiled_hot(const spmv_dims &d, const int64_t *row_ptr, const int32_t *col,
-                         const double *val, const double *x, double *y, int64_t H, const int32_t *hot,
+                         const V *val, const double *x, double *y, int64_t H, const int32_t *hot,
                          double *xh, const int32_t *own_lo_plan, int32_t *own_lo, int32_t *carry_row,
                          double *carry_val);
 int launch_cmrs_tiled(const spmv_dims &d, int32_t h, int64_t n_strips, const int64_t *strip_ptr,
@@ -120,6 +121,29 @@ __device__ __forceinline__ int2 stream_load2(const int32_t *p)
 {
     const v2i32 v = stream_load<NT>(reinterpret_cast<const v2i32 *>(p));
     return int2{v.x, v.y};
+}
+
+// Value loads of the staged kernels: fp64 values, or fp32 values (CSR-f32,
+// SURVEY.md §8f row 4) widened to fp64 before the product.
+typedef float v2f32 __attribute__((ext_vector_type(2)));
+
+template <bool NT>
+__device__ __forceinline__ double2 vpair(const double *p)
+{
+    return stream_load2<NT>(p);
+}
+
+template <bool NT>
+__device__ __forceinline__ double2 vpair(const float *p)
+{
+    const v2f32 v = stream_load<NT>(reinterpret_cast<const v2f32 *>(p));
+    return double2{(double)v.x, (double)v.y};
+}
+
+template <bool NT, typename V>
+__device__ __forceinline__ double vone(const V *p)
+{
+    return (double)stream_load<NT>(p);
 }
 
 // Load-policy switch for the streamed arrays: SPMV_STREAM_NT=1 / 0 forces

@@ -269,29 +269,6 @@ __device__ __forceinline__ double slice_sum(const double *prod, int64_t lo64, in
     return a0 + a1;
 }
 
-// Value loads of the staged kernels: fp64 values, or fp32 values (CSR-f32v,
-// SURVEY.md §8f row 4) widened to fp64 before the product.
-typedef float v2f32 __attribute__((ext_vector_type(2)));
-
-template <bool NT>
-__device__ __forceinline__ double2 vpair(const double *p)
-{
-    return stream_load2<NT>(p);
-}
-
-template <bool NT>
-__device__ __forceinline__ double2 vpair(const float *p)
-{
-    const v2f32 v = stream_load<NT>(reinterpret_cast<const v2f32 *>(p));
-    return double2{(double)v.x, (double)v.y};
-}
-
-template <bool NT, typename V>
-__device__ __forceinline__ double vone(const V *p)
-{
-    return (double)stream_load<NT>(p);
-}
-
 template <int L, int R, bool NT, typename Cols = Col32<NT>, int BATCH = 0, typename XS = XGlobal,
           typename V = double>
 __device__ __forceinline__ void staged_group(
@@ -1248,4 +1225,38 @@ extern "C" int spmv_csr_f32v_run_xwin(spmv_dims d, const int64_t *row_ptr, const
 #undef SPMV_XWIN32
     SPMV_CHECK_LAUNCH("csr_xwin_kernel (fp32 values)");
     return SPMV_SUCCESS;
+}
+
+// fp32 values, entry-balanced tiles (+ hot-column table, build-once tile
+// plan), as spmv_csr_run_tiled_hot: bit-identical to it on the fp32-rounded
+// values.  own_lo_plan from spmv_csr_tiled_plan, or NULL.
+extern "C" int spmv_csr_f32v_run_tiled_hot(spmv_dims d, const int64_t *row_ptr, const int32_t *col_hot,
+                                           const float *val, const double *x, double *y, int64_t H,
+                                           const int32_t *hot, const int32_t *own_lo_plan, void *ws,
+                                           size_t ws_bytes)
+{
+    if (d.n_rows < 0 || d.n_cols < 0 || d.nnz < 0 || d.n_rows > INT32_MAX || H < 0 ||
+        d.n_cols + H > INT32_MAX)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_f32v_run_tiled_hot: bad sizes");
+    if (d.n_rows == 0)
+        return SPMV_SUCCESS;
+    SPMV_GUARD(d);
+    if (d.nnz == 0) {
+        hipError_t e = hipMemsetAsync(y, 0, (size_t)d.n_rows * sizeof(double), (hipStream_t)d.stream);
+        return e == hipSuccess ? SPMV_SUCCESS : fail(SPMV_PROGRAM_ERROR, "memset y", e);
+    }
+    if ((H > 0 && !hot) || !ws || ws_bytes < spmv_csr_hot_ws_bytes(d.n_rows, d.nnz, H))
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_f32v_run_tiled_hot: hot list or workspace missing");
+    const int64_t tiles = (d.nnz + csr_tiled_tile() - 1) / csr_tiled_tile();
+    if (tiles > INT32_MAX)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_f32v_run_tiled_hot: grid too large");
+    double *xh = (double *)ws;
+    double *carry_val = xh + H;
+    int32_t *own_lo = (int32_t *)(carry_val + tiles);
+    int32_t *carry_row = own_lo + tiles + 1;
+    int rc = launch_csr_tiled_hot(d, row_ptr, col_hot, val, x, y, H, hot, xh, own_lo_plan, own_lo, carry_row,
+                                  carry_val);
+    if (rc != SPMV_SUCCESS)
+        return rc;
+    return launch_carry(tiles, carry_row, carry_val, y, (hipStream_t)d.stream);
 }

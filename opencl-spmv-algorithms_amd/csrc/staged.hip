@@ -41,9 +41,9 @@ __device__ __forceinline__ int lower_bound_lds(const K *keys, int lo, int hi, in
 // is read.
 // NT: non-temporal stream loads (the skewed-matrix kernels: x, gathered
 // from a vector far larger than L2, keeps the cache).
-template <int R, bool NT = false, typename XS, typename KeyFn>
+template <int R, bool NT = false, typename XS, typename KeyFn, typename V>
 __device__ __forceinline__ void stage_chunk(int64_t cb, int64_t ce, const int32_t *__restrict__ col,
-                                            const double *__restrict__ val, const XS &xs,
+                                            const V *__restrict__ val, const XS &xs,
                                             double2 *s_prod, KeyFn key)
 {
 #pragma unroll
@@ -52,13 +52,13 @@ __device__ __forceinline__ void stage_chunk(int64_t cb, int64_t ce, const int32_
         const int64_t p = cb + 2 * (int64_t)t;
         double2 pr = {0.0, 0.0};
         if (p + 1 < ce) {
-            const double2 v = stream_load2<NT>(val + p);
+            const double2 v = vpair<NT>(val + p);
             const int2 c = stream_load2<NT>(col + p);
             pr.x = v.x * xs(c.x);
             pr.y = v.y * xs(c.y);
             key(t, p, 2);
         } else if (p < ce) {
-            pr.x = stream_load<NT>(val + p) * xs(stream_load<NT>(col + p));
+            pr.x = vone<NT>(val + p) * xs(stream_load<NT>(col + p));
             key(t, p, 1);
         }
         s_prod[t] = pr;
@@ -319,10 +319,10 @@ __global__ __launch_bounds__(kBlock) void csr_tile_rows_kernel(int64_t n_rows, i
 // on R-MAT (tools/rmat_exp.hip mode 2).
 constexpr int kTiledRowCap = 1024;
 
-template <int L, int R, bool NT, typename XS>
+template <int L, int R, bool NT, typename XS, typename V = double>
 __global__ __launch_bounds__(kBlock) void csr_tiled_kernel(
     int64_t n_rows, int64_t nnz, const int64_t *__restrict__ row_ptr,
-    const int32_t *__restrict__ col, const double *__restrict__ val,
+    const int32_t *__restrict__ col, const V *__restrict__ val,
     const XS xs, double *__restrict__ y,
     const int32_t *__restrict__ own_lo, int32_t *__restrict__ carry_row,
     double *__restrict__ carry_val)
@@ -525,9 +525,9 @@ int launch_cmrs_tiled(const spmv_dims &d, int32_t h, int64_t n_strips, const int
 
 int64_t csr_tiled_tile() { return 2 * kBlock * 3; }
 
-template <typename XS>
+template <typename XS, typename V>
 static void launch_tiled_xs(const spmv_dims &d, int64_t tiles, const int64_t *row_ptr, const int32_t *col,
-                            const double *val, XS xs, double *y, const int32_t *own_lo, int32_t *carry_row,
+                            const V *val, XS xs, double *y, const int32_t *own_lo, int32_t *carry_row,
                             double *carry_val)
 {
     constexpr int R = 3;
@@ -537,10 +537,10 @@ static void launch_tiled_xs(const spmv_dims &d, int64_t tiles, const int64_t *ro
 #define SPMV_TILED(LL)                                                                                    \
     do {                                                                                                  \
         if (nt)                                                                                           \
-            hipLaunchKernelGGL((csr_tiled_kernel<LL, R, true, XS>), dim3((unsigned)tiles), dim3(kBlock), 0, \
+            hipLaunchKernelGGL((csr_tiled_kernel<LL, R, true, XS, V>), dim3((unsigned)tiles), dim3(kBlock), 0, \
                                st, d.n_rows, d.nnz, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val); \
         else                                                                                              \
-            hipLaunchKernelGGL((csr_tiled_kernel<LL, R, false, XS>), dim3((unsigned)tiles), dim3(kBlock),  \
+            hipLaunchKernelGGL((csr_tiled_kernel<LL, R, false, XS, V>), dim3((unsigned)tiles), dim3(kBlock),  \
                                0, st, d.n_rows, d.nnz, row_ptr, col, val, xs, y, own_lo, carry_row,        \
                                carry_val);                                                                \
     } while (0)
@@ -570,8 +570,9 @@ int launch_csr_tiled(const spmv_dims &d, const int64_t *row_ptr, const int32_t *
     return SPMV_SUCCESS;
 }
 
+template <typename V>
 int launch_csr_tiled_hot(const spmv_dims &d, const int64_t *row_ptr, const int32_t *col,
-                         const double *val, const double *x, double *y, int64_t H, const int32_t *hot,
+                         const V *val, const double *x, double *y, int64_t H, const int32_t *hot,
                          double *xh, const int32_t *own_lo_plan, int32_t *own_lo, int32_t *carry_row,
                          double *carry_val)
 {
@@ -593,6 +594,13 @@ int launch_csr_tiled_hot(const spmv_dims &d, const int64_t *row_ptr, const int32
     SPMV_CHECK_LAUNCH("csr_tiled_kernel (hot columns)");
     return SPMV_SUCCESS;
 }
+
+template int launch_csr_tiled_hot<double>(const spmv_dims &, const int64_t *, const int32_t *, const double *,
+                                          const double *, double *, int64_t, const int32_t *, double *,
+                                          const int32_t *, int32_t *, int32_t *, double *);
+template int launch_csr_tiled_hot<float>(const spmv_dims &, const int64_t *, const int32_t *, const float *,
+                                         const double *, double *, int64_t, const int32_t *, double *,
+                                         const int32_t *, int32_t *, int32_t *, double *);
 
 // ----------------------------------------------------------- launchers
 // Geometry of the strip-run CMRS kernel: lanes per row as the staged CSR

@@ -86,6 +86,8 @@ HIP_SYMBOLS = {
     "spmv_csr_run_tiled": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t]),
     "spmv_csr_hot_ws_bytes": (ctypes.c_size_t, [_c_i64, _c_i64, _c_i64]),
     "spmv_csr_f32v_run_xwin": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, ctypes.c_int, _c_i32, _vp, _c_i32]),
+    "spmv_csr_f32v_run_tiled_hot": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, _c_i64, _vp, _vp, _vp,
+                                                   ctypes.c_size_t]),
     "spmv_csr_run_tiled_hot": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, _c_i64, _vp, _vp, _vp,
                                               ctypes.c_size_t]),
     "spmv_csr_tiled_plan_len": (_c_i64, [_c_i64]),
@@ -578,6 +580,10 @@ class DeviceMatrix:
             else:
                 rc = lib.spmv_csr_run_variant(d, _ptr(a["row_ptr"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x),
                                               _ptr(y), p["lanes"], p.get("variant", 0))
+        elif self.fmt == "csrf32" and p.get("variant") == 4:
+            rc = lib.spmv_csr_f32v_run_tiled_hot(d, _ptr(a["row_ptr"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x),
+                                                 _ptr(y), p["H"], _ptr(a.get("hot")), _ptr(a.get("own_lo")),
+                                                 _ptr(a["ws"]), a["ws"].numel())
         elif self.fmt == "csrf32":
             rc = lib.spmv_csr_f32v_run_xwin(d, _ptr(a["row_ptr"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
                                             p["lanes"], p.get("xwin_rows", 0), _ptr(a["win"]), p["xcap"])
@@ -822,15 +828,28 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
             _csr_xwin(dm)
         dm.stored_bytes = 12 * m.nnz + 8 * (m.n_rows + 1)
     elif fmt == "csrf32":
-        # fp32 values, fp64 products and sums (§8f row 4); the row-group x-window
-        # kernel, so power-law rows (the tiled CSR's case) are not applicable
-        if host_lib().spmv_csr_pick_variant(m.n_rows, _ptr(ptr)) == 4:
-            raise SpmvError(OTHER_ERROR, "csrf32", "skewed rows: use the entry-balanced CSR (variant 4)")
-        dm.params = dict(lanes=lanes, xwin_rows=xwin_rows)
+        # fp32 values, fp64 products and sums (§8f row 4): the row-group x-window
+        # kernel, or for skewed rows the entry-balanced one with the hot table
+        v = variant or host_lib().spmv_csr_pick_variant(m.n_rows, _ptr(ptr))
+        dm.params = dict(lanes=lanes, xwin_rows=xwin_rows, variant=4 if v == 4 else 3, H=0)
         dm.arrays = dict(row_ptr=_dev_tensor(ptr, device), col=_dev_tensor(col, device),
                          val=_dev_tensor(val.astype(np.float32), device))
         dm.stored_bytes = 8 * m.nnz + 8 * (m.n_rows + 1)
-        _csr_xwin(dm)
+        if v == 4:
+            H, hot_cols, col_hot = hot_columns(m.n_cols, col, 0 if hot is None else hot) if hot != 0 else (0, None, col)
+            dm.params["H"] = H
+            if H > 0:
+                dm.arrays["col"] = _dev_tensor(col_hot, device)
+                dm.arrays["hot"] = _dev_tensor(hot_cols, device)
+            dm.arrays["ws"] = torch.empty(hip_lib().spmv_csr_hot_ws_bytes(m.n_rows, m.nnz, H), dtype=torch.uint8,
+                                          device=device)
+            n_plan = hip_lib().spmv_csr_tiled_plan_len(m.nnz)
+            if n_plan > 0:
+                dm.arrays["own_lo"] = torch.empty(n_plan, dtype=torch.int32, device=device)
+                _check(hip_lib().spmv_csr_tiled_plan(dm.dims(), _ptr(dm.arrays["row_ptr"]), _ptr(dm.arrays["own_lo"])),
+                       "spmv_csr_tiled_plan")
+        else:
+            _csr_xwin(dm)
     elif fmt == "csr16":
         c = csr16_build(col)
         if csr16_max_escape is not None and c["n_esc"] > csr16_max_escape * max(c["n_blocks"], 1):

@@ -613,8 +613,22 @@ def test_csrf32_equals_csr_on_rounded_values(torch_dev, case):
         assert_parity(m, ya.cpu().numpy()[: m.n_rows], x.cpu().numpy())
 
 
-def test_csrf32_refuses_skewed_rows(torch_dev):
+@pytest.mark.parametrize("H", [0, 4096])
+def test_csrf32_tiled_on_skewed_rows(torch_dev, H):
+    """Skewed rows: the fp32-value CSR runs the entry-balanced kernel (with
+    or without the hot table) and equals the fp64 tiled CSR on the rounded
+    values bit for bit."""
     torch, dev = torch_dev
     m = sa.gen_rmat(1_000_000, 10_000_000, scale=20, seed=1)
-    with pytest.raises(sa.SpmvError):
-        sa.to_device(m, "csrf32", dev)
+    m32 = sa.Coo(m.n_rows, m.n_cols, m.row, m.col, m.val.astype(np.float32).astype(np.float64))
+    a = sa.to_device(m, "csrf32", dev, hot=H)
+    b = sa.to_device(m32, "csr", dev, variant=4, hot=H)
+    assert a.params["variant"] == 4 and a.params["H"] == H
+    x = torch.from_numpy(np.random.default_rng(10).uniform(-1, 1, m.n_cols)).to(dev)
+    ya = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
+    yb = torch.full_like(ya, float("nan"))
+    a.run(x, ya)
+    b.run(x, yb)
+    torch.cuda.synchronize()
+    assert torch.equal(ya.view(torch.int64), yb.view(torch.int64))
+    assert_parity(m, ya.cpu().numpy(), x.cpu().numpy())

@@ -63,6 +63,7 @@ for s in "${steps[@]}"; do
     sweephyb) run sweep_hyb_rmat 600 python tools/sweep.py --matrix rmat --rounds 2 --reps 10 --only hyb &&
               run sweep_hyb_cant 600 python tools/sweep.py --rounds 2 --only hyb;;
     testf32) run gpu_tests_f32 600 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "csrf32 or bitwise";;
+    rehearse2r) run rehearse2_rmat 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --backend gloo --share-gpu --workload rmat --steps 10;;
     rehearse2) run rehearse2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --backend gloo --share-gpu --steps 20;;
     drivers) run drivers 600 python -m pytest tests/test_drivers_gpu.py -q;;
     sweepremap) SPMV_XCD_REMAP=1 run sweep_remap 600 python tools/sweep.py --rounds 2 --only csr,sell,ell;;

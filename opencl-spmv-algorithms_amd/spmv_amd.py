@@ -227,7 +227,7 @@ def hip_lib() -> ctypes.CDLL:
     """libspmv_hip.so — raises if it was not built (no CPU fallback)."""
     global _hip
     if _hip is None:
-        path = LIB_DIR / "libspmv_hip.so"
+        path = Path(os.environ.get("SPMV_HIP_LIB", LIB_DIR / "libspmv_hip.so"))  # override: A/B runs
         if not path.exists():
             raise SpmvError(PROGRAM_ERROR, "load libspmv_hip.so", f"{path} missing: run `make lib`")
         _hip = _bind(ctypes.CDLL(str(path), mode=ctypes.RTLD_GLOBAL), HIP_SYMBOLS)

@@ -528,6 +528,57 @@ def test_csr_hot_bit_identical(torch_dev, H):
     assert_parity(m, ya.cpu().numpy(), x.cpu().numpy())
 
 
+def _empty_run_matrix(seed=11):
+    """Nonempty rows scattered among long runs of empty rows (a tile of the
+    tiled CSR kernel then owns thousands of rows), one 20000-entry row that
+    runs over several tiles right after an empty run, trailing empty rows."""
+    rng = np.random.default_rng(seed)
+    n, nc = 400_000, 50_000
+    rows = np.sort(rng.choice(np.arange(1, n - 5000), 4000, replace=False))
+    lens = rng.integers(2, 20, rows.size)
+    lens[rows.size // 2] = 20_000
+    r = np.repeat(rows, lens).astype(np.int32)
+    c = rng.integers(0, nc, r.size).astype(np.int32)
+    v = rng.uniform(-1, 1, r.size)
+    return sa.Coo(n, nc, r, c, v), rows
+
+
+@pytest.mark.parametrize("H", [0, 1024])
+def test_csr_tiled_empty_row_runs(torch_dev, H):
+    """Rows a tile owns past its LDS table go to the sweep blocks: the same
+    bits as the compacted matrix (3 empty rows after each nonempty one, so
+    the same lanes per row and every row staged by its tile: the same
+    entries in the same tiles), zeros for empty rows."""
+    torch, dev = torch_dev
+    m, rows = _empty_run_matrix()
+    inv = np.zeros(m.n_rows, np.int32)
+    inv[rows] = 4 * np.arange(rows.size, dtype=np.int32)
+    mc = sa.Coo(4 * rows.size, m.n_cols, inv[m.row], m.col, m.val)
+    x = torch.from_numpy(np.random.default_rng(3).uniform(-1, 1, m.n_cols)).to(dev)
+    a = sa.to_device(m, "csr", dev, variant=4, hot=H)
+    c = sa.to_device(mc, "csr", dev, variant=4, hot=H)
+    ya = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
+    yc = torch.full((mc.n_rows,), float("nan"), dtype=torch.float64, device=dev)
+    a.run(x, ya)
+    c.run(x, yc)
+    yp = torch.full_like(ya, float("nan"))
+    if H == 0:  # and without the build-once tile plan
+        aa = a.arrays
+        rc = sa.hip_lib().spmv_csr_run_tiled(a.dims(), sa._ptr(aa["row_ptr"]), sa._ptr(aa["col"]),
+                                             sa._ptr(aa["val"]), sa._ptr(x), sa._ptr(yp), sa._ptr(aa["ws"]),
+                                             aa["ws"].numel())
+        assert rc == 0
+    torch.cuda.synchronize()
+    idx = torch.from_numpy(rows.astype(np.int64)).to(dev)
+    assert torch.equal(ya[idx].view(torch.int64), yc[::4].view(torch.int64))
+    mask = torch.ones(m.n_rows, dtype=torch.bool, device=dev)
+    mask[idx] = False
+    assert bool((ya[mask] == 0).all())
+    if H == 0:
+        assert torch.equal(yp.view(torch.int64), ya.view(torch.int64))
+    assert_parity(m, ya.cpu().numpy(), x.cpu().numpy())
+
+
 @pytest.mark.parametrize("fmt,kw", [("coo", {}), ("cmrs", {"cmrs_variant": 1}), ("cmrs", {"cmrs_variant": 1, "h": 32}),
                                     ("sell", {"xwin": False}), ("sell", {"sigma": 1 << 24, "ki": 2, "xwin": False}),
                                     ("sell", {"split": 0, "xwin": False}), ("hyb", {}), ("hyb", {"ki": 1})])

@@ -48,6 +48,16 @@ for s in "${steps[@]}"; do
     rehearsew2) run shard_rehearse_w2 900 python tools/shard_rehearse.py --gpus 8 --row-weights 4,6,8;;
     rehearseh) run shard_rehearse_h17 600 python tools/shard_rehearse.py --gpus 8 --row-weights 4 --hot 131072 &&
                run shard_rehearse_h18 600 python tools/shard_rehearse.py --gpus 8 --row-weights 4 --hot 262144;;
+    rehearse18) run shard_rehearse_18 900 python tools/shard_rehearse.py --gpus 1,8;;
+    testempty) run gpu_tests_empty 600 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "empty_row_runs or csr_hot";;
+    profreh8) run prof_rehearse8 900 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/prof_reh8 -o run -- python3 tools/shard_rehearse.py --gpus 8;;
+    abreh) SPMV_HIP_LIB=$PWD/tools/ab/libspmv_hip_head.so run reh_head 600 python tools/shard_rehearse.py --gpus 1,8 &&
+           run reh_new 600 python tools/shard_rehearse.py --gpus 1,8 &&
+           SPMV_HIP_LIB=$PWD/tools/ab/libspmv_hip_head.so run reh_head2 600 python tools/shard_rehearse.py --gpus 1,8 &&
+           run reh_new2 600 python tools/shard_rehearse.py --gpus 1,8;;
+    abcmrs) SPMV_HIP_LIB=$PWD/tools/ab/libspmv_hip_head.so run cmrs_head 600 python tools/shard_rehearse.py --gpus 1,8 --format cmrs &&
+            run cmrs_new 600 python tools/shard_rehearse.py --gpus 1,8 --format cmrs;;
+    rehearsec) run shard_rehearse_cmrs 900 python tools/shard_rehearse.py --gpus 1,8 --format cmrs;;
     rehearseg) run shard_rehearse_graph 900 python tools/shard_rehearse.py --gpus 1,8 --row-weights 4 --graph;;
     profrmat) run prof_rmat 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_rmat -o run -- python3 bench.py --workload rmat --profile --steps 50;;
     testhot) run gpu_tests_hot 900 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "hot or rmat_skewed or bitwise or split";;

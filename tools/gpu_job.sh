@@ -57,6 +57,15 @@ for s in "${steps[@]}"; do
            run reh_new2 600 python tools/shard_rehearse.py --gpus 1,8;;
     abcmrs) SPMV_HIP_LIB=$PWD/tools/ab/libspmv_hip_head.so run cmrs_head 600 python tools/shard_rehearse.py --gpus 1,8 --format cmrs &&
             run cmrs_new 600 python tools/shard_rehearse.py --gpus 1,8 --format cmrs;;
+    coont) run coo_base 300 python bench.py --format coo --per-format no --cpu-seconds 0 &&
+           SPMV_STREAM_NT=1 run coo_nt 300 python bench.py --format coo --per-format no --cpu-seconds 0 &&
+           run coo_base2 300 python bench.py --format coo --per-format no --cpu-seconds 0 &&
+           SPMV_STREAM_NT=1 run coo_nt2 300 python bench.py --format coo --per-format no --cpu-seconds 0;;
+    cmrsnt) run cmrs_base 300 python bench.py --format cmrs --per-format no --cpu-seconds 0 &&
+            SPMV_STREAM_NT=1 run cmrs_nt 300 python bench.py --format cmrs --per-format no --cpu-seconds 0 &&
+            run cmrs_base2 300 python bench.py --format cmrs --per-format no --cpu-seconds 0 &&
+            SPMV_STREAM_NT=1 run cmrs_nt2 300 python bench.py --format cmrs --per-format no --cpu-seconds 0 &&
+            run coo_ntdef 300 python bench.py --format coo --per-format no --cpu-seconds 0;;
     rehearsec) run shard_rehearse_cmrs 900 python tools/shard_rehearse.py --gpus 1,8 --format cmrs;;
     rehearseg) run shard_rehearse_graph 900 python tools/shard_rehearse.py --gpus 1,8 --row-weights 4 --graph;;
     profrmat) run prof_rmat 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_rmat -o run -- python3 bench.py --workload rmat --profile --steps 50;;

@@ -142,6 +142,11 @@ __global__ __launch_bounds__(kBlock) void cmrs_staged_kernel(
 
 // ------------------------------------------------------------------- COO
 constexpr int kCooRowCap = 1024;
+// entry pairs staged per thread by the COO kernels (tile = 2·256·kCooR entries)
+#ifndef SPMV_COO_R
+#define SPMV_COO_R 3
+#endif
+constexpr int kCooR = SPMV_COO_R;
 
 // A workgroup owns one tile of CH consecutive row-sorted entries and
 // writes y for rows (row[t0-1], row[t1-1]] (rows without entries get 0;
@@ -659,13 +664,13 @@ int launch_cmrs_staged(const spmv_dims &d, int32_t h, int64_t n_strips,
     return SPMV_SUCCESS;
 }
 
-int64_t coo_staged_tile() { return 2 * kBlock * 3; }
+int64_t coo_staged_tile() { return 2 * kBlock * kCooR; }
 
 int launch_coo_staged_acc(const spmv_dims &d, const int32_t *row, const int32_t *col,
                           const double *val, const double *x, double *y, int32_t *carry_row,
                           double *carry_val)
 {
-    constexpr int R = 3;
+    constexpr int R = kCooR;
     const int64_t tiles = (d.nnz + coo_staged_tile() - 1) / coo_staged_tile();
     if (tiles > INT32_MAX)
         return fail_msg(SPMV_OTHER_ERROR, "coo tail: grid too large");
@@ -682,7 +687,7 @@ int launch_coo_staged_acc_hot(const spmv_dims &d, const int32_t *row, const int3
                               const double *val, const double *x, double *y, int32_t *carry_row,
                               double *carry_val, const XHot xs)
 {
-    constexpr int R = 3;
+    constexpr int R = kCooR;
     const int64_t tiles = (d.nnz + coo_staged_tile() - 1) / coo_staged_tile();
     if (tiles > INT32_MAX)
         return fail_msg(SPMV_OTHER_ERROR, "hyb tail: grid too large");
@@ -699,7 +704,7 @@ int launch_coo_staged(const spmv_dims &d, const int32_t *row, const int32_t *col
                       const double *val, const double *x, double *y, int32_t *carry_row,
                       double *carry_val, const int2 *win, int32_t xcap)
 {
-    constexpr int R = 3;
+    constexpr int R = kCooR;
     const int64_t tiles = (d.nnz + coo_staged_tile() - 1) / coo_staged_tile();
     if (tiles > INT32_MAX)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_coo_run: grid too large");
@@ -740,7 +745,7 @@ int launch_coo_staged_hot(const spmv_dims &d, const int32_t *row, const int32_t 
                           const double *x, double *y, int32_t *carry_row, double *carry_val, int64_t H,
                           const int32_t *hot, double *xh)
 {
-    constexpr int R = 3;
+    constexpr int R = kCooR;
     const int64_t tiles = (d.nnz + coo_staged_tile() - 1) / coo_staged_tile();
     if (tiles > INT32_MAX)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_coo_run_hot: grid too large");

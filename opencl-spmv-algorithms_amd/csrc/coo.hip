@@ -269,7 +269,10 @@ using namespace spmv;
 
 extern "C" size_t spmv_coo_ws_bytes(int64_t nnz)
 {
-    const int64_t tiles = nnz > 0 ? (nnz + kTile - 1) / kTile : 0;
+    // the wave kernel's kTile and the staged kernels' tile share this
+    // workspace: size it for the smaller tile (more tiles)
+    const int64_t t = kTile < coo_staged_tile() ? kTile : coo_staged_tile();
+    const int64_t tiles = nnz > 0 ? (nnz + t - 1) / t : 0;
     // carry_val (8-byte aligned) first, then carry_row
     return (size_t)(tiles * (int64_t)sizeof(double) + tiles * (int64_t)sizeof(int32_t) + 16);
 }
@@ -292,7 +295,7 @@ extern "C" int spmv_coo_run(spmv_dims d, const int32_t *row,
     if (!ws || ws_bytes < spmv_coo_ws_bytes(d.nnz))
         return fail_msg(SPMV_OTHER_ERROR, "spmv_coo_run: workspace too small");
     if (staged_variant("SPMV_COO_VARIANT")) {
-        // staged tiles are larger than kTile, so the workspace suffices
+        // spmv_coo_ws_bytes counts the smaller of the two tiles
         const int64_t st_tiles = (d.nnz + coo_staged_tile() - 1) / coo_staged_tile();
         double *cv = (double *)ws;
         int32_t *cr = (int32_t *)(cv + st_tiles);

@@ -147,6 +147,9 @@ constexpr int kCooRowCap = 1024;
 #define SPMV_COO_R 3
 #endif
 constexpr int kCooR = SPMV_COO_R;
+// the tile must hold at least one pair per thread; spmv_coo_ws_bytes sizes
+// the carry arrays from the smaller of this tile and coo.hip's kTile
+static_assert(kCooR >= 1 && kCooR <= 8, "SPMV_COO_R must be in [1, 8]");
 
 // A workgroup owns one tile of CH consecutive row-sorted entries and
 // writes y for rows (row[t0-1], row[t1-1]] (rows without entries get 0;
@@ -712,7 +715,10 @@ int launch_coo_staged(const spmv_dims &d, const int32_t *row, const int32_t *col
     const size_t lds = win ? (size_t)xcap * sizeof(double) : 0;
     // rows per tile ~ tile / mean row length; 4 lanes per row unless rows are long
     const double mean = d.n_rows > 0 ? (double)d.nnz / (double)d.n_rows : 0.0;
-    const bool nt = stream_nt(true);  // +2 % on the cant batch (0.434 vs 0.443 ms)
+    // non-temporal stream loads: 0.4451 vs 0.4570 ms on the cant batch
+    // (SPMV_STREAM_NT=0), three interleaved pairs on one box,
+    // profiles/round2/ab_coo_nt.log
+    const bool nt = stream_nt(true);
 #define SPMV_COO_STAGED(LL)                                                                              \
     do {                                                                                                 \
         if (win)                                                                                         \

@@ -557,6 +557,15 @@ class DeviceMatrix:
             raise SpmvError(OTHER_ERROR, "run", "x and y must be float64")
         if x.numel() < self.n_cols or y.numel() < self.n_rows:
             raise SpmvError(OTHER_ERROR, "run", "x or y too short")
+        # raw data_ptr()s go to the C-ABI: a strided view or a tensor on
+        # another device would give a wrong y or a GPU fault
+        if not (x.is_contiguous() and y.is_contiguous()):
+            raise SpmvError(OTHER_ERROR, "run", "x and y must be contiguous")
+        here = _torch().device(self.device)
+        idx = here.index or 0  # the device dims() passes to the C-ABI
+        for t in (x, y):
+            if t.device.type != here.type or (t.device.index or 0) != idx:
+                raise SpmvError(OTHER_ERROR, "run", f"x and y must be on {here.type}:{idx}")
         if self.fmt == "coo" and p.get("H", 0) > 0:
             rc = lib.spmv_coo_run_hot(d, _ptr(a["row"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y), p["H"],
                                       _ptr(a["hot"]), _ptr(a["ws"]), a["ws"].numel())

@@ -545,7 +545,8 @@ def _empty_run_matrix(seed=11):
 
 @pytest.mark.parametrize("H", [0, 1024])
 def test_csr_tiled_empty_row_runs(torch_dev, H):
-    """Rows a tile owns past its LDS table go to the sweep blocks: the same
+    """Rows a tile owns past its 1024-entry LDS offset table read row_ptr
+    from global memory instead (csr_tiled_kernel, rp_lds false): the same
     bits as the compacted matrix (3 empty rows after each nonempty one, so
     the same lanes per row and every row staged by its tile: the same
     entries in the same tiles), zeros for empty rows."""

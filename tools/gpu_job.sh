@@ -61,6 +61,12 @@ for s in "${steps[@]}"; do
            SPMV_STREAM_NT=1 run coo_nt 300 python bench.py --format coo --per-format no --cpu-seconds 0 &&
            run coo_base2 300 python bench.py --format coo --per-format no --cpu-seconds 0 &&
            SPMV_STREAM_NT=1 run coo_nt2 300 python bench.py --format coo --per-format no --cpu-seconds 0;;
+    abcoo) # interleaved on one box: library before NT COO loads vs current (NT on / off)
+           for i in 1 2 3; do
+             SPMV_HIP_LIB=$PWD/tools/ab/libspmv_hip_prev.so run coo_prev$i 300 python bench.py --format coo --per-format no --cpu-seconds 0 &&
+             run coo_cur_nt$i 300 python bench.py --format coo --per-format no --cpu-seconds 0 &&
+             SPMV_STREAM_NT=0 run coo_cur_nt0_$i 300 python bench.py --format coo --per-format no --cpu-seconds 0
+           done;;
     cmrsnt) run cmrs_base 300 python bench.py --format cmrs --per-format no --cpu-seconds 0 &&
             SPMV_STREAM_NT=1 run cmrs_nt 300 python bench.py --format cmrs --per-format no --cpu-seconds 0 &&
             run cmrs_base2 300 python bench.py --format cmrs --per-format no --cpu-seconds 0 &&

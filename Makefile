@@ -40,9 +40,16 @@ all: lib $(TARGETS)
 
 lib: $(LIB_HIP) $(LIB_HOST)
 
-$(LIB_HIP): $(HIP_SRC) $(HIP_HDR)
+# one object per .hip (parallel with make -j), linked into one library
+HIP_OBJ  := $(patsubst $(PKG)/csrc/%.hip,build/hip/%.o,$(HIP_SRC))
+
+build/hip/%.o: $(PKG)/csrc/%.hip $(HIP_HDR)
+	@mkdir -p build/hip
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB_HIP): $(HIP_OBJ)
 	@mkdir -p $(LIBDIR)
-	$(HIPCC) $(HIPFLAGS) -shared $(HIP_SRC) -o $@
+	$(HIPCC) $(HIPFLAGS) -shared $(HIP_OBJ) -o $@
 
 $(LIB_HOST): $(HOST_SRC) include/spmv_host.h include/spmv_rc.h
 	@mkdir -p $(LIBDIR)
@@ -68,4 +75,4 @@ test-gpu: all oracle
 	python -m pytest tests/ -x -q -m gpu
 
 clean:
-	$(RM) -r $(BINDIR) $(LIBDIR) $(ORACLE)
+	$(RM) -r $(BINDIR) $(LIBDIR) $(ORACLE) build

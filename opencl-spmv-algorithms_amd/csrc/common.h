@@ -32,8 +32,9 @@ class DeviceGuard {
 // XCD-contiguous blockIdx remap switch (SPMV_XCD_REMAP=1 enables; read once).
 bool xcd_remap_enabled();
 // XCD-contiguous window placement of the CSR / SELL x-window kernels:
-// SPMV_XWIN_REMAP=1 (read on every call, so a sweep can flip it).
-bool xwin_remap();
+// SPMV_XWIN_REMAP=1 / 0 forces it (read on every call, so a sweep can flip
+// it), otherwise `dflt` (each kernel's measured best).
+bool xwin_remap(bool dflt);
 
 // LDS-staged CMRS / COO launchers (staged.hip)
 // win != nullptr: the x-window kernels (win/xcap from *_xwin_build)
@@ -163,6 +164,29 @@ struct XWindow {
     int32_t lo;
     __device__ __forceinline__ double operator()(int32_t c) const { return s[c - lo]; }
 };
+
+// Copies x[lo .. lo+span) into LDS (s_x[0 .. span)) with U loads in flight
+// per thread: all U loads are issued before the first LDS store (a plain
+// strided loop waits out one L2/HBM round trip per T entries).  Lanes past
+// the window load its last entry again (same line, never stored).
+template <int T = kBlock, int U = 8>
+__device__ __forceinline__ void copy_window(double *s_x, const double *__restrict__ x, int32_t lo, int32_t span)
+{
+    for (int32_t b = 0; b < span; b += U * T) {
+        double v[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const int32_t i = b + (int32_t)threadIdx.x + k * T;
+            v[k] = x[lo + (i < span ? i : span - 1)];
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const int32_t i = b + (int32_t)threadIdx.x + k * T;
+            if (i < span)
+                s_x[i] = v[k];
+        }
+    }
+}
 
 // Hot-column CSR (spmv_csr_run_tiled_hot): ids >= M name the compact table
 // xh of the most frequent columns, gathered from x at the start of the run.

@@ -143,9 +143,11 @@ __global__ __launch_bounds__(kBlock) void csr_vector_xwin_kernel(
 // 1 across lanes) and reduces with the same shuffle butterfly.  Ranges
 // longer than the LDS chunk are processed in chunks; a row's partial sum
 // stays in its lanes' registers across chunks.
-constexpr int kStageRoundsDefault = 4;  // pairs per lane per chunk: 2048 products, 16 KiB
-// (16 KiB keeps 8 workgroups = 32 waves per CU; 20 KiB (R = 5) capped the
-// CU at 7 and measured slower, R = 8 at 4 and much slower)
+constexpr int kStageRoundsDefault = 3;  // pairs per lane per chunk: 1536 products, 12 KiB
+// (round 1, persistent kernel: R = 3 0.3008 ms, R = 4 0.3013, R = 5 and
+// R = 8 slower; round 2, x-window kernel MODE 3: R = 3 0.2591-0.2607 ms,
+// R = 4 0.2639-0.2642 — one default for every staged CSR kernel keeps
+// their chunk boundaries, hence their bits, identical)
 constexpr bool kCsrStreamNtDefault = false;  // SPMV_STREAM_NT overrides
 // the x-window kernel (x gathers from LDS) streams faster non-temporal:
 // 0.2991 vs 0.3077 ms on the cant-like batch
@@ -206,9 +208,9 @@ struct Col16 {
 // GATHERS_TOGETHER: also issue all 2R x gathers before the first product
 // (more loads in flight per wave, more VGPRs, lower occupancy) instead of
 // gathering round by round.
-template <int R, bool NT, bool GATHERS_TOGETHER, typename Cols, typename XS>
+template <int R, bool NT, bool GATHERS_TOGETHER, typename Cols, typename XS, typename V = double>
 __device__ __forceinline__ void stage_products(int64_t cb, int64_t ce, int64_t nz, const Cols &cols,
-                                               const double *__restrict__ val, const XS &xs,
+                                               const V *__restrict__ val, const XS &xs,
                                                double2 *s_prod)
 {
     double2 v[R];
@@ -218,7 +220,7 @@ __device__ __forceinline__ void stage_products(int64_t cb, int64_t ce, int64_t n
         for (int k = 0; k < R; ++k) {
             const int64_t p = cb + 2 * (int64_t)(threadIdx.x + k * kBlock);
             const int64_t q = (p < ce && p + 1 < nz) ? p : 0;
-            v[k] = stream_load2<NT>(val + q);
+            v[k] = vpair<NT>(val + q);
             c[k] = cols.pair(q);
         }
     } else {
@@ -245,7 +247,7 @@ __device__ __forceinline__ void stage_products(int64_t cb, int64_t ce, int64_t n
     const int64_t tail = nz - 1 - cb;
     if ((nz & 1) && nz - 1 < ce && tail >= 0 && tail < 2 * R * kBlock && (tail >> 1) % kBlock == threadIdx.x) {
         const int64_t p = nz - 1;
-        s_prod[tail >> 1].x = stream_load<NT>(val + p) * xs(cols.one(p));
+        s_prod[tail >> 1].x = vone<NT>(val + p) * xs(cols.one(p));
     }
 }
 
@@ -254,12 +256,26 @@ __device__ __forceinline__ void stage_products(int64_t cb, int64_t ce, int64_t n
 // One lane's share of a row's products in the staged chunk: entries
 // [lo, hi) of the chunk (chunk-relative, < 2^31), every L-th from lo+lane,
 // two partial sums so consecutive LDS reads do not wait on each other.
+// Eight products are read per step before the first add (one LDS round
+// trip per 8·L entries instead of per 2·L); the adds keep the a0/a1
+// alternation, so the sums are the same bits as the two-at-a-time loop.
 template <int L>
 __device__ __forceinline__ double slice_sum(const double *prod, int64_t lo64, int64_t hi64, int lane)
 {
     const int lo = (int)lo64, hi = (int)hi64;
     double a0 = 0.0, a1 = 0.0;
     int j = lo + lane;
+    for (; j + 7 * L < hi; j += 8 * L) {
+        double p[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            p[k] = prod[j + k * L];
+#pragma unroll
+        for (int k = 0; k < 8; k += 2) {
+            a0 += p[k];
+            a1 += p[k + 1];
+        }
+    }
     for (; j + L < hi; j += 2 * L) {
         a0 += prod[j];
         a1 += prod[j + L];
@@ -316,6 +332,195 @@ __device__ __forceinline__ void staged_group(
     if (lane == 0 && row < n_rows)
         y[row] = acc;
     __syncthreads();
+}
+
+// SPMV_XWIN_PROBE (timing-only builds, tools/gpu_job.sh abprobe; y is WRONG
+// in them): bit 1 no x gathers, 2 no row reduction, 8 no x-window copy —
+// prices each part of the MODE 3 kernel
+#ifndef SPMV_XWIN_PROBE
+#define SPMV_XWIN_PROBE 0
+#endif
+struct XConst {
+    __device__ __forceinline__ double operator()(int32_t c) const { return (double)c; }
+};
+
+// One lane's share of a staged chunk in flight: R value pairs and R column
+// pairs, loaded branch-free (pairs past the chunk load pair 0 and are
+// never summed), so all 2R loads are outstanding together and can stay in
+// flight across a barrier while the previous chunk is reduced.
+template <int R, bool NT, typename V>
+struct StreamRegs {
+    double2 v[R];
+    int2 c[R];
+
+    __device__ __forceinline__ void issue(int64_t cb, int64_t ce, int64_t nz, const int32_t *__restrict__ col,
+                                          const V *__restrict__ val)
+    {
+        if (nz < 2) {  // uniform; a 1-entry array has no pair 0 (its entry: products())
+#pragma unroll
+            for (int k = 0; k < R; ++k) {
+                v[k] = double2{0.0, 0.0};
+                c[k] = int2{0, 0};
+            }
+            return;
+        }
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const int64_t p = cb + 2 * (int64_t)(threadIdx.x + k * kBlock);
+            const int64_t q = (p < ce && p + 1 < nz) ? p : 0;
+            v[k] = vpair<NT>(val + q);
+            c[k] = stream_load2<NT>(col + q);
+        }
+    }
+
+    // products of the issued chunk [cb, ce) into s_prod (as stage_products)
+    template <typename XS>
+    __device__ __forceinline__ void products(int64_t cb, int64_t ce, int64_t nz, const int32_t *__restrict__ col,
+                                             const V *__restrict__ val, const XS &xs, double2 *s_prod) const
+    {
+#pragma unroll
+        for (int k = 0; k < R; ++k)
+            s_prod[threadIdx.x + k * kBlock] = double2{v[k].x * xs(c[k].x), v[k].y * xs(c[k].y)};
+        const int64_t tail = nz - 1 - cb;  // the array's odd last entry
+        if ((nz & 1) && nz - 1 < ce && tail >= 0 && tail < 2 * R * kBlock && (tail >> 1) % kBlock == threadIdx.x) {
+            const int64_t p = nz - 1;
+            s_prod[tail >> 1].x = vone<NT>(val + p) * xs(col[p]);
+        }
+    }
+};
+
+// The row groups of one x window, software-pipelined (csr_xwin_kernel
+// MODE 3): the loads of the NEXT chunk — of this row group or of the
+// window's next group — are issued right after the current chunk's
+// products are in LDS, so they are in flight during the barrier and the
+// L-lane reduction instead of after it.  s_off holds the window's
+// ngroups·RPB + 1 row offsets.  Chunks and per-row sums are exactly those
+// of staged_group (same boundaries, same order): the same bits.
+// NBUF = 2 (MODE 4): chunks alternate between two product buffers, so the
+// barrier that protected the buffer from the next chunk's products is gone
+// (one barrier per chunk); the caller adds a barrier before reusing LDS.
+template <int L, int R, bool NT, typename XS, typename V, int NBUF = 1>
+__device__ __forceinline__ void staged_window_pipelined(int64_t row0, int ngroups, const int64_t *s_off,
+                                                        double2 *s_prod_base, const int32_t *__restrict__ col,
+                                                        const V *__restrict__ val, const XS xs,
+                                                        double *__restrict__ y, int64_t n_rows, int64_t nz)
+{
+    constexpr int RPB = kBlock / L;
+    constexpr int CH = 2 * kBlock * R;
+    const int g = threadIdx.x / L;
+    const int lane = threadIdx.x % L;
+    int buf = 0;
+    // first chunk of group j at or after `from` that has one (staged_group's
+    // loop runs a chunk iff (start & ~1) < end); ngroups when none
+    auto next_group = [&](int from) {
+        int j = from;
+        while (j < ngroups && (s_off[j * RPB] & ~(int64_t)1) >= s_off[(j + 1) * RPB])
+            ++j;
+        return j;
+    };
+    StreamRegs<R, NT, V> st;
+    int jn = next_group(0);
+    if (jn < ngroups) {
+        const int64_t b = s_off[jn * RPB] & ~(int64_t)1, e = s_off[(jn + 1) * RPB];
+        st.issue(b, b + CH < e ? b + CH : e, nz, col, val);
+    }
+    for (int gi = 0; gi < ngroups; ++gi) {
+        const int64_t *gp = s_off + gi * RPB;
+        const int64_t beg = gp[g], end = gp[g + 1];
+        const int64_t blk_end = gp[RPB];
+        double acc = 0.0;
+        for (int64_t cb = gp[0] & ~(int64_t)1; cb < blk_end; cb += CH) {
+            const int64_t ce = cb + CH < blk_end ? cb + CH : blk_end;
+            double2 *s_prod = s_prod_base + buf * (kBlock * R);
+            const double *prod = reinterpret_cast<const double *>(s_prod);
+#if SPMV_XWIN_PROBE & 1  // timing probe: no x gathers (wrong y)
+            st.products(cb, ce, nz, col, val, XConst{}, s_prod);
+#else
+            st.products(cb, ce, nz, col, val, xs, s_prod);
+#endif
+            // the next chunk: this group's, else the next group's first
+            if (cb + CH < blk_end) {
+                const int64_t nb = cb + CH;
+                st.issue(nb, nb + CH < blk_end ? nb + CH : blk_end, nz, col, val);
+            } else if ((jn = next_group(gi + 1)) < ngroups) {
+                const int64_t b = s_off[jn * RPB] & ~(int64_t)1, e = s_off[(jn + 1) * RPB];
+                st.issue(b, b + CH < e ? b + CH : e, nz, col, val);
+            }
+            __syncthreads();
+#if SPMV_XWIN_PROBE & 2  // timing probe: one product per lane instead of the row slice (wrong y)
+            acc += prod[threadIdx.x];
+#else
+            acc += slice_sum<L>(prod, beg > cb ? beg - cb : 0, (end < ce ? end : ce) - cb, lane);
+#endif
+            if constexpr (NBUF == 1)
+                __syncthreads();
+            else
+                buf ^= 1;
+        }
+        acc = group_sum<L>(acc);
+        const int64_t row = row0 + (int64_t)gi * RPB + g;
+        if (lane == 0 && row < n_rows)
+            y[row] = acc;
+    }
+}
+
+// The window's rows as ONE entry range (csr_xwin_kernel MODE 5): instead of
+// chunking each 256/L-row group on its own (a 64-row group of the cant
+// batch is 4,107 entries: two full 2,048-entry chunks and an 11-entry one,
+// every chunk one memory round trip and two barriers), the window's whole
+// range [s_off[0], s_off[WR]) is cut into the fewest chunks of at most
+// 2·256·R entries, all of (nearly) equal size, streamed pipelined as in
+// MODE 3.  L-lane group g owns the RW consecutive rows g·RW .. g·RW+RW-1 of
+// the window (WR = RW·256/L rows) and adds each chunk's slice of each row.
+// Rows that lie in one chunk sum exactly as in the other modes; a row cut
+// by a chunk boundary is summed in the same order over other boundaries.
+template <int L, int R, int RW, bool NT, typename XS, typename V>
+__device__ __forceinline__ void staged_window_flat(int64_t row0, const int64_t *s_off, double2 *s_prod,
+                                                   const int32_t *__restrict__ col, const V *__restrict__ val,
+                                                   const XS xs, double *__restrict__ y, int64_t n_rows, int64_t nz)
+{
+    constexpr int G = kBlock / L;
+    constexpr int64_t CHMAX = 2 * kBlock * R;
+    const int g = threadIdx.x / L;
+    const int lane = threadIdx.x % L;
+    const double *prod = reinterpret_cast<const double *>(s_prod);
+    int64_t rb[RW + 1];
+#pragma unroll
+    for (int k = 0; k <= RW; ++k)
+        rb[k] = s_off[g * RW + k];
+    const int64_t e0 = s_off[0] & ~(int64_t)1, e1 = s_off[G * RW];
+    const int64_t nch = e1 > e0 ? (e1 - e0 + CHMAX - 1) / CHMAX : 0;
+    const int64_t cs = nch > 0 ? (((e1 - e0 + nch - 1) / nch) + 1) & ~(int64_t)1 : 0;  // even, <= CHMAX
+    double acc[RW];
+#pragma unroll
+    for (int k = 0; k < RW; ++k)
+        acc[k] = 0.0;
+    StreamRegs<R, NT, V> st;
+    if (nch > 0)
+        st.issue(e0, e0 + cs < e1 ? e0 + cs : e1, nz, col, val);
+    for (int64_t c = 0; c < nch; ++c) {
+        const int64_t cb = e0 + c * cs;
+        const int64_t ce = cb + cs < e1 ? cb + cs : e1;
+        st.products(cb, ce, nz, col, val, xs, s_prod);
+        if (c + 1 < nch)
+            st.issue(ce, ce + cs < e1 ? ce + cs : e1, nz, col, val);
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < RW; ++k) {
+            const int64_t lo = rb[k] > cb ? rb[k] : cb;
+            const int64_t hi = rb[k + 1] < ce ? rb[k + 1] : ce;
+            if (lo < hi)  // uniform over the L-lane group
+                acc[k] += slice_sum<L>(prod, lo - cb, hi - cb, lane);
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int k = 0; k < RW; ++k) {
+        const double s = group_sum<L>(acc[k]);
+        const int64_t row = row0 + (int64_t)g * RW + k;
+        if (lane == 0 && row < n_rows)
+            y[row] = s;
+    }
 }
 
 // Variant 2: one workgroup per row group.
@@ -396,42 +601,120 @@ __global__ __launch_bounds__(kBlock) void csr_window_kernel(int64_t n_rows, int6
 // Windows of several groups overlap less than per-group windows, so less
 // x is re-read.  A window wider than xcap gathers from global memory.
 // Same products, same order: y is bit-identical to variant 3.
-template <int L, int R, bool NT, typename V = double>
-__global__ __launch_bounds__(kBlock) void csr_xwin_kernel(
+// MODE (load schedule; products, sums and y are the same bits in every mode):
+//   0 = window copied by a strided loop (one round trip per 256 entries),
+//       each stream round's loads waited for before the next round's issue;
+//   1 = the window's row offsets (all its groups, staged in LDS after the x
+//       range: dynamic LDS of xcap + rows_per_window + 1 doubles) and its x
+//       range loaded together, 8 loads in flight per thread, before ONE
+//       barrier; no offset loads between the groups;
+//   2 = as 1, and all R value/column pair loads of a chunk issued together
+//       before the first product (stage_products; x gathers from LDS);
+//   3 = as 2, software-pipelined: the next chunk's loads are issued before
+//       the current chunk's barrier and reduction (staged_window_pipelined);
+//   4 = as 3 with two product buffers: one barrier per chunk;
+//   5 = as 3, the window's rows chunked as one entry range
+//       (staged_window_flat; gpw in {1, 2, 4}, else MODE 3).
+// MODE 3/4 kernels are built for kXwinWaves waves per SIMD (workgroups per
+// CU), which caps their VGPRs (8 -> 64)
+#ifndef SPMV_XWIN_WAVES
+#define SPMV_XWIN_WAVES 1
+#endif
+constexpr int kXwinWaves = SPMV_XWIN_WAVES;
+template <int L, int R, bool NT, typename V = double, int MODE = 0>
+__global__ __launch_bounds__(kBlock, MODE >= 3 ? kXwinWaves : 1) void csr_xwin_kernel(
     int64_t n_rows, int64_t n_groups, int64_t gpw, const int64_t *__restrict__ row_ptr,
     const int32_t *__restrict__ col, const V *__restrict__ val,
     const double *__restrict__ x, double *__restrict__ y, const int2 *__restrict__ win, int32_t xcap,
     int remap)
 {
     constexpr int RPB = kBlock / L;
+    constexpr int BATCH = MODE == 2 ? 1 : 0;
     extern __shared__ double s_x[];
-    __shared__ int64_t s_ptr[RPB + 1];
-    __shared__ double2 s_prod[kBlock * R];
+    __shared__ int64_t s_ptr[MODE > 0 ? 1 : RPB + 1];
+    __shared__ double2 s_prod[kBlock * R * (MODE == 4 ? 2 : 1)];
+    int64_t *s_off = reinterpret_cast<int64_t *>(s_x + xcap);  // MODE > 0: the window's offsets
     const int64_t nz = row_ptr[n_rows];
     const int64_t n_win = (n_groups + gpw - 1) / gpw;
     // remap: consecutive windows on one XCD, so the overlapping x ranges of
     // neighbouring windows are copied from that XCD's L2
     for (int64_t wi = xcd_block(remap); wi < n_win; wi += gridDim.x) {
+        const int64_t g_beg = wi * gpw;
+        const int64_t g_end = (wi + 1) * gpw < n_groups ? (wi + 1) * gpw : n_groups;
         const int2 wnd = win[wi];
         const int32_t span = wnd.y - wnd.x + 1;
         const bool staged = span > 0 && span <= xcap;  // uniform per workgroup
-        if (staged)
+        if constexpr (MODE > 0) {
+            // offsets r0 .. r0 + nr of the window's rows (clamped past
+            // n_rows), then the x range: every load issued before the stores
+            const int64_t r0 = g_beg * RPB;
+            const int32_t nr = (int32_t)((g_end - g_beg) * RPB) + 1;
+            constexpr int U = 2;  // offsets per thread per pass (nr <= U·256 in one pass)
+            for (int32_t b = 0; b < nr; b += U * kBlock) {
+                int64_t o[U];
+#pragma unroll
+                for (int k = 0; k < U; ++k) {
+                    const int64_t r = r0 + b + threadIdx.x + k * kBlock;
+                    o[k] = row_ptr[r < n_rows ? r : n_rows];
+                }
+                if (staged && b == 0)
+#if !(SPMV_XWIN_PROBE & 8)  // timing probe: no window copy (wrong y)
+                    copy_window(s_x, x, wnd.x, span);
+#endif
+#pragma unroll
+                for (int k = 0; k < U; ++k) {
+                    const int32_t i = b + (int32_t)threadIdx.x + k * kBlock;
+                    if (i < nr)
+                        s_off[i] = o[k];
+                }
+            }
+        } else if (staged) {
             for (int32_t i = threadIdx.x; i < span; i += kBlock)
                 s_x[i] = x[wnd.x + i];
-        const int64_t g_end = (wi + 1) * gpw < n_groups ? (wi + 1) * gpw : n_groups;
-        for (int64_t grp = wi * gpw; grp < g_end; ++grp) {
-            if (threadIdx.x <= RPB) {
-                const int64_t r = grp * RPB + threadIdx.x;
-                s_ptr[threadIdx.x] = row_ptr[r < n_rows ? r : n_rows];
+        }
+        if constexpr (MODE >= 5) {  // flat chunks; MODE 5/6/7 = gpw 1/2/4 (the launcher's pick)
+            constexpr int RW = MODE == 5 ? 1 : MODE == 6 ? 2 : 4;
+            __syncthreads();  // window and offsets visible
+            const int64_t r0 = g_beg * RPB;
+            if (staged)
+                staged_window_flat<L, R, RW, NT>(r0, s_off, s_prod, col, val, XWindow{s_x, wnd.x}, y, n_rows, nz);
+            else
+                staged_window_flat<L, R, RW, NT>(r0, s_off, s_prod, col, val, XGlobal{x}, y, n_rows, nz);
+            continue;
+        }
+        if constexpr (MODE >= 3) {
+            constexpr int NB = MODE == 4 ? 2 : 1;
+            __syncthreads();  // window and offsets visible
+            if (staged)
+                staged_window_pipelined<L, R, NT, XWindow, V, NB>(g_beg * RPB, (int)(g_end - g_beg), s_off, s_prod,
+                                                                  col, val, XWindow{s_x, wnd.x}, y, n_rows, nz);
+            else
+                staged_window_pipelined<L, R, NT, XGlobal, V, NB>(g_beg * RPB, (int)(g_end - g_beg), s_off, s_prod,
+                                                                  col, val, XGlobal{x}, y, n_rows, nz);
+            if constexpr (NB == 2)
+                __syncthreads();  // the last chunk's buffer is read before the next window writes LDS
+            continue;
+        }
+        for (int64_t grp = g_beg; grp < g_end; ++grp) {
+            const int64_t *gp = s_ptr;
+            if constexpr (MODE > 0) {
+                gp = s_off + (grp - g_beg) * RPB;
+                if (grp == g_beg)
+                    __syncthreads();  // window and offsets visible
+            } else {
+                if (threadIdx.x <= RPB) {
+                    const int64_t r = grp * RPB + threadIdx.x;
+                    s_ptr[threadIdx.x] = row_ptr[r < n_rows ? r : n_rows];
+                }
+                __syncthreads();  // offsets (and, for the first group, the window) visible
             }
-            __syncthreads();  // offsets (and, for the first group, the window) visible
             const int64_t row = grp * RPB + threadIdx.x / L;
             if (staged)
-                staged_group<L, R, NT, Col32<NT>, 0, XWindow, V>(row, s_ptr, s_prod, Col32<NT>{col}, val,
-                                                                 XWindow{s_x, wnd.x}, y, n_rows, nz);
+                staged_group<L, R, NT, Col32<NT>, BATCH, XWindow, V>(row, gp, s_prod, Col32<NT>{col}, val,
+                                                                     XWindow{s_x, wnd.x}, y, n_rows, nz);
             else
-                staged_group<L, R, NT, Col32<NT>, 0, XGlobal, V>(row, s_ptr, s_prod, Col32<NT>{col}, val,
-                                                                 XGlobal{x}, y, n_rows, nz);
+                staged_group<L, R, NT, Col32<NT>, BATCH, XGlobal, V>(row, gp, s_prod, Col32<NT>{col}, val,
+                                                                     XGlobal{x}, y, n_rows, nz);
         }
     }
 }
@@ -926,6 +1209,38 @@ static bool csr_xwin_prefetch()
     return s && s[0] == '1';
 }
 
+// Load schedule of csr_xwin_kernel (its MODE): SPMV_CSR_XWIN_MODE=0..3,
+// read on every call (A/B runs, tools/ab_env.py); default kCsrXwinMode.
+// MODE 3 with XCD-contiguous windows: 0.2644 ms vs 0.2678 (MODE 3, round
+// robin), 0.2701 (MODE 0, remap) and 0.2717 (MODE 0, round robin), five
+// interleaved rounds on one box (profiles/round2/ab_csr_xwin.log)
+constexpr int kCsrXwinMode = 3;
+constexpr bool kCsrXwinRemap = true;
+// pairs per lane per chunk of the x-window kernel (1,536-entry chunks):
+// MODE 3 with R = 3 measured 0.2591-0.2607 ms against 0.2639-0.2642 with
+// R = 4 on two boxes (equal on a third); R = 6 / 8 slower (0.273 / 0.280)
+constexpr int kCsrXwinRounds = kStageRoundsDefault;
+static int csr_xwin_mode()
+{
+    const char *s = getenv("SPMV_CSR_XWIN_MODE");
+    return (s && s[0] >= '0' && s[0] <= '5' && s[1] == 0) ? s[0] - '0' : kCsrXwinMode;
+}
+
+// SPMV_CSR_XWIN_R in {2,3,4,6,8}: value/column pairs per lane per chunk of
+// the MODE 3 kernel (non-temporal loads only; sweep knob, read per call)
+static int csr_xwin_rounds()
+{
+    const char *s = getenv("SPMV_CSR_XWIN_R");
+    return s ? atoi(s) : kCsrXwinRounds;
+}
+
+// dynamic LDS of csr_xwin_kernel: the x window, and from MODE 1 on the
+// window's row offsets behind it
+static size_t csr_xwin_lds(int mode, int32_t xcap, int64_t gpw, int rpb)
+{
+    return ((size_t)xcap + (mode > 0 ? (size_t)(gpw * rpb + 1) : 0)) * sizeof(double);
+}
+
 // rows per x window: a multiple of the row group (256/L rows), default
 // kCsrXwinRows, at least one group
 static int64_t csr_xwin_gpw(int L, int32_t rows_per_window)
@@ -944,20 +1259,81 @@ static void launch_csr_xwin(const spmv_dims &d, const int64_t *row_ptr, const in
     constexpr int RPB = kBlock / L;
     const int64_t groups = (d.n_rows + RPB - 1) / RPB;
     const int64_t n_win = (groups + gpw - 1) / gpw;
-    const size_t lds = (size_t)xcap * sizeof(double);
+    const int mode = csr_xwin_mode();
+    const size_t lds = csr_xwin_lds(mode, xcap, gpw, RPB);
     // one workgroup per window (the dispatcher balances) unless
     // SPMV_CSR_XWIN_PERSISTENT=1 (resident workgroups walk the windows)
     const char *ps = getenv("SPMV_CSR_XWIN_PERSISTENT");
     const int64_t grid = (ps && ps[0] == '1') ? persistent_grid(csr_xwin_kernel<L, R, NT>, n_win, lds) : n_win;
     if (grid > INT32_MAX)
         return;
-    if (csr_xwin_prefetch())
-        hipLaunchKernelGGL((csr_xwin_pf_kernel<L, R, NT>), dim3((unsigned)grid), dim3(kBlock), lds,
-                           (hipStream_t)d.stream, d.n_rows, groups, gpw, row_ptr, col, val, x, y, win, xcap);
-    else
-        hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT>), dim3((unsigned)grid), dim3(kBlock), lds,
-                           (hipStream_t)d.stream, d.n_rows, groups, gpw, row_ptr, col, val, x, y, win, xcap,
-                           xwin_remap() ? 1 : 0);
+    const int remap = xwin_remap(kCsrXwinRemap) ? 1 : 0;
+    const hipStream_t st = (hipStream_t)d.stream;
+    if (csr_xwin_prefetch()) {
+        const size_t lds0 = (size_t)xcap * sizeof(double);
+        hipLaunchKernelGGL((csr_xwin_pf_kernel<L, R, NT>), dim3((unsigned)grid), dim3(kBlock), lds0, st, d.n_rows,
+                           groups, gpw, row_ptr, col, val, x, y, win, xcap);
+        return;
+    }
+    switch (mode) {
+    case 0:
+        hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, double, 0>), dim3((unsigned)grid), dim3(kBlock), lds, st,
+                           d.n_rows, groups, gpw, row_ptr, col, val, x, y, win, xcap, remap);
+        break;
+    case 1:
+        hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, double, 1>), dim3((unsigned)grid), dim3(kBlock), lds, st,
+                           d.n_rows, groups, gpw, row_ptr, col, val, x, y, win, xcap, remap);
+        break;
+    case 2:
+        hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, double, 2>), dim3((unsigned)grid), dim3(kBlock), lds, st,
+                           d.n_rows, groups, gpw, row_ptr, col, val, x, y, win, xcap, remap);
+        break;
+    case 3:
+        if constexpr (NT) {  // SPMV_CSR_XWIN_R: pairs per lane per chunk (sweep knob)
+            const int rr = csr_xwin_rounds();
+            if (rr != R) {
+                const size_t l2 = lds;  // the chunk buffer is static LDS
+#define SPMV_XWIN_R(RR)                                                                                      \
+    hipLaunchKernelGGL((csr_xwin_kernel<L, RR, NT, double, 3>), dim3((unsigned)grid), dim3(kBlock), l2, st, \
+                       d.n_rows, groups, gpw, row_ptr, col, val, x, y, win, xcap, remap)
+                switch (rr) {
+                case 2: SPMV_XWIN_R(2); return;
+                case 3: SPMV_XWIN_R(3); return;
+                case 4: SPMV_XWIN_R(4); return;
+                case 6: SPMV_XWIN_R(6); return;
+                case 8: SPMV_XWIN_R(8); return;
+                default: break;
+                }
+#undef SPMV_XWIN_R
+            }
+        }
+        hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, double, 3>), dim3((unsigned)grid), dim3(kBlock), lds, st,
+                           d.n_rows, groups, gpw, row_ptr, col, val, x, y, win, xcap, remap);
+        break;
+    case 4:
+        hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, double, 4>), dim3((unsigned)grid), dim3(kBlock), lds, st,
+                           d.n_rows, groups, gpw, row_ptr, col, val, x, y, win, xcap, remap);
+        break;
+    case 5:
+        if (gpw == 1 || gpw == 2 || gpw == 4) {
+            const bool r3 = NT && csr_xwin_rounds() == 3;  // SPMV_CSR_XWIN_R (sweep knob)
+#define SPMV_FLAT(RR, MM)                                                                                     \
+    hipLaunchKernelGGL((csr_xwin_kernel<L, RR, NT, double, MM>), dim3((unsigned)grid), dim3(kBlock), lds, st, \
+                       d.n_rows, groups, gpw, row_ptr, col, val, x, y, win, xcap, remap)
+            if (gpw == 1) {
+                if (r3) SPMV_FLAT(3, 5); else SPMV_FLAT(R, 5);
+            } else if (gpw == 2) {
+                if (r3) SPMV_FLAT(3, 6); else SPMV_FLAT(R, 6);
+            } else {
+                if (r3) SPMV_FLAT(3, 7); else SPMV_FLAT(R, 7);
+            }
+#undef SPMV_FLAT
+        } else {
+            hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, double, 3>), dim3((unsigned)grid), dim3(kBlock), lds, st,
+                               d.n_rows, groups, gpw, row_ptr, col, val, x, y, win, xcap, remap);
+        }
+        break;
+    }
 }
 
 template <int L>
@@ -1050,7 +1426,7 @@ extern "C" int spmv_csr_run_xwin(spmv_dims d, const int64_t *row_ptr, const int3
         return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_run_xwin: lanes_per_row must be 0 or a power of two in [2,64]");
     const int64_t gpw = csr_xwin_gpw(L, rows_per_window);
     const bool nt = stream_nt(kCsrXwinNtDefault);
-    constexpr int R = kStageRoundsDefault;
+    constexpr int R = kCsrXwinRounds;
     const int2 *w = (const int2 *)win;
     const bool direct = csr_xwin_direct();
 #define SPMV_XWIN(LL)                                                                  \
@@ -1205,14 +1581,15 @@ extern "C" int spmv_csr_f32v_run_xwin(spmv_dims d, const int64_t *row_ptr, const
         const int64_t n_win = (groups + gpw - 1) / gpw;                                                     \
         if (n_win > INT32_MAX)                                                                              \
             return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_f32v_run_xwin: grid too large");                    \
+        const size_t lds = csr_xwin_lds(kCsrXwinMode, xcap, gpw, RPB);                                      \
         if (nt)                                                                                             \
-            hipLaunchKernelGGL((csr_xwin_kernel<LL, R, true, float>), dim3((unsigned)n_win), dim3(kBlock),   \
-                               (size_t)xcap * sizeof(double), (hipStream_t)d.stream, d.n_rows, groups, gpw, \
-                               row_ptr, col, val, x, y, w, xcap, 0);                                        \
+            hipLaunchKernelGGL((csr_xwin_kernel<LL, R, true, float, kCsrXwinMode>), dim3((unsigned)n_win),  \
+                               dim3(kBlock), lds, (hipStream_t)d.stream, d.n_rows, groups, gpw, row_ptr, col, \
+                               val, x, y, w, xcap, 0);                                                      \
         else                                                                                                \
-            hipLaunchKernelGGL((csr_xwin_kernel<LL, R, false, float>), dim3((unsigned)n_win), dim3(kBlock),  \
-                               (size_t)xcap * sizeof(double), (hipStream_t)d.stream, d.n_rows, groups, gpw, \
-                               row_ptr, col, val, x, y, w, xcap, 0);                                        \
+            hipLaunchKernelGGL((csr_xwin_kernel<LL, R, false, float, kCsrXwinMode>), dim3((unsigned)n_win), \
+                               dim3(kBlock), lds, (hipStream_t)d.stream, d.n_rows, groups, gpw, row_ptr, col, \
+                               val, x, y, w, xcap, 0);                                                      \
     } while (0)
     switch (L) {
     case 2: SPMV_XWIN32(2); break;

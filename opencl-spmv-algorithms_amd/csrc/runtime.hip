@@ -48,10 +48,12 @@ DeviceGuard::~DeviceGuard()
         (void)hipSetDevice(prev_);
 }
 
-bool xwin_remap()
+bool xwin_remap(bool dflt)
 {
     const char *s = getenv("SPMV_XWIN_REMAP");
-    return s && s[0] == '1';
+    if (s && (s[0] == '0' || s[0] == '1'))
+        return s[0] == '1';
+    return dflt;
 }
 
 bool xcd_remap_enabled()

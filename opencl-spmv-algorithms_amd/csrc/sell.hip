@@ -466,7 +466,7 @@ extern "C" int spmv_sell_run_xwin(spmv_dims d, int32_t C, int32_t sigma, int32_t
                         : (nt ? sell_xwin_kernel<1, true, 4> : sell_xwin_kernel<1, false, 4>);
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(bt), (size_t)xcap * sizeof(double),
                        (hipStream_t)d.stream, C, n_slices, slice_ptr, perm, col, val, x, y,
-                       (const int2 *)win, xcap, (int64_t)INT64_MAX, xwin_remap() ? 1 : 0);
+                       (const int2 *)win, xcap, (int64_t)INT64_MAX, xwin_remap(false) ? 1 : 0);
     SPMV_CHECK_LAUNCH("sell_xwin_kernel");
     return SPMV_SUCCESS;
 }
@@ -634,7 +634,7 @@ extern "C" int spmv_sell_run_split(spmv_dims d, int32_t C, int32_t sigma, int32_
                             : (nt ? sell_xwin_kernel<1, true, 4> : sell_xwin_kernel<1, false, 4>);
         hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(bt), (size_t)xcap * sizeof(double), st, C, n_slices,
                            slice_ptr, perm, col, val, x, y, (const int2 *)win, xcap, (int64_t)T,
-                           xwin_remap() ? 1 : 0);
+                           xwin_remap(false) ? 1 : 0);
     } else {
         auto kern = ki == 2 ? (nt ? sell_kernel<2, true, 4> : sell_kernel<2, false, 4>)
                             : (nt ? sell_kernel<1, true, 4> : sell_kernel<1, false, 4>);

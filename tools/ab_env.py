@@ -1,0 +1,88 @@
+#!/usr/bin/env python3
+"""Interleaved A/B of library knobs that are read on every call (SPMV_*
+environment variables) on ONE device matrix built once.
+
+    python tools/ab_env.py --format csr --env SPMV_CSR_XWIN_MODE=0,1,2 [--rounds 5]
+
+Every configuration runs `--reps` back-to-back launches per round (HIP events
+on the launch stream), configurations interleaved round by round in one
+process; prints the median of the per-round means and whether y is
+bit-identical to the first configuration's.
+"""
+from __future__ import annotations
+
+import argparse
+import itertools
+import json
+import os
+import sys
+from pathlib import Path
+
+import numpy as np
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(REPO / "opencl-spmv-algorithms_amd"), str(REPO)]
+import spmv_amd as sa  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--format", default="csr")
+    ap.add_argument("--matrix", default="cantlike", choices=["cantlike", "rmat"])
+    ap.add_argument("--copies", type=int, default=32)
+    ap.add_argument("--env", action="append", default=[], help="KEY=v1,v2 (several: cartesian product)")
+    ap.add_argument("--kw", default="{}", help="to_device keyword arguments (JSON)")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=50)
+    a = ap.parse_args()
+    import torch
+
+    dev = torch.device("cuda:0")
+    m = sa.gen_cantlike(0, a.copies) if a.matrix == "cantlike" else sa.gen_rmat()
+    b = sa.bytes_alg(m.n_rows, m.n_cols, m.nnz)
+    keys, vals = [], []
+    for e in a.env:
+        k, v = e.split("=", 1)
+        keys.append(k)
+        vals.append(v.split(","))
+    configs = [dict(zip(keys, c)) for c in itertools.product(*vals)] or [{}]
+    x = torch.from_numpy(np.random.default_rng(7).uniform(-1, 1, m.n_cols)).to(dev)
+    y = torch.empty(m.n_rows, dtype=torch.float64, device=dev)
+    dm = sa.to_device(m, a.format, dev, **json.loads(a.kw))
+    s = torch.cuda.current_stream()
+    res = [[] for _ in configs]
+    same = [True for _ in configs]
+    y0 = None
+    for _ in range(a.rounds):
+        for i, env in enumerate(configs):
+            saved = {k: os.environ.get(k) for k in env}
+            os.environ.update(env)
+            for _ in range(5):
+                dm.run(x, y, s)
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(a.reps + 1)]
+            ev[0].record(s)
+            for k in range(a.reps):
+                dm.run(x, y, s)
+                ev[k + 1].record(s)
+            torch.cuda.synchronize()
+            res[i].append(float(np.mean([ev[k].elapsed_time(ev[k + 1]) for k in range(a.reps)])))
+            if y0 is None:
+                y0 = y.clone()
+            elif not torch.equal(y.view(torch.int64), y0.view(torch.int64)):
+                same[i] = False
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+    for i, env in enumerate(configs):
+        ms = float(np.median(res[i]))
+        print(json.dumps(dict(fmt=a.format, env=env, ms=round(ms, 5), GBs_alg=round(b / ms * 1e-6, 1),
+                              frac=round(b / ms * 1e-6 / sa.HBM_PEAK_GBS, 4),
+                              spread=round((max(res[i]) - min(res[i])) / ms, 4), bit_identical=same[i])),
+              flush=True)
+    print(json.dumps({"matrix": a.matrix, "copies": a.copies, "bytes_alg": b, "params": dm.params}, default=str))
+
+
+if __name__ == "__main__":
+    main()

@@ -73,6 +73,39 @@ __global__ __launch_bounds__(256) void tile_read_kernel(const double2 *__restric
         out[0] = s;
 }
 
+// The CSR kernels' stream without their LDS work: each workgroup reads the
+// values (16-B pairs) and columns (8-B pairs) of CH-entry chunks of its
+// E-entry tile, R pairs per lane per chunk, nt, and folds them (the
+// ceiling of the csr_xwin_kernel access pattern: two arrays, 24 B per pair).
+template <int R>
+__global__ __launch_bounds__(256) void csr_stream_kernel(const double *__restrict__ val,
+                                                         const int *__restrict__ col, size_t nnz, size_t tile,
+                                                         double *__restrict__ out)
+{
+    typedef double v2 __attribute__((ext_vector_type(2)));
+    typedef int i2 __attribute__((ext_vector_type(2)));
+    constexpr size_t CH = 2 * 256 * R;
+    const size_t t0 = (size_t)blockIdx.x * tile;
+    const size_t t1 = t0 + tile < nnz ? t0 + tile : nnz;
+    double s = 0.0;
+    for (size_t cb = t0; cb < t1; cb += CH) {
+        v2 v[R];
+        i2 c[R];
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const size_t p = cb + 2 * (threadIdx.x + (size_t)k * 256);
+            const size_t q = p + 1 < t1 ? p : t0;
+            v[k] = __builtin_nontemporal_load(reinterpret_cast<const v2 *>(val + q));
+            c[k] = __builtin_nontemporal_load(reinterpret_cast<const i2 *>(col + q));
+        }
+#pragma unroll
+        for (int k = 0; k < R; ++k)
+            s += v[k].x * (double)c[k].x + v[k].y * (double)c[k].y;
+    }
+    if (s == 123.456)
+        out[0] = s;
+}
+
 __global__ __launch_bounds__(256) void copy_kernel(const double2 *__restrict__ a,
                                                    double2 *__restrict__ b, size_t n)
 {
@@ -146,6 +179,29 @@ int main(int argc, char **argv)
                                          (const double2 *)a, n16, out); }, reps);
     printf("{\"probe\": \"tile_read_dwordx4_u16_nt\", \"bytes\": %zu, \"ms\": %.4f, \"GBs\": %.1f}\n", bytes, t,
            bytes / t * 1e-6);
+    {   // CSR-shaped stream: 128M entries (the cant-like batch), 8-B values + 4-B columns
+        const size_t nnz = (size_t)128 << 20;
+        double *val;
+        int *col;
+        CHECK(hipMalloc(&val, nnz * 8));
+        CHECK(hipMalloc(&col, nnz * 4));
+        CHECK(hipMemset(val, 0, nnz * 8));
+        CHECK(hipMemset(col, 0, nnz * 4));
+        const size_t tiles[] = {2048, 8192, 32768};
+        for (size_t tile : tiles) {
+            const unsigned g = (unsigned)((nnz + tile - 1) / tile);
+            t = time_ms([&] { hipLaunchKernelGGL((csr_stream_kernel<4>), dim3(g), dim3(256), 0, 0, val, col, nnz,
+                                                 tile, out); }, reps);
+            printf("{\"probe\": \"csr_stream_r4_tile%zu_nt\", \"bytes\": %zu, \"ms\": %.4f, \"GBs\": %.1f}\n",
+                   tile, nnz * 12, t, nnz * 12 / t * 1e-6);
+        }
+        t = time_ms([&] { hipLaunchKernelGGL((csr_stream_kernel<8>), dim3((unsigned)(nnz / 8192)), dim3(256), 0,
+                                             0, val, col, nnz, (size_t)8192, out); }, reps);
+        printf("{\"probe\": \"csr_stream_r8_tile8192_nt\", \"bytes\": %zu, \"ms\": %.4f, \"GBs\": %.1f}\n",
+               nnz * 12, t, nnz * 12 / t * 1e-6);
+        CHECK(hipFree(val));
+        CHECK(hipFree(col));
+    }
     t = time_ms([&] { hipLaunchKernelGGL(copy_kernel, dim3(grid), dim3(256), 0, 0,
                                          (const double2 *)a, (double2 *)b, n16); }, reps);
     printf("{\"probe\": \"copy_dwordx4\", \"bytes\": %zu, \"ms\": %.4f, \"GBs\": %.1f}\n", 2 * bytes, t,

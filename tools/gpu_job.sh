@@ -1,8 +1,8 @@
 #!/usr/bin/env bash
 # GPU-box job: smoke, GPU parity tests, bench, rocprofv3 kernel-trace.
-# Each GPU step has its own time limit; a crash/timeout/abort stops the job
-# (exit codes 124/137 timeout, 134 abort, 139 segfault), plain test
-# failures (exit 1) do not stop the later measurement steps.
+# Each GPU step has its own time limit; ANY failing step stops the job (a
+# Python process that hit a GPU fault exits 1, like a failed test, so no
+# exit code is safe to run past).
 # usage: tools/gpu_job.sh [steps...]   steps: smoke tests bench prof pmc
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -10,7 +10,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 steps=("$@")
 [ ${#steps[@]} -eq 0 ] && steps=(smoke tests bench prof)
-fatal() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
+fatal() { [ "$1" -ne 0 ]; }
 run() { # name timeout cmd...
   local name=$1 t=$2; shift 2
   echo "=== $name: $*" | tee -a gpurun_out/job.log
@@ -67,6 +67,24 @@ for s in "${steps[@]}"; do
              run coo_cur_nt$i 300 python bench.py --format coo --per-format no --cpu-seconds 0 &&
              SPMV_STREAM_NT=0 run coo_cur_nt0_$i 300 python bench.py --format coo --per-format no --cpu-seconds 0
            done;;
+    abremap) run ab_csr_xwin_remap 600 python tools/ab_env.py --format csr --env SPMV_CSR_XWIN_MODE=0,3 --env SPMV_XWIN_REMAP=0,1 --rounds 5;;
+    abxr) run ab_csr_xwin_r 600 python tools/ab_env.py --format csr --env SPMV_CSR_XWIN_R=2,3,4,6,8 --rounds 5;;
+    abx4) run ab_csr_xwin_m34 600 python tools/ab_env.py --format csr --env SPMV_CSR_XWIN_MODE=0,3,4 --env SPMV_CSR_XWIN_R=3,4 --rounds 5;;
+    abwaves) for i in 1 2; do
+               run ab_w1_$i 300 python tools/ab_env.py --format csr --env SPMV_CSR_XWIN_R=3,4 --rounds 3 &&
+               SPMV_HIP_LIB=$PWD/tools/ab/libspmv_hip_w7.so run ab_w7_$i 300 python tools/ab_env.py --format csr --env SPMV_CSR_XWIN_R=3,4 --rounds 3 &&
+               SPMV_HIP_LIB=$PWD/tools/ab/libspmv_hip_w8.so run ab_w8_$i 300 python tools/ab_env.py --format csr --env SPMV_CSR_XWIN_R=3,4 --rounds 3
+             done;;
+    abprobe) for i in 1 2; do  # (bit 4 = no second barrier faulted: not built any more)
+               run abp_base_$i 300 python tools/ab_env.py --format csr --env SPMV_CSR_XWIN_R=3,4 --rounds 3
+               for p in 1 2 8; do
+                 SPMV_HIP_LIB=$PWD/tools/ab/libspmv_hip_p$p.so run abp_p${p}_$i 300 python tools/ab_env.py --format csr --env SPMV_CSR_XWIN_R=3,4 --rounds 3
+               done
+             done;;
+    abflat) run ab_flat_l4 600 python tools/ab_env.py --format csr --env SPMV_CSR_XWIN_MODE=3,5 --env SPMV_CSR_XWIN_R=3,4 --rounds 5 &&
+            run ab_flat_l2 600 python tools/ab_env.py --format csr --kw '{"lanes": 2}' --env SPMV_CSR_XWIN_MODE=3,5 --env SPMV_CSR_XWIN_R=3,4 --rounds 5 &&
+            run ab_flat_l8 600 python tools/ab_env.py --format csr --kw '{"lanes": 8}' --env SPMV_CSR_XWIN_MODE=3,5 --env SPMV_CSR_XWIN_R=3,4 --rounds 5;;
+    abxwin) run ab_csr_xwin_mode 600 python tools/ab_env.py --format csr --env SPMV_CSR_XWIN_MODE=0,2,3 --rounds 5;;
     cmrsnt) run cmrs_base 300 python bench.py --format cmrs --per-format no --cpu-seconds 0 &&
             SPMV_STREAM_NT=1 run cmrs_nt 300 python bench.py --format cmrs --per-format no --cpu-seconds 0 &&
             run cmrs_base2 300 python bench.py --format cmrs --per-format no --cpu-seconds 0 &&
@@ -109,6 +127,7 @@ for s in "${steps[@]}"; do
     sweepnt) run sweep_nt 600 python tools/sweep.py --env-only --rounds 3;;
     pmcnt) run pmc_nt 1100 python tools/pmc_traffic.py --out traffic_nt.json --formats "csr@SPMV_STREAM_NT=1,sell@SPMV_STREAM_NT=1,ell@SPMV_STREAM_NT=1,coo,cmrs";;
     ldsconf) run pmc_lds 600 python tools/pmc_stalls.py --formats csr,sell,cmrs --passes ta,sq,lds --out pmc_lds.json;;
+    stalls2) run pmc_stalls2 1150 python tools/pmc_stalls.py --formats "csr,csr@SPMV_CSR_XWIN_MODE=0" --passes sq,sq2,tcc,lat,lds,ta --out pmc_stalls_r2.json;;
     stalls) run pmc_stalls 1150 python tools/pmc_stalls.py --formats csr,sell;;
     iterbench) run iter_power 300 python tools/iterate_bench.py --what power --matrix cantlike --iters 200 &&
                run iter_power_graph 300 python tools/iterate_bench.py --what power --matrix cantlike --iters 200 --graph &&

@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import os
 import sys
 from pathlib import Path
 
@@ -44,22 +45,31 @@ def main():
     a = ap.parse_args()
     passes = {k: v for k, v in PASSES.items() if not a.passes or k in a.passes.split(",")}
     probe = REPO / "tools" / "bw_probe"
-    jobs = [("probe_tile_nt", [str(probe), str(2 << 30), "3"], "tile_read_kernel<true, 8>")]
+    jobs = [("probe_tile_nt", [str(probe), str(2 << 30), "3"], "tile_read_kernel<true, 8>", {}),
+            # the CSR access pattern without the LDS work (values + columns, R = 4)
+            ("probe_csr_stream", [str(probe), str(2 << 30), "3"], "csr_stream_kernel<4>", {})]
     for spec in a.formats.split(","):
         spec_main, *env_parts = spec.split("@")
         env_kv = dict(e.split("=", 1) for e in env_parts)
         fmt = spec_main.partition(":")[0]
         cmd = ["python3", "bench.py", "--profile", "--format", fmt, "--steps", str(a.steps), "--warmup", "2"]
-        jobs.append((spec, cmd, kernel_for(fmt, env_kv)))
+        jobs.append((spec, cmd, kernel_for(fmt, env_kv), env_kv))
     out = {}
-    for name, cmd, kern in jobs:
+    for name, cmd, kern, env_kv in jobs:
         counters = {}
+        saved = {k: os.environ.get(k) for k in env_kv}
+        os.environ.update(env_kv)  # run_pass hands os.environ to the profiled command
         for tag, cs in passes.items():
             tagdir = f"stall_{name}_{tag}".replace(":", "_").replace("=", "").replace("@", "_")
             f = run_pass(tagdir, cs, cmd, timeout=150)
             if f:
                 c, _ = mean_per_dispatch(f, kern)
                 counters.update(c)
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
         gui = counters.get("GRBM_GUI_ACTIVE")
         frac = {}
         if gui:

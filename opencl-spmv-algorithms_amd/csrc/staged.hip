@@ -36,32 +36,74 @@ __device__ __forceinline__ int lower_bound_lds(const K *keys, int lo, int hi, in
     return lo;
 }
 
-// Streams entries [cb, ce) into LDS: products in s_prod, keys via `key`.
-// cb is even, so value pairs are 16-byte aligned; nothing at or past ce
-// is read.
-// NT: non-temporal stream loads (the skewed-matrix kernels: x, gathered
-// from a vector far larger than L2, keeps the cache).
-template <int R, bool NT = false, typename XS, typename KeyFn, typename V>
-__device__ __forceinline__ void stage_chunk(int64_t cb, int64_t ce, const int32_t *__restrict__ col,
+// Row keys staged next to the products, in two phases so their loads are
+// batched with the value/column loads: load(q) the key pair of entries
+// (q, q+1), store(t, pair), and one(t, p) for the array's odd last entry.
+// COO: int32 row ids (int2 pairs); CMRS: uint8 row-in-strip (2-byte pairs).
+template <bool NT>
+struct KeysRow32 {
+    const int32_t *__restrict__ k;
+    int2 *s;
+    using P = int2;
+    __device__ __forceinline__ P load(int64_t q) const { return stream_load2<NT>(k + q); }
+    __device__ __forceinline__ void store(int t, P v) const { s[t] = v; }
+    __device__ __forceinline__ void one(int t, int64_t p) const { s[t] = make_int2(stream_load<NT>(k + p), 0); }
+};
+
+struct KeysU8 {
+    const uint8_t *__restrict__ k;
+    uint16_t *s;
+    using P = uint16_t;
+    __device__ __forceinline__ P load(int64_t q) const { return *reinterpret_cast<const uint16_t *>(k + q); }
+    __device__ __forceinline__ void store(int t, P v) const { s[t] = v; }
+    __device__ __forceinline__ void one(int t, int64_t p) const { s[t] = (uint16_t)k[p]; }
+};
+
+struct KeysNone {  // the tiled CSR: rows come from row_ptr, no keys
+    using P = uint8_t;
+    __device__ __forceinline__ P load(int64_t) const { return 0; }
+    __device__ __forceinline__ void store(int, P) const {}
+    __device__ __forceinline__ void one(int, int64_t) const {}
+};
+
+// Streams entries [cb, ce) (cb even) of an nz-entry array into LDS:
+// products in s_prod, row keys through `keys`.  Every lane issues its R
+// value, column and key pair loads before the first product (branch-free:
+// a pair starting at or past ce loads pair 0, a cached line, and is never
+// read back), so 3R loads per lane are in flight together; a pair that
+// straddles ce reads one entry past the chunk, inside the array, that no
+// reduction reads.  The array's odd last entry is loaded singly.
+// NT: non-temporal stream loads.
+template <int R, bool NT = false, typename XS, typename Keys, typename V>
+__device__ __forceinline__ void stage_chunk(int64_t cb, int64_t ce, int64_t nz, const int32_t *__restrict__ col,
                                             const V *__restrict__ val, const XS &xs,
-                                            double2 *s_prod, KeyFn key)
+                                            double2 *s_prod, const Keys &keys)
 {
+    double2 v[R];
+    int2 c[R];
+    typename Keys::P kp[R];
+    if (nz >= 2) {  // uniform; a 1-entry array has no pair 0 (its entry: the tail below)
 #pragma unroll
-    for (int k = 0; k < R; ++k) {
-        const int t = threadIdx.x + k * kBlock;
-        const int64_t p = cb + 2 * (int64_t)t;
-        double2 pr = {0.0, 0.0};
-        if (p + 1 < ce) {
-            const double2 v = vpair<NT>(val + p);
-            const int2 c = stream_load2<NT>(col + p);
-            pr.x = v.x * xs(c.x);
-            pr.y = v.y * xs(c.y);
-            key(t, p, 2);
-        } else if (p < ce) {
-            pr.x = vone<NT>(val + p) * xs(stream_load<NT>(col + p));
-            key(t, p, 1);
+        for (int k = 0; k < R; ++k) {
+            const int64_t p = cb + 2 * (int64_t)(threadIdx.x + k * kBlock);
+            const int64_t q = (p < ce && p + 1 < nz) ? p : 0;
+            v[k] = vpair<NT>(val + q);
+            c[k] = stream_load2<NT>(col + q);
+            kp[k] = keys.load(q);
         }
-        s_prod[t] = pr;
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const int t = threadIdx.x + k * kBlock;
+            s_prod[t] = double2{v[k].x * xs(c[k].x), v[k].y * xs(c[k].y)};
+            keys.store(t, kp[k]);
+        }
+    }
+    const int64_t tail = nz - 1 - cb;
+    if ((nz & 1) && nz - 1 < ce && tail >= 0 && tail < 2 * R * kBlock && (tail >> 1) % kBlock == threadIdx.x) {
+        const int64_t p = nz - 1;
+        const int t = (int)(tail >> 1);
+        s_prod[t] = double2{vone<NT>(val + p) * xs(stream_load<NT>(col + p)), 0.0};
+        keys.one(t, p);
     }
 }
 
@@ -101,8 +143,7 @@ __global__ __launch_bounds__(kBlock) void cmrs_staged_kernel(
         staged = span > 0 && span <= xcap;
         wlo = wnd.x;
         if (staged)
-            for (int32_t i = threadIdx.x; i < span; i += kBlock)
-                s_x[i] = x[wlo + i];
+            copy_window(s_x, x, wlo, span);
     }
     __syncthreads();
 
@@ -113,17 +154,16 @@ __global__ __launch_bounds__(kBlock) void cmrs_staged_kernel(
     const int64_t sb = s_sp[si], se = active ? s_sp[si + 1] : s_sp[si];
     const int64_t row = (s0 + si) * h + key;
     const int64_t blk_end = s_sp[G];
-    auto keys = [&](int t, int64_t p, int n) {
-        s_key2[t] = n == 2 ? *reinterpret_cast<const uint16_t *>(rin + p) : (uint16_t)rin[p];
-    };
+    const KeysU8 keys{rin, s_key2};
+    const int64_t nz = strip_ptr[n_strips];
 
     double acc = 0.0;
     for (int64_t cb = s_sp[0] & ~(int64_t)1; cb < blk_end; cb += CH) {
         const int64_t ce = cb + CH < blk_end ? cb + CH : blk_end;
         if (staged)
-            stage_chunk<R, NT>(cb, ce, col, val, XWindow{s_x, wlo}, s_prod, keys);
+            stage_chunk<R, NT>(cb, ce, nz, col, val, XWindow{s_x, wlo}, s_prod, keys);
         else
-            stage_chunk<R, NT>(cb, ce, col, val, XGlobal{x}, s_prod, keys);
+            stage_chunk<R, NT>(cb, ce, nz, col, val, XGlobal{x}, s_prod, keys);
         __syncthreads();
         const int64_t lo = sb > cb ? sb : cb;
         const int64_t hi = se < ce ? se : ce;
@@ -181,9 +221,7 @@ __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
     const int n = (int)(t1 - t0);
     if (threadIdx.x == 0)
         s_prev = t0 > 0 ? row[t0 - 1] : -1;
-    auto keys = [&](int t, int64_t p, int cnt) {
-        s_row2[t] = cnt == 2 ? stream_load2<NT>(row + p) : make_int2(stream_load<NT>(row + p), 0);
-    };
+    const KeysRow32<NT> keys{row, s_row2};
     bool staged = false;  // uniform per workgroup
     int32_t wlo = 0;
     if constexpr (XW) {
@@ -192,15 +230,14 @@ __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
         staged = span > 0 && span <= xcap;
         wlo = wnd.x;
         if (staged) {
-            for (int32_t i = threadIdx.x; i < span; i += kBlock)
-                s_x[i] = x[wlo + i];
+            copy_window(s_x, x, wlo, span);
             __syncthreads();
         }
     }
     if (staged)
-        stage_chunk<R, NT>(t0, t1, col, val, XWindow{s_x, wlo}, s_prod, keys);
+        stage_chunk<R, NT>(t0, t1, nnz, col, val, XWindow{s_x, wlo}, s_prod, keys);
     else
-        stage_chunk<R, NT>(t0, t1, col, val, xs, s_prod, keys);
+        stage_chunk<R, NT>(t0, t1, nnz, col, val, xs, s_prod, keys);
     __syncthreads();
 
     const int32_t prev = s_prev;
@@ -353,7 +390,7 @@ __global__ __launch_bounds__(kBlock) void csr_tiled_kernel(
             const int64_t o = row_ptr[r_lo + i];
             s_rp[i] = (int32_t)((o < t1 ? o : t1) - t0);
         }
-    stage_chunk<R, NT>(t0, t1, col, val, xs, s_prod, [](int, int64_t, int) {});
+    stage_chunk<R, NT>(t0, t1, nnz, col, val, xs, s_prod, KeysNone{});
     __syncthreads();
     const int g = threadIdx.x / L, lane = threadIdx.x % L;
 
@@ -422,9 +459,7 @@ __global__ __launch_bounds__(kBlock) void cmrs_tiled_kernel(
     const int64_t t1 = t0 + CH < nnz ? t0 + CH : nnz;
     const int64_t s_lo = own_lo[tile];
     const int64_t s_hi = t1 == nnz ? n_strips - 1 : (int64_t)own_lo[tile + 1] - 1;
-    stage_chunk<R, true>(t0, t1, col, val, xs, s_prod, [&](int t, int64_t p, int n) {
-        s_key2[t] = n == 2 ? *reinterpret_cast<const uint16_t *>(rin + p) : (uint16_t)rin[p];
-    });
+    stage_chunk<R, true>(t0, t1, nnz, col, val, xs, s_prod, KeysU8{rin, s_key2});
     __syncthreads();
     const int g = threadIdx.x / L, lane = threadIdx.x % L;
 

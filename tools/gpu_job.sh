@@ -84,6 +84,14 @@ for s in "${steps[@]}"; do
     abflat) run ab_flat_l4 600 python tools/ab_env.py --format csr --env SPMV_CSR_XWIN_MODE=3,5 --env SPMV_CSR_XWIN_R=3,4 --rounds 5 &&
             run ab_flat_l2 600 python tools/ab_env.py --format csr --kw '{"lanes": 2}' --env SPMV_CSR_XWIN_MODE=3,5 --env SPMV_CSR_XWIN_R=3,4 --rounds 5 &&
             run ab_flat_l8 600 python tools/ab_env.py --format csr --kw '{"lanes": 8}' --env SPMV_CSR_XWIN_MODE=3,5 --env SPMV_CSR_XWIN_R=3,4 --rounds 5;;
+    abformats) for i in 1 2; do
+                 SPMV_HIP_LIB=$PWD/tools/ab/libspmv_hip_head.so run abf_head_$i 600 python tools/time_formats.py &&
+                 run abf_new_$i 600 python tools/time_formats.py
+               done;;
+    abformatsr) for i in 1 2; do
+                 SPMV_HIP_LIB=$PWD/tools/ab/libspmv_hip_head.so run abfr_head_$i 600 python tools/time_formats.py --matrix rmat --formats csr,cmrs,coo,hyb,sell --rounds 2 --reps 10 &&
+                 run abfr_new_$i 600 python tools/time_formats.py --matrix rmat --formats csr,cmrs,coo,hyb,sell --rounds 2 --reps 10
+               done;;
     abxwin) run ab_csr_xwin_mode 600 python tools/ab_env.py --format csr --env SPMV_CSR_XWIN_MODE=0,2,3 --rounds 5;;
     cmrsnt) run cmrs_base 300 python bench.py --format cmrs --per-format no --cpu-seconds 0 &&
             SPMV_STREAM_NT=1 run cmrs_nt 300 python bench.py --format cmrs --per-format no --cpu-seconds 0 &&

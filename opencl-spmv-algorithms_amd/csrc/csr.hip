@@ -399,11 +399,12 @@ struct StreamRegs {
 // NBUF = 2 (MODE 4): chunks alternate between two product buffers, so the
 // barrier that protected the buffer from the next chunk's products is gone
 // (one barrier per chunk); the caller adds a barrier before reusing LDS.
-template <int L, int R, bool NT, typename XS, typename V, int NBUF = 1>
+template <int L, int R, bool NT, typename XS, typename V, int NBUF = 1, bool PRE = false>
 __device__ __forceinline__ void staged_window_pipelined(int64_t row0, int ngroups, const int64_t *s_off,
                                                         double2 *s_prod_base, const int32_t *__restrict__ col,
                                                         const V *__restrict__ val, const XS xs,
-                                                        double *__restrict__ y, int64_t n_rows, int64_t nz)
+                                                        double *__restrict__ y, int64_t n_rows, int64_t nz,
+                                                        const StreamRegs<R, NT, V> pre_st = {}, bool pre = false)
 {
     constexpr int RPB = kBlock / L;
     constexpr int CH = 2 * kBlock * R;
@@ -419,10 +420,16 @@ __device__ __forceinline__ void staged_window_pipelined(int64_t row0, int ngroup
         return j;
     };
     StreamRegs<R, NT, V> st;
-    int jn = next_group(0);
-    if (jn < ngroups) {
-        const int64_t b = s_off[jn * RPB] & ~(int64_t)1, e = s_off[(jn + 1) * RPB];
-        st.issue(b, b + CH < e ? b + CH : e, nz, col, val);
+    int jn;
+    if (PRE && pre) {  // the caller issued group 0's first chunk (it has one)
+        st = pre_st;
+        jn = 0;
+    } else {
+        jn = next_group(0);
+        if (jn < ngroups) {
+            const int64_t b = s_off[jn * RPB] & ~(int64_t)1, e = s_off[(jn + 1) * RPB];
+            st.issue(b, b + CH < e ? b + CH : e, nz, col, val);
+        }
     }
     for (int gi = 0; gi < ngroups; ++gi) {
         const int64_t *gp = s_off + gi * RPB;
@@ -621,7 +628,7 @@ __global__ __launch_bounds__(kBlock) void csr_window_kernel(int64_t n_rows, int6
 #define SPMV_XWIN_WAVES 1
 #endif
 constexpr int kXwinWaves = SPMV_XWIN_WAVES;
-template <int L, int R, bool NT, typename V = double, int MODE = 0>
+template <int L, int R, bool NT, typename V = double, int MODE = 0, bool PRE = false>
 __global__ __launch_bounds__(kBlock, MODE >= 3 ? kXwinWaves : 1) void csr_xwin_kernel(
     int64_t n_rows, int64_t n_groups, int64_t gpw, const int64_t *__restrict__ row_ptr,
     const int32_t *__restrict__ col, const V *__restrict__ val,
@@ -644,6 +651,20 @@ __global__ __launch_bounds__(kBlock, MODE >= 3 ? kXwinWaves : 1) void csr_xwin_k
         const int2 wnd = win[wi];
         const int32_t span = wnd.y - wnd.x + 1;
         const bool staged = span > 0 && span <= xcap;  // uniform per workgroup
+        // MODE 3 (kCsrXwinPre): group 0's first chunk is issued before the
+        // window copy — its range needs only two row offsets, loaded beside
+        // the window bounds — so the copy and the first chunk's loads share
+        // one round trip instead of following each other
+        StreamRegs<R, NT, V> st_pre;
+        bool pre = false;
+        if constexpr (MODE == 3 && PRE) {
+            const int64_t rr0 = g_beg * RPB;
+            const int64_t rr1 = rr0 + RPB < n_rows ? rr0 + RPB : n_rows;
+            const int64_t b = row_ptr[rr0] & ~(int64_t)1, e = row_ptr[rr1];
+            pre = b < e;  // uniform
+            if (pre)
+                st_pre.issue(b, b + 2 * kBlock * R < e ? b + 2 * kBlock * R : e, nz, col, val);
+        }
         if constexpr (MODE > 0) {
             // offsets r0 .. r0 + nr of the window's rows (clamped past
             // n_rows), then the x range: every load issued before the stores
@@ -686,11 +707,13 @@ __global__ __launch_bounds__(kBlock, MODE >= 3 ? kXwinWaves : 1) void csr_xwin_k
             constexpr int NB = MODE == 4 ? 2 : 1;
             __syncthreads();  // window and offsets visible
             if (staged)
-                staged_window_pipelined<L, R, NT, XWindow, V, NB>(g_beg * RPB, (int)(g_end - g_beg), s_off, s_prod,
-                                                                  col, val, XWindow{s_x, wnd.x}, y, n_rows, nz);
+                staged_window_pipelined<L, R, NT, XWindow, V, NB, PRE>(g_beg * RPB, (int)(g_end - g_beg), s_off,
+                                                                       s_prod, col, val, XWindow{s_x, wnd.x}, y,
+                                                                       n_rows, nz, st_pre, pre);
             else
-                staged_window_pipelined<L, R, NT, XGlobal, V, NB>(g_beg * RPB, (int)(g_end - g_beg), s_off, s_prod,
-                                                                  col, val, XGlobal{x}, y, n_rows, nz);
+                staged_window_pipelined<L, R, NT, XGlobal, V, NB, PRE>(g_beg * RPB, (int)(g_end - g_beg), s_off,
+                                                                       s_prod, col, val, XGlobal{x}, y, n_rows,
+                                                                       nz, st_pre, pre);
             if constexpr (NB == 2)
                 __syncthreads();  // the last chunk's buffer is read before the next window writes LDS
             continue;
@@ -1226,6 +1249,17 @@ static int csr_xwin_mode()
     return (s && s[0] >= '0' && s[0] <= '5' && s[1] == 0) ? s[0] - '0' : kCsrXwinMode;
 }
 
+// SPMV_CSR_XWIN_PRE=1: MODE 3 issues the first chunk before the window copy
+// (read per call; A/B knob).  Off: the prefetched registers live across the
+// copy (100 VGPRs instead of 78, 4 instead of 6 workgroups per CU) and it
+// measured 0.2646 vs 0.2589 ms (profiles/round2/ab_csr_xwin_pre.log)
+constexpr bool kCsrXwinPre = false;
+static bool csr_xwin_pre()
+{
+    const char *s = getenv("SPMV_CSR_XWIN_PRE");
+    return s && (s[0] == '0' || s[0] == '1') ? s[0] == '1' : kCsrXwinPre;
+}
+
 // SPMV_CSR_XWIN_R in {2,3,4,6,8}: value/column pairs per lane per chunk of
 // the MODE 3 kernel (non-temporal loads only; sweep knob, read per call)
 static int csr_xwin_rounds()
@@ -1307,8 +1341,12 @@ static void launch_csr_xwin(const spmv_dims &d, const int64_t *row_ptr, const in
 #undef SPMV_XWIN_R
             }
         }
-        hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, double, 3>), dim3((unsigned)grid), dim3(kBlock), lds, st,
-                           d.n_rows, groups, gpw, row_ptr, col, val, x, y, win, xcap, remap);
+        if (csr_xwin_pre())
+            hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, double, 3, true>), dim3((unsigned)grid), dim3(kBlock), lds,
+                               st, d.n_rows, groups, gpw, row_ptr, col, val, x, y, win, xcap, remap);
+        else
+            hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, double, 3>), dim3((unsigned)grid), dim3(kBlock), lds, st,
+                               d.n_rows, groups, gpw, row_ptr, col, val, x, y, win, xcap, remap);
         break;
     case 4:
         hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, double, 4>), dim3((unsigned)grid), dim3(kBlock), lds, st,

@@ -199,6 +199,15 @@ int main(int argc, char **argv)
                                              0, val, col, nnz, (size_t)8192, out); }, reps);
         printf("{\"probe\": \"csr_stream_r8_tile8192_nt\", \"bytes\": %zu, \"ms\": %.4f, \"GBs\": %.1f}\n",
                nnz * 12, t, nnz * 12 / t * 1e-6);
+        // the same stream with dynamic LDS reserved per workgroup, so only
+        // 160 KiB / lds workgroups fit a CU (occupancy of the LDS-staged kernels)
+        const size_t ldss[] = {20 << 10, 26 << 10, 32 << 10, 40 << 10};
+        for (size_t lds : ldss) {
+            t = time_ms([&] { hipLaunchKernelGGL((csr_stream_kernel<4>), dim3((unsigned)(nnz / 8192)), dim3(256), lds,
+                                                 0, val, col, nnz, (size_t)8192, out); }, reps);
+            printf("{\"probe\": \"csr_stream_r4_tile8192_nt_lds%zuk\", \"bytes\": %zu, \"ms\": %.4f, \"GBs\": %.1f}\n",
+                   lds >> 10, nnz * 12, t, nnz * 12 / t * 1e-6);
+        }
         CHECK(hipFree(val));
         CHECK(hipFree(col));
     }

@@ -92,6 +92,7 @@ for s in "${steps[@]}"; do
                  SPMV_HIP_LIB=$PWD/tools/ab/libspmv_hip_head.so run abfr_head_$i 600 python tools/time_formats.py --matrix rmat --formats csr,cmrs,coo,hyb,sell --rounds 2 --reps 10 &&
                  run abfr_new_$i 600 python tools/time_formats.py --matrix rmat --formats csr,cmrs,coo,hyb,sell --rounds 2 --reps 10
                done;;
+    abpre) run ab_csr_xwin_pre 600 python tools/ab_env.py --format csr --env SPMV_CSR_XWIN_PRE=0,1 --rounds 6;;
     abxwin) run ab_csr_xwin_mode 600 python tools/ab_env.py --format csr --env SPMV_CSR_XWIN_MODE=0,2,3 --rounds 5;;
     cmrsnt) run cmrs_base 300 python bench.py --format cmrs --per-format no --cpu-seconds 0 &&
             SPMV_STREAM_NT=1 run cmrs_nt 300 python bench.py --format cmrs --per-format no --cpu-seconds 0 &&

@@ -93,6 +93,10 @@ for s in "${steps[@]}"; do
                  run abfr_new_$i 600 python tools/time_formats.py --matrix rmat --formats csr,cmrs,coo,hyb,sell --rounds 2 --reps 10
                done;;
     abpre) run ab_csr_xwin_pre 600 python tools/ab_env.py --format csr --env SPMV_CSR_XWIN_PRE=0,1 --rounds 6;;
+    abrows) for r in 64 128 256 512; do
+              run ab_csr_rows$r 300 python tools/ab_env.py --format csr --kw "{\"xwin_rows\": $r}" --env SPMV_CSR_XWIN_MODE=3,5 --rounds 4
+            done &&
+            run ab_sell_unroll 300 python tools/ab_env.py --format sell --env SPMV_SLOT_UNROLL=4,8 --env SPMV_XWIN_REMAP=0,1 --rounds 4;;
     abxwin) run ab_csr_xwin_mode 600 python tools/ab_env.py --format csr --env SPMV_CSR_XWIN_MODE=0,2,3 --rounds 5;;
     cmrsnt) run cmrs_base 300 python bench.py --format cmrs --per-format no --cpu-seconds 0 &&
             SPMV_STREAM_NT=1 run cmrs_nt 300 python bench.py --format cmrs --per-format no --cpu-seconds 0 &&

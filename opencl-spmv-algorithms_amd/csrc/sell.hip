@@ -88,6 +88,103 @@ __device__ __forceinline__ double slot_dot(const double *__restrict__ vp,
     return a[0];
 }
 
+// One slot group (KI consecutive entries of a lane's row) held in registers.
+template <int KI, bool NT>
+struct SlotRegs;
+
+template <bool NT>
+struct SlotRegs<1, NT> {
+    double v;
+    int32_t c;
+    __device__ __forceinline__ void load(const double *vp, const int32_t *cp)
+    {
+        v = stream_load<NT>(vp);
+        c = stream_load<NT>(cp);
+    }
+    template <typename XS>
+    __device__ __forceinline__ double fma(const XS &xs, double acc) const { return acc + v * xs(c); }
+};
+
+template <bool NT>
+struct SlotRegs<2, NT> {
+    double2 v;
+    int2 c;
+    __device__ __forceinline__ void load(const double *vp, const int32_t *cp)
+    {
+        v = stream_load2<NT>(vp);
+        c = stream_load2<NT>(cp);
+    }
+    template <typename XS>
+    __device__ __forceinline__ double fma(const XS &xs, double acc) const { return acc + v.x * xs(c.x) + v.y * xs(c.y); }
+};
+
+// slot_dot, software-pipelined: the loads of the next U groups are issued
+// before the FMAs of the current U, so a lane always has a batch in flight
+// while it multiplies (the plain loop waits for every batch).  The same
+// adds in the same order as slot_dot: the same bits.
+template <int KI, bool NT, int U, typename XS>
+__device__ __forceinline__ double slot_dot_pipelined(const double *__restrict__ vp,
+                                                     const int32_t *__restrict__ cp,
+                                                     int64_t w, int64_t step, const XS &xs)
+{
+    double a[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        a[u] = 0.0;
+    const int64_t groups = w / KI;
+    const int64_t full = groups / U * U;
+    SlotRegs<KI, NT> cur[U], nxt[U];
+    if (full > 0) {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            cur[u].load(vp + u * step, cp + u * step);
+    }
+    for (int64_t g = 0; g < full; g += U) {
+        const bool more = g + U < full;  // uniform over the slice's lanes
+        if (more) {
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                nxt[u].load(vp + (g + U + u) * step, cp + (g + U + u) * step);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            a[u] = cur[u].fma(xs, a[u]);
+        if (more) {
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                cur[u] = nxt[u];
+        }
+    }
+    for (int64_t g = full; g < groups; ++g)
+        a[0] = Step<KI, NT>::fma(vp + g * step, cp + g * step, xs, a[0]);
+#pragma unroll
+    for (int h = U / 2; h > 0; h /= 2) {
+#pragma unroll
+        for (int u = 0; u < h; ++u)
+            a[u] += a[u + h];
+    }
+    return a[0];
+}
+
+template <int KI, bool NT, int U, bool PIPE, typename XS>
+__device__ __forceinline__ double slot_dot_sel(const double *__restrict__ vp, const int32_t *__restrict__ cp,
+                                               int64_t w, int64_t step, const XS &xs)
+{
+    if constexpr (PIPE)
+        return slot_dot_pipelined<KI, NT, U>(vp, cp, w, step, xs);
+    else
+        return slot_dot<KI, NT, U>(vp, cp, w, step, xs);
+}
+
+// SPMV_SLOT_PIPE=0/1: the SELL / ELL x-window kernels' slot loop plain or
+// software-pipelined (read per call; A/B knob), default kSlotPipe
+constexpr bool kSlotPipe = false;
+static bool slot_pipe()
+{
+    const char *s = getenv("SPMV_SLOT_PIPE");
+    return s && (s[0] == '0' || s[0] == '1') ? s[0] == '1' : kSlotPipe;
+}
+
 // One workgroup covers one sigma window (up to 1024 slots): every y[perm]
 // store of a window then comes from ONE CU, so its L2 merges the window's
 // scattered 8-byte stores into whole lines.  With 256-slot workgroups a
@@ -152,7 +249,7 @@ __global__ __launch_bounds__(kBlock) void ell_window_kernel(int64_t n_rows, int3
 }
 
 // ELL with the workgroup's x window staged in LDS (as sell_xwin_kernel).
-template <int KI, bool NT, int U>
+template <int KI, bool NT, int U, bool PIPE = false>
 __global__ __launch_bounds__(kBlock) void ell_xwin_kernel(
     int64_t n_rows, int32_t K, int64_t ld, const int32_t *__restrict__ col,
     const double *__restrict__ val, const double *__restrict__ x,
@@ -173,8 +270,8 @@ __global__ __launch_bounds__(kBlock) void ell_xwin_kernel(
     if (i >= n_rows)
         return;
     const int64_t off = i * KI;
-    y[i] = staged ? slot_dot<KI, NT, U>(val + off, col + off, K, ld * KI, XWindow{s_x, wnd.x})
-                  : slot_dot<KI, NT, U>(val + off, col + off, K, ld * KI, XGlobal{x});
+    y[i] = staged ? slot_dot_sel<KI, NT, U, PIPE>(val + off, col + off, K, ld * KI, XWindow{s_x, wnd.x})
+                  : slot_dot_sel<KI, NT, U, PIPE>(val + off, col + off, K, ld * KI, XGlobal{x});
 }
 
 constexpr int32_t kEllXwinCap = 2048;  // 16 KiB per 256-row workgroup
@@ -250,7 +347,7 @@ __global__ __launch_bounds__(kBlock) void sell_window_kernel(int32_t C, int bt, 
 // profiles/round1/pmc_stalls.json).  Here the window is copied into LDS
 // once with coalesced loads and every gather is a ds_read_b64.  A
 // workgroup whose window exceeds xcap entries gathers from global memory.
-template <int KI, bool NT, int U>
+template <int KI, bool NT, int U, bool PIPE = false>
 __global__ __launch_bounds__(1024) void sell_xwin_kernel(
     int32_t C, int64_t n_slices, const int64_t *__restrict__ slice_ptr,
     const int32_t *__restrict__ perm, const int32_t *__restrict__ col,
@@ -279,8 +376,9 @@ __global__ __launch_bounds__(1024) void sell_xwin_kernel(
     int64_t w = (slice_ptr[s + 1] - base) / C;
     w = w < wcap ? w : wcap;
     const int64_t off = base + r * KI;
-    const double sum = staged ? slot_dot<KI, NT, U>(val + off, col + off, w, (int64_t)C * KI, XWindow{s_x, wnd.x})
-                              : slot_dot<KI, NT, U>(val + off, col + off, w, (int64_t)C * KI, XGlobal{x});
+    const double sum = staged ? slot_dot_sel<KI, NT, U, PIPE>(val + off, col + off, w, (int64_t)C * KI,
+                                                              XWindow{s_x, wnd.x})
+                              : slot_dot_sel<KI, NT, U, PIPE>(val + off, col + off, w, (int64_t)C * KI, XGlobal{x});
     const int32_t row = perm[slot];
     if (row >= 0)
         y[row] = sum;
@@ -467,8 +565,11 @@ extern "C" int spmv_sell_run_xwin(spmv_dims d, int32_t C, int32_t sigma, int32_t
     if (blocks > INT32_MAX)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_run_xwin: grid too large");
     const bool nt = stream_nt(kSellStreamNtDefault);
-    auto kern = ki == 2 ? (nt ? sell_xwin_kernel<2, true, 4> : sell_xwin_kernel<2, false, 4>)
-                        : (nt ? sell_xwin_kernel<1, true, 4> : sell_xwin_kernel<1, false, 4>);
+    const bool pipe = slot_pipe();
+    auto kern = ki == 2 ? (nt ? (pipe ? sell_xwin_kernel<2, true, 4, true> : sell_xwin_kernel<2, true, 4>)
+                              : sell_xwin_kernel<2, false, 4>)
+                        : (nt ? (pipe ? sell_xwin_kernel<1, true, 4, true> : sell_xwin_kernel<1, true, 4>)
+                              : sell_xwin_kernel<1, false, 4>);
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(bt), (size_t)xcap * sizeof(double),
                        (hipStream_t)d.stream, C, n_slices, slice_ptr, perm, col, val, x, y,
                        (const int2 *)win, xcap, (int64_t)INT64_MAX, xwin_remap(false) ? 1 : 0);
@@ -558,8 +659,11 @@ extern "C" int spmv_ell_run_xwin(spmv_dims d, int32_t K, int64_t ld, int32_t ki,
     SPMV_GUARD(d);
     const int64_t blocks = (d.n_rows + kBlock - 1) / kBlock;
     const bool nt = stream_nt(kSellStreamNtDefault);
-    auto kern = ki == 2 ? (nt ? ell_xwin_kernel<2, true, 4> : ell_xwin_kernel<2, false, 4>)
-                        : (nt ? ell_xwin_kernel<1, true, 4> : ell_xwin_kernel<1, false, 4>);
+    const bool pipe = slot_pipe();
+    auto kern = ki == 2 ? (nt ? (pipe ? ell_xwin_kernel<2, true, 4, true> : ell_xwin_kernel<2, true, 4>)
+                              : ell_xwin_kernel<2, false, 4>)
+                        : (nt ? (pipe ? ell_xwin_kernel<1, true, 4, true> : ell_xwin_kernel<1, true, 4>)
+                              : ell_xwin_kernel<1, false, 4>);
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock), (size_t)xcap * sizeof(double),
                        (hipStream_t)d.stream, d.n_rows, K, ld, col, val, x, y, (const int2 *)win, xcap);
     SPMV_CHECK_LAUNCH("ell_xwin_kernel");

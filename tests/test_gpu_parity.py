@@ -684,3 +684,38 @@ def test_csrf32_tiled_on_skewed_rows(torch_dev, H):
     torch.cuda.synchronize()
     assert torch.equal(ya.view(torch.int64), yb.view(torch.int64))
     assert_parity(m, ya.cpu().numpy(), x.cpu().numpy())
+
+
+@pytest.mark.parametrize("case", ["cantlike", "ragged", "fixtures", "empty_runs"])
+def test_csr_xwin_load_modes(torch_dev, monkeypatch, case):
+    """Every load schedule of csr_xwin_kernel (SPMV_CSR_XWIN_MODE 0-4 and the
+    first-chunk prefetch) forms the same chunks and sums: the same bits.
+    MODE 5 cuts the window into equal chunks: other bits for rows that cross
+    a chunk boundary, still within the parity criterion."""
+    torch, dev = torch_dev
+    if case == "cantlike":
+        ms = [sa.gen_cantlike(0, copies=2)]
+    elif case == "ragged":
+        ms = [sa.gen_random(20_000, 50_000, 0, 2_000, seed=21)]
+    elif case == "empty_runs":
+        ms = [_empty_run_matrix()[0]]
+    else:
+        ms = [sa.read_mtx(GOLDEN / f"{n}.mtx") for n in CASES]
+    for m in ms:
+        if m.n_rows == 0:
+            continue
+        dm = sa.to_device(m, "csr", dev, variant=3, xwin=True)
+        x = torch.from_numpy(np.random.default_rng(12).uniform(-1, 1, max(m.n_cols, 1))).to(dev)
+        ys = {}
+        for mode, pre in (("0", "0"), ("1", "0"), ("2", "0"), ("3", "0"), ("3", "1"), ("4", "0"), ("5", "0")):
+            monkeypatch.setenv("SPMV_CSR_XWIN_MODE", mode)
+            monkeypatch.setenv("SPMV_CSR_XWIN_PRE", pre)
+            y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
+            dm.run(x, y)
+            ys[mode + pre] = y
+        torch.cuda.synchronize()
+        ref = ys["00"].view(torch.int64)
+        for k in ("10", "20", "30", "31", "40"):
+            assert torch.equal(ys[k].view(torch.int64), ref), (m.label, k)
+        for k in ("00", "50"):
+            assert_parity(m, ys[k].cpu().numpy(), x.cpu().numpy()[: m.n_cols])

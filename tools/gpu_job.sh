@@ -97,6 +97,8 @@ for s in "${steps[@]}"; do
               run ab_csr_rows$r 300 python tools/ab_env.py --format csr --kw "{\"xwin_rows\": $r}" --env SPMV_CSR_XWIN_MODE=3,5 --rounds 4
             done &&
             run ab_sell_unroll 300 python tools/ab_env.py --format sell --env SPMV_SLOT_UNROLL=4,8 --env SPMV_XWIN_REMAP=0,1 --rounds 4;;
+    abpipe) run ab_sell_pipe 300 python tools/ab_env.py --format sell --env SPMV_SLOT_PIPE=0,1 --rounds 5 &&
+            run ab_ell_pipe 300 python tools/ab_env.py --format ell --env SPMV_SLOT_PIPE=0,1 --rounds 5;;
     abxwin) run ab_csr_xwin_mode 600 python tools/ab_env.py --format csr --env SPMV_CSR_XWIN_MODE=0,2,3 --rounds 5;;
     cmrsnt) run cmrs_base 300 python bench.py --format cmrs --per-format no --cpu-seconds 0 &&
             SPMV_STREAM_NT=1 run cmrs_nt 300 python bench.py --format cmrs --per-format no --cpu-seconds 0 &&

@@ -1023,13 +1023,30 @@ static int csr_default_variant()
     return cached;
 }
 
-// SPMV_CSR_STAGE_ROUNDS in {3,4,5,8}: chunk = 2*256*R products (tuning
-// knob, read per call so a sweep can change it inside one process)
-static int csr_stage_rounds()
+// Chunk size of the staged CSR kernels for a matrix: R = 3 (1,536-entry
+// chunks) unless R = 4 (2,048) cuts a row group of 256/L rows of the mean
+// length into FEWER chunks — every chunk is a memory round trip and two
+// barriers.  Cant-like (L = 4, 64 rows x 64.2 = 4,107 entries): 3 chunks
+// either way, R = 3 (measured 0.2591 vs 0.2639 ms).  Banded (L = 2, 128
+// rows x 16 = 2,048): 1 chunk with R = 4 against 2 with R = 3 (configs[4]
+// measured 4.50 ms with R = 3).  Every staged CSR path uses this rule, so
+// their chunk boundaries, hence their bits, stay identical.
+static int csr_auto_rounds(int64_t n_rows, int64_t nnz, int L)
+{
+    if (n_rows <= 0 || L <= 0)
+        return kStageRoundsDefault;
+    const double eg = (double)(kBlock / L) * ((double)nnz / (double)n_rows);
+    const int64_t c3 = (int64_t)((eg + 1535.0) / 1536.0), c4 = (int64_t)((eg + 2047.0) / 2048.0);
+    return c4 < c3 ? 4 : 3;
+}
+
+// SPMV_CSR_STAGE_ROUNDS in {2,3,4,5,8} overrides the rule (tuning knob,
+// read per call so a sweep can change it inside one process)
+static int csr_stage_rounds(int64_t n_rows, int64_t nnz, int L)
 {
     const char *s = getenv("SPMV_CSR_STAGE_ROUNDS");
-    const int r = s ? atoi(s) : kStageRoundsDefault;
-    return (r == 2 || r == 3 || r == 4 || r == 5 || r == 8) ? r : kStageRoundsDefault;
+    const int r = s ? atoi(s) : csr_auto_rounds(n_rows, nnz, L);
+    return (r == 2 || r == 3 || r == 4 || r == 5 || r == 8) ? r : csr_auto_rounds(n_rows, nnz, L);
 }
 
 static int cu_count()
@@ -1103,12 +1120,21 @@ static void launch_csr16(const spmv_dims &d, const int64_t *row_ptr, const Col16
                          const double *val, const double *x, double *y)
 {
     constexpr int RPB = kBlock / L;
-    constexpr int R = kStageRoundsDefault;
     const int64_t groups = (d.n_rows + RPB - 1) / RPB;
+    const bool r4 = csr_stage_rounds(d.n_rows, d.nnz, L) == 4;  // R = 3 or 4 (the rule)
     switch (csr_batch_mode(kCsrBatchDefault)) {
-    case 1: launch_persistent_cols<L, R, NT, Col16<NT>, 1>(d, row_ptr, cols, val, x, y, groups); break;
-    case 2: launch_persistent_cols<L, R, NT, Col16<NT>, 2>(d, row_ptr, cols, val, x, y, groups); break;
-    default: launch_persistent_cols<L, R, NT, Col16<NT>, 0>(d, row_ptr, cols, val, x, y, groups); break;
+    case 1:
+        if (r4) launch_persistent_cols<L, 4, NT, Col16<NT>, 1>(d, row_ptr, cols, val, x, y, groups);
+        else launch_persistent_cols<L, 3, NT, Col16<NT>, 1>(d, row_ptr, cols, val, x, y, groups);
+        break;
+    case 2:
+        if (r4) launch_persistent_cols<L, 4, NT, Col16<NT>, 2>(d, row_ptr, cols, val, x, y, groups);
+        else launch_persistent_cols<L, 3, NT, Col16<NT>, 2>(d, row_ptr, cols, val, x, y, groups);
+        break;
+    default:
+        if (r4) launch_persistent_cols<L, 4, NT, Col16<NT>, 0>(d, row_ptr, cols, val, x, y, groups);
+        else launch_persistent_cols<L, 3, NT, Col16<NT>, 0>(d, row_ptr, cols, val, x, y, groups);
+        break;
     }
 }
 
@@ -1140,7 +1166,7 @@ static void launch_csr(const spmv_dims &d, const int64_t *row_ptr,
     const int remap = xcd_remap_enabled() ? 1 : 0;
     const hipStream_t st = (hipStream_t)d.stream;
     if (variant >= 2) {
-        switch (csr_stage_rounds()) {
+        switch (csr_stage_rounds(d.n_rows, d.nnz, L)) {
         case 2: launch_staged<L, 2>(d, row_ptr, col, val, x, y, variant); break;
         case 3: launch_staged<L, 3>(d, row_ptr, col, val, x, y, variant); break;
         case 4: launch_staged<L, 4>(d, row_ptr, col, val, x, y, variant); break;
@@ -1239,14 +1265,30 @@ static bool csr_xwin_prefetch()
 // interleaved rounds on one box (profiles/round2/ab_csr_xwin.log)
 constexpr int kCsrXwinMode = 3;
 constexpr bool kCsrXwinRemap = true;
-// pairs per lane per chunk of the x-window kernel (1,536-entry chunks):
-// MODE 3 with R = 3 measured 0.2591-0.2607 ms against 0.2639-0.2642 with
-// R = 4 on two boxes (equal on a third); R = 6 / 8 slower (0.273 / 0.280)
-constexpr int kCsrXwinRounds = kStageRoundsDefault;
-static int csr_xwin_mode()
+// pairs per lane per chunk of the x-window kernel: csr_stage_rounds (the
+// chunk-count rule; R = 3 on the cant batch, 4 on the banded matrix)
+// Without the knob: MODE 3 when a window's entries make more than one
+// chunk (there is a next chunk to pipeline: cant-like, 128 rows x 64.2 =
+// 8,214 entries in 1,536-entry chunks), else MODE 0 — a one-chunk window
+// gains nothing from the pipeline and its 86 instead of 64 VGPRs cost
+// workgroups per CU (banded, 128 rows x 16 = one 2,048-entry chunk: 0.765
+// ms MODE 0 vs 0.815 ms MODE 3, profiles/round2/ab_banded.log).
+static int csr_xwin_mode(int64_t n_rows, int64_t nnz, int64_t rows_per_window, int R)
 {
     const char *s = getenv("SPMV_CSR_XWIN_MODE");
-    return (s && s[0] >= '0' && s[0] <= '5' && s[1] == 0) ? s[0] - '0' : kCsrXwinMode;
+    if (s && s[0] >= '0' && s[0] <= '5' && s[1] == 0)
+        return s[0] - '0';
+    const double ew = n_rows > 0 ? (double)rows_per_window * ((double)nnz / (double)n_rows) : 0.0;
+    return ew > 2.0 * kBlock * R ? kCsrXwinMode : 0;
+}
+
+// XCD-contiguous windows pay when neighbouring windows share x lines: the
+// widest window spans several times its rows (cant-like: 678 columns for 128
+// rows; on), not when each row reads a narrow band (banded: 143 columns for
+// 128 rows; 0.765 vs 0.782 ms with remap, off)
+static bool csr_xwin_remap_rule(int32_t xcap, int64_t rows_per_window)
+{
+    return xwin_remap(kCsrXwinRemap && (int64_t)xcap > 2 * rows_per_window);
 }
 
 // SPMV_CSR_XWIN_PRE=1: MODE 3 issues the first chunk before the window copy
@@ -1261,11 +1303,12 @@ static bool csr_xwin_pre()
 }
 
 // SPMV_CSR_XWIN_R in {2,3,4,6,8}: value/column pairs per lane per chunk of
-// the MODE 3 kernel (non-temporal loads only; sweep knob, read per call)
+// the MODE 3 kernel (non-temporal loads only; sweep knob, read per call);
+// 0 = the launcher's R
 static int csr_xwin_rounds()
 {
     const char *s = getenv("SPMV_CSR_XWIN_R");
-    return s ? atoi(s) : kCsrXwinRounds;
+    return s ? atoi(s) : 0;
 }
 
 // dynamic LDS of csr_xwin_kernel: the x window, and from MODE 1 on the
@@ -1293,7 +1336,7 @@ static void launch_csr_xwin(const spmv_dims &d, const int64_t *row_ptr, const in
     constexpr int RPB = kBlock / L;
     const int64_t groups = (d.n_rows + RPB - 1) / RPB;
     const int64_t n_win = (groups + gpw - 1) / gpw;
-    const int mode = csr_xwin_mode();
+    const int mode = csr_xwin_mode(d.n_rows, d.nnz, gpw * RPB, R);
     const size_t lds = csr_xwin_lds(mode, xcap, gpw, RPB);
     // one workgroup per window (the dispatcher balances) unless
     // SPMV_CSR_XWIN_PERSISTENT=1 (resident workgroups walk the windows)
@@ -1301,7 +1344,7 @@ static void launch_csr_xwin(const spmv_dims &d, const int64_t *row_ptr, const in
     const int64_t grid = (ps && ps[0] == '1') ? persistent_grid(csr_xwin_kernel<L, R, NT>, n_win, lds) : n_win;
     if (grid > INT32_MAX)
         return;
-    const int remap = xwin_remap(kCsrXwinRemap) ? 1 : 0;
+    const int remap = csr_xwin_remap_rule(xcap, gpw * RPB) ? 1 : 0;
     const hipStream_t st = (hipStream_t)d.stream;
     if (csr_xwin_prefetch()) {
         const size_t lds0 = (size_t)xcap * sizeof(double);
@@ -1325,7 +1368,7 @@ static void launch_csr_xwin(const spmv_dims &d, const int64_t *row_ptr, const in
     case 3:
         if constexpr (NT) {  // SPMV_CSR_XWIN_R: pairs per lane per chunk (sweep knob)
             const int rr = csr_xwin_rounds();
-            if (rr != R) {
+            if (rr != 0 && rr != R) {
                 const size_t l2 = lds;  // the chunk buffer is static LDS
 #define SPMV_XWIN_R(RR)                                                                                      \
     hipLaunchKernelGGL((csr_xwin_kernel<L, RR, NT, double, 3>), dim3((unsigned)grid), dim3(kBlock), l2, st, \
@@ -1354,7 +1397,7 @@ static void launch_csr_xwin(const spmv_dims &d, const int64_t *row_ptr, const in
         break;
     case 5:
         if (gpw == 1 || gpw == 2 || gpw == 4) {
-            const bool r3 = NT && csr_xwin_rounds() == 3;  // SPMV_CSR_XWIN_R (sweep knob)
+            const bool r3 = NT && csr_xwin_rounds() == 3 && R != 3;  // SPMV_CSR_XWIN_R (sweep knob)
 #define SPMV_FLAT(RR, MM)                                                                                     \
     hipLaunchKernelGGL((csr_xwin_kernel<L, RR, NT, double, MM>), dim3((unsigned)grid), dim3(kBlock), lds, st, \
                        d.n_rows, groups, gpw, row_ptr, col, val, x, y, win, xcap, remap)
@@ -1464,13 +1507,15 @@ extern "C" int spmv_csr_run_xwin(spmv_dims d, const int64_t *row_ptr, const int3
         return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_run_xwin: lanes_per_row must be 0 or a power of two in [2,64]");
     const int64_t gpw = csr_xwin_gpw(L, rows_per_window);
     const bool nt = stream_nt(kCsrXwinNtDefault);
-    constexpr int R = kCsrXwinRounds;
+    const bool r4 = csr_stage_rounds(d.n_rows, d.nnz, L) == 4;  // R = 3 or 4 (the rule)
     const int2 *w = (const int2 *)win;
     const bool direct = csr_xwin_direct();
-#define SPMV_XWIN(LL)                                                                  \
-    (direct ? launch_csr_vector_xwin<LL>(d, row_ptr, col, val, x, y, w, xcap, gpw)     \
-     : nt   ? launch_csr_xwin<LL, R, true>(d, row_ptr, col, val, x, y, w, xcap, gpw)   \
-            : launch_csr_xwin<LL, R, false>(d, row_ptr, col, val, x, y, w, xcap, gpw))
+#define SPMV_XWIN(LL)                                                                          \
+    (direct ? launch_csr_vector_xwin<LL>(d, row_ptr, col, val, x, y, w, xcap, gpw)             \
+     : nt   ? (r4 ? launch_csr_xwin<LL, 4, true>(d, row_ptr, col, val, x, y, w, xcap, gpw)     \
+                  : launch_csr_xwin<LL, 3, true>(d, row_ptr, col, val, x, y, w, xcap, gpw))    \
+            : (r4 ? launch_csr_xwin<LL, 4, false>(d, row_ptr, col, val, x, y, w, xcap, gpw)    \
+                  : launch_csr_xwin<LL, 3, false>(d, row_ptr, col, val, x, y, w, xcap, gpw)))
     switch (L) {
     case 2: SPMV_XWIN(2); break;
     case 4: SPMV_XWIN(4); break;
@@ -1609,7 +1654,7 @@ extern "C" int spmv_csr_f32v_run_xwin(spmv_dims d, const int64_t *row_ptr, const
         return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_f32v_run_xwin: lanes_per_row must be 0 or a power of two in [2,64]");
     const int64_t gpw = csr_xwin_gpw(L, rows_per_window);
     const bool nt = stream_nt(kCsrXwinNtDefault);
-    constexpr int R = kStageRoundsDefault;
+    const int remap = csr_xwin_remap_rule(xcap, gpw * (kBlock / L)) ? 1 : 0;
     const int2 *w = (const int2 *)win;
     const int64_t groups_base = d.n_rows;
 #define SPMV_XWIN32(LL)                                                                                     \
@@ -1620,14 +1665,23 @@ extern "C" int spmv_csr_f32v_run_xwin(spmv_dims d, const int64_t *row_ptr, const
         if (n_win > INT32_MAX)                                                                              \
             return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_f32v_run_xwin: grid too large");                    \
         const size_t lds = csr_xwin_lds(kCsrXwinMode, xcap, gpw, RPB);                                      \
-        if (nt)                                                                                             \
-            hipLaunchKernelGGL((csr_xwin_kernel<LL, R, true, float, kCsrXwinMode>), dim3((unsigned)n_win),  \
+        const bool r4 = csr_stage_rounds(d.n_rows, d.nnz, LL) == 4;                                         \
+        if (nt && r4)                                                                                       \
+            hipLaunchKernelGGL((csr_xwin_kernel<LL, 4, true, float, kCsrXwinMode>), dim3((unsigned)n_win),  \
                                dim3(kBlock), lds, (hipStream_t)d.stream, d.n_rows, groups, gpw, row_ptr, col, \
-                               val, x, y, w, xcap, 0);                                                      \
+                               val, x, y, w, xcap, remap);                                                  \
+        else if (nt)                                                                                        \
+            hipLaunchKernelGGL((csr_xwin_kernel<LL, 3, true, float, kCsrXwinMode>), dim3((unsigned)n_win),  \
+                               dim3(kBlock), lds, (hipStream_t)d.stream, d.n_rows, groups, gpw, row_ptr, col, \
+                               val, x, y, w, xcap, remap);                                                  \
+        else if (r4)                                                                                        \
+            hipLaunchKernelGGL((csr_xwin_kernel<LL, 4, false, float, kCsrXwinMode>), dim3((unsigned)n_win), \
+                               dim3(kBlock), lds, (hipStream_t)d.stream, d.n_rows, groups, gpw, row_ptr, col, \
+                               val, x, y, w, xcap, remap);                                                  \
         else                                                                                                \
-            hipLaunchKernelGGL((csr_xwin_kernel<LL, R, false, float, kCsrXwinMode>), dim3((unsigned)n_win), \
+            hipLaunchKernelGGL((csr_xwin_kernel<LL, 3, false, float, kCsrXwinMode>), dim3((unsigned)n_win), \
                                dim3(kBlock), lds, (hipStream_t)d.stream, d.n_rows, groups, gpw, row_ptr, col, \
-                               val, x, y, w, xcap, 0);                                                      \
+                               val, x, y, w, xcap, remap);                                                  \
     } while (0)
     switch (L) {
     case 2: SPMV_XWIN32(2); break;

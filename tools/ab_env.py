@@ -28,7 +28,8 @@ import spmv_amd as sa  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--format", default="csr")
-    ap.add_argument("--matrix", default="cantlike", choices=["cantlike", "rmat"])
+    ap.add_argument("--matrix", default="cantlike", choices=["cantlike", "rmat", "banded"])
+    ap.add_argument("--banded-rows", type=int, default=20_000_000, help="banded: rows (16 entries each)")
     ap.add_argument("--copies", type=int, default=32)
     ap.add_argument("--env", action="append", default=[], help="KEY=v1,v2 (several: cartesian product)")
     ap.add_argument("--kw", default="{}", help="to_device keyword arguments (JSON)")
@@ -38,8 +39,13 @@ def main():
     import torch
 
     dev = torch.device("cuda:0")
-    m = sa.gen_cantlike(0, a.copies) if a.matrix == "cantlike" else sa.gen_rmat()
-    b = sa.bytes_alg(m.n_rows, m.n_cols, m.nnz)
+    if a.matrix == "banded":  # generated in HBM (BASELINE.json configs[4] structure)
+        nb = a.banded_rows
+        m = sa.Coo(nb, nb, np.zeros(0, np.int32), np.zeros(0, np.int32), np.zeros(0))  # sizes only
+        b = sa.bytes_alg(nb, nb, 16 * nb)
+    else:
+        m = sa.gen_cantlike(0, a.copies) if a.matrix == "cantlike" else sa.gen_rmat()
+        b = sa.bytes_alg(m.n_rows, m.n_cols, m.nnz)
     keys, vals = [], []
     for e in a.env:
         k, v = e.split("=", 1)
@@ -48,7 +54,10 @@ def main():
     configs = [dict(zip(keys, c)) for c in itertools.product(*vals)] or [{}]
     x = torch.from_numpy(np.random.default_rng(7).uniform(-1, 1, m.n_cols)).to(dev)
     y = torch.empty(m.n_rows, dtype=torch.float64, device=dev)
-    dm = sa.to_device(m, a.format, dev, **json.loads(a.kw))
+    if a.matrix == "banded":
+        dm = sa.banded_to_device(m.n_rows, a.format, dev, **json.loads(a.kw))
+    else:
+        dm = sa.to_device(m, a.format, dev, **json.loads(a.kw))
     s = torch.cuda.current_stream()
     res = [[] for _ in configs]
     same = [True for _ in configs]

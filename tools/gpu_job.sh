@@ -99,6 +99,13 @@ for s in "${steps[@]}"; do
             run ab_sell_unroll 300 python tools/ab_env.py --format sell --env SPMV_SLOT_UNROLL=4,8 --env SPMV_XWIN_REMAP=0,1 --rounds 4;;
     abpipe) run ab_sell_pipe 300 python tools/ab_env.py --format sell --env SPMV_SLOT_PIPE=0,1 --rounds 5 &&
             run ab_ell_pipe 300 python tools/ab_env.py --format ell --env SPMV_SLOT_PIPE=0,1 --rounds 5;;
+    reh2) run reh2_w 900 python tools/shard_rehearse.py --gpus 1,8 --row-weights 2,4,8 &&
+          run reh2_trace 900 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/reh2_trace -o run -- python3 tools/shard_rehearse.py --gpus 8 --row-weights 4 --reps 10;;
+    abbanded) run ab_banded_csr 600 python tools/ab_env.py --matrix banded --format csr --env SPMV_CSR_XWIN_MODE=0,3 --env SPMV_XWIN_REMAP=0,1 --rounds 4 --reps 20 &&
+              run ab_banded_csr_r 600 python tools/ab_env.py --matrix banded --format csr --env SPMV_CSR_XWIN_MODE=3 --env SPMV_CSR_XWIN_R=3,4 --rounds 4 --reps 20 &&
+              run ab_banded_sell 600 python tools/ab_env.py --matrix banded --format sell --kw '{"ki": 1}' --env SPMV_XWIN_REMAP=0,1 --rounds 4 --reps 20;;
+    abbanded2) run ab_banded2_csr 600 python tools/ab_env.py --matrix banded --format csr --env SPMV_CSR_XWIN_MODE=0,2,3,auto --rounds 4 --reps 20 &&
+               run ab_cant2_csr 600 python tools/ab_env.py --format csr --env SPMV_CSR_XWIN_MODE=0,3,auto --rounds 4;;
     abxwin) run ab_csr_xwin_mode 600 python tools/ab_env.py --format csr --env SPMV_CSR_XWIN_MODE=0,2,3 --rounds 5;;
     cmrsnt) run cmrs_base 300 python bench.py --format cmrs --per-format no --cpu-seconds 0 &&
             SPMV_STREAM_NT=1 run cmrs_nt 300 python bench.py --format cmrs --per-format no --cpu-seconds 0 &&

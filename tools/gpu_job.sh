@@ -106,6 +106,12 @@ for s in "${steps[@]}"; do
               run ab_banded_sell 600 python tools/ab_env.py --matrix banded --format sell --kw '{"ki": 1}' --env SPMV_XWIN_REMAP=0,1 --rounds 4 --reps 20;;
     abbanded2) run ab_banded2_csr 600 python tools/ab_env.py --matrix banded --format csr --env SPMV_CSR_XWIN_MODE=0,2,3,auto --rounds 4 --reps 20 &&
                run ab_cant2_csr 600 python tools/ab_env.py --format csr --env SPMV_CSR_XWIN_MODE=0,3,auto --rounds 4;;
+    absellcopy) for i in 1 2; do
+                  SPMV_HIP_LIB=$PWD/tools/ab/libspmv_hip_head.so run ab_sellcopy_head_$i 300 python tools/ab_env.py --matrix banded --format sell --kw '{"ki": 1}' --rounds 3 --reps 20 &&
+                  run ab_sellcopy_new_$i 300 python tools/ab_env.py --matrix banded --format sell --kw '{"ki": 1}' --rounds 3 --reps 20 &&
+                  SPMV_HIP_LIB=$PWD/tools/ab/libspmv_hip_head.so run ab_sellcopy_cant_head_$i 300 python tools/ab_env.py --format sell --rounds 3 &&
+                  run ab_sellcopy_cant_new_$i 300 python tools/ab_env.py --format sell --rounds 3
+                done;;
     abxwin) run ab_csr_xwin_mode 600 python tools/ab_env.py --format csr --env SPMV_CSR_XWIN_MODE=0,2,3 --rounds 5;;
     cmrsnt) run cmrs_base 300 python bench.py --format cmrs --per-format no --cpu-seconds 0 &&
             SPMV_STREAM_NT=1 run cmrs_nt 300 python bench.py --format cmrs --per-format no --cpu-seconds 0 &&

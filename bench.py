@@ -93,6 +93,8 @@ def kernel_name(args, dm=None):
     if dm is not None and "win" in getattr(dm, "arrays", {}):
         if args.format == "csr" and os.environ.get("SPMV_CSR_XWIN_DIRECT") == "1":
             return "csr_vector_xwin_kernel"
+        if args.format in ("csr16", "csrf32"):  # the CSR x-window kernel with another column / value source
+            return "csr_xwin_kernel"
         return f"{args.format}_xwin_kernel"
     if args.format == "csr":
         v = (getattr(dm, "params", {}) or {}).get("variant", 0) or args.variant

@@ -106,6 +106,13 @@ int spmv_csr_run_xwin(spmv_dims d, const int64_t *row_ptr, const int32_t *col, c
 int spmv_csr16_run(spmv_dims d, const int64_t *row_ptr, const int32_t *blk_base,
                    const uint16_t *col_off, const int32_t *col_esc, const double *val,
                    const double *x, double *y, int lanes_per_row);
+/* CSR16 on the x-window pipeline of spmv_csr_run_xwin (same chunks, same
+ * order: y bit-identical to it).  win/xcap from spmv_csr_xwin_build over
+ * the matrix's int32 columns with the same lanes_per_row/rows_per_window. */
+int spmv_csr16_run_xwin(spmv_dims d, const int64_t *row_ptr, const int32_t *blk_base,
+                        const uint16_t *col_off, const int32_t *col_esc, const double *val,
+                        const double *x, double *y, int lanes_per_row, int32_t rows_per_window,
+                        const void *win, int32_t xcap);
 /* CSR with fp32 values (§8f row 4): 8 bytes per entry instead of 12.  The
  * x-window kernel widens each value to fp64 and sums in fp64, so y equals
  * spmv_csr_run_xwin on the fp32-rounded values bit for bit (|y - y64| <=

@@ -13,6 +13,8 @@
 // Bytes per row: 12·len + 8 (row_ptr) + 8 (y), plus x gathers.
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "common.h"
 
 namespace spmv {
@@ -166,11 +168,18 @@ constexpr int kCsrBatchDefault = 0;
 // 64-entry block's columns span < 65536, else the block is stored whole in
 // esc (base = -1 - slot).  10.06 instead of 12 bytes per entry; the
 // columns, hence products and sums, are exactly CSR's.
+// Two-phase form for the pipelined kernels: raw(p) only issues loads (no
+// load depends on another), decode(raw, p) turns them into the column pair
+// (CSR16's escaped blocks load their int32 columns there, a second round
+// trip for those blocks only).
 template <bool NT>
 struct Col32 {
     const int32_t *__restrict__ col;
+    using Raw = int2;
     __device__ __forceinline__ int2 pair(int64_t p) const { return stream_load2<NT>(col + p); }
     __device__ __forceinline__ int32_t one(int64_t p) const { return stream_load<NT>(col + p); }
+    __device__ __forceinline__ Raw raw(int64_t p) const { return stream_load2<NT>(col + p); }
+    __device__ __forceinline__ int2 decode(Raw r, int64_t) const { return r; }
 };
 
 template <bool NT>
@@ -192,6 +201,20 @@ struct Col16 {
     {
         const int32_t b = base[p >> 6];
         return b >= 0 ? b + (int32_t)stream_load<NT>(off + p) : esc[(int64_t)(-1 - b) * 64 + (p & 63)];
+    }
+    struct Raw {
+        int32_t b;   // the block's base, or -1 - escape slot
+        uint32_t w;  // the pair's two 16-bit offsets
+    };
+    __device__ __forceinline__ Raw raw(int64_t p) const
+    {
+        return Raw{base[p >> 6], stream_load<NT>(reinterpret_cast<const uint32_t *>(off + p))};
+    }
+    __device__ __forceinline__ int2 decode(Raw r, int64_t p) const
+    {
+        if (r.b >= 0)
+            return int2{r.b + (int32_t)(r.w & 0xffffu), r.b + (int32_t)(r.w >> 16)};
+        return stream_load2<NT>(esc + (int64_t)(-1 - r.b) * 64 + (p & 63));
     }
 };
 
@@ -348,43 +371,47 @@ struct XConst {
 // pairs, loaded branch-free (pairs past the chunk load pair 0 and are
 // never summed), so all 2R loads are outstanding together and can stay in
 // flight across a barrier while the previous chunk is reduced.
-template <int R, bool NT, typename V>
+template <int R, bool NT, typename V, typename Cols = Col32<NT>>
 struct StreamRegs {
     double2 v[R];
-    int2 c[R];
+    typename Cols::Raw c[R];
+    int64_t q[R];  // the pair each lane loaded (decode needs it for escaped blocks only)
 
-    __device__ __forceinline__ void issue(int64_t cb, int64_t ce, int64_t nz, const int32_t *__restrict__ col,
+    __device__ __forceinline__ void issue(int64_t cb, int64_t ce, int64_t nz, const Cols &cols,
                                           const V *__restrict__ val)
     {
         if (nz < 2) {  // uniform; a 1-entry array has no pair 0 (its entry: products())
 #pragma unroll
             for (int k = 0; k < R; ++k) {
                 v[k] = double2{0.0, 0.0};
-                c[k] = int2{0, 0};
+                c[k] = cols.raw(0);
+                q[k] = 0;
             }
             return;
         }
 #pragma unroll
         for (int k = 0; k < R; ++k) {
             const int64_t p = cb + 2 * (int64_t)(threadIdx.x + k * kBlock);
-            const int64_t q = (p < ce && p + 1 < nz) ? p : 0;
-            v[k] = vpair<NT>(val + q);
-            c[k] = stream_load2<NT>(col + q);
+            q[k] = (p < ce && p + 1 < nz) ? p : 0;
+            v[k] = vpair<NT>(val + q[k]);
+            c[k] = cols.raw(q[k]);
         }
     }
 
     // products of the issued chunk [cb, ce) into s_prod (as stage_products)
     template <typename XS>
-    __device__ __forceinline__ void products(int64_t cb, int64_t ce, int64_t nz, const int32_t *__restrict__ col,
+    __device__ __forceinline__ void products(int64_t cb, int64_t ce, int64_t nz, const Cols &cols,
                                              const V *__restrict__ val, const XS &xs, double2 *s_prod) const
     {
 #pragma unroll
-        for (int k = 0; k < R; ++k)
-            s_prod[threadIdx.x + k * kBlock] = double2{v[k].x * xs(c[k].x), v[k].y * xs(c[k].y)};
+        for (int k = 0; k < R; ++k) {
+            const int2 cc = cols.decode(c[k], q[k]);
+            s_prod[threadIdx.x + k * kBlock] = double2{v[k].x * xs(cc.x), v[k].y * xs(cc.y)};
+        }
         const int64_t tail = nz - 1 - cb;  // the array's odd last entry
         if ((nz & 1) && nz - 1 < ce && tail >= 0 && tail < 2 * R * kBlock && (tail >> 1) % kBlock == threadIdx.x) {
             const int64_t p = nz - 1;
-            s_prod[tail >> 1].x = vone<NT>(val + p) * xs(col[p]);
+            s_prod[tail >> 1].x = vone<NT>(val + p) * xs(cols.one(p));
         }
     }
 };
@@ -399,12 +426,14 @@ struct StreamRegs {
 // NBUF = 2 (MODE 4): chunks alternate between two product buffers, so the
 // barrier that protected the buffer from the next chunk's products is gone
 // (one barrier per chunk); the caller adds a barrier before reusing LDS.
-template <int L, int R, bool NT, typename XS, typename V, int NBUF = 1, bool PRE = false>
+template <int L, int R, bool NT, typename XS, typename V, int NBUF = 1, bool PRE = false,
+          typename Cols = Col32<NT>>
 __device__ __forceinline__ void staged_window_pipelined(int64_t row0, int ngroups, const int64_t *s_off,
-                                                        double2 *s_prod_base, const int32_t *__restrict__ col,
+                                                        double2 *s_prod_base, const Cols cols,
                                                         const V *__restrict__ val, const XS xs,
                                                         double *__restrict__ y, int64_t n_rows, int64_t nz,
-                                                        const StreamRegs<R, NT, V> pre_st = {}, bool pre = false)
+                                                        const StreamRegs<R, NT, V, Cols> pre_st = {},
+                                                        bool pre = false)
 {
     constexpr int RPB = kBlock / L;
     constexpr int CH = 2 * kBlock * R;
@@ -419,7 +448,7 @@ __device__ __forceinline__ void staged_window_pipelined(int64_t row0, int ngroup
             ++j;
         return j;
     };
-    StreamRegs<R, NT, V> st;
+    StreamRegs<R, NT, V, Cols> st;
     int jn;
     if (PRE && pre) {  // the caller issued group 0's first chunk (it has one)
         st = pre_st;
@@ -428,7 +457,7 @@ __device__ __forceinline__ void staged_window_pipelined(int64_t row0, int ngroup
         jn = next_group(0);
         if (jn < ngroups) {
             const int64_t b = s_off[jn * RPB] & ~(int64_t)1, e = s_off[(jn + 1) * RPB];
-            st.issue(b, b + CH < e ? b + CH : e, nz, col, val);
+            st.issue(b, b + CH < e ? b + CH : e, nz, cols, val);
         }
     }
     for (int gi = 0; gi < ngroups; ++gi) {
@@ -441,17 +470,17 @@ __device__ __forceinline__ void staged_window_pipelined(int64_t row0, int ngroup
             double2 *s_prod = s_prod_base + buf * (kBlock * R);
             const double *prod = reinterpret_cast<const double *>(s_prod);
 #if SPMV_XWIN_PROBE & 1  // timing probe: no x gathers (wrong y)
-            st.products(cb, ce, nz, col, val, XConst{}, s_prod);
+            st.products(cb, ce, nz, cols, val, XConst{}, s_prod);
 #else
-            st.products(cb, ce, nz, col, val, xs, s_prod);
+            st.products(cb, ce, nz, cols, val, xs, s_prod);
 #endif
             // the next chunk: this group's, else the next group's first
             if (cb + CH < blk_end) {
                 const int64_t nb = cb + CH;
-                st.issue(nb, nb + CH < blk_end ? nb + CH : blk_end, nz, col, val);
+                st.issue(nb, nb + CH < blk_end ? nb + CH : blk_end, nz, cols, val);
             } else if ((jn = next_group(gi + 1)) < ngroups) {
                 const int64_t b = s_off[jn * RPB] & ~(int64_t)1, e = s_off[(jn + 1) * RPB];
-                st.issue(b, b + CH < e ? b + CH : e, nz, col, val);
+                st.issue(b, b + CH < e ? b + CH : e, nz, cols, val);
             }
             __syncthreads();
 #if SPMV_XWIN_PROBE & 2  // timing probe: one product per lane instead of the row slice (wrong y)
@@ -481,9 +510,9 @@ __device__ __forceinline__ void staged_window_pipelined(int64_t row0, int ngroup
 // the window (WR = RW·256/L rows) and adds each chunk's slice of each row.
 // Rows that lie in one chunk sum exactly as in the other modes; a row cut
 // by a chunk boundary is summed in the same order over other boundaries.
-template <int L, int R, int RW, bool NT, typename XS, typename V>
+template <int L, int R, int RW, bool NT, typename XS, typename V, typename Cols>
 __device__ __forceinline__ void staged_window_flat(int64_t row0, const int64_t *s_off, double2 *s_prod,
-                                                   const int32_t *__restrict__ col, const V *__restrict__ val,
+                                                   const Cols cols, const V *__restrict__ val,
                                                    const XS xs, double *__restrict__ y, int64_t n_rows, int64_t nz)
 {
     constexpr int G = kBlock / L;
@@ -502,15 +531,15 @@ __device__ __forceinline__ void staged_window_flat(int64_t row0, const int64_t *
 #pragma unroll
     for (int k = 0; k < RW; ++k)
         acc[k] = 0.0;
-    StreamRegs<R, NT, V> st;
+    StreamRegs<R, NT, V, Cols> st;
     if (nch > 0)
-        st.issue(e0, e0 + cs < e1 ? e0 + cs : e1, nz, col, val);
+        st.issue(e0, e0 + cs < e1 ? e0 + cs : e1, nz, cols, val);
     for (int64_t c = 0; c < nch; ++c) {
         const int64_t cb = e0 + c * cs;
         const int64_t ce = cb + cs < e1 ? cb + cs : e1;
-        st.products(cb, ce, nz, col, val, xs, s_prod);
+        st.products(cb, ce, nz, cols, val, xs, s_prod);
         if (c + 1 < nch)
-            st.issue(ce, ce + cs < e1 ? ce + cs : e1, nz, col, val);
+            st.issue(ce, ce + cs < e1 ? ce + cs : e1, nz, cols, val);
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < RW; ++k) {
@@ -628,10 +657,10 @@ __global__ __launch_bounds__(kBlock) void csr_window_kernel(int64_t n_rows, int6
 #define SPMV_XWIN_WAVES 1
 #endif
 constexpr int kXwinWaves = SPMV_XWIN_WAVES;
-template <int L, int R, bool NT, typename V = double, int MODE = 0, bool PRE = false>
+template <int L, int R, bool NT, typename V = double, int MODE = 0, bool PRE = false, typename Cols = Col32<NT>>
 __global__ __launch_bounds__(kBlock, MODE >= 3 ? kXwinWaves : 1) void csr_xwin_kernel(
     int64_t n_rows, int64_t n_groups, int64_t gpw, const int64_t *__restrict__ row_ptr,
-    const int32_t *__restrict__ col, const V *__restrict__ val,
+    const Cols cols, const V *__restrict__ val,
     const double *__restrict__ x, double *__restrict__ y, const int2 *__restrict__ win, int32_t xcap,
     int remap)
 {
@@ -655,7 +684,7 @@ __global__ __launch_bounds__(kBlock, MODE >= 3 ? kXwinWaves : 1) void csr_xwin_k
         // window copy — its range needs only two row offsets, loaded beside
         // the window bounds — so the copy and the first chunk's loads share
         // one round trip instead of following each other
-        StreamRegs<R, NT, V> st_pre;
+        StreamRegs<R, NT, V, Cols> st_pre;
         bool pre = false;
         if constexpr (MODE == 3 && PRE) {
             const int64_t rr0 = g_beg * RPB;
@@ -663,7 +692,7 @@ __global__ __launch_bounds__(kBlock, MODE >= 3 ? kXwinWaves : 1) void csr_xwin_k
             const int64_t b = row_ptr[rr0] & ~(int64_t)1, e = row_ptr[rr1];
             pre = b < e;  // uniform
             if (pre)
-                st_pre.issue(b, b + 2 * kBlock * R < e ? b + 2 * kBlock * R : e, nz, col, val);
+                st_pre.issue(b, b + 2 * kBlock * R < e ? b + 2 * kBlock * R : e, nz, cols, val);
         }
         if constexpr (MODE > 0) {
             // offsets r0 .. r0 + nr of the window's rows (clamped past
@@ -698,21 +727,21 @@ __global__ __launch_bounds__(kBlock, MODE >= 3 ? kXwinWaves : 1) void csr_xwin_k
             __syncthreads();  // window and offsets visible
             const int64_t r0 = g_beg * RPB;
             if (staged)
-                staged_window_flat<L, R, RW, NT>(r0, s_off, s_prod, col, val, XWindow{s_x, wnd.x}, y, n_rows, nz);
+                staged_window_flat<L, R, RW, NT>(r0, s_off, s_prod, cols, val, XWindow{s_x, wnd.x}, y, n_rows, nz);
             else
-                staged_window_flat<L, R, RW, NT>(r0, s_off, s_prod, col, val, XGlobal{x}, y, n_rows, nz);
+                staged_window_flat<L, R, RW, NT>(r0, s_off, s_prod, cols, val, XGlobal{x}, y, n_rows, nz);
             continue;
         }
         if constexpr (MODE >= 3) {
             constexpr int NB = MODE == 4 ? 2 : 1;
             __syncthreads();  // window and offsets visible
             if (staged)
-                staged_window_pipelined<L, R, NT, XWindow, V, NB, PRE>(g_beg * RPB, (int)(g_end - g_beg), s_off,
-                                                                       s_prod, col, val, XWindow{s_x, wnd.x}, y,
+                staged_window_pipelined<L, R, NT, XWindow, V, NB, PRE, Cols>(g_beg * RPB, (int)(g_end - g_beg), s_off,
+                                                                       s_prod, cols, val, XWindow{s_x, wnd.x}, y,
                                                                        n_rows, nz, st_pre, pre);
             else
-                staged_window_pipelined<L, R, NT, XGlobal, V, NB, PRE>(g_beg * RPB, (int)(g_end - g_beg), s_off,
-                                                                       s_prod, col, val, XGlobal{x}, y, n_rows,
+                staged_window_pipelined<L, R, NT, XGlobal, V, NB, PRE, Cols>(g_beg * RPB, (int)(g_end - g_beg), s_off,
+                                                                       s_prod, cols, val, XGlobal{x}, y, n_rows,
                                                                        nz, st_pre, pre);
             if constexpr (NB == 2)
                 __syncthreads();  // the last chunk's buffer is read before the next window writes LDS
@@ -733,10 +762,10 @@ __global__ __launch_bounds__(kBlock, MODE >= 3 ? kXwinWaves : 1) void csr_xwin_k
             }
             const int64_t row = grp * RPB + threadIdx.x / L;
             if (staged)
-                staged_group<L, R, NT, Col32<NT>, BATCH, XWindow, V>(row, gp, s_prod, Col32<NT>{col}, val,
+                staged_group<L, R, NT, Cols, BATCH, XWindow, V>(row, gp, s_prod, cols, val,
                                                                      XWindow{s_x, wnd.x}, y, n_rows, nz);
             else
-                staged_group<L, R, NT, Col32<NT>, BATCH, XGlobal, V>(row, gp, s_prod, Col32<NT>{col}, val,
+                staged_group<L, R, NT, Cols, BATCH, XGlobal, V>(row, gp, s_prod, cols, val,
                                                                      XGlobal{x}, y, n_rows, nz);
         }
     }
@@ -1328,8 +1357,8 @@ static int64_t csr_xwin_gpw(int L, int32_t rows_per_window)
     return g < 1 ? 1 : g;
 }
 
-template <int L, int R, bool NT>
-static void launch_csr_xwin(const spmv_dims &d, const int64_t *row_ptr, const int32_t *col,
+template <int L, int R, bool NT, typename Cols>
+static void launch_csr_xwin(const spmv_dims &d, const int64_t *row_ptr, const Cols cols,
                             const double *val, const double *x, double *y, const int2 *win, int32_t xcap,
                             int64_t gpw)
 {
@@ -1341,29 +1370,31 @@ static void launch_csr_xwin(const spmv_dims &d, const int64_t *row_ptr, const in
     // one workgroup per window (the dispatcher balances) unless
     // SPMV_CSR_XWIN_PERSISTENT=1 (resident workgroups walk the windows)
     const char *ps = getenv("SPMV_CSR_XWIN_PERSISTENT");
-    const int64_t grid = (ps && ps[0] == '1') ? persistent_grid(csr_xwin_kernel<L, R, NT>, n_win, lds) : n_win;
+    const int64_t grid = (ps && ps[0] == '1') ? persistent_grid(csr_xwin_kernel<L, R, NT, double, 0, false, Cols>, n_win, lds) : n_win;
     if (grid > INT32_MAX)
         return;
     const int remap = csr_xwin_remap_rule(xcap, gpw * RPB) ? 1 : 0;
     const hipStream_t st = (hipStream_t)d.stream;
-    if (csr_xwin_prefetch()) {
-        const size_t lds0 = (size_t)xcap * sizeof(double);
-        hipLaunchKernelGGL((csr_xwin_pf_kernel<L, R, NT>), dim3((unsigned)grid), dim3(kBlock), lds0, st, d.n_rows,
-                           groups, gpw, row_ptr, col, val, x, y, win, xcap);
-        return;
+    if constexpr (std::is_same<Cols, Col32<NT>>::value) {  // the round-1 prefetch kernel reads int32 columns
+        if (csr_xwin_prefetch()) {
+            const size_t lds0 = (size_t)xcap * sizeof(double);
+            hipLaunchKernelGGL((csr_xwin_pf_kernel<L, R, NT>), dim3((unsigned)grid), dim3(kBlock), lds0, st, d.n_rows,
+                               groups, gpw, row_ptr, cols.col, val, x, y, win, xcap);
+            return;
+        }
     }
     switch (mode) {
     case 0:
-        hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, double, 0>), dim3((unsigned)grid), dim3(kBlock), lds, st,
-                           d.n_rows, groups, gpw, row_ptr, col, val, x, y, win, xcap, remap);
+        hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, double, 0, false, Cols>), dim3((unsigned)grid), dim3(kBlock), lds, st,
+                           d.n_rows, groups, gpw, row_ptr, cols, val, x, y, win, xcap, remap);
         break;
     case 1:
-        hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, double, 1>), dim3((unsigned)grid), dim3(kBlock), lds, st,
-                           d.n_rows, groups, gpw, row_ptr, col, val, x, y, win, xcap, remap);
+        hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, double, 1, false, Cols>), dim3((unsigned)grid), dim3(kBlock), lds, st,
+                           d.n_rows, groups, gpw, row_ptr, cols, val, x, y, win, xcap, remap);
         break;
     case 2:
-        hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, double, 2>), dim3((unsigned)grid), dim3(kBlock), lds, st,
-                           d.n_rows, groups, gpw, row_ptr, col, val, x, y, win, xcap, remap);
+        hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, double, 2, false, Cols>), dim3((unsigned)grid), dim3(kBlock), lds, st,
+                           d.n_rows, groups, gpw, row_ptr, cols, val, x, y, win, xcap, remap);
         break;
     case 3:
         if constexpr (NT) {  // SPMV_CSR_XWIN_R: pairs per lane per chunk (sweep knob)
@@ -1371,8 +1402,8 @@ static void launch_csr_xwin(const spmv_dims &d, const int64_t *row_ptr, const in
             if (rr != 0 && rr != R) {
                 const size_t l2 = lds;  // the chunk buffer is static LDS
 #define SPMV_XWIN_R(RR)                                                                                      \
-    hipLaunchKernelGGL((csr_xwin_kernel<L, RR, NT, double, 3>), dim3((unsigned)grid), dim3(kBlock), l2, st, \
-                       d.n_rows, groups, gpw, row_ptr, col, val, x, y, win, xcap, remap)
+    hipLaunchKernelGGL((csr_xwin_kernel<L, RR, NT, double, 3, false, Cols>), dim3((unsigned)grid), dim3(kBlock), l2, st, \
+                       d.n_rows, groups, gpw, row_ptr, cols, val, x, y, win, xcap, remap)
                 switch (rr) {
                 case 2: SPMV_XWIN_R(2); return;
                 case 3: SPMV_XWIN_R(3); return;
@@ -1385,22 +1416,22 @@ static void launch_csr_xwin(const spmv_dims &d, const int64_t *row_ptr, const in
             }
         }
         if (csr_xwin_pre())
-            hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, double, 3, true>), dim3((unsigned)grid), dim3(kBlock), lds,
-                               st, d.n_rows, groups, gpw, row_ptr, col, val, x, y, win, xcap, remap);
+            hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, double, 3, true, Cols>), dim3((unsigned)grid), dim3(kBlock), lds,
+                               st, d.n_rows, groups, gpw, row_ptr, cols, val, x, y, win, xcap, remap);
         else
-            hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, double, 3>), dim3((unsigned)grid), dim3(kBlock), lds, st,
-                               d.n_rows, groups, gpw, row_ptr, col, val, x, y, win, xcap, remap);
+            hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, double, 3, false, Cols>), dim3((unsigned)grid), dim3(kBlock), lds, st,
+                               d.n_rows, groups, gpw, row_ptr, cols, val, x, y, win, xcap, remap);
         break;
     case 4:
-        hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, double, 4>), dim3((unsigned)grid), dim3(kBlock), lds, st,
-                           d.n_rows, groups, gpw, row_ptr, col, val, x, y, win, xcap, remap);
+        hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, double, 4, false, Cols>), dim3((unsigned)grid), dim3(kBlock), lds, st,
+                           d.n_rows, groups, gpw, row_ptr, cols, val, x, y, win, xcap, remap);
         break;
     case 5:
         if (gpw == 1 || gpw == 2 || gpw == 4) {
             const bool r3 = NT && csr_xwin_rounds() == 3 && R != 3;  // SPMV_CSR_XWIN_R (sweep knob)
 #define SPMV_FLAT(RR, MM)                                                                                     \
-    hipLaunchKernelGGL((csr_xwin_kernel<L, RR, NT, double, MM>), dim3((unsigned)grid), dim3(kBlock), lds, st, \
-                       d.n_rows, groups, gpw, row_ptr, col, val, x, y, win, xcap, remap)
+    hipLaunchKernelGGL((csr_xwin_kernel<L, RR, NT, double, MM, false, Cols>), dim3((unsigned)grid), dim3(kBlock), lds, st, \
+                       d.n_rows, groups, gpw, row_ptr, cols, val, x, y, win, xcap, remap)
             if (gpw == 1) {
                 if (r3) SPMV_FLAT(3, 5); else SPMV_FLAT(R, 5);
             } else if (gpw == 2) {
@@ -1410,8 +1441,8 @@ static void launch_csr_xwin(const spmv_dims &d, const int64_t *row_ptr, const in
             }
 #undef SPMV_FLAT
         } else {
-            hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, double, 3>), dim3((unsigned)grid), dim3(kBlock), lds, st,
-                               d.n_rows, groups, gpw, row_ptr, col, val, x, y, win, xcap, remap);
+            hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, double, 3, false, Cols>), dim3((unsigned)grid), dim3(kBlock), lds, st,
+                               d.n_rows, groups, gpw, row_ptr, cols, val, x, y, win, xcap, remap);
         }
         break;
     }
@@ -1512,10 +1543,10 @@ extern "C" int spmv_csr_run_xwin(spmv_dims d, const int64_t *row_ptr, const int3
     const bool direct = csr_xwin_direct();
 #define SPMV_XWIN(LL)                                                                          \
     (direct ? launch_csr_vector_xwin<LL>(d, row_ptr, col, val, x, y, w, xcap, gpw)             \
-     : nt   ? (r4 ? launch_csr_xwin<LL, 4, true>(d, row_ptr, col, val, x, y, w, xcap, gpw)     \
-                  : launch_csr_xwin<LL, 3, true>(d, row_ptr, col, val, x, y, w, xcap, gpw))    \
-            : (r4 ? launch_csr_xwin<LL, 4, false>(d, row_ptr, col, val, x, y, w, xcap, gpw)    \
-                  : launch_csr_xwin<LL, 3, false>(d, row_ptr, col, val, x, y, w, xcap, gpw)))
+     : nt   ? (r4 ? launch_csr_xwin<LL, 4, true>(d, row_ptr, Col32<true>{col}, val, x, y, w, xcap, gpw)   \
+                  : launch_csr_xwin<LL, 3, true>(d, row_ptr, Col32<true>{col}, val, x, y, w, xcap, gpw))  \
+            : (r4 ? launch_csr_xwin<LL, 4, false>(d, row_ptr, Col32<false>{col}, val, x, y, w, xcap, gpw) \
+                  : launch_csr_xwin<LL, 3, false>(d, row_ptr, Col32<false>{col}, val, x, y, w, xcap, gpw)))
     switch (L) {
     case 2: SPMV_XWIN(2); break;
     case 4: SPMV_XWIN(4); break;
@@ -1558,6 +1589,57 @@ extern "C" int spmv_csr16_run(spmv_dims d, const int64_t *row_ptr, const int32_t
     }
 #undef SPMV_CSR16
     SPMV_CHECK_LAUNCH("csr16 kernel");
+    return SPMV_SUCCESS;
+}
+
+// CSR16 on the x-window pipeline: the same kernel, load schedule and chunks
+// as spmv_csr_run_xwin with the columns decoded from the 16-bit offsets
+// (escaped blocks from their int32 copy), so y is bit-identical to it.
+// Windows from spmv_csr_xwin_build over the CSR's int32 columns (the same
+// column values) with the same lanes_per_row and rows_per_window.
+extern "C" int spmv_csr16_run_xwin(spmv_dims d, const int64_t *row_ptr, const int32_t *blk_base,
+                                   const uint16_t *col_off, const int32_t *col_esc, const double *val,
+                                   const double *x, double *y, int lanes_per_row, int32_t rows_per_window,
+                                   const void *win, int32_t xcap)
+{
+    if (d.n_rows < 0 || d.n_cols < 0 || d.nnz < 0 || rows_per_window < 0)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_csr16_run_xwin: bad sizes");
+    if (d.n_rows == 0)
+        return SPMV_SUCCESS;
+    if (d.nnz > 0 && (!blk_base || !col_off))
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_csr16_run_xwin: missing index arrays");
+    if (!win || xcap < 0 || xcap > kCsrXwinCap)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_csr16_run_xwin: bad window arguments");
+    SPMV_GUARD(d);
+    const int L = lanes_per_row > 0 ? lanes_per_row : spmv_csr_auto_lanes(d.n_rows, d.nnz);
+    if (L < 2 || L > 64 || (L & (L - 1)))
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_csr16_run_xwin: lanes_per_row must be 0 or a power of two in [2,64]");
+    const int64_t gpw = csr_xwin_gpw(L, rows_per_window);
+    const bool nt = stream_nt(kCsrXwinNtDefault);
+    const bool r4 = csr_stage_rounds(d.n_rows, d.nnz, L) == 4;
+    const int2 *w = (const int2 *)win;
+#define SPMV_XWIN16(LL)                                                                                           \
+    do {                                                                                                          \
+        if (nt) {                                                                                                 \
+            const Col16<true> cs{blk_base, col_off, col_esc};                                                     \
+            if (r4) launch_csr_xwin<LL, 4, true>(d, row_ptr, cs, val, x, y, w, xcap, gpw);                        \
+            else launch_csr_xwin<LL, 3, true>(d, row_ptr, cs, val, x, y, w, xcap, gpw);                           \
+        } else {                                                                                                  \
+            const Col16<false> cs{blk_base, col_off, col_esc};                                                    \
+            if (r4) launch_csr_xwin<LL, 4, false>(d, row_ptr, cs, val, x, y, w, xcap, gpw);                       \
+            else launch_csr_xwin<LL, 3, false>(d, row_ptr, cs, val, x, y, w, xcap, gpw);                          \
+        }                                                                                                         \
+    } while (0)
+    switch (L) {
+    case 2: SPMV_XWIN16(2); break;
+    case 4: SPMV_XWIN16(4); break;
+    case 8: SPMV_XWIN16(8); break;
+    case 16: SPMV_XWIN16(16); break;
+    case 32: SPMV_XWIN16(32); break;
+    default: SPMV_XWIN16(64); break;
+    }
+#undef SPMV_XWIN16
+    SPMV_CHECK_LAUNCH("csr_xwin_kernel (16-bit columns)");
     return SPMV_SUCCESS;
 }
 
@@ -1668,19 +1750,19 @@ extern "C" int spmv_csr_f32v_run_xwin(spmv_dims d, const int64_t *row_ptr, const
         const bool r4 = csr_stage_rounds(d.n_rows, d.nnz, LL) == 4;                                         \
         if (nt && r4)                                                                                       \
             hipLaunchKernelGGL((csr_xwin_kernel<LL, 4, true, float, kCsrXwinMode>), dim3((unsigned)n_win),  \
-                               dim3(kBlock), lds, (hipStream_t)d.stream, d.n_rows, groups, gpw, row_ptr, col, \
+                               dim3(kBlock), lds, (hipStream_t)d.stream, d.n_rows, groups, gpw, row_ptr, Col32<true>{col}, \
                                val, x, y, w, xcap, remap);                                                  \
         else if (nt)                                                                                        \
             hipLaunchKernelGGL((csr_xwin_kernel<LL, 3, true, float, kCsrXwinMode>), dim3((unsigned)n_win),  \
-                               dim3(kBlock), lds, (hipStream_t)d.stream, d.n_rows, groups, gpw, row_ptr, col, \
+                               dim3(kBlock), lds, (hipStream_t)d.stream, d.n_rows, groups, gpw, row_ptr, Col32<true>{col}, \
                                val, x, y, w, xcap, remap);                                                  \
         else if (r4)                                                                                        \
             hipLaunchKernelGGL((csr_xwin_kernel<LL, 4, false, float, kCsrXwinMode>), dim3((unsigned)n_win), \
-                               dim3(kBlock), lds, (hipStream_t)d.stream, d.n_rows, groups, gpw, row_ptr, col, \
+                               dim3(kBlock), lds, (hipStream_t)d.stream, d.n_rows, groups, gpw, row_ptr, Col32<false>{col}, \
                                val, x, y, w, xcap, remap);                                                  \
         else                                                                                                \
             hipLaunchKernelGGL((csr_xwin_kernel<LL, 3, false, float, kCsrXwinMode>), dim3((unsigned)n_win), \
-                               dim3(kBlock), lds, (hipStream_t)d.stream, d.n_rows, groups, gpw, row_ptr, col, \
+                               dim3(kBlock), lds, (hipStream_t)d.stream, d.n_rows, groups, gpw, row_ptr, Col32<false>{col}, \
                                val, x, y, w, xcap, remap);                                                  \
     } while (0)
     switch (L) {

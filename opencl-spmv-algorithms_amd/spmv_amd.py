@@ -93,6 +93,8 @@ HIP_SYMBOLS = {
     "spmv_csr_tiled_plan_len": (_c_i64, [_c_i64]),
     "spmv_csr_tiled_plan": (ctypes.c_int, [Dims, _vp, _vp]),
     "spmv_csr16_run": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_int]),
+    "spmv_csr16_run_xwin": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_int, _c_i32, _vp,
+                                           _c_i32]),
     "spmv_hyb_ws_bytes": (ctypes.c_size_t, [_c_i64]),
     "spmv_hyb_run": (ctypes.c_int, [Dims, _c_i32, _c_i64, _c_i32, _vp, _vp, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp,
                                     ctypes.c_size_t]),
@@ -596,6 +598,10 @@ class DeviceMatrix:
         elif self.fmt == "csrf32":
             rc = lib.spmv_csr_f32v_run_xwin(d, _ptr(a["row_ptr"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
                                             p["lanes"], p.get("xwin_rows", 0), _ptr(a["win"]), p["xcap"])
+        elif self.fmt == "csr16" and "win" in a:
+            rc = lib.spmv_csr16_run_xwin(d, _ptr(a["row_ptr"]), _ptr(a["blk_base"]), _ptr(a["col_off"]),
+                                         _ptr(a["col_esc"]), _ptr(a["val"]), _ptr(x), _ptr(y), p["lanes"],
+                                         p.get("xwin_rows", 0), _ptr(a["win"]), p["xcap"])
         elif self.fmt == "csr16":
             rc = lib.spmv_csr16_run(d, _ptr(a["row_ptr"]), _ptr(a["blk_base"]), _ptr(a["col_off"]),
                                     _ptr(a["col_esc"]), _ptr(a["val"]), _ptr(x), _ptr(y), p["lanes"])
@@ -794,7 +800,7 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
     if xwin is None:
         # COO: per-tile windows measured slower (0.534 vs 0.491 ms on the
         # cant-like batch), so they stay opt-in; CMRS 0.352 vs 0.404 ms
-        xwin = fmt in ("csr", "ell", "sell", "cmrs")
+        xwin = fmt in ("csr", "csr16", "ell", "sell", "cmrs")
     device = torch.device(device)
     dm = DeviceMatrix(fmt, m.n_rows, m.n_cols, m.nnz, device)
     if fmt == "coo":
@@ -871,6 +877,14 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
                          col_off=_dev_tensor(c["col_off"], device), col_esc=_dev_tensor(c["col_esc"], device),
                          val=_dev_tensor(val, device))
         dm.stored_bytes = 10 * m.nnz + 4 * c["n_blocks"] + 256 * c["n_esc"] + 8 * (m.n_rows + 1)
+        if xwin:
+            # windows of the x-window pipeline from the int32 columns (the
+            # same values), uploaded only for the build
+            dm.arrays["col"] = _dev_tensor(col, device)
+            dm.params["xwin_rows"] = xwin_rows
+            _csr_xwin(dm)
+            dm.params.pop("variant", None)
+            del dm.arrays["col"]
     elif fmt == "ell":
         ki = ki or 2  # measured best for ELL (profiles/round1_sweep.md)
         e = ell_build(m.n_rows, ptr, col, val, ki=ki, max_padding=ell_max_padding)
@@ -933,7 +947,7 @@ def device_build(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, ki: int =
     if fmt not in ("csr", "ell", "sell", "cmrs"):
         raise SpmvError(OTHER_ERROR, "device_build", "format must be csr, ell, sell or cmrs")
     if xwin is None:
-        xwin = fmt in ("csr", "ell", "sell", "cmrs")
+        xwin = fmt in ("csr", "csr16", "ell", "sell", "cmrs")
     lib = hip_lib()
     N, Z = m.n_rows, m.nnz
     d_row, d_col, d_val = (_dev_tensor(a, device) for a in (m.row, m.col, m.val))

@@ -74,15 +74,21 @@ struct KeysNone {  // the tiled CSR: rows come from row_ptr, no keys
 // straddles ce reads one entry past the chunk, inside the array, that no
 // reduction reads.  The array's odd last entry is loaded singly.
 // NT: non-temporal stream loads.
-template <int R, bool NT = false, typename XS, typename Keys, typename V>
-__device__ __forceinline__ void stage_chunk(int64_t cb, int64_t ce, int64_t nz, const int32_t *__restrict__ col,
-                                            const V *__restrict__ val, const XS &xs,
-                                            double2 *s_prod, const Keys &keys)
-{
+// stage_chunk in two halves: issue() puts a lane's 3R pair loads in flight,
+// commit() writes the products and keys of the issued chunk to LDS.  A
+// kernel may issue the next chunk between a commit and the barrier that
+// publishes it (software pipelining), with the same result as stage_chunk.
+template <int R, bool NT, typename V, typename Keys>
+struct StageRegs {
     double2 v[R];
     int2 c[R];
     typename Keys::P kp[R];
-    if (nz >= 2) {  // uniform; a 1-entry array has no pair 0 (its entry: the tail below)
+
+    __device__ __forceinline__ void issue(int64_t cb, int64_t ce, int64_t nz, const int32_t *__restrict__ col,
+                                          const V *__restrict__ val, const Keys &keys)
+    {
+        if (nz < 2)  // uniform; a 1-entry array has no pair 0 (its entry: the tail in commit)
+            return;
 #pragma unroll
         for (int k = 0; k < R; ++k) {
             const int64_t p = cb + 2 * (int64_t)(threadIdx.x + k * kBlock);
@@ -91,20 +97,47 @@ __device__ __forceinline__ void stage_chunk(int64_t cb, int64_t ce, int64_t nz, 
             c[k] = stream_load2<NT>(col + q);
             kp[k] = keys.load(q);
         }
+    }
+
+    template <typename XS>
+    __device__ __forceinline__ void commit(int64_t cb, int64_t ce, int64_t nz, const int32_t *__restrict__ col,
+                                           const V *__restrict__ val, const XS &xs, double2 *s_prod,
+                                           const Keys &keys) const
+    {
+        if (nz >= 2) {
 #pragma unroll
-        for (int k = 0; k < R; ++k) {
-            const int t = threadIdx.x + k * kBlock;
-            s_prod[t] = double2{v[k].x * xs(c[k].x), v[k].y * xs(c[k].y)};
-            keys.store(t, kp[k]);
+            for (int k = 0; k < R; ++k) {
+                const int t = threadIdx.x + k * kBlock;
+                s_prod[t] = double2{v[k].x * xs(c[k].x), v[k].y * xs(c[k].y)};
+                keys.store(t, kp[k]);
+            }
+        }
+        const int64_t tail = nz - 1 - cb;
+        if ((nz & 1) && nz - 1 < ce && tail >= 0 && tail < 2 * R * kBlock && (tail >> 1) % kBlock == threadIdx.x) {
+            const int64_t p = nz - 1;
+            const int t = (int)(tail >> 1);
+            s_prod[t] = double2{vone<NT>(val + p) * xs(stream_load<NT>(col + p)), 0.0};
+            keys.one(t, p);
         }
     }
-    const int64_t tail = nz - 1 - cb;
-    if ((nz & 1) && nz - 1 < ce && tail >= 0 && tail < 2 * R * kBlock && (tail >> 1) % kBlock == threadIdx.x) {
-        const int64_t p = nz - 1;
-        const int t = (int)(tail >> 1);
-        s_prod[t] = double2{vone<NT>(val + p) * xs(stream_load<NT>(col + p)), 0.0};
-        keys.one(t, p);
-    }
+};
+
+// Streams entries [cb, ce) (cb even) of an nz-entry array into LDS:
+// products in s_prod, row keys through `keys`.  Every lane issues its R
+// value, column and key pair loads before the first product (branch-free:
+// a pair starting at or past ce loads pair 0, a cached line, and is never
+// read back), so 3R loads per lane are in flight together; a pair that
+// straddles ce reads one entry past the chunk, inside the array, that no
+// reduction reads.  The array's odd last entry is loaded singly.
+// NT: non-temporal stream loads.
+template <int R, bool NT = false, typename XS, typename Keys, typename V>
+__device__ __forceinline__ void stage_chunk(int64_t cb, int64_t ce, int64_t nz, const int32_t *__restrict__ col,
+                                            const V *__restrict__ val, const XS &xs,
+                                            double2 *s_prod, const Keys &keys)
+{
+    StageRegs<R, NT, V, Keys> st;
+    st.issue(cb, ce, nz, col, val, keys);
+    st.commit(cb, ce, nz, col, val, xs, s_prod, keys);
 }
 
 // ------------------------------------------------------------------ CMRS
@@ -114,7 +147,7 @@ __device__ __forceinline__ void stage_chunk(int64_t cb, int64_t ce, int64_t nz, 
 // products gather from LDS; a window wider than xcap gathers from global
 // memory.  Same products, same order: y is bit-identical either way.
 // NT: non-temporal loads of the entry stream.
-template <int L, int R, bool XW, bool NT = false>
+template <int L, int R, bool XW, bool NT = false, bool PIPE = false>
 __global__ __launch_bounds__(kBlock) void cmrs_staged_kernel(
     int64_t n_rows, int32_t h, int32_t G, int64_t n_strips,
     const int64_t *__restrict__ strip_ptr, const uint8_t *__restrict__ rin,
@@ -158,12 +191,26 @@ __global__ __launch_bounds__(kBlock) void cmrs_staged_kernel(
     const int64_t nz = strip_ptr[n_strips];
 
     double acc = 0.0;
-    for (int64_t cb = s_sp[0] & ~(int64_t)1; cb < blk_end; cb += CH) {
+    // PIPE: the next chunk's loads are issued before this chunk's barrier
+    // and reduction (as the MODE 3 CSR kernel); same chunks, same bits
+    StageRegs<R, NT, double, KeysU8> st;
+    const int64_t c0 = s_sp[0] & ~(int64_t)1;
+    if (PIPE && c0 < blk_end)
+        st.issue(c0, c0 + CH < blk_end ? c0 + CH : blk_end, nz, col, val, keys);
+    for (int64_t cb = c0; cb < blk_end; cb += CH) {
         const int64_t ce = cb + CH < blk_end ? cb + CH : blk_end;
-        if (staged)
+        if constexpr (PIPE) {
+            if (staged)
+                st.commit(cb, ce, nz, col, val, XWindow{s_x, wlo}, s_prod, keys);
+            else
+                st.commit(cb, ce, nz, col, val, XGlobal{x}, s_prod, keys);
+            if (ce < blk_end)
+                st.issue(ce, ce + CH < blk_end ? ce + CH : blk_end, nz, col, val, keys);
+        } else if (staged) {
             stage_chunk<R, NT>(cb, ce, nz, col, val, XWindow{s_x, wlo}, s_prod, keys);
-        else
+        } else {
             stage_chunk<R, NT>(cb, ce, nz, col, val, XGlobal{x}, s_prod, keys);
+        }
         __syncthreads();
         const int64_t lo = sb > cb ? sb : cb;
         const int64_t hi = se < ce ? se : ce;
@@ -660,6 +707,14 @@ void cmrs_geometry(const spmv_dims &d, int32_t h, int64_t n_strips, int *L, int 
     *blocks = (n_strips + *G - 1) / *G;
 }
 
+// SPMV_CMRS_PIPE=0/1: the pipelined CMRS chunk loop (read per call; A/B knob)
+constexpr bool kCmrsPipe = false;
+static bool cmrs_pipe()
+{
+    const char *s = getenv("SPMV_CMRS_PIPE");
+    return s && (s[0] == '0' || s[0] == '1') ? s[0] == '1' : kCmrsPipe;
+}
+
 int launch_cmrs_staged(const spmv_dims &d, int32_t h, int64_t n_strips,
                        const int64_t *strip_ptr, const uint8_t *rin, const int32_t *col,
                        const double *val, const double *x, double *y, const int2 *win, int32_t xcap)
@@ -673,9 +728,14 @@ int launch_cmrs_staged(const spmv_dims &d, int32_t h, int64_t n_strips,
     constexpr int R = 3;
     const size_t lds = win ? (size_t)xcap * sizeof(double) : 0;
     const bool nt = stream_nt(true);  // +5 % on the cant batch (0.321 vs 0.338 ms)
+    const bool pipe = cmrs_pipe();
 #define SPMV_CMRS_STAGED(LL)                                                                            \
     do {                                                                                                \
-        if (win && nt)                                                                                  \
+        if (win && nt && pipe)                                                                          \
+            hipLaunchKernelGGL((cmrs_staged_kernel<LL, R, true, true, true>), dim3((unsigned)blocks),    \
+                               dim3(kBlock), lds, st, d.n_rows, h, G, n_strips, strip_ptr, rin, col, val, \
+                               x, y, win, xcap);                                                        \
+        else if (win && nt)                                                                             \
             hipLaunchKernelGGL((cmrs_staged_kernel<LL, R, true, true>), dim3((unsigned)blocks),          \
                                dim3(kBlock), lds, st, d.n_rows, h, G, n_strips, strip_ptr, rin, col, val, \
                                x, y, win, xcap);                                                        \

@@ -113,6 +113,8 @@ for s in "${steps[@]}"; do
                   run ab_sellcopy_cant_new_$i 300 python tools/ab_env.py --format sell --rounds 3
                 done;;
     test16) run gpu_tests_csr16 900 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "csr16 or csrf32 or xwin";;
+    abcmrspipe) run ab_cmrs_pipe 300 python tools/ab_env.py --format cmrs --env SPMV_CMRS_PIPE=0,1 --rounds 5 &&
+                run ab_cmrs_pipe_h16 300 python tools/ab_env.py --format cmrs --kw '{"h": 16}' --env SPMV_CMRS_PIPE=0,1 --rounds 4;;
     abxwin) run ab_csr_xwin_mode 600 python tools/ab_env.py --format csr --env SPMV_CSR_XWIN_MODE=0,2,3 --rounds 5;;
     cmrsnt) run cmrs_base 300 python bench.py --format cmrs --per-format no --cpu-seconds 0 &&
             SPMV_STREAM_NT=1 run cmrs_nt 300 python bench.py --format cmrs --per-format no --cpu-seconds 0 &&

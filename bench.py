@@ -291,7 +291,7 @@ def cpu_baseline(m_single_csr, copies, budget_s):
     t_end = time.perf_counter() + budget_s
     while time.perf_counter() < t_end or len(times) < 3:
         times.append(oracle.cpu_csr_omp(B * n_rows, bptr, bcol, bval, x, y, threads))
-        if len(times) >= 1000:
+        if len(times) >= 5000:  # ~10 s of passes on the cant batch (4-5 ms each)
             break
     t = float(np.median(times))
     b = sa.bytes_alg(B * n_rows, B * n_cols, B * int(ptr[-1]))

@@ -1357,25 +1357,32 @@ static int64_t csr_xwin_gpw(int L, int32_t rows_per_window)
     return g < 1 ? 1 : g;
 }
 
-template <int L, int R, bool NT, typename Cols>
+template <int L, int R, bool NT, typename Cols, typename V = double>
 static void launch_csr_xwin(const spmv_dims &d, const int64_t *row_ptr, const Cols cols,
-                            const double *val, const double *x, double *y, const int2 *win, int32_t xcap,
+                            const V *val, const double *x, double *y, const int2 *win, int32_t xcap,
                             int64_t gpw)
 {
     constexpr int RPB = kBlock / L;
     const int64_t groups = (d.n_rows + RPB - 1) / RPB;
     const int64_t n_win = (groups + gpw - 1) / gpw;
-    const int mode = csr_xwin_mode(d.n_rows, d.nnz, gpw * RPB, R);
+    int mode = csr_xwin_mode(d.n_rows, d.nnz, gpw * RPB, R);
+    // a very tall window's offsets would not fit beside the x range in the
+    // 64 KiB of dynamic LDS: MODE 0 stages them per row group instead
+    if (mode > 0 && csr_xwin_lds(mode, xcap, gpw, RPB) + sizeof(double2) * kBlock * R * 2 > 64 * 1024)
+        mode = 0;
     const size_t lds = csr_xwin_lds(mode, xcap, gpw, RPB);
     // one workgroup per window (the dispatcher balances) unless
     // SPMV_CSR_XWIN_PERSISTENT=1 (resident workgroups walk the windows)
     const char *ps = getenv("SPMV_CSR_XWIN_PERSISTENT");
-    const int64_t grid = (ps && ps[0] == '1') ? persistent_grid(csr_xwin_kernel<L, R, NT, double, 0, false, Cols>, n_win, lds) : n_win;
+    const int64_t grid = (ps && ps[0] == '1') ? persistent_grid(csr_xwin_kernel<L, R, NT, V, 0, false, Cols>, n_win, lds) : n_win;
     if (grid > INT32_MAX)
         return;
     const int remap = csr_xwin_remap_rule(xcap, gpw * RPB) ? 1 : 0;
     const hipStream_t st = (hipStream_t)d.stream;
-    if constexpr (std::is_same<Cols, Col32<NT>>::value) {  // the round-1 prefetch kernel reads int32 columns
+    constexpr bool kFp64 = std::is_same<V, double>::value;  // fp32 values: modes 0 and 3 only
+    if (!kFp64 && mode != 0)
+        mode = 3;
+    if constexpr (kFp64 && std::is_same<Cols, Col32<NT>>::value) {  // the round-1 prefetch kernel reads int32 columns
         if (csr_xwin_prefetch()) {
             const size_t lds0 = (size_t)xcap * sizeof(double);
             hipLaunchKernelGGL((csr_xwin_pf_kernel<L, R, NT>), dim3((unsigned)grid), dim3(kBlock), lds0, st, d.n_rows,
@@ -1385,24 +1392,26 @@ static void launch_csr_xwin(const spmv_dims &d, const int64_t *row_ptr, const Co
     }
     switch (mode) {
     case 0:
-        hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, double, 0, false, Cols>), dim3((unsigned)grid), dim3(kBlock), lds, st,
+        hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, V, 0, false, Cols>), dim3((unsigned)grid), dim3(kBlock), lds, st,
                            d.n_rows, groups, gpw, row_ptr, cols, val, x, y, win, xcap, remap);
         break;
     case 1:
-        hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, double, 1, false, Cols>), dim3((unsigned)grid), dim3(kBlock), lds, st,
+        if constexpr (kFp64)
+        hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, V, 1, false, Cols>), dim3((unsigned)grid), dim3(kBlock), lds, st,
                            d.n_rows, groups, gpw, row_ptr, cols, val, x, y, win, xcap, remap);
         break;
     case 2:
-        hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, double, 2, false, Cols>), dim3((unsigned)grid), dim3(kBlock), lds, st,
+        if constexpr (kFp64)
+        hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, V, 2, false, Cols>), dim3((unsigned)grid), dim3(kBlock), lds, st,
                            d.n_rows, groups, gpw, row_ptr, cols, val, x, y, win, xcap, remap);
         break;
     case 3:
-        if constexpr (NT) {  // SPMV_CSR_XWIN_R: pairs per lane per chunk (sweep knob)
+        if constexpr (NT && kFp64) {  // SPMV_CSR_XWIN_R: pairs per lane per chunk (sweep knob)
             const int rr = csr_xwin_rounds();
             if (rr != 0 && rr != R) {
                 const size_t l2 = lds;  // the chunk buffer is static LDS
 #define SPMV_XWIN_R(RR)                                                                                      \
-    hipLaunchKernelGGL((csr_xwin_kernel<L, RR, NT, double, 3, false, Cols>), dim3((unsigned)grid), dim3(kBlock), l2, st, \
+    hipLaunchKernelGGL((csr_xwin_kernel<L, RR, NT, V, 3, false, Cols>), dim3((unsigned)grid), dim3(kBlock), l2, st, \
                        d.n_rows, groups, gpw, row_ptr, cols, val, x, y, win, xcap, remap)
                 switch (rr) {
                 case 2: SPMV_XWIN_R(2); return;
@@ -1415,22 +1424,25 @@ static void launch_csr_xwin(const spmv_dims &d, const int64_t *row_ptr, const Co
 #undef SPMV_XWIN_R
             }
         }
-        if (csr_xwin_pre())
-            hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, double, 3, true, Cols>), dim3((unsigned)grid), dim3(kBlock), lds,
+        if (kFp64 && csr_xwin_pre())
+            hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, V, 3, kFp64, Cols>), dim3((unsigned)grid), dim3(kBlock), lds,
                                st, d.n_rows, groups, gpw, row_ptr, cols, val, x, y, win, xcap, remap);
         else
-            hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, double, 3, false, Cols>), dim3((unsigned)grid), dim3(kBlock), lds, st,
+            hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, V, 3, false, Cols>), dim3((unsigned)grid), dim3(kBlock), lds, st,
                                d.n_rows, groups, gpw, row_ptr, cols, val, x, y, win, xcap, remap);
         break;
     case 4:
-        hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, double, 4, false, Cols>), dim3((unsigned)grid), dim3(kBlock), lds, st,
+        if constexpr (kFp64)
+        hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, V, 4, false, Cols>), dim3((unsigned)grid), dim3(kBlock), lds, st,
                            d.n_rows, groups, gpw, row_ptr, cols, val, x, y, win, xcap, remap);
         break;
     case 5:
-        if (gpw == 1 || gpw == 2 || gpw == 4) {
+        if constexpr (!kFp64) {
+            break;
+        } else if (gpw == 1 || gpw == 2 || gpw == 4) {
             const bool r3 = NT && csr_xwin_rounds() == 3 && R != 3;  // SPMV_CSR_XWIN_R (sweep knob)
 #define SPMV_FLAT(RR, MM)                                                                                     \
-    hipLaunchKernelGGL((csr_xwin_kernel<L, RR, NT, double, MM, false, Cols>), dim3((unsigned)grid), dim3(kBlock), lds, st, \
+    hipLaunchKernelGGL((csr_xwin_kernel<L, RR, NT, V, MM, false, Cols>), dim3((unsigned)grid), dim3(kBlock), lds, st, \
                        d.n_rows, groups, gpw, row_ptr, cols, val, x, y, win, xcap, remap)
             if (gpw == 1) {
                 if (r3) SPMV_FLAT(3, 5); else SPMV_FLAT(R, 5);
@@ -1441,7 +1453,7 @@ static void launch_csr_xwin(const spmv_dims &d, const int64_t *row_ptr, const Co
             }
 #undef SPMV_FLAT
         } else {
-            hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, double, 3, false, Cols>), dim3((unsigned)grid), dim3(kBlock), lds, st,
+            hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, V, 3, false, Cols>), dim3((unsigned)grid), dim3(kBlock), lds, st,
                                d.n_rows, groups, gpw, row_ptr, cols, val, x, y, win, xcap, remap);
         }
         break;
@@ -1736,34 +1748,23 @@ extern "C" int spmv_csr_f32v_run_xwin(spmv_dims d, const int64_t *row_ptr, const
         return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_f32v_run_xwin: lanes_per_row must be 0 or a power of two in [2,64]");
     const int64_t gpw = csr_xwin_gpw(L, rows_per_window);
     const bool nt = stream_nt(kCsrXwinNtDefault);
-    const int remap = csr_xwin_remap_rule(xcap, gpw * (kBlock / L)) ? 1 : 0;
     const int2 *w = (const int2 *)win;
     const int64_t groups_base = d.n_rows;
 #define SPMV_XWIN32(LL)                                                                                     \
     do {                                                                                                    \
         constexpr int RPB = kBlock / LL;                                                                    \
         const int64_t groups = (groups_base + RPB - 1) / RPB;                                               \
-        const int64_t n_win = (groups + gpw - 1) / gpw;                                                     \
-        if (n_win > INT32_MAX)                                                                              \
+        if ((groups + gpw - 1) / gpw > INT32_MAX)                                                           \
             return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_f32v_run_xwin: grid too large");                    \
-        const size_t lds = csr_xwin_lds(kCsrXwinMode, xcap, gpw, RPB);                                      \
         const bool r4 = csr_stage_rounds(d.n_rows, d.nnz, LL) == 4;                                         \
         if (nt && r4)                                                                                       \
-            hipLaunchKernelGGL((csr_xwin_kernel<LL, 4, true, float, kCsrXwinMode>), dim3((unsigned)n_win),  \
-                               dim3(kBlock), lds, (hipStream_t)d.stream, d.n_rows, groups, gpw, row_ptr, Col32<true>{col}, \
-                               val, x, y, w, xcap, remap);                                                  \
+            launch_csr_xwin<LL, 4, true>(d, row_ptr, Col32<true>{col}, val, x, y, w, xcap, gpw);            \
         else if (nt)                                                                                        \
-            hipLaunchKernelGGL((csr_xwin_kernel<LL, 3, true, float, kCsrXwinMode>), dim3((unsigned)n_win),  \
-                               dim3(kBlock), lds, (hipStream_t)d.stream, d.n_rows, groups, gpw, row_ptr, Col32<true>{col}, \
-                               val, x, y, w, xcap, remap);                                                  \
+            launch_csr_xwin<LL, 3, true>(d, row_ptr, Col32<true>{col}, val, x, y, w, xcap, gpw);            \
         else if (r4)                                                                                        \
-            hipLaunchKernelGGL((csr_xwin_kernel<LL, 4, false, float, kCsrXwinMode>), dim3((unsigned)n_win), \
-                               dim3(kBlock), lds, (hipStream_t)d.stream, d.n_rows, groups, gpw, row_ptr, Col32<false>{col}, \
-                               val, x, y, w, xcap, remap);                                                  \
+            launch_csr_xwin<LL, 4, false>(d, row_ptr, Col32<false>{col}, val, x, y, w, xcap, gpw);          \
         else                                                                                                \
-            hipLaunchKernelGGL((csr_xwin_kernel<LL, 3, false, float, kCsrXwinMode>), dim3((unsigned)n_win), \
-                               dim3(kBlock), lds, (hipStream_t)d.stream, d.n_rows, groups, gpw, row_ptr, Col32<false>{col}, \
-                               val, x, y, w, xcap, remap);                                                  \
+            launch_csr_xwin<LL, 3, false>(d, row_ptr, Col32<false>{col}, val, x, y, w, xcap, gpw);          \
     } while (0)
     switch (L) {
     case 2: SPMV_XWIN32(2); break;

@@ -150,6 +150,16 @@ constexpr int kStageRoundsDefault = 3;  // pairs per lane per chunk: 1536 produc
 // R = 8 slower; round 2, x-window kernel MODE 3: R = 3 0.2591-0.2607 ms,
 // R = 4 0.2639-0.2642 — one default for every staged CSR kernel keeps
 // their chunk boundaries, hence their bits, identical)
+// Chunks of the staged kernels start on a kChunkAlign-entry boundary at or
+// before the row group's first entry (up to 31 entries of the previous group
+// are loaded and never summed), so a wave's 64 value pairs (1 KiB) and column
+// pairs (512 B) cover whole 128-B lines, 8 + 4 instead of 9 + 5: the
+// CSR-shaped stream probe reads 6.81 TB/s from aligned tiles and 6.47 TB/s
+// from tiles that start on any even entry (tools/bw_probe,
+// csr_prologue_dep1[_unaligned]).  Every staged CSR kernel cuts the same
+// chunks, so their sums stay bit-identical to each other.
+constexpr int64_t kChunkAlign = 32;
+__host__ __device__ __forceinline__ int64_t chunk_start(int64_t e) { return e & ~(kChunkAlign - 1); }
 constexpr bool kCsrStreamNtDefault = false;  // SPMV_STREAM_NT overrides
 // the x-window kernel (x gathers from LDS) streams faster non-temporal:
 // 0.2991 vs 0.3077 ms on the cant-like batch
@@ -324,9 +334,9 @@ __device__ __forceinline__ void staged_group(
     const double *prod = reinterpret_cast<const double *>(s_prod);
 
     double acc = 0.0;
-    // chunks start on an even entry so value pairs stay 16-byte aligned;
-    // an entry before the group's range is loaded but never summed.
-    for (int64_t cb = s_ptr[0] & ~(int64_t)1; cb < blk_end; cb += CH) {
+    // chunks start on a kChunkAlign boundary (whole cache lines per wave);
+    // entries before the group's range are loaded but never summed.
+    for (int64_t cb = chunk_start(s_ptr[0]); cb < blk_end; cb += CH) {
         const int64_t ce = cb + CH < blk_end ? cb + CH : blk_end;
         if constexpr (BATCH > 0) {
             stage_products<R, NT, BATCH == 2>(cb, ce, nz, cols, val, xs, s_prod);
@@ -380,11 +390,11 @@ struct StreamRegs {
     __device__ __forceinline__ void issue(int64_t cb, int64_t ce, int64_t nz, const Cols &cols,
                                           const V *__restrict__ val)
     {
-        if (nz < 2) {  // uniform; a 1-entry array has no pair 0 (its entry: products())
+        if (nz < 2) {  // uniform; a 0/1-entry array has no pair 0 (its entry: products()), nothing is loaded
 #pragma unroll
             for (int k = 0; k < R; ++k) {
                 v[k] = double2{0.0, 0.0};
-                c[k] = cols.raw(0);
+                c[k] = typename Cols::Raw{};
                 q[k] = 0;
             }
             return;
@@ -403,10 +413,16 @@ struct StreamRegs {
     __device__ __forceinline__ void products(int64_t cb, int64_t ce, int64_t nz, const Cols &cols,
                                              const V *__restrict__ val, const XS &xs, double2 *s_prod) const
     {
+        if (nz >= 2) {  // uniform (no gathers for a 0/1-entry array: x may be empty)
 #pragma unroll
-        for (int k = 0; k < R; ++k) {
-            const int2 cc = cols.decode(c[k], q[k]);
-            s_prod[threadIdx.x + k * kBlock] = double2{v[k].x * xs(cc.x), v[k].y * xs(cc.y)};
+            for (int k = 0; k < R; ++k) {
+                const int2 cc = cols.decode(c[k], q[k]);
+                s_prod[threadIdx.x + k * kBlock] = double2{v[k].x * xs(cc.x), v[k].y * xs(cc.y)};
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < R; ++k)
+                s_prod[threadIdx.x + k * kBlock] = double2{0.0, 0.0};
         }
         const int64_t tail = nz - 1 - cb;  // the array's odd last entry
         if ((nz & 1) && nz - 1 < ce && tail >= 0 && tail < 2 * R * kBlock && (tail >> 1) % kBlock == threadIdx.x) {
@@ -441,10 +457,10 @@ __device__ __forceinline__ void staged_window_pipelined(int64_t row0, int ngroup
     const int lane = threadIdx.x % L;
     int buf = 0;
     // first chunk of group j at or after `from` that has one (staged_group's
-    // loop runs a chunk iff (start & ~1) < end); ngroups when none
+    // loop runs a chunk iff chunk_start(start) < end); ngroups when none
     auto next_group = [&](int from) {
         int j = from;
-        while (j < ngroups && (s_off[j * RPB] & ~(int64_t)1) >= s_off[(j + 1) * RPB])
+        while (j < ngroups && chunk_start(s_off[j * RPB]) >= s_off[(j + 1) * RPB])
             ++j;
         return j;
     };
@@ -456,7 +472,7 @@ __device__ __forceinline__ void staged_window_pipelined(int64_t row0, int ngroup
     } else {
         jn = next_group(0);
         if (jn < ngroups) {
-            const int64_t b = s_off[jn * RPB] & ~(int64_t)1, e = s_off[(jn + 1) * RPB];
+            const int64_t b = chunk_start(s_off[jn * RPB]), e = s_off[(jn + 1) * RPB];
             st.issue(b, b + CH < e ? b + CH : e, nz, cols, val);
         }
     }
@@ -465,7 +481,7 @@ __device__ __forceinline__ void staged_window_pipelined(int64_t row0, int ngroup
         const int64_t beg = gp[g], end = gp[g + 1];
         const int64_t blk_end = gp[RPB];
         double acc = 0.0;
-        for (int64_t cb = gp[0] & ~(int64_t)1; cb < blk_end; cb += CH) {
+        for (int64_t cb = chunk_start(gp[0]); cb < blk_end; cb += CH) {
             const int64_t ce = cb + CH < blk_end ? cb + CH : blk_end;
             double2 *s_prod = s_prod_base + buf * (kBlock * R);
             const double *prod = reinterpret_cast<const double *>(s_prod);
@@ -479,7 +495,7 @@ __device__ __forceinline__ void staged_window_pipelined(int64_t row0, int ngroup
                 const int64_t nb = cb + CH;
                 st.issue(nb, nb + CH < blk_end ? nb + CH : blk_end, nz, cols, val);
             } else if ((jn = next_group(gi + 1)) < ngroups) {
-                const int64_t b = s_off[jn * RPB] & ~(int64_t)1, e = s_off[(jn + 1) * RPB];
+                const int64_t b = chunk_start(s_off[jn * RPB]), e = s_off[(jn + 1) * RPB];
                 st.issue(b, b + CH < e ? b + CH : e, nz, cols, val);
             }
             __syncthreads();
@@ -524,9 +540,9 @@ __device__ __forceinline__ void staged_window_flat(int64_t row0, const int64_t *
 #pragma unroll
     for (int k = 0; k <= RW; ++k)
         rb[k] = s_off[g * RW + k];
-    const int64_t e0 = s_off[0] & ~(int64_t)1, e1 = s_off[G * RW];
+    const int64_t e0 = chunk_start(s_off[0]), e1 = s_off[G * RW];
     const int64_t nch = e1 > e0 ? (e1 - e0 + CHMAX - 1) / CHMAX : 0;
-    const int64_t cs = nch > 0 ? (((e1 - e0 + nch - 1) / nch) + 1) & ~(int64_t)1 : 0;  // even, <= CHMAX
+    const int64_t cs = nch > 0 ? chunk_start(((e1 - e0 + nch - 1) / nch) + kChunkAlign - 1) : 0;  // aligned, <= CHMAX
     double acc[RW];
 #pragma unroll
     for (int k = 0; k < RW; ++k)
@@ -689,7 +705,7 @@ __global__ __launch_bounds__(kBlock, MODE >= 3 ? kXwinWaves : 1) void csr_xwin_k
         if constexpr (MODE == 3 && PRE) {
             const int64_t rr0 = g_beg * RPB;
             const int64_t rr1 = rr0 + RPB < n_rows ? rr0 + RPB : n_rows;
-            const int64_t b = row_ptr[rr0] & ~(int64_t)1, e = row_ptr[rr1];
+            const int64_t b = chunk_start(row_ptr[rr0]), e = row_ptr[rr1];
             pre = b < e;  // uniform
             if (pre)
                 st_pre.issue(b, b + 2 * kBlock * R < e ? b + 2 * kBlock * R : e, nz, cols, val);
@@ -768,6 +784,199 @@ __global__ __launch_bounds__(kBlock, MODE >= 3 ? kXwinWaves : 1) void csr_xwin_k
                 staged_group<L, R, NT, Cols, BATCH, XGlobal, V>(row, gp, s_prod, cols, val,
                                                                      XGlobal{x}, y, n_rows, nz);
         }
+    }
+}
+
+// x ring of csr_xstream_kernel: column c lives in slot c & mask of a
+// power-of-two LDS array at least as long as the widest row group's column
+// span, so the ranges of consecutive groups share every column they overlap
+// on and a new group copies only the columns the previous one lacked.
+struct XRing {
+    const double *s;  // LDS
+    int32_t mask;
+    __device__ __forceinline__ double operator()(int32_t c) const { return s[c & mask]; }
+};
+
+// x[lo .. lo+span) into the ring, U loads in flight per thread
+template <int U = 8>
+__device__ __forceinline__ void copy_ring(double *s_x, const double *__restrict__ x, int32_t lo, int32_t span,
+                                          int32_t mask)
+{
+    for (int32_t b = 0; b < span; b += U * kBlock) {
+        double v[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const int32_t i = b + (int32_t)threadIdx.x + k * kBlock;
+            v[k] = x[lo + (i < span ? i : span - 1)];
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const int32_t i = b + (int32_t)threadIdx.x + k * kBlock;
+            if (i < span)
+                s_x[(lo + i) & mask] = v[k];
+        }
+    }
+}
+
+// The streaming CSR kernel (spmv_csr_run_xwin with one row group per window
+// and SPMV_CSR_XSTREAM=1): persistent workgroups, each owning ONE contiguous
+// range of row groups (256/L rows each; the ranges differ by at most one
+// group), streamed as one software pipeline that does not stop at group
+// boundaries.  Per chunk: products of chunk k (x from the ring) -> the loads
+// of chunk k+1 issued (the next group's first chunk at a group's end) ->
+// barrier -> the L-lane row slices of chunk k -> barrier.  What the x-window
+// kernel pays per window, this kernel hides inside that pipeline:
+//  - the next group's row offsets are loaded two groups ahead (three LDS
+//    offset buffers), so issuing its first chunk never waits on them;
+//  - the next group's column range (win, one int2 per group) is loaded a
+//    group ahead, and the columns it adds to the ring are loaded beside the
+//    next chunk's stream and stored after the first barrier, when no lane
+//    gathers from the ring any more.
+// Chunks, products and sums are those of staged_group: y is bit-identical to
+// the other staged CSR kernels.  A group whose range does not fit in the ring
+// gathers from global memory.
+template <int L, int R, bool NT, typename V = double, typename Cols = Col32<NT>, int WAVES = 1>
+__global__ __launch_bounds__(kBlock, WAVES) void csr_xstream_kernel(
+    int64_t n_rows, int64_t n_groups, const int64_t *__restrict__ row_ptr, const Cols cols,
+    const V *__restrict__ val, const double *__restrict__ x, double *__restrict__ y,
+    const int2 *__restrict__ gwin, int32_t cap)
+{
+    constexpr int RPB = kBlock / L;
+    constexpr int CH = 2 * kBlock * R;
+    constexpr int U = 2;  // new ring columns per thread loaded ahead of the barrier
+    extern __shared__ double s_x[];
+    __shared__ int64_t s_off[3][RPB + 1];
+    __shared__ double2 s_prod[kBlock * R];
+    const double *prod = reinterpret_cast<const double *>(s_prod);
+    const int64_t nz = row_ptr[n_rows];
+    const int64_t gb = (int64_t)blockIdx.x * n_groups / gridDim.x;
+    const int64_t ge = ((int64_t)blockIdx.x + 1) * n_groups / gridDim.x;
+    if (gb >= ge)
+        return;  // uniform
+    const int t = threadIdx.x, g = t / L, lane = t % L;
+    const int32_t mask = cap - 1;
+    const XRing xr{s_x, mask};
+    auto offs = [&](int64_t j) {  // offset of row j·RPB + t (threads 0..RPB), clamped
+        const int64_t r = j * RPB + t;
+        return row_ptr[r < n_rows ? r : n_rows];
+    };
+    auto fits = [&](int2 w) { return w.x <= w.y && (int64_t)w.y - w.x + 1 <= cap; };
+
+    // prologue: offsets of the first two groups (the third's in a register),
+    // the first group's columns copied whole
+    int64_t onext = 0;
+    {
+        int64_t o0 = 0, o1 = 0;
+        if (t <= RPB) {
+            o0 = offs(gb);
+            o1 = offs(gb + 1);
+            onext = offs(gb + 2);
+        }
+        const int2 w = gwin[gb];
+        if (fits(w))
+            copy_ring(s_x, x, w.x, w.y - w.x + 1, mask);
+        if (t <= RPB) {
+            s_off[0][t] = o0;
+            s_off[1][t] = o1;
+        }
+    }
+    int2 w0 = gwin[gb];
+    bool fit = fits(w0);
+    int32_t rlo = fit ? w0.x : 1, rhi = fit ? w0.y : 0;  // columns the ring holds (none: rlo > rhi)
+    int2 wnext = gwin[gb + 1 < n_groups ? gb + 1 : gb];
+    __syncthreads();
+
+    StreamRegs<R, NT, V, Cols> st;
+    {
+        const int64_t b = chunk_start(s_off[0][0]), e = s_off[0][RPB];
+        st.issue(b, b + CH < e ? b + CH : e, nz, cols, val);
+    }
+    int bi = 0;  // s_off buffer of group gi
+    for (int64_t gi = gb; gi < ge; ++gi) {
+        const int64_t *gp = s_off[bi];
+        const int64_t beg = gp[g], end = gp[g + 1];
+        const int64_t gend = gp[RPB];
+        const int bn = bi == 2 ? 0 : bi + 1, bnn = bn == 2 ? 0 : bn + 1;
+        double acc = 0.0;
+        // chunks as staged_group's; a group without one runs one empty chunk
+        for (int64_t cb = chunk_start(gp[0]), k = 0;; ++k) {
+            const int64_t ce = cb + CH < gend ? cb + CH : gend;
+            const bool last = ce >= gend;
+            if (fit)
+                st.products(cb, ce, nz, cols, val, xr, s_prod);
+            else
+                st.products(cb, ce, nz, cols, val, XGlobal{x}, s_prod);
+            if (k == 0) {  // the group after next: offsets to LDS, the one after that loaded
+                if (t <= RPB)
+                    s_off[bnn][t] = onext;
+                if (t <= RPB)
+                    onext = offs(gi + 3);
+            }
+            // the next group's new ring columns: [A0, A1] below the ring's
+            // range and [B0, B1] above it
+            const bool more = last && gi + 1 < ge;
+            const int2 wn = wnext;
+            const bool nfit = more && fits(wn);
+            int32_t A0 = 0, nA = 0, B0 = 0, nB = 0;
+            double rv[U];
+            if (nfit) {
+                if (rlo > rhi) {
+                    A0 = wn.x;
+                    nA = wn.y - wn.x + 1;
+                } else {
+                    const int32_t a1 = wn.y < rlo - 1 ? wn.y : rlo - 1;
+                    A0 = wn.x;
+                    nA = a1 >= A0 ? a1 - A0 + 1 : 0;
+                    B0 = wn.x > rhi + 1 ? wn.x : rhi + 1;
+                    nB = wn.y >= B0 ? wn.y - B0 + 1 : 0;
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int32_t i = t + u * kBlock;
+                    const int32_t c = i < nA ? A0 + i : i < nA + nB ? B0 + (i - nA) : wn.x;
+                    rv[u] = x[c];
+                }
+            }
+            if (more) {  // the next group's first chunk
+                const int64_t *np = s_off[bn];
+                const int64_t b = chunk_start(np[0]), e = np[RPB];
+                st.issue(b, b + CH < e ? b + CH : e, nz, cols, val);
+                wnext = gwin[gi + 2 < n_groups ? gi + 2 : gi + 1];
+            } else if (!last) {
+                st.issue(ce, ce + CH < gend ? ce + CH : gend, nz, cols, val);
+            }
+            __syncthreads();  // products visible; nobody gathers from the ring any more
+            acc += slice_sum<L>(prod, beg > cb ? beg - cb : 0, (end < ce ? end : ce) - cb, lane);
+            if (nfit) {
+                const int32_t n = nA + nB;
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int32_t i = t + u * kBlock;
+                    if (i < n)
+                        s_x[(i < nA ? A0 + i : B0 + (i - nA)) & mask] = rv[u];
+                }
+                for (int32_t i = t + U * kBlock; i < n; i += kBlock) {
+                    const int32_t c = i < nA ? A0 + i : B0 + (i - nA);
+                    s_x[c & mask] = x[c];
+                }
+                rlo = wn.x;
+                rhi = wn.y;
+                fit = true;
+            } else if (more && wn.x <= wn.y) {  // too wide: global gathers, ring forgotten
+                rlo = 1;
+                rhi = 0;
+                fit = false;
+            }  // an empty next group keeps the ring (and `fit`)
+            __syncthreads();
+            if (last)
+                break;
+            cb = ce;
+        }
+        acc = group_sum<L>(acc);
+        const int64_t row = gi * RPB + g;
+        if (lane == 0 && row < n_rows)
+            y[row] = acc;
+        bi = bn;
     }
 }
 
@@ -850,7 +1059,7 @@ __device__ __forceinline__ void staged_group_pf(int64_t row, const int64_t *s_pt
     const double *prod = reinterpret_cast<const double *>(s_prod);
     double acc = 0.0;
     bool first = true;
-    for (int64_t cb = s_ptr[0] & ~(int64_t)1; cb < blk_end; cb += CH) {
+    for (int64_t cb = chunk_start(s_ptr[0]); cb < blk_end; cb += CH) {
         const int64_t ce = cb + CH < blk_end ? cb + CH : blk_end;
         if (first) {
             pre.products_xs(xs, s_prod);
@@ -901,7 +1110,7 @@ __global__ __launch_bounds__(kBlock) void csr_xwin_pf_kernel(
         {
             const int64_t r0 = g_beg * RPB;
             const int64_t r1 = r0 + RPB < n_rows ? r0 + RPB : n_rows;
-            const int64_t b0 = row_ptr[r0] & ~(int64_t)1;
+            const int64_t b0 = chunk_start(row_ptr[r0]);
             const int64_t e0 = row_ptr[r1];
             pre.issue(col, val, b0, b0 + CH < e0 ? b0 + CH : e0);
         }
@@ -985,7 +1194,7 @@ __global__ __launch_bounds__(kBlock) void csr_pipelined_kernel(
         blk_end = s_ptr[b][RPB];
     };
     start_group();
-    int64_t cb = s_ptr[b][0] & ~(int64_t)1;
+    int64_t cb = chunk_start(s_ptr[b][0]);
     int64_t ce = cb + CH < blk_end ? cb + CH : blk_end;
     ChunkRegs<R, NT> regs;
     regs.issue(col, val, cb, ce);
@@ -1002,7 +1211,7 @@ __global__ __launch_bounds__(kBlock) void csr_pipelined_kernel(
             ngrp = grp + grid;
             if (ngrp < n_groups) {
                 const int64_t nend = s_ptr[1 - b][RPB];
-                ncb = s_ptr[1 - b][0] & ~(int64_t)1;
+                ncb = chunk_start(s_ptr[1 - b][0]);
                 nce = ncb + CH < nend ? ncb + CH : nend;
             }
         }
@@ -1357,12 +1566,61 @@ static int64_t csr_xwin_gpw(int L, int32_t rows_per_window)
     return g < 1 ? 1 : g;
 }
 
+// SPMV_CSR_LDS_PAD=<bytes>: extra dynamic LDS per workgroup of the x-window
+// kernels (an occupancy sweep knob: fewer workgroups per CU); default 0
+static size_t csr_lds_pad()
+{
+    const char *s = getenv("SPMV_CSR_LDS_PAD");
+    return s ? (size_t)atol(s) : 0;
+}
+
+// SPMV_CSR_XSTREAM=1 / 0: csr_xstream_kernel for x windows of one row group
+// (read per call; default kCsrXstream)
+constexpr bool kCsrXstream = false;
+static bool csr_xstream()
+{
+    const char *s = getenv("SPMV_CSR_XSTREAM");
+    return (s && (s[0] == '0' || s[0] == '1')) ? s[0] == '1' : kCsrXstream;
+}
+
+// win: one column range per row group; the ring is the smallest power of
+// two >= xcap (at least 64 entries)
+template <int L, int R, bool NT, typename Cols, typename V>
+static void launch_csr_xstream(const spmv_dims &d, const int64_t *row_ptr, const Cols cols, const V *val,
+                               const double *x, double *y, const int2 *win, int32_t xcap)
+{
+    constexpr int RPB = kBlock / L;
+    const int64_t groups = (d.n_rows + RPB - 1) / RPB;
+    int lg = 6;
+    while ((1 << lg) < xcap)
+        ++lg;
+    const int32_t cap = 1 << lg;
+    const size_t lds = (size_t)cap * sizeof(double) + csr_lds_pad();
+    const char *ws = getenv("SPMV_CSR_XSTREAM_WAVES");  // sweep knob: 6 = VGPRs capped for 6 waves/SIMD
+    const bool w6 = ws && ws[0] == '6';
+    static int64_t resident[2][16] = {};  // per ring size (the occupancy calculator once per size)
+    if (resident[w6][lg] == 0 || csr_lds_pad() != 0)
+        resident[w6][lg] = w6 ? persistent_grid(csr_xstream_kernel<L, R, NT, V, Cols, 6>, INT64_MAX, lds)
+                              : persistent_grid(csr_xstream_kernel<L, R, NT, V, Cols>, INT64_MAX, lds);
+    const int64_t grid = resident[w6][lg] < groups ? resident[w6][lg] : groups;
+    if (w6)
+        hipLaunchKernelGGL((csr_xstream_kernel<L, R, NT, V, Cols, 6>), dim3((unsigned)grid), dim3(kBlock), lds,
+                           (hipStream_t)d.stream, d.n_rows, groups, row_ptr, cols, val, x, y, win, cap);
+    else
+        hipLaunchKernelGGL((csr_xstream_kernel<L, R, NT, V, Cols>), dim3((unsigned)grid), dim3(kBlock), lds,
+                           (hipStream_t)d.stream, d.n_rows, groups, row_ptr, cols, val, x, y, win, cap);
+}
+
 template <int L, int R, bool NT, typename Cols, typename V = double>
 static void launch_csr_xwin(const spmv_dims &d, const int64_t *row_ptr, const Cols cols,
                             const V *val, const double *x, double *y, const int2 *win, int32_t xcap,
                             int64_t gpw)
 {
     constexpr int RPB = kBlock / L;
+    if (gpw == 1 && csr_xstream()) {
+        launch_csr_xstream<L, R, NT, Cols, V>(d, row_ptr, cols, val, x, y, win, xcap);
+        return;
+    }
     const int64_t groups = (d.n_rows + RPB - 1) / RPB;
     const int64_t n_win = (groups + gpw - 1) / gpw;
     int mode = csr_xwin_mode(d.n_rows, d.nnz, gpw * RPB, R);
@@ -1370,7 +1628,7 @@ static void launch_csr_xwin(const spmv_dims &d, const int64_t *row_ptr, const Co
     // 64 KiB of dynamic LDS: MODE 0 stages them per row group instead
     if (mode > 0 && csr_xwin_lds(mode, xcap, gpw, RPB) + sizeof(double2) * kBlock * R * 2 > 64 * 1024)
         mode = 0;
-    const size_t lds = csr_xwin_lds(mode, xcap, gpw, RPB);
+    const size_t lds = csr_xwin_lds(mode, xcap, gpw, RPB) + csr_lds_pad();
     // one workgroup per window (the dispatcher balances) unless
     // SPMV_CSR_XWIN_PERSISTENT=1 (resident workgroups walk the windows)
     const char *ps = getenv("SPMV_CSR_XWIN_PERSISTENT");

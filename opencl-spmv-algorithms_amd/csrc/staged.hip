@@ -194,7 +194,9 @@ __global__ __launch_bounds__(kBlock) void cmrs_staged_kernel(
     // PIPE: the next chunk's loads are issued before this chunk's barrier
     // and reduction (as the MODE 3 CSR kernel); same chunks, same bits
     StageRegs<R, NT, double, KeysU8> st;
-    const int64_t c0 = s_sp[0] & ~(int64_t)1;
+    // chunks start on a 32-entry boundary: whole 128-B lines per wave (as
+    // csr.hip kChunkAlign); the previous strip's entries are never summed
+    const int64_t c0 = s_sp[0] & ~(int64_t)31;
     if (PIPE && c0 < blk_end)
         st.issue(c0, c0 + CH < blk_end ? c0 + CH : blk_end, nz, col, val, keys);
     for (int64_t cb = c0; cb < blk_end; cb += CH) {

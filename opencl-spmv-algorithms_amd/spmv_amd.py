@@ -1015,7 +1015,7 @@ def device_build(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, ki: int =
 
 def banded_to_device(n: int, fmt: str, device="cuda:0", row_begin: int = 0, row_end: int | None = None,
                      seed: int = 2, C: int = 64, sigma: int = 1024, ki: int = 2, lanes: int = 0,
-                     variant: int = 0, xwin: bool = True) -> DeviceMatrix:
+                     variant: int = 0, xwin: bool = True, xwin_rows: int = 0) -> DeviceMatrix:
     """Rows [row_begin, row_end) of the banded matrix (BASELINE.json
     configs[4]) generated directly in HBM by spmv_gen_banded_device, as CSR
     or SELL.  Row ids are local to the shard; columns are global (x is the
@@ -1032,7 +1032,7 @@ def banded_to_device(n: int, fmt: str, device="cuda:0", row_begin: int = 0, row_
         val = torch.empty(16 * m, dtype=torch.float64, device=device)
         rc = hip_lib().spmv_gen_banded_device(n, seed, row_begin, row_end, 0, 0, 0, _ptr(ptr), None, _ptr(col),
                                               _ptr(val), device.index or 0, stream.cuda_stream)
-        dm.params = dict(lanes=lanes, variant=variant)
+        dm.params = dict(lanes=lanes, variant=variant, xwin_rows=xwin_rows)
         dm.arrays = dict(row_ptr=ptr, col=col, val=val)
         dm.stored_bytes = 12 * 16 * m + 8 * (m + 1)
     elif fmt == "sell":

@@ -686,6 +686,61 @@ def test_csrf32_tiled_on_skewed_rows(torch_dev, H):
     assert_parity(m, ya.cpu().numpy(), x.cpu().numpy())
 
 
+def _xstream_cases(case):
+    if case == "cantlike":
+        return [sa.gen_cantlike(0, copies=2)]
+    if case == "ragged":  # random columns: most row groups span more than the ring
+        return [sa.gen_random(20_000, 50_000, 0, 2_000, seed=21)]
+    if case == "empty_runs":
+        return [_empty_run_matrix()[0]]
+    if case == "shuffled_bands":
+        # banded blocks in shuffled order: column ranges jump up and down
+        # between neighbouring row groups (both ends of the ring update), and
+        # some jumps leave no overlap at all
+        n, blk = 40_000, 500
+        rng = np.random.default_rng(5)
+        perm = rng.permutation(n // blk)
+        rows, cols = [], []
+        for b, pb in enumerate(perm):
+            r = np.repeat(np.arange(b * blk, (b + 1) * blk), 9)
+            c = (np.repeat(np.arange(pb * blk, (pb + 1) * blk), 9) + np.tile(np.arange(-4, 5), blk)) % n
+            rows.append(r)
+            cols.append(c)
+        r, c = np.concatenate(rows), np.concatenate(cols)
+        return [sa.Coo(n, n, r.astype(np.int32), c.astype(np.int32), rng.uniform(-1, 1, r.size))]
+    return [sa.read_mtx(GOLDEN / f"{n}.mtx") for n in CASES]
+
+
+@pytest.mark.parametrize("fmt", ["csr", "csr16", "csrf32"])
+@pytest.mark.parametrize("case", ["cantlike", "ragged", "fixtures", "empty_runs", "shuffled_bands"])
+def test_csr_xstream(torch_dev, monkeypatch, case, fmt):
+    """csr_xstream_kernel (persistent workgroups, one x ring each, the
+    pipeline running across row groups) forms staged_group's chunks and sums:
+    y equals the one-group-window x-window kernel's bit for bit, at every lane
+    width, also where groups outgrow the ring (global gathers) or their
+    column ranges jump."""
+    torch, dev = torch_dev
+    for m in _xstream_cases(case):
+        if m.n_rows == 0:
+            continue
+        if fmt == "csr16" and case == "ragged":
+            continue  # 16-bit offsets: escapes in most blocks, refused by to_device
+        x = torch.from_numpy(np.random.default_rng(12).uniform(-1, 1, max(m.n_cols, 1))).to(dev)
+        for lanes in (2, 4, 16, 64):
+            dm = sa.to_device(m, fmt, dev, lanes=lanes, variant=3, xwin=True, xwin_rows=1)
+            ys = []
+            for on in ("0", "1"):
+                monkeypatch.setenv("SPMV_CSR_XSTREAM", on)
+                y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
+                dm.run(x, y)
+                dm.run(x, y)  # twice: nothing carried between runs
+                ys.append(y)
+            torch.cuda.synchronize()
+            assert torch.equal(ys[1].view(torch.int64), ys[0].view(torch.int64)), (m.label, fmt, lanes)
+            if fmt == "csr":
+                assert_parity(m, ys[1].cpu().numpy(), x.cpu().numpy()[: m.n_cols])
+
+
 @pytest.mark.parametrize("case", ["cantlike", "ragged", "fixtures", "empty_runs"])
 def test_csr_xwin_load_modes(torch_dev, monkeypatch, case):
     """Every load schedule of csr_xwin_kernel (SPMV_CSR_XWIN_MODE 0-4 and the

@@ -2,7 +2,7 @@
 """Interleaved A/B of library knobs that are read on every call (SPMV_*
 environment variables) on ONE device matrix built once.
 
-    python tools/ab_env.py --format csr --env SPMV_CSR_XWIN_MODE=0,1,2 [--rounds 5]
+    python tools/ab_env.py --format csr --env SPMV_CSR_XWIN_MODE=0,1,2 [--kw JSON ...] [--rounds 5]
 
 Every configuration runs `--reps` back-to-back launches per round (HIP events
 on the launch stream), configurations interleaved round by round in one
@@ -32,7 +32,8 @@ def main():
     ap.add_argument("--banded-rows", type=int, default=20_000_000, help="banded: rows (16 entries each)")
     ap.add_argument("--copies", type=int, default=32)
     ap.add_argument("--env", action="append", default=[], help="KEY=v1,v2 (several: cartesian product)")
-    ap.add_argument("--kw", default="{}", help="to_device keyword arguments (JSON)")
+    ap.add_argument("--kw", action="append", default=[],
+                    help="to_device keyword arguments (JSON; several: one device matrix each, crossed with --env)")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=50)
     a = ap.parse_args()
@@ -51,19 +52,24 @@ def main():
         k, v = e.split("=", 1)
         keys.append(k)
         vals.append(v.split(","))
-    configs = [dict(zip(keys, c)) for c in itertools.product(*vals)] or [{}]
+    envs = [dict(zip(keys, c)) for c in itertools.product(*vals)] or [{}]
+    kws = a.kw or ["{}"]
     x = torch.from_numpy(np.random.default_rng(7).uniform(-1, 1, m.n_cols)).to(dev)
     y = torch.empty(m.n_rows, dtype=torch.float64, device=dev)
-    if a.matrix == "banded":
-        dm = sa.banded_to_device(m.n_rows, a.format, dev, **json.loads(a.kw))
-    else:
-        dm = sa.to_device(m, a.format, dev, **json.loads(a.kw))
+    dms = []
+    for kw in kws:
+        if a.matrix == "banded":
+            dms.append(sa.banded_to_device(m.n_rows, a.format, dev, **json.loads(kw)))
+        else:
+            dms.append(sa.to_device(m, a.format, dev, **json.loads(kw)))
+    configs = [(i, env) for i in range(len(kws)) for env in envs]
     s = torch.cuda.current_stream()
     res = [[] for _ in configs]
     same = [True for _ in configs]
     y0 = None
     for _ in range(a.rounds):
-        for i, env in enumerate(configs):
+        for i, (di, env) in enumerate(configs):
+            dm = dms[di]
             saved = {k: os.environ.get(k) for k in env}
             os.environ.update(env)
             for _ in range(5):
@@ -84,13 +90,14 @@ def main():
                     os.environ.pop(k, None)
                 else:
                     os.environ[k] = v
-    for i, env in enumerate(configs):
+    for i, (di, env) in enumerate(configs):
         ms = float(np.median(res[i]))
-        print(json.dumps(dict(fmt=a.format, env=env, ms=round(ms, 5), GBs_alg=round(b / ms * 1e-6, 1),
+        print(json.dumps(dict(fmt=a.format, kw=kws[di], env=env, ms=round(ms, 5), GBs_alg=round(b / ms * 1e-6, 1),
                               frac=round(b / ms * 1e-6 / sa.HBM_PEAK_GBS, 4),
                               spread=round((max(res[i]) - min(res[i])) / ms, 4), bit_identical=same[i])),
               flush=True)
-    print(json.dumps({"matrix": a.matrix, "copies": a.copies, "bytes_alg": b, "params": dm.params}, default=str))
+    print(json.dumps({"matrix": a.matrix, "copies": a.copies, "bytes_alg": b, "params": [d.params for d in dms]},
+                     default=str))
 
 
 if __name__ == "__main__":

@@ -112,6 +112,11 @@ for s in "${steps[@]}"; do
                   SPMV_HIP_LIB=$PWD/tools/ab/libspmv_hip_head.so run ab_sellcopy_cant_head_$i 300 python tools/ab_env.py --format sell --rounds 3 &&
                   run ab_sellcopy_cant_new_$i 300 python tools/ab_env.py --format sell --rounds 3
                 done;;
+    testxs) run gpu_tests_xstream 600 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "xstream";;
+    abxs) run ab_xstream 600 python tools/ab_env.py --format csr --kw '{}' --kw '{"xwin_rows": 1}' --env SPMV_CSR_XSTREAM=0,1 --rounds 5 &&
+          run ab_xstream_banded 600 python tools/ab_env.py --format csr --matrix banded --kw '{}' --kw '{"xwin_rows": 1}' --env SPMV_CSR_XSTREAM=0,1 --rounds 3 --reps 20;;
+    abpad) run ab_lds_pad 600 python tools/ab_env.py --format csr --kw '{}' --env SPMV_CSR_LDS_PAD=0,9216,15360,30000 --rounds 5 &&
+           run ab_lds_pad_xs 600 python tools/ab_env.py --format csr --kw '{"xwin_rows": 1}' --env SPMV_CSR_XSTREAM=1 --env SPMV_CSR_LDS_PAD=0,12288 --rounds 5;;
     test16) run gpu_tests_csr16 900 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "csr16 or csrf32 or xwin";;
     abcmrspipe) run ab_cmrs_pipe 300 python tools/ab_env.py --format cmrs --env SPMV_CMRS_PIPE=0,1 --rounds 5 &&
                 run ab_cmrs_pipe_h16 300 python tools/ab_env.py --format cmrs --kw '{"h": 16}' --env SPMV_CMRS_PIPE=0,1 --rounds 4;;

@@ -147,6 +147,18 @@ __device__ __forceinline__ double vone(const V *p)
     return (double)stream_load<NT>(p);
 }
 
+// y stores of the SpMV kernels: relaxed agent-scope atomic stores, i.e.
+// `global_store … sc1`, written through the XCD's L2 instead of sitting
+// there dirty until the matrix stream evicts them into HBM mid-kernel.  The
+// 16 MB of y of the cant batch cost the staged stream 0.2254 -> 0.2547 ms as
+// plain stores and 0.2428 ms as sc1 stores (csr_stream_probe_kernel P3/P4/PA,
+// profiles/round2/probe_ystore.log); the same stores into 64 KiB cost nothing,
+// so it is y's HBM write traffic, not the store instructions.
+__device__ __forceinline__ void store_y(double *p, double v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Load-policy switch for the streamed arrays: SPMV_STREAM_NT=1 / 0 forces
 // it, otherwise `dflt` (each kernel's measured best).  Read on every call
 // so a sweep can flip it inside one process.

@@ -124,7 +124,7 @@ __global__ __launch_bounds__(kBlock) void coo_tile_kernel(
             const int32_t r0 = __shfl(r, 0, kWave);
             if (lane == 0 && run_row >= 0 && r0 != run_row &&
                 !(first_continues && run_row == first_row))
-                y[run_row] = run;
+                store_y(y + (run_row), run);
 
             // Rows strictly between the previous entry's row and r are empty.
             int32_t rp = __shfl_up(r, 1, kWave);
@@ -132,7 +132,7 @@ __global__ __launch_bounds__(kBlock) void coo_tile_kernel(
                 rp = prev_r;
             if (valid)
                 for (int32_t g = rp + 1; g < r; ++g)
-                    y[g] = 0.0;
+                    store_y(y + (g), 0.0);
 
             if (first_continues && r == first_row) {
                 pref += p;  // goes to the carry, not through the scan
@@ -144,20 +144,20 @@ __global__ __launch_bounds__(kBlock) void coo_tile_kernel(
             const int32_t rn = __shfl_down(r, 1, kWave);
             const bool tail = valid && lane < nvalid - 1 && rn != r;
             if (tail && !(first_continues && r == first_row))
-                y[r] = p;
+                store_y(y + (r), p);
             run_row = __shfl(r, nvalid - 1, kWave);
             run = __shfl(p, nvalid - 1, kWave);
             prev_r = run_row;
         }
     }
     if (lane == 0 && run_row >= 0 && !(first_continues && run_row == first_row))
-        y[run_row] = run;
+        store_y(y + (run_row), run);
 
     // trailing empty rows after the last entry of the matrix
     if (t1 == nnz) {
         const int32_t last = row[nnz - 1];
         for (int64_t g = (int64_t)last + 1 + lane; g < n_rows; g += kWave)
-            y[g] = 0.0;
+            store_y(y + (g), 0.0);
     }
 
     pref = group_sum<kWave>(pref);
@@ -259,7 +259,7 @@ __global__ __launch_bounds__(kBlock) void cmrs_kernel(
     if (lane < h) {
         const int64_t r = s * h + lane;
         if (r < n_rows)  // reference Cmrs.cl:38-42 stored past y here
-            y[r] = acc[lane];
+            store_y(y + (r), acc[lane]);
     }
 }
 

@@ -78,7 +78,7 @@ __global__ __launch_bounds__(kBlock) void csr_vector_kernel(
     if constexpr (PAIR) {
         const double sum = row_dot_pairs<L>(beg, end, lane, col, val, XGlobal{x});
         if (lane == 0 && row < n_rows)
-            y[row] = sum;
+            store_y(y + (row), sum);
         return;
     }
     double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
@@ -97,7 +97,7 @@ __global__ __launch_bounds__(kBlock) void csr_vector_kernel(
         s0 += val[j] * x[col[j]];
     double sum = group_sum<L>((s0 + s1) + (s2 + s3));
     if (lane == 0 && row < n_rows)
-        y[row] = sum;
+        store_y(y + (row), sum);
 }
 
 // CSR-vector (direct: every L-lane group walks its own row) with the
@@ -131,7 +131,7 @@ __global__ __launch_bounds__(kBlock) void csr_vector_xwin_kernel(
     const double sum = staged ? row_dot_pairs<L>(beg, end, lane, col, val, XWindow{s_x, wnd.x})
                               : row_dot_pairs<L>(beg, end, lane, col, val, XGlobal{x});
     if (lane == 0 && row < n_rows)
-        y[row] = sum;
+        store_y(y + (row), sum);
 }
 
 // CSR-vector with the entry stream staged through LDS ("staged" variant).
@@ -232,8 +232,10 @@ struct Col16 {
 // value/column pairs FIRST (branch-free, so all 2R loads are in flight
 // together), then gathers x and stores the products in LDS.  A lane whose
 // pair starts at or past ce, or would reach past the array (nz entries),
-// loads pair 0 instead — always valid memory, one cached line — and its
-// products are never read: the reductions only read [cb, ce).  The one
+// loads the chunk's first pair instead — valid memory on a line the wave
+// reads anyway (pair 0 of the array, the former fallback, was one line
+// every workgroup of the grid hit) — and its products are never read: the
+// reductions only read [cb, ce).  The one
 // entry that can need more is the array's last entry when nz is odd; it
 // is loaded singly in a branch almost every wave skips.  (With the guarded
 // loads inside per-round branches the compiler serialised the rounds:
@@ -249,10 +251,11 @@ __device__ __forceinline__ void stage_products(int64_t cb, int64_t ce, int64_t n
     double2 v[R];
     int2 c[R];
     if (nz >= 2) {  // uniform; a 1-entry array has no pair 0
+        const int64_t spare = cb + 1 < nz ? cb : (nz - 2) & ~(int64_t)1;  // this chunk's first pair
 #pragma unroll
         for (int k = 0; k < R; ++k) {
             const int64_t p = cb + 2 * (int64_t)(threadIdx.x + k * kBlock);
-            const int64_t q = (p < ce && p + 1 < nz) ? p : 0;
+            const int64_t q = (p < ce && p + 1 < nz) ? p : spare;
             v[k] = vpair<NT>(val + q);
             c[k] = cols.pair(q);
         }
@@ -363,7 +366,7 @@ __device__ __forceinline__ void staged_group(
     }
     acc = group_sum<L>(acc);
     if (lane == 0 && row < n_rows)
-        y[row] = acc;
+        store_y(y + (row), acc);
     __syncthreads();
 }
 
@@ -378,8 +381,8 @@ struct XConst {
 };
 
 // One lane's share of a staged chunk in flight: R value pairs and R column
-// pairs, loaded branch-free (pairs past the chunk load pair 0 and are
-// never summed), so all 2R loads are outstanding together and can stay in
+// pairs, loaded branch-free (pairs past the chunk load the chunk's first
+// pair again and are never summed), so all 2R loads are outstanding together and can stay in
 // flight across a barrier while the previous chunk is reduced.
 template <int R, bool NT, typename V, typename Cols = Col32<NT>>
 struct StreamRegs {
@@ -399,10 +402,11 @@ struct StreamRegs {
             }
             return;
         }
+        const int64_t spare = cb + 1 < nz ? cb : (nz - 2) & ~(int64_t)1;  // this chunk's first pair
 #pragma unroll
         for (int k = 0; k < R; ++k) {
             const int64_t p = cb + 2 * (int64_t)(threadIdx.x + k * kBlock);
-            q[k] = (p < ce && p + 1 < nz) ? p : 0;
+            q[k] = (p < ce && p + 1 < nz) ? p : spare;
             v[k] = vpair<NT>(val + q[k]);
             c[k] = cols.raw(q[k]);
         }
@@ -443,8 +447,8 @@ struct StreamRegs {
 // barrier that protected the buffer from the next chunk's products is gone
 // (one barrier per chunk); the caller adds a barrier before reusing LDS.
 template <int L, int R, bool NT, typename XS, typename V, int NBUF = 1, bool PRE = false,
-          typename Cols = Col32<NT>>
-__device__ __forceinline__ void staged_window_pipelined(int64_t row0, int ngroups, const int64_t *s_off,
+          typename Cols = Col32<NT>, bool YST = false>
+__device__ __forceinline__ void staged_window_pipelined(int64_t row0, int ngroups, int64_t *s_off,
                                                         double2 *s_prod_base, const Cols cols,
                                                         const V *__restrict__ val, const XS xs,
                                                         double *__restrict__ y, int64_t n_rows, int64_t nz,
@@ -511,8 +515,21 @@ __device__ __forceinline__ void staged_window_pipelined(int64_t row0, int ngroup
         }
         acc = group_sum<L>(acc);
         const int64_t row = row0 + (int64_t)gi * RPB + g;
-        if (lane == 0 && row < n_rows)
-            y[row] = acc;
+        if constexpr (YST) {  // over the group's own offsets: nobody reads them any more
+            if (lane == 0)
+                reinterpret_cast<double *>(s_off)[gi * RPB + g] = acc;
+        } else if (lane == 0 && row < n_rows) {
+            store_y(y + (row), acc);
+        }
+    }
+    if constexpr (YST) {  // the window's y in whole-wave stores, after its last load
+        __syncthreads();
+        const double *sy = reinterpret_cast<const double *>(s_off);
+        const int nr = ngroups * RPB;
+        for (int i = threadIdx.x; i < nr; i += kBlock)
+            if (row0 + i < n_rows)
+                store_y(y + (row0 + i), sy[i]);
+        __syncthreads();  // s_off free for the next window
     }
 }
 
@@ -571,7 +588,7 @@ __device__ __forceinline__ void staged_window_flat(int64_t row0, const int64_t *
         const double s = group_sum<L>(acc[k]);
         const int64_t row = row0 + (int64_t)g * RW + k;
         if (lane == 0 && row < n_rows)
-            y[row] = s;
+            store_y(y + (row), s);
     }
 }
 
@@ -673,7 +690,8 @@ __global__ __launch_bounds__(kBlock) void csr_window_kernel(int64_t n_rows, int6
 #define SPMV_XWIN_WAVES 1
 #endif
 constexpr int kXwinWaves = SPMV_XWIN_WAVES;
-template <int L, int R, bool NT, typename V = double, int MODE = 0, bool PRE = false, typename Cols = Col32<NT>>
+template <int L, int R, bool NT, typename V = double, int MODE = 0, bool PRE = false, typename Cols = Col32<NT>,
+          bool YST = false>
 __global__ __launch_bounds__(kBlock, MODE >= 3 ? kXwinWaves : 1) void csr_xwin_kernel(
     int64_t n_rows, int64_t n_groups, int64_t gpw, const int64_t *__restrict__ row_ptr,
     const Cols cols, const V *__restrict__ val,
@@ -752,13 +770,13 @@ __global__ __launch_bounds__(kBlock, MODE >= 3 ? kXwinWaves : 1) void csr_xwin_k
             constexpr int NB = MODE == 4 ? 2 : 1;
             __syncthreads();  // window and offsets visible
             if (staged)
-                staged_window_pipelined<L, R, NT, XWindow, V, NB, PRE, Cols>(g_beg * RPB, (int)(g_end - g_beg), s_off,
-                                                                       s_prod, cols, val, XWindow{s_x, wnd.x}, y,
-                                                                       n_rows, nz, st_pre, pre);
+                staged_window_pipelined<L, R, NT, XWindow, V, NB, PRE, Cols, YST>(
+                    g_beg * RPB, (int)(g_end - g_beg), s_off, s_prod, cols, val, XWindow{s_x, wnd.x}, y, n_rows, nz,
+                    st_pre, pre);
             else
-                staged_window_pipelined<L, R, NT, XGlobal, V, NB, PRE, Cols>(g_beg * RPB, (int)(g_end - g_beg), s_off,
-                                                                       s_prod, cols, val, XGlobal{x}, y, n_rows,
-                                                                       nz, st_pre, pre);
+                staged_window_pipelined<L, R, NT, XGlobal, V, NB, PRE, Cols, YST>(
+                    g_beg * RPB, (int)(g_end - g_beg), s_off, s_prod, cols, val, XGlobal{x}, y, n_rows, nz, st_pre,
+                    pre);
             if constexpr (NB == 2)
                 __syncthreads();  // the last chunk's buffer is read before the next window writes LDS
             continue;
@@ -785,6 +803,167 @@ __global__ __launch_bounds__(kBlock, MODE >= 3 ? kXwinWaves : 1) void csr_xwin_k
                                                                      XGlobal{x}, y, n_rows, nz);
         }
     }
+}
+
+// Timing probes on the matrix's own arrays (SPMV_CSR_STREAM_PROBE=P; y is
+// WRONG): tools/bw_probe's staged stream — 1536-entry chunks of value/column
+// pairs, products to LDS, barrier, a 6-product read per lane, barrier — made
+// step by step more like csr_xwin_kernel, to find what the structure costs:
+//   P = 1: fixed 8192-entry tiles of the entry array (the bare probe);
+//   P = 2: one tile per 128-row window, bounds from row_ptr (chunk_start);
+//   P = 3: as 2, chunks restart at every 64-row group (as the kernel);
+//   P = 4: as 3, plus one y store per row (lane 0 of 4-lane groups);
+//   P = 5: as 4, windows placed XCD-contiguously;
+//   P = 6: as 3, the window's y values stored once at its end (128 lanes);
+//   P = 7: as 4 with non-temporal y stores;
+//   P = 8: as 6 with non-temporal y stores;
+//   P = 9 / A: as 4 with relaxed system- / agent-scope atomic stores;
+//   P = B: as 3 with one y store at the START of each workgroup;
+//   P = C: as 4 with two windows per workgroup;
+//   P = D / E: as 4 with "sc1 nt" / "sc0 sc1 nt" stores;
+//   P = F: as 4 with every store into the first 64 KiB of y;
+//   P = G / H / I: as 4, the stream loaded "sc1 nt" / "sc0 sc1 nt" / "sc1";
+//   P = J: as G with sc1 y stores.
+template <int P>
+__global__ __launch_bounds__(kBlock) void csr_stream_probe_kernel(const int64_t *__restrict__ row_ptr, int64_t n_rows,
+                                                                  const double *__restrict__ val,
+                                                                  const int32_t *__restrict__ col, int64_t nnz,
+                                                                  double *__restrict__ y)
+{
+    constexpr int R = 3;
+    constexpr int64_t CH = 2 * kBlock * R, TILE = 8192;
+    __shared__ double2 s_prod[kBlock * R];
+    const double *prod = reinterpret_cast<const double *>(s_prod);
+    const int64_t w = P >= 5 ? xcd_block(1) : blockIdx.x;
+    double s = 0.0;
+    auto stream = [&](int64_t t0, int64_t t1) {
+        for (int64_t cb = t0; cb < t1; cb += CH) {
+            double2 v[R];
+            int2 c[R];
+            if constexpr (P >= 16 && P <= 19) {  // stream loads with explicit cache-policy bits
+                v2f64 va[R];
+                v2i32 ca[R];
+#pragma unroll
+                for (int k = 0; k < R; ++k) {
+                    const int64_t p = cb + 2 * (int64_t)(threadIdx.x + k * kBlock);
+                    const int64_t q = p + 1 < t1 ? p : t0;
+                    if constexpr (P == 16 || P == 19) {
+                        asm volatile("global_load_dwordx4 %0, %1, off sc1 nt" : "=v"(va[k]) : "v"(val + q));
+                        asm volatile("global_load_dwordx2 %0, %1, off sc1 nt" : "=v"(ca[k]) : "v"(col + q));
+                    } else if constexpr (P == 17) {
+                        asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1 nt" : "=v"(va[k]) : "v"(val + q));
+                        asm volatile("global_load_dwordx2 %0, %1, off sc0 sc1 nt" : "=v"(ca[k]) : "v"(col + q));
+                    } else {
+                        asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(va[k]) : "v"(val + q));
+                        asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=v"(ca[k]) : "v"(col + q));
+                    }
+                }
+                asm volatile("s_waitcnt vmcnt(0)"
+                             : "+v"(va[0]), "+v"(va[1]), "+v"(va[2]), "+v"(ca[0]), "+v"(ca[1]), "+v"(ca[2])
+                             :
+                             : "memory");
+#pragma unroll
+                for (int k = 0; k < R; ++k) {
+                    v[k] = double2{va[k].x, va[k].y};
+                    c[k] = int2{ca[k].x, ca[k].y};
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < R; ++k) {
+                    const int64_t p = cb + 2 * (int64_t)(threadIdx.x + k * kBlock);
+                    const int64_t q = p + 1 < t1 ? p : t0;
+                    v[k] = stream_load2<true>(val + q);
+                    c[k] = stream_load2<true>(col + q);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < R; ++k)
+                s_prod[threadIdx.x + k * kBlock] = double2{v[k].x * (double)c[k].x, v[k].y * (double)c[k].y};
+            __syncthreads();
+            const int g = threadIdx.x / 4, lane = threadIdx.x % 4;
+#pragma unroll
+            for (int k = 0; k < 2 * R; ++k)
+                s += prod[g * 8 * R + lane + 4 * k];
+            __syncthreads();
+        }
+    };
+    if constexpr (P == 11) {  // a y store at the START of the workgroup only (then the P3 stream)
+        const int64_t row = w * 128 + threadIdx.x;
+        if (threadIdx.x < 128 && row < n_rows)
+            y[row] = 0.0;
+    }
+    if constexpr (P == 12) {  // as 4, two windows per workgroup (one end-of-workgroup per 256 rows)
+        for (int64_t ww = 2 * (int64_t)blockIdx.x; ww < 2 * (int64_t)blockIdx.x + 2; ++ww)
+            for (int gi = 0; gi < 2; ++gi) {
+                const int64_t r0 = ww * 128 + gi * 64;
+                if (r0 >= n_rows)
+                    break;
+                const int64_t r1 = r0 + 64 < n_rows ? r0 + 64 : n_rows;
+                stream(chunk_start(row_ptr[r0]), row_ptr[r1]);
+                const int64_t row = r0 + threadIdx.x / 4;
+                if (threadIdx.x % 4 == 0 && row < r1)
+                    y[row] = s;
+            }
+    } else if constexpr (P == 1) {
+        const int64_t t0 = w * TILE;
+        stream(t0, t0 + TILE < nnz ? t0 + TILE : nnz);
+    } else if constexpr (P == 2) {
+        const int64_t r0 = w * 128, r1 = r0 + 128 < n_rows ? r0 + 128 : n_rows;
+        stream(chunk_start(row_ptr[r0]), row_ptr[r1]);
+    } else {
+        for (int gi = 0; gi < 2; ++gi) {
+            const int64_t r0 = w * 128 + gi * 64;
+            if (r0 >= n_rows)
+                break;
+            const int64_t r1 = r0 + 64 < n_rows ? r0 + 64 : n_rows;
+            stream(chunk_start(row_ptr[r0]), row_ptr[r1]);
+            if constexpr (P == 4 || P == 5) {
+                const int64_t row = r0 + threadIdx.x / 4;
+                if (threadIdx.x % 4 == 0 && row < r1)
+                    y[row] = s;
+            } else if constexpr (P == 7) {
+                const int64_t row = r0 + threadIdx.x / 4;
+                if (threadIdx.x % 4 == 0 && row < r1)
+                    __builtin_nontemporal_store(s, y + row);
+            } else if constexpr (P == 13 || P == 14) {
+                const int64_t row = r0 + threadIdx.x / 4;
+                if (threadIdx.x % 4 == 0 && row < r1) {
+                    if constexpr (P == 13)
+                        asm volatile("global_store_dwordx2 %0, %1, off sc1 nt" ::"v"(y + row), "v"(s) : "memory");
+                    else
+                        asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1 nt" ::"v"(y + row), "v"(s) : "memory");
+                }
+            } else if constexpr (P == 15) {  // plain stores into 64 KiB of y (no HBM write traffic to speak of)
+                const int64_t row = r0 + threadIdx.x / 4;
+                if (threadIdx.x % 4 == 0 && row < r1)
+                    y[row & 8191] = s;
+            } else if constexpr (P >= 16 && P <= 18) {  // plain y stores beside the policy loads
+                const int64_t row = r0 + threadIdx.x / 4;
+                if (threadIdx.x % 4 == 0 && row < r1)
+                    y[row] = s;
+            } else if constexpr (P == 19) {
+                const int64_t row = r0 + threadIdx.x / 4;
+                if (threadIdx.x % 4 == 0 && row < r1)
+                    store_y(y + row, s);
+            } else if constexpr (P == 9 || P == 10) {
+                const int64_t row = r0 + threadIdx.x / 4;
+                if (threadIdx.x % 4 == 0 && row < r1)
+                    __hip_atomic_store(y + row, s, __ATOMIC_RELAXED,
+                                       P == 9 ? __HIP_MEMORY_SCOPE_SYSTEM : __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        if constexpr (P == 6 || P == 8) {  // the window's 128 y values at its end, one coalesced store
+            const int64_t row = w * 128 + threadIdx.x;
+            if (threadIdx.x < 128 && row < n_rows) {
+                if constexpr (P == 8)
+                    __builtin_nontemporal_store(s, y + row);
+                else
+                    y[row] = s;
+            }
+        }
+    }
+    if (s == 123.456)
+        y[0] = s;
 }
 
 // x ring of csr_xstream_kernel: column c lives in slot c & mask of a
@@ -975,7 +1154,7 @@ __global__ __launch_bounds__(kBlock, WAVES) void csr_xstream_kernel(
         acc = group_sum<L>(acc);
         const int64_t row = gi * RPB + g;
         if (lane == 0 && row < n_rows)
-            y[row] = acc;
+            store_y(y + (row), acc);
         bi = bn;
     }
 }
@@ -1087,7 +1266,7 @@ __device__ __forceinline__ void staged_group_pf(int64_t row, const int64_t *s_pt
     }
     acc = group_sum<L>(acc);
     if (lane == 0 && row < n_rows)
-        y[row] = acc;
+        store_y(y + (row), acc);
     __syncthreads();
 }
 
@@ -1222,7 +1401,7 @@ __global__ __launch_bounds__(kBlock) void csr_pipelined_kernel(
             acc = group_sum<L>(acc);
             const int64_t row = grp * RPB + g;
             if (lane == 0 && row < n_rows)
-                y[row] = acc;
+                store_y(y + (row), acc);
             acc = 0.0;
         }
         __syncthreads();  // s_prod free again
@@ -1540,6 +1719,15 @@ static bool csr_xwin_pre()
     return s && (s[0] == '0' || s[0] == '1') ? s[0] == '1' : kCsrXwinPre;
 }
 
+// SPMV_CSR_XWIN_YSTAGE=1 / 0: MODE 3 keeps the window's y values in LDS and
+// stores them once, after the window's last load (read per call)
+constexpr bool kCsrXwinYStage = false;
+static bool csr_xwin_ystage()
+{
+    const char *s = getenv("SPMV_CSR_XWIN_YSTAGE");
+    return s && (s[0] == '0' || s[0] == '1') ? s[0] == '1' : kCsrXwinYStage;
+}
+
 // SPMV_CSR_XWIN_R in {2,3,4,6,8}: value/column pairs per lane per chunk of
 // the MODE 3 kernel (non-temporal loads only; sweep knob, read per call);
 // 0 = the launcher's R
@@ -1685,6 +1873,9 @@ static void launch_csr_xwin(const spmv_dims &d, const int64_t *row_ptr, const Co
         if (kFp64 && csr_xwin_pre())
             hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, V, 3, kFp64, Cols>), dim3((unsigned)grid), dim3(kBlock), lds,
                                st, d.n_rows, groups, gpw, row_ptr, cols, val, x, y, win, xcap, remap);
+        else if (csr_xwin_ystage())
+            hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, V, 3, false, Cols, true>), dim3((unsigned)grid), dim3(kBlock),
+                               lds, st, d.n_rows, groups, gpw, row_ptr, cols, val, x, y, win, xcap, remap);
         else
             hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, V, 3, false, Cols>), dim3((unsigned)grid), dim3(kBlock), lds, st,
                                d.n_rows, groups, gpw, row_ptr, cols, val, x, y, win, xcap, remap);
@@ -1807,6 +1998,36 @@ extern "C" int spmv_csr_run_xwin(spmv_dims d, const int64_t *row_ptr, const int3
     if (L < 2 || L > 64 || (L & (L - 1)))
         return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_run_xwin: lanes_per_row must be 0 or a power of two in [2,64]");
     const int64_t gpw = csr_xwin_gpw(L, rows_per_window);
+    {
+        const char *pr = getenv("SPMV_CSR_STREAM_PROBE");
+        if (pr && pr[0] == 'P' && d.nnz >= 2) {  // timing probes P1..P5 (y wrong)
+            const unsigned gt = (unsigned)((d.nnz + 8191) / 8192), gw = (unsigned)((d.n_rows + 127) / 128);
+            const hipStream_t st = (hipStream_t)d.stream;
+            switch (pr[1]) {
+            case '2': hipLaunchKernelGGL((csr_stream_probe_kernel<2>), dim3(gw), dim3(kBlock), 0, st, row_ptr, d.n_rows, val, col, d.nnz, y); break;
+            case '3': hipLaunchKernelGGL((csr_stream_probe_kernel<3>), dim3(gw), dim3(kBlock), 0, st, row_ptr, d.n_rows, val, col, d.nnz, y); break;
+            case '4': hipLaunchKernelGGL((csr_stream_probe_kernel<4>), dim3(gw), dim3(kBlock), 0, st, row_ptr, d.n_rows, val, col, d.nnz, y); break;
+            case '5': hipLaunchKernelGGL((csr_stream_probe_kernel<5>), dim3(gw), dim3(kBlock), 0, st, row_ptr, d.n_rows, val, col, d.nnz, y); break;
+            case '6': hipLaunchKernelGGL((csr_stream_probe_kernel<6>), dim3(gw), dim3(kBlock), 0, st, row_ptr, d.n_rows, val, col, d.nnz, y); break;
+            case '7': hipLaunchKernelGGL((csr_stream_probe_kernel<7>), dim3(gw), dim3(kBlock), 0, st, row_ptr, d.n_rows, val, col, d.nnz, y); break;
+            case '8': hipLaunchKernelGGL((csr_stream_probe_kernel<8>), dim3(gw), dim3(kBlock), 0, st, row_ptr, d.n_rows, val, col, d.nnz, y); break;
+            case '9': hipLaunchKernelGGL((csr_stream_probe_kernel<9>), dim3(gw), dim3(kBlock), 0, st, row_ptr, d.n_rows, val, col, d.nnz, y); break;
+            case 'A': hipLaunchKernelGGL((csr_stream_probe_kernel<10>), dim3(gw), dim3(kBlock), 0, st, row_ptr, d.n_rows, val, col, d.nnz, y); break;
+            case 'B': hipLaunchKernelGGL((csr_stream_probe_kernel<11>), dim3(gw), dim3(kBlock), 0, st, row_ptr, d.n_rows, val, col, d.nnz, y); break;
+            case 'C': hipLaunchKernelGGL((csr_stream_probe_kernel<12>), dim3((gw + 1) / 2), dim3(kBlock), 0, st, row_ptr, d.n_rows, val, col, d.nnz, y); break;
+            case 'D': hipLaunchKernelGGL((csr_stream_probe_kernel<13>), dim3(gw), dim3(kBlock), 0, st, row_ptr, d.n_rows, val, col, d.nnz, y); break;
+            case 'E': hipLaunchKernelGGL((csr_stream_probe_kernel<14>), dim3(gw), dim3(kBlock), 0, st, row_ptr, d.n_rows, val, col, d.nnz, y); break;
+            case 'F': hipLaunchKernelGGL((csr_stream_probe_kernel<15>), dim3(gw), dim3(kBlock), 0, st, row_ptr, d.n_rows, val, col, d.nnz, y); break;
+            case 'G': hipLaunchKernelGGL((csr_stream_probe_kernel<16>), dim3(gw), dim3(kBlock), 0, st, row_ptr, d.n_rows, val, col, d.nnz, y); break;
+            case 'H': hipLaunchKernelGGL((csr_stream_probe_kernel<17>), dim3(gw), dim3(kBlock), 0, st, row_ptr, d.n_rows, val, col, d.nnz, y); break;
+            case 'I': hipLaunchKernelGGL((csr_stream_probe_kernel<18>), dim3(gw), dim3(kBlock), 0, st, row_ptr, d.n_rows, val, col, d.nnz, y); break;
+            case 'J': hipLaunchKernelGGL((csr_stream_probe_kernel<19>), dim3(gw), dim3(kBlock), 0, st, row_ptr, d.n_rows, val, col, d.nnz, y); break;
+            default: hipLaunchKernelGGL((csr_stream_probe_kernel<1>), dim3(gt), dim3(kBlock), 0, st, row_ptr, d.n_rows, val, col, d.nnz, y); break;
+            }
+            SPMV_CHECK_LAUNCH("csr_stream_probe_kernel");
+            return SPMV_SUCCESS;
+        }
+    }
     const bool nt = stream_nt(kCsrXwinNtDefault);
     const bool r4 = csr_stage_rounds(d.n_rows, d.nnz, L) == 4;  // R = 3 or 4 (the rule)
     const int2 *w = (const int2 *)win;

@@ -210,7 +210,7 @@ __global__ __launch_bounds__(1024) void sell_kernel(
     const double sum = slot_dot<KI, NT, U>(val + off, col + off, w, (int64_t)C * KI, xs);
     const int32_t row = perm[slot];
     if (row >= 0)
-        y[row] = sum;
+        y[row] = sum;  // scattered by perm: plain stores (sc1 measured 1.8 % slower, profiles/round2/ab_ystore.log)
 }
 
 template <int KI, bool NT, int U, typename XS = XGlobal>
@@ -223,7 +223,7 @@ __global__ __launch_bounds__(kBlock) void ell_kernel(
     if (i >= n_rows)
         return;
     const int64_t off = i * KI;
-    y[i] = slot_dot<KI, NT, U>(val + off, col + off, K, ld * KI, xs);
+    store_y(y + (i), slot_dot<KI, NT, U>(val + off, col + off, K, ld * KI, xs));
 }
 
 // Column window of every 256-row ELL workgroup: its rows' entries of
@@ -270,8 +270,8 @@ __global__ __launch_bounds__(kBlock) void ell_xwin_kernel(
     if (i >= n_rows)
         return;
     const int64_t off = i * KI;
-    y[i] = staged ? slot_dot_sel<KI, NT, U, PIPE>(val + off, col + off, K, ld * KI, XWindow{s_x, wnd.x})
-                  : slot_dot_sel<KI, NT, U, PIPE>(val + off, col + off, K, ld * KI, XGlobal{x});
+    store_y(y + i, staged ? slot_dot_sel<KI, NT, U, PIPE>(val + off, col + off, K, ld * KI, XWindow{s_x, wnd.x})
+                          : slot_dot_sel<KI, NT, U, PIPE>(val + off, col + off, K, ld * KI, XGlobal{x}));
 }
 
 constexpr int32_t kEllXwinCap = 2048;  // 16 KiB per 256-row workgroup
@@ -381,7 +381,7 @@ __global__ __launch_bounds__(1024) void sell_xwin_kernel(
                               : slot_dot_sel<KI, NT, U, PIPE>(val + off, col + off, w, (int64_t)C * KI, XGlobal{x});
     const int32_t row = perm[slot];
     if (row >= 0)
-        y[row] = sum;
+        y[row] = sum;  // scattered by perm: plain stores (sc1 measured 1.8 % slower, profiles/round2/ab_ystore.log)
 }
 
 // Wide slices (SELL split plan, spmv_sell_split_plan): a slice wider than

@@ -69,8 +69,9 @@ struct KeysNone {  // the tiled CSR: rows come from row_ptr, no keys
 // Streams entries [cb, ce) (cb even) of an nz-entry array into LDS:
 // products in s_prod, row keys through `keys`.  Every lane issues its R
 // value, column and key pair loads before the first product (branch-free:
-// a pair starting at or past ce loads pair 0, a cached line, and is never
-// read back), so 3R loads per lane are in flight together; a pair that
+// a pair starting at or past ce loads the chunk's first pair again, a line
+// the wave already reads, and is never read back), so 3R loads per lane are
+// in flight together; a pair that
 // straddles ce reads one entry past the chunk, inside the array, that no
 // reduction reads.  The array's odd last entry is loaded singly.
 // NT: non-temporal stream loads.
@@ -89,10 +90,11 @@ struct StageRegs {
     {
         if (nz < 2)  // uniform; a 1-entry array has no pair 0 (its entry: the tail in commit)
             return;
+        const int64_t spare = cb + 1 < nz ? cb : (nz - 2) & ~(int64_t)1;  // this chunk's first pair
 #pragma unroll
         for (int k = 0; k < R; ++k) {
             const int64_t p = cb + 2 * (int64_t)(threadIdx.x + k * kBlock);
-            const int64_t q = (p < ce && p + 1 < nz) ? p : 0;
+            const int64_t q = (p < ce && p + 1 < nz) ? p : spare;
             v[k] = vpair<NT>(val + q);
             c[k] = stream_load2<NT>(col + q);
             kp[k] = keys.load(q);
@@ -125,8 +127,9 @@ struct StageRegs {
 // Streams entries [cb, ce) (cb even) of an nz-entry array into LDS:
 // products in s_prod, row keys through `keys`.  Every lane issues its R
 // value, column and key pair loads before the first product (branch-free:
-// a pair starting at or past ce loads pair 0, a cached line, and is never
-// read back), so 3R loads per lane are in flight together; a pair that
+// a pair starting at or past ce loads the chunk's first pair again, a line
+// the wave already reads, and is never read back), so 3R loads per lane are
+// in flight together; a pair that
 // straddles ce reads one entry past the chunk, inside the array, that no
 // reduction reads.  The array's odd last entry is loaded singly.
 // NT: non-temporal stream loads.
@@ -226,7 +229,7 @@ __global__ __launch_bounds__(kBlock) void cmrs_staged_kernel(
     }
     acc = group_sum<L>(acc);
     if (active && lane == 0 && row < n_rows && s0 + si < n_strips)
-        y[row] = acc;
+        store_y(y + (row), acc);
 }
 
 // ------------------------------------------------------------------- COO
@@ -373,7 +376,7 @@ __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
         }
         s = group_sum<L>(s);
         if (lane == 0)
-            y[r] = s;
+            store_y(y + (r), s);
     }
 }
 
@@ -474,7 +477,7 @@ __global__ __launch_bounds__(kBlock) void csr_tiled_kernel(
             s += prod[j];
         s = group_sum<L>(s);
         if (lane == 0)
-            y[r] = s;
+            store_y(y + (r), s);
     }
 }
 
@@ -551,7 +554,7 @@ __global__ __launch_bounds__(kBlock) void cmrs_tiled_kernel(
         acc = group_sum<L>(acc);
         const int64_t r = s * h + k;
         if (lane == 0 && r < n_rows)
-            y[r] = acc;
+            store_y(y + (r), acc);
     }
 }
 

@@ -36,6 +36,8 @@ def main():
                     help="to_device keyword arguments (JSON; several: one device matrix each, crossed with --env)")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--total", action="store_true",
+                    help="time the reps as one span (two events) instead of an event after every launch")
     a = ap.parse_args()
     import torch
 
@@ -74,13 +76,22 @@ def main():
             os.environ.update(env)
             for _ in range(5):
                 dm.run(x, y, s)
-            ev = [torch.cuda.Event(enable_timing=True) for _ in range(a.reps + 1)]
-            ev[0].record(s)
-            for k in range(a.reps):
-                dm.run(x, y, s)
-                ev[k + 1].record(s)
-            torch.cuda.synchronize()
-            res[i].append(float(np.mean([ev[k].elapsed_time(ev[k + 1]) for k in range(a.reps)])))
+            if a.total:
+                ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+                ev[0].record(s)
+                for k in range(a.reps):
+                    dm.run(x, y, s)
+                ev[1].record(s)
+                torch.cuda.synchronize()
+                res[i].append(ev[0].elapsed_time(ev[1]) / a.reps)
+            else:
+                ev = [torch.cuda.Event(enable_timing=True) for _ in range(a.reps + 1)]
+                ev[0].record(s)
+                for k in range(a.reps):
+                    dm.run(x, y, s)
+                    ev[k + 1].record(s)
+                torch.cuda.synchronize()
+                res[i].append(float(np.mean([ev[k].elapsed_time(ev[k + 1]) for k in range(a.reps)])))
             if y0 is None:
                 y0 = y.clone()
             elif not torch.equal(y.view(torch.int64), y0.view(torch.int64)):

@@ -84,7 +84,7 @@ for s in "${steps[@]}"; do
     abflat) run ab_flat_l4 600 python tools/ab_env.py --format csr --env SPMV_CSR_XWIN_MODE=3,5 --env SPMV_CSR_XWIN_R=3,4 --rounds 5 &&
             run ab_flat_l2 600 python tools/ab_env.py --format csr --kw '{"lanes": 2}' --env SPMV_CSR_XWIN_MODE=3,5 --env SPMV_CSR_XWIN_R=3,4 --rounds 5 &&
             run ab_flat_l8 600 python tools/ab_env.py --format csr --kw '{"lanes": 8}' --env SPMV_CSR_XWIN_MODE=3,5 --env SPMV_CSR_XWIN_R=3,4 --rounds 5;;
-    abformats) for i in 1 2; do
+    abformats) for i in 1 2; do  # head = tools/ab/libspmv_hip_head.so
                  SPMV_HIP_LIB=$PWD/tools/ab/libspmv_hip_head.so run abf_head_$i 600 python tools/time_formats.py &&
                  run abf_new_$i 600 python tools/time_formats.py
                done;;
@@ -117,6 +117,17 @@ for s in "${steps[@]}"; do
           run ab_xstream_banded 600 python tools/ab_env.py --format csr --matrix banded --kw '{}' --kw '{"xwin_rows": 1}' --env SPMV_CSR_XSTREAM=0,1 --rounds 3 --reps 20;;
     abpad) run ab_lds_pad 600 python tools/ab_env.py --format csr --kw '{}' --env SPMV_CSR_LDS_PAD=0,9216,15360,30000 --rounds 5 &&
            run ab_lds_pad_xs 600 python tools/ab_env.py --format csr --kw '{"xwin_rows": 1}' --env SPMV_CSR_XSTREAM=1 --env SPMV_CSR_LDS_PAD=0,12288 --rounds 5;;
+    abp11) for i in 1 2; do
+             run abp11_base_$i 300 python tools/ab_env.py --format csr --rounds 3 &&
+             SPMV_HIP_LIB=$PWD/tools/ab/libspmv_hip_p11.so run abp11_probe_$i 300 python tools/ab_env.py --format csr --rounds 3
+           done && run bw_probe 300 tools/bw_probe;;
+    abp11m) run abmodes_real 300 python tools/ab_env.py --format csr --env SPMV_CSR_XWIN_MODE=0,3 --rounds 3 &&
+            run abmodes_real_total 300 python tools/ab_env.py --format csr --env SPMV_CSR_XWIN_MODE=0,3 --rounds 3 --total &&
+            SPMV_HIP_LIB=$PWD/tools/ab/libspmv_hip_p11.so run abp11_total 300 python tools/ab_env.py --format csr --rounds 3 --total &&
+            run bw_probe 300 tools/bw_probe;;
+    abdata) run ab_stream_probe 300 python tools/ab_env.py --format csr --env SPMV_CSR_STREAM_PROBE=P3,P4,PA,PG,PH,PI,PJ --rounds 5 --total &&
+
+            run bw_probe 300 tools/bw_probe;;
     test16) run gpu_tests_csr16 900 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "csr16 or csrf32 or xwin";;
     abcmrspipe) run ab_cmrs_pipe 300 python tools/ab_env.py --format cmrs --env SPMV_CMRS_PIPE=0,1 --rounds 5 &&
                 run ab_cmrs_pipe_h16 300 python tools/ab_env.py --format cmrs --kw '{"h": 16}' --env SPMV_CMRS_PIPE=0,1 --rounds 4;;

@@ -128,6 +128,7 @@ for s in "${steps[@]}"; do
     abdata) run ab_stream_probe 300 python tools/ab_env.py --format csr --env SPMV_CSR_STREAM_PROBE=P3,P4,PA,PG,PH,PI,PJ --rounds 5 --total &&
 
             run bw_probe 300 tools/bw_probe;;
+    rehot) run shard_rehearse_hot 1100 python tools/shard_rehearse.py --gpus 1,8 --hot -1,262144,131072,65536 --reps 10;;
     test16) run gpu_tests_csr16 900 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "csr16 or csrf32 or xwin";;
     abcmrspipe) run ab_cmrs_pipe 300 python tools/ab_env.py --format cmrs --env SPMV_CMRS_PIPE=0,1 --rounds 5 &&
                 run ab_cmrs_pipe_h16 300 python tools/ab_env.py --format cmrs --kw '{"h": 16}' --env SPMV_CMRS_PIPE=0,1 --rounds 4;;

@@ -64,7 +64,7 @@ def main():
     ap.add_argument("--format", default="csr")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--row-weights", default="4", help="spmv_partition_rows_weighted weights to try")
-    ap.add_argument("--hot", type=int, default=-1, help="CSR hot-column table: -1 library rule, 0 off, H")
+    ap.add_argument("--hot", default="-1", help="CSR hot-column table(s), comma-separated: -1 library rule, 0 off, H")
     ap.add_argument("--graph", action="store_true", help="replay each SpMV as a captured HIP graph")
     a = ap.parse_args()
     import torch
@@ -78,10 +78,11 @@ def main():
     x = torch.from_numpy(xh).to(dev)
     b_total = sa.bytes_alg(n, n, z)
     base = None
-    kw = {"hot": None if a.hot < 0 else a.hot} if a.format in ("csr", "coo", "cmrs", "sell") else {}
-    if a.format == "sell":
-        kw["sigma"] = 1 << 24  # whole-matrix sort on R-MAT (bench.py's R-MAT default)
-    for G, w in [(int(g), float(w)) for w in a.row_weights.split(",") for g in a.gpus.split(",")]:
+    for G, w, hot in [(int(g), float(w), int(h)) for h in a.hot.split(",") for w in a.row_weights.split(",")
+                      for g in a.gpus.split(",")]:
+        kw = {"hot": None if hot < 0 else hot} if a.format in ("csr", "coo", "cmrs", "sell") else {}
+        if a.format == "sell":
+            kw["sigma"] = 1 << 24  # whole-matrix sort on R-MAT (bench.py's R-MAT default)
         bounds = sa.partition_rows(n, ptr, G, align=1024, row_weight=w)
         times, nnzs, params = [], [], None
         for r in range(G):
@@ -103,7 +104,7 @@ def main():
         agg = b_total / (tmax * 1e-3) * 1e-9
         base = base or agg
         print(json.dumps({"workload": "rmat 1e7/1e8", "format": a.format, "params_shard0": params, "gpus": G,
-                          "row_weight": w, "graph": a.graph, "shard_rows": np.diff(bounds).tolist(), "shard_nnz": nnzs, "shard_ms": [round(t, 4) for t in times], "max_ms": round(tmax, 4),
+                          "row_weight": w, "hot": hot, "graph": a.graph, "shard_rows": np.diff(bounds).tolist(), "shard_nnz": nnzs, "shard_ms": [round(t, 4) for t in times], "max_ms": round(tmax, 4),
                           "aggregate_GBs_warm": round(agg, 1), "speedup_vs_first": round(agg / base, 2)}),
               flush=True)
 

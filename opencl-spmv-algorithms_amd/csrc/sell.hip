@@ -287,6 +287,16 @@ namespace spmv {
 // A small matrix (fewer than ~2 windows per CU) needs the parallelism of
 // 256-slot groups more than merged stores: one cant-like copy has only 61
 // windows of 1024 rows for 256 CUs.
+// y of a σ = 1024 window staged in LDS and stored in row order
+// (sell_xwin_kernel); SPMV_SELL_YSTAGE=0 / 1 overrides, read per call
+constexpr bool kSellYStage = true;  // cant batch 0.2583 -> 0.2490 ms (profiles/round2/ab_sell_ystage.log)
+static bool sell_ystage(int bt, int32_t sigma)
+{
+    const char *s = getenv("SPMV_SELL_YSTAGE");
+    const bool on = (s && (s[0] == '0' || s[0] == '1')) ? s[0] == '1' : kSellYStage;
+    return on && bt == 1024 && sigma == 1024;
+}
+
 static void sell_geometry(int32_t C, int32_t sigma, int64_t n_slices, int *bt, int64_t *blocks)
 {
     static const int force256 = [] {
@@ -352,34 +362,63 @@ __global__ __launch_bounds__(1024) void sell_xwin_kernel(
     int32_t C, int64_t n_slices, const int64_t *__restrict__ slice_ptr,
     const int32_t *__restrict__ perm, const int32_t *__restrict__ col,
     const double *__restrict__ val, const double *__restrict__ x,
-    double *__restrict__ y, const int2 *__restrict__ win, int32_t xcap, int64_t wcap, int remap)
+    double *__restrict__ y, const int2 *__restrict__ win, int32_t xcap, int64_t wcap, int remap,
+    int64_t ystage_rows)
 {
     extern __shared__ double s_x[];
     const int64_t blk = xcd_block(remap);  // remap: neighbouring windows on one XCD (shared x lines in L2)
     const int2 wnd = win[blk];
     const int32_t span = wnd.y - wnd.x + 1;
     const bool staged = span > 0 && span <= xcap;  // uniform per workgroup
+    const int64_t slot = blk * blockDim.x + threadIdx.x;
+    const int64_t s = slot / C;
+    const int32_t row = s < n_slices ? perm[slot] : -1;
     if (staged) {
         if (blockDim.x == 1024)  // one sigma window per workgroup (the default geometry)
             copy_window<1024, 2>(s_x, x, wnd.x, span);
         else
             for (int32_t i = threadIdx.x; i < span; i += blockDim.x)
                 s_x[i] = x[wnd.x + i];
-        __syncthreads();
     }
-    const int64_t slot = blk * blockDim.x + threadIdx.x;
-    const int64_t s = slot / C;
-    if (s >= n_slices)
-        return;
-    const int64_t r = slot - s * C;
-    const int64_t base = slice_ptr[s];
-    int64_t w = (slice_ptr[s + 1] - base) / C;
-    w = w < wcap ? w : wcap;
-    const int64_t off = base + r * KI;
-    const double sum = staged ? slot_dot_sel<KI, NT, U, PIPE>(val + off, col + off, w, (int64_t)C * KI,
-                                                              XWindow{s_x, wnd.x})
-                              : slot_dot_sel<KI, NT, U, PIPE>(val + off, col + off, w, (int64_t)C * KI, XGlobal{x});
-    const int32_t row = perm[slot];
+    // ystage_rows > 0 (σ = 1024 = the workgroup): does the window keep its
+    // rows in order (equal lengths, e.g. the banded matrix)?  Asked at the
+    // barrier that publishes the x window anyway.
+    bool in_order = false;
+    if (ystage_rows > 0)
+        in_order = __syncthreads_and(row < 0 || row == slot);  // uniform
+    else if (staged)
+        __syncthreads();
+    double sum = 0.0;
+    if (s < n_slices) {
+        const int64_t r = slot - s * C;
+        const int64_t base = slice_ptr[s];
+        int64_t w = (slice_ptr[s + 1] - base) / C;
+        w = w < wcap ? w : wcap;
+        const int64_t off = base + r * KI;
+        sum = staged ? slot_dot_sel<KI, NT, U, PIPE>(val + off, col + off, w, (int64_t)C * KI, XWindow{s_x, wnd.x})
+                     : slot_dot_sel<KI, NT, U, PIPE>(val + off, col + off, w, (int64_t)C * KI, XGlobal{x});
+    }
+    if (ystage_rows > 0) {
+        if (in_order) {  // whole rows in order already: written through L2 directly
+            if (row >= 0)
+                store_y(y + row, sum);
+            return;
+        }
+        // the window's slots hold a permutation of its 1024 rows: y goes
+        // through LDS and out in row order (store_y) instead of as 8-byte
+        // stores scattered by perm
+        __shared__ double s_y[1024];
+        const int64_t r0 = blk * 1024;
+        if (__syncthreads_and(row < 0 || (row >= r0 && row < r0 + 1024))) {  // uniform
+            if (row >= 0)
+                s_y[row - r0] = sum;
+            __syncthreads();
+            const int64_t rr = r0 + threadIdx.x;
+            if (rr < ystage_rows)
+                store_y(y + rr, s_y[threadIdx.x]);
+            return;
+        }
+    }
     if (row >= 0)
         y[row] = sum;  // scattered by perm: plain stores (sc1 measured 1.8 % slower, profiles/round2/ab_ystore.log)
 }
@@ -572,7 +611,8 @@ extern "C" int spmv_sell_run_xwin(spmv_dims d, int32_t C, int32_t sigma, int32_t
                               : sell_xwin_kernel<1, false, 4>);
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(bt), (size_t)xcap * sizeof(double),
                        (hipStream_t)d.stream, C, n_slices, slice_ptr, perm, col, val, x, y,
-                       (const int2 *)win, xcap, (int64_t)INT64_MAX, xwin_remap(false) ? 1 : 0);
+                       (const int2 *)win, xcap, (int64_t)INT64_MAX, xwin_remap(false) ? 1 : 0,
+                       sell_ystage(bt, sigma) ? d.n_rows : (int64_t)0);
     SPMV_CHECK_LAUNCH("sell_xwin_kernel");
     return SPMV_SUCCESS;
 }
@@ -743,7 +783,7 @@ extern "C" int spmv_sell_run_split(spmv_dims d, int32_t C, int32_t sigma, int32_
                             : (nt ? sell_xwin_kernel<1, true, 4> : sell_xwin_kernel<1, false, 4>);
         hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(bt), (size_t)xcap * sizeof(double), st, C, n_slices,
                            slice_ptr, perm, col, val, x, y, (const int2 *)win, xcap, (int64_t)T,
-                           xwin_remap(false) ? 1 : 0);
+                           xwin_remap(false) ? 1 : 0, sell_ystage(bt, sigma) ? d.n_rows : (int64_t)0);
     } else {
         auto kern = ki == 2 ? (nt ? sell_kernel<2, true, 4> : sell_kernel<2, false, 4>)
                             : (nt ? sell_kernel<1, true, 4> : sell_kernel<1, false, 4>);

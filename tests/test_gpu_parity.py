@@ -742,6 +742,28 @@ def test_csr_xstream(torch_dev, monkeypatch, case, fmt):
 
 
 @pytest.mark.parametrize("case", ["cantlike", "ragged", "fixtures", "empty_runs"])
+def test_sell_ystage(torch_dev, monkeypatch, case):
+    """SELL-64-1024 with y staged per σ-window in LDS and stored in row order
+    (SPMV_SELL_YSTAGE=1) writes exactly the values of the perm-scattered
+    stores, including a partial last window and padding slots."""
+    torch, dev = torch_dev
+    for m in _xstream_cases(case):
+        if m.n_rows == 0:
+            continue
+        dm = sa.to_device(m, "sell", dev)
+        x = torch.from_numpy(np.random.default_rng(14).uniform(-1, 1, max(m.n_cols, 1))).to(dev)
+        ys = []
+        for on in ("0", "1"):
+            monkeypatch.setenv("SPMV_SELL_YSTAGE", on)
+            y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
+            dm.run(x, y)
+            ys.append(y)
+        torch.cuda.synchronize()
+        assert torch.equal(ys[1].view(torch.int64), ys[0].view(torch.int64)), m.label
+        assert_parity(m, ys[1].cpu().numpy(), x.cpu().numpy()[: m.n_cols])
+
+
+@pytest.mark.parametrize("case", ["cantlike", "ragged", "fixtures", "empty_runs"])
 def test_csr_xwin_load_modes(torch_dev, monkeypatch, case):
     """Every load schedule of csr_xwin_kernel (SPMV_CSR_XWIN_MODE 0-4 and the
     first-chunk prefetch) forms the same chunks and sums: the same bits.

@@ -128,7 +128,12 @@ for s in "${steps[@]}"; do
     abdata) run ab_stream_probe 300 python tools/ab_env.py --format csr --env SPMV_CSR_STREAM_PROBE=P3,P4,PA,PG,PH,PI,PJ --rounds 5 --total &&
 
             run bw_probe 300 tools/bw_probe;;
-    rehot) run shard_rehearse_hot 1100 python tools/shard_rehearse.py --gpus 1,8 --hot -1,262144,131072,65536 --reps 10;;
+    rehot) run shard_rehearse_hot 1100 python tools/shard_rehearse.py --gpus 1,8 --hot=-1,262144,131072,65536 --reps 10;;
+    rew) run shard_rehearse_w3 1100 python tools/shard_rehearse.py --gpus 8 --row-weights 2,3,5 --reps 10 &&
+         run shard_rehearse_graph 1100 python tools/shard_rehearse.py --gpus 1,8 --row-weights 4 --reps 10 --graph;;
+    absy) run test_sell_ystage 600 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "sell" &&
+          run ab_sell_ystage 300 python tools/ab_env.py --format sell --env SPMV_SELL_YSTAGE=0,1 --rounds 5 --total &&
+          run ab_sell_ystage_banded 300 python tools/ab_env.py --format sell --matrix banded --env SPMV_SELL_YSTAGE=0,1 --rounds 3 --reps 20 --total;;
     test16) run gpu_tests_csr16 900 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "csr16 or csrf32 or xwin";;
     abcmrspipe) run ab_cmrs_pipe 300 python tools/ab_env.py --format cmrs --env SPMV_CMRS_PIPE=0,1 --rounds 5 &&
                 run ab_cmrs_pipe_h16 300 python tools/ab_env.py --format cmrs --kw '{"h": 16}' --env SPMV_CMRS_PIPE=0,1 --rounds 4;;

@@ -447,8 +447,8 @@ struct StreamRegs {
 // barrier that protected the buffer from the next chunk's products is gone
 // (one barrier per chunk); the caller adds a barrier before reusing LDS.
 template <int L, int R, bool NT, typename XS, typename V, int NBUF = 1, bool PRE = false,
-          typename Cols = Col32<NT>, bool YST = false>
-__device__ __forceinline__ void staged_window_pipelined(int64_t row0, int ngroups, int64_t *s_off,
+          typename Cols = Col32<NT>>
+__device__ __forceinline__ void staged_window_pipelined(int64_t row0, int ngroups, const int64_t *s_off,
                                                         double2 *s_prod_base, const Cols cols,
                                                         const V *__restrict__ val, const XS xs,
                                                         double *__restrict__ y, int64_t n_rows, int64_t nz,
@@ -515,21 +515,10 @@ __device__ __forceinline__ void staged_window_pipelined(int64_t row0, int ngroup
         }
         acc = group_sum<L>(acc);
         const int64_t row = row0 + (int64_t)gi * RPB + g;
-        if constexpr (YST) {  // over the group's own offsets: nobody reads them any more
-            if (lane == 0)
-                reinterpret_cast<double *>(s_off)[gi * RPB + g] = acc;
-        } else if (lane == 0 && row < n_rows) {
+        // (the window's y staged in LDS and stored once at its end measured
+        // the same: 0.2481 vs 0.2478 ms, profiles/round2/ab_ystage.log)
+        if (lane == 0 && row < n_rows)
             store_y(y + (row), acc);
-        }
-    }
-    if constexpr (YST) {  // the window's y in whole-wave stores, after its last load
-        __syncthreads();
-        const double *sy = reinterpret_cast<const double *>(s_off);
-        const int nr = ngroups * RPB;
-        for (int i = threadIdx.x; i < nr; i += kBlock)
-            if (row0 + i < n_rows)
-                store_y(y + (row0 + i), sy[i]);
-        __syncthreads();  // s_off free for the next window
     }
 }
 
@@ -690,8 +679,7 @@ __global__ __launch_bounds__(kBlock) void csr_window_kernel(int64_t n_rows, int6
 #define SPMV_XWIN_WAVES 1
 #endif
 constexpr int kXwinWaves = SPMV_XWIN_WAVES;
-template <int L, int R, bool NT, typename V = double, int MODE = 0, bool PRE = false, typename Cols = Col32<NT>,
-          bool YST = false>
+template <int L, int R, bool NT, typename V = double, int MODE = 0, bool PRE = false, typename Cols = Col32<NT>>
 __global__ __launch_bounds__(kBlock, MODE >= 3 ? kXwinWaves : 1) void csr_xwin_kernel(
     int64_t n_rows, int64_t n_groups, int64_t gpw, const int64_t *__restrict__ row_ptr,
     const Cols cols, const V *__restrict__ val,
@@ -770,11 +758,11 @@ __global__ __launch_bounds__(kBlock, MODE >= 3 ? kXwinWaves : 1) void csr_xwin_k
             constexpr int NB = MODE == 4 ? 2 : 1;
             __syncthreads();  // window and offsets visible
             if (staged)
-                staged_window_pipelined<L, R, NT, XWindow, V, NB, PRE, Cols, YST>(
+                staged_window_pipelined<L, R, NT, XWindow, V, NB, PRE, Cols>(
                     g_beg * RPB, (int)(g_end - g_beg), s_off, s_prod, cols, val, XWindow{s_x, wnd.x}, y, n_rows, nz,
                     st_pre, pre);
             else
-                staged_window_pipelined<L, R, NT, XGlobal, V, NB, PRE, Cols, YST>(
+                staged_window_pipelined<L, R, NT, XGlobal, V, NB, PRE, Cols>(
                     g_beg * RPB, (int)(g_end - g_beg), s_off, s_prod, cols, val, XGlobal{x}, y, n_rows, nz, st_pre,
                     pre);
             if constexpr (NB == 2)
@@ -1014,8 +1002,8 @@ __device__ __forceinline__ void copy_ring(double *s_x, const double *__restrict_
 // Chunks, products and sums are those of staged_group: y is bit-identical to
 // the other staged CSR kernels.  A group whose range does not fit in the ring
 // gathers from global memory.
-template <int L, int R, bool NT, typename V = double, typename Cols = Col32<NT>, int WAVES = 1>
-__global__ __launch_bounds__(kBlock, WAVES) void csr_xstream_kernel(
+template <int L, int R, bool NT, typename V = double, typename Cols = Col32<NT>>
+__global__ __launch_bounds__(kBlock) void csr_xstream_kernel(
     int64_t n_rows, int64_t n_groups, const int64_t *__restrict__ row_ptr, const Cols cols,
     const V *__restrict__ val, const double *__restrict__ x, double *__restrict__ y,
     const int2 *__restrict__ gwin, int32_t cap)
@@ -1719,15 +1707,6 @@ static bool csr_xwin_pre()
     return s && (s[0] == '0' || s[0] == '1') ? s[0] == '1' : kCsrXwinPre;
 }
 
-// SPMV_CSR_XWIN_YSTAGE=1 / 0: MODE 3 keeps the window's y values in LDS and
-// stores them once, after the window's last load (read per call)
-constexpr bool kCsrXwinYStage = false;
-static bool csr_xwin_ystage()
-{
-    const char *s = getenv("SPMV_CSR_XWIN_YSTAGE");
-    return s && (s[0] == '0' || s[0] == '1') ? s[0] == '1' : kCsrXwinYStage;
-}
-
 // SPMV_CSR_XWIN_R in {2,3,4,6,8}: value/column pairs per lane per chunk of
 // the MODE 3 kernel (non-temporal loads only; sweep knob, read per call);
 // 0 = the launcher's R
@@ -1784,19 +1763,13 @@ static void launch_csr_xstream(const spmv_dims &d, const int64_t *row_ptr, const
         ++lg;
     const int32_t cap = 1 << lg;
     const size_t lds = (size_t)cap * sizeof(double) + csr_lds_pad();
-    const char *ws = getenv("SPMV_CSR_XSTREAM_WAVES");  // sweep knob: 6 = VGPRs capped for 6 waves/SIMD
-    const bool w6 = ws && ws[0] == '6';
-    static int64_t resident[2][16] = {};  // per ring size (the occupancy calculator once per size)
-    if (resident[w6][lg] == 0 || csr_lds_pad() != 0)
-        resident[w6][lg] = w6 ? persistent_grid(csr_xstream_kernel<L, R, NT, V, Cols, 6>, INT64_MAX, lds)
-                              : persistent_grid(csr_xstream_kernel<L, R, NT, V, Cols>, INT64_MAX, lds);
-    const int64_t grid = resident[w6][lg] < groups ? resident[w6][lg] : groups;
-    if (w6)
-        hipLaunchKernelGGL((csr_xstream_kernel<L, R, NT, V, Cols, 6>), dim3((unsigned)grid), dim3(kBlock), lds,
-                           (hipStream_t)d.stream, d.n_rows, groups, row_ptr, cols, val, x, y, win, cap);
-    else
-        hipLaunchKernelGGL((csr_xstream_kernel<L, R, NT, V, Cols>), dim3((unsigned)grid), dim3(kBlock), lds,
-                           (hipStream_t)d.stream, d.n_rows, groups, row_ptr, cols, val, x, y, win, cap);
+    // (capping its VGPRs for 6 waves per SIMD spills 13 registers)
+    static int64_t resident[16] = {};  // per ring size (the occupancy calculator once per size)
+    if (resident[lg] == 0 || csr_lds_pad() != 0)
+        resident[lg] = persistent_grid(csr_xstream_kernel<L, R, NT, V, Cols>, INT64_MAX, lds);
+    const int64_t grid = resident[lg] < groups ? resident[lg] : groups;
+    hipLaunchKernelGGL((csr_xstream_kernel<L, R, NT, V, Cols>), dim3((unsigned)grid), dim3(kBlock), lds,
+                       (hipStream_t)d.stream, d.n_rows, groups, row_ptr, cols, val, x, y, win, cap);
 }
 
 template <int L, int R, bool NT, typename Cols, typename V = double>
@@ -1873,9 +1846,6 @@ static void launch_csr_xwin(const spmv_dims &d, const int64_t *row_ptr, const Co
         if (kFp64 && csr_xwin_pre())
             hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, V, 3, kFp64, Cols>), dim3((unsigned)grid), dim3(kBlock), lds,
                                st, d.n_rows, groups, gpw, row_ptr, cols, val, x, y, win, xcap, remap);
-        else if (csr_xwin_ystage())
-            hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, V, 3, false, Cols, true>), dim3((unsigned)grid), dim3(kBlock),
-                               lds, st, d.n_rows, groups, gpw, row_ptr, cols, val, x, y, win, xcap, remap);
         else
             hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, V, 3, false, Cols>), dim3((unsigned)grid), dim3(kBlock), lds, st,
                                d.n_rows, groups, gpw, row_ptr, cols, val, x, y, win, xcap, remap);

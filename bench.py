@@ -82,6 +82,8 @@ def parse():
     p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                    help="collective backend for N>1 (nccl = RCCL; gloo only to rehearse on one GPU)")
     p.add_argument("--share-gpu", action="store_true", help="all ranks on cuda:0 (rehearsal only)")
+    p.add_argument("--graph", default="yes", choices=["yes", "no"],
+                   help="replay the timed launches from one HIP graph (yes) or launch them eagerly")
     return p.parse_args()
 
 
@@ -123,12 +125,58 @@ def fmt_kwargs(args, fmt):
     return {}
 
 
+GRAPH = {"on": True}  # --graph: the timed launches replayed from one HIP graph
+
+
+def capture(torch, dm, x, y, steps):
+    """`steps` launches of one SpMV captured into a HIP graph (None if the
+    capture fails: then the launches are timed eagerly)."""
+    try:
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(steps):
+                dm.run(x, y)
+        torch.cuda.synchronize()
+        return g
+    except Exception as e:  # noqa: BLE001 — fall back to eager launches, say so
+        print(f"warning: HIP graph capture failed ({e}); timing eager launches", file=sys.stderr)
+        return None
+
+
 def time_steps(torch, dm, x, y, steps, warmup, dist=None):
     """W warm-up launches, then exactly `steps` launches bracketed by a
-    barrier + synchronize; per-launch HIP events on the launch stream."""
+    barrier + synchronize.  Default: the `steps` launches are captured into
+    one HIP graph and replayed once (one SpMV kernel per step, as eager; the
+    graph removes the host launch path between them: 0.2473 vs 0.2537 ms per
+    step, profiles/round2/ab_graph.log), timed by two HIP events on the
+    launch stream, so the per-launch time is the span / steps.  --graph no:
+    eager launches with one HIP event after each."""
     stream = torch.cuda.current_stream()
     for _ in range(warmup):
         dm.run(x, y, stream)
+    g = capture(torch, dm, x, y, steps) if GRAPH["on"] else None
+    if g is not None:
+        g.replay()  # first replay (uploads the graph), untimed
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        a.record(stream)
+        g.replay()
+        b.record(stream)
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        per = a.elapsed_time(b) / steps
+        del g
+        GRAPH["last"] = "hip-graph"
+        return wall, [per] * steps
+    GRAPH["last"] = "eager"
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
     torch.cuda.synchronize()
     if dist is not None:
@@ -303,6 +351,7 @@ def cpu_baseline(m_single_csr, copies, budget_s):
 
 def main():
     args = parse()
+    GRAPH["on"] = args.graph == "yes"
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -329,6 +378,8 @@ def main():
     dm, x, y = w["dm"], w["x"], w["y"]
     n_rows, nnz, bytes_step = w["rows"], w["nnz"], w["bytes_rank"]
     wall, kern = time_steps(torch, dm, x, y, args.steps, args.warmup, dist)
+    launch = ("hip-graph: the K launches captured once, replayed once; kernel_ms = span / K"
+              if GRAPH.get("last") == "hip-graph" else "eager launches, one HIP event after each")
     if args.profile:
         if rank == 0:
             print(json.dumps({"profile_run": args.format, "ms_per_launch": float(np.mean(kern))}))
@@ -479,7 +530,8 @@ def main():
             "data": w["data"],
             "config": dict(w["config"], format=args.format, params=fmt_kwargs(args, args.format) or None,
                            rows_rank0=n_rows, nnz_rank0=nnz, bytes_alg_rank0_step=bytes_step,
-                           bytes_alg_all_ranks_step=total_bytes, parallelism=f"row-shard x{world}"),
+                           bytes_alg_all_ranks_step=total_bytes, parallelism=f"row-shard x{world}",
+                           launch=launch),
             "gflops": round(gflops, 1),
             "roofline": roofline,
             "cpu_baseline": cpu,

@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--total", action="store_true",
                     help="time the reps as one span (two events) instead of an event after every launch")
+    ap.add_argument("--graph", action="store_true",
+                    help="with --total: capture the reps launches into one HIP graph and time its replay")
     a = ap.parse_args()
     import torch
 
@@ -76,7 +78,22 @@ def main():
             os.environ.update(env)
             for _ in range(5):
                 dm.run(x, y, s)
-            if a.total:
+            if a.total and a.graph:
+                torch.cuda.synchronize()
+                gr = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gr):
+                    for k in range(a.reps):
+                        dm.run(x, y)
+                torch.cuda.synchronize()
+                gr.replay()
+                ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+                ev[0].record(s)
+                gr.replay()
+                ev[1].record(s)
+                torch.cuda.synchronize()
+                res[i].append(ev[0].elapsed_time(ev[1]) / a.reps)
+                del gr
+            elif a.total:
                 ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
                 ev[0].record(s)
                 for k in range(a.reps):

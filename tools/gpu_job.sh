@@ -136,6 +136,9 @@ for s in "${steps[@]}"; do
           run ab_sell_ystage_banded 300 python tools/ab_env.py --format sell --matrix banded --env SPMV_SELL_YSTAGE=0,1 --rounds 3 --reps 20 --total;;
     abr32) run ab_r_csrf32 300 python tools/ab_env.py --format csrf32 --env SPMV_CSR_XWIN_R=0,4,6 --rounds 4 --total &&
            run ab_r_csr16 300 python tools/ab_env.py --format csr16 --env SPMV_CSR_XWIN_R=0,4,6 --rounds 4 --total;;
+    abgraph) run ab_graph_events 300 python tools/ab_env.py --format csr --rounds 4 &&
+             run ab_graph_span 300 python tools/ab_env.py --format csr --rounds 4 --total &&
+             run ab_graph_replay 300 python tools/ab_env.py --format csr --rounds 4 --total --graph;;
     test16) run gpu_tests_csr16 900 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "csr16 or csrf32 or xwin";;
     abcmrspipe) run ab_cmrs_pipe 300 python tools/ab_env.py --format cmrs --env SPMV_CMRS_PIPE=0,1 --rounds 5 &&
                 run ab_cmrs_pipe_h16 300 python tools/ab_env.py --format cmrs --kw '{"h": 16}' --env SPMV_CMRS_PIPE=0,1 --rounds 4;;

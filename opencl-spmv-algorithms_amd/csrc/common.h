@@ -163,6 +163,11 @@ __device__ __forceinline__ void store_y(double *p, double v)
 // it, otherwise `dflt` (each kernel's measured best).  Read on every call
 // so a sweep can flip it inside one process.
 bool stream_nt(bool dflt);
+// SPMV_XHOT_COLD_NT=1: hot-table kernels gather the cold columns non-temporally
+bool xhot_cold_nt();
+// SPMV_TILED_FUSED_CARRY=1: spanning rows finished inside the tiled kernel
+// (tiled CSR with a plan; default: the carry pass)
+bool tiled_fused_carry();
 
 // Where x[c] comes from: global memory (XGlobal) or the workgroup's
 // window x[lo..hi] staged in LDS (XWindow: the x-window kernels).
@@ -202,12 +207,25 @@ __device__ __forceinline__ void copy_window(double *s_x, const double *__restric
 
 // Hot-column CSR (spmv_csr_run_tiled_hot): ids >= M name the compact table
 // xh of the most frequent columns, gathered from x at the start of the run.
-struct XHot {
+// CNT = true gathers the cold columns non-temporally, so their lines (each
+// used about once per launch) do not evict the hot table from L2.
+template <bool CNT>
+struct XHotT {
     const double *__restrict__ x;
     const double *__restrict__ xh;
     int32_t M;
-    __device__ __forceinline__ double operator()(int32_t c) const { return c >= M ? xh[c - M] : x[c]; }
+    __device__ __forceinline__ double operator()(int32_t c) const
+    {
+        if (c >= M)
+            return xh[c - M];
+        if constexpr (CNT)
+            return __builtin_nontemporal_load(x + c);
+        else
+            return x[c];
+    }
 };
+struct XHot : XHotT<false> {};
+struct XHotNT : XHotT<true> {};
 
 // [min, max] of col[e0..e1) over one 256-thread workgroup ({0, -1} when
 // empty); the result is valid in thread 0.  Build-time pass of the

@@ -2169,11 +2169,8 @@ extern "C" int spmv_csr_run_tiled_hot(spmv_dims d, const int64_t *row_ptr, const
     double *carry_val = xh + H;
     int32_t *own_lo = (int32_t *)(carry_val + tiles);
     int32_t *carry_row = own_lo + tiles + 1;
-    int rc = launch_csr_tiled_hot(d, row_ptr, col_hot, val, x, y, H, hot, xh, own_lo_plan, own_lo, carry_row,
-                                  carry_val);
-    if (rc != SPMV_SUCCESS)
-        return rc;
-    return launch_carry(tiles, carry_row, carry_val, y, (hipStream_t)d.stream);
+    return launch_csr_tiled_hot(d, row_ptr, col_hot, val, x, y, H, hot, xh, own_lo_plan, own_lo, carry_row,
+                                carry_val);
 }
 
 // CSR with fp32 values (8 bytes per entry instead of
@@ -2255,9 +2252,6 @@ extern "C" int spmv_csr_f32v_run_tiled_hot(spmv_dims d, const int64_t *row_ptr, 
     double *carry_val = xh + H;
     int32_t *own_lo = (int32_t *)(carry_val + tiles);
     int32_t *carry_row = own_lo + tiles + 1;
-    int rc = launch_csr_tiled_hot(d, row_ptr, col_hot, val, x, y, H, hot, xh, own_lo_plan, own_lo, carry_row,
-                                  carry_val);
-    if (rc != SPMV_SUCCESS)
-        return rc;
-    return launch_carry(tiles, carry_row, carry_val, y, (hipStream_t)d.stream);
+    return launch_csr_tiled_hot(d, row_ptr, col_hot, val, x, y, H, hot, xh, own_lo_plan, own_lo, carry_row,
+                                carry_val);
 }

@@ -417,13 +417,49 @@ __global__ __launch_bounds__(kBlock) void csr_tile_rows_kernel(int64_t n_rows, i
 // on R-MAT (tools/rmat_exp.hip mode 2).
 constexpr int kTiledRowCap = 1024;
 
-template <int L, int R, bool NT, typename XS, typename V = double>
+// Fused carry (FC, plan given): a row spanning tiles t_own..t_last is
+// finished by whichever of its tiles arrives last, so no carry pass runs.
+// Every participant stores its partial in part[t] (carry_val), then adds
+// one to cnt[t_own] (release, agent scope); the tile that sees P - 1 sums
+// part[t_own+1..t_last] from zero in tile order, adds it to part[t_own]
+// exactly as coo_carry_kernel adds its sum to the owner's y (same bits),
+// and resets the counter, so the plan's counters are zero between runs.
+__device__ __forceinline__ void tiled_arrive(int64_t r, int64_t t_own, int64_t t_last, int64_t tile, double v,
+                                             double *__restrict__ part, uint32_t *__restrict__ cnt,
+                                             double *__restrict__ y)
+{
+    __hip_atomic_store(part + tile, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t P = (uint32_t)(t_last - t_own + 1);
+    // release only: the acquire (an L2 invalidate on gfx950) is paid once,
+    // by the last arriver, not by every participant
+    const uint32_t old = __hip_atomic_fetch_add(cnt + t_own, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (old + 1 != P)
+        return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    double s = 0.0;
+    for (int64_t u = t_own + 1; u <= t_last; u += 8) {
+        double vv[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            vv[k] = u + k <= t_last ? __hip_atomic_load(part + u + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                    : 0.0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (u + k <= t_last)
+                s += vv[k];
+    }
+    const double own = __hip_atomic_load(part + t_own, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    store_y(y + r, own + s);
+    __hip_atomic_store(cnt + t_own, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int L, int R, bool NT, typename XS, typename V = double, bool FC = false>
 __global__ __launch_bounds__(kBlock) void csr_tiled_kernel(
     int64_t n_rows, int64_t nnz, const int64_t *__restrict__ row_ptr,
     const int32_t *__restrict__ col, const V *__restrict__ val,
     const XS xs, double *__restrict__ y,
     const int32_t *__restrict__ own_lo, int32_t *__restrict__ carry_row,
-    double *__restrict__ carry_val)
+    double *__restrict__ carry_val, uint32_t *__restrict__ cnt = nullptr)
 {
     constexpr int CH = 2 * kBlock * R;
     constexpr int GROUPS = kBlock / L;
@@ -457,7 +493,12 @@ __global__ __launch_bounds__(kBlock) void csr_tiled_kernel(
                 c += prod[j - t0];
         }
         c = group_sum<L>(c);
-        if (lane == 0) {
+        if constexpr (FC) {
+            if (lane == 0 && cr >= 0) {
+                const int64_t b0 = row_ptr[cr], b1 = r_lo < n_rows ? row_ptr[r_lo] : nnz;
+                tiled_arrive(cr, b0 / CH, (b1 - 1) / CH, tile, c, carry_val, cnt, y);
+            }
+        } else if (lane == 0) {
             carry_row[tile] = cr;
             carry_val[tile] = c;
         }
@@ -476,8 +517,16 @@ __global__ __launch_bounds__(kBlock) void csr_tiled_kernel(
         for (int j = a + lane; j < b; j += L)
             s += prod[j];
         s = group_sum<L>(s);
-        if (lane == 0)
+        if (lane == 0) {
+            if constexpr (FC) {
+                const int64_t e = r == r_hi && r < n_rows ? row_ptr[r + 1] : 0;
+                if (e > t1) {  // the tile's last row runs on: owner's part
+                    tiled_arrive(r, tile, (e - 1) / CH, tile, s, carry_val, cnt, y);
+                    continue;
+                }
+            }
             store_y(y + (r), s);
+        }
     }
 }
 
@@ -624,7 +673,7 @@ int64_t csr_tiled_tile() { return 2 * kBlock * 3; }
 template <typename XS, typename V>
 static void launch_tiled_xs(const spmv_dims &d, int64_t tiles, const int64_t *row_ptr, const int32_t *col,
                             const V *val, XS xs, double *y, const int32_t *own_lo, int32_t *carry_row,
-                            double *carry_val)
+                            double *carry_val, uint32_t *cnt = nullptr)
 {
     constexpr int R = 3;
     const hipStream_t st = (hipStream_t)d.stream;
@@ -632,7 +681,11 @@ static void launch_tiled_xs(const spmv_dims &d, int64_t tiles, const int64_t *ro
     const bool nt = stream_nt(true);
 #define SPMV_TILED(LL)                                                                                    \
     do {                                                                                                  \
-        if (nt)                                                                                           \
+        if (cnt)                                                                                          \
+            hipLaunchKernelGGL((csr_tiled_kernel<LL, R, true, XS, V, true>), dim3((unsigned)tiles),      \
+                               dim3(kBlock), 0, st, d.n_rows, d.nnz, row_ptr, col, val, xs, y, own_lo,     \
+                               carry_row, carry_val, cnt);                                                \
+        else if (nt)                                                                                      \
             hipLaunchKernelGGL((csr_tiled_kernel<LL, R, true, XS, V>), dim3((unsigned)tiles), dim3(kBlock), 0, \
                                st, d.n_rows, d.nnz, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val); \
         else                                                                                              \
@@ -676,19 +729,25 @@ int launch_csr_tiled_hot(const spmv_dims &d, const int64_t *row_ptr, const int32
     const int64_t tiles = (d.nnz + ch - 1) / ch;
     const hipStream_t st = (hipStream_t)d.stream;
     launch_hot_gather(H, hot, x, xh, st);
+    // a plan carries the fused carry's arrival counters (kept zero between
+    // runs): rows spanning tiles are finished inside the tiled kernel
+    uint32_t *cnt = own_lo_plan && tiled_fused_carry() ? (uint32_t *)(own_lo_plan + tiles + 1) : nullptr;
     if (!own_lo_plan) {
         hipLaunchKernelGGL(csr_tile_rows_kernel, dim3((unsigned)((tiles + 1 + kBlock - 1) / kBlock)),
                            dim3(kBlock), 0, st, d.n_rows, d.nnz, tiles, ch, row_ptr, own_lo);
         SPMV_CHECK_LAUNCH("csr_tile_rows_kernel");
         own_lo_plan = own_lo;
     }
-    if (H > 0)
+    if (H > 0 && xhot_cold_nt())
+        launch_tiled_xs(d, tiles, row_ptr, col, val, XHotNT{x, xh, (int32_t)d.n_cols}, y, own_lo_plan,
+                        carry_row, carry_val, cnt);
+    else if (H > 0)
         launch_tiled_xs(d, tiles, row_ptr, col, val, XHot{x, xh, (int32_t)d.n_cols}, y, own_lo_plan, carry_row,
-                        carry_val);
+                        carry_val, cnt);
     else
-        launch_tiled_xs(d, tiles, row_ptr, col, val, XGlobal{x}, y, own_lo_plan, carry_row, carry_val);
+        launch_tiled_xs(d, tiles, row_ptr, col, val, XGlobal{x}, y, own_lo_plan, carry_row, carry_val, cnt);
     SPMV_CHECK_LAUNCH("csr_tiled_kernel (hot columns)");
-    return SPMV_SUCCESS;
+    return cnt ? SPMV_SUCCESS : launch_carry(tiles, carry_row, carry_val, y, st);
 }
 
 template int launch_csr_tiled_hot<double>(const spmv_dims &, const int64_t *, const int32_t *, const double *,
@@ -990,7 +1049,8 @@ extern "C" int spmv_cmrs_xwin_build(spmv_dims d, int32_t h, int64_t n_strips, co
 // row_ptr only: built once here, the runs skip their pre-pass.
 extern "C" int64_t spmv_csr_tiled_plan_len(int64_t nnz)
 {
-    return nnz > 0 ? (nnz + csr_tiled_tile() - 1) / csr_tiled_tile() + 1 : 0;
+    // own_lo[tiles + 1], then one arrival counter per tile (fused carry)
+    return nnz > 0 ? 2 * ((nnz + csr_tiled_tile() - 1) / csr_tiled_tile()) + 1 : 0;
 }
 
 extern "C" int spmv_csr_tiled_plan(spmv_dims d, const int64_t *row_ptr, int32_t *own_lo)
@@ -1007,5 +1067,6 @@ extern "C" int spmv_csr_tiled_plan(spmv_dims d, const int64_t *row_ptr, int32_t 
     hipLaunchKernelGGL(csr_tile_rows_kernel, dim3((unsigned)((tiles + 1 + kBlock - 1) / kBlock)), dim3(kBlock), 0,
                        (hipStream_t)d.stream, d.n_rows, d.nnz, tiles, ch, row_ptr, own_lo);
     SPMV_CHECK_LAUNCH("csr_tile_rows_kernel (plan)");
-    return SPMV_SUCCESS;
+    const hipError_t e = hipMemsetAsync(own_lo + tiles + 1, 0, (size_t)tiles * sizeof(uint32_t), (hipStream_t)d.stream);
+    return e == hipSuccess ? SPMV_SUCCESS : fail(SPMV_PROGRAM_ERROR, "spmv_csr_tiled_plan: zero counters", e);
 }

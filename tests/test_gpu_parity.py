@@ -580,6 +580,41 @@ def test_csr_tiled_empty_row_runs(torch_dev, H):
     assert_parity(m, ya.cpu().numpy(), x.cpu().numpy())
 
 
+@pytest.mark.parametrize("case", ["rmat", "empty_runs", "one_hub"])
+@pytest.mark.parametrize("fmt,H", [("csr", 0), ("csr", 4096), ("csrf32", 4096)])
+def test_csr_tiled_fused_carry(torch_dev, monkeypatch, case, fmt, H):
+    """Fused carry (SPMV_TILED_FUSED_CARRY=1): rows spanning tiles finished
+    by their last-arriving tile inside csr_tiled_kernel give the same bits as
+    the carry pass, run after run (the plan's arrival counters return to
+    zero), including a hub row over ~700 tiles and rows after empty runs."""
+    torch, dev = torch_dev
+    if case == "rmat":
+        m = sa.gen_rmat(1_000_000, 10_000_000, scale=20, seed=1)
+    elif case == "empty_runs":
+        m, _ = _empty_run_matrix()
+    else:  # row 3 holds 1e6 entries, the rest 1-3 each
+        rng = np.random.default_rng(5)
+        n = 200_000
+        lens = rng.integers(1, 4, n)
+        lens[3] = 1_000_000
+        r = np.repeat(np.arange(n, dtype=np.int32), lens)
+        m = sa.Coo(n, n, r, rng.integers(0, n, r.size).astype(np.int32), rng.uniform(-1, 1, r.size))
+    dm = sa.to_device(m, fmt, dev, hot=H, variant=4)
+    assert dm.params["variant"] == 4
+    x = torch.from_numpy(np.random.default_rng(8).uniform(-1, 1, m.n_cols)).to(dev)
+    monkeypatch.setenv("SPMV_TILED_FUSED_CARRY", "0")
+    y0 = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
+    dm.run(x, y0)
+    monkeypatch.setenv("SPMV_TILED_FUSED_CARRY", "1")
+    for _ in range(3):
+        y1 = torch.full_like(y0, float("nan"))
+        dm.run(x, y1)
+        torch.cuda.synchronize()
+        assert torch.equal(y1.view(torch.int64), y0.view(torch.int64))
+    if fmt == "csr":
+        assert_parity(m, y1.cpu().numpy(), x.cpu().numpy())
+
+
 @pytest.mark.parametrize("fmt,kw", [("coo", {}), ("cmrs", {"cmrs_variant": 1}), ("cmrs", {"cmrs_variant": 1, "h": 32}),
                                     ("sell", {"xwin": False}), ("sell", {"sigma": 1 << 24, "ki": 2, "xwin": False}),
                                     ("sell", {"split": 0, "xwin": False}), ("hyb", {}), ("hyb", {"ki": 1})])

@@ -22,7 +22,9 @@ card, not a substitute for the driver's 8-GPU run.
 from __future__ import annotations
 
 import argparse
+import itertools
 import json
+import os
 import sys
 from pathlib import Path
 
@@ -66,7 +68,16 @@ def main():
     ap.add_argument("--row-weights", default="4", help="spmv_partition_rows_weighted weights to try")
     ap.add_argument("--hot", default="-1", help="CSR hot-column table(s), comma-separated: -1 library rule, 0 off, H")
     ap.add_argument("--graph", action="store_true", help="replay each SpMV as a captured HIP graph")
+    ap.add_argument("--env", action="append", default=[],
+                    help="KEY=v1,v2: library knobs timed interleaved on every shard (several: cartesian product)")
+    ap.add_argument("--rounds", type=int, default=1, help="interleaved rounds per shard (median of rounds)")
     a = ap.parse_args()
+    keys, vals = [], []
+    for e in a.env:
+        k, v = e.split("=", 1)
+        keys.append(k)
+        vals.append(v.split(","))
+    envs = [dict(zip(keys, c)) for c in itertools.product(*vals)] or [{}]
     import torch
 
     dev = torch.device("cuda:0")
@@ -84,7 +95,7 @@ def main():
         if a.format == "sell":
             kw["sigma"] = 1 << 24  # whole-matrix sort on R-MAT (bench.py's R-MAT default)
         bounds = sa.partition_rows(n, ptr, G, align=1024, row_weight=w)
-        times, nnzs, params = [], [], None
+        times, nnzs, params = [[] for _ in envs], [], None
         for r in range(G):
             lo, hi = int(bounds[r]), int(bounds[r + 1])
             lptr = ptr[lo:hi + 1] - ptr[lo]
@@ -93,21 +104,29 @@ def main():
             dm = sa.to_device(loc, a.format, dev, **kw)
             params = params or {k: v for k, v in dm.params.items() if isinstance(v, (int, float, str))}
             y = torch.empty(max(loc.n_rows, 1), dtype=torch.float64, device=dev)
-            times.append(time_shard(torch, dm, x, y, a.reps, a.graph))
+            per = [[] for _ in envs]
+            for _ in range(a.rounds):
+                for i, env in enumerate(envs):
+                    os.environ.update(env)
+                    per[i].append(time_shard(torch, dm, x, y, a.reps, a.graph))
+                    bad, first = sa.check(loc, xh, y[:loc.n_rows].cpu().numpy())
+                    if bad:
+                        raise SystemExit(f"G={G} shard {r} env {env}: parity failure at row {first}")
+            for i in range(len(envs)):
+                times[i].append(float(np.median(per[i])))
             nnzs.append(loc.nnz)
-            bad, first = sa.check(loc, xh, y[:loc.n_rows].cpu().numpy())
-            if bad:
-                raise SystemExit(f"G={G} shard {r}: parity failure at row {first}")
             del dm, y, loc
             torch.cuda.empty_cache()
-        tmax = max(times)
-        agg = b_total / (tmax * 1e-3) * 1e-9
-        base = base or agg
-        print(json.dumps({"workload": "rmat 1e7/1e8", "format": a.format, "params_shard0": params, "gpus": G,
-                          "row_weight": w, "hot": hot, "graph": a.graph, "shard_rows": np.diff(bounds).tolist(), "shard_nnz": nnzs, "shard_ms": [round(t, 4) for t in times], "max_ms": round(tmax, 4),
-                          "aggregate_GBs_warm": round(agg, 1), "speedup_vs_first": round(agg / base, 2)}),
-              flush=True)
-
+        for i, env in enumerate(envs):
+            tmax = max(times[i])
+            agg = b_total / (tmax * 1e-3) * 1e-9
+            base = base or agg
+            print(json.dumps({"workload": "rmat 1e7/1e8", "format": a.format, "env": env, "params_shard0": params,
+                              "gpus": G, "row_weight": w, "hot": hot, "graph": a.graph,
+                              "shard_rows": np.diff(bounds).tolist(), "shard_nnz": nnzs,
+                              "shard_ms": [round(t, 4) for t in times[i]], "max_ms": round(tmax, 4),
+                              "aggregate_GBs_warm": round(agg, 1), "speedup_vs_first": round(agg / base, 2)}),
+                  flush=True)
 
 if __name__ == "__main__":
     main()

@@ -82,6 +82,9 @@ def parse():
     p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                    help="collective backend for N>1 (nccl = RCCL; gloo only to rehearse on one GPU)")
     p.add_argument("--share-gpu", action="store_true", help="all ranks on cuda:0 (rehearsal only)")
+    p.add_argument("--rmat-strong", default="auto", choices=["auto", "yes", "no"],
+                   help="also time CSR on the R-MAT 1e7/1e8 row-sharded over all ranks (strong scaling, "
+                        "north-star sweep; auto: with the default cant-like workload)")
     p.add_argument("--graph", default="yes", choices=["yes", "no"],
                    help="replay the timed launches from one HIP graph (yes) or launch them eagerly")
     return p.parse_args()
@@ -349,6 +352,45 @@ def cpu_baseline(m_single_csr, copies, budget_s):
             "gflops": round(2 * B * int(ptr[-1]) / t * 1e-9, 2)}
 
 
+def rmat_strong(args, torch, dev, rank, world, dist, cdev):
+    """North-star sweep (BASELINE.json north_star, configs[3]): CSR on the
+    1e7 x 1e7 / 1e8-entry R-MAT, rows cut into `world` shards (entries +
+    RMAT_ROW_WEIGHT x rows balanced, 1024-aligned), one per rank, x
+    replicated; aggregate GB/s = bytes_alg(whole matrix) / max over ranks
+    of the per-step time (HIP-graph replay between barriers).  Every rank's
+    shard output is checked against the host rule before it counts."""
+    a = argparse.Namespace(**vars(args))
+    a.workload, a.format, a.variant, a.lanes = "rmat", "csr", 0, 0
+    t0 = time.perf_counter()
+    w = build_workload(a, torch, dev, rank, world)
+    build_s = time.perf_counter() - t0
+    steps = max(20, args.steps // 2)
+    wall, kern = time_steps(torch, w["dm"], w["x"], w["y"], steps, 5, dist)
+    bad = w["check"]()
+    if bad:
+        raise SystemExit(f"rank {rank}: R-MAT parity failure ({bad})")
+    t = torch.tensor([wall / steps * 1e3, float(np.mean(kern))], dtype=torch.float64, device=cdev)
+    shard_ms = [float(np.mean(kern))]
+    if dist is not None:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        g = [torch.zeros(1, dtype=torch.float64, device=cdev) for _ in range(world)]
+        dist.all_gather(g, torch.tensor([float(np.mean(kern))], dtype=torch.float64, device=cdev))
+        shard_ms = [float(v.item()) for v in g]
+    step_ms, kern_ms = float(t[0].item()), float(t[1].item())
+    params = {k: v for k, v in w["dm"].params.items() if isinstance(v, (int, float, str))}
+    out = {"workload": "csr SpMV on R-MAT 1e7/1e8 (configs[3]) row-sharded over all ranks, x replicated",
+           "scaling": "strong", "steps": steps,
+           "aggregate_GBs": round(w["bytes_total"] / (step_ms * 1e-3) * 1e-9, 1),
+           "GFLOPs": round(2 * w["nnz_total"] / (step_ms * 1e-3) * 1e-9, 1),
+           "frac_of_one_gpu_peak": round(w["bytes_total"] / (step_ms * 1e-3) * 1e-9 / sa.HBM_PEAK_GBS, 4),
+           "ms_per_step": round(step_ms, 5), "max_shard_kernel_ms": round(kern_ms, 5),
+           "shard_ms": [round(v, 5) for v in shard_ms], "bytes_alg_whole": w["bytes_total"],
+           "params_rank0": params, "parity_ok": True, "host_build_s": round(build_s, 1)}
+    del w
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     args = parse()
     GRAPH["on"] = args.graph == "yes"
@@ -514,6 +556,16 @@ def main():
             ptr, col, val = sa.csr_from_coo(single)
             cpu = cpu_baseline((ptr, col, val, single.n_rows, single.n_cols), B, args.cpu_seconds)
 
+    rstrong = None
+    if args.rmat_strong == "yes" or (args.rmat_strong == "auto" and args.workload == "cantlike"):
+        w.pop("dm", None)
+        try:
+            del dm
+        except NameError:
+            pass
+        torch.cuda.empty_cache()
+        rstrong = rmat_strong(args, torch, dev, rank, world, dist, cdev)
+
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -538,6 +590,7 @@ def main():
             "per_format": per_format,
             "cant_single": cant_single,
             "allgather": allgather,
+            "rmat_strong": rstrong,
             "device": sa.device_name(gpu),
         }
         print(json.dumps(line), flush=True)

@@ -151,7 +151,10 @@ int spmv_csr_run_tiled_hot(spmv_dims d, const int64_t *row_ptr, const int32_t *c
                            size_t ws_bytes);
 /* The tile -> first owned row table of the entry-balanced CSR (int32,
  * spmv_csr_tiled_plan_len(nnz) entries) built once from row_ptr; passed as
- * own_lo_plan it saves every run its pre-pass (NULL: built per run).    */
+ * own_lo_plan it saves every run its pre-pass (NULL: built per run).  Its
+ * tail holds one arrival counter per tile, zeroed here, that the fused
+ * carry (rows spanning tiles finished inside the tiled kernel) leaves at
+ * zero after every run; runs sharing one plan must not overlap in time. */
 int64_t spmv_csr_tiled_plan_len(int64_t nnz);
 int spmv_csr_tiled_plan(spmv_dims d, const int64_t *row_ptr, int32_t *own_lo);
 

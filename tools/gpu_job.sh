@@ -118,7 +118,7 @@ for s in "${steps[@]}"; do
     abpad) run ab_lds_pad 600 python tools/ab_env.py --format csr --kw '{}' --env SPMV_CSR_LDS_PAD=0,9216,15360,30000 --rounds 5 &&
            run ab_lds_pad_xs 600 python tools/ab_env.py --format csr --kw '{"xwin_rows": 1}' --env SPMV_CSR_XSTREAM=1 --env SPMV_CSR_LDS_PAD=0,12288 --rounds 5;;
     abfused) run gpu_tests_fused 600 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "fused_carry or csr_hot or empty_row_runs" &&
-             run ab_fused_rehearse 900 python tools/shard_rehearse.py --gpus 1,8 --env SPMV_TILED_FUSED_CARRY=0,1 --env SPMV_XHOT_COLD_NT=0,1 --rounds 2;;
+             run ab_fused_rehearse 900 python tools/shard_rehearse.py --gpus 1,8 --env SPMV_TILED_FUSED_CARRY=0,1 --rounds 3;;
     abp11) for i in 1 2; do
              run abp11_base_$i 300 python tools/ab_env.py --format csr --rounds 3 &&
              SPMV_HIP_LIB=$PWD/tools/ab/libspmv_hip_p11.so run abp11_probe_$i 300 python tools/ab_env.py --format csr --rounds 3

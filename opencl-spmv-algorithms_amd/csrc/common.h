@@ -56,7 +56,9 @@ int launch_coo_staged_acc(const spmv_dims &d, const int32_t *row, const int32_t 
 int launch_csr_tiled(const spmv_dims &d, const int64_t *row_ptr, const int32_t *col,
                      const double *val, const double *x, double *y, int32_t *own_lo,
                      int32_t *carry_row, double *carry_val);
-int64_t csr_tiled_tile();
+// entries per tile of the tiled CSR for this matrix, and the smallest it picks
+int64_t csr_tiled_tile(int64_t n_rows, int64_t nnz);
+int64_t csr_tiled_tile_min();
 template <typename V>  // double or float values (instantiated in staged.hip)
 int launch_csr_tiled_hot(const spmv_dims &d, const int64_t *row_ptr, const int32_t *col,
                          const V *val, const double *x, double *y, int64_t H, const int32_t *hot,
@@ -163,8 +165,6 @@ __device__ __forceinline__ void store_y(double *p, double v)
 // it, otherwise `dflt` (each kernel's measured best).  Read on every call
 // so a sweep can flip it inside one process.
 bool stream_nt(bool dflt);
-// SPMV_XHOT_COLD_NT=1: hot-table kernels gather the cold columns non-temporally
-bool xhot_cold_nt();
 // SPMV_TILED_FUSED_CARRY=1: spanning rows finished inside the tiled kernel
 // (tiled CSR with a plan; default: the carry pass)
 bool tiled_fused_carry();
@@ -207,25 +207,12 @@ __device__ __forceinline__ void copy_window(double *s_x, const double *__restric
 
 // Hot-column CSR (spmv_csr_run_tiled_hot): ids >= M name the compact table
 // xh of the most frequent columns, gathered from x at the start of the run.
-// CNT = true gathers the cold columns non-temporally, so their lines (each
-// used about once per launch) do not evict the hot table from L2.
-template <bool CNT>
-struct XHotT {
+struct XHot {
     const double *__restrict__ x;
     const double *__restrict__ xh;
     int32_t M;
-    __device__ __forceinline__ double operator()(int32_t c) const
-    {
-        if (c >= M)
-            return xh[c - M];
-        if constexpr (CNT)
-            return __builtin_nontemporal_load(x + c);
-        else
-            return x[c];
-    }
+    __device__ __forceinline__ double operator()(int32_t c) const { return c >= M ? xh[c - M] : x[c]; }
 };
-struct XHot : XHotT<false> {};
-struct XHotNT : XHotT<true> {};
 
 // [min, max] of col[e0..e1) over one 256-thread workgroup ({0, -1} when
 // empty); the result is valid in thread 0.  Build-time pass of the

@@ -2107,7 +2107,8 @@ extern "C" int spmv_csr16_run_xwin(spmv_dims d, const int64_t *row_ptr, const in
 extern "C" size_t spmv_csr_tiled_ws_bytes(int64_t n_rows, int64_t nnz)
 {
     (void)n_rows;
-    const int64_t tiles = nnz > 0 ? (nnz + csr_tiled_tile() - 1) / csr_tiled_tile() : 0;
+    // sized for the smallest tile the run may pick
+    const int64_t tiles = nnz > 0 ? (nnz + csr_tiled_tile_min() - 1) / csr_tiled_tile_min() : 0;
     // carry_val[tiles] f64, own_lo[tiles+1] i32, carry_row[tiles] i32
     return (size_t)(8 * tiles + 4 * (tiles + 1) + 4 * tiles + 16);
 }
@@ -2127,7 +2128,7 @@ extern "C" int spmv_csr_run_tiled(spmv_dims d, const int64_t *row_ptr, const int
     }
     if (!ws || ws_bytes < spmv_csr_tiled_ws_bytes(d.n_rows, d.nnz))
         return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_run_tiled: workspace too small");
-    const int64_t tiles = (d.nnz + csr_tiled_tile() - 1) / csr_tiled_tile();
+    const int64_t tiles = (d.nnz + csr_tiled_tile(d.n_rows, d.nnz) - 1) / csr_tiled_tile(d.n_rows, d.nnz);
     if (tiles > INT32_MAX)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_run_tiled: grid too large");
     double *carry_val = (double *)ws;
@@ -2162,7 +2163,7 @@ extern "C" int spmv_csr_run_tiled_hot(spmv_dims d, const int64_t *row_ptr, const
     if ((H > 0 && !hot) || !ws || ws_bytes < spmv_csr_hot_ws_bytes(d.n_rows, d.nnz, H))
         return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_run_tiled_hot: hot list or workspace missing");
     SPMV_GUARD(d);
-    const int64_t tiles = (d.nnz + csr_tiled_tile() - 1) / csr_tiled_tile();
+    const int64_t tiles = (d.nnz + csr_tiled_tile(d.n_rows, d.nnz) - 1) / csr_tiled_tile(d.n_rows, d.nnz);
     if (tiles > INT32_MAX)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_run_tiled_hot: grid too large");
     double *xh = (double *)ws;
@@ -2245,7 +2246,7 @@ extern "C" int spmv_csr_f32v_run_tiled_hot(spmv_dims d, const int64_t *row_ptr, 
     }
     if ((H > 0 && !hot) || !ws || ws_bytes < spmv_csr_hot_ws_bytes(d.n_rows, d.nnz, H))
         return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_f32v_run_tiled_hot: hot list or workspace missing");
-    const int64_t tiles = (d.nnz + csr_tiled_tile() - 1) / csr_tiled_tile();
+    const int64_t tiles = (d.nnz + csr_tiled_tile(d.n_rows, d.nnz) - 1) / csr_tiled_tile(d.n_rows, d.nnz);
     if (tiles > INT32_MAX)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_f32v_run_tiled_hot: grid too large");
     double *xh = (double *)ws;

@@ -83,12 +83,6 @@ bool tiled_fused_carry()
     return s && s[0] == '1';
 }
 
-bool xhot_cold_nt()
-{
-    const char *s = getenv("SPMV_XHOT_COLD_NT");
-    return s && s[0] == '1';
-}
-
 // One flush buffer per device, allocated on first use, freed by
 // spmv_release().
 static void *g_flush[64];

@@ -688,30 +688,63 @@ int launch_cmrs_tiled(const spmv_dims &d, int32_t h, int64_t n_strips, const int
     return launch_carry((int64_t)h * tiles, carry_row, carry_val, y, st);
 }
 
-int64_t csr_tiled_tile() { return 2 * kBlock * 3; }
-
-template <typename XS, typename V>
-static void launch_tiled_xs(const spmv_dims &d, int64_t tiles, const int64_t *row_ptr, const int32_t *col,
-                            const V *val, XS xs, double *y, const int32_t *own_lo, int32_t *carry_row,
-                            double *carry_val, uint32_t *cnt = nullptr, double *part_own = nullptr)
+// Tile = 2·kBlock·R entries.  R = 1 (512-entry tiles) unless the mean row
+// is long (>= 48 entries, the L = 8 kernels): on the R-MAT 1e7/1e8 the whole
+// matrix ran 0.826 / 0.831 / 0.861 / 0.887 ms with R = 1 / 2 / 3 / 4, the
+// 8 row shards of mean 4-34 fastest with R = 1 (0.118-0.150 ms against
+// 0.147-0.173 with R = 3) and the hub shard (mean 129, rows over many
+// tiles, more carries) with R = 3 (0.155 vs 0.167): shorter tiles finish
+// the grid with a shorter tail (profiles/round2/ab_tiled_r.log).
+// SPMV_TILED_R in [1, 4] forces R; it is read ONCE per process, since
+// plans and runs must agree on it.  Workspaces and plans are sized for the
+// smallest tile, so any R fits them.
+static int tiled_r_env()
 {
-    constexpr int R = 3;
+    static const int r = [] {
+        const char *s = getenv("SPMV_TILED_R");
+        const int v = s ? atoi(s) : 0;
+        return v >= 1 && v <= 4 ? v : 0;
+    }();
+    return r;
+}
+
+static int tiled_r(int64_t n_rows, int64_t nnz)
+{
+    if (tiled_r_env())
+        return tiled_r_env();
+    return n_rows > 0 && (double)nnz >= 48.0 * (double)n_rows ? 3 : 1;
+}
+
+int64_t csr_tiled_tile(int64_t n_rows, int64_t nnz) { return 2 * kBlock * tiled_r(n_rows, nnz); }
+int64_t csr_tiled_tile_min() { return 2 * kBlock; }
+
+template <int R, typename XS, typename V>
+static void launch_tiled_r(const spmv_dims &d, int64_t tiles, const int64_t *row_ptr, const int32_t *col,
+                           const V *val, XS xs, double *y, const int32_t *own_lo, int32_t *carry_row,
+                           double *carry_val, uint32_t *cnt, double *part_own)
+{
     const hipStream_t st = (hipStream_t)d.stream;
     const double mean = d.n_rows > 0 ? (double)d.nnz / (double)d.n_rows : 0.0;
-    const bool nt = stream_nt(true);
+    // the carry-pass-free and plain-load variants exist for R = 3 only
+    const bool nt = R != 3 || stream_nt(true);
 #define SPMV_TILED(LL)                                                                                    \
     do {                                                                                                  \
-        if (cnt)                                                                                          \
-            hipLaunchKernelGGL((csr_tiled_kernel<LL, R, true, XS, V, true>), dim3((unsigned)tiles),      \
-                               dim3(kBlock), 0, st, d.n_rows, d.nnz, row_ptr, col, val, xs, y, own_lo,     \
-                               carry_row, carry_val, cnt, part_own);                                      \
-        else if (nt)                                                                                      \
-            hipLaunchKernelGGL((csr_tiled_kernel<LL, R, true, XS, V>), dim3((unsigned)tiles), dim3(kBlock), 0, \
-                               st, d.n_rows, d.nnz, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val); \
-        else                                                                                              \
-            hipLaunchKernelGGL((csr_tiled_kernel<LL, R, false, XS, V>), dim3((unsigned)tiles), dim3(kBlock),  \
-                               0, st, d.n_rows, d.nnz, row_ptr, col, val, xs, y, own_lo, carry_row,        \
-                               carry_val);                                                                \
+        if constexpr (R == 3) {                                                                           \
+            if (cnt) {                                                                                    \
+                hipLaunchKernelGGL((csr_tiled_kernel<LL, R, true, XS, V, true>), dim3((unsigned)tiles),  \
+                                   dim3(kBlock), 0, st, d.n_rows, d.nnz, row_ptr, col, val, xs, y, own_lo, \
+                                   carry_row, carry_val, cnt, part_own);                                  \
+                break;                                                                                    \
+            }                                                                                             \
+            if (!nt) {                                                                                    \
+                hipLaunchKernelGGL((csr_tiled_kernel<LL, R, false, XS, V>), dim3((unsigned)tiles),       \
+                                   dim3(kBlock), 0, st, d.n_rows, d.nnz, row_ptr, col, val, xs, y, own_lo, \
+                                   carry_row, carry_val);                                                 \
+                break;                                                                                    \
+            }                                                                                             \
+        }                                                                                                 \
+        hipLaunchKernelGGL((csr_tiled_kernel<LL, R, true, XS, V>), dim3((unsigned)tiles), dim3(kBlock), 0, \
+                           st, d.n_rows, d.nnz, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val);  \
     } while (0)
     if (mean >= 48.0)
         SPMV_TILED(8);
@@ -724,11 +757,24 @@ static void launch_tiled_xs(const spmv_dims &d, int64_t tiles, const int64_t *ro
 #undef SPMV_TILED
 }
 
+template <typename XS, typename V>
+static void launch_tiled_xs(const spmv_dims &d, int64_t tiles, const int64_t *row_ptr, const int32_t *col,
+                            const V *val, XS xs, double *y, const int32_t *own_lo, int32_t *carry_row,
+                            double *carry_val, uint32_t *cnt = nullptr, double *part_own = nullptr)
+{
+    switch (tiled_r(d.n_rows, d.nnz)) {
+    case 1: launch_tiled_r<1>(d, tiles, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val, nullptr, nullptr); break;
+    case 2: launch_tiled_r<2>(d, tiles, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val, nullptr, nullptr); break;
+    case 4: launch_tiled_r<4>(d, tiles, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val, nullptr, nullptr); break;
+    default: launch_tiled_r<3>(d, tiles, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val, cnt, part_own);
+    }
+}
+
 int launch_csr_tiled(const spmv_dims &d, const int64_t *row_ptr, const int32_t *col,
                      const double *val, const double *x, double *y, int32_t *own_lo,
                      int32_t *carry_row, double *carry_val)
 {
-    const int64_t ch = csr_tiled_tile();
+    const int64_t ch = csr_tiled_tile(d.n_rows, d.nnz);
     const int64_t tiles = (d.nnz + ch - 1) / ch;
     const hipStream_t st = (hipStream_t)d.stream;
     hipLaunchKernelGGL(csr_tile_rows_kernel, dim3((unsigned)((tiles + 1 + kBlock - 1) / kBlock)),
@@ -745,13 +791,14 @@ int launch_csr_tiled_hot(const spmv_dims &d, const int64_t *row_ptr, const int32
                          double *xh, const int32_t *own_lo_plan, int32_t *own_lo, int32_t *carry_row,
                          double *carry_val)
 {
-    const int64_t ch = csr_tiled_tile();
+    const int64_t ch = csr_tiled_tile(d.n_rows, d.nnz);
     const int64_t tiles = (d.nnz + ch - 1) / ch;
     const hipStream_t st = (hipStream_t)d.stream;
     launch_hot_gather(H, hot, x, xh, st);
     // a plan carries the fused carry's arrival counters (kept zero between
     // runs): rows spanning tiles are finished inside the tiled kernel
-    uint32_t *cnt = own_lo_plan && tiled_fused_carry() ? (uint32_t *)(own_lo_plan + tiles + 1) : nullptr;
+    uint32_t *cnt = own_lo_plan && tiled_fused_carry() && tiled_r(d.n_rows, d.nnz) == 3 ? (uint32_t *)(own_lo_plan + tiles + 1)
+                                                                         : nullptr;
     // the owners' partials reuse the workspace's own_lo + carry_row words
     // (2 tiles + 1 int32 after carry_val, 8-byte aligned), idle with a plan
     double *part_own = reinterpret_cast<double *>(own_lo);
@@ -761,10 +808,7 @@ int launch_csr_tiled_hot(const spmv_dims &d, const int64_t *row_ptr, const int32
         SPMV_CHECK_LAUNCH("csr_tile_rows_kernel");
         own_lo_plan = own_lo;
     }
-    if (H > 0 && xhot_cold_nt())
-        launch_tiled_xs(d, tiles, row_ptr, col, val, XHotNT{x, xh, (int32_t)d.n_cols}, y, own_lo_plan,
-                        carry_row, carry_val, cnt, part_own);
-    else if (H > 0)
+    if (H > 0)
         launch_tiled_xs(d, tiles, row_ptr, col, val, XHot{x, xh, (int32_t)d.n_cols}, y, own_lo_plan, carry_row,
                         carry_val, cnt, part_own);
     else
@@ -1074,7 +1118,7 @@ extern "C" int spmv_cmrs_xwin_build(spmv_dims d, int32_t h, int64_t n_strips, co
 extern "C" int64_t spmv_csr_tiled_plan_len(int64_t nnz)
 {
     // own_lo[tiles + 1], then one arrival counter per tile (fused carry)
-    return nnz > 0 ? 2 * ((nnz + csr_tiled_tile() - 1) / csr_tiled_tile()) + 1 : 0;
+    return nnz > 0 ? 2 * ((nnz + csr_tiled_tile_min() - 1) / csr_tiled_tile_min()) + 1 : 0;
 }
 
 extern "C" int spmv_csr_tiled_plan(spmv_dims d, const int64_t *row_ptr, int32_t *own_lo)
@@ -1084,7 +1128,7 @@ extern "C" int spmv_csr_tiled_plan(spmv_dims d, const int64_t *row_ptr, int32_t 
     if (d.nnz == 0 || d.n_rows == 0)
         return SPMV_SUCCESS;
     SPMV_GUARD(d);
-    const int64_t ch = csr_tiled_tile();
+    const int64_t ch = csr_tiled_tile(d.n_rows, d.nnz);
     const int64_t tiles = (d.nnz + ch - 1) / ch;
     if (tiles > INT32_MAX)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_tiled_plan: grid too large");

@@ -119,6 +119,11 @@ for s in "${steps[@]}"; do
            run ab_lds_pad_xs 600 python tools/ab_env.py --format csr --kw '{"xwin_rows": 1}' --env SPMV_CSR_XSTREAM=1 --env SPMV_CSR_LDS_PAD=0,12288 --rounds 5;;
     abfused) run gpu_tests_fused 600 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "fused_carry or csr_hot or empty_row_runs" &&
              run ab_fused_rehearse 900 python tools/shard_rehearse.py --gpus 1,8 --env SPMV_TILED_FUSED_CARRY=0,1 --rounds 3;;
+    abtiler) for r in 3 2 1 4 3; do
+               SPMV_TILED_R=$r run reh_tiled_r$r 600 python tools/shard_rehearse.py --gpus 1,8 --rounds 2 || exit 1
+             done;;
+    tiledw) run gpu_tests_tiled 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "tiled or hot or fused or rmat or csrf32" &&
+            run reh_tiled_w 900 python tools/shard_rehearse.py --gpus 1,8 --row-weights 1,2,3,4 --rounds 2;;
     abp11) for i in 1 2; do
              run abp11_base_$i 300 python tools/ab_env.py --format csr --rounds 3 &&
              SPMV_HIP_LIB=$PWD/tools/ab/libspmv_hip_p11.so run abp11_probe_$i 300 python tools/ab_env.py --format csr --rounds 3

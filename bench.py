@@ -51,10 +51,11 @@ KERNEL_NAMES = {  # dominant kernel per format (as rocprofv3 names it)
     "coo": "coo_tile_kernel",
     "cmrs": "cmrs_kernel",
 }
-# R-MAT shards balance entries + RMAT_ROW_WEIGHT * rows: at 8 shards the
-# slowest one took 0.2134 / 0.2023 / 0.1715 / 0.1767 / 0.1950 ms with
-# weights 0 / 2 / 4 / 6 / 8 (tools/shard_rehearse.py, one MI355X)
-RMAT_ROW_WEIGHT = 4.0
+# R-MAT shards balance entries + RMAT_ROW_WEIGHT * rows: with 512-entry
+# tiles the slowest of 8 shards took 0.1421 / 0.1411 / 0.1464 / 0.1549 ms
+# with weights 1 / 2 / 3 / 4 (profiles/round2/shard_rehearse_tiled_w.log;
+# round 1, 1536-entry tiles: 4 was best)
+RMAT_ROW_WEIGHT = 2.0
 CSR_DEFAULT_VARIANT = 3  # must match csr_default_variant() in csrc/csr.hip
 
 

@@ -86,7 +86,8 @@ int spmv_csr_pick_variant(int64_t n_rows, const int64_t *row_ptr);
  * decreasing count (ties: lower column first) into hot[], and col_out
  * (may alias col) = col with every hot column c renumbered n_cols +
  * rank(c).  H_req > 0 takes min(H_req, non-empty columns); H_req = 0 is
- * the rule: 2^19 columns (4 MiB of x, one XCD's L2) when n_cols > 2^21,
+ * the rule: 2^19 columns (4 MiB of x, one XCD's L2; halved down to 2^16
+ * while above nnz / 32) when n_cols > 2^21,
  * they hold at least half of the entries and at least 8 entries each on
  * average (the table fill re-reads each once), else none (col_out = col).
  * hot[] holds max(H_req, 2^19) entries.  Returns H, -1 on bad input.    */

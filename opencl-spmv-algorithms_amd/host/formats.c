@@ -117,7 +117,15 @@ static int by_count_desc(const void *a, const void *b)
 int64_t spmv_hot_columns(int64_t n_cols, int64_t nnz, const int32_t *col, int64_t H_req, int32_t *hot,
                          int32_t *col_out)
 {
-    const int64_t kAutoH = (int64_t)1 << 19;
+    /* auto table: 2^19 columns (4 MiB, one XCD's L2), halved down to 2^16
+     * while it exceeds nnz / 32: an eighth of the R-MAT 1e7/1e8 (1.25e7
+     * entries, one of 8 row shards) ran 0.1330-0.1345 ms mean per shard with
+     * 2^18 columns against 0.1343-0.1355 with 2^19 and 0.138-0.140 with 2^17
+     * (profiles/round2/shard_rehearse_tiled_h.log): a smaller matrix reuses
+     * each table entry less, so the per-run fill costs more than it saves */
+    int64_t kAutoH = (int64_t)1 << 19;
+    while (kAutoH > ((int64_t)1 << 16) && kAutoH > nnz / 32)
+        kAutoH >>= 1;
     const int64_t cap = H_req > 0 ? H_req : kAutoH;
     if (n_cols <= 0 || nnz < 0 || H_req < 0 || !hot || !col_out || (nnz > 0 && !col) ||
         n_cols + cap > INT32_MAX)

@@ -400,9 +400,10 @@ def test_hot_columns_selection_and_renumbering(H):
 
 @pytest.mark.parametrize("skewed", [True, False])
 def test_hot_columns_rule(skewed):
-    """H = 0 picks 2^19 columns when they hold at least half the entries of
-    a matrix with more than 2^21 columns, 8 or more each on average; a
-    uniform column spread (little reuse) gets none."""
+    """H = 0 picks 2^19 columns, halved while above nnz / 32 (5.6e6
+    entries: 2^17), when they hold at least half the entries of a matrix
+    with more than 2^21 columns, 8 or more each on average; a uniform
+    column spread (little reuse) gets none."""
     rng = np.random.default_rng(9)
     n_cols = 3_000_000
     if skewed:
@@ -412,6 +413,6 @@ def test_hot_columns_rule(skewed):
     col = col.astype(np.int32)
     n, hot, ch = sa.hot_columns(n_cols, col, 0)
     if skewed:
-        assert n == 1 << 19 and np.all(hot[:1000] < 1000)
+        assert n == 1 << 17 and np.all(hot[:1000] < 1000)
     else:
         assert n == 0 and np.array_equal(ch, col)

@@ -124,6 +124,9 @@ for s in "${steps[@]}"; do
              done;;
     tiledw) run gpu_tests_tiled 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "tiled or hot or fused or rmat or csrf32" &&
             run reh_tiled_w 900 python tools/shard_rehearse.py --gpus 1,8 --row-weights 1,2,3,4 --rounds 2;;
+    tiledh) run reh_tiled_h 900 python tools/shard_rehearse.py --gpus 8 --row-weights 1.5,2,2.5 --hot 131072,262144,-1 --rounds 2;;
+    reh3) run reh3_eager 900 python tools/shard_rehearse.py --gpus 1,2,4,8 --rounds 2 &&
+          run reh3_graph 900 python tools/shard_rehearse.py --gpus 1,2,4,8 --rounds 2 --graph --reps 50;;
     abp11) for i in 1 2; do
              run abp11_base_$i 300 python tools/ab_env.py --format csr --rounds 3 &&
              SPMV_HIP_LIB=$PWD/tools/ab/libspmv_hip_p11.so run abp11_probe_$i 300 python tools/ab_env.py --format csr --rounds 3

@@ -36,25 +36,31 @@ import spmv_amd as sa  # noqa: E402
 
 
 def time_shard(torch, dm, x, y, reps, graph=False):
-    """Mean ms per SpMV over back-to-back launches; graph=True captures one
-    SpMV (its 3-4 kernels) into a HIP graph and replays it."""
+    """Mean ms per SpMV over back-to-back launches; graph=True captures the
+    `reps` SpMVs (3-4 kernels each) into one HIP graph and times its replay
+    as one span (as bench.py times its steps)."""
     s = torch.cuda.current_stream()
     for _ in range(3):
         dm.run(x, y, s)
-    step = lambda: dm.run(x, y, s)  # noqa: E731
     if graph:
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            dm.run(x, y)
+            for _ in range(reps):
+                dm.run(x, y)
         torch.cuda.synchronize()
-        step = g.replay
-        for _ in range(3):
-            step()
+        g.replay()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        a.record(s)
+        g.replay()
+        b.record(s)
+        torch.cuda.synchronize()
+        return a.elapsed_time(b) / reps
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
     ev[0].record(s)
     for k in range(reps):
-        step()
+        dm.run(x, y, s)
         ev[k + 1].record(s)
     torch.cuda.synchronize()
     return float(np.mean([ev[k].elapsed_time(ev[k + 1]) for k in range(reps)]))
@@ -65,9 +71,9 @@ def main():
     ap.add_argument("--gpus", default="1,2,4,8")
     ap.add_argument("--format", default="csr")
     ap.add_argument("--reps", type=int, default=20)
-    ap.add_argument("--row-weights", default="4", help="spmv_partition_rows_weighted weights to try")
+    ap.add_argument("--row-weights", default="2", help="spmv_partition_rows_weighted weights to try")
     ap.add_argument("--hot", default="-1", help="CSR hot-column table(s), comma-separated: -1 library rule, 0 off, H")
-    ap.add_argument("--graph", action="store_true", help="replay each SpMV as a captured HIP graph")
+    ap.add_argument("--graph", action="store_true", help="time the reps as one captured HIP graph replay (bench.py's timing)")
     ap.add_argument("--env", action="append", default=[],
                     help="KEY=v1,v2: library knobs timed interleaved on every shard (several: cartesian product)")
     ap.add_argument("--rounds", type=int, default=1, help="interleaved rounds per shard (median of rounds)")

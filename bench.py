@@ -355,40 +355,69 @@ def cpu_baseline(m_single_csr, copies, budget_s):
 
 def rmat_strong(args, torch, dev, rank, world, dist, cdev):
     """North-star sweep (BASELINE.json north_star, configs[3]): CSR on the
-    1e7 x 1e7 / 1e8-entry R-MAT, rows cut into `world` shards (entries +
-    RMAT_ROW_WEIGHT x rows balanced, 1024-aligned), one per rank, x
-    replicated; aggregate GB/s = bytes_alg(whole matrix) / max over ranks
-    of the per-step time (HIP-graph replay between barriers).  Every rank's
-    shard output is checked against the host rule before it counts."""
-    a = argparse.Namespace(**vars(args))
-    a.workload, a.format, a.variant, a.lanes = "rmat", "csr", 0, 0
+    1e7 x 1e7 / 1e8-entry R-MAT, rows cut into `world` shards, one per
+    rank, x replicated; aggregate GB/s = bytes_alg(whole matrix) / max over
+    ranks of the per-step time (HIP-graph replay between barriers).
+
+    The cut is profile-guided: the weighted cut (entries + RMAT_ROW_WEIGHT
+    x rows, 1024-aligned) is timed once (`calibration`), every rank's shard
+    time is all-gathered, and spmv_partition_rows_calibrated re-cuts the
+    rows into equal shares of the measured cost (the R-MAT's hub shard
+    costs more per entry than shards of short rows; no single row weight
+    balances 2, 4 and 8 shards: profiles/round2/shard_rehearse_w_g248.log).
+    Setup only: the timed steps are the same SpMV on the final shards.
+    Every rank's output is checked against the host rule before it counts."""
     t0 = time.perf_counter()
-    w = build_workload(a, torch, dev, rank, world)
-    build_s = time.perf_counter() - t0
+    full = sa.gen_rmat()  # deterministic: every rank builds the same matrix
+    ptr, col, val = sa.csr_from_coo(full)
+    n, z = full.n_rows, full.nnz
+    del full
+    x = torch.from_numpy(sa.ramp_x(n)).to(dev)
+    b_total = sa.bytes_alg(n, n, z)
     steps = max(20, args.steps // 2)
-    wall, kern = time_steps(torch, w["dm"], w["x"], w["y"], steps, 5, dist)
-    bad = w["check"]()
-    if bad:
-        raise SystemExit(f"rank {rank}: R-MAT parity failure ({bad})")
-    t = torch.tensor([wall / steps * 1e3, float(np.mean(kern))], dtype=torch.float64, device=cdev)
-    shard_ms = [float(np.mean(kern))]
-    if dist is not None:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        g = [torch.zeros(1, dtype=torch.float64, device=cdev) for _ in range(world)]
-        dist.all_gather(g, torch.tensor([float(np.mean(kern))], dtype=torch.float64, device=cdev))
-        shard_ms = [float(v.item()) for v in g]
-    step_ms, kern_ms = float(t[0].item()), float(t[1].item())
-    params = {k: v for k, v in w["dm"].params.items() if isinstance(v, (int, float, str))}
+
+    def run(bounds, k):
+        lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+        lptr = ptr[lo:hi + 1] - ptr[lo]
+        loc = sa.Coo(hi - lo, n, np.repeat(np.arange(hi - lo, dtype=np.int32), np.diff(lptr)),
+                     col[ptr[lo]:ptr[hi]], val[ptr[lo]:ptr[hi]])
+        dm = sa.to_device(loc, "csr", dev)
+        y = torch.empty(max(loc.n_rows, 1), dtype=torch.float64, device=dev)
+        wall, kern = time_steps(torch, dm, x, y, k, 5, dist)
+        bad, first = sa.check(loc, sa.ramp_x(n), y[:loc.n_rows].cpu().numpy())
+        if bad:
+            raise SystemExit(f"rank {rank}: R-MAT parity failure (row {first})")
+        params = {kk: v for kk, v in dm.params.items() if isinstance(v, (int, float, str))}
+        t = torch.tensor([wall / k * 1e3, float(np.mean(kern))], dtype=torch.float64, device=cdev)
+        shard_ms = [float(np.mean(kern))]
+        if dist is not None:
+            g = [torch.zeros(1, dtype=torch.float64, device=cdev) for _ in range(world)]
+            dist.all_gather(g, torch.tensor([float(np.mean(kern))], dtype=torch.float64, device=cdev))
+            shard_ms = [float(v.item()) for v in g]
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        del dm, y
+        torch.cuda.empty_cache()
+        return float(t[0].item()), float(t[1].item()), shard_ms, params
+
+    bounds0 = sa.partition_rows(n, ptr, world, align=1024, row_weight=RMAT_ROW_WEIGHT)
+    step0, _, shard0, _ = run(bounds0, 20)
+    bounds = bounds0
+    if world > 1:
+        bounds = sa.partition_rows_calibrated(n, ptr, world, bounds0, shard0, align=1024, row_weight=RMAT_ROW_WEIGHT)
+    step_ms, kern_ms, shard_ms, params = run(bounds, steps)
     out = {"workload": "csr SpMV on R-MAT 1e7/1e8 (configs[3]) row-sharded over all ranks, x replicated",
            "scaling": "strong", "steps": steps,
-           "aggregate_GBs": round(w["bytes_total"] / (step_ms * 1e-3) * 1e-9, 1),
-           "GFLOPs": round(2 * w["nnz_total"] / (step_ms * 1e-3) * 1e-9, 1),
-           "frac_of_one_gpu_peak": round(w["bytes_total"] / (step_ms * 1e-3) * 1e-9 / sa.HBM_PEAK_GBS, 4),
+           "aggregate_GBs": round(b_total / (step_ms * 1e-3) * 1e-9, 1),
+           "GFLOPs": round(2 * z / (step_ms * 1e-3) * 1e-9, 1),
+           "frac_of_one_gpu_peak": round(b_total / (step_ms * 1e-3) * 1e-9 / sa.HBM_PEAK_GBS, 4),
            "ms_per_step": round(step_ms, 5), "max_shard_kernel_ms": round(kern_ms, 5),
-           "shard_ms": [round(v, 5) for v in shard_ms], "bytes_alg_whole": w["bytes_total"],
-           "params_rank0": params, "parity_ok": True, "host_build_s": round(build_s, 1)}
-    del w
-    torch.cuda.empty_cache()
+           "shard_ms": [round(v, 5) for v in shard_ms], "shard_rows": np.diff(bounds).tolist(),
+           "bytes_alg_whole": b_total, "params_rank0": params, "parity_ok": True,
+           "partition": ("profile-guided: weighted cut (row weight %g) timed, then re-cut by measured cost"
+                         % RMAT_ROW_WEIGHT) if world > 1 else "whole matrix",
+           "calibration": {"shard_rows": np.diff(bounds0).tolist(), "shard_ms": [round(v, 5) for v in shard0],
+                           "aggregate_GBs": round(b_total / (step0 * 1e-3) * 1e-9, 1)},
+           "setup_s": round(time.perf_counter() - t0, 1)}
     return out
 
 

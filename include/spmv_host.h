@@ -170,6 +170,15 @@ int spmv_partition_rows(int64_t n_rows, const int64_t *row_ptr, int parts,
  * its reduction; 0 = spmv_partition_rows).                              */
 int spmv_partition_rows_weighted(int64_t n_rows, const int64_t *row_ptr, int parts, int64_t align,
                                  double row_weight, int64_t *bounds);
+/* Profile-guided re-cut: old_bounds (old_parts + 1) with the measured time
+ * of each old shard (old_ms) give every row the cost rate_g * (entries +
+ * row_weight) of the old shard g holding it (rate_g = ms_g / that shard's
+ * entries + row_weight * rows); the new `parts` ranges hold equal shares
+ * of that cost, aligned as spmv_partition_rows.  For shards whose cost per
+ * entry differs (R-MAT hub shards against shards of short rows).         */
+int spmv_partition_rows_calibrated(int64_t n_rows, const int64_t *row_ptr, int parts, int64_t align,
+                                   double row_weight, int old_parts, const int64_t *old_bounds,
+                                   const double *old_ms, int64_t *bounds);
 
 /* ---------------------------------------------------------- CPU loops ---
  * OpenMP restatements of the reference's compute_using_cpu loops, with

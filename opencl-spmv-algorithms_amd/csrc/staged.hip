@@ -689,12 +689,13 @@ int launch_cmrs_tiled(const spmv_dims &d, int32_t h, int64_t n_strips, const int
 }
 
 // Tile = 2·kBlock·R entries.  R = 1 (512-entry tiles) unless the mean row
-// is long (>= 48 entries, the L = 8 kernels): on the R-MAT 1e7/1e8 the whole
-// matrix ran 0.826 / 0.831 / 0.861 / 0.887 ms with R = 1 / 2 / 3 / 4, the
-// 8 row shards of mean 4-34 fastest with R = 1 (0.118-0.150 ms against
-// 0.147-0.173 with R = 3) and the hub shard (mean 129, rows over many
-// tiles, more carries) with R = 3 (0.155 vs 0.167): shorter tiles finish
-// the grid with a shorter tail (profiles/round2/ab_tiled_r.log).
+// is long (>= 96 entries): on the R-MAT 1e7/1e8 the whole matrix ran
+// 0.826 / 0.831 / 0.861 / 0.887 ms with R = 1 / 2 / 3 / 4, the 8 row shards
+// of mean 4-34 fastest with R = 1 (0.118-0.150 ms against 0.147-0.173 with
+// R = 3): shorter tiles finish the grid with a shorter tail
+// (profiles/round2/ab_tiled_r.log).  Hub shards, whose rows run over many
+// tiles (more carries), split: mean 179 (1 of 8) 0.1366 ms with R = 3 vs
+// 0.1475 with R = 1, mean 55 (1 of 4) 0.2855 vs 0.2667 (ab_tiled_r_hub.log).
 // SPMV_TILED_R in [1, 4] forces R; it is read ONCE per process, since
 // plans and runs must agree on it.  Workspaces and plans are sized for the
 // smallest tile, so any R fits them.
@@ -712,7 +713,7 @@ static int tiled_r(int64_t n_rows, int64_t nnz)
 {
     if (tiled_r_env())
         return tiled_r_env();
-    return n_rows > 0 && (double)nnz >= 48.0 * (double)n_rows ? 3 : 1;
+    return n_rows > 0 && (double)nnz >= 96.0 * (double)n_rows ? 3 : 1;
 }
 
 int64_t csr_tiled_tile(int64_t n_rows, int64_t nnz) { return 2 * kBlock * tiled_r(n_rows, nnz); }

@@ -679,6 +679,64 @@ int spmv_partition_rows_weighted(int64_t n_rows, const int64_t *row_ptr, int par
     return SPMV_SUCCESS;
 }
 
+/* Cost prefix of rows [0, r) under measured shard times: inside old shard
+ * g a row costs rate_g * (entries + row_weight), rate_g = ms_g / (the
+ * shard's entries + row_weight * rows). */
+static double calibrated_prefix(int64_t r, const int64_t *row_ptr, int old_parts, const int64_t *ob,
+                                const double *ms, double w)
+{
+    double c = 0.0;
+    for (int g = 0; g < old_parts; ++g) {
+        const int64_t lo = ob[g], hi = ob[g + 1];
+        const double W = (double)(row_ptr[hi] - row_ptr[lo]) + w * (double)(hi - lo);
+        if (r >= hi) {
+            c += ms[g];
+            continue;
+        }
+        if (r > lo && W > 0.0)
+            c += ms[g] * ((double)(row_ptr[r] - row_ptr[lo]) + w * (double)(r - lo)) / W;
+        break;
+    }
+    return c;
+}
+
+int spmv_partition_rows_calibrated(int64_t n_rows, const int64_t *row_ptr, int parts, int64_t align,
+                                   double row_weight, int old_parts, const int64_t *old_bounds,
+                                   const double *old_ms, int64_t *bounds)
+{
+    if (parts < 1 || old_parts < 1 || n_rows < 0 || align < 1 || !(row_weight >= 0.0) || !old_bounds ||
+        !old_ms || old_bounds[0] != 0 || old_bounds[old_parts] != n_rows)
+        return SPMV_OTHER_ERROR;
+    double total = 0.0;
+    for (int g = 0; g < old_parts; ++g) {
+        if (old_bounds[g + 1] < old_bounds[g] || !(old_ms[g] >= 0.0))
+            return SPMV_OTHER_ERROR;
+        total += old_ms[g];
+    }
+    if (!(total > 0.0))
+        return spmv_partition_rows_weighted(n_rows, row_ptr, parts, align, row_weight, bounds);
+    bounds[0] = 0;
+    for (int p = 1; p < parts; ++p) {
+        const double target = total * p / parts;
+        int64_t lo = 0, hi = n_rows;
+        while (lo < hi) {
+            const int64_t mid = lo + (hi - lo) / 2;
+            if (calibrated_prefix(mid, row_ptr, old_parts, old_bounds, old_ms, row_weight) < target)
+                lo = mid + 1;
+            else
+                hi = mid;
+        }
+        int64_t b = (lo + align / 2) / align * align;
+        if (b < bounds[p - 1])
+            b = bounds[p - 1];
+        if (b > n_rows)
+            b = n_rows;
+        bounds[p] = b;
+    }
+    bounds[parts] = n_rows;
+    return SPMV_SUCCESS;
+}
+
 int spmv_partition_rows(int64_t n_rows, const int64_t *row_ptr, int parts,
                         int64_t align, int64_t *bounds)
 {

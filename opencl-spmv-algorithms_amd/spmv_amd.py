@@ -192,6 +192,8 @@ HOST_SYMBOLS = {
     "spmv_sell_split_plan": (_c_i64, [_c_i64, _vp, _c_i32, _c_i32, _vp, _vp]),
     "spmv_partition_rows": (ctypes.c_int, [_c_i64, _vp, ctypes.c_int, _c_i64, _vp]),
     "spmv_partition_rows_weighted": (ctypes.c_int, [_c_i64, _vp, ctypes.c_int, _c_i64, ctypes.c_double, _vp]),
+    "spmv_partition_rows_calibrated": (ctypes.c_int, [_c_i64, _vp, ctypes.c_int, _c_i64, ctypes.c_double, ctypes.c_int,
+                                                      _vp, _vp, _vp]),
     "spmv_csr16_plan": (ctypes.c_int, [_c_i64, _vp, ctypes.POINTER(_c_i64), ctypes.POINTER(_c_i64)]),
     "spmv_hyb_plan": (ctypes.c_int, [_c_i64, _vp, _c_i32, _c_i32, ctypes.POINTER(_c_i32), ctypes.POINTER(_c_i64),
                                      ctypes.POINTER(_c_i64)]),
@@ -486,6 +488,23 @@ def partition_rows(n_rows: int, ptr: np.ndarray, parts: int, align: int = 1024,
     else:
         rc = host_lib().spmv_partition_rows(n_rows, _ptr(ptr), parts, align, _ptr(bounds))
     _check_host(rc, "partition_rows")
+    return bounds
+
+
+def partition_rows_calibrated(n_rows: int, ptr: np.ndarray, parts: int, old_bounds, old_ms, align: int = 1024,
+                              row_weight: float = 0.0) -> np.ndarray:
+    """Re-cut rows into `parts` ranges of equal measured cost: each row
+    costs its old shard's time per (entries + row_weight * rows) unit
+    (spmv_partition_rows_calibrated)."""
+    bounds = np.empty(parts + 1, np.int64)
+    ptr = np.ascontiguousarray(ptr, dtype=np.int64)
+    ob = np.ascontiguousarray(old_bounds, dtype=np.int64)
+    ms = np.ascontiguousarray(old_ms, dtype=np.float64)
+    if ms.size + 1 != ob.size:
+        raise SpmvError(OTHER_ERROR, "partition_rows_calibrated", "one time per old shard")
+    _check_host(host_lib().spmv_partition_rows_calibrated(n_rows, _ptr(ptr), parts, align, float(row_weight),
+                                                          ms.size, _ptr(ob), _ptr(ms), _ptr(bounds)),
+                "partition_rows_calibrated")
     return bounds
 
 

@@ -588,14 +588,14 @@ def test_csr_tiled_fused_carry(torch_dev, monkeypatch, case, fmt, H):
     the carry pass, run after run (the plan's arrival counters return to
     zero), including a hub row over ~700 tiles and rows after empty runs."""
     torch, dev = torch_dev
-    # the fused carry runs with 1536-entry tiles, picked for mean rows >= 48
+    # the fused carry runs with 1536-entry tiles, picked for mean rows >= 96
     if case == "rmat":
         m = sa.gen_rmat(100_000, 10_000_000, scale=17, seed=1)
     elif case == "empty_runs":  # mean 0.2: 512-entry tiles, the carry pass (same bits either way)
         m, _ = _empty_run_matrix()
-    else:  # row 3 holds 1e6 entries, the rest 1-3 each (mean 52)
+    else:  # row 3 holds 1e6 entries, the rest 1-3 each (mean 102)
         rng = np.random.default_rng(5)
-        n = 20_000
+        n = 10_000
         lens = rng.integers(1, 4, n)
         lens[3] = 1_000_000
         r = np.repeat(np.arange(n, dtype=np.int32), lens)

@@ -416,3 +416,61 @@ def test_hot_columns_rule(skewed):
         assert n == 1 << 17 and np.all(hot[:1000] < 1000)
     else:
         assert n == 0 and np.array_equal(ch, col)
+
+
+def _rmat_like_ptr(n=200_000, seed=3):
+    rng = np.random.default_rng(seed)
+    lens = (rng.pareto(1.2, n) * 3).astype(np.int64)
+    return np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+
+
+@pytest.mark.parametrize("w", [0.0, 2.0])
+def test_partition_calibrated_uniform_rate_is_weighted(w):
+    """Times proportional to each old shard's weighted cost (one rate for
+    all) give exactly the weighted partition back."""
+    ptr = _rmat_like_ptr()
+    n = ptr.size - 1
+    old = sa.partition_rows(n, ptr, 8, align=1024, row_weight=w or 1e-300)
+    W = np.diff(ptr[old]) + w * np.diff(old)
+    new = sa.partition_rows_calibrated(n, ptr, 8, old, 1e-6 * W, align=1024, row_weight=w)
+    assert np.array_equal(new, sa.partition_rows(n, ptr, 8, align=1024, row_weight=w or 1e-300))
+
+
+def test_partition_calibrated_balances_measured_cost():
+    """A shard measured 3x slower per unit gives rows away; every new range
+    then holds 1/parts of the calibrated cost (within one aligned block)."""
+    ptr = _rmat_like_ptr()
+    n, w, parts = ptr.size - 1, 2.0, 4
+    old = sa.partition_rows(n, ptr, parts, align=1024, row_weight=w)
+    W = np.diff(ptr[old]) + w * np.diff(old)
+    ms = W * np.array([3.0, 1.0, 1.0, 1.0]) * 1e-6
+    new = sa.partition_rows_calibrated(n, ptr, parts, old, ms, align=1024, row_weight=w)
+    assert new[0] == 0 and new[-1] == n and np.all(np.diff(new) >= 0) and np.all(new[1:-1] % 1024 == 0)
+    assert new[1] < old[1]
+
+    def prefix(r):  # restatement of the cost model
+        c = 0.0
+        for g in range(parts):
+            lo, hi = old[g], old[g + 1]
+            if r >= hi:
+                c += ms[g]
+                continue
+            if r > lo:
+                c += ms[g] * ((ptr[r] - ptr[lo]) + w * (r - lo)) / W[g]
+            break
+        return c
+
+    tot = ms.sum()
+    blk = max(ms[g] / W[g] * (ptr[min(r + 1024, n)] - ptr[r] + w * 1024)
+              for g in range(parts) for r in range(int(old[g]), int(old[g + 1]), 1024))
+    for p in range(1, parts):
+        assert abs(prefix(int(new[p])) - tot * p / parts) <= blk
+
+
+def test_partition_calibrated_bad_input():
+    ptr = _rmat_like_ptr(10_000)
+    n = ptr.size - 1
+    with pytest.raises(sa.SpmvError):
+        sa.partition_rows_calibrated(n, ptr, 4, np.array([0, 5000, n - 1]), [1.0, 1.0])  # does not end at n
+    with pytest.raises(sa.SpmvError):
+        sa.partition_rows_calibrated(n, ptr, 4, np.array([0, 5000, n]), [1.0, -1.0])

@@ -127,6 +127,12 @@ for s in "${steps[@]}"; do
     tiledh) run reh_tiled_h 900 python tools/shard_rehearse.py --gpus 8 --row-weights 1.5,2,2.5 --hot 131072,262144,-1 --rounds 2;;
     reh3) run reh3_eager 900 python tools/shard_rehearse.py --gpus 1,2,4,8 --rounds 2 &&
           run reh3_graph 900 python tools/shard_rehearse.py --gpus 1,2,4,8 --rounds 2 --graph --reps 50;;
+    reh4) SPMV_TILED_R=1 run reh4_r1 900 python tools/shard_rehearse.py --gpus 2,4,8 --graph --reps 50 &&
+          run reh4_rule 900 python tools/shard_rehearse.py --gpus 2,4,8 --graph --reps 50 &&
+          SPMV_TILED_R=3 run reh4_r3 900 python tools/shard_rehearse.py --gpus 2,4,8 --graph --reps 50;;
+    reh5) run reh5_w 1000 python tools/shard_rehearse.py --gpus 1,2,4,8 --row-weights 0.5,1,1.5,2 --graph --reps 50;;
+    reh6) run reh6_cal 1000 python tools/shard_rehearse.py --gpus 2,4,8 --row-weights 1,2 --graph --reps 50 --calibrate 2 &&
+          run rehearse2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --backend gloo --share-gpu --steps 20;;
     abp11) for i in 1 2; do
              run abp11_base_$i 300 python tools/ab_env.py --format csr --rounds 3 &&
              SPMV_HIP_LIB=$PWD/tools/ab/libspmv_hip_p11.so run abp11_probe_$i 300 python tools/ab_env.py --format csr --rounds 3

@@ -77,6 +77,9 @@ def main():
     ap.add_argument("--env", action="append", default=[],
                     help="KEY=v1,v2: library knobs timed interleaved on every shard (several: cartesian product)")
     ap.add_argument("--rounds", type=int, default=1, help="interleaved rounds per shard (median of rounds)")
+    ap.add_argument("--calibrate", type=int, default=0,
+                    help="profile-guided re-cuts after the weighted cut (spmv_partition_rows_calibrated, "
+                         "from the first --env config's shard times), each timed again")
     a = ap.parse_args()
     keys, vals = [], []
     for e in a.env:
@@ -101,38 +104,48 @@ def main():
         if a.format == "sell":
             kw["sigma"] = 1 << 24  # whole-matrix sort on R-MAT (bench.py's R-MAT default)
         bounds = sa.partition_rows(n, ptr, G, align=1024, row_weight=w)
-        times, nnzs, params = [[] for _ in envs], [], None
-        for r in range(G):
-            lo, hi = int(bounds[r]), int(bounds[r + 1])
-            lptr = ptr[lo:hi + 1] - ptr[lo]
-            loc = sa.Coo(hi - lo, n, np.repeat(np.arange(hi - lo, dtype=np.int32), np.diff(lptr)),
-                         col[ptr[lo]:ptr[hi]], val[ptr[lo]:ptr[hi]])
-            dm = sa.to_device(loc, a.format, dev, **kw)
-            params = params or {k: v for k, v in dm.params.items() if isinstance(v, (int, float, str))}
-            y = torch.empty(max(loc.n_rows, 1), dtype=torch.float64, device=dev)
-            per = [[] for _ in envs]
-            for _ in range(a.rounds):
-                for i, env in enumerate(envs):
-                    os.environ.update(env)
-                    per[i].append(time_shard(torch, dm, x, y, a.reps, a.graph))
-                    bad, first = sa.check(loc, xh, y[:loc.n_rows].cpu().numpy())
-                    if bad:
-                        raise SystemExit(f"G={G} shard {r} env {env}: parity failure at row {first}")
-            for i in range(len(envs)):
-                times[i].append(float(np.median(per[i])))
-            nnzs.append(loc.nnz)
-            del dm, y, loc
-            torch.cuda.empty_cache()
-        for i, env in enumerate(envs):
-            tmax = max(times[i])
-            agg = b_total / (tmax * 1e-3) * 1e-9
-            base = base or agg
-            print(json.dumps({"workload": "rmat 1e7/1e8", "format": a.format, "env": env, "params_shard0": params,
-                              "gpus": G, "row_weight": w, "hot": hot, "graph": a.graph,
-                              "shard_rows": np.diff(bounds).tolist(), "shard_nnz": nnzs,
-                              "shard_ms": [round(t, 4) for t in times[i]], "max_ms": round(tmax, 4),
-                              "aggregate_GBs_warm": round(agg, 1), "speedup_vs_first": round(agg / base, 2)}),
-                  flush=True)
+        for cpass in range(a.calibrate + 1):
+            if cpass:
+                bounds = sa.partition_rows_calibrated(n, ptr, G, bounds, times[0], align=1024, row_weight=w)
+            times, base = run_split(a, torch, sa, dev, ptr, col, val, n, x, xh, b_total, envs, kw, G, w, hot,
+                                    bounds, cpass, base)
+
+
+def run_split(a, torch, sa, dev, ptr, col, val, n, x, xh, b_total, envs, kw, G, w, hot, bounds, cpass, base):
+    times, nnzs, params = [[] for _ in envs], [], None
+    for r in range(G):
+        lo, hi = int(bounds[r]), int(bounds[r + 1])
+        lptr = ptr[lo:hi + 1] - ptr[lo]
+        loc = sa.Coo(hi - lo, n, np.repeat(np.arange(hi - lo, dtype=np.int32), np.diff(lptr)),
+                     col[ptr[lo]:ptr[hi]], val[ptr[lo]:ptr[hi]])
+        dm = sa.to_device(loc, a.format, dev, **kw)
+        params = params or {k: v for k, v in dm.params.items() if isinstance(v, (int, float, str))}
+        y = torch.empty(max(loc.n_rows, 1), dtype=torch.float64, device=dev)
+        per = [[] for _ in envs]
+        for _ in range(a.rounds):
+            for i, env in enumerate(envs):
+                os.environ.update(env)
+                per[i].append(time_shard(torch, dm, x, y, a.reps, a.graph))
+                bad, first = sa.check(loc, xh, y[:loc.n_rows].cpu().numpy())
+                if bad:
+                    raise SystemExit(f"G={G} shard {r} env {env}: parity failure at row {first}")
+        for i in range(len(envs)):
+            times[i].append(float(np.median(per[i])))
+        nnzs.append(loc.nnz)
+        del dm, y, loc
+        torch.cuda.empty_cache()
+    for i, env in enumerate(envs):
+        tmax = max(times[i])
+        agg = b_total / (tmax * 1e-3) * 1e-9
+        base = base or agg
+        print(json.dumps({"workload": "rmat 1e7/1e8", "format": a.format, "env": env, "params_shard0": params,
+                          "gpus": G, "row_weight": w, "hot": hot, "graph": a.graph, "calibration_pass": cpass,
+                          "shard_rows": np.diff(bounds).tolist(), "shard_nnz": nnzs,
+                          "shard_ms": [round(t, 4) for t in times[i]], "max_ms": round(tmax, 4),
+                          "aggregate_GBs_warm": round(agg, 1), "speedup_vs_first": round(agg / base, 2)}),
+              flush=True)
+    return times, base
+
 
 if __name__ == "__main__":
     main()

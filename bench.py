@@ -360,11 +360,13 @@ def rmat_strong(args, torch, dev, rank, world, dist, cdev):
     ranks of the per-step time (HIP-graph replay between barriers).
 
     The cut is profile-guided: the weighted cut (entries + RMAT_ROW_WEIGHT
-    x rows, 1024-aligned) is timed once (`calibration`), every rank's shard
-    time is all-gathered, and spmv_partition_rows_calibrated re-cuts the
-    rows into equal shares of the measured cost (the R-MAT's hub shard
-    costs more per entry than shards of short rows; no single row weight
-    balances 2, 4 and 8 shards: profiles/round2/shard_rehearse_w_g248.log).
+    x rows, 1024-aligned) is timed (20 steps), every rank's shard time is
+    all-gathered, and spmv_partition_rows_calibrated re-cuts the rows into
+    equal shares of the measured cost, twice (`calibration`); the measured
+    cut with the lowest max shard time is kept (the same on every rank).
+    The R-MAT's hub shard costs more per entry than shards of short rows,
+    and no single row weight balances 2, 4 and 8 shards
+    (profiles/round2/shard_rehearse_w_g248.log, shard_rehearse_calibrated.log).
     Setup only: the timed steps are the same SpMV on the final shards.
     Every rank's output is checked against the host rule before it counts."""
     t0 = time.perf_counter()
@@ -401,9 +403,15 @@ def rmat_strong(args, torch, dev, rank, world, dist, cdev):
 
     bounds0 = sa.partition_rows(n, ptr, world, align=1024, row_weight=RMAT_ROW_WEIGHT)
     step0, _, shard0, _ = run(bounds0, 20)
-    bounds = bounds0
-    if world > 1:
-        bounds = sa.partition_rows_calibrated(n, ptr, world, bounds0, shard0, align=1024, row_weight=RMAT_ROW_WEIGHT)
+    bounds, passes = bounds0, []
+    if world > 1:  # two re-cuts, each from the previous cut's measured times;
+        b, t, best = bounds0, shard0, (max(shard0), bounds0)  # the measured cut with the lowest max is kept
+        for _ in range(2):
+            b = sa.partition_rows_calibrated(n, ptr, world, b, t, align=1024, row_weight=RMAT_ROW_WEIGHT)
+            _, _, t, _ = run(b, 20)
+            passes.append({"shard_rows": np.diff(b).tolist(), "shard_ms": [round(v, 5) for v in t]})
+            best = min(best, (max(t), b), key=lambda c: c[0])
+        bounds = best[1]
     step_ms, kern_ms, shard_ms, params = run(bounds, steps)
     out = {"workload": "csr SpMV on R-MAT 1e7/1e8 (configs[3]) row-sharded over all ranks, x replicated",
            "scaling": "strong", "steps": steps,
@@ -413,10 +421,12 @@ def rmat_strong(args, torch, dev, rank, world, dist, cdev):
            "ms_per_step": round(step_ms, 5), "max_shard_kernel_ms": round(kern_ms, 5),
            "shard_ms": [round(v, 5) for v in shard_ms], "shard_rows": np.diff(bounds).tolist(),
            "bytes_alg_whole": b_total, "params_rank0": params, "parity_ok": True,
-           "partition": ("profile-guided: weighted cut (row weight %g) timed, then re-cut by measured cost"
-                         % RMAT_ROW_WEIGHT) if world > 1 else "whole matrix",
-           "calibration": {"shard_rows": np.diff(bounds0).tolist(), "shard_ms": [round(v, 5) for v in shard0],
-                           "aggregate_GBs": round(b_total / (step0 * 1e-3) * 1e-9, 1)},
+           "partition": ("profile-guided: weighted cut (row weight %g) and two re-cuts by measured cost timed, "
+                         "the one with the lowest max shard time kept" % RMAT_ROW_WEIGHT) if world > 1 else "whole matrix",
+           "calibration": {"weighted_cut": {"shard_rows": np.diff(bounds0).tolist(),
+                                            "shard_ms": [round(v, 5) for v in shard0],
+                                            "aggregate_GBs": round(b_total / (step0 * 1e-3) * 1e-9, 1)},
+                           "recuts": passes},
            "setup_s": round(time.perf_counter() - t0, 1)}
     return out
 

@@ -174,26 +174,35 @@ __global__ __launch_bounds__(kBlock) void coo_carry_kernel(
     const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (t >= n_tiles)
         return;
-    const int32_t r = carry_row[t];
-    if (r < 0 || (t > 0 && carry_row[t - 1] == r))
-        return;  // not a carry, or not the head of its run
-    // A hub row runs over ~100 tiles: 8 tiles' loads in flight per step
-    // instead of one dependent load per tile; still added in tile order.
-    double s = 0.0;
-    for (int64_t u = t;; u += 8) {
-        int32_t rr[8];
-        double vv[8];
+    // The head test and the first 8 tiles' loads are issued together (one
+    // round trip for a row over <= 8 tiles, the common case); a hub row over
+    // ~100 tiles then loads 8 tiles per step.  Still added in tile order.
+    const int32_t prev = t > 0 ? carry_row[t - 1] : -1;
+    int32_t rr[8];
+    double vv[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const bool in = u + k < n_tiles;
-            rr[k] = in ? carry_row[u + k] : -2;
-            vv[k] = in ? carry_val[u + k] : 0.0;
-        }
+    for (int k = 0; k < 8; ++k) {
+        const bool in = t + k < n_tiles;
+        rr[k] = in ? carry_row[t + k] : -2;
+        vv[k] = in ? carry_val[t + k] : 0.0;
+    }
+    const int32_t r = rr[0];
+    if (r < 0 || prev == r)
+        return;  // not a carry, or not the head of its run
+    double s = 0.0;
+    for (int64_t u = t;;) {
         int k = 0;
         for (; k < 8 && rr[k] == r; ++k)
             s += vv[k];
         if (k < 8)
             break;
+        u += 8;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const bool in = u + q < n_tiles;
+            rr[q] = in ? carry_row[u + q] : -2;
+            vv[q] = in ? carry_val[u + q] : 0.0;
+        }
     }
     y[r] += s;
 }

@@ -629,20 +629,31 @@ __global__ __launch_bounds__(kBlock) void cmrs_tiled_kernel(
 
 int64_t cmrs_tiled_tile() { return 2 * kBlock * 3; }
 
+// xh[i] = x[hot[i]], 4 entries per thread: the 4 index loads go out as one
+// 16-byte load, then the 4 gathers together (two round trips per thread,
+// a quarter of the workgroups).  vec: hot and xh 16-byte aligned (checked
+// by the launcher; otherwise element loads)
 __global__ __launch_bounds__(kBlock) void hot_gather_kernel(int64_t H, const int32_t *__restrict__ hot,
                                                             const double *__restrict__ x,
-                                                            double *__restrict__ xh)
+                                                            double *__restrict__ xh, int vec)
 {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i < H)
-        xh[i] = x[hot[i]];
+    const int64_t i = 4 * ((int64_t)blockIdx.x * kBlock + threadIdx.x);
+    if (vec && i + 3 < H) {
+        const int4 c = *reinterpret_cast<const int4 *>(hot + i);
+        const double a = x[c.x], b = x[c.y], d = x[c.z], e = x[c.w];
+        *reinterpret_cast<double2 *>(xh + i) = double2{a, b};
+        *reinterpret_cast<double2 *>(xh + i + 2) = double2{d, e};
+    } else {
+        for (int64_t j = i; j < i + 4 && j < H; ++j)
+            xh[j] = x[hot[j]];
+    }
 }
 
 static void launch_hot_gather(int64_t H, const int32_t *hot, const double *x, double *xh, hipStream_t st)
 {
     if (H > 0)
-        hipLaunchKernelGGL(hot_gather_kernel, dim3((unsigned)((H + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, H,
-                           hot, x, xh);
+        hipLaunchKernelGGL(hot_gather_kernel, dim3((unsigned)((H + 4 * kBlock - 1) / (4 * kBlock))), dim3(kBlock), 0,
+                           st, H, hot, x, xh, (int)((((uintptr_t)hot | (uintptr_t)xh) & 15) == 0));
 }
 
 int launch_cmrs_tiled(const spmv_dims &d, int32_t h, int64_t n_strips, const int64_t *strip_ptr,

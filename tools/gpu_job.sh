@@ -133,6 +133,13 @@ for s in "${steps[@]}"; do
     reh5) run reh5_w 1000 python tools/shard_rehearse.py --gpus 1,2,4,8 --row-weights 0.5,1,1.5,2 --graph --reps 50;;
     reh6) run reh6_cal 1000 python tools/shard_rehearse.py --gpus 2,4,8 --row-weights 1,2 --graph --reps 50 --calibrate 2 &&
           run rehearse2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --backend gloo --share-gpu --steps 20;;
+    abgather) run gpu_tests_gather 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "coo or hot or tiled or hyb or sell or rmat" &&
+              for i in 1 2; do
+                SPMV_HIP_LIB=$PWD/tools/ab/libspmv_hip_head.so run abg_head_$i 600 python tools/shard_rehearse.py --gpus 1,8 --graph --reps 50 || exit 1
+                run abg_new_$i 600 python tools/shard_rehearse.py --gpus 1,8 --graph --reps 50 || exit 1
+              done &&
+              SPMV_HIP_LIB=$PWD/tools/ab/libspmv_hip_head.so run abg_coo_head 600 python tools/time_formats.py --formats coo,csr --rounds 2 &&
+              run abg_coo_new 600 python tools/time_formats.py --formats coo,csr --rounds 2;;
     abp11) for i in 1 2; do
              run abp11_base_$i 300 python tools/ab_env.py --format csr --rounds 3 &&
              SPMV_HIP_LIB=$PWD/tools/ab/libspmv_hip_p11.so run abp11_probe_$i 300 python tools/ab_env.py --format csr --rounds 3

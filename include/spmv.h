@@ -267,8 +267,12 @@ int spmv_cmrs_run(spmv_dims d, int32_t h, int64_t n_strips,
                   double *y);
 /* COO and entry-balanced CMRS over a hot-column table (col_hot / hot from
  * spmv_hot_columns on the format's own column array), as
- * spmv_csr_run_tiled_hot: bit-identical to spmv_coo_run /
- * spmv_cmrs_run_tiled on the original columns; H = 0 is those runs.     */
+ * spmv_csr_run_tiled_hot: the CMRS run is bit-identical to
+ * spmv_cmrs_run_tiled on the original columns; the COO run cuts 512-entry
+ * tiles below a mean row of 96 (R-MAT 1e7/1e8: 0.951 vs 1.242 ms), so a
+ * row spanning tiles sums in another order than spmv_coo_run's (within
+ * the 1e-6 parity rule; bit-identical for any two tables).  H = 0 is
+ * spmv_coo_run / spmv_cmrs_run_tiled.                                     */
 size_t spmv_coo_hot_ws_bytes(int64_t nnz, int64_t H);
 int spmv_coo_run_hot(spmv_dims d, const int32_t *row, const int32_t *col_hot, const double *val,
                      const double *x, double *y, int64_t H, const int32_t *hot, void *ws, size_t ws_bytes);

@@ -49,6 +49,8 @@ int launch_coo_staged(const spmv_dims &d, const int32_t *row, const int32_t *col
 // LDS entries of x a staged COO tile / CMRS strip run may stage (16 KiB)
 constexpr int32_t kStagedXwinCap = 2048;
 int64_t coo_staged_tile();
+// tile of the hot-column COO (spmv_coo_run_hot) for this matrix
+int64_t coo_hot_tile(int64_t n_rows, int64_t nnz);
 // accumulate mode: y[r] += entries of the rows present (HYB tail)
 int launch_coo_staged_acc(const spmv_dims &d, const int32_t *row, const int32_t *col,
                           const double *val, const double *x, double *y, int32_t *carry_row,
@@ -75,7 +77,8 @@ int launch_coo_staged_acc_hot(const spmv_dims &d, const int32_t *row, const int3
 int launch_coo_staged_hot(const spmv_dims &d, const int32_t *row, const int32_t *col, const double *val,
                           const double *x, double *y, int32_t *carry_row, double *carry_val, int64_t H,
                           const int32_t *hot, double *xh);
-int64_t cmrs_tiled_tile();
+int64_t cmrs_tiled_tile(int64_t n_rows, int64_t nnz);
+int64_t cmrs_tiled_tile_min();
 // the deterministic carry pass shared by COO and tiled CSR (coo.hip)
 int launch_carry(int64_t tiles, const int32_t *carry_row, const double *carry_val, double *y,
                  hipStream_t stream);

@@ -378,7 +378,8 @@ extern "C" size_t spmv_cmrs_tiled_ws_bytes(int64_t n_strips, int64_t nnz, int32_
     (void)n_strips;
     if (h < 1)
         return 0;
-    const int64_t tiles = nnz > 0 ? (nnz + cmrs_tiled_tile() - 1) / cmrs_tiled_tile() : 0;
+    // sized for the smallest tile a run may use
+    const int64_t tiles = nnz > 0 ? (nnz + cmrs_tiled_tile_min() - 1) / cmrs_tiled_tile_min() : 0;
     // carry_val[h·tiles] f64, own_lo[tiles+1] i32, carry_row[h·tiles] i32
     return (size_t)(8 * h * tiles + 4 * (tiles + 1) + 4 * h * tiles + 16);
 }
@@ -404,7 +405,7 @@ extern "C" int spmv_cmrs_run_tiled(spmv_dims d, int32_t h, int64_t n_strips, con
     }
     if (!ws || ws_bytes < spmv_cmrs_tiled_ws_bytes(n_strips, d.nnz, h))
         return fail_msg(SPMV_OTHER_ERROR, "spmv_cmrs_run_tiled: workspace too small");
-    const int64_t tiles = (d.nnz + cmrs_tiled_tile() - 1) / cmrs_tiled_tile();
+    const int64_t tiles = (d.nnz + cmrs_tiled_tile(d.n_rows, d.nnz) - 1) / cmrs_tiled_tile(d.n_rows, d.nnz);
     if (tiles * h > INT32_MAX)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_cmrs_run_tiled: grid too large");
     double *carry_val = (double *)ws;
@@ -456,7 +457,13 @@ extern "C" int spmv_cmrs_run_xwin(spmv_dims d, int32_t h, int64_t n_strips, cons
 
 extern "C" size_t spmv_coo_hot_ws_bytes(int64_t nnz, int64_t H)
 {
-    return (size_t)(H > 0 ? H : 0) * sizeof(double) + spmv_coo_ws_bytes(nnz);
+    // the hot path may use 512-entry tiles (coo_hot_tile): size the carry
+    // for them, at least as large as spmv_coo_ws_bytes (H = 0 runs spmv_coo_run)
+    const int64_t t = 2 * kBlock;
+    const int64_t tiles = nnz > 0 ? (nnz + t - 1) / t : 0;
+    const size_t carry = (size_t)(tiles * (int64_t)(sizeof(double) + sizeof(int32_t)) + 16);
+    const size_t base = spmv_coo_ws_bytes(nnz);
+    return (size_t)(H > 0 ? H : 0) * sizeof(double) + (carry > base ? carry : base);
 }
 
 // COO whose column ids >= n_cols name the hot-column table (host
@@ -473,7 +480,7 @@ extern "C" int spmv_coo_run_hot(spmv_dims d, const int32_t *row, const int32_t *
     if (!hot || !ws || ws_bytes < spmv_coo_hot_ws_bytes(d.nnz, H))
         return fail_msg(SPMV_OTHER_ERROR, "spmv_coo_run_hot: hot list or workspace missing");
     SPMV_GUARD(d);
-    const int64_t st_tiles = (d.nnz + coo_staged_tile() - 1) / coo_staged_tile();
+    const int64_t st_tiles = (d.nnz + coo_hot_tile(d.n_rows, d.nnz) - 1) / coo_hot_tile(d.n_rows, d.nnz);
     double *xh = (double *)ws;
     double *cv = xh + H;
     int32_t *cr = (int32_t *)(cv + st_tiles);
@@ -503,7 +510,7 @@ extern "C" int spmv_cmrs_run_tiled_hot(spmv_dims d, int32_t h, int64_t n_strips,
     if (!hot || !ws || ws_bytes < spmv_cmrs_hot_ws_bytes(n_strips, d.nnz, h, H))
         return fail_msg(SPMV_OTHER_ERROR, "spmv_cmrs_run_tiled_hot: hot list or workspace missing");
     SPMV_GUARD(d);
-    const int64_t tiles = (d.nnz + cmrs_tiled_tile() - 1) / cmrs_tiled_tile();
+    const int64_t tiles = (d.nnz + cmrs_tiled_tile(d.n_rows, d.nnz) - 1) / cmrs_tiled_tile(d.n_rows, d.nnz);
     if (tiles * h > INT32_MAX)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_cmrs_run_tiled_hot: grid too large");
     double *xh = (double *)ws;

@@ -627,7 +627,24 @@ __global__ __launch_bounds__(kBlock) void cmrs_tiled_kernel(
     }
 }
 
-int64_t cmrs_tiled_tile() { return 2 * kBlock * 3; }
+// CMRS tile = 2·kBlock·R entries, R as the tiled CSR's rule (1 below a mean
+// row of 96, else 3): R-MAT 1e7/1e8 0.877 vs 0.902 ms, 8 row shards max
+// 0.166 vs 0.244 ms (profiles/round2/ab_cmrs_tiled_r.log).
+// SPMV_CMRS_TILED_R = 1 / 3 forces it (read once per process); workspaces
+// are sized for R = 1.
+static int cmrs_tiled_r(int64_t n_rows, int64_t nnz)
+{
+    static const int forced = [] {
+        const char *s = getenv("SPMV_CMRS_TILED_R");
+        return s && (s[0] == '1' || s[0] == '3') ? s[0] - '0' : 0;
+    }();
+    if (forced)
+        return forced;
+    return n_rows > 0 && (double)nnz >= 96.0 * (double)n_rows ? 3 : 1;
+}
+
+int64_t cmrs_tiled_tile(int64_t n_rows, int64_t nnz) { return 2 * kBlock * cmrs_tiled_r(n_rows, nnz); }
+int64_t cmrs_tiled_tile_min() { return 2 * kBlock; }
 
 // xh[i] = x[hot[i]], 4 entries per thread: the 4 index loads go out as one
 // 16-byte load, then the 4 gathers together (two round trips per thread,
@@ -661,8 +678,7 @@ int launch_cmrs_tiled(const spmv_dims &d, int32_t h, int64_t n_strips, const int
                       double *y, int32_t *own_lo, int32_t *carry_row, double *carry_val, int64_t H,
                       const int32_t *hot, double *xh)
 {
-    constexpr int R = 3;
-    const int64_t ch = cmrs_tiled_tile();
+    const int64_t ch = cmrs_tiled_tile(d.n_rows, d.nnz);
     const int64_t tiles = (d.nnz + ch - 1) / ch;
     const hipStream_t st = (hipStream_t)d.stream;
     launch_hot_gather(H, hot, x, xh, st);
@@ -674,7 +690,7 @@ int launch_cmrs_tiled(const spmv_dims &d, int32_t h, int64_t n_strips, const int
     int L = spmv_csr_auto_lanes(d.n_rows, d.nnz);
     while (L > 1 && L * h > kBlock)
         L >>= 1;
-#define SPMV_CMRS_TILED(LL)                                                                          \
+#define SPMV_CMRS_TILED_R(LL, R)                                                                     \
     do {                                                                                             \
         if (H > 0)                                                                                   \
             hipLaunchKernelGGL((cmrs_tiled_kernel<LL, R, XHot>), dim3((unsigned)tiles), dim3(kBlock), 0, \
@@ -684,6 +700,13 @@ int launch_cmrs_tiled(const spmv_dims &d, int32_t h, int64_t n_strips, const int
             hipLaunchKernelGGL((cmrs_tiled_kernel<LL, R, XGlobal>), dim3((unsigned)tiles), dim3(kBlock), \
                                0, st, d.n_rows, h, n_strips, d.nnz, tiles, strip_ptr, rin, col, val,    \
                                XGlobal{x}, y, own_lo, carry_row, carry_val);                            \
+    } while (0)
+#define SPMV_CMRS_TILED(LL)                 \
+    do {                                    \
+        if (ch == 2 * kBlock)               \
+            SPMV_CMRS_TILED_R(LL, 1);       \
+        else                                \
+            SPMV_CMRS_TILED_R(LL, 3);       \
     } while (0)
     switch (L) {
     case 1: SPMV_CMRS_TILED(1); break;
@@ -695,6 +718,7 @@ int launch_cmrs_tiled(const spmv_dims &d, int32_t h, int64_t n_strips, const int
     default: SPMV_CMRS_TILED(64); break;
     }
 #undef SPMV_CMRS_TILED
+#undef SPMV_CMRS_TILED_R
     SPMV_CHECK_LAUNCH("cmrs_tiled_kernel");
     return launch_carry((int64_t)h * tiles, carry_row, carry_val, y, st);
 }
@@ -908,6 +932,20 @@ int launch_cmrs_staged(const spmv_dims &d, int32_t h, int64_t n_strips,
 
 int64_t coo_staged_tile() { return 2 * kBlock * kCooR; }
 
+// COO over the hot-column table (power-law matrices): 512-entry tiles (R =
+// 1) below a mean row of 96, as the tiled CSR and CMRS; SPMV_COO_HOT_R=0
+// keeps the kCooR tile (read once per process).
+static int coo_hot_r(int64_t n_rows, int64_t nnz)
+{
+    static const bool keep = [] {
+        const char *s = getenv("SPMV_COO_HOT_R");
+        return s && s[0] == '0';
+    }();
+    return !keep && n_rows > 0 && (double)nnz < 96.0 * (double)n_rows ? 1 : kCooR;
+}
+
+int64_t coo_hot_tile(int64_t n_rows, int64_t nnz) { return 2 * kBlock * coo_hot_r(n_rows, nnz); }
+
 int launch_coo_staged_acc(const spmv_dims &d, const int32_t *row, const int32_t *col,
                           const double *val, const double *x, double *y, int32_t *carry_row,
                           double *carry_val)
@@ -990,18 +1028,25 @@ int launch_coo_staged_hot(const spmv_dims &d, const int32_t *row, const int32_t 
                           const double *x, double *y, int32_t *carry_row, double *carry_val, int64_t H,
                           const int32_t *hot, double *xh)
 {
-    constexpr int R = kCooR;
-    const int64_t tiles = (d.nnz + coo_staged_tile() - 1) / coo_staged_tile();
+    const int R = coo_hot_r(d.n_rows, d.nnz);
+    const int64_t tiles = (d.nnz + coo_hot_tile(d.n_rows, d.nnz) - 1) / coo_hot_tile(d.n_rows, d.nnz);
     if (tiles > INT32_MAX)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_coo_run_hot: grid too large");
     const hipStream_t st = (hipStream_t)d.stream;
     launch_hot_gather(H, hot, x, xh, st);
     const XHot xs{x, xh, (int32_t)d.n_cols};
     const double mean = d.n_rows > 0 ? (double)d.nnz / (double)d.n_rows : 0.0;
-#define SPMV_COO_HOT(LL)                                                                                 \
-    hipLaunchKernelGGL((coo_staged_kernel<LL, R, false, false, true, XHot>), dim3((unsigned)tiles),       \
+#define SPMV_COO_HOT_R(LL, RR)                                                                           \
+    hipLaunchKernelGGL((coo_staged_kernel<LL, RR, false, false, true, XHot>), dim3((unsigned)tiles),      \
                        dim3(kBlock), 0, st, d.n_rows, d.nnz, row, col, val, x, y, carry_row, carry_val,    \
                        (const int2 *)nullptr, 0, xs)
+#define SPMV_COO_HOT(LL)                \
+    do {                                \
+        if (R == 1)                     \
+            SPMV_COO_HOT_R(LL, 1);      \
+        else                            \
+            SPMV_COO_HOT_R(LL, kCooR);  \
+    } while (0)
     if (mean >= 48.0)
         SPMV_COO_HOT(8);
     else if (mean >= 12.0)
@@ -1009,6 +1054,7 @@ int launch_coo_staged_hot(const spmv_dims &d, const int32_t *row, const int32_t 
     else
         SPMV_COO_HOT(2);
 #undef SPMV_COO_HOT
+#undef SPMV_COO_HOT_R
     SPMV_CHECK_LAUNCH("coo_staged_kernel (hot columns)");
     return SPMV_SUCCESS;
 }

@@ -621,13 +621,17 @@ def test_csr_tiled_fused_carry(torch_dev, monkeypatch, case, fmt, H):
                                     ("sell", {"split": 0, "xwin": False}), ("hyb", {}), ("hyb", {"ki": 1})])
 @pytest.mark.parametrize("H", [1, 4096])
 def test_coo_cmrs_hot_bit_identical(torch_dev, fmt, kw, H):
-    """COO / tiled CMRS over the hot-column table: the same products in the
-    same order as over the original columns."""
+    """COO / tiled CMRS / SELL / HYB over the hot-column table: the same
+    products in the same order as over the original columns.  The hot COO
+    cuts 512-entry tiles below a mean row of 96 (spmv_coo_run cuts
+    1536), so rows spanning tiles sum in another order: it is compared
+    bitwise with a one-column table (same tiles) and against the oracle."""
     torch, dev = torch_dev
     m = sa.gen_rmat(1_000_000, 10_000_000, scale=20, seed=1)
     a = sa.to_device(m, fmt, dev, hot=H, **kw)
-    b = sa.to_device(m, fmt, dev, hot=0, **kw)
-    assert a.params["H"] == H and b.params["H"] == 0
+    H_ref = (2 if H == 1 else 1) if fmt == "coo" else 0
+    b = sa.to_device(m, fmt, dev, hot=H_ref, **kw)
+    assert a.params["H"] == H and b.params["H"] == H_ref
     x = torch.from_numpy(np.random.default_rng(7).uniform(-1, 1, m.n_cols)).to(dev)
     ya = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
     yb = torch.full_like(ya, float("nan"))
@@ -636,6 +640,12 @@ def test_coo_cmrs_hot_bit_identical(torch_dev, fmt, kw, H):
     torch.cuda.synchronize()
     assert torch.equal(ya.view(torch.int64), yb.view(torch.int64))
     assert_parity(m, ya.cpu().numpy(), x.cpu().numpy())
+    if fmt == "coo":  # and the plain COO (1536-entry tiles) within the parity rule
+        c = sa.to_device(m, fmt, dev, hot=0, **kw)
+        yc = torch.full_like(ya, float("nan"))
+        c.run(x, yc)
+        torch.cuda.synchronize()
+        assert_parity(m, yc.cpu().numpy(), x.cpu().numpy())
 
 
 def test_csr16_refuses_escape_heavy_matrix(torch_dev):

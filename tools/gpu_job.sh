@@ -140,6 +140,14 @@ for s in "${steps[@]}"; do
               done &&
               SPMV_HIP_LIB=$PWD/tools/ab/libspmv_hip_head.so run abg_coo_head 600 python tools/time_formats.py --formats coo,csr --rounds 2 &&
               run abg_coo_new 600 python tools/time_formats.py --formats coo,csr --rounds 2;;
+    rmatfmt) run bench_rmat 600 python bench.py --workload rmat --steps 20 --rmat-strong no &&
+             run gpu_tests_cmrs1 600 env SPMV_CMRS_TILED_R=1 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "cmrs" &&
+             SPMV_CMRS_TILED_R=1 run reh_cmrs_r1 600 python tools/shard_rehearse.py --format cmrs --gpus 1,8 --graph --reps 30 &&
+             run reh_cmrs_r3 600 python tools/shard_rehearse.py --format cmrs --gpus 1,8 --graph --reps 30;;
+    rmatfmt2) run gpu_tests_fmt2 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "coo or cmrs or hot or rmat or hyb or tiled" &&
+              run bench_rmat2 600 python bench.py --workload rmat --steps 20 --rmat-strong no &&
+              SPMV_COO_HOT_R=0 run reh_coo_r3 600 python tools/shard_rehearse.py --format coo --gpus 1,8 --graph --reps 30 &&
+              run reh_coo_r1 600 python tools/shard_rehearse.py --format coo --gpus 1,8 --graph --reps 30;;
     abp11) for i in 1 2; do
              run abp11_base_$i 300 python tools/ab_env.py --format csr --rounds 3 &&
              SPMV_HIP_LIB=$PWD/tools/ab/libspmv_hip_p11.so run abp11_probe_$i 300 python tools/ab_env.py --format csr --rounds 3

@@ -86,6 +86,9 @@ def parse():
     p.add_argument("--rmat-strong", default="auto", choices=["auto", "yes", "no"],
                    help="also time CSR on the R-MAT 1e7/1e8 row-sharded over all ranks (strong scaling, "
                         "north-star sweep; auto: with the default cant-like workload)")
+    p.add_argument("--banded-strong", default="auto", choices=["auto", "yes", "no"],
+                   help="also time CSR and SELL on the banded 1e8-row / 1.6e9-entry matrix row-sharded over all "
+                        "ranks (configs[4], generated on device; auto: with the default cant-like workload)")
     p.add_argument("--graph", default="yes", choices=["yes", "no"],
                    help="replay the timed launches from one HIP graph (yes) or launch them eagerly")
     return p.parse_args()
@@ -431,6 +434,41 @@ def rmat_strong(args, torch, dev, rank, world, dist, cdev):
     return out
 
 
+def banded_strong(args, torch, dev, rank, world, dist, cdev):
+    """BASELINE.json configs[4]: CSR and SELL-C-sigma on the banded
+    --banded-rows x 16-entry matrix, equal 1024-aligned row ranges, each
+    rank's shard generated in its HBM (spmv_gen_banded_device), x = 1
+    replicated; aggregate GB/s = bytes_alg(whole matrix) / max over ranks of
+    the per-step time (HIP-graph replay between barriers).  Each rank checks
+    its first 4096 rows against the host generator's row sums."""
+    out = {}
+    for fmt in ("csr", "sell"):
+        a = argparse.Namespace(**vars(args))
+        a.workload, a.format, a.variant, a.lanes, a.ki, a.sigma = "banded", fmt, 0, 0, 0, 0
+        t0 = time.perf_counter()
+        w = build_workload(a, torch, dev, rank, world)
+        torch.cuda.synchronize()  # the shard is generated on the device
+        build_s = time.perf_counter() - t0
+        steps = 20
+        wall, kern = time_steps(torch, w["dm"], w["x"], w["y"], steps, 3, dist)
+        bad = w["check"]()
+        if bad:
+            raise SystemExit(f"rank {rank}: banded {fmt} parity failure ({bad})")
+        t = torch.tensor([wall / steps * 1e3, float(np.mean(kern))], dtype=torch.float64, device=cdev)
+        if dist is not None:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        step_ms = float(t[0].item())
+        out[fmt] = {"aggregate_GBs": round(w["bytes_total"] / (step_ms * 1e-3) * 1e-9, 1),
+                    "GFLOPs": round(2 * w["nnz_total"] / (step_ms * 1e-3) * 1e-9, 1),
+                    "ms_per_step": round(step_ms, 5), "max_shard_kernel_ms": round(float(t[1].item()), 5),
+                    "rows_rank0": w["rows"], "bytes_alg_whole": w["bytes_total"], "parity_ok": True,
+                    "build_s": round(build_s, 1)}
+        del w
+        torch.cuda.empty_cache()
+    return {"workload": f"banded {args.banded_rows} rows x 16 entries (configs[4]), equal row shards over all "
+                        "ranks, generated on device, x = 1 replicated", "scaling": "strong", "steps": 20, **out}
+
+
 def main():
     args = parse()
     GRAPH["on"] = args.graph == "yes"
@@ -605,6 +643,9 @@ def main():
             pass
         torch.cuda.empty_cache()
         rstrong = rmat_strong(args, torch, dev, rank, world, dist, cdev)
+    bstrong = None
+    if args.banded_strong == "yes" or (args.banded_strong == "auto" and args.workload == "cantlike"):
+        bstrong = banded_strong(args, torch, dev, rank, world, dist, cdev)
 
     if rank == 0:
         line = {
@@ -631,6 +672,7 @@ def main():
             "cant_single": cant_single,
             "allgather": allgather,
             "rmat_strong": rstrong,
+            "banded_strong": bstrong,
             "device": sa.device_name(gpu),
         }
         print(json.dumps(line), flush=True)

@@ -123,3 +123,79 @@ def test_weighted_partition_balances_cost(w):
     # every cut is within one aligned block (+ its longest row) of its target
     slack = 64 * (w + 1) + np.diff(ptr).max()
     assert np.all(np.abs(cost - total / parts) <= 2 * slack)
+
+
+def _recut_worker(rank, world, port, q):
+    """bench.py's profile-guided cut on CPU: time the weighted cut's shard,
+    all-gather the times, re-cut (every rank alike), compute again, gather y."""
+    sys.path[:0] = [str(PKG), str(REPO)]
+    import time
+
+    import torch
+    import torch.distributed as dist
+
+    import spmv_amd as sa
+    from oracle import oracle
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        m = sa.gen_rmat(200_000, 2_000_000, scale=18, seed=3)
+        ptr, col, val = sa.csr_from_coo(m)
+        x = sa.ramp_x(m.n_cols)
+        L = sa.host_lib()
+
+        def shard_y(b):
+            lo, hi = int(b[rank]), int(b[rank + 1])
+            lptr = np.ascontiguousarray(ptr[lo:hi + 1] - ptr[lo])
+            lcol = np.ascontiguousarray(col[ptr[lo]:ptr[hi]])
+            lval = np.ascontiguousarray(val[ptr[lo]:ptr[hi]])
+            y = np.zeros(max(hi - lo, 1))
+            t0 = time.perf_counter()
+            for _ in range(3):
+                L.spmv_cpu_csr(hi - lo, sa._ptr(lptr), sa._ptr(lcol), sa._ptr(lval), sa._ptr(x), sa._ptr(y), 1)
+            return y[:hi - lo], (time.perf_counter() - t0) / 3 * 1e3
+
+        b0 = sa.partition_rows(m.n_rows, ptr, world, align=1024, row_weight=2.0)
+        _, ms = shard_y(b0)
+        g = [torch.zeros(1, dtype=torch.float64) for _ in range(world)]
+        dist.all_gather(g, torch.tensor([ms], dtype=torch.float64))
+        b1 = sa.partition_rows_calibrated(m.n_rows, ptr, world, b0, [float(v.item()) for v in g],
+                                          align=1024, row_weight=2.0)
+        bs = [torch.zeros(world + 1, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(bs, torch.from_numpy(b1))
+        agree = all(torch.equal(bs[0], v) for v in bs)
+        y, _ = shard_y(b1)
+        sizes = np.diff(b1)
+        pad = max(int(sizes.max()), 1)
+        buf = torch.zeros(pad, dtype=torch.float64)
+        buf[:y.size] = torch.from_numpy(y)
+        out = [torch.zeros_like(buf) for _ in range(world)]
+        dist.all_gather(out, buf)
+        y_full = np.concatenate([out[r][:sizes[r]].numpy() for r in range(world)])
+        y_ref = oracle.file_order_spmv(m.n_rows, m.row, m.col, m.val, x)
+        bad = oracle.parity(y_full, y_ref, m.row, m.col, m.val, x, m.n_rows)
+        q.put((rank, int(bad.size), bool(agree), b1.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_calibrated_recut():
+    """World 2 over gloo: the measured-cost re-cut is the same on both ranks
+    (times all-gathered first), covers every row once, and the re-sharded
+    product still equals the oracle's whole y."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_recut_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(180)
+        assert p.exitcode == 0
+    res = sorted(q.get() for _ in range(2))
+    assert all(bad == 0 and agree for _, bad, agree, _ in res)
+    b = res[0][3]
+    assert b == res[1][3] and b[0] == 0 and b[-1] == 200_000 and b[1] % 1024 == 0

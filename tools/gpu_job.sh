@@ -149,6 +149,7 @@ for s in "${steps[@]}"; do
               SPMV_COO_HOT_R=0 run reh_coo_r3 600 python tools/shard_rehearse.py --format coo --gpus 1,8 --graph --reps 30 &&
               run reh_coo_r1 600 python tools/shard_rehearse.py --format coo --gpus 1,8 --graph --reps 30;;
     proffmt) run prof_fmt 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_fmt -o run -- python3 bench.py --steps 50 --rmat-strong no --cpu-seconds 0;;
+    abbanded3) run ab_banded3 900 python tools/ab_env.py --matrix banded --format csr --kw '{}' --kw '{"xwin_rows": 256}' --kw '{"xwin_rows": 512}' --kw '{"lanes": 4}' --env SPMV_CSR_XWIN_MODE=0,3 --rounds 3 --reps 20;;
     abp11) for i in 1 2; do
              run abp11_base_$i 300 python tools/ab_env.py --format csr --rounds 3 &&
              SPMV_HIP_LIB=$PWD/tools/ab/libspmv_hip_p11.so run abp11_probe_$i 300 python tools/ab_env.py --format csr --rounds 3

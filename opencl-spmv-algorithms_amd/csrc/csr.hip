@@ -718,9 +718,11 @@ __global__ __launch_bounds__(kBlock, MODE >= 3 ? kXwinWaves : 1) void csr_xwin_k
         }
         if constexpr (MODE > 0) {
             // offsets r0 .. r0 + nr of the window's rows (clamped past
-            // n_rows), then the x range: every load issued before the stores
+            // n_rows), then the x range: every load issued before the stores.
+            // The flat modes read all gpw groups' offsets, also in a last
+            // window with fewer groups (clamped: empty rows)
             const int64_t r0 = g_beg * RPB;
-            const int32_t nr = (int32_t)((g_end - g_beg) * RPB) + 1;
+            const int32_t nr = (int32_t)((MODE >= 5 ? gpw : g_end - g_beg) * RPB) + 1;
             constexpr int U = 2;  // offsets per thread per pass (nr <= U·256 in one pass)
             for (int32_t b = 0; b < nr; b += U * kBlock) {
                 int64_t o[U];
@@ -1724,13 +1726,17 @@ static size_t csr_xwin_lds(int mode, int32_t xcap, int64_t gpw, int rpb)
 }
 
 // rows per x window: a multiple of the row group (256/L rows), default
-// kCsrXwinRows, at least one group
+// kCsrXwinRows but at least two groups, so a window whose groups are one
+// chunk each still has a next chunk to pipeline (MODE 3): the banded matrix
+// (L = 2, 128-row groups of 2,048 entries) 0.7534 ms with one-group windows
+// (MODE 0) against 0.7261 ms with two (profiles/round2/ab_banded3.log);
+// explicit rows_per_window: at least one group.  Same chunks, same bits.
 static int64_t csr_xwin_gpw(int L, int32_t rows_per_window)
 {
     const int64_t rpb = kBlock / L;
     const int64_t rows = rows_per_window > 0 ? rows_per_window : kCsrXwinRows;
     const int64_t g = (rows + rpb - 1) / rpb;
-    return g < 1 ? 1 : g;
+    return g < (rows_per_window > 0 ? 1 : 2) ? (rows_per_window > 0 ? 1 : 2) : g;
 }
 
 // SPMV_CSR_LDS_PAD=<bytes>: extra dynamic LDS per workgroup of the x-window

@@ -5,6 +5,8 @@
 #   make            libraries + the five drivers
 #   make lib        libspmv_hip.so (gfx950 kernels, C-ABI) + libspmv_host.so
 #   make oracle     oracle/liboracle.so (test infrastructure only)
+#   make probes     libspmv_probe.so (measurement helpers: stream ceiling,
+#                   flush, trace tags; never linked into the product)
 #   make test-cpu   pytest -m "not gpu"
 #   make test-gpu   pytest -m gpu (needs an MI355X)
 #   DEBUG=yes       adds -g (reference Makefile:20-22)
@@ -33,10 +35,10 @@ LIB_HIP  := $(LIBDIR)/libspmv_hip.so
 LIB_HOST := $(LIBDIR)/libspmv_host.so
 ORACLE   := oracle/liboracle.so
 
-.PHONY: all default lib oracle test-cpu test-gpu clean $(TARGETS)
+.PHONY: all default lib oracle probes test-cpu test-gpu clean $(TARGETS)
 
 default: all
-all: lib $(TARGETS)
+all: lib $(TARGETS) probes
 
 lib: $(LIB_HIP) $(LIB_HOST)
 
@@ -64,6 +66,13 @@ $(BINDIR)/%: $(PKG)/drivers/%.c $(PKG)/drivers/driver.c $(PKG)/drivers/driver.h 
 	  -Wl,-rpath,$(ROCM)/lib -lm
 
 oracle: $(ORACLE)
+
+LIB_PROBE := $(LIBDIR)/libspmv_probe.so
+probes: $(LIB_PROBE)
+
+$(LIB_PROBE): tools/probe.hip
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -shared $< -o $@
 
 $(ORACLE): oracle/oracle.c
 	$(CC) -O2 -std=c11 -Wall -Wextra -fPIC -fopenmp -shared $< -o $@ -lm

@@ -44,19 +44,12 @@ sys.path.insert(0, str(REPO))
 import spmv_amd as sa  # noqa: E402
 
 METRIC = "effective HBM GB/s + GFLOP/s per format on cant.mtx, 1/2/4/8 MI355X"
-KERNEL_NAMES = {  # dominant kernel per format (as rocprofv3 names it)
-    "csr": "csr_vector_kernel",
-    "sell": "sell_kernel",
-    "ell": "ell_kernel",
-    "coo": "coo_tile_kernel",
-    "cmrs": "cmrs_kernel",
-}
 # R-MAT shards balance entries + RMAT_ROW_WEIGHT * rows: with 512-entry
 # tiles the slowest of 8 shards took 0.1421 / 0.1411 / 0.1464 / 0.1549 ms
 # with weights 1 / 2 / 3 / 4 (profiles/round2/shard_rehearse_tiled_w.log;
 # round 1, 1536-entry tiles: 4 was best)
 RMAT_ROW_WEIGHT = 2.0
-CSR_DEFAULT_VARIANT = 3  # must match csr_default_variant() in csrc/csr.hip
+CSR_DEFAULT_VARIANT = 3  # spmv_csr_run_variant's default (csrc/csr.hip)
 
 
 def parse():
@@ -100,21 +93,18 @@ def kernel_name(args, dm=None):
     if args.format == "cmrs" and params.get("variant") == 1:
         return "cmrs_tiled_kernel"
     if dm is not None and "win" in getattr(dm, "arrays", {}):
-        if args.format == "csr" and os.environ.get("SPMV_CSR_XWIN_DIRECT") == "1":
-            return "csr_vector_xwin_kernel"
         if args.format in ("csr16", "csrf32"):  # the CSR x-window kernel with another column / value source
             return "csr_xwin_kernel"
         return f"{args.format}_xwin_kernel"
     if args.format == "csr":
-        v = (getattr(dm, "params", {}) or {}).get("variant", 0) or args.variant
-        v = v or int(os.environ.get("SPMV_CSR_VARIANT", "0") or 0) or CSR_DEFAULT_VARIANT
+        v = params.get("variant", 0) or args.variant or CSR_DEFAULT_VARIANT
         return {2: "csr_staged_kernel", 3: "csr_staged_persistent_kernel",
                 4: "csr_tiled_kernel"}.get(v, "csr_vector_kernel")
     if args.format == "csr16":
         return "csr_staged_persistent_kernel"
-    if args.format in ("coo", "cmrs") and os.environ.get(f"SPMV_{args.format.upper()}_VARIANT", "2") != "1":
+    if args.format in ("coo", "cmrs"):
         return f"{args.format}_staged_kernel"
-    return KERNEL_NAMES[args.format]
+    return {"sell": "sell_kernel", "ell": "ell_kernel"}.get(args.format, args.format)
 
 
 def fmt_kwargs(args, fmt):

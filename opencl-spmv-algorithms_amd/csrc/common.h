@@ -29,6 +29,8 @@ class DeviceGuard {
     int rc_ = SPMV_SUCCESS;
 };
 
+// The library's only environment switches; each changes placement or cache
+// policy, never a result bit (tests/test_gpu_parity.py checks that):
 // XCD-contiguous blockIdx remap switch (SPMV_XCD_REMAP=1 enables; read once).
 bool xcd_remap_enabled();
 // XCD-contiguous window placement of the CSR / SELL x-window kernels:
@@ -168,9 +170,6 @@ __device__ __forceinline__ void store_y(double *p, double v)
 // it, otherwise `dflt` (each kernel's measured best).  Read on every call
 // so a sweep can flip it inside one process.
 bool stream_nt(bool dflt);
-// SPMV_TILED_FUSED_CARRY=1: spanning rows finished inside the tiled kernel
-// (tiled CSR with a plan; default: the carry pass)
-bool tiled_fused_carry();
 
 // Where x[c] comes from: global memory (XGlobal) or the workgroup's
 // window x[lo..hi] staged in LDS (XWindow: the x-window kernels).

@@ -77,12 +77,6 @@ bool stream_nt(bool dflt)
     return dflt;
 }
 
-bool tiled_fused_carry()
-{
-    const char *s = getenv("SPMV_TILED_FUSED_CARRY");
-    return s && s[0] == '1';
-}
-
 // One flush buffer per device, allocated on first use, freed by
 // spmv_release().
 static void *g_flush[64];

@@ -26,13 +26,6 @@ namespace spmv {
 // interleaved (profiles/round1/sweeps.md).  SPMV_STREAM_NT overrides.
 constexpr bool kSellStreamNtDefault = true;
 
-// slot groups in flight per lane: SPMV_SLOT_UNROLL = 4 (default) or 8
-static int slot_unroll()
-{
-    const char *s = getenv("SPMV_SLOT_UNROLL");
-    return (s && s[0] == '8') ? 8 : 4;
-}
-
 template <int KI, bool NT>
 struct Step;
 
@@ -88,102 +81,63 @@ __device__ __forceinline__ double slot_dot(const double *__restrict__ vp,
     return a[0];
 }
 
-// One slot group (KI consecutive entries of a lane's row) held in registers.
-template <int KI, bool NT>
-struct SlotRegs;
+// U slot groups [g, g+U) of one lane, loaded branch-free: a group at or
+// past `end` re-loads group g (valid memory, lines the wave reads anyway)
+// and is not added, so all U value and column loads are in flight together.
+template <int KI, bool NT, int U>
+struct SlotBatch;
 
-template <bool NT>
-struct SlotRegs<1, NT> {
-    double v;
-    int32_t c;
-    __device__ __forceinline__ void load(const double *vp, const int32_t *cp)
+template <bool NT, int U>
+struct SlotBatch<1, NT, U> {
+    double v[U];
+    int32_t c[U];
+    __device__ __forceinline__ void load(const double *vp, const int32_t *cp, int64_t g, int64_t end, int64_t step)
     {
-        v = stream_load<NT>(vp);
-        c = stream_load<NT>(cp);
-    }
-    template <typename XS>
-    __device__ __forceinline__ double fma(const XS &xs, double acc) const { return acc + v * xs(c); }
-};
-
-template <bool NT>
-struct SlotRegs<2, NT> {
-    double2 v;
-    int2 c;
-    __device__ __forceinline__ void load(const double *vp, const int32_t *cp)
-    {
-        v = stream_load2<NT>(vp);
-        c = stream_load2<NT>(cp);
-    }
-    template <typename XS>
-    __device__ __forceinline__ double fma(const XS &xs, double acc) const { return acc + v.x * xs(c.x) + v.y * xs(c.y); }
-};
-
-// slot_dot, software-pipelined: the loads of the next U groups are issued
-// before the FMAs of the current U, so a lane always has a batch in flight
-// while it multiplies (the plain loop waits for every batch).  The same
-// adds in the same order as slot_dot: the same bits.
-template <int KI, bool NT, int U, typename XS>
-__device__ __forceinline__ double slot_dot_pipelined(const double *__restrict__ vp,
-                                                     const int32_t *__restrict__ cp,
-                                                     int64_t w, int64_t step, const XS &xs)
-{
-    double a[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u)
-        a[u] = 0.0;
-    const int64_t groups = w / KI;
-    const int64_t full = groups / U * U;
-    SlotRegs<KI, NT> cur[U], nxt[U];
-    if (full > 0) {
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            cur[u].load(vp + u * step, cp + u * step);
-    }
-    for (int64_t g = 0; g < full; g += U) {
-        const bool more = g + U < full;  // uniform over the slice's lanes
-        if (more) {
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                nxt[u].load(vp + (g + U + u) * step, cp + (g + U + u) * step);
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            a[u] = cur[u].fma(xs, a[u]);
-        if (more) {
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                cur[u] = nxt[u];
+        for (int u = 0; u < U; ++u) {
+            const int64_t gg = g + u < end ? g + u : g;
+            v[u] = stream_load<NT>(vp + gg * step);
+            c[u] = stream_load<NT>(cp + gg * step);
         }
     }
-    for (int64_t g = full; g < groups; ++g)
-        a[0] = Step<KI, NT>::fma(vp + g * step, cp + g * step, xs, a[0]);
+    template <typename XS>
+    __device__ __forceinline__ void fma(const XS &xs, int64_t g, int64_t end, double *a) const
+    {
 #pragma unroll
-    for (int h = U / 2; h > 0; h /= 2) {
-#pragma unroll
-        for (int u = 0; u < h; ++u)
-            a[u] += a[u + h];
+        for (int u = 0; u < U; ++u)  // branch-free: a guarded add lets the compiler sink the loads into branches
+            a[u] += (g + u < end ? v[u] : 0.0) * xs(c[u]);
     }
-    return a[0];
-}
+};
 
-template <int KI, bool NT, int U, bool PIPE, typename XS>
-__device__ __forceinline__ double slot_dot_sel(const double *__restrict__ vp, const int32_t *__restrict__ cp,
-                                               int64_t w, int64_t step, const XS &xs)
-{
-    if constexpr (PIPE)
-        return slot_dot_pipelined<KI, NT, U>(vp, cp, w, step, xs);
-    else
-        return slot_dot<KI, NT, U>(vp, cp, w, step, xs);
-}
+template <bool NT, int U>
+struct SlotBatch<2, NT, U> {
+    double2 v[U];
+    int2 c[U];
+    __device__ __forceinline__ void load(const double *vp, const int32_t *cp, int64_t g, int64_t end, int64_t step)
+    {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t gg = g + u < end ? g + u : g;
+            v[u] = stream_load2<NT>(vp + gg * step);
+            c[u] = stream_load2<NT>(cp + gg * step);
+        }
+    }
+    template <typename XS>
+    __device__ __forceinline__ void fma(const XS &xs, int64_t g, int64_t end, double *a) const
+    {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool in = g + u < end;
+            a[u] += (in ? v[u].x : 0.0) * xs(c[u].x) + (in ? v[u].y : 0.0) * xs(c[u].y);
+        }
+    }
+};
 
-// SPMV_SLOT_PIPE=0/1: the SELL / ELL x-window kernels' slot loop plain or
-// software-pipelined (read per call; A/B knob), default kSlotPipe
-constexpr bool kSlotPipe = false;
-static bool slot_pipe()
-{
-    const char *s = getenv("SPMV_SLOT_PIPE");
-    return s && (s[0] == '0' || s[0] == '1') ? s[0] == '1' : kSlotPipe;
-}
+// (A software-pipelined slot loop — the next U groups' loads issued before
+// the current U's FMAs, same bits — measured SELL 0.2682 vs 0.2624 ms and ELL
+// equal: 78 instead of 60 VGPRs halve the 1024-thread workgroups per CU;
+// U = 8 groups in flight: equal. profiles/round2/ab_slot_pipe.log,
+// ab_rows_sell.log.)
 
 // One workgroup covers one sigma window (up to 1024 slots): every y[perm]
 // store of a window then comes from ONE CU, so its L2 merges the window's
@@ -249,7 +203,7 @@ __global__ __launch_bounds__(kBlock) void ell_window_kernel(int64_t n_rows, int3
 }
 
 // ELL with the workgroup's x window staged in LDS (as sell_xwin_kernel).
-template <int KI, bool NT, int U, bool PIPE = false>
+template <int KI, bool NT, int U>
 __global__ __launch_bounds__(kBlock) void ell_xwin_kernel(
     int64_t n_rows, int32_t K, int64_t ld, const int32_t *__restrict__ col,
     const double *__restrict__ val, const double *__restrict__ x,
@@ -270,8 +224,8 @@ __global__ __launch_bounds__(kBlock) void ell_xwin_kernel(
     if (i >= n_rows)
         return;
     const int64_t off = i * KI;
-    store_y(y + i, staged ? slot_dot_sel<KI, NT, U, PIPE>(val + off, col + off, K, ld * KI, XWindow{s_x, wnd.x})
-                          : slot_dot_sel<KI, NT, U, PIPE>(val + off, col + off, K, ld * KI, XGlobal{x}));
+    store_y(y + i, staged ? slot_dot<KI, NT, U>(val + off, col + off, K, ld * KI, XWindow{s_x, wnd.x})
+                          : slot_dot<KI, NT, U>(val + off, col + off, K, ld * KI, XGlobal{x}));
 }
 
 constexpr int32_t kEllXwinCap = 2048;  // 16 KiB per 256-row workgroup
@@ -288,24 +242,18 @@ namespace spmv {
 // 256-slot groups more than merged stores: one cant-like copy has only 61
 // windows of 1024 rows for 256 CUs.
 // y of a σ = 1024 window staged in LDS and stored in row order
-// (sell_xwin_kernel); SPMV_SELL_YSTAGE=0 / 1 overrides, read per call
-constexpr bool kSellYStage = true;  // cant batch 0.2583 -> 0.2490 ms (profiles/round2/ab_sell_ystage.log)
+// (sell_xwin_kernel): cant batch 0.2583 -> 0.2490 ms
+// (profiles/round2/ab_sell_ystage.log)
 static bool sell_ystage(int bt, int32_t sigma)
 {
-    const char *s = getenv("SPMV_SELL_YSTAGE");
-    const bool on = (s && (s[0] == '0' || s[0] == '1')) ? s[0] == '1' : kSellYStage;
-    return on && bt == 1024 && sigma == 1024;
+    return bt == 1024 && sigma == 1024;
 }
 
 static void sell_geometry(int32_t C, int32_t sigma, int64_t n_slices, int *bt, int64_t *blocks)
 {
-    static const int force256 = [] {
-        const char *s = getenv("SPMV_SELL_BT");  // tuning knob: "256" forces 256-slot groups
-        return s && atoi(s) == 256;
-    }();
     const int64_t slots = n_slices * C;
     const int64_t windows = sigma > 1 ? (slots + sigma - 1) / sigma : 0;
-    const bool wide = !force256 && windows >= 512 && sigma >= kBlock && sigma <= 1024 &&
+    const bool wide = windows >= 512 && sigma >= kBlock && sigma <= 1024 &&
                       sigma % kWave == 0;
     *bt = wide ? sigma : kBlock;
     *blocks = (slots + *bt - 1) / *bt;
@@ -357,7 +305,7 @@ __global__ __launch_bounds__(kBlock) void sell_window_kernel(int32_t C, int bt, 
 // profiles/round1/pmc_stalls.json).  Here the window is copied into LDS
 // once with coalesced loads and every gather is a ds_read_b64.  A
 // workgroup whose window exceeds xcap entries gathers from global memory.
-template <int KI, bool NT, int U, bool PIPE = false>
+template <int KI, bool NT, int U>
 __global__ __launch_bounds__(1024) void sell_xwin_kernel(
     int32_t C, int64_t n_slices, const int64_t *__restrict__ slice_ptr,
     const int32_t *__restrict__ perm, const int32_t *__restrict__ col,
@@ -395,8 +343,8 @@ __global__ __launch_bounds__(1024) void sell_xwin_kernel(
         int64_t w = (slice_ptr[s + 1] - base) / C;
         w = w < wcap ? w : wcap;
         const int64_t off = base + r * KI;
-        sum = staged ? slot_dot_sel<KI, NT, U, PIPE>(val + off, col + off, w, (int64_t)C * KI, XWindow{s_x, wnd.x})
-                     : slot_dot_sel<KI, NT, U, PIPE>(val + off, col + off, w, (int64_t)C * KI, XGlobal{x});
+        sum = staged ? slot_dot<KI, NT, U>(val + off, col + off, w, (int64_t)C * KI, XWindow{s_x, wnd.x})
+                     : slot_dot<KI, NT, U>(val + off, col + off, w, (int64_t)C * KI, XGlobal{x});
     }
     if (ystage_rows > 0) {
         if (in_order) {  // whole rows in order already: written through L2 directly
@@ -421,6 +369,117 @@ __global__ __launch_bounds__(1024) void sell_xwin_kernel(
     }
     if (row >= 0)
         y[row] = sum;  // scattered by perm: plain stores (sc1 measured 1.8 % slower, profiles/round2/ab_ystore.log)
+}
+
+// Small matrices (BASELINE.json configs[2]: one cant-like matrix is 976
+// slices of C = 64, i.e. 976 waves for 1,024 SIMDs): with one wave per slice
+// each SIMD holds about one wave, 64 lanes x 4 loads x 12 B = 3 KiB in
+// flight, and every lane walks its ~64-entry row in ~16 dependent round
+// trips — latency-bound, 29-33 % of the HBM peak cold.  Here a workgroup of
+// S waves owns ONE slice and splits its slot columns into S contiguous
+// ranges, one per wave (lane = row of the slice, as before); each lane
+// issues U slot loads at a time, branch-free (past its range it re-reads
+// its range's first slot, the same lines, and adds nothing).  The S partial
+// sums of a row meet in LDS and wave 0 adds them in wave order and stores
+// y[perm].  Deterministic; a row's sum is grouped differently from
+// sell_kernel's, so the bits differ from it (the parity rule holds).
+template <int KI, bool NT, int S, typename XS>
+__global__ __launch_bounds__(kWave * S) void sell_small_kernel(
+    int64_t n_slices, const int64_t *__restrict__ slice_ptr,
+    const int32_t *__restrict__ perm, const int32_t *__restrict__ col,
+    const double *__restrict__ val, const XS xs, double *__restrict__ y, int64_t wcap)
+{
+    constexpr int U = 4;
+    constexpr int64_t step = (int64_t)kWave * KI;  // elements between slot groups
+    const int64_t s = blockIdx.x;  // grid = n_slices
+    (void)n_slices;
+    const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+    const int32_t row = wv == 0 ? perm[s * kWave + lane] : -1;  // in flight with the stream
+    const int64_t base = slice_ptr[s];
+    int64_t w = (slice_ptr[s + 1] - base) / kWave;
+    w = w < wcap ? w : wcap;
+    const int64_t groups = w / KI;
+    const int64_t per = (groups + S - 1) / S;
+    const int64_t g0 = wv * per;
+    const int64_t g1 = g0 + per < groups ? g0 + per : groups;
+    const double *vp = val + base + lane * KI;
+    const int32_t *cp = col + base + lane * KI;
+    double a[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        a[u] = 0.0;
+    for (int64_t g = g0; g < g1; g += U) {
+        SlotBatch<KI, NT, U> b;
+        b.load(vp, cp, g, g1, step);
+        b.fma(xs, g, g1, a);
+    }
+    double sum = (a[0] + a[2]) + (a[1] + a[3]);
+    if constexpr (S > 1) {
+        __shared__ double part[S][kWave];
+        part[wv][lane] = sum;
+        __syncthreads();
+        if (wv == 0) {
+#pragma unroll
+            for (int k = 1; k < S; ++k)
+                sum += part[k][lane];
+        }
+    }
+    if (row >= 0)
+        y[row] = sum;  // scattered by perm: plain stores, as sell_kernel
+}
+
+// Waves per slice of sell_small_kernel: the smallest power of two that puts
+// about four waves on every SIMD, at most 8; 1 = the one-wave-per-slice
+// kernels.  Only C = 64 (a slice is one wave).
+#ifndef SPMV_SELL_SMALL_S  // A/B builds only (tools/ab): force S (1 = one wave per slice)
+#define SPMV_SELL_SMALL_S 0
+#endif
+int sell_small_waves(int32_t C, int64_t n_slices)
+{
+    if (C != kWave || n_slices <= 0)
+        return 1;
+    if (SPMV_SELL_SMALL_S > 0)
+        return SPMV_SELL_SMALL_S;
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+        cus = 256;
+    const int64_t want = 4 * 4 * (int64_t)cus;  // 4 waves on each of a CU's 4 SIMDs
+    int S = 1;
+    while (S < 8 && n_slices * S < want)
+        S *= 2;
+    return S;
+}
+
+template <int KI, bool NT, typename XS>
+static void launch_sell_small(int S, int64_t n_slices, const int64_t *slice_ptr, const int32_t *perm,
+                              const int32_t *col, const double *val, const XS xs, double *y, int64_t wcap,
+                              hipStream_t st)
+{
+#define SPMV_SELL_SMALL(SS)                                                                                \
+    hipLaunchKernelGGL((sell_small_kernel<KI, NT, SS, XS>), dim3((unsigned)n_slices), dim3(kWave * SS), 0, st, \
+                       n_slices, slice_ptr, perm, col, val, xs, y, wcap)
+    switch (S) {
+    case 2: SPMV_SELL_SMALL(2); break;
+    case 4: SPMV_SELL_SMALL(4); break;
+    case 16: SPMV_SELL_SMALL(16); break;
+    default: SPMV_SELL_SMALL(8); break;
+    }
+#undef SPMV_SELL_SMALL
+}
+
+template <typename XS>
+static void launch_sell_small_any(int S, int32_t ki, bool nt, int64_t n_slices, const int64_t *slice_ptr,
+                                  const int32_t *perm, const int32_t *col, const double *val, const XS xs, double *y,
+                                  int64_t wcap, hipStream_t st)
+{
+    if (ki == 2) {
+        if (nt) launch_sell_small<2, true>(S, n_slices, slice_ptr, perm, col, val, xs, y, wcap, st);
+        else launch_sell_small<2, false>(S, n_slices, slice_ptr, perm, col, val, xs, y, wcap, st);
+    } else {
+        if (nt) launch_sell_small<1, true>(S, n_slices, slice_ptr, perm, col, val, xs, y, wcap, st);
+        else launch_sell_small<1, false>(S, n_slices, slice_ptr, perm, col, val, xs, y, wcap, st);
+    }
 }
 
 // Wide slices (SELL split plan, spmv_sell_split_plan): a slice wider than
@@ -518,11 +577,15 @@ extern "C" int spmv_sell_run(spmv_dims d, int32_t C, int32_t sigma, int32_t ki,
         return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_run: grid too large");
     const int remap = xcd_remap_enabled() ? 1 : 0;
     const bool nt = stream_nt(kSellStreamNtDefault);
-    const bool u8 = slot_unroll() == 8;
-    auto kern = ki == 2 ? (nt ? (u8 ? sell_kernel<2, true, 8> : sell_kernel<2, true, 4>)
-                              : (u8 ? sell_kernel<2, false, 8> : sell_kernel<2, false, 4>))
-                        : (nt ? (u8 ? sell_kernel<1, true, 8> : sell_kernel<1, true, 4>)
-                              : (u8 ? sell_kernel<1, false, 8> : sell_kernel<1, false, 4>));
+    const int S = sell_small_waves(C, n_slices);
+    if (S > 1) {
+        launch_sell_small_any(S, ki, nt, n_slices, slice_ptr, perm, col, val, XGlobal{x}, y, INT64_MAX,
+                              (hipStream_t)d.stream);
+        SPMV_CHECK_LAUNCH("sell_small_kernel");
+        return SPMV_SUCCESS;
+    }
+    auto kern = ki == 2 ? (nt ? sell_kernel<2, true, 4> : sell_kernel<2, false, 4>)
+                        : (nt ? sell_kernel<1, true, 4> : sell_kernel<1, false, 4>);
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(bt), 0, (hipStream_t)d.stream, C,
                        n_slices, slice_ptr, perm, col, val, XGlobal{x}, y, remap, (int64_t)INT64_MAX);
     SPMV_CHECK_LAUNCH("sell_kernel");
@@ -604,11 +667,15 @@ extern "C" int spmv_sell_run_xwin(spmv_dims d, int32_t C, int32_t sigma, int32_t
     if (blocks > INT32_MAX)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_run_xwin: grid too large");
     const bool nt = stream_nt(kSellStreamNtDefault);
-    const bool pipe = slot_pipe();
-    auto kern = ki == 2 ? (nt ? (pipe ? sell_xwin_kernel<2, true, 4, true> : sell_xwin_kernel<2, true, 4>)
-                              : sell_xwin_kernel<2, false, 4>)
-                        : (nt ? (pipe ? sell_xwin_kernel<1, true, 4, true> : sell_xwin_kernel<1, true, 4>)
-                              : sell_xwin_kernel<1, false, 4>);
+    const int S = sell_small_waves(C, n_slices);
+    if (S > 1) {  // few slices: the waves-per-slice kernel (global gathers; same bits as spmv_sell_run)
+        launch_sell_small_any(S, ki, nt, n_slices, slice_ptr, perm, col, val, XGlobal{x}, y, INT64_MAX,
+                              (hipStream_t)d.stream);
+        SPMV_CHECK_LAUNCH("sell_small_kernel");
+        return SPMV_SUCCESS;
+    }
+    auto kern = ki == 2 ? (nt ? sell_xwin_kernel<2, true, 4> : sell_xwin_kernel<2, false, 4>)
+                        : (nt ? sell_xwin_kernel<1, true, 4> : sell_xwin_kernel<1, false, 4>);
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(bt), (size_t)xcap * sizeof(double),
                        (hipStream_t)d.stream, C, n_slices, slice_ptr, perm, col, val, x, y,
                        (const int2 *)win, xcap, (int64_t)INT64_MAX, xwin_remap(false) ? 1 : 0,
@@ -631,11 +698,8 @@ extern "C" int spmv_ell_run(spmv_dims d, int32_t K, int64_t ld, int32_t ki,
     const int64_t blocks = (d.n_rows + kBlock - 1) / kBlock;
     const int remap = xcd_remap_enabled() ? 1 : 0;
     const bool nt = stream_nt(kSellStreamNtDefault);
-    const bool u8 = slot_unroll() == 8;
-    auto kern = ki == 2 ? (nt ? (u8 ? ell_kernel<2, true, 8> : ell_kernel<2, true, 4>)
-                              : (u8 ? ell_kernel<2, false, 8> : ell_kernel<2, false, 4>))
-                        : (nt ? (u8 ? ell_kernel<1, true, 8> : ell_kernel<1, true, 4>)
-                              : (u8 ? ell_kernel<1, false, 8> : ell_kernel<1, false, 4>));
+    auto kern = ki == 2 ? (nt ? ell_kernel<2, true, 4> : ell_kernel<2, false, 4>)
+                        : (nt ? ell_kernel<1, true, 4> : ell_kernel<1, false, 4>);
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock), 0, (hipStream_t)d.stream,
                        d.n_rows, K, ld, col, val, XGlobal{x}, y, remap);
     SPMV_CHECK_LAUNCH("ell_kernel");
@@ -699,11 +763,8 @@ extern "C" int spmv_ell_run_xwin(spmv_dims d, int32_t K, int64_t ld, int32_t ki,
     SPMV_GUARD(d);
     const int64_t blocks = (d.n_rows + kBlock - 1) / kBlock;
     const bool nt = stream_nt(kSellStreamNtDefault);
-    const bool pipe = slot_pipe();
-    auto kern = ki == 2 ? (nt ? (pipe ? ell_xwin_kernel<2, true, 4, true> : ell_xwin_kernel<2, true, 4>)
-                              : ell_xwin_kernel<2, false, 4>)
-                        : (nt ? (pipe ? ell_xwin_kernel<1, true, 4, true> : ell_xwin_kernel<1, true, 4>)
-                              : ell_xwin_kernel<1, false, 4>);
+    auto kern = ki == 2 ? (nt ? ell_xwin_kernel<2, true, 4> : ell_xwin_kernel<2, false, 4>)
+                        : (nt ? ell_xwin_kernel<1, true, 4> : ell_xwin_kernel<1, false, 4>);
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock), (size_t)xcap * sizeof(double),
                        (hipStream_t)d.stream, d.n_rows, K, ld, col, val, x, y, (const int2 *)win, xcap);
     SPMV_CHECK_LAUNCH("ell_xwin_kernel");
@@ -778,7 +839,10 @@ extern "C" int spmv_sell_run_split(spmv_dims d, int32_t C, int32_t sigma, int32_
         return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_run_split: grid too large");
     const hipStream_t st = (hipStream_t)d.stream;
     const bool nt = stream_nt(kSellStreamNtDefault);
-    if (win) {
+    const int S = sell_small_waves(C, n_slices);
+    if (S > 1) {
+        launch_sell_small_any(S, ki, nt, n_slices, slice_ptr, perm, col, val, XGlobal{x}, y, (int64_t)T, st);
+    } else if (win) {
         auto kern = ki == 2 ? (nt ? sell_xwin_kernel<2, true, 4> : sell_xwin_kernel<2, false, 4>)
                             : (nt ? sell_xwin_kernel<1, true, 4> : sell_xwin_kernel<1, false, 4>);
         hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(bt), (size_t)xcap * sizeof(double), st, C, n_slices,
@@ -845,10 +909,15 @@ extern "C" int spmv_sell_run_hot(spmv_dims d, int32_t C, int32_t sigma, int32_t 
                            H, hot, x, xh);
     const XHot xs{x, xh, (int32_t)d.n_cols};
     const bool nt = stream_nt(kSellStreamNtDefault);
-    auto kern = ki == 2 ? (nt ? sell_kernel<2, true, 4, XHot> : sell_kernel<2, false, 4, XHot>)
-                        : (nt ? sell_kernel<1, true, 4, XHot> : sell_kernel<1, false, 4, XHot>);
-    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(bt), 0, st, C, n_slices, slice_ptr, perm, col_hot, val, xs,
-                       y, 0, (int64_t)T);
+    const int S = sell_small_waves(C, n_slices);
+    if (S > 1) {
+        launch_sell_small_any(S, ki, nt, n_slices, slice_ptr, perm, col_hot, val, xs, y, (int64_t)T, st);
+    } else {
+        auto kern = ki == 2 ? (nt ? sell_kernel<2, true, 4, XHot> : sell_kernel<2, false, 4, XHot>)
+                            : (nt ? sell_kernel<1, true, 4, XHot> : sell_kernel<1, false, 4, XHot>);
+        hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(bt), 0, st, C, n_slices, slice_ptr, perm, col_hot, val,
+                           xs, y, 0, (int64_t)T);
+    }
     SPMV_CHECK_LAUNCH("sell kernel (hot columns)");
     if (n_chunks == 0)
         return SPMV_SUCCESS;

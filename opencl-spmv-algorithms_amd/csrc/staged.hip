@@ -150,7 +150,7 @@ __device__ __forceinline__ void stage_chunk(int64_t cb, int64_t ce, int64_t nz, 
 // products gather from LDS; a window wider than xcap gathers from global
 // memory.  Same products, same order: y is bit-identical either way.
 // NT: non-temporal loads of the entry stream.
-template <int L, int R, bool XW, bool NT = false, bool PIPE = false>
+template <int L, int R, bool XW, bool NT = false>
 __global__ __launch_bounds__(kBlock) void cmrs_staged_kernel(
     int64_t n_rows, int32_t h, int32_t G, int64_t n_strips,
     const int64_t *__restrict__ strip_ptr, const uint8_t *__restrict__ rin,
@@ -194,24 +194,15 @@ __global__ __launch_bounds__(kBlock) void cmrs_staged_kernel(
     const int64_t nz = strip_ptr[n_strips];
 
     double acc = 0.0;
-    // PIPE: the next chunk's loads are issued before this chunk's barrier
-    // and reduction (as the MODE 3 CSR kernel); same chunks, same bits
-    StageRegs<R, NT, double, KeysU8> st;
     // chunks start on a 32-entry boundary: whole 128-B lines per wave (as
-    // csr.hip kChunkAlign); the previous strip's entries are never summed
+    // csr.hip kChunkAlign); the previous strip's entries are never summed.
+    // (A software-pipelined chunk loop, the next chunk's loads issued before
+    // this chunk's barrier, measured 0.3227 vs 0.2896 ms: 78 instead of 66
+    // VGPRs; profiles/round2/ab_cmrs_pipe.log.)
     const int64_t c0 = s_sp[0] & ~(int64_t)31;
-    if (PIPE && c0 < blk_end)
-        st.issue(c0, c0 + CH < blk_end ? c0 + CH : blk_end, nz, col, val, keys);
     for (int64_t cb = c0; cb < blk_end; cb += CH) {
         const int64_t ce = cb + CH < blk_end ? cb + CH : blk_end;
-        if constexpr (PIPE) {
-            if (staged)
-                st.commit(cb, ce, nz, col, val, XWindow{s_x, wlo}, s_prod, keys);
-            else
-                st.commit(cb, ce, nz, col, val, XGlobal{x}, s_prod, keys);
-            if (ce < blk_end)
-                st.issue(ce, ce + CH < blk_end ? ce + CH : blk_end, nz, col, val, keys);
-        } else if (staged) {
+        if (staged) {
             stage_chunk<R, NT>(cb, ce, nz, col, val, XWindow{s_x, wlo}, s_prod, keys);
         } else {
             stage_chunk<R, NT>(cb, ce, nz, col, val, XGlobal{x}, s_prod, keys);
@@ -235,13 +226,7 @@ __global__ __launch_bounds__(kBlock) void cmrs_staged_kernel(
 // ------------------------------------------------------------------- COO
 constexpr int kCooRowCap = 1024;
 // entry pairs staged per thread by the COO kernels (tile = 2·256·kCooR entries)
-#ifndef SPMV_COO_R
-#define SPMV_COO_R 3
-#endif
-constexpr int kCooR = SPMV_COO_R;
-// the tile must hold at least one pair per thread; spmv_coo_ws_bytes sizes
-// the carry arrays from the smaller of this tile and coo.hip's kTile
-static_assert(kCooR >= 1 && kCooR <= 8, "SPMV_COO_R must be in [1, 8]");
+constexpr int kCooR = 3;
 
 // A workgroup owns one tile of CH consecutive row-sorted entries and
 // writes y for rows (row[t0-1], row[t1-1]] (rows without entries get 0;
@@ -417,69 +402,17 @@ __global__ __launch_bounds__(kBlock) void csr_tile_rows_kernel(int64_t n_rows, i
 // on R-MAT (tools/rmat_exp.hip mode 2).
 constexpr int kTiledRowCap = 1024;
 
-// Fused carry (FC, plan given): a row spanning tiles t_own..t_last is
-// finished by whichever of its tiles arrives last, so no carry pass runs.
-// The owner puts its partial in part_own[t_own], each later tile in
-// part_in[t] (a tile can be both: continuation of the row running in and
-// owner of the row running out, hence two arrays), then adds one to
-// cnt[t_own]; the tile that sees P - 1 sums part_in[t_own+1..t_last] from
-// zero in tile order and adds it to the owner's part exactly as
-// coo_carry_kernel adds its sum to the owner's y (same bits), and resets
-// the counter, so the plan's counters are zero between runs.
-// The partials travel through agent-scope atomic RMWs (exchange to put,
-// OR 0 to get), performed where the counter's RMWs are, and a put has
-// returned before its counter add issues.  No release/acquire fence: on
-// gfx950 those write back / invalidate the whole L2 and measured 7x slower
-// on R-MAT (5.9 vs 0.86 ms).
-__device__ __forceinline__ void part_put(double *p, double v)
-{
-    (void)__hip_atomic_exchange(reinterpret_cast<unsigned long long *>(p), (unsigned long long)__double_as_longlong(v),
-                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// zero: a 0 the compiler cannot prove (an idempotent RMW would be folded
-// into a plain atomic load)
-__device__ __forceinline__ double part_get(const double *p, unsigned long long zero)
-{
-    return __longlong_as_double((long long)__hip_atomic_fetch_or(
-        reinterpret_cast<unsigned long long *>(const_cast<double *>(p)), zero, __ATOMIC_RELAXED,
-        __HIP_MEMORY_SCOPE_AGENT));
-}
-
-__device__ __forceinline__ void tiled_arrive(int64_t r, int64_t t_own, int64_t t_last, double *slot, double v,
-                                             const double *part_in, const double *part_own,
-                                             uint32_t *__restrict__ cnt, double *__restrict__ y)
-{
-    part_put(slot, v);
-    __builtin_amdgcn_s_waitcnt(0);  // the put has been performed
-    const uint32_t P = (uint32_t)(t_last - t_own + 1);
-    const uint32_t old = __hip_atomic_fetch_add(cnt + t_own, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (old + 1 != P)
-        return;
-    const unsigned long long zero = (unsigned long long)(r < 0);
-    double s = 0.0;
-    for (int64_t u = t_own + 1; u <= t_last; u += 8) {
-        double vv[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-            vv[k] = u + k <= t_last ? part_get(part_in + u + k, zero) : 0.0;
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-            if (u + k <= t_last)
-                s += vv[k];
-    }
-    store_y(y + r, part_get(part_own + t_own, zero) + s);
-    __hip_atomic_store(cnt + t_own, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <int L, int R, bool NT, typename XS, typename V = double, bool FC = false>
+// (A fused carry — the last-arriving tile of a spanning row finishing it —
+// was bit-identical but slower: 0.890 vs 0.856 ms on R-MAT with the
+// partials passed through RMW atomics, 5.9 ms with agent-scope
+// release/acquire; removed)
+template <int L, int R, bool NT, typename XS, typename V = double>
 __global__ __launch_bounds__(kBlock) void csr_tiled_kernel(
     int64_t n_rows, int64_t nnz, const int64_t *__restrict__ row_ptr,
     const int32_t *__restrict__ col, const V *__restrict__ val,
     const XS xs, double *__restrict__ y,
     const int32_t *__restrict__ own_lo, int32_t *__restrict__ carry_row,
-    double *__restrict__ carry_val, uint32_t *__restrict__ cnt = nullptr,
-    double *__restrict__ part_own = nullptr)
+    double *__restrict__ carry_val)
 {
     constexpr int CH = 2 * kBlock * R;
     constexpr int GROUPS = kBlock / L;
@@ -513,12 +446,7 @@ __global__ __launch_bounds__(kBlock) void csr_tiled_kernel(
                 c += prod[j - t0];
         }
         c = group_sum<L>(c);
-        if constexpr (FC) {
-            if (lane == 0 && cr >= 0) {
-                const int64_t b0 = row_ptr[cr], b1 = r_lo < n_rows ? row_ptr[r_lo] : nnz;
-                tiled_arrive(cr, b0 / CH, (b1 - 1) / CH, carry_val + tile, c, carry_val, part_own, cnt, y);
-            }
-        } else if (lane == 0) {
+        if (lane == 0) {
             carry_row[tile] = cr;
             carry_val[tile] = c;
         }
@@ -537,16 +465,8 @@ __global__ __launch_bounds__(kBlock) void csr_tiled_kernel(
         for (int j = a + lane; j < b; j += L)
             s += prod[j];
         s = group_sum<L>(s);
-        if (lane == 0) {
-            if constexpr (FC) {
-                const int64_t e = r == r_hi && r < n_rows ? row_ptr[r + 1] : 0;
-                if (e > t1) {  // the tile's last row runs on: owner's part
-                    tiled_arrive(r, tile, (e - 1) / CH, part_own + tile, s, carry_val, part_own, cnt, y);
-                    continue;
-                }
-            }
+        if (lane == 0)
             store_y(y + (r), s);
-        }
     }
 }
 
@@ -630,16 +550,9 @@ __global__ __launch_bounds__(kBlock) void cmrs_tiled_kernel(
 // CMRS tile = 2·kBlock·R entries, R as the tiled CSR's rule (1 below a mean
 // row of 96, else 3): R-MAT 1e7/1e8 0.877 vs 0.902 ms, 8 row shards max
 // 0.166 vs 0.244 ms (profiles/round2/ab_cmrs_tiled_r.log).
-// SPMV_CMRS_TILED_R = 1 / 3 forces it (read once per process); workspaces
-// are sized for R = 1.
+// Workspaces are sized for R = 1.
 static int cmrs_tiled_r(int64_t n_rows, int64_t nnz)
 {
-    static const int forced = [] {
-        const char *s = getenv("SPMV_CMRS_TILED_R");
-        return s && (s[0] == '1' || s[0] == '3') ? s[0] - '0' : 0;
-    }();
-    if (forced)
-        return forced;
     return n_rows > 0 && (double)nnz >= 96.0 * (double)n_rows ? 3 : 1;
 }
 
@@ -731,23 +644,9 @@ int launch_cmrs_tiled(const spmv_dims &d, int32_t h, int64_t n_strips, const int
 // (profiles/round2/ab_tiled_r.log).  Hub shards, whose rows run over many
 // tiles (more carries), split: mean 179 (1 of 8) 0.1366 ms with R = 3 vs
 // 0.1475 with R = 1, mean 55 (1 of 4) 0.2855 vs 0.2667 (ab_tiled_r_hub.log).
-// SPMV_TILED_R in [1, 4] forces R; it is read ONCE per process, since
-// plans and runs must agree on it.  Workspaces and plans are sized for the
-// smallest tile, so any R fits them.
-static int tiled_r_env()
-{
-    static const int r = [] {
-        const char *s = getenv("SPMV_TILED_R");
-        const int v = s ? atoi(s) : 0;
-        return v >= 1 && v <= 4 ? v : 0;
-    }();
-    return r;
-}
-
+// Workspaces and plans are sized for the smallest tile.
 static int tiled_r(int64_t n_rows, int64_t nnz)
 {
-    if (tiled_r_env())
-        return tiled_r_env();
     return n_rows > 0 && (double)nnz >= 96.0 * (double)n_rows ? 3 : 1;
 }
 
@@ -757,21 +656,15 @@ int64_t csr_tiled_tile_min() { return 2 * kBlock; }
 template <int R, typename XS, typename V>
 static void launch_tiled_r(const spmv_dims &d, int64_t tiles, const int64_t *row_ptr, const int32_t *col,
                            const V *val, XS xs, double *y, const int32_t *own_lo, int32_t *carry_row,
-                           double *carry_val, uint32_t *cnt, double *part_own)
+                           double *carry_val)
 {
     const hipStream_t st = (hipStream_t)d.stream;
     const double mean = d.n_rows > 0 ? (double)d.nnz / (double)d.n_rows : 0.0;
-    // the carry-pass-free and plain-load variants exist for R = 3 only
+    // the plain-load variant exists for R = 3 only
     const bool nt = R != 3 || stream_nt(true);
 #define SPMV_TILED(LL)                                                                                    \
     do {                                                                                                  \
         if constexpr (R == 3) {                                                                           \
-            if (cnt) {                                                                                    \
-                hipLaunchKernelGGL((csr_tiled_kernel<LL, R, true, XS, V, true>), dim3((unsigned)tiles),  \
-                                   dim3(kBlock), 0, st, d.n_rows, d.nnz, row_ptr, col, val, xs, y, own_lo, \
-                                   carry_row, carry_val, cnt, part_own);                                  \
-                break;                                                                                    \
-            }                                                                                             \
             if (!nt) {                                                                                    \
                 hipLaunchKernelGGL((csr_tiled_kernel<LL, R, false, XS, V>), dim3((unsigned)tiles),       \
                                    dim3(kBlock), 0, st, d.n_rows, d.nnz, row_ptr, col, val, xs, y, own_lo, \
@@ -796,14 +689,12 @@ static void launch_tiled_r(const spmv_dims &d, int64_t tiles, const int64_t *row
 template <typename XS, typename V>
 static void launch_tiled_xs(const spmv_dims &d, int64_t tiles, const int64_t *row_ptr, const int32_t *col,
                             const V *val, XS xs, double *y, const int32_t *own_lo, int32_t *carry_row,
-                            double *carry_val, uint32_t *cnt = nullptr, double *part_own = nullptr)
+                            double *carry_val)
 {
-    switch (tiled_r(d.n_rows, d.nnz)) {
-    case 1: launch_tiled_r<1>(d, tiles, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val, nullptr, nullptr); break;
-    case 2: launch_tiled_r<2>(d, tiles, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val, nullptr, nullptr); break;
-    case 4: launch_tiled_r<4>(d, tiles, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val, nullptr, nullptr); break;
-    default: launch_tiled_r<3>(d, tiles, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val, cnt, part_own);
-    }
+    if (tiled_r(d.n_rows, d.nnz) == 1)
+        launch_tiled_r<1>(d, tiles, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val);
+    else
+        launch_tiled_r<3>(d, tiles, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val);
 }
 
 int launch_csr_tiled(const spmv_dims &d, const int64_t *row_ptr, const int32_t *col,
@@ -831,13 +722,6 @@ int launch_csr_tiled_hot(const spmv_dims &d, const int64_t *row_ptr, const int32
     const int64_t tiles = (d.nnz + ch - 1) / ch;
     const hipStream_t st = (hipStream_t)d.stream;
     launch_hot_gather(H, hot, x, xh, st);
-    // a plan carries the fused carry's arrival counters (kept zero between
-    // runs): rows spanning tiles are finished inside the tiled kernel
-    uint32_t *cnt = own_lo_plan && tiled_fused_carry() && tiled_r(d.n_rows, d.nnz) == 3 ? (uint32_t *)(own_lo_plan + tiles + 1)
-                                                                         : nullptr;
-    // the owners' partials reuse the workspace's own_lo + carry_row words
-    // (2 tiles + 1 int32 after carry_val, 8-byte aligned), idle with a plan
-    double *part_own = reinterpret_cast<double *>(own_lo);
     if (!own_lo_plan) {
         hipLaunchKernelGGL(csr_tile_rows_kernel, dim3((unsigned)((tiles + 1 + kBlock - 1) / kBlock)),
                            dim3(kBlock), 0, st, d.n_rows, d.nnz, tiles, ch, row_ptr, own_lo);
@@ -846,12 +730,11 @@ int launch_csr_tiled_hot(const spmv_dims &d, const int64_t *row_ptr, const int32
     }
     if (H > 0)
         launch_tiled_xs(d, tiles, row_ptr, col, val, XHot{x, xh, (int32_t)d.n_cols}, y, own_lo_plan, carry_row,
-                        carry_val, cnt, part_own);
+                        carry_val);
     else
-        launch_tiled_xs(d, tiles, row_ptr, col, val, XGlobal{x}, y, own_lo_plan, carry_row, carry_val, cnt,
-                        part_own);
+        launch_tiled_xs(d, tiles, row_ptr, col, val, XGlobal{x}, y, own_lo_plan, carry_row, carry_val);
     SPMV_CHECK_LAUNCH("csr_tiled_kernel (hot columns)");
-    return cnt ? SPMV_SUCCESS : launch_carry(tiles, carry_row, carry_val, y, st);
+    return launch_carry(tiles, carry_row, carry_val, y, st);
 }
 
 template int launch_csr_tiled_hot<double>(const spmv_dims &, const int64_t *, const int32_t *, const double *,
@@ -875,14 +758,6 @@ void cmrs_geometry(const spmv_dims &d, int32_t h, int64_t n_strips, int *L, int 
     *blocks = (n_strips + *G - 1) / *G;
 }
 
-// SPMV_CMRS_PIPE=0/1: the pipelined CMRS chunk loop (read per call; A/B knob)
-constexpr bool kCmrsPipe = false;
-static bool cmrs_pipe()
-{
-    const char *s = getenv("SPMV_CMRS_PIPE");
-    return s && (s[0] == '0' || s[0] == '1') ? s[0] == '1' : kCmrsPipe;
-}
-
 int launch_cmrs_staged(const spmv_dims &d, int32_t h, int64_t n_strips,
                        const int64_t *strip_ptr, const uint8_t *rin, const int32_t *col,
                        const double *val, const double *x, double *y, const int2 *win, int32_t xcap)
@@ -896,14 +771,9 @@ int launch_cmrs_staged(const spmv_dims &d, int32_t h, int64_t n_strips,
     constexpr int R = 3;
     const size_t lds = win ? (size_t)xcap * sizeof(double) : 0;
     const bool nt = stream_nt(true);  // +5 % on the cant batch (0.321 vs 0.338 ms)
-    const bool pipe = cmrs_pipe();
 #define SPMV_CMRS_STAGED(LL)                                                                            \
     do {                                                                                                \
-        if (win && nt && pipe)                                                                          \
-            hipLaunchKernelGGL((cmrs_staged_kernel<LL, R, true, true, true>), dim3((unsigned)blocks),    \
-                               dim3(kBlock), lds, st, d.n_rows, h, G, n_strips, strip_ptr, rin, col, val, \
-                               x, y, win, xcap);                                                        \
-        else if (win && nt)                                                                             \
+        if (win && nt)                                                                             \
             hipLaunchKernelGGL((cmrs_staged_kernel<LL, R, true, true>), dim3((unsigned)blocks),          \
                                dim3(kBlock), lds, st, d.n_rows, h, G, n_strips, strip_ptr, rin, col, val, \
                                x, y, win, xcap);                                                        \
@@ -933,15 +803,10 @@ int launch_cmrs_staged(const spmv_dims &d, int32_t h, int64_t n_strips,
 int64_t coo_staged_tile() { return 2 * kBlock * kCooR; }
 
 // COO over the hot-column table (power-law matrices): 512-entry tiles (R =
-// 1) below a mean row of 96, as the tiled CSR and CMRS; SPMV_COO_HOT_R=0
-// keeps the kCooR tile (read once per process).
+// 1) below a mean row of 96, as the tiled CSR and CMRS.
 static int coo_hot_r(int64_t n_rows, int64_t nnz)
 {
-    static const bool keep = [] {
-        const char *s = getenv("SPMV_COO_HOT_R");
-        return s && s[0] == '0';
-    }();
-    return !keep && n_rows > 0 && (double)nnz < 96.0 * (double)n_rows ? 1 : kCooR;
+    return n_rows > 0 && (double)nnz < 96.0 * (double)n_rows ? 1 : kCooR;
 }
 
 int64_t coo_hot_tile(int64_t n_rows, int64_t nnz) { return 2 * kBlock * coo_hot_r(n_rows, nnz); }
@@ -1078,9 +943,19 @@ __global__ __launch_bounds__(kBlock) void cmrs_window_kernel(int64_t n_strips, i
                                                              const int32_t *__restrict__ col,
                                                              int2 *__restrict__ win)
 {
+    // every entry the staged kernel LOADS for the run (as csr.hip
+    // csr_window_kernel): from two before the 32-entry-aligned first chunk to
+    // one past the run's last entry; those outside the run are never summed,
+    // but their gathers read LDS and must stay inside the window
     const int64_t s0 = (int64_t)blockIdx.x * G;
     const int64_t s1 = s0 + G < n_strips ? s0 + G : n_strips;
-    const int2 r = block_col_range(col, strip_ptr[s0], strip_ptr[s1]);
+    const int64_t nz = strip_ptr[n_strips];
+    const int64_t b = strip_ptr[s0], e = strip_ptr[s1];
+    int2 r = {0, -1};
+    if (b < e) {  // uniform
+        const int64_t c0 = b & ~(int64_t)31;
+        r = block_col_range(col, c0 >= 2 ? c0 - 2 : 0, e + 1 < nz ? e + 1 : nz);
+    }
     if (threadIdx.x == 0)
         win[blockIdx.x] = r;
 }
@@ -1175,8 +1050,8 @@ extern "C" int spmv_cmrs_xwin_build(spmv_dims d, int32_t h, int64_t n_strips, co
 // row_ptr only: built once here, the runs skip their pre-pass.
 extern "C" int64_t spmv_csr_tiled_plan_len(int64_t nnz)
 {
-    // own_lo[tiles + 1], then one arrival counter per tile (fused carry)
-    return nnz > 0 ? 2 * ((nnz + csr_tiled_tile_min() - 1) / csr_tiled_tile_min()) + 1 : 0;
+    // own_lo[tiles + 1]
+    return nnz > 0 ? (nnz + csr_tiled_tile_min() - 1) / csr_tiled_tile_min() + 1 : 0;
 }
 
 extern "C" int spmv_csr_tiled_plan(spmv_dims d, const int64_t *row_ptr, int32_t *own_lo)
@@ -1193,6 +1068,5 @@ extern "C" int spmv_csr_tiled_plan(spmv_dims d, const int64_t *row_ptr, int32_t 
     hipLaunchKernelGGL(csr_tile_rows_kernel, dim3((unsigned)((tiles + 1 + kBlock - 1) / kBlock)), dim3(kBlock), 0,
                        (hipStream_t)d.stream, d.n_rows, d.nnz, tiles, ch, row_ptr, own_lo);
     SPMV_CHECK_LAUNCH("csr_tile_rows_kernel (plan)");
-    const hipError_t e = hipMemsetAsync(own_lo + tiles + 1, 0, (size_t)tiles * sizeof(uint32_t), (hipStream_t)d.stream);
-    return e == hipSuccess ? SPMV_SUCCESS : fail(SPMV_PROGRAM_ERROR, "spmv_csr_tiled_plan: zero counters", e);
+    return SPMV_SUCCESS;
 }

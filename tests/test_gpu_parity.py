@@ -33,9 +33,9 @@ FMT_PARAMS = [
     ("csr", {"lanes": 64, "variant": 2}),
     ("csr", {"variant": 3}),
     ("csr", {"variant": 4}),
-    ("csr", {"variant": 5}),
-    ("csr", {"lanes": 2, "variant": 5}),
-    ("csr", {"lanes": 64, "variant": 5}),
+    ("csr", {"variant": 1}),
+    ("csr", {"lanes": 2, "variant": 1}),
+    ("csr", {"lanes": 64, "variant": 1}),
     ("csr16", {}),
     ("csrf32", {}),
     ("csrf32", {"lanes": 2}),
@@ -132,7 +132,7 @@ def test_cantlike_batch_random_x(torch_dev, fmt):
 
 
 @pytest.mark.parametrize("fmt,kw", [("coo", {}), ("csr", {}), ("csr", {"variant": 2}), ("csr", {"variant": 4}),
-                                    ("csr", {"variant": 5}), ("sell", {}), ("cmrs", {}), ("hyb", {}),
+                                    ("csr", {"variant": 1}), ("sell", {}), ("cmrs", {}), ("hyb", {}),
                                     ("sell", {"split": 0}), ("sell", {"split": 256, "ki": 2}),
                                     ("sell", {"split": 64, "ki": 1, "xwin": False}),
                                     ("sell", {"sigma": 65536, "ki": 2}),
@@ -156,8 +156,8 @@ def test_ell_refuses_rmat_padding(torch_dev):
 
 @pytest.mark.parametrize("fmt,kw", [("coo", {}), ("csr", {}), ("sell", {}), ("cmrs", {"h": 8}),
                                     ("cmrs", {"h": 32}), ("csr", {"lanes": 64}), ("csr", {"variant": 2}),
-                                    ("csr", {"lanes": 2, "variant": 2}), ("csr", {"variant": 5}),
-                                    ("csr", {"lanes": 2, "variant": 5})])
+                                    ("csr", {"lanes": 2, "variant": 2}), ("csr", {"variant": 1}),
+                                    ("csr", {"lanes": 2, "variant": 1})])
 def test_ragged_long_rows(torch_dev, fmt, kw):
     torch, dev = torch_dev
     m = sa.gen_random(20_000, 50_000, 0, 2_000, seed=21)
@@ -165,7 +165,7 @@ def test_ragged_long_rows(torch_dev, fmt, kw):
     assert_parity(m, y, x)
 
 
-@pytest.mark.parametrize("fmt,kw", [(f, {}) for f in sa.ALL_FORMATS] + [("csr", {"variant": 4}), ("csr", {"variant": 5}),
+@pytest.mark.parametrize("fmt,kw", [(f, {}) for f in sa.ALL_FORMATS] + [("csr", {"variant": 4}), ("csr", {"variant": 1}),
                                                                      ("sell", {"split": 2}), ("cmrs", {"cmrs_variant": 1})])
 def test_bitwise_reproducible(torch_dev, fmt, kw):
     """No atomics anywhere: two launches give identical bits (the reference
@@ -184,14 +184,14 @@ def test_bitwise_reproducible(torch_dev, fmt, kw):
 
 @pytest.mark.parametrize("lanes", [2, 4, 16])
 def test_csr_staged_variants_bit_identical(torch_dev, lanes):
-    """Variants 2, 3 and 5 form the same products and sum each row in the
-    same order, so their y agree bit for bit."""
+    """Variants 2 and 3 and the x-window kernel form the same products and
+    sum each row in the same order, so their y agree bit for bit."""
     torch, dev = torch_dev
     m = sa.gen_random(40_000, 40_000, 0, 700, seed=9)
     x = torch.from_numpy(np.random.default_rng(4).uniform(-1, 1, m.n_cols)).to(dev)
     ys = []
-    for v in (2, 3, 5):
-        dm = sa.to_device(m, "csr", dev, lanes=lanes, variant=v)
+    for v, xw in ((2, False), (3, False), (3, True)):
+        dm = sa.to_device(m, "csr", dev, lanes=lanes, variant=v, xwin=xw)
         y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
         dm.run(x, y)
         ys.append(y)
@@ -223,7 +223,7 @@ def test_csr16_bit_identical_to_csr(torch_dev, case):
     assert_parity(m, ys[1].cpu().numpy(), x.cpu().numpy())
 
 
-@pytest.mark.parametrize("fmt,kw", [("csr", {"variant": 3}), ("csr", {"variant": 5}), ("csr", {"variant": 2}),
+@pytest.mark.parametrize("fmt,kw", [("csr", {"variant": 3}), ("csr", {"variant": 3, "xwin": True}), ("csr", {"variant": 2}),
                                     ("sell", {"ki": 1}), ("sell", {"ki": 2}), ("ell", {"ki": 1}), ("ell", {"ki": 2})])
 def test_stream_load_policy_same_bits(torch_dev, monkeypatch, fmt, kw):
     """SPMV_STREAM_NT only changes the cache policy of the matrix loads."""
@@ -436,25 +436,6 @@ def test_csr_xwin_bit_identical(torch_dev, case, lanes):
         assert_parity(m, ys[1].cpu().numpy(), x.cpu().numpy()[: m.n_cols])
 
 
-@pytest.mark.parametrize("lanes", [4, 8, 32])
-def test_csr_xwin_direct_bit_identical(torch_dev, monkeypatch, lanes):
-    """SPMV_CSR_XWIN_DIRECT=1: the row-walking kernel with LDS x windows
-    gives variant 1's bits."""
-    torch, dev = torch_dev
-    for m in (sa.gen_cantlike(0, copies=2), sa.gen_random(20_000, 20_000, 0, 700, seed=21)):
-        x = torch.from_numpy(np.random.default_rng(8).uniform(-1, 1, m.n_cols)).to(dev)
-        ref = sa.to_device(m, "csr", dev, lanes=lanes, variant=1)
-        y0 = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
-        ref.run(x, y0)
-        monkeypatch.setenv("SPMV_CSR_XWIN_DIRECT", "1")
-        dm = sa.to_device(m, "csr", dev, lanes=lanes, variant=3, xwin=True)
-        y1 = torch.full_like(y0, float("nan"))
-        dm.run(x, y1)
-        monkeypatch.delenv("SPMV_CSR_XWIN_DIRECT")
-        torch.cuda.synchronize()
-        assert torch.equal(y0.view(torch.int64), y1.view(torch.int64))
-
-
 @pytest.mark.parametrize("ki", [1, 2])
 def test_ell_xwin_bit_identical(torch_dev, ki):
     torch, dev = torch_dev
@@ -580,42 +561,6 @@ def test_csr_tiled_empty_row_runs(torch_dev, H):
     assert_parity(m, ya.cpu().numpy(), x.cpu().numpy())
 
 
-@pytest.mark.parametrize("case", ["rmat", "empty_runs", "one_hub"])
-@pytest.mark.parametrize("fmt,H", [("csr", 0), ("csr", 4096), ("csrf32", 4096)])
-def test_csr_tiled_fused_carry(torch_dev, monkeypatch, case, fmt, H):
-    """Fused carry (SPMV_TILED_FUSED_CARRY=1): rows spanning tiles finished
-    by their last-arriving tile inside csr_tiled_kernel give the same bits as
-    the carry pass, run after run (the plan's arrival counters return to
-    zero), including a hub row over ~700 tiles and rows after empty runs."""
-    torch, dev = torch_dev
-    # the fused carry runs with 1536-entry tiles, picked for mean rows >= 96
-    if case == "rmat":
-        m = sa.gen_rmat(100_000, 10_000_000, scale=17, seed=1)
-    elif case == "empty_runs":  # mean 0.2: 512-entry tiles, the carry pass (same bits either way)
-        m, _ = _empty_run_matrix()
-    else:  # row 3 holds 1e6 entries, the rest 1-3 each (mean 102)
-        rng = np.random.default_rng(5)
-        n = 10_000
-        lens = rng.integers(1, 4, n)
-        lens[3] = 1_000_000
-        r = np.repeat(np.arange(n, dtype=np.int32), lens)
-        m = sa.Coo(n, n, r, rng.integers(0, n, r.size).astype(np.int32), rng.uniform(-1, 1, r.size))
-    dm = sa.to_device(m, fmt, dev, hot=H, variant=4)
-    assert dm.params["variant"] == 4
-    x = torch.from_numpy(np.random.default_rng(8).uniform(-1, 1, m.n_cols)).to(dev)
-    monkeypatch.setenv("SPMV_TILED_FUSED_CARRY", "0")
-    y0 = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
-    dm.run(x, y0)
-    monkeypatch.setenv("SPMV_TILED_FUSED_CARRY", "1")
-    for _ in range(3):
-        y1 = torch.full_like(y0, float("nan"))
-        dm.run(x, y1)
-        torch.cuda.synchronize()
-        assert torch.equal(y1.view(torch.int64), y0.view(torch.int64))
-    if fmt == "csr":
-        assert_parity(m, y1.cpu().numpy(), x.cpu().numpy())
-
-
 @pytest.mark.parametrize("fmt,kw", [("coo", {}), ("cmrs", {"cmrs_variant": 1}), ("cmrs", {"cmrs_variant": 1, "h": 32}),
                                     ("sell", {"xwin": False}), ("sell", {"sigma": 1 << 24, "ki": 2, "xwin": False}),
                                     ("sell", {"split": 0, "xwin": False}), ("hyb", {}), ("hyb", {"ki": 1})])
@@ -655,33 +600,6 @@ def test_csr16_refuses_escape_heavy_matrix(torch_dev):
     m = sa.gen_rmat(1_000_000, 10_000_000, scale=20, seed=1)
     with pytest.raises(sa.SpmvError):
         sa.to_device(m, "csr16", dev)
-
-
-@pytest.mark.parametrize("case", ["cantlike", "ragged", "fixtures", "rmat"])
-def test_csr_xwin_prefetch_bit_identical(torch_dev, monkeypatch, case):
-    """csr_xwin_pf_kernel (first chunk's loads issued before the x-window
-    copy) gives csr_xwin_kernel's bits."""
-    torch, dev = torch_dev
-    if case == "cantlike":
-        ms = [sa.gen_cantlike(0, copies=2)]
-    elif case == "ragged":
-        ms = [sa.gen_random(20_000, 50_000, 0, 2_000, seed=21)]
-    elif case == "rmat":
-        ms = [sa.gen_rmat(100_000, 1_000_000, scale=17, seed=2)]
-    else:
-        ms = [sa.read_mtx(GOLDEN / f"{n}.mtx") for n in CASES]
-    for m in ms:
-        dm = sa.to_device(m, "csr", dev, variant=3, xwin=True)
-        x = torch.from_numpy(np.random.default_rng(8).uniform(-1, 1, m.n_cols)).to(dev)
-        ys = []
-        for pf in ("0", "1"):
-            monkeypatch.setenv("SPMV_CSR_XWIN_PF", pf)
-            y = torch.full((max(m.n_rows, 1),), float("nan"), dtype=torch.float64, device=dev)
-            dm.run(x, y)
-            ys.append(y)
-        torch.cuda.synchronize()
-        assert torch.equal(ys[0].view(torch.int64), ys[1].view(torch.int64))
-        assert_parity(m, ys[1].cpu().numpy()[: m.n_rows], x.cpu().numpy())
 
 
 @pytest.mark.parametrize("case", ["cantlike", "ragged", "fixtures"])
@@ -757,88 +675,26 @@ def _xstream_cases(case):
     return [sa.read_mtx(GOLDEN / f"{n}.mtx") for n in CASES]
 
 
-@pytest.mark.parametrize("fmt", ["csr", "csr16", "csrf32"])
 @pytest.mark.parametrize("case", ["cantlike", "ragged", "fixtures", "empty_runs", "shuffled_bands"])
-def test_csr_xstream(torch_dev, monkeypatch, case, fmt):
-    """csr_xstream_kernel (persistent workgroups, one x ring each, the
-    pipeline running across row groups) forms staged_group's chunks and sums:
-    y equals the one-group-window x-window kernel's bit for bit, at every lane
-    width, also where groups outgrow the ring (global gathers) or their
-    column ranges jump."""
+def test_csr_xwin_window_sizes(torch_dev, case):
+    """x windows of 1 row group up to 1024 rows (the MODE 0 / MODE 3 load
+    schedules, windows that fit LDS and windows that gather globally) form
+    staged_group's chunks and sums: the same bits as variant 3 at every lane
+    width, also where column ranges jump between neighbouring groups."""
     torch, dev = torch_dev
     for m in _xstream_cases(case):
         if m.n_rows == 0:
             continue
-        if fmt == "csr16" and case == "ragged":
-            continue  # 16-bit offsets: escapes in most blocks, refused by to_device
         x = torch.from_numpy(np.random.default_rng(12).uniform(-1, 1, max(m.n_cols, 1))).to(dev)
         for lanes in (2, 4, 16, 64):
-            dm = sa.to_device(m, fmt, dev, lanes=lanes, variant=3, xwin=True, xwin_rows=1)
-            ys = []
-            for on in ("0", "1"):
-                monkeypatch.setenv("SPMV_CSR_XSTREAM", on)
+            ref = sa.to_device(m, "csr", dev, lanes=lanes, variant=3, xwin=False)
+            y0 = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
+            ref.run(x, y0)
+            for rows in (1, 128, 1024):
+                dm = sa.to_device(m, "csr", dev, lanes=lanes, variant=3, xwin=True, xwin_rows=rows)
                 y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
                 dm.run(x, y)
                 dm.run(x, y)  # twice: nothing carried between runs
-                ys.append(y)
-            torch.cuda.synchronize()
-            assert torch.equal(ys[1].view(torch.int64), ys[0].view(torch.int64)), (m.label, fmt, lanes)
-            if fmt == "csr":
-                assert_parity(m, ys[1].cpu().numpy(), x.cpu().numpy()[: m.n_cols])
-
-
-@pytest.mark.parametrize("case", ["cantlike", "ragged", "fixtures", "empty_runs"])
-def test_sell_ystage(torch_dev, monkeypatch, case):
-    """SELL-64-1024 with y staged per σ-window in LDS and stored in row order
-    (SPMV_SELL_YSTAGE=1) writes exactly the values of the perm-scattered
-    stores, including a partial last window and padding slots."""
-    torch, dev = torch_dev
-    for m in _xstream_cases(case):
-        if m.n_rows == 0:
-            continue
-        dm = sa.to_device(m, "sell", dev)
-        x = torch.from_numpy(np.random.default_rng(14).uniform(-1, 1, max(m.n_cols, 1))).to(dev)
-        ys = []
-        for on in ("0", "1"):
-            monkeypatch.setenv("SPMV_SELL_YSTAGE", on)
-            y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
-            dm.run(x, y)
-            ys.append(y)
-        torch.cuda.synchronize()
-        assert torch.equal(ys[1].view(torch.int64), ys[0].view(torch.int64)), m.label
-        assert_parity(m, ys[1].cpu().numpy(), x.cpu().numpy()[: m.n_cols])
-
-
-@pytest.mark.parametrize("case", ["cantlike", "ragged", "fixtures", "empty_runs"])
-def test_csr_xwin_load_modes(torch_dev, monkeypatch, case):
-    """Every load schedule of csr_xwin_kernel (SPMV_CSR_XWIN_MODE 0-4 and the
-    first-chunk prefetch) forms the same chunks and sums: the same bits.
-    MODE 5 cuts the window into equal chunks: other bits for rows that cross
-    a chunk boundary, still within the parity criterion."""
-    torch, dev = torch_dev
-    if case == "cantlike":
-        ms = [sa.gen_cantlike(0, copies=2)]
-    elif case == "ragged":
-        ms = [sa.gen_random(20_000, 50_000, 0, 2_000, seed=21)]
-    elif case == "empty_runs":
-        ms = [_empty_run_matrix()[0]]
-    else:
-        ms = [sa.read_mtx(GOLDEN / f"{n}.mtx") for n in CASES]
-    for m in ms:
-        if m.n_rows == 0:
-            continue
-        dm = sa.to_device(m, "csr", dev, variant=3, xwin=True)
-        x = torch.from_numpy(np.random.default_rng(12).uniform(-1, 1, max(m.n_cols, 1))).to(dev)
-        ys = {}
-        for mode, pre in (("0", "0"), ("1", "0"), ("2", "0"), ("3", "0"), ("3", "1"), ("4", "0"), ("5", "0")):
-            monkeypatch.setenv("SPMV_CSR_XWIN_MODE", mode)
-            monkeypatch.setenv("SPMV_CSR_XWIN_PRE", pre)
-            y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
-            dm.run(x, y)
-            ys[mode + pre] = y
-        torch.cuda.synchronize()
-        ref = ys["00"].view(torch.int64)
-        for k in ("10", "20", "30", "31", "40"):
-            assert torch.equal(ys[k].view(torch.int64), ref), (m.label, k)
-        for k in ("00", "50"):
-            assert_parity(m, ys[k].cpu().numpy(), x.cpu().numpy()[: m.n_cols])
+                torch.cuda.synchronize()
+                assert torch.equal(y.view(torch.int64), y0.view(torch.int64)), (m.label, lanes, rows)
+        assert_parity(m, y0.cpu().numpy(), x.cpu().numpy()[: m.n_cols])

@@ -31,8 +31,7 @@ KERNELS = {"csr": "csr_xwin_kernel", "sell": "sell_xwin_kernel", "ell": "ell_xwi
 
 def kernel_for(fmt, env):
     """The dominant kernel's name (substring) for `fmt` under `env`."""
-    if fmt in ("coo", "cmrs") and env.get(f"SPMV_{fmt.upper()}_VARIANT") == "1":
-        return {"coo": "coo_tile_kernel", "cmrs": "cmrs_kernel"}[fmt]
+    del env  # placement / cache-policy knobs do not change the kernel
     return KERNELS[fmt]
 PASSES = {
     "fetch": ["FETCH_SIZE"],

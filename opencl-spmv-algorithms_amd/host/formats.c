@@ -561,7 +561,10 @@ int spmv_hyb_fill(int64_t n_rows, const int64_t *row_ptr, const int32_t *col, co
             b = row_ptr[i];
             e = row_ptr[i + 1];
         }
-        const int32_t pad_col = e > b ? col[(e - b > K ? b + K : e) - 1] : 0;
+        /* padding reuses the row's last ELL column (a valid gather); with K = 0
+         * there is no ELL part and no column to read (found by `make test-san`:
+         * col[b - 1] was read for K = 0) */
+        const int32_t pad_col = (K > 0 && e > b) ? col[(e - b > K ? b + K : e) - 1] : 0;
         for (int64_t k = 0; k < K; ++k) {
             const int64_t pos = (k / ki) * ld * ki + i * ki + (k % ki);
             if (b + k < e) {

@@ -241,7 +241,7 @@ def hip_lib() -> ctypes.CDLL:
 def host_lib() -> ctypes.CDLL:
     global _host
     if _host is None:
-        path = LIB_DIR / "libspmv_host.so"
+        path = Path(os.environ.get("SPMV_HOST_LIB", LIB_DIR / "libspmv_host.so"))  # `make test-san` build
         if not path.exists():
             raise SpmvError(PROGRAM_ERROR, "load libspmv_host.so", f"{path} missing: run `make lib`")
         _host = _bind(ctypes.CDLL(str(path)), HOST_SYMBOLS)

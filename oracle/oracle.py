@@ -10,6 +10,7 @@ reference was denied).
 from __future__ import annotations
 
 import ctypes
+import os
 import subprocess
 from pathlib import Path
 
@@ -43,8 +44,10 @@ def build() -> Path:
 def lib() -> ctypes.CDLL:
     global _lib
     if _lib is None:
-        build()
-        L = ctypes.CDLL(str(LIB))
+        path = os.environ.get("SPMV_ORACLE_LIB")  # `make test-san`: the sanitizer build
+        if not path:
+            build()
+        L = ctypes.CDLL(str(path or LIB))
         L.oracle_read_info.argtypes = [ctypes.c_char_p, ctypes.POINTER(_i64), ctypes.POINTER(_i64),
                                        ctypes.POINTER(_i64), ctypes.POINTER(ctypes.c_int)]
         L.oracle_read_mtx.argtypes = [ctypes.c_char_p, _vp, _vp, _vp]

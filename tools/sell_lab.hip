@@ -1,0 +1,188 @@
+// sell_lab.hip — diagnostic copies of the small-matrix SELL kernel with
+// per-wave timestamps (s_memrealtime, 100 MHz), NOT part of the product.
+// Built into lib/libspmv_lab.so by `make lab`; driven by tools/sell_lab.py on
+// the arrays the library's own builders made.  Stamps go to a buffer of
+// their own (never into y): per wave {start, end, hw_id}.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+constexpr int kWave = 64;
+typedef double v2f64 __attribute__((ext_vector_type(2)));
+typedef int32_t v2i32 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint64_t now() { return __builtin_amdgcn_s_memrealtime(); }
+
+__device__ __forceinline__ uint32_t hw_id()
+{
+    uint32_t v;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(v));
+    return v;
+}
+
+struct XG {
+    const double *x;
+    __device__ __forceinline__ double operator()(int32_t c) const { return x[c]; }
+};
+struct XW {
+    const double *s;
+    int32_t lo;
+    __device__ __forceinline__ double operator()(int32_t c) const { return s[c - lo]; }
+};
+
+// KI = 1: one slot per lane per group; KI = 2: two consecutive slots.
+template <int KI, int U, typename XS>
+__device__ __forceinline__ void slots(const double *vp, const int32_t *cp, int64_t g0, int64_t g1, int64_t step,
+                                      const XS &xs, double *a)
+{
+    for (int64_t g = g0; g < g1; g += U) {
+        if constexpr (KI == 1) {
+            double v[U];
+            int32_t c[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t gg = g + u < g1 ? g + u : g;
+                v[u] = __builtin_nontemporal_load(vp + gg * step);
+                c[u] = __builtin_nontemporal_load(cp + gg * step);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                a[u % 4] += (g + u < g1 ? v[u] : 0.0) * xs(c[u]);
+        } else {
+            v2f64 v[U];
+            v2i32 c[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t gg = g + u < g1 ? g + u : g;
+                v[u] = __builtin_nontemporal_load(reinterpret_cast<const v2f64 *>(vp + gg * step));
+                c[u] = __builtin_nontemporal_load(reinterpret_cast<const v2i32 *>(cp + gg * step));
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const bool in = g + u < g1;
+                a[u % 4] += (in ? v[u].x : 0.0) * xs(c[u].x) + (in ? v[u].y : 0.0) * xs(c[u].y);
+            }
+        }
+    }
+}
+
+// one workgroup of S waves per slice; XWIN: the slice's column window
+// (win[s] = {lo, hi}) copied into LDS first
+template <int KI, int S, int U, bool XWIN>
+__global__ __launch_bounds__(kWave * S) void lab_kernel(const int64_t *__restrict__ slice_ptr,
+                                                        const int32_t *__restrict__ perm,
+                                                        const int32_t *__restrict__ col,
+                                                        const double *__restrict__ val,
+                                                        const double *__restrict__ x, double *__restrict__ y,
+                                                        const int2 *__restrict__ win, int32_t xcap,
+                                                        uint64_t *__restrict__ stamps)
+{
+    const uint64_t t0 = now();
+    extern __shared__ double s_x[];
+    const int64_t s = blockIdx.x;
+    const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+    const int32_t row = wv == 0 ? perm[s * kWave + lane] : -1;
+    const int64_t base = slice_ptr[s];
+    const int64_t w = (slice_ptr[s + 1] - base) / kWave;
+    const int64_t groups = w / KI;
+    const int64_t per = (groups + S - 1) / S;
+    const int64_t g0 = wv * per;
+    const int64_t g1 = g0 + per < groups ? g0 + per : groups;
+    const double *vp = val + base + lane * KI;
+    const int32_t *cp = col + base + lane * KI;
+    double a[4] = {0.0, 0.0, 0.0, 0.0};
+    if constexpr (XWIN) {
+        const int2 wd = win[s];
+        const int32_t span = wd.y - wd.x + 1;
+        if (span > 0 && span <= xcap) {
+            for (int32_t i = threadIdx.x; i < span; i += kWave * S)
+                s_x[i] = x[wd.x + i];
+            __syncthreads();
+            slots<KI, U>(vp, cp, g0, g1, (int64_t)kWave * KI, XW{s_x, wd.x}, a);
+        } else {
+            slots<KI, U>(vp, cp, g0, g1, (int64_t)kWave * KI, XG{x}, a);
+        }
+    } else {
+        slots<KI, U>(vp, cp, g0, g1, (int64_t)kWave * KI, XG{x}, a);
+    }
+    double sum = (a[0] + a[2]) + (a[1] + a[3]);
+    __shared__ double part[S][kWave];
+    if constexpr (S > 1) {
+        part[wv][lane] = sum;
+        __syncthreads();
+        if (wv == 0)
+            for (int k = 1; k < S; ++k)
+                sum += part[k][lane];
+    }
+    if (row >= 0)
+        y[row] = sum;
+    if (lane == 0) {
+        const int64_t i = (s * S + wv) * 3;
+        stamps[i] = t0;
+        stamps[i + 1] = now();
+        stamps[i + 2] = hw_id();
+    }
+}
+
+// column window of every slice: [min, max] of its stored columns
+__global__ void lab_window_kernel(const int64_t *__restrict__ slice_ptr, const int32_t *__restrict__ col,
+                                  int2 *__restrict__ win)
+{
+    const int64_t s = blockIdx.x;
+    int lo = INT32_MAX, hi = INT32_MIN;
+    for (int64_t e = slice_ptr[s] + threadIdx.x; e < slice_ptr[s + 1]; e += blockDim.x) {
+        const int c = col[e];
+        lo = c < lo ? c : lo;
+        hi = c > hi ? c : hi;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const int l2 = __shfl_xor(lo, off), h2 = __shfl_xor(hi, off);
+        lo = l2 < lo ? l2 : lo;
+        hi = h2 > hi ? h2 : hi;
+    }
+    if (threadIdx.x == 0)
+        win[s] = lo <= hi ? int2{lo, hi} : int2{0, -1};
+}
+
+template <int KI, int S, int U, bool XW>
+void launch(int64_t n, const int64_t *sp, const int32_t *perm, const int32_t *col, const double *val,
+            const double *x, double *y, const int2 *win, int32_t xcap, uint64_t *st, hipStream_t s)
+{
+    hipLaunchKernelGGL((lab_kernel<KI, S, U, XW>), dim3((unsigned)n), dim3(kWave * S),
+                       XW ? (size_t)xcap * sizeof(double) : 0, s, sp, perm, col, val, x, y, win, xcap, st);
+}
+
+}  // namespace
+
+extern "C" {
+
+int lab_windows(int64_t n_slices, const int64_t *sp, const int32_t *col, void *win, void *stream)
+{
+    hipLaunchKernelGGL(lab_window_kernel, dim3((unsigned)n_slices), dim3(kWave), 0, (hipStream_t)stream, sp, col,
+                       (int2 *)win);
+    return (int)hipGetLastError();
+}
+
+// code = KI*1000 + S*10 + U (U in {4, 8}), xw = 0/1
+int lab_run(int code, int xw, int64_t n_slices, const int64_t *sp, const int32_t *perm, const int32_t *col,
+            const double *val, const double *x, double *y, const void *win, int32_t xcap, uint64_t *stamps,
+            void *stream)
+{
+    const hipStream_t s = (hipStream_t)stream;
+    const int2 *w = (const int2 *)win;
+#define LAB(KI, S, U)                                                                                     \
+    case KI * 1000 + S * 10 + U:                                                                          \
+        if (xw) launch<KI, S, U, true>(n_slices, sp, perm, col, val, x, y, w, xcap, stamps, s);           \
+        else launch<KI, S, U, false>(n_slices, sp, perm, col, val, x, y, w, xcap, stamps, s);             \
+        break;
+    switch (code) {
+        LAB(1, 1, 4) LAB(1, 1, 8) LAB(1, 2, 4) LAB(1, 4, 4) LAB(1, 4, 8) LAB(1, 8, 4) LAB(1, 8, 8)
+        LAB(1, 16, 4) LAB(2, 1, 4) LAB(2, 2, 4) LAB(2, 4, 4) LAB(2, 4, 8) LAB(2, 8, 4) LAB(2, 16, 4)
+    default: return (int)hipErrorInvalidValue;
+    }
+#undef LAB
+    return (int)hipGetLastError();
+}
+
+}  // extern "C"

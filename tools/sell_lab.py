@@ -1,0 +1,94 @@
+#!/usr/bin/env python3
+"""sell_lab — where the time of the small-matrix SELL kernel goes.
+
+Runs diagnostic copies of the waves-per-slice SELL kernel (tools/sell_lab.hip,
+lib/libspmv_lab.so) on the library's own SELL-64-1024 arrays of one cant-like
+matrix, cold (512 MiB flush first) and warm, and reads per-wave timestamps
+(s_memrealtime, 10 ns): kernel span (first wave start to last wave end),
+wave durations, and how late the last wave started.  Diagnostic only."""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(REPO / "opencl-spmv-algorithms_amd"), str(REPO), str(REPO / "tools")]
+import spmv_amd as sa  # noqa: E402
+from cant_single import FLUSH_BYTES, probe_lib  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--codes", default="1014,1084,1088,2014,2044,2084,2044x,2084x,1084x,2024x,2164x")
+    ap.add_argument("--reps", type=int, default=20)
+    a = ap.parse_args()
+    import torch
+
+    dev = torch.device("cuda:0")
+    st = torch.cuda.current_stream(dev)
+    sp = st.cuda_stream
+    lab = ctypes.CDLL(str(sa.LIB_DIR / "libspmv_lab.so"))
+    vp = ctypes.c_void_p
+    lab.lab_run.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int64, vp, vp, vp, vp, vp, vp, vp, ctypes.c_int32, vp,
+                            vp]
+    lab.lab_windows.argtypes = [ctypes.c_int64, vp, vp, vp, vp]
+    P = probe_lib()
+    scratch = torch.empty(FLUSH_BYTES, dtype=torch.uint8, device=dev)
+    m = sa.gen_cantlike(0, 1)
+    xh = sa.ramp_x(m.n_cols)
+    x = torch.from_numpy(xh).to(dev)
+    b = sa.bytes_alg(m.n_rows, m.n_cols, m.nnz)
+    mats = {}
+    for ki in (1, 2):
+        dm = sa.to_device(m, "sell", dev, ki=ki, xwin=False)
+        A = dm.arrays
+        n = dm.params["n_slices"]
+        win = torch.empty(2 * n, dtype=torch.int32, device=dev)
+        assert lab.lab_windows(n, A["slice_ptr"].data_ptr(), A["col"].data_ptr(), win.data_ptr(), sp) == 0
+        torch.cuda.synchronize()
+        w = win.view(-1, 2).cpu().numpy()
+        xcap = int((w[:, 1] - w[:, 0] + 1).max())
+        mats[ki] = (dm, n, win, xcap)
+    for code in a.codes.split(","):
+        xw = code.endswith("x")
+        c = int(code.rstrip("x"))
+        ki, S, U = c // 1000, (c % 1000) // 10, c % 10
+        dm, n, win, xcap = mats[ki]
+        A = dm.arrays
+        stamps = torch.zeros(n * S * 3, dtype=torch.int64, device=dev)
+        y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
+
+        def run():
+            rc = lab.lab_run(c, int(xw), n, A["slice_ptr"].data_ptr(), A["perm"].data_ptr(), A["col"].data_ptr(),
+                             A["val"].data_ptr(), x.data_ptr(), y.data_ptr(), win.data_ptr(), xcap,
+                             stamps.data_ptr(), sp)
+            assert rc == 0, rc
+
+        res = {}
+        for mode in ("warm", "cold"):
+            spans, durs, late = [], [], []
+            for r in range(a.reps):
+                if mode == "cold":
+                    P.spmv_probe_flush(scratch.data_ptr(), FLUSH_BYTES, sp)
+                run()
+                torch.cuda.synchronize()
+                s = stamps.view(-1, 3).cpu().numpy().astype(np.int64)
+                t0, t1 = s[:, 0], s[:, 1]
+                spans.append((t1.max() - t0.min()) * 10e-3)  # us
+                durs.append(np.median(t1 - t0) * 10e-3)
+                late.append((t0.max() - t0.min()) * 10e-3)
+            res[mode] = {"span_us": round(float(np.median(spans)), 2), "wave_us_med": round(float(np.median(durs)), 2),
+                         "last_start_us": round(float(np.median(late)), 2)}
+        bad, _ = sa.check(m, xh, y.cpu().numpy())
+        span = res["cold"]["span_us"]
+        print(json.dumps({"code": code, "ki": ki, "S": S, "U": U, "xwin": xw, "xcap": xcap, **res,
+                          "cold_GBs_span": round(b / (span * 1e-6) * 1e-9, 1), "parity_ok": bad == 0}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -51,7 +51,7 @@ build/hip/%.o: $(PKG)/csrc/%.hip $(HIP_HDR)
 
 $(LIB_HIP): $(HIP_OBJ)
 	@mkdir -p $(LIBDIR)
-	$(HIPCC) $(HIPFLAGS) -shared $(HIP_OBJ) -o $@
+	$(HIPCC) $(HIPFLAGS) -shared $(HIP_OBJ) -o $@ -ldl
 
 $(LIB_HOST): $(HOST_SRC) include/spmv_host.h include/spmv_rc.h
 	@mkdir -p $(LIBDIR)
@@ -126,7 +126,7 @@ test-san: build/san/host_harness build/san/libspmv_host.so build/san/liboracle.s
 	@for f in $(TARGETS); do for m in tests/golden/empty_rows.mtx tests/golden/n67.mtx tests/golden/longest_last.mtx; do \
 	  $(SANENV) build/san/bin/$$f --matrix $$m > build/san/$$f.log 2>&1; rc=$$?; \
 	  if [ $$rc -ne 0 ] && [ $$rc -ne 1 ]; then echo "$$f $$m: exit $$rc"; cat build/san/$$f.log; exit 1; fi; \
-	done; done; echo "sanitized drivers: parse + build clean (exit 0, or 1 = no GPU)"
+	done; done; echo "sanitized drivers: clean (exit 0 on a GPU; 1 = no GPU found, before any input is read)"
 
 test-gpu: all oracle
 	python -m pytest tests/ -x -q -m gpu

@@ -395,6 +395,32 @@ int spmv_time_launch(spmv_launch_fn launch, void *arg, void *stream,
                      double *ms);
 /* Frees library-owned scratch on the current device. */
 int spmv_release(void);
+/* ---------------------------------------------------------- multi-GPU ---
+ * Single-process row sharding over several GPUs: the
+ * reference creates its OpenCL context over every GPU it finds but uses
+ * device 0 only (reference csr.c:107,115; its device loop breaks after the
+ * first, csr.c:30,279).  spmv_multi_init builds one RCCL communicator per
+ * device with ncclCommInitAll and one non-blocking stream each; the caller
+ * cuts contiguous row ranges (spmv_partition_rows), runs every shard's
+ * spmv_<fmt>_run on its device's stream writing y_full_d + bounds[d], and
+ * spmv_multi_allgatherv completes every device's y_full in place: one
+ * ncclBroadcast of each shard's REAL row count from its owner, all in one
+ * ncclGroupStart/End (an allgatherv; no padding to the largest shard).  */
+typedef struct spmv_multi spmv_multi;
+int spmv_multi_init(int n_gpus, const int *devices /* NULL: 0..n_gpus-1 */, spmv_multi **out);
+int spmv_multi_free(spmv_multi *m);
+int spmv_multi_size(const spmv_multi *m);
+int spmv_multi_device(const spmv_multi *m, int i);
+void *spmv_multi_stream(const spmv_multi *m, int i);
+/* y_full[i]: device i's n-row y (device pointer); bounds[n_gpus + 1]      */
+int spmv_multi_allgatherv(spmv_multi *m, double *const *y_full, const int64_t *bounds);
+int spmv_multi_sync(spmv_multi *m);
+/* Time one launch on every device together: optional flush on each, an
+ * event pair around launch(arg, i) on each device's stream, all devices
+ * synchronised; ms[i] = device i's elapsed time.                        */
+typedef int (*spmv_multi_launch_fn)(void *arg, int i);
+int spmv_multi_time(spmv_multi *m, spmv_multi_launch_fn launch, void *arg, int flush, double *ms);
+
 const char *spmv_strerror(int rc);
 const char *spmv_last_error(void);
 /* Version string of the library build, e.g. "spmv-hip 0.1 gfx950". */

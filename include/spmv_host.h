@@ -165,6 +165,13 @@ int spmv_csr16_fill(int64_t nnz, const int32_t *col, int32_t *blk_base, uint16_t
  * bounds has parts+1 entries, bounds[0] = 0, bounds[parts] = n_rows.    */
 int spmv_partition_rows(int64_t n_rows, const int64_t *row_ptr, int parts,
                         int64_t align, int64_t *bounds);
+/* The entries of rows [lo, hi) in FILE ORDER with rows renumbered to the
+ * shard (row - lo), for a device that owns those rows; returns the count
+ * (output arrays NULL: count only), -1 on bad arguments.  Every entry
+ * lands in exactly one shard of a partition, so the shards' y slices,
+ * written at y + lo, reassemble y.                                      */
+int64_t spmv_coo_row_shard(int64_t nnz, const int32_t *row, const int32_t *col, const double *val,
+                           int64_t lo, int64_t hi, int32_t *row_out, int32_t *col_out, double *val_out);
 /* Same cut, balancing entries + row_weight per row (a row costs the
  * kernels about as much as row_weight entries: its offset, its y store and
  * its reduction; 0 = spmv_partition_rows).                              */

@@ -27,13 +27,20 @@
  * Options: --matrix PATH  --gen cantlike[0|1|2]|rmat|banded|random
  *          --copies B  --reps N  --warmup W  --warm  --device D
  *          --C C --sigma S --ki K --h H --lanes L  --threads T
- *          --cpu / --no-cpu  --strict  --write-mtx PATH  --cache  --no-xwin  --help
+ *          --cpu / --no-cpu  --strict  --write-mtx PATH  --cache  --no-xwin  --gpus N  --help
  *   --cache keeps a binary copy of the parsed file at PATH.bin (SURVEY.md
  *   §8f row 1) and reads it instead of the text whenever it is at least as
  *   new as PATH; the entries, their order and the result are unchanged.
  *   CSR, ELL and SELL run the x-window kernels (each workgroup's x range
  *   staged in LDS, include/spmv.h); --no-xwin runs the global-gather ones.
  *   Device buffers are released by spmv_release() / process exit.
+ *   --gpus N (N >= 1) shards the rows over GPUs 0..N-1 from ONE process
+ *   (run_multi below): contiguous row ranges (spmv_partition_rows, aligned
+ *   to 1024 rows so SELL windows never straddle two GPUs), x replicated,
+ *   every shard's kernel writing its rows of a full-length y on its GPU, and
+ *   the y exchange as RCCL broadcasts of the real shard sizes
+ *   (spmv_multi_allgatherv).  The reference builds its context over every
+ *   GPU but runs on the first only (reference csr.c:30,107,115,279).
  */
 #define _POSIX_C_SOURCE 200809L
 #include <errno.h>
@@ -55,7 +62,7 @@ typedef struct {
     const char *gen;
     const char *write_mtx;
     int64_t copies;
-    int reps, warmup, warm, device, C, sigma, ki, h, lanes, threads, cpu, strict, cache, xwin;
+    int reps, warmup, warm, device, C, sigma, ki, h, lanes, threads, cpu, strict, cache, xwin, gpus;
 } opts_t;
 
 static void usage(const char *prog)
@@ -64,7 +71,7 @@ static void usage(const char *prog)
            "          [--copies B] [--reps N] [--warmup W] [--warm] [--device D]\n"
            "          [--C C] [--sigma S] [--ki 1|2] [--h H] [--lanes L]\n"
            "          [--threads T] [--cpu|--no-cpu] [--strict] [--write-mtx PATH] [--cache]\n"
-           "          [--no-xwin]\n",
+           "          [--no-xwin] [--gpus N]\n",
            prog);
 }
 
@@ -105,6 +112,7 @@ static int parse_opts(int argc, char **argv, spmv_format fmt, opts_t *o)
         else if (!strcmp(a, "--h")) { NEEDV(); o->h = atoi(v); }
         else if (!strcmp(a, "--lanes")) { NEEDV(); o->lanes = atoi(v); }
         else if (!strcmp(a, "--threads")) { NEEDV(); o->threads = atoi(v); }
+        else if (!strcmp(a, "--gpus")) { NEEDV(); o->gpus = atoi(v); }
         else if (!strcmp(a, "--warm")) o->warm = 1;
         else if (!strcmp(a, "--cpu")) o->cpu = 1;
         else if (!strcmp(a, "--no-cpu")) o->cpu = 0;
@@ -120,7 +128,7 @@ static int parse_opts(int argc, char **argv, spmv_format fmt, opts_t *o)
 #undef NEEDV
     }
     if (o->reps < 1 || o->warmup < 0 || o->copies < 1 || (o->ki < 0 || o->ki > 2) ||
-        o->h < 1 || o->h > 64 || o->C < 1 || o->C > 1024)
+        o->h < 1 || o->h > 64 || o->C < 1 || o->C > 1024 || o->gpus < 0 || o->gpus > 64)
         return SPMV_OTHER_ERROR;
     return SPMV_SUCCESS;
 }
@@ -628,6 +636,178 @@ static const char *fmt_name(spmv_format f)
     return n[f];
 }
 
+/* ------------------------------------------------------------ --gpus N */
+
+typedef struct {
+    dev_fmt_t *f;
+} multi_arg_t;
+
+static int launch_shard(void *arg, int i)
+{
+    return launch(&((multi_arg_t *)arg)->f[i]);
+}
+
+static double median_of(double *v, int n)
+{
+    qsort(v, (size_t)n, sizeof(double), cmp_double);
+    return v[n / 2];
+}
+
+static int run_multi(const opts_t *o, spmv_format fmt, const coo_t *m, const double *x, double *y, double *y_cpu)
+{
+    const int G = o->gpus;
+    const int64_t N = m->n_rows, Z = m->nnz;
+    int rc;
+    /* contiguous row ranges with ~Z/G entries each, 1024-aligned */
+    int64_t *ptr = malloc((size_t)(N + 1) * sizeof(int64_t));
+    int32_t *tc = malloc((size_t)(Z + 1) * sizeof(int32_t));
+    double *tv = malloc((size_t)(Z + 1) * sizeof(double));
+    int64_t *bounds = malloc((size_t)(G + 1) * sizeof(int64_t));
+    dev_fmt_t *f = calloc((size_t)G, sizeof(dev_fmt_t));
+    double **y_full = calloc((size_t)G, sizeof(double *));
+    double *ms = malloc((size_t)G * sizeof(double));
+    double *t = malloc((size_t)o->reps * sizeof(double)), *tag = malloc((size_t)o->reps * sizeof(double));
+    double *tall = malloc((size_t)o->reps * sizeof(double)), *tdev = malloc((size_t)o->reps * G * sizeof(double));
+    if (!ptr || !tc || !tv || !bounds || !f || !y_full || !ms || !t || !tag || !tall || !tdev)
+        return SPMV_OTHER_ERROR;
+    if ((rc = spmv_csr_from_coo(N, Z, m->row, m->col, m->val, ptr, tc, tv)) ||
+        (rc = spmv_partition_rows(N, ptr, G, 1024, bounds)))
+        return rc;
+    free(tc);
+    free(tv);
+    spmv_multi *mg = NULL;
+    if ((rc = spmv_multi_init(G, NULL, &mg)) != SPMV_SUCCESS) {
+        printf("RCCL init over %d GPUs failed: %s\n", G, spmv_last_error());
+        return rc;
+    }
+    for (int g = 0; g < G; ++g) {
+        const int64_t lo = bounds[g], hi = bounds[g + 1];
+        coo_t s = {hi - lo, m->n_cols, 0, NULL, NULL, NULL, m->label};
+        s.nnz = spmv_coo_row_shard(Z, m->row, m->col, m->val, lo, hi, NULL, NULL, NULL);
+        s.row = malloc((size_t)(s.nnz + 1) * sizeof(int32_t));
+        s.col = malloc((size_t)(s.nnz + 1) * sizeof(int32_t));
+        s.val = malloc((size_t)(s.nnz + 1) * sizeof(double));
+        if (s.nnz < 0 || !s.row || !s.col || !s.val)
+            return SPMV_OTHER_ERROR;
+        spmv_coo_row_shard(Z, m->row, m->col, m->val, lo, hi, s.row, s.col, s.val);
+        opts_t og = *o;
+        og.device = spmv_multi_device(mg, g);
+        if ((rc = spmv_set_device(og.device)) != SPMV_SUCCESS)
+            return rc;
+        rc = build_format(&og, fmt, &s, &f[g]);
+        f[g].d.stream = spmv_multi_stream(mg, g);
+        if (rc == SPMV_SUCCESS && o->xwin)
+            rc = build_windows(&f[g]);
+        if (rc != SPMV_SUCCESS) {
+            printf("shard %d: format build/upload failed: %s %s\n", g, spmv_strerror(rc), spmv_last_error());
+            return rc == SPMV_OTHER_ERROR ? SPMV_OTHER_ERROR : SPMV_PROGRAM_ERROR;
+        }
+        /* x replicated; this shard's kernel writes rows [lo, hi) of y_full */
+        if ((rc = upload((void **)&f[g].d_x, x, (size_t)m->n_cols * 8, NULL)) ||
+            (rc = spmv_malloc((void **)&y_full[g], (size_t)(N + 1) * 8)) ||
+            (rc = spmv_memset(y_full[g], 0xFF, (size_t)(N + 1) * 8, NULL))) /* NaN: every row must arrive */
+            return SPMV_PROGRAM_ERROR;
+        f[g].d_y = y_full[g] + lo;
+        free(s.row);
+        free(s.col);
+        free(s.val);
+    }
+    multi_arg_t arg = {f};
+    for (int i = 0; i < o->warmup; ++i)
+        for (int g = 0; g < G; ++g) {
+            spmv_set_device(spmv_multi_device(mg, g));
+            if ((rc = launch(&f[g])) != SPMV_SUCCESS) {
+                printf("kernel launch error: %s\n", spmv_last_error());
+                return SPMV_PROGRAM_ERROR;
+            }
+        }
+    if ((rc = spmv_multi_sync(mg)))
+        return SPMV_PROGRAM_ERROR;
+    /* SpMV alone: every GPU's shard launched together (cold unless --warm),
+     * the step's time is the slowest GPU's */
+    for (int i = 0; i < o->reps; ++i) {
+        if ((rc = spmv_multi_time(mg, launch_shard, &arg, !o->warm, ms)) != SPMV_SUCCESS) {
+            printf("kernel launch error: %s\n", spmv_last_error());
+            return SPMV_PROGRAM_ERROR;
+        }
+        t[i] = 0.0;
+        for (int g = 0; g < G; ++g) {
+            tdev[(size_t)g * o->reps + i] = ms[g];
+            t[i] = ms[g] > t[i] ? ms[g] : t[i];
+        }
+    }
+    const double spmv_ms = median_of(t, o->reps); /* sorts t */
+    const double t_min = t[0];
+    /* the y exchange alone, and SpMV + exchange (host wall, all GPUs synchronised) */
+    for (int i = 0; i < o->reps; ++i) {
+        double t0 = now_s();
+        if ((rc = spmv_multi_allgatherv(mg, y_full, bounds)) || (rc = spmv_multi_sync(mg))) {
+            printf("RCCL all-gather failed: %s\n", spmv_last_error());
+            return SPMV_PROGRAM_ERROR;
+        }
+        tag[i] = (now_s() - t0) * 1e3;
+        t0 = now_s();
+        for (int g = 0; g < G && rc == SPMV_SUCCESS; ++g) {
+            spmv_set_device(spmv_multi_device(mg, g));
+            rc = launch(&f[g]);
+        }
+        if (rc || (rc = spmv_multi_allgatherv(mg, y_full, bounds)) || (rc = spmv_multi_sync(mg))) {
+            printf("SpMV + all-gather failed: %s\n", spmv_last_error());
+            return SPMV_PROGRAM_ERROR;
+        }
+        tall[i] = (now_s() - t0) * 1e3;
+    }
+    const double ag_ms = median_of(tag, o->reps), all_ms = median_of(tall, o->reps);
+
+    if (fmt == FMT_COO)
+        printf("GPU calculations\n"); /* reference coo.c:201 */
+    print_performance(spmv_ms, Z);
+    print_speed(spmv_ms, Z);
+    const double bytes_alg = 12.0 * (double)Z + 4.0 * (double)(N + 1) + 8.0 * (double)m->n_cols + 8.0 * (double)N;
+    printf("  [%s] %s | N=%lld M=%lld Z=%lld | %d GPUs, median of %d %s reps of the slowest GPU (min %.4f ms)\n",
+           fmt_name(fmt), m->label, (long long)N, (long long)m->n_cols, (long long)Z, G, o->reps,
+           o->warm ? "warm (cache-resident)" : "cold (512 MiB flush on every GPU)", t_min);
+    printf("  [%s] aggregate effective %.1f GB/s (bytes_alg %.1f MB) = %.1f%% of %d x %.0f GB/s HBM3E\n",
+           fmt_name(fmt), bytes_alg / spmv_ms * 1e-6, bytes_alg * 1e-6,
+           100.0 * bytes_alg / spmv_ms * 1e-6 / (HBM_PEAK_GBS * G), G, HBM_PEAK_GBS);
+    for (int g = 0; g < G; ++g)
+        printf("  [multi] GPU %d: rows [%lld, %lld) %lld entries, median %.4f ms\n", spmv_multi_device(mg, g),
+               (long long)bounds[g], (long long)bounds[g + 1], (long long)f[g].d.nnz,
+               median_of(tdev + (size_t)g * o->reps, o->reps));
+    printf("  [multi] y all-gather over RCCL (%d broadcasts of the real shard rows, %.1f MB per GPU received): "
+           "%.4f ms; SpMV + all-gather %.4f ms = %.1f GB/s aggregate\n",
+           G, 8e-6 * (double)N * (G - 1) / G, ag_ms, all_ms, bytes_alg / all_ms * 1e-6);
+
+    /* every GPU must now hold the same, complete y */
+    int same = 1;
+    double *yg = malloc((size_t)(N + 1) * sizeof(double));
+    for (int g = 0; g < G; ++g) {
+        spmv_set_device(spmv_multi_device(mg, g));
+        if (spmv_download(g == 0 ? y : yg, y_full[g], (size_t)N * 8, NULL) != SPMV_SUCCESS) {
+            printf("read back error: %s\n", spmv_last_error());
+            return SPMV_PROGRAM_ERROR;
+        }
+        if (g > 0 && memcmp(y, yg, (size_t)N * 8) != 0)
+            same = 0;
+    }
+    free(yg);
+    printf("  [multi] y identical on all %d GPUs: %s\n", G, same ? "yes" : "NO");
+    int ok = check_and_report(m, x, y, "") && same;
+    if (o->cpu) {
+        int threads = o->threads > 0 ? o->threads : spmv_cpu_threads();
+        double t0 = now_s();
+        for (int g = 0; g < G; ++g) /* each shard's loop into its rows: the same reassembly */
+            run_cpu(&f[g], x, y_cpu + bounds[g], threads);
+        double cms = (now_s() - t0) * 1e3;
+        printf("\nCPU calculations\n"); /* reference csr.c:306 */
+        print_performance(cms, Z);
+        printf("  [cpu] %d OpenMP threads, effective %.1f GB/s\n", threads, bytes_alg / cms * 1e-6);
+        ok &= check_and_report(m, x, y_cpu, "cpu ");
+    }
+    spmv_multi_free(mg);
+    return (o->strict && !ok) ? SPMV_OTHER_ERROR : SPMV_SUCCESS;
+}
+
 int spmv_driver_main(int argc, char **argv, spmv_format fmt)
 {
     setvbuf(stdout, NULL, _IOLBF, 0);
@@ -636,7 +816,7 @@ int spmv_driver_main(int argc, char **argv, spmv_format fmt)
         return SPMV_OTHER_ERROR;
 
     int ndev = 0;
-    if (spmv_device_count(&ndev) != SPMV_SUCCESS || ndev <= o.device) {
+    if (spmv_device_count(&ndev) != SPMV_SUCCESS || ndev <= o.device || ndev < o.gpus) {
         printf("No HIP GPU device found (%s)\n", spmv_last_error());
         return SPMV_DEVICE_ERROR; /* reference csr.c:25-28 */
     }
@@ -658,6 +838,8 @@ int spmv_driver_main(int argc, char **argv, spmv_format fmt)
         return SPMV_OTHER_ERROR;
     for (int64_t j = 0; j < m.n_cols; ++j)
         x[j] = (double)j; /* reference csr.c:95-99 */
+    if (o.gpus >= 1)
+        return run_multi(&o, fmt, &m, x, y, y_cpu);
 
     dev_fmt_t f;
     rc = build_format(&o, fmt, &m, &f);

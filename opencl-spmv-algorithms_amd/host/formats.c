@@ -740,6 +740,25 @@ int spmv_partition_rows_calibrated(int64_t n_rows, const int64_t *row_ptr, int p
     return SPMV_SUCCESS;
 }
 
+int64_t spmv_coo_row_shard(int64_t nnz, const int32_t *row, const int32_t *col, const double *val,
+                           int64_t lo, int64_t hi, int32_t *row_out, int32_t *col_out, double *val_out)
+{
+    if (nnz < 0 || lo < 0 || hi < lo || (nnz > 0 && (!row || !col || !val)) || hi - lo > INT32_MAX)
+        return -1;
+    int64_t k = 0;
+    for (int64_t e = 0; e < nnz; ++e) {
+        if (row[e] < lo || row[e] >= hi)
+            continue;
+        if (row_out) {
+            row_out[k] = (int32_t)(row[e] - lo);
+            col_out[k] = col[e];
+            val_out[k] = val[e];
+        }
+        ++k;
+    }
+    return k;
+}
+
 int spmv_partition_rows(int64_t n_rows, const int64_t *row_ptr, int parts,
                         int64_t align, int64_t *bounds)
 {

@@ -165,6 +165,14 @@ HIP_SYMBOLS = {
     "spmv_flush_cache": (ctypes.c_int, [_vp, ctypes.c_size_t]),
     "spmv_time_launch": (ctypes.c_int, [_vp, _vp, _vp, ctypes.POINTER(ctypes.c_double)]),
     "spmv_release": (ctypes.c_int, []),
+    "spmv_multi_init": (ctypes.c_int, [ctypes.c_int, _vp, _vp]),
+    "spmv_multi_free": (ctypes.c_int, [_vp]),
+    "spmv_multi_size": (ctypes.c_int, [_vp]),
+    "spmv_multi_device": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "spmv_multi_stream": (_vp, [_vp, ctypes.c_int]),
+    "spmv_multi_allgatherv": (ctypes.c_int, [_vp, _vp, _vp]),
+    "spmv_multi_sync": (ctypes.c_int, [_vp]),
+    "spmv_multi_time": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int, _vp]),
     "spmv_strerror": (ctypes.c_char_p, [ctypes.c_int]),
     "spmv_last_error": (ctypes.c_char_p, []),
     "spmv_version": (ctypes.c_char_p, []),
@@ -191,6 +199,7 @@ HOST_SYMBOLS = {
     "spmv_sell_split_auto": (_c_i32, [_c_i64, _vp, _c_i32, _c_i32]),
     "spmv_sell_split_plan": (_c_i64, [_c_i64, _vp, _c_i32, _c_i32, _vp, _vp]),
     "spmv_partition_rows": (ctypes.c_int, [_c_i64, _vp, ctypes.c_int, _c_i64, _vp]),
+    "spmv_coo_row_shard": (_c_i64, [_c_i64, _vp, _vp, _vp, _c_i64, _c_i64, _vp, _vp, _vp]),
     "spmv_partition_rows_weighted": (ctypes.c_int, [_c_i64, _vp, ctypes.c_int, _c_i64, ctypes.c_double, _vp]),
     "spmv_partition_rows_calibrated": (ctypes.c_int, [_c_i64, _vp, ctypes.c_int, _c_i64, ctypes.c_double, ctypes.c_int,
                                                       _vp, _vp, _vp]),

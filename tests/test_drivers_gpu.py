@@ -107,3 +107,23 @@ def test_xwin_and_global_paths_agree(prog):
                 "--no-cpu", *extra)
         assert r.returncode == 0, r.stdout + r.stderr
         assert "\nresult is ok\n" in "\n" + r.stdout
+
+
+@pytest.mark.parametrize("prog", ["csr", "sigma_c", "coo", "cmrs", "ell"])
+def test_program_gpus_flag_rccl_path(prog):
+    """--gpus 1: the single-process multi-GPU path (RCCL communicator over
+    the devices, row shards, y completed by grouped RCCL broadcasts of the
+    real shard sizes) on the box's one GPU; the check is the same."""
+    r = run(prog, "--gen", "cantlike", "--gpus", "1", "--reps", "3", "--warmup", "1", "--strict", "--cpu")
+    assert r.returncode == 0, r.stdout + r.stderr
+    out = r.stdout
+    assert re.search(r"^Your calculations took [0-9.]+ ms to run\.$", out, re.M)
+    assert "\nresult is ok\n" in "\n" + out and "\ncpu result is ok\n" in out
+    assert "[multi] y identical on all 1 GPUs: yes" in out
+    assert re.search(r"\[multi\] y all-gather over RCCL .*: [0-9.]+ ms; SpMV \+ all-gather [0-9.]+ ms", out)
+
+
+def test_program_gpus_flag_more_gpus_than_present():
+    """Asking for more GPUs than the node has is the reference's device error (1)."""
+    r = run("csr", "--gen", "cantlike", "--gpus", "64", "--reps", "1")
+    assert r.returncode == 1, r.stdout + r.stderr

@@ -474,3 +474,51 @@ def test_partition_calibrated_bad_input():
         sa.partition_rows_calibrated(n, ptr, 4, np.array([0, 5000, n - 1]), [1.0, 1.0])  # does not end at n
     with pytest.raises(sa.SpmvError):
         sa.partition_rows_calibrated(n, ptr, 4, np.array([0, 5000, n]), [1.0, -1.0])
+
+
+@pytest.mark.parametrize("parts", [1, 2, 3, 5, 8])
+@pytest.mark.parametrize("kind", ["ragged", "empty_rows", "rmat"])
+def test_row_shards_reassemble(parts, kind):
+    """The drivers' --gpus N path on the host: spmv_partition_rows cuts the
+    rows, spmv_coo_row_shard hands each shard its entries in file order with
+    local row ids, each shard's CSR loop writes y[lo:hi] — the concatenation
+    is bit-identical to the unsharded loop (rows never straddle shards),
+    every entry lands in exactly one shard."""
+    L = sa.host_lib()
+    if kind == "ragged":
+        m = sa.gen_random(3001, 2500, 0, 90, seed=4)
+    elif kind == "empty_rows":
+        m = sa.read_mtx(GOLDEN / "empty_rows.mtx")
+    else:
+        m = sa.gen_rmat(20_000, 200_000, scale=15, seed=3)
+    x = np.random.default_rng(5).uniform(-1, 1, m.n_cols)
+    ptr, col, val = sa.csr_from_coo(m)
+    full = np.empty(m.n_rows)
+    assert L.spmv_cpu_csr(m.n_rows, sa._ptr(ptr), sa._ptr(col), sa._ptr(val), sa._ptr(x), sa._ptr(full), 1) == 0
+    bounds = np.empty(parts + 1, np.int64)
+    assert L.spmv_partition_rows(m.n_rows, sa._ptr(ptr), parts, 1024, sa._ptr(bounds)) == 0
+    y = np.full(m.n_rows, np.nan)
+    total = 0
+    for g in range(parts):
+        lo, hi = int(bounds[g]), int(bounds[g + 1])
+        n = L.spmv_coo_row_shard(m.nnz, sa._ptr(m.row), sa._ptr(m.col), sa._ptr(m.val), lo, hi, None, None, None)
+        r, c, v = np.empty(max(n, 1), np.int32), np.empty(max(n, 1), np.int32), np.empty(max(n, 1))
+        assert L.spmv_coo_row_shard(m.nnz, sa._ptr(m.row), sa._ptr(m.col), sa._ptr(m.val), lo, hi, sa._ptr(r),
+                                    sa._ptr(c), sa._ptr(v)) == n
+        total += n
+        keep = (m.row >= lo) & (m.row < hi)  # file order kept
+        assert np.array_equal(r[:n], m.row[keep] - lo) and np.array_equal(c[:n], m.col[keep])
+        s = sa.Coo(hi - lo, m.n_cols, r[:n], c[:n], v[:n])
+        sp, sc, sv = sa.csr_from_coo(s)
+        if hi > lo:
+            assert L.spmv_cpu_csr(hi - lo, sa._ptr(sp), sa._ptr(sc), sa._ptr(sv), sa._ptr(x),
+                                  sa._ptr(y[lo:hi]), 1) == 0
+    assert total == m.nnz
+    assert np.array_equal(y.view(np.int64), full.view(np.int64))
+
+
+def test_row_shard_bad_arguments():
+    L = sa.host_lib()
+    assert L.spmv_coo_row_shard(-1, None, None, None, 0, 1, None, None, None) == -1
+    assert L.spmv_coo_row_shard(0, None, None, None, 5, 3, None, None, None) == -1
+    assert L.spmv_coo_row_shard(0, None, None, None, 0, 0, None, None, None) == 0

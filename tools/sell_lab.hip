@@ -6,6 +6,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace {
 
 constexpr int kWave = 64;
@@ -125,6 +127,105 @@ __global__ __launch_bounds__(kWave * S) void lab_kernel(const int64_t *__restric
     }
 }
 
+// One-shot variant: a workgroup of S waves per slice, every lane's first G
+// slot groups loaded (predicated, branch-free) BEFORE the x-window copy, so
+// the matrix stream and the window copy are in flight together; the rest
+// (per > G) in batches of G after the barrier.
+template <int KI, int S, int G>
+__global__ __launch_bounds__(kWave * S) void lab2_kernel(const int64_t *__restrict__ slice_ptr,
+                                                         const int32_t *__restrict__ perm,
+                                                         const int32_t *__restrict__ col,
+                                                         const double *__restrict__ val,
+                                                         const double *__restrict__ x, double *__restrict__ y,
+                                                         const int2 *__restrict__ win, int32_t xcap,
+                                                         uint64_t *__restrict__ stamps)
+{
+    const uint64_t t0 = now();
+    extern __shared__ double s_x[];
+    const int64_t s = blockIdx.x;
+    const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+    const int64_t base = slice_ptr[s];
+    const int64_t w = (slice_ptr[s + 1] - base) / kWave;
+    const int2 wd = win[s];
+    const int64_t groups = w / KI;
+    const int64_t per = (groups + S - 1) / S;
+    const int64_t g0 = wv * per;
+    const int64_t g1 = g0 + per < groups ? g0 + per : groups;
+    const int64_t step = (int64_t)kWave * KI;
+    const double *vp = val + base + lane * KI;
+    const int32_t *cp = col + base + lane * KI;
+    typedef typename std::conditional<KI == 1, double, v2f64>::type VT;
+    typedef typename std::conditional<KI == 1, int32_t, v2i32>::type CT;
+    VT v[G];
+    CT c[G];
+    const bool any = g1 > g0;  // uniform per wave
+    if (any) {
+#pragma unroll
+        for (int u = 0; u < G; ++u) {
+            const int64_t gg = g0 + u < g1 ? g0 + u : g0;
+            v[u] = __builtin_nontemporal_load(reinterpret_cast<const VT *>(vp + gg * step));
+            c[u] = __builtin_nontemporal_load(reinterpret_cast<const CT *>(cp + gg * step));
+        }
+    }
+    const int32_t span = wd.y - wd.x + 1;
+    const bool staged = span > 0 && span <= xcap;
+    if (staged) {
+        constexpr int T = kWave * S, CU = 8;
+        for (int32_t b0 = 0; b0 < span; b0 += CU * T) {
+            double t[CU];
+#pragma unroll
+            for (int k = 0; k < CU; ++k) {
+                const int32_t i = b0 + threadIdx.x + k * T;
+                t[k] = x[wd.x + (i < span ? i : span - 1)];
+            }
+#pragma unroll
+            for (int k = 0; k < CU; ++k) {
+                const int32_t i = b0 + threadIdx.x + k * T;
+                if (i < span)
+                    s_x[i] = t[k];
+            }
+        }
+    }
+    const int32_t row = wv == 0 ? perm[s * kWave + lane] : -1;
+    __syncthreads();
+    double a[4] = {0.0, 0.0, 0.0, 0.0};
+    auto body = [&](auto xs) {
+        if (any) {
+#pragma unroll
+            for (int u = 0; u < G; ++u) {
+                const bool in = g0 + u < g1;
+                if constexpr (KI == 1)
+                    a[u % 4] += (in ? v[u] : 0.0) * xs(c[u]);
+                else
+                    a[u % 4] += (in ? v[u].x : 0.0) * xs(c[u].x) + (in ? v[u].y : 0.0) * xs(c[u].y);
+            }
+        }
+        if (g0 + G < g1)
+            slots<KI, 4>(vp, cp, g0 + G, g1, step, xs, a);
+    };
+    if (staged)
+        body(XW{s_x, wd.x});
+    else
+        body(XG{x});
+    double sum = (a[0] + a[2]) + (a[1] + a[3]);
+    __shared__ double part[S][kWave];
+    if constexpr (S > 1) {
+        part[wv][lane] = sum;
+        __syncthreads();
+        if (wv == 0)
+            for (int k = 1; k < S; ++k)
+                sum += part[k][lane];
+    }
+    if (row >= 0)
+        y[row] = sum;
+    if (lane == 0) {
+        const int64_t i = (s * S + wv) * 3;
+        stamps[i] = t0;
+        stamps[i + 1] = now();
+        stamps[i + 2] = hw_id();
+    }
+}
+
 // column window of every slice: [min, max] of its stored columns
 __global__ void lab_window_kernel(const int64_t *__restrict__ slice_ptr, const int32_t *__restrict__ col,
                                   int2 *__restrict__ win)
@@ -179,6 +280,14 @@ int lab_run(int code, int xw, int64_t n_slices, const int64_t *sp, const int32_t
     switch (code) {
         LAB(1, 1, 4) LAB(1, 1, 8) LAB(1, 2, 4) LAB(1, 4, 4) LAB(1, 4, 8) LAB(1, 8, 4) LAB(1, 8, 8)
         LAB(1, 16, 4) LAB(2, 1, 4) LAB(2, 2, 4) LAB(2, 4, 4) LAB(2, 4, 8) LAB(2, 8, 4) LAB(2, 16, 4)
+#define LAB2(KI, S, G)                                                                                    \
+    case 100000 + KI * 10000 + S * 100 + G:                                                               \
+        hipLaunchKernelGGL((lab2_kernel<KI, S, G>), dim3((unsigned)n_slices), dim3(kWave * S),             \
+                           (size_t)xcap * sizeof(double), s, sp, perm, col, val, x, y, w, xcap, stamps);     \
+        break;
+        LAB2(1, 4, 16) LAB2(1, 4, 24) LAB2(1, 8, 12) LAB2(1, 2, 24) LAB2(2, 4, 8) LAB2(2, 4, 12) LAB2(2, 2, 12)
+        LAB2(2, 2, 16) LAB2(2, 1, 16) LAB2(2, 8, 6)
+#undef LAB2
     default: return (int)hipErrorInvalidValue;
     }
 #undef LAB

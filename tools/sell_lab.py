@@ -24,7 +24,7 @@ from cant_single import FLUSH_BYTES, probe_lib  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--codes", default="1014,1084,1088,2014,2044,2084,2044x,2084x,1084x,2024x,2164x")
+    ap.add_argument("--codes", default="1084x,2044x,110416,110424,110812,110224,120408,120412,120212,120216,120116,120806")
     ap.add_argument("--reps", type=int, default=20)
     a = ap.parse_args()
     import torch
@@ -57,7 +57,10 @@ def main():
     for code in a.codes.split(","):
         xw = code.endswith("x")
         c = int(code.rstrip("x"))
-        ki, S, U = c // 1000, (c % 1000) // 10, c % 10
+        if c >= 100000:  # one-shot variant: 1KSSGG
+            ki, S, U = (c // 10000) % 10, (c // 100) % 100, c % 100
+        else:
+            ki, S, U = c // 1000, (c % 1000) // 10, c % 10
         dm, n, win, xcap = mats[ki]
         A = dm.arrays
         stamps = torch.zeros(n * S * 3, dtype=torch.int64, device=dev)

@@ -6,21 +6,28 @@ format on cant.mtx.  The real cant.mtx is a Git-LFS pointer in the
 reference, so the matrix is the cant-like stand-in
 (spmv_gen_cantlike: N = 62,451, Z = 4,007,383, the real cant's counts).
 
-Step = ONE SpMV launch over a batch of B independent cant-like matrices
-stacked block-diagonally (default B = 32: 1.58 GB of CSR, 6x the 256 MiB
-Infinity Cache, so the stream comes from HBM, not from the cache), all
-arrays resident in HBM before timing starts.  Default format: CSR-vector
-(BASELINE.json configs[1]).  At N=1 the other four formats are measured on
-the same batch too (`per_format`), plus a single cant-like copy cold
-(512 MiB flush before every launch) and warm (`cant_single`).
+Headline step = ONE SpMV launch over a batch of B = 32 independent
+cant-like matrices stacked block-diagonally (the configs[1] matrix,
+CSR-vector, batched): 1.58 GB of CSR, 6x the 256 MiB Infinity Cache, so
+the matrix streams from HBM; all arrays resident in HBM before timing
+starts.  ONE cant-like matrix is 49 MB and sits in the Infinity Cache after
+one pass, so its figures are reported beside the headline, not as it
+(`cant_single`): every format on the single matrix, cold (512 MiB flush
+first) and warm, timed from a rocprofv3 kernel trace (tools/cant_single.py,
+run as a child process before this process touches the GPU), next to the
+pure-stream ceiling of the same 49 MB.  At N=1 every format is also
+measured on the batch (`per_format`).
 
-Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): rows are
-sharded — rank r owns copies [r·B, (r+1)·B) of an N·B-copy matrix (weak
-scaling, no collective in the timed step).  The y all-gather over RCCL that
-concatenates the shards is timed separately (`allgather`).
+Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): rank r
+owns copies [r·B, (r+1)·B) of an N·B-copy matrix (weak scaling, no
+collective in the timed step).  `rmat_strong` (configs[3]) and
+`banded_strong` (configs[4]) cut ONE matrix into N row shards (strong
+scaling, x replicated) and report SpMV-only, the y all-gather of the real
+shard sizes over RCCL (an allgatherv), SpMV + all-gather, and cold shards
+(512 MiB flush before each step).
 
 value = algorithmic bytes of all ranks / (max over ranks of the wall time
-of K steps / K).  bytes_alg = 12·Z + 4·(N+1) + 8·M + 8·N per copy
+of K steps / K).  bytes_alg = 12·Z + 4·(N+1) + 8·M + 8·N per matrix
 (SURVEY.md §8d): values, columns, row offsets, x and y once each.
 roofline.achieved uses the same bytes over the kernel's mean duration from
 HIP events recorded on the launch stream; roofline.traffic comes from the
@@ -31,7 +38,10 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import shutil
+import subprocess
 import sys
+import tempfile
 import time
 from pathlib import Path
 
@@ -40,16 +50,22 @@ import numpy as np
 REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO / "opencl-spmv-algorithms_amd"))
 sys.path.insert(0, str(REPO))
+sys.path.insert(0, str(REPO / "tools"))
 
+import iterate  # noqa: E402
 import spmv_amd as sa  # noqa: E402
 
 METRIC = "effective HBM GB/s + GFLOP/s per format on cant.mtx, 1/2/4/8 MI355X"
 # R-MAT shards balance entries + RMAT_ROW_WEIGHT * rows: with 512-entry
 # tiles the slowest of 8 shards took 0.1421 / 0.1411 / 0.1464 / 0.1549 ms
-# with weights 1 / 2 / 3 / 4 (profiles/round2/shard_rehearse_tiled_w.log;
-# round 1, 1536-entry tiles: 4 was best)
+# with weights 1 / 2 / 3 / 4 (profiles/round2/shard_rehearse_tiled_w.log)
 RMAT_ROW_WEIGHT = 2.0
 CSR_DEFAULT_VARIANT = 3  # spmv_csr_run_variant's default (csrc/csr.hip)
+# untimed replays of a freshly captured graph before the timed replay, at
+# least this much GPU time: the first replays of a new graph ran ~4 % slower
+# than later ones (headline 0.2659 vs per-format 0.2557 ms
+# for the same kernel in the same process)
+WARM_REPLAY_MS = 100.0
 
 
 def parse():
@@ -64,6 +80,9 @@ def parse():
     p.add_argument("--banded-rows", type=int, default=100_000_000)
     p.add_argument("--per-format", default="auto", choices=["auto", "yes", "no"],
                    help="also measure the other formats (default: at N=1 only)")
+    p.add_argument("--single", default="auto", choices=["auto", "yes", "no"],
+                   help="cant_single: ONE cant-like matrix, every format, cold and warm, from a rocprofv3 "
+                        "kernel trace of a child process (default: at N=1 with the cant-like workload)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0: skip)")
     p.add_argument("--lanes", type=int, default=0)
     p.add_argument("--variant", type=int, default=0, help="CSR kernel variant (0 auto, 1 direct, 2 staged)")
@@ -82,6 +101,8 @@ def parse():
     p.add_argument("--banded-strong", default="auto", choices=["auto", "yes", "no"],
                    help="also time CSR and SELL on the banded 1e8-row / 1.6e9-entry matrix row-sharded over all "
                         "ranks (configs[4], generated on device; auto: with the default cant-like workload)")
+    p.add_argument("--flush", default="yes", choices=["yes", "no"],
+                   help="strong-scaling legs: also time every shard cold (512 MiB flush before each step)")
     p.add_argument("--graph", default="yes", choices=["yes", "no"],
                    help="replay the timed launches from one HIP graph (yes) or launch them eagerly")
     return p.parse_args()
@@ -125,15 +146,15 @@ def fmt_kwargs(args, fmt):
 GRAPH = {"on": True}  # --graph: the timed launches replayed from one HIP graph
 
 
-def capture(torch, dm, x, y, steps):
-    """`steps` launches of one SpMV captured into a HIP graph (None if the
-    capture fails: then the launches are timed eagerly)."""
+def capture(torch, fn, steps):
+    """`steps` calls of fn() captured into one HIP graph (None if the capture
+    fails: then the launches are timed eagerly)."""
     try:
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             for _ in range(steps):
-                dm.run(x, y)
+                fn()
         torch.cuda.synchronize()
         return g
     except Exception as e:  # noqa: BLE001 — fall back to eager launches, say so
@@ -141,22 +162,35 @@ def capture(torch, dm, x, y, steps):
         return None
 
 
+def warm_replays(torch, g, steps, est_ms):
+    """Untimed replays of a fresh graph: at least WARM_REPLAY_MS of GPU work
+    (est_ms = one launch's time from the eager warm-up), at most 50."""
+    n = int(np.ceil(WARM_REPLAY_MS / max(est_ms * steps, 1e-3)))
+    for _ in range(min(max(n, 1), 50)):
+        g.replay()
+    torch.cuda.synchronize()
+
+
 def time_steps(torch, dm, x, y, steps, warmup, dist=None):
     """W warm-up launches, then exactly `steps` launches bracketed by a
     barrier + synchronize.  Default: the `steps` launches are captured into
-    one HIP graph and replayed once (one SpMV kernel per step, as eager; the
-    graph removes the host launch path between them: 0.2473 vs 0.2537 ms per
-    step, profiles/round2/ab_graph.log), timed by two HIP events on the
-    launch stream, so the per-launch time is the span / steps.  --graph no:
-    eager launches with one HIP event after each."""
+    one HIP graph (one SpMV kernel per step, as eager; the graph removes the
+    host launch path between them: 0.2473 vs 0.2537 ms per step,
+    profiles/round2/ab_graph.log), replayed untimed for >= WARM_REPLAY_MS,
+    then replayed once between two HIP events on the launch stream: the
+    per-launch time is the span / steps.  --graph no: eager launches with
+    one HIP event after each."""
     stream = torch.cuda.current_stream()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
     for _ in range(warmup):
         dm.run(x, y, stream)
-    g = capture(torch, dm, x, y, steps) if GRAPH["on"] else None
+    torch.cuda.synchronize()
+    est_ms = (time.perf_counter() - t0) * 1e3 / max(warmup, 1)
+    g = capture(torch, lambda: dm.run(x, y), steps) if GRAPH["on"] else None
     if g is not None:
-        g.replay()  # first replay (uploads the graph), untimed
+        warm_replays(torch, g, steps, est_ms)
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
@@ -193,21 +227,29 @@ def time_steps(torch, dm, x, y, steps, warmup, dist=None):
     return wall, kern
 
 
-def cold_single(torch, dm, x, y, reps=30):
-    """Single-matrix launch after a 512 MiB flush (cold) and back-to-back (warm)."""
+def cold_step_ms(torch, dm, x, y, steps):
+    """Mean time of an SpMV that starts from cold caches: one graph of
+    `steps` x (512 MiB flush + SpMV) minus one graph of `steps` flushes, each
+    replayed once untimed and once between HIP events on the stream (the
+    flush is ~80 us; the difference of the two spans is the SpMV's)."""
     stream = torch.cuda.current_stream()
-    cold = []
-    for _ in range(reps):
-        sa.flush_cache(stream)
-        a = torch.cuda.Event(enable_timing=True)
-        b = torch.cuda.Event(enable_timing=True)
+    sa.flush_cache(stream)  # allocates the scratch outside the capture
+    torch.cuda.synchronize()
+    spans = {}
+    for key, fn in (("both", lambda: (sa.flush_cache(), dm.run(x, y))), ("flush", lambda: sa.flush_cache())):
+        g = capture(torch, fn, steps)
+        if g is None:
+            return None
+        g.replay()
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(stream)
-        dm.run(x, y, stream)
+        g.replay()
         b.record(stream)
         torch.cuda.synchronize()
-        cold.append(a.elapsed_time(b))
-    _, warm = time_steps(torch, dm, x, y, reps, 3)
-    return float(np.median(cold)), float(np.median(warm))
+        spans[key] = a.elapsed_time(b)
+        del g
+    return (spans["both"] - spans["flush"]) / steps
 
 
 def traffic_for(fmt, workload_bytes, kernel=None):
@@ -229,6 +271,69 @@ def traffic_for(fmt, workload_bytes, kernel=None):
     return None
 
 
+def all_ok(dist, cdev, torch, ok: bool, what: str, rank: int):
+    """Parity gate shared by all ranks: the failure flags are all-reduced
+    first, so every rank exits non-zero together instead of the healthy ones
+    blocking in the next collective."""
+    if dist is not None:
+        t = torch.tensor([0.0 if ok else 1.0], dtype=torch.float64, device=cdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        if float(t.item()) != 0.0:
+            where = "this rank" if not ok else "another rank"
+            raise SystemExit(f"rank {rank}: parity failure on {where} ({what})")
+    elif not ok:
+        raise SystemExit(f"parity failure ({what})")
+
+
+def banded_bounds(n, world):
+    """Equal 1024-aligned row ranges of the banded matrix."""
+    step = (n // world + 1023) // 1024 * 1024
+    return [min(r * step, n) for r in range(world)] + [n]
+
+
+def banded_sample_rows(n, lo, hi):
+    """Rows of shard [lo, hi) checked at full size: the first and last 512,
+    128 around every 2-, 4- and 8-way cut point, 4096 spread evenly, and
+    rows whose CSR entries lie past 2^31 and 2^32 bytes of values (entry
+    2^28 = row 2^24 onward: the int64-offset path)."""
+    cand = [np.arange(lo, min(lo + 512, hi)), np.arange(max(hi - 512, lo), hi),
+            np.linspace(lo, hi - 1, 4096).astype(np.int64)]
+    for parts in (2, 4, 8):
+        for cut in banded_bounds(n, parts)[1:-1]:
+            cand.append(np.arange(max(cut - 64, lo), min(cut + 64, hi)))
+    for r0 in (1 << 24, 1 << 25, 3 << 24, 1 << 26):  # value bytes 2^31, 2^32, 3*2^31, 2^33
+        cand.append(np.arange(max(r0 - 32, lo), min(r0 + 32, hi)))
+    cand = [c for c in cand if c.size]
+    rows = np.unique(np.concatenate(cand)) if cand else np.zeros(0, np.int64)
+    return rows[(rows >= lo) & (rows < hi)]
+
+
+def banded_check(n, lo, hi, y_shard):
+    """Full-range banded parity with x[j] = j (a wrong column index changes
+    y, unlike with x = 1): every sampled row (banded_sample_rows) recomputed
+    from the host generator in file order (the check_result rule, reference
+    csr.c:225-233), relative 1e-6 of sum |a_ij x_j|.  Returns (rows checked,
+    first bad rows or None)."""
+    rows = banded_sample_rows(n, lo, hi)
+    if rows.size == 0:
+        return 0, None
+    got = y_shard.cpu().numpy()[rows - lo]
+    runs = np.split(rows, np.nonzero(np.diff(rows) != 1)[0] + 1)
+    bad, k = [], 0
+    for run in runs:
+        _, c, v = sa.gen_banded_csr(n, int(run[0]), int(run[-1]) + 1)
+        c, v = c.reshape(-1, 16), v.reshape(-1, 16)
+        xv = c.astype(np.float64)  # x[j] = j
+        ref = np.zeros(run.size)
+        for e in range(16):  # file order
+            ref = ref + v[:, e] * xv[:, e]
+        scale = np.sum(np.abs(v * xv), axis=1)
+        err = np.abs(got[k:k + run.size] - ref) > 1e-6 * scale
+        bad.extend(run[err].tolist())
+        k += run.size
+    return int(rows.size), (bad[:5] if bad else None)
+
+
 def build_workload(args, torch, dev, rank, world):
     """This rank's share of the workload, resident in HBM.
 
@@ -248,19 +353,19 @@ def build_workload(args, torch, dev, rank, world):
         y = torch.empty(m.n_rows, dtype=torch.float64, device=dev)
         dm = sa.to_device(m, args.format, dev, **fk)
         b = sa.bytes_alg(m.n_rows, m.n_cols, m.nnz)
-        single = sa.gen_cantlike(0, 1)
 
-        def check():
-            bad, first = sa.check(single, x[:single.n_cols].cpu().numpy(), y[:single.n_rows].cpu().numpy())
+        def check():  # the whole batch, all B copies (host check_result rule)
+            bad, first = sa.check(m, x.cpu().numpy(), y.cpu().numpy())
             return f"row {first}" if bad else None
 
         return dict(dm=dm, x=x, y=y, m=m, rows=m.n_rows, nnz=m.nnz, bytes_rank=b, bytes_total=b * world,
-                    nnz_total=m.nnz * world, max_rows=m.n_rows, check=check, scaling="weak",
+                    nnz_total=m.nnz * world, check=check, scaling="weak",
                     data="synthetic: cant-like stand-in (62,451 rows, 4,007,383 entries = SuiteSparse cant's "
                          "counts; the reference's cant.mtx is an unfetched Git-LFS pointer), x[j] = j",
-                    config={"workload": f"{args.format} SpMV on a block-diagonal batch of {B} cant-like copies "
-                                        "per GPU (BASELINE.json configs[1]"
-                                        + (")" if args.format == "csr" else "-style)"),
+                    config={"workload": f"{args.format} SpMV over a batch: {B} independent cant-like matrices "
+                                        "(BASELINE.json configs[1]'s matrix) per GPU stacked block-diagonally, "
+                                        "one launch per step, 1.58 GB per GPU streamed from HBM; the single "
+                                        "49 MB matrix (Infinity-Cache resident when warm) is cant_single",
                             "copies_per_gpu": B})
     if args.workload == "rmat":
         full = sa.gen_rmat()  # deterministic: every rank builds the same matrix
@@ -275,7 +380,6 @@ def build_workload(args, torch, dev, rank, world):
         y = torch.empty(max(loc.n_rows, 1), dtype=torch.float64, device=dev)
         dm = sa.to_device(loc, args.format, dev, **fk)
         n, z = 10_000_000, 100_000_000
-        max_rows = int(np.max(np.diff(bounds)))
 
         def check():
             bad, first = sa.check(loc, sa.ramp_x(loc.n_cols), y[:loc.n_rows].cpu().numpy())
@@ -283,36 +387,31 @@ def build_workload(args, torch, dev, rank, world):
 
         return dict(dm=dm, x=x, y=y, loc=loc, rows=loc.n_rows, nnz=loc.nnz,
                     bytes_rank=sa.bytes_alg(loc.n_rows, loc.n_cols, loc.nnz), bytes_total=sa.bytes_alg(n, n, z),
-                    nnz_total=z, max_rows=max_rows, check=check, scaling="strong",
+                    nnz_total=z, check=check, scaling="strong",
                     data="synthetic: R-MAT (a,b,c,d)=(.57,.19,.19,.05), 1e7 rows, 1e8 entries, seed 1, x[j] = j",
                     config={"workload": f"{args.format} SpMV on R-MAT 1e7/1e8 row-sharded over {world} GPU(s) "
                                         "(BASELINE.json configs[3])"})
     # banded
     n = args.banded_rows
-    step = (n // world + 1023) // 1024 * 1024
-    lo, hi = min(rank * step, n), min((rank + 1) * step, n)
-    ksell = {k: v for k, v in fk.items() if k in ("C", "sigma", "ki")}
+    lo, hi = banded_bounds(n, world)[rank:rank + 2]
     if args.format == "sell":
-        ksell["ki"] = ksell.get("ki") or 1
-        dm = sa.banded_to_device(n, "sell", dev, lo, hi, **ksell)
+        dm = sa.banded_to_device(n, "sell", dev, lo, hi, C=args.C, sigma=1024, ki=args.ki or 1)
     elif args.format == "csr":
         dm = sa.banded_to_device(n, "csr", dev, lo, hi, lanes=args.lanes, variant=args.variant)
     else:
         raise SystemExit("--workload banded supports --format csr or sell")
-    x = torch.ones(n, dtype=torch.float64, device=dev)
+    x = torch.from_numpy(sa.ramp_x(n)).to(dev)
     y = torch.empty(max(hi - lo, 1), dtype=torch.float64, device=dev)
 
-    def check():  # x = 1: y_i is the sum of row i's 16 values (host generator)
-        k = min(hi - lo, 4096)
-        _, _, v = sa.gen_banded_csr(n, lo, lo + k)
-        ok = np.allclose(y[:k].cpu().numpy(), v.reshape(-1, 16).sum(axis=1), rtol=1e-12, atol=1e-12)
-        return None if ok else "banded row sums"
+    def check():
+        k, bad = banded_check(n, lo, hi, y)
+        return f"banded rows {bad} ({k} rows sampled)" if bad else None
 
-    return dict(dm=dm, x=x, y=y, rows=hi - lo, nnz=16 * (hi - lo),
+    return dict(dm=dm, x=x, y=y, rows=hi - lo, nnz=16 * (hi - lo), lo=lo, hi=hi, bounds=banded_bounds(n, world),
                 bytes_rank=sa.bytes_alg(hi - lo, n, 16 * (hi - lo)) - 8 * n + 8 * (hi - lo),
-                bytes_total=sa.bytes_alg(n, n, 16 * n), nnz_total=16 * n, max_rows=step, check=check,
-                scaling="strong",
-                data=f"synthetic: banded, {n} rows x 16 entries at offsets -8..7 (mod n), generated on device, x = 1",
+                bytes_total=sa.bytes_alg(n, n, 16 * n), nnz_total=16 * n, check=check, scaling="strong",
+                data=f"synthetic: banded, {n} rows x 16 entries at offsets -8..7 (mod n), generated on device, "
+                     "x[j] = j",
                 config={"workload": f"{args.format} SpMV on the banded {n}-row / {16 * n}-entry matrix "
                                     f"row-sharded over {world} GPU(s) (BASELINE.json configs[4])"})
 
@@ -346,6 +445,87 @@ def cpu_baseline(m_single_csr, copies, budget_s):
             "gflops": round(2 * B * int(ptr[-1]) / t * 1e-9, 2)}
 
 
+def cant_single_rocprof():
+    """tools/cant_single.py under `rocprofv3 --kernel-trace` as a child
+    process, run before this process touches the GPU: every format on ONE
+    cant-like matrix, cold and warm, kernel durations from the trace, beside
+    the stream ceiling of the same bytes.  Without rocprofv3 (or if the
+    profiled run fails) the child runs unprofiled and its HIP-event figures
+    are reported, labelled so."""
+    tool = REPO / "tools" / "cant_single.py"
+    rocprof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    with tempfile.TemporaryDirectory(prefix="cant_single_") as tmp:
+        out = Path(tmp) / "cant_single.json"
+        plain = [sys.executable, str(tool), "--json", str(out)]
+        traced = Path(rocprof).exists()
+        cmd = ([rocprof, "--kernel-trace", "--output-format", "csv", "-d", tmp, "-o", "run", "--"] + plain
+               if traced else plain)
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=420, cwd=str(REPO))
+            if traced and (r.returncode != 0 or not out.exists()):
+                traced = False
+                r = subprocess.run(plain, capture_output=True, text=True, timeout=300, cwd=str(REPO))
+        except subprocess.TimeoutExpired:
+            return {"error": "cant_single timed out"}
+        if r.returncode != 0 or not out.exists():
+            return {"error": f"cant_single failed (rc {r.returncode}): {r.stderr[-400:]}"}
+        res = json.loads(out.read_text())
+        if traced:
+            from cant_single import attach_trace
+
+            attach_trace(res, tmp)
+        else:
+            res["timing"] = "HIP events around each launch (no rocprofv3 trace): includes event overhead"
+    res.pop("phases", None)
+    return res
+
+
+def strong_exchange(torch, comm, cdev, dm, x, y_full, lo, hi, bounds, steps, flush):
+    """The exchange step of a row-sharded SpMV: y all-gathered with the REAL
+    shard sizes (iterate.Comm.allgatherv), timed alone and after the SpMV,
+    per step, max over ranks; with `flush` also the shard's cold SpMV time
+    (cold_step_ms), all ranks' values gathered.  y_full holds this rank's
+    rows [lo, hi); the all-gather fills the rest in place."""
+    dist = comm.dist
+    yv = y_full[lo:hi]
+
+    def spmv():
+        if hi > lo:
+            dm.run(x, yv)
+
+    how = comm.allgatherv(y_full, bounds)
+
+    def timed(fn, k):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            fn()
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        return (time.perf_counter() - t0) * 1e3 / k
+
+    ag_ms = timed(lambda: comm.allgatherv(y_full, bounds), steps)
+    both_ms = timed(lambda: (spmv(), comm.allgatherv(y_full, bounds)), steps)
+    t = torch.tensor([ag_ms, both_ms], dtype=torch.float64, device=cdev)
+    cold = None
+    if flush:
+        c = cold_step_ms(torch, dm, x, yv, max(5, steps // 2)) if hi > lo else 0.0
+        cold = [c if c is not None else -1.0]
+        if dist is not None:
+            g = [torch.zeros(1, dtype=torch.float64, device=cdev) for _ in range(comm.world)]
+            dist.all_gather(g, torch.tensor(cold, dtype=torch.float64, device=cdev))
+            cold = [float(v.item()) for v in g]
+    if dist is not None:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return how, float(t[0].item()), float(t[1].item()), cold
+
+
 def rmat_strong(args, torch, dev, rank, world, dist, cdev):
     """North-star sweep (BASELINE.json north_star, configs[3]): CSR on the
     1e7 x 1e7 / 1e8-entry R-MAT, rows cut into `world` shards, one per
@@ -361,27 +541,32 @@ def rmat_strong(args, torch, dev, rank, world, dist, cdev):
     and no single row weight balances 2, 4 and 8 shards
     (profiles/round2/shard_rehearse_w_g248.log, shard_rehearse_calibrated.log).
     Setup only: the timed steps are the same SpMV on the final shards.
-    Every rank's output is checked against the host rule before it counts."""
+    Then the exchange on the final cut (strong_exchange): y all-gathered
+    with the real shard sizes, SpMV + all-gather, cold shards.  Every rank
+    checks its shard; rank 0 checks the whole gathered y."""
     t0 = time.perf_counter()
     full = sa.gen_rmat()  # deterministic: every rank builds the same matrix
     ptr, col, val = sa.csr_from_coo(full)
     n, z = full.n_rows, full.nnz
-    del full
+    if rank != 0:
+        del full
     x = torch.from_numpy(sa.ramp_x(n)).to(dev)
     b_total = sa.bytes_alg(n, n, z)
     steps = max(20, args.steps // 2)
 
-    def run(bounds, k):
+    def shard(bounds):
         lo, hi = int(bounds[rank]), int(bounds[rank + 1])
         lptr = ptr[lo:hi + 1] - ptr[lo]
         loc = sa.Coo(hi - lo, n, np.repeat(np.arange(hi - lo, dtype=np.int32), np.diff(lptr)),
                      col[ptr[lo]:ptr[hi]], val[ptr[lo]:ptr[hi]])
-        dm = sa.to_device(loc, "csr", dev)
+        return loc, sa.to_device(loc, "csr", dev), lo, hi
+
+    def run(bounds, k):
+        loc, dm, _, _ = shard(bounds)
         y = torch.empty(max(loc.n_rows, 1), dtype=torch.float64, device=dev)
         wall, kern = time_steps(torch, dm, x, y, k, 5, dist)
         bad, first = sa.check(loc, sa.ramp_x(n), y[:loc.n_rows].cpu().numpy())
-        if bad:
-            raise SystemExit(f"rank {rank}: R-MAT parity failure (row {first})")
+        all_ok(dist, cdev, torch, bad == 0, f"R-MAT shard row {first}", rank)
         params = {kk: v for kk, v in dm.params.items() if isinstance(v, (int, float, str))}
         t = torch.tensor([wall / k * 1e3, float(np.mean(kern))], dtype=torch.float64, device=cdev)
         shard_ms = [float(np.mean(kern))]
@@ -406,32 +591,64 @@ def rmat_strong(args, torch, dev, rank, world, dist, cdev):
             best = min(best, (max(t), b), key=lambda c: c[0])
         bounds = best[1]
     step_ms, kern_ms, shard_ms, params = run(bounds, steps)
+
+    # the exchange on the final cut
+    comm = iterate.Comm(dist)
+    _, dm, lo, hi = shard(bounds)
+    y_full = torch.full((n,), float("nan"), dtype=torch.float64, device=dev)
+    how, ag_ms, both_ms, cold = strong_exchange(torch, comm, cdev, dm, x, y_full, lo, hi, bounds, steps,
+                                                args.flush == "yes")
+    whole = None
+    if rank == 0:  # the gathered y of the whole matrix against the host rule
+        bad, first = sa.check(full, sa.ramp_x(n), y_full.cpu().numpy())
+        whole = None if bad == 0 else f"gathered R-MAT y, row {first}"
+        del full
+    all_ok(dist, cdev, torch, whole is None, str(whole), rank)
+    del dm, y_full
+    torch.cuda.empty_cache()
+
+    def gbs(ms):
+        return round(b_total / (ms * 1e-3) * 1e-9, 1) if ms and ms > 0 else None
+
     out = {"workload": "csr SpMV on R-MAT 1e7/1e8 (configs[3]) row-sharded over all ranks, x replicated",
            "scaling": "strong", "steps": steps,
-           "aggregate_GBs": round(b_total / (step_ms * 1e-3) * 1e-9, 1),
+           "aggregate_GBs": gbs(step_ms),
            "GFLOPs": round(2 * z / (step_ms * 1e-3) * 1e-9, 1),
            "frac_of_one_gpu_peak": round(b_total / (step_ms * 1e-3) * 1e-9 / sa.HBM_PEAK_GBS, 4),
            "ms_per_step": round(step_ms, 5), "max_shard_kernel_ms": round(kern_ms, 5),
            "shard_ms": [round(v, 5) for v in shard_ms], "shard_rows": np.diff(bounds).tolist(),
            "bytes_alg_whole": b_total, "params_rank0": params, "parity_ok": True,
+           "allgather": {"how": how, "bytes_received_rank0": 8 * (n - (hi - lo)) if rank == 0 else None,
+                         "ms": round(ag_ms, 5), "spmv_plus_allgather_ms": round(both_ms, 5),
+                         "aggregate_GBs_with_allgather": gbs(both_ms),
+                         "gathered_y_parity": "rank 0 checks all 1e7 rows of the gathered y"},
            "partition": ("profile-guided: weighted cut (row weight %g) and two re-cuts by measured cost timed, "
                          "the one with the lowest max shard time kept" % RMAT_ROW_WEIGHT) if world > 1 else "whole matrix",
            "calibration": {"weighted_cut": {"shard_rows": np.diff(bounds0).tolist(),
                                             "shard_ms": [round(v, 5) for v in shard0],
-                                            "aggregate_GBs": round(b_total / (step0 * 1e-3) * 1e-9, 1)},
+                                            "aggregate_GBs": gbs(step0)},
                            "recuts": passes},
            "setup_s": round(time.perf_counter() - t0, 1)}
+    if cold is not None:
+        cm = max(cold)
+        out["cold"] = {"how": "per rank: graph of K x (512 MiB flush + SpMV) minus a graph of K flushes",
+                       "shard_ms": [round(v, 5) for v in cold], "max_shard_ms": round(cm, 5),
+                       "aggregate_GBs": gbs(cm)}
     return out
 
 
 def banded_strong(args, torch, dev, rank, world, dist, cdev):
     """BASELINE.json configs[4]: CSR and SELL-C-sigma on the banded
     --banded-rows x 16-entry matrix, equal 1024-aligned row ranges, each
-    rank's shard generated in its HBM (spmv_gen_banded_device), x = 1
+    rank's shard generated in its HBM (spmv_gen_banded_device), x[j] = j
     replicated; aggregate GB/s = bytes_alg(whole matrix) / max over ranks of
-    the per-step time (HIP-graph replay between barriers).  Each rank checks
-    its first 4096 rows against the host generator's row sums."""
+    the per-step time (HIP-graph replay between barriers).  Every rank
+    checks sampled rows across its whole shard (banded_check); then the
+    exchange (strong_exchange): the y all-gather of the real shard sizes
+    (800 MB of y in all), SpMV + all-gather, cold shards."""
     out = {}
+    n = args.banded_rows
+    comm = iterate.Comm(dist)
     for fmt in ("csr", "sell"):
         a = argparse.Namespace(**vars(args))
         a.workload, a.format, a.variant, a.lanes, a.ki, a.sigma = "banded", fmt, 0, 0, 0, 0
@@ -442,31 +659,58 @@ def banded_strong(args, torch, dev, rank, world, dist, cdev):
         steps = 20
         wall, kern = time_steps(torch, w["dm"], w["x"], w["y"], steps, 3, dist)
         bad = w["check"]()
-        if bad:
-            raise SystemExit(f"rank {rank}: banded {fmt} parity failure ({bad})")
+        all_ok(dist, cdev, torch, bad is None, f"banded {fmt}: {bad}", rank)
         t = torch.tensor([wall / steps * 1e3, float(np.mean(kern))], dtype=torch.float64, device=cdev)
         if dist is not None:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         step_ms = float(t[0].item())
-        out[fmt] = {"aggregate_GBs": round(w["bytes_total"] / (step_ms * 1e-3) * 1e-9, 1),
-                    "GFLOPs": round(2 * w["nnz_total"] / (step_ms * 1e-3) * 1e-9, 1),
-                    "ms_per_step": round(step_ms, 5), "max_shard_kernel_ms": round(float(t[1].item()), 5),
-                    "rows_rank0": w["rows"], "bytes_alg_whole": w["bytes_total"], "parity_ok": True,
-                    "build_s": round(build_s, 1)}
-        del w
+        tot = w["bytes_total"]
+
+        def gbs(ms):
+            return round(tot / (ms * 1e-3) * 1e-9, 1) if ms and ms > 0 else None
+
+        rec = {"aggregate_GBs": gbs(step_ms),
+               "GFLOPs": round(2 * w["nnz_total"] / (step_ms * 1e-3) * 1e-9, 1),
+               "ms_per_step": round(step_ms, 5), "max_shard_kernel_ms": round(float(t[1].item()), 5),
+               "rows_rank0": w["rows"], "bytes_alg_whole": tot, "parity_ok": True,
+               "parity": f"{banded_sample_rows(n, w['lo'], w['hi']).size} rows of rank 0's shard (first/last 512, "
+                         "around 2/4/8-way cuts, past 2^31..2^33 value bytes, 4096 spread) against the host "
+                         "generator, x[j] = j; every rank checks its own",
+               "build_s": round(build_s, 1)}
+        w["y"] = None
+        torch.cuda.empty_cache()
+        y_full = torch.empty(n, dtype=torch.float64, device=dev)
+        how, ag_ms, both_ms, cold = strong_exchange(torch, comm, cdev, w["dm"], w["x"], y_full, w["lo"], w["hi"],
+                                                    w["bounds"], 10, args.flush == "yes")
+        rec["allgather"] = {"how": how, "ms": round(ag_ms, 5),
+                            "bytes_received_rank0": 8 * (n - w["rows"]) if rank == 0 else None,
+                            "spmv_plus_allgather_ms": round(both_ms, 5),
+                            "aggregate_GBs_with_allgather": gbs(both_ms)}
+        if cold is not None:
+            rec["cold"] = {"shard_ms": [round(v, 5) for v in cold], "max_shard_ms": round(max(cold), 5),
+                           "aggregate_GBs": gbs(max(cold))}
+        out[fmt] = rec
+        del w, y_full
         torch.cuda.empty_cache()
     return {"workload": f"banded {args.banded_rows} rows x 16 entries (configs[4]), equal row shards over all "
-                        "ranks, generated on device, x = 1 replicated", "scaling": "strong", "steps": 20, **out}
+                        "ranks, generated on device, x[j] = j replicated", "scaling": "strong", "steps": 20, **out}
 
 
 def main():
     args = parse()
     GRAPH["on"] = args.graph == "yes"
-    import torch
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # the single-matrix figures come from a profiled CHILD process, run
+    # before this process initialises the GPU
+    single = None
+    if rank == 0 and not args.profile and (
+            args.single == "yes" or (args.single == "auto" and world == 1 and args.workload == "cantlike")):
+        single = cant_single_rocprof()
+
+    import torch
+
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     dist = None
@@ -488,46 +732,39 @@ def main():
     dm, x, y = w["dm"], w["x"], w["y"]
     n_rows, nnz, bytes_step = w["rows"], w["nnz"], w["bytes_rank"]
     wall, kern = time_steps(torch, dm, x, y, args.steps, args.warmup, dist)
-    launch = ("hip-graph: the K launches captured once, replayed once; kernel_ms = span / K"
+    launch = (f"hip-graph: the K launches captured once, replayed untimed for >= {WARM_REPLAY_MS:g} ms of GPU "
+              "work, then once timed; kernel_ms = span / K"
               if GRAPH.get("last") == "hip-graph" else "eager launches, one HIP event after each")
     if args.profile:
         if rank == 0:
             print(json.dumps({"profile_run": args.format, "ms_per_launch": float(np.mean(kern))}))
         return
 
-    # parity spot check of this step's output (host check_result rule)
+    # parity of this step's output (host check_result rule), all ranks agree
     bad = w["check"]()
-    if bad:
-        raise SystemExit(f"rank {rank}: parity failure ({bad})")
-    single = sa.gen_cantlike(0, 1)
+    all_ok(dist, cdev, torch, bad is None, str(bad), rank)
 
     wall_t = torch.tensor([wall], dtype=torch.float64, device=cdev)
-    kern_mean = float(np.mean(kern))
-    kern_t = torch.tensor([kern_mean], dtype=torch.float64, device=cdev)
+    kern_t = torch.tensor([float(np.mean(kern))], dtype=torch.float64, device=cdev)
     if dist is not None:
         dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
         dist.all_reduce(kern_t, op=dist.ReduceOp.MAX)
-    wall_max = float(wall_t.item())
-    ms_per_step = wall_max / args.steps * 1e3
+    ms_per_step = float(wall_t.item()) / args.steps * 1e3
     total_bytes = w["bytes_total"]
     value = total_bytes / (ms_per_step * 1e-3) * 1e-9
     gflops = 2.0 * w["nnz_total"] / (ms_per_step * 1e-3) * 1e-9
 
-    # ---- y all-gather over RCCL (timed separately, not in `value`);
-    # shards are padded to the largest one (all_gather_into_tensor needs
-    # equal sizes), then the real rows are the concatenation of the shards
+    # ---- weak-scaling batch: the y blocks (all the same size) all-gathered
+    # over RCCL, timed separately, not in `value`
     allgather = None
-    if dist is not None:
-        pad = w["max_rows"]
-        y_loc = torch.zeros(pad, dtype=torch.float64, device=cdev)
-        y_loc[:n_rows] = y if cdev.type == "cuda" else y.cpu()
-        y_all = torch.empty(pad * world, dtype=torch.float64, device=cdev)
+    if dist is not None and args.workload == "cantlike":
+        y_loc = y if cdev.type == "cuda" else y.cpu()
+        y_all = torch.empty(n_rows * world, dtype=torch.float64, device=cdev)
         for _ in range(3):
             dist.all_gather_into_tensor(y_all, y_loc)
         torch.cuda.synchronize()
-        # the gathered vector must hold every rank's shard in rank order
-        if not torch.equal(y_all[rank * pad:(rank + 1) * pad], y_loc):
-            raise SystemExit(f"rank {rank}: all-gathered y does not match the local shard")
+        ok = bool(torch.equal(y_all[rank * n_rows:(rank + 1) * n_rows], y_loc))
+        all_ok(dist, cdev, torch, ok, "all-gathered y block", rank)
         dist.barrier()
         t0 = time.perf_counter()
         reps = 20
@@ -542,22 +779,22 @@ def main():
 
     kern_ms = float(kern_t.item())
     achieved = bytes_step / (kern_ms * 1e-3) * 1e-9
-    traffic = traffic_for(args.format, bytes_step, kernel_name(args, dm))
+    kname = kernel_name(args, dm)
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": sa.HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / sa.HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": kernel_name(args, dm), "kernel_ms": round(kern_ms, 5),
-                "bytes_alg_per_launch": bytes_step}
+                "frac": round(achieved / sa.HBM_PEAK_GBS, 4),
+                "traffic": traffic_for(args.format, bytes_step, kname),
+                "kernel": kname, "kernel_ms": round(kern_ms, 5), "bytes_alg_per_launch": bytes_step}
 
     per_format = None
-    cant_single = None
     cpu = None
-    do_pf = args.per_format == "yes" or (args.per_format == "auto" and world == 1)
-    if rank == 0 and do_pf and args.workload == "rmat":
-        # configs[3]: every format on the same R-MAT (ELL: N/A, padding)
-        m = w["loc"]
+    do_pf = rank == 0 and (args.per_format == "yes" or (args.per_format == "auto" and world == 1))
+    if do_pf and args.workload in ("rmat", "cantlike"):
+        # every format on the same matrix (R-MAT: ELL is N/A, padding)
+        m = w["loc"] if args.workload == "rmat" else w["m"]
         del dm, w["dm"]
         torch.cuda.empty_cache()
         per_format = {}
+        x_host = x.cpu().numpy()
         for fmt in sa.ALL_FORMATS:
             kw = fmt_kwargs(args, fmt)
             try:
@@ -565,72 +802,37 @@ def main():
             except sa.SpmvError as e:
                 per_format[fmt] = {"na": str(e)}
                 continue
-            _, k2 = time_steps(torch, d2, x, y, max(10, args.steps // 2), 3)
+            _, k2 = time_steps(torch, d2, x, y, max(20, args.steps // 2), 5)
             km = float(np.mean(k2))
-            bad2, _ = sa.check(m, sa.ramp_x(m.n_cols), y[:m.n_rows].cpu().numpy())
+            # the output of every format is checked (host check_result rule,
+            # 1e-6 relative); csrf32 rounds the values to fp32, so its check
+            # shows fp32-value tolerance, not fp64 parity
+            badf, _ = sa.check(m, x_host, y[:m.n_rows].cpu().numpy())
             per_format[fmt] = {"GBs": round(bytes_step / (km * 1e-3) * 1e-9, 1),
                                "GFLOPs": round(2 * nnz / (km * 1e-3) * 1e-9, 1),
                                "frac": round(bytes_step / (km * 1e-3) * 1e-9 / sa.HBM_PEAK_GBS, 4),
                                "kernel_ms": round(km, 5), "stored_MB": round(d2.stored_bytes * 1e-6, 1),
                                "params": dict(kw, **{k: v for k, v in d2.params.items()
                                                      if k in ("variant", "split_T", "n_chunks", "H")}) or None,
-                               "parity_ok": bad2 == 0}
-            del d2
-            torch.cuda.empty_cache()
-        if args.cpu_seconds > 0:
-            ptr, col, val = sa.csr_from_coo(m)
-            cpu = cpu_baseline((ptr, col, val, m.n_rows, m.n_cols), 1, args.cpu_seconds)
-            cpu["sample"] = cpu["sample"].replace("the same 1-copy batch", "the same R-MAT")
-    do_pf = do_pf and args.workload == "cantlike"
-    if rank == 0 and do_pf:
-        m, B = w["m"], args.copies
-        del dm, w["dm"]
-        torch.cuda.empty_cache()
-        per_format = {}
-        cant_single = {}
-        xs = torch.from_numpy(sa.ramp_x(single.n_cols)).to(dev)
-        ys = torch.empty(single.n_rows, dtype=torch.float64, device=dev)
-        bs = sa.bytes_alg(single.n_rows, single.n_cols, single.nnz)
-        x_host = x.cpu().numpy()
-        for fmt in sa.ALL_FORMATS:
-            kw = fmt_kwargs(args, fmt)
-            d2 = sa.to_device(m, fmt, dev, **kw)
-            w2, k2 = time_steps(torch, d2, x, y, max(20, args.steps // 2), 5)
-            km = float(np.mean(k2))
-            # the batch output of every format is checked (host check_result
-            # rule, 1e-6 relative); csrf32 rounds the values to fp32, so its
-            # check shows fp32-value tolerance, not fp64 parity
-            badb, _ = sa.check(m, x_host, y[:m.n_rows].cpu().numpy())
-            per_format[fmt] = {"GBs": round(bytes_step / (km * 1e-3) * 1e-9, 1),
-                               "GFLOPs": round(2 * nnz / (km * 1e-3) * 1e-9, 1),
-                               "frac": round(bytes_step / (km * 1e-3) * 1e-9 / sa.HBM_PEAK_GBS, 4),
-                               "kernel_ms": round(km, 5),
-                               "stored_MB": round(d2.stored_bytes * 1e-6, 1), "params": kw or None,
-                               "parity_ok": badb == 0}
+                               "parity_ok": badf == 0}
             if fmt == "csrf32":
                 per_format[fmt]["parity"] = "within fp32-value tolerance (values rounded to fp32)"
             del d2
             torch.cuda.empty_cache()
-            d1 = sa.to_device(single, fmt, dev, **kw)
-            c_ms, w_ms = cold_single(torch, d1, xs, ys)
-            bad1, _ = sa.check(single, sa.ramp_x(single.n_cols), ys.cpu().numpy())
-            cant_single[fmt] = {"cold_ms": round(c_ms, 5), "cold_GBs": round(bs / (c_ms * 1e-3) * 1e-9, 1),
-                                "warm_ms": round(w_ms, 5), "warm_GBs_cache_resident": round(bs / (w_ms * 1e-3) * 1e-9, 1),
-                                "parity_ok": bad1 == 0}
-            if fmt == "csrf32":
-                cant_single[fmt]["parity"] = "within fp32-value tolerance (values rounded to fp32)"
-            del d1
         if args.cpu_seconds > 0:
-            ptr, col, val = sa.csr_from_coo(single)
-            cpu = cpu_baseline((ptr, col, val, single.n_rows, single.n_cols), B, args.cpu_seconds)
+            if args.workload == "rmat":
+                ptr, col, val = sa.csr_from_coo(m)
+                cpu = cpu_baseline((ptr, col, val, m.n_rows, m.n_cols), 1, args.cpu_seconds)
+                cpu["sample"] = cpu["sample"].replace("the same 1-copy batch", "the same R-MAT")
+            else:
+                sm = sa.gen_cantlike(0, 1)
+                ptr, col, val = sa.csr_from_coo(sm)
+                cpu = cpu_baseline((ptr, col, val, sm.n_rows, sm.n_cols), args.copies, args.cpu_seconds)
 
     rstrong = None
     if args.rmat_strong == "yes" or (args.rmat_strong == "auto" and args.workload == "cantlike"):
         w.pop("dm", None)
-        try:
-            del dm
-        except NameError:
-            pass
+        dm = None
         torch.cuda.empty_cache()
         rstrong = rmat_strong(args, torch, dev, rank, world, dist, cdev)
     bstrong = None
@@ -658,8 +860,8 @@ def main():
             "gflops": round(gflops, 1),
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "cant_single": single,
             "per_format": per_format,
-            "cant_single": cant_single,
             "allgather": allgather,
             "rmat_strong": rstrong,
             "banded_strong": bstrong,

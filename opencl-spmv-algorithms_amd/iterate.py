@@ -107,6 +107,24 @@ class Comm:
         elif out.data_ptr() != inp.data_ptr():
             out[: inp.numel()].copy_(inp)
 
+    def allgatherv(self, full, bounds) -> str:
+        """In-place all-gather of row shards of their REAL sizes: `full`
+        holds this rank's rows [bounds[rank], bounds[rank+1]) and receives
+        every other rank's, no padding to the largest shard.  Over RCCL one
+        torch all_gather of unequal parts (ProcessGroupNCCL issues it as
+        grouped broadcasts, one per shard); over gloo one broadcast per
+        non-empty shard.  Returns how it was done."""
+        if self.dist is None or self.world == 1:
+            return "none (one rank)"
+        parts = [full[int(bounds[r]):int(bounds[r + 1])] for r in range(self.world)]
+        if self.dist.get_backend() == "nccl":
+            self.dist.all_gather(parts, parts[self.rank])
+            return "rccl all_gather of unequal parts (grouped broadcasts)"
+        for r in range(self.world):
+            if parts[r].numel():
+                self.dist.broadcast(parts[r], src=r)
+        return "gloo broadcast per shard"
+
 
 # ---------------------------------------------------------------- kernels
 class HipKernels:

@@ -180,6 +180,65 @@ def _recut_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
+def _allgatherv_worker(rank, world, port, case, q):
+    """bench.py's exchange step (rmat_strong / banded_strong): every rank
+    writes its shard of y into a full-length vector, iterate.Comm.allgatherv
+    fills in the other shards with their REAL sizes (no padding)."""
+    sys.path[:0] = [str(PKG), str(REPO)]
+    import torch
+    import torch.distributed as dist
+
+    import iterate
+    import spmv_amd as sa
+    from oracle import oracle
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        m = sa.gen_rmat(200_000, 2_000_000, scale=18, seed=3) if case == "rmat" else sa.read_mtx(GOLDEN / f"{case}.mtx")
+        ptr, col, val = sa.csr_from_coo(m)
+        x = sa.ramp_x(m.n_cols)
+        if case == "rmat":
+            bounds = sa.partition_rows(m.n_rows, ptr, world, align=1024, row_weight=2.0)
+        else:  # golden file: rank 1 owns the last 3 rows
+            cut = max(m.n_rows - 3, 0)
+            bounds = np.array([0, cut, m.n_rows] if world == 2 else [0, m.n_rows], np.int64)
+        lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+        y_full = torch.full((m.n_rows,), float("nan"), dtype=torch.float64)
+        lptr = np.ascontiguousarray(ptr[lo:hi + 1] - ptr[lo])
+        lcol, lval = np.ascontiguousarray(col[ptr[lo]:ptr[hi]]), np.ascontiguousarray(val[ptr[lo]:ptr[hi]])
+        ys = np.zeros(max(hi - lo, 1))
+        sa.host_lib().spmv_cpu_csr(hi - lo, sa._ptr(lptr), sa._ptr(lcol), sa._ptr(lval), sa._ptr(x), sa._ptr(ys), 1)
+        y_full[lo:hi] = torch.from_numpy(ys[:hi - lo])
+        how = iterate.Comm(dist).allgatherv(y_full, bounds)
+        y_ref = oracle.file_order_spmv(m.n_rows, m.row, m.col, m.val, x)
+        bad = oracle.parity(y_full.numpy(), y_ref, m.row, m.col, m.val, x, m.n_rows)
+        q.put((rank, int(bad.size), bool(torch.isnan(y_full).any()), how))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case", ["rmat", "ragged_shuffled", "all_empty"])
+def test_two_rank_allgatherv_real_sizes(case):
+    """World 2 over gloo: the unequal-shard all-gather of bench.py's strong-
+    scaling legs assembles the whole y (oracle parity, no NaN left) from
+    shards of their real sizes; the golden files give rank 1 the last three rows."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_allgatherv_worker, args=(r, 2, port, case, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(180)
+        assert p.exitcode == 0
+    res = sorted(q.get() for _ in range(2))
+    assert all(bad == 0 and not nan for _, bad, nan, _ in res), res
+    assert all(how == "gloo broadcast per shard" for *_, how in res)
+
+
 def test_two_rank_calibrated_recut():
     """World 2 over gloo: the measured-cost re-cut is the same on both ranks
     (times all-gathered first), covers every row once, and the re-sharded

@@ -131,7 +131,11 @@ __global__ __launch_bounds__(kWave * S) void lab_kernel(const int64_t *__restric
 // slot groups loaded (predicated, branch-free) BEFORE the x-window copy, so
 // the matrix stream and the window copy are in flight together; the rest
 // (per > G) in batches of G after the barrier.
-template <int KI, int S, int G>
+struct XC {  // no gather: the column itself as the x value
+    __device__ __forceinline__ double operator()(int32_t c) const { return (double)c; }
+};
+
+template <int KI, int S, int G, int MODE = 0>
 __global__ __launch_bounds__(kWave * S) void lab2_kernel(const int64_t *__restrict__ slice_ptr,
                                                          const int32_t *__restrict__ perm,
                                                          const int32_t *__restrict__ col,
@@ -158,7 +162,7 @@ __global__ __launch_bounds__(kWave * S) void lab2_kernel(const int64_t *__restri
     typedef typename std::conditional<KI == 1, int32_t, v2i32>::type CT;
     VT v[G];
     CT c[G];
-    const bool any = g1 > g0;  // uniform per wave
+    const bool any = g1 > g0 && MODE != 2;  // uniform per wave
     if (any) {
 #pragma unroll
         for (int u = 0; u < G; ++u) {
@@ -168,7 +172,7 @@ __global__ __launch_bounds__(kWave * S) void lab2_kernel(const int64_t *__restri
         }
     }
     const int32_t span = wd.y - wd.x + 1;
-    const bool staged = span > 0 && span <= xcap;
+    const bool staged = span > 0 && span <= xcap && MODE != 1;
     if (staged) {
         constexpr int T = kWave * S, CU = 8;
         for (int32_t b0 = 0; b0 < span; b0 += CU * T) {
@@ -200,10 +204,12 @@ __global__ __launch_bounds__(kWave * S) void lab2_kernel(const int64_t *__restri
                     a[u % 4] += (in ? v[u].x : 0.0) * xs(c[u].x) + (in ? v[u].y : 0.0) * xs(c[u].y);
             }
         }
-        if (g0 + G < g1)
+        if (g0 + G < g1 && MODE != 2)
             slots<KI, 4>(vp, cp, g0 + G, g1, step, xs, a);
     };
-    if (staged)
+    if (MODE == 1)
+        body(XC{});
+    else if (staged)
         body(XW{s_x, wd.x});
     else
         body(XG{x});
@@ -288,6 +294,13 @@ int lab_run(int code, int xw, int64_t n_slices, const int64_t *sp, const int32_t
         LAB2(1, 4, 16) LAB2(1, 4, 24) LAB2(1, 8, 12) LAB2(1, 2, 24) LAB2(2, 4, 8) LAB2(2, 4, 12) LAB2(2, 2, 12)
         LAB2(2, 2, 16) LAB2(2, 1, 16) LAB2(2, 8, 6)
 #undef LAB2
+#define LAB3(KI, S, G, MODE)                                                                              \
+    case 200000 + MODE * 100000 + KI * 10000 + S * 100 + G:                                               \
+        hipLaunchKernelGGL((lab2_kernel<KI, S, G, MODE>), dim3((unsigned)n_slices), dim3(kWave * S),       \
+                           (size_t)xcap * sizeof(double), s, sp, perm, col, val, x, y, w, xcap, stamps);     \
+        break;
+        LAB3(2, 4, 12, 1) LAB3(2, 4, 12, 2) LAB3(1, 4, 16, 1) LAB3(1, 4, 16, 2) LAB3(2, 2, 16, 1)
+#undef LAB3
     default: return (int)hipErrorInvalidValue;
     }
 #undef LAB

@@ -24,7 +24,7 @@ from cant_single import FLUSH_BYTES, probe_lib  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--codes", default="1084x,2044x,110416,110424,110812,110224,120408,120412,120212,120216,120116,120806")
+    ap.add_argument("--codes", default="120412,320412,420412,110416,310416,410416,120216,320216,1084x")
     ap.add_argument("--reps", type=int, default=20)
     a = ap.parse_args()
     import torch
@@ -54,10 +54,28 @@ def main():
         w = win.view(-1, 2).cpu().numpy()
         xcap = int((w[:, 1] - w[:, 0] + 1).max())
         mats[ki] = (dm, n, win, xcap)
+    # the stream ceiling of the same bytes in this process (cold / warm)
+    nb = (b + 15) // 16 * 16
+    buf = torch.ones(nb // 8, dtype=torch.float64, device=dev)
+    sink = torch.zeros(1 << 16, dtype=torch.float64, device=dev)
+    for mode in ("warm", "cold"):
+        ts = []
+        for r in range(a.reps):
+            if mode == "cold":
+                P.spmv_probe_flush(scratch.data_ptr(), FLUSH_BYTES, sp)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            P.spmv_probe_stream(buf.data_ptr(), nb, sink.data_ptr(), sp)
+            e1.record(st)
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1) * 1e3)
+        print(json.dumps({"probe": mode, "event_us": round(float(np.median(ts)), 2)}), flush=True)
     for code in a.codes.split(","):
         xw = code.endswith("x")
         c = int(code.rstrip("x"))
-        if c >= 100000:  # one-shot variant: 1KSSGG
+        if c >= 200000:  # diagnostic modes of the one-shot variant: (2+MODE)KSSGG
+            ki, S, U = (c // 10000) % 10, (c // 100) % 100, c % 100
+        elif c >= 100000:  # one-shot variant: 1KSSGG
             ki, S, U = (c // 10000) % 10, (c // 100) % 100, c % 100
         else:
             ki, S, U = c // 1000, (c % 1000) // 10, c % 10

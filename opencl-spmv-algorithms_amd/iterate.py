@@ -13,6 +13,17 @@ time, so `all_gather_into_tensor` of each rank's padded block IS the next
 x — no reorder pass, and the y all-gather becomes the input
 of the next SpMV directly.
 
+Overlap (build_operator(..., overlap=True), world > 1).  The shard is
+split by column into a LOCAL part (columns in this rank's own block, which
+it already holds) and a REMOTE part (every other column).  One step of
+A·x then starts the all-gather of the own block (RCCL runs it on its own
+stream), runs the local SpMV on the compute stream while the exchange is in
+flight, waits, runs the remote SpMV into a scratch y and adds it
+(spmv_axpy_ratio with ratio 1: an exact add).  overlap=False with split=True
+runs the same launches with the wait first, so the two produce the same
+bits; the split itself regroups each row's sum (local entries, then
+remote) and so differs from the unsplit SpMV within the parity rule.
+
 Per iteration everything stays on the device: SpMV (libspmv_hip), the
 deterministic dot product, and the vector updates read their scalars
 (norms, CG's alpha = rr/pAp and beta = rr'/rr) from device memory; the
@@ -86,6 +97,21 @@ def local_shard(m: sa.Coo, layout: ShardLayout, rank: int) -> sa.Coo:
                   f"{m.label} rank {rank}/{layout.world}")
 
 
+def split_local_remote(loc: sa.Coo, layout: ShardLayout, rank: int):
+    """(local, remote) parts of a gathered-layout shard: `local` keeps the
+    entries whose column lies in this rank's own block, renumbered to
+    [0, pad) so it multiplies the rank's send block directly; `remote` keeps
+    the rest with gathered-layout columns.  Both keep all the shard's rows
+    and their entries in the shard's order."""
+    base = rank * layout.pad
+    own = (loc.col >= base) & (loc.col < base + layout.pad)
+    local = sa.Coo(loc.n_rows, layout.pad, loc.row[own], (loc.col[own] - base).astype(np.int32), loc.val[own],
+                   False, f"{loc.label} local")
+    remote = sa.Coo(loc.n_rows, loc.n_cols, loc.row[~own], loc.col[~own], loc.val[~own], False,
+                    f"{loc.label} remote")
+    return local, remote
+
+
 # ------------------------------------------------------------- collectives
 class Comm:
     """In-place collectives over torch.distributed (nccl = RCCL on ROCm);
@@ -106,6 +132,22 @@ class Comm:
             self.dist.all_gather_into_tensor(out, inp)
         elif out.data_ptr() != inp.data_ptr():
             out[: inp.numel()].copy_(inp)
+
+    def allgather_start(self, out, inp):
+        """Start the all-gather; returns a handle for wait() (None when
+        alone: the copy is done at once)."""
+        if self.dist is not None and self.world > 1:
+            return self.dist.all_gather_into_tensor(out, inp, async_op=True)
+        if out.data_ptr() != inp.data_ptr():
+            out[: inp.numel()].copy_(inp)
+        return None
+
+    @staticmethod
+    def wait(work) -> None:
+        """Make the compute stream wait for a started collective (NCCL: a
+        stream dependency, the host does not block)."""
+        if work is not None:
+            work.wait()
 
     def allgatherv(self, full, bounds) -> str:
         """In-place all-gather of row shards of their REAL sizes: `full`
@@ -175,8 +217,10 @@ class DistOperator:
     layout: ShardLayout
     rank: int
     n: int  # global rows
-    kernels: object  # HipKernels (or a test double)
+    kernels: object  # HipKernels (or a test double); the LOCAL part when split
     device: object = None
+    remote: object = None  # kernels of the remote-column part (split shards only)
+    overlap: bool = False  # split shards: run the local part while the all-gather is in flight
 
     @property
     def world(self) -> int:
@@ -196,18 +240,51 @@ class DistOperator:
 
 
 def build_operator(m: sa.Coo, rank: int = 0, world: int = 1, fmt: str = "csr", device="cuda:0", align: int = 1024,
-                   **fmt_kw) -> DistOperator:
-    """Partition, renumber and upload this rank's shard (HIP kernels)."""
+                   split: bool = False, overlap: bool = False, **fmt_kw) -> DistOperator:
+    """Partition, renumber and upload this rank's shard (HIP kernels).
+    split (implied by overlap): local / remote column parts
+    (split_local_remote), each its own device matrix."""
     counts = np.bincount(m.row, minlength=m.n_rows).astype(np.int64)
     layout = layout_for(m.n_rows, counts, world, align)
     loc = local_shard(m, layout, rank)
-    dm = sa.to_device(loc, fmt, device, **fmt_kw)
-    return DistOperator(layout, rank, m.n_rows, HipKernels(dm), device)
+    if not (split or overlap):
+        return DistOperator(layout, rank, m.n_rows, HipKernels(sa.to_device(loc, fmt, device, **fmt_kw)), device)
+    local, remote = split_local_remote(loc, layout, rank)
+    return DistOperator(layout, rank, m.n_rows, HipKernels(sa.to_device(local, fmt, device, **fmt_kw)), device,
+                        HipKernels(sa.to_device(remote, fmt, device, **fmt_kw)), overlap)
 
 
 def _zeros(op, n):
     torch = sa._torch()
     return torch.zeros(n, dtype=torch.float64, device=op.device)
+
+
+class _Apply:
+    """y = A·x for the vector whose own block is `send` (gathered into
+    `full` by this call).  Unsplit: all-gather, then one SpMV on `full`.
+    Split: start the all-gather, local SpMV on `send` (before or after the
+    wait: overlap), wait, remote SpMV on `full` into a scratch vector, exact
+    add."""
+
+    def __init__(self, op, comm, full, send):
+        self.op, self.comm, self.full, self.send = op, comm, full, send
+        if op.remote is not None:
+            self.y2 = _zeros(op, max(op.rows, 1))
+            self.one = _zeros(op, 1) + 1.0
+
+    def __call__(self, y) -> None:
+        op, comm = self.op, self.comm
+        if op.remote is None:
+            comm.allgather(self.full, self.send)
+            op.kernels.spmv(self.full, y)
+            return
+        work = comm.allgather_start(self.full, self.send)
+        if not op.overlap:
+            comm.wait(work)
+        op.kernels.spmv(self.send, y)  # own block only: runs while the exchange is in flight
+        comm.wait(work)
+        op.remote.spmv(self.full, self.y2)
+        op.kernels.axpy_ratio(op.rows, self.one, self.one, 1.0, self.y2, y)  # y += y_remote, exact
 
 
 def _gathered_pair(op, comm):
@@ -243,17 +320,16 @@ def power_iteration(op: DistOperator, iters: int, comm: Comm | None = None, x0=N
     k.dot(rows, x_loc, x_loc, s0, ws)
     comm.allreduce(s0)
     k.scale_rsqrt(rows, s0, x_loc, x_loc)
-    comm.allgather(full, send)
     y = _zeros(op, max(rows, 1))
     hist = _zeros(op, 2 * max(iters, 1)).view(-1, 2)
+    apply = _Apply(op, comm, full, send)
 
     def step(h):
-        k.spmv(full, y)
+        apply(y)  # gathers x (overlapped with the local part when split)
         k.dot(rows, x_loc, y, h[0:1], ws)
         k.dot(rows, y, y, h[1:2], ws)
         comm.allreduce(h)  # both scalars in one collective
         k.scale_rsqrt(rows, h[1:2], y, x_loc)
-        comm.allgather(full, send)
 
     done = 0
     if graph and comm.world == 1 and iters > block:
@@ -288,7 +364,7 @@ def cg(op: DistOperator, b_loc, comm: Comm | None = None, tol: float = 1e-10, ma
     x = _zeros(op, rows)
     r = b_loc.clone()
     p.copy_(b_loc)
-    comm.allgather(full, send)
+    apply = _Apply(op, comm, full, send)
     Ap = _zeros(op, max(rows, 1))
     ws = k.dot_ws(rows)
     rr, rr_new, pAp = _zeros(op, 1), _zeros(op, 1), _zeros(op, 1)
@@ -299,7 +375,7 @@ def cg(op: DistOperator, b_loc, comm: Comm | None = None, tol: float = 1e-10, ma
         return x, 0, 0.0
     it = 0
     while it < maxit:
-        k.spmv(full, Ap)
+        apply(Ap)  # gathers p (overlapped with the local part when split)
         k.dot(rows, p, Ap, pAp, ws)
         comm.allreduce(pAp)
         k.axpy_ratio(rows, rr, pAp, 1.0, p, x)  # x += alpha p
@@ -307,7 +383,6 @@ def cg(op: DistOperator, b_loc, comm: Comm | None = None, tol: float = 1e-10, ma
         k.dot(rows, r, r, rr_new, ws)
         comm.allreduce(rr_new)
         k.xpay_ratio(rows, rr_new, rr, r, p)  # p = r + beta p
-        comm.allgather(full, send)
         rr, rr_new = rr_new, rr
         it += 1
         if it % check_every == 0 or it == maxit:

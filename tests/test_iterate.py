@@ -38,11 +38,18 @@ def _sym_random(n=3000, seed=4):
     return sa.Coo(n, n, r.astype(np.int32), c.astype(np.int32), v, False, "sym random")
 
 
-def _np_operator(m, rank, world, align=64):
+def _np_operator(m, rank, world, align=64, mode="plain"):
+    """mode: plain (one SpMV on the gathered x), split (local / remote
+    column parts, all-gather first), overlap (local part while the
+    all-gather is in flight)."""
     counts = np.bincount(m.row, minlength=m.n_rows).astype(np.int64)
     layout = it.layout_for(m.n_rows, counts, world, align)
     loc = it.local_shard(m, layout, rank)
-    return it.DistOperator(layout, rank, m.n_rows, NumpyKernels(loc), "cpu")
+    if mode == "plain":
+        return it.DistOperator(layout, rank, m.n_rows, NumpyKernels(loc), "cpu")
+    local, remote = it.split_local_remote(loc, layout, rank)
+    return it.DistOperator(layout, rank, m.n_rows, NumpyKernels(local), "cpu", NumpyKernels(remote),
+                           mode == "overlap")
 
 
 @pytest.mark.parametrize("world", [1, 2, 3, 8])
@@ -94,7 +101,27 @@ def test_cg_single_rank_solves_laplacian():
     assert np.linalg.norm(A @ x.numpy() - 1.0) <= 1e-9 * np.sqrt(m.n_rows)
 
 
-def _worker(rank, world, port, what, q):
+def test_split_local_remote_parts():
+    """The local part holds exactly the own-block columns (renumbered to the
+    send block), the remote part the rest; together they are the shard."""
+    m = sa.gen_random(4000, 4000, 0, 30, seed=5)
+    counts = np.bincount(m.row, minlength=m.n_rows).astype(np.int64)
+    lay = it.layout_for(m.n_rows, counts, 3, align=64)
+    v = np.random.default_rng(2).uniform(-1, 1, m.n_rows)
+    xg = lay.to_gathered(v)
+    for r in range(3):
+        loc = it.local_shard(m, lay, r)
+        local, remote = it.split_local_remote(loc, lay, r)
+        assert local.nnz + remote.nnz == loc.nnz and local.n_cols == lay.pad
+        assert local.col.size == 0 or (local.col.min() >= 0 and local.col.max() < lay.pad)
+        own = (remote.col >= r * lay.pad) & (remote.col < (r + 1) * lay.pad)
+        assert not own.any()
+        A = lambda c: sp.csr_matrix((c.val, (c.row, c.col)), shape=(c.n_rows, c.n_cols))  # noqa: E731
+        send = xg[r * lay.pad:(r + 1) * lay.pad]
+        assert np.allclose(A(local) @ send + A(remote) @ xg, A(loc) @ xg, rtol=1e-13, atol=1e-13)
+
+
+def _worker(rank, world, port, what, q, mode="plain"):
     sys.path[:0] = [str(PKG), str(REPO), str(REPO / "tests")]
     import torch
     import torch.distributed as dist
@@ -107,12 +134,12 @@ def _worker(rank, world, port, what, q):
         comm = it2.Comm(dist)
         if what == "power":
             m = _sym_random()
-            op = _np_operator(m, rank, world)
+            op = _np_operator(m, rank, world, mode=mode)
             hist, x = it2.power_iteration(op, 60, comm)
             q.put((rank, hist, op.lo, x.numpy().copy()))
         else:
             m = laplacian_2d(40)
-            op = _np_operator(m, rank, world)
+            op = _np_operator(m, rank, world, mode=mode)
             b = torch.ones(op.rows, dtype=torch.float64)
             x, its, rel = it2.cg(op, b, comm, tol=1e-10, maxit=500, check_every=5)
             q.put((rank, (its, rel), op.lo, x.numpy().copy()))
@@ -120,13 +147,13 @@ def _worker(rank, world, port, what, q):
         dist.destroy_process_group()
 
 
-def _run_ranks(world, what):
+def _run_ranks(world, what, mode="plain"):
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, what, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, what, q, mode)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted((q.get(timeout=240) for _ in range(world)), key=lambda t: t[0])
@@ -156,3 +183,22 @@ def test_cg_two_ranks():
     (its0, rel0), (its1, rel1) = res[0][1], res[1][1]
     assert its0 == its1 and rel0 == rel1 and rel0 <= 1e-10
     assert np.linalg.norm(A @ x - 1.0) <= 1e-9 * np.sqrt(m.n_rows)
+
+
+@pytest.mark.parametrize("what,world", [("power", 2), ("power", 3), ("cg", 2)])
+def test_overlap_same_bits_as_sequential(what, world):
+    """§8f row 3: the overlapped loop (local-column SpMV while the x
+    all-gather is in flight) gives the same bits as the same split run
+    sequentially, on every rank, and the answer of the unsplit loop within
+    the parity rule."""
+    seq = _run_ranks(world, what, "split")
+    ovl = _run_ranks(world, what, "overlap")
+    plain = _run_ranks(world, what, "plain")
+    for a, b, c in zip(seq, ovl, plain):
+        assert np.array_equal(a[3], b[3])  # x: bit-identical
+        if what == "power":
+            assert np.array_equal(a[1], b[1])  # the all-reduced scalars too
+            assert np.allclose(a[1], c[1], rtol=1e-12)
+        else:
+            assert a[1] == b[1]  # iterations and residual
+        assert np.allclose(a[3], c[3], rtol=1e-9, atol=1e-12)

@@ -153,3 +153,36 @@ def test_two_ranks_sharing_the_gpu(tmp_path, what):
         assert r2[0]["rel_residual"] <= 1e-10 and r1["rel_residual"] <= 1e-10
     sq = r2[0]["x_sq"] + r2[1]["x_sq"]
     assert abs(sq - r1["x_sq"]) <= 1e-9 * r1["x_sq"]
+
+
+def test_two_ranks_overlap_same_bits_as_split(tmp_path):
+    """§8f row 3 on the device: two ranks (gloo, sharing cuda:0) run power
+    iteration with the shard split into local / remote column parts, once
+    sequentially and once with the local part launched while the x
+    all-gather is in flight: the same bits on every rank, and the unsplit
+    answer within the parity rule."""
+    base = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+            "--master-addr", "127.0.0.1", "--master-port", "29563", str(REPO / "tools" / "iterate_bench.py"),
+            "--what", "power", "--iters", "40", "--matrix", "sym", "--sym-rows", "20000", "--backend", "gloo", "--share-gpu"]
+    res = {}
+    for mode in ("plain", "split", "overlap"):
+        p = subprocess.run(base + ["--mode", mode, "--out", str(tmp_path / mode)], capture_output=True, text=True,
+                           timeout=600, env=dict(os.environ))
+        assert p.returncode == 0, p.stdout + p.stderr
+        res[mode] = [json.loads((tmp_path / f"{mode}.rank{k}").read_text()) for k in range(2)]
+    for k in range(2):
+        s, o, pl = res["split"][k], res["overlap"][k], res["plain"][k]
+        assert s["x_head"] == o["x_head"] and s["x_sum"] == o["x_sum"] and s["x_sq"] == o["x_sq"]
+        assert s["lambda"] == o["lambda"] and s["hist_tail"] == o["hist_tail"]
+        assert abs(s["lambda"] - pl["lambda"]) <= 1e-10 * abs(pl["lambda"])
+
+
+def test_overlap_rehearsal_runs(tmp_path):
+    """The one-GPU rehearsal: overlapped and sequential launches give the
+    same bits, and the split SpMV passes the parity rule on every rank."""
+    p = subprocess.run([sys.executable, str(REPO / "tools" / "iterate_bench.py"), "--rehearse", "2", "--matrix",
+                        "laplacian", "--k", "300", "--reps", "5"], capture_output=True, text=True, timeout=600,
+                       env=dict(os.environ))
+    assert p.returncode == 0, p.stdout + p.stderr
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    assert all(r["overlap_same_bits"] and r["parity_ok"] for r in line["ranks"])

@@ -43,6 +43,11 @@ for s in "${steps[@]}"; do
     rehearse2) run rehearse2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --backend gloo --share-gpu --steps 20;;
     rehearse2r) run rehearse2_rmat 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --backend gloo --share-gpu --workload rmat --steps 10;;
     drivers) run drivers 600 $PYT tests/test_drivers_gpu.py;;
+    itertests) run iter_tests 600 $PYT tests/test_iterate_gpu.py;;
+    lab) run sell_lab 400 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/lab -o run -- python3 tools/sell_lab.py &&
+         run lab_medians 60 python tools/trace_medians.py gpurun_out/lab;;
+    overlap) run overlap_rmat 600 python tools/iterate_bench.py --rehearse 8 --matrix rmat --reps 20 &&
+             run overlap_lap 600 python tools/iterate_bench.py --rehearse 8 --matrix laplacian --k 3000 --reps 20;;
     counters) run counters 120 rocprofv3 -L;;
     probe) [ -x tools/bw_probe ] || hipcc --offload-arch=gfx950 -O3 tools/bw_probe.hip -o tools/bw_probe; run bw_probe 300 tools/bw_probe;;
     pmc) run pmc 1100 python tools/pmc_traffic.py;;

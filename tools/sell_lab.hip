@@ -232,6 +232,56 @@ __global__ __launch_bounds__(kWave * S) void lab2_kernel(const int64_t *__restri
     }
 }
 
+// Flat one-shot read of the SELL arrays (ki = 2 pairs: 16 B of values +
+// 8 B of columns per lane per load), slices ignored: U pairs per lane, all
+// in flight together, 256-thread workgroups like the stream probe.
+// GATHER = 1 multiplies by x[col] (L2 gathers), 0 by the column itself.
+// The sum is kept alive by an impossible compare (probe trick).
+// GATHER = 2: as 1, and every workgroup first touches 16 lines of x (one
+// load per line from 16 lanes) so that the workgroups of each XCD pull all
+// of x into that XCD's L2 while the matrix stream is in flight.
+template <int U, int GATHER>
+__global__ __launch_bounds__(256) void lab_flat_kernel(const v2f64 *__restrict__ val, const v2i32 *__restrict__ col,
+                                                       int64_t n2, const double *__restrict__ x,
+                                                       double *__restrict__ out, uint64_t *__restrict__ stamps)
+{
+    const uint64_t t0 = now();
+    const int64_t base = (int64_t)blockIdx.x * 256 * U + threadIdx.x;
+    double pre = 0.0;
+    if constexpr (GATHER == 2) {
+        if (threadIdx.x < 4 * U) {  // 4U lines per workgroup: all of x per XCD for cant
+            const int64_t line = (int64_t)(blockIdx.x / 8) * (4 * U) + threadIdx.x;
+            const int64_t j = line * 16 < (int64_t)out[-1] ? line * 16 : 0;  // out[-1] = n_x
+            pre = x[j];
+        }
+    }
+    v2f64 v[U];
+    v2i32 c[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int64_t i = base + (int64_t)u * 256;
+        const int64_t j = i < n2 ? i : n2 - 1;
+        v[u] = __builtin_nontemporal_load(val + j);
+        c[u] = __builtin_nontemporal_load(col + j);
+    }
+    double s = 0.0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        if constexpr (GATHER)
+            s += v[u].x * x[c[u].x] + v[u].y * x[c[u].y];
+        else
+            s += v[u].x * (double)c[u].x + v[u].y * (double)c[u].y;
+    }
+    if (s + pre == 1.2345e-300)
+        out[blockIdx.x] = s;
+    if ((threadIdx.x & 63) == 0) {
+        const int64_t i = ((int64_t)blockIdx.x * 4 + threadIdx.x / 64) * 3;
+        stamps[i] = t0;
+        stamps[i + 1] = now();
+        stamps[i + 2] = hw_id();
+    }
+}
+
 // column window of every slice: [min, max] of its stored columns
 __global__ void lab_window_kernel(const int64_t *__restrict__ slice_ptr, const int32_t *__restrict__ col,
                                   int2 *__restrict__ win)
@@ -268,6 +318,21 @@ int lab_windows(int64_t n_slices, const int64_t *sp, const int32_t *col, void *w
 {
     hipLaunchKernelGGL(lab_window_kernel, dim3((unsigned)n_slices), dim3(kWave), 0, (hipStream_t)stream, sp, col,
                        (int2 *)win);
+    return (int)hipGetLastError();
+}
+
+// flat one-shot read: blocks = ceil(n2 / (256 U)), 4 waves each
+int lab_flat(int U, int gather, int64_t n2, const void *val, const void *col, const double *x, double *out,
+             uint64_t *stamps, void *stream)
+{
+    const hipStream_t s = (hipStream_t)stream;
+    const unsigned blocks = (unsigned)((n2 + 256 * U - 1) / (256 * U));
+#define FLAT(UU, GG)                                                                                      \
+    if (U == UU && gather == GG)                                                                          \
+        hipLaunchKernelGGL((lab_flat_kernel<UU, GG>), dim3(blocks), dim3(256), 0, s, (const v2f64 *)val,   \
+                           (const v2i32 *)col, n2, x, out, stamps);
+    FLAT(2, 0) FLAT(2, 1) FLAT(4, 0) FLAT(4, 1) FLAT(8, 0) FLAT(8, 1) FLAT(4, 2) FLAT(8, 2)
+#undef FLAT
     return (int)hipGetLastError();
 }
 

@@ -24,7 +24,7 @@ from cant_single import FLUSH_BYTES, probe_lib  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--codes", default="120412,320412,420412,110416,310416,410416,120216,320216,1084x")
+    ap.add_argument("--codes", default="F40,F41,F42,F80,F81,F82")
     ap.add_argument("--reps", type=int, default=20)
     a = ap.parse_args()
     import torch
@@ -37,6 +37,7 @@ def main():
     lab.lab_run.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int64, vp, vp, vp, vp, vp, vp, vp, ctypes.c_int32, vp,
                             vp]
     lab.lab_windows.argtypes = [ctypes.c_int64, vp, vp, vp, vp]
+    lab.lab_flat.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int64, vp, vp, vp, vp, vp, vp]
     P = probe_lib()
     scratch = torch.empty(FLUSH_BYTES, dtype=torch.uint8, device=dev)
     m = sa.gen_cantlike(0, 1)
@@ -71,6 +72,9 @@ def main():
             ts.append(e0.elapsed_time(e1) * 1e3)
         print(json.dumps({"probe": mode, "event_us": round(float(np.median(ts)), 2)}), flush=True)
     for code in a.codes.split(","):
+        if code.startswith("F"):  # flat one-shot read of the ki = 2 arrays: F<U><gather>
+            flat(a, torch, lab, P, scratch, st, sp, mats[2][0], x, b, int(code[1:-1]), int(code[-1]), code)
+            continue
         xw = code.endswith("x")
         c = int(code.rstrip("x"))
         if c >= 200000:  # diagnostic modes of the one-shot variant: (2+MODE)KSSGG
@@ -109,6 +113,35 @@ def main():
         span = res["cold"]["span_us"]
         print(json.dumps({"code": code, "ki": ki, "S": S, "U": U, "xwin": xw, "xcap": xcap, **res,
                           "cold_GBs_span": round(b / (span * 1e-6) * 1e-9, 1), "parity_ok": bad == 0}), flush=True)
+
+
+def flat(a, torch, lab, P, scratch, st, sp, dm, x, b, U, gather, code):
+    A = dm.arrays
+    n2 = A["val"].numel() // 2
+    blocks = (n2 + 256 * U - 1) // (256 * U)
+    stamps = torch.zeros(blocks * 4 * 3, dtype=torch.int64, device=x.device)
+    out_all = torch.zeros(blocks + 1, dtype=torch.float64, device=x.device)
+    out_all[0] = float(x.numel())  # the kernel reads n_x from out[-1]
+    out = out_all[1:]
+    res = {}
+    for mode in ("warm", "cold"):
+        spans, durs, late = [], [], []
+        for r in range(a.reps):
+            if mode == "cold":
+                P.spmv_probe_flush(scratch.data_ptr(), FLUSH_BYTES, sp)
+            assert lab.lab_flat(U, gather, n2, A["val"].data_ptr(), A["col"].data_ptr(), x.data_ptr(),
+                                out.data_ptr(), stamps.data_ptr(), sp) == 0
+            torch.cuda.synchronize()
+            s = stamps.view(-1, 3).cpu().numpy().astype(np.int64)
+            t0, t1 = s[:, 0], s[:, 1]
+            spans.append((t1.max() - t0.min()) * 10e-3)
+            durs.append(np.median(t1 - t0) * 10e-3)
+            late.append((t0.max() - t0.min()) * 10e-3)
+        res[mode] = {"span_us": round(float(np.median(spans)), 2), "wave_us_med": round(float(np.median(durs)), 2),
+                     "last_start_us": round(float(np.median(late)), 2)}
+    nbytes = 24 * n2
+    print(json.dumps({"code": code, "flat_U": U, "gather": gather, "bytes": nbytes, "blocks": blocks, **res,
+                      "cold_GBs_span": round(nbytes / (res["cold"]["span_us"] * 1e-6) * 1e-9, 1)}), flush=True)
 
 
 if __name__ == "__main__":

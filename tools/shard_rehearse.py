@@ -13,7 +13,10 @@ step time.  Here every shard of every G is built and timed ALONE on cuda:0
 is the SpMV-only figure a G-GPU run reports when every GPU runs its shard
 concurrently (the GPUs share nothing on the SpMV path).  Back-to-back
 launches keep part of a small shard and of x in the 256 MiB Infinity Cache,
-on every GPU alike, so the figure is labelled warm.  The y all-gather over
+on every GPU alike, so the figure is labelled warm.  --flush also times
+every shard cold (a 512 MiB flush before each SpMV, bench.cold_step_ms:
+a graph of flush + SpMV minus a graph of flushes) and reports the cold
+aggregate beside the warm one.  The y all-gather over
 RCCL is not included (bench.py times it separately).  A rehearsal on one
 card, not a substitute for the driver's 8-GPU run.
 
@@ -77,6 +80,7 @@ def main():
     ap.add_argument("--env", action="append", default=[],
                     help="KEY=v1,v2: library knobs timed interleaved on every shard (several: cartesian product)")
     ap.add_argument("--rounds", type=int, default=1, help="interleaved rounds per shard (median of rounds)")
+    ap.add_argument("--flush", action="store_true", help="also time every shard cold (512 MiB flush first)")
     ap.add_argument("--calibrate", type=int, default=0,
                     help="profile-guided re-cuts after the weighted cut (spmv_partition_rows_calibrated, "
                          "from the first --env config's shard times), each timed again")
@@ -112,7 +116,7 @@ def main():
 
 
 def run_split(a, torch, sa, dev, ptr, col, val, n, x, xh, b_total, envs, kw, G, w, hot, bounds, cpass, base):
-    times, nnzs, params = [[] for _ in envs], [], None
+    times, nnzs, params, cold = [[] for _ in envs], [], None, []
     for r in range(G):
         lo, hi = int(bounds[r]), int(bounds[r + 1])
         lptr = ptr[lo:hi + 1] - ptr[lo]
@@ -131,6 +135,10 @@ def run_split(a, torch, sa, dev, ptr, col, val, n, x, xh, b_total, envs, kw, G, 
                     raise SystemExit(f"G={G} shard {r} env {env}: parity failure at row {first}")
         for i in range(len(envs)):
             times[i].append(float(np.median(per[i])))
+        if a.flush:
+            from bench import cold_step_ms
+
+            cold.append(cold_step_ms(torch, dm, x, y, a.reps))
         nnzs.append(loc.nnz)
         del dm, y, loc
         torch.cuda.empty_cache()
@@ -138,11 +146,15 @@ def run_split(a, torch, sa, dev, ptr, col, val, n, x, xh, b_total, envs, kw, G, 
         tmax = max(times[i])
         agg = b_total / (tmax * 1e-3) * 1e-9
         base = base or agg
+        extra = {}
+        if cold:
+            extra = {"shard_ms_cold": [round(t, 4) for t in cold], "max_ms_cold": round(max(cold), 4),
+                     "aggregate_GBs_cold": round(b_total / (max(cold) * 1e-3) * 1e-9, 1)}
         print(json.dumps({"workload": "rmat 1e7/1e8", "format": a.format, "env": env, "params_shard0": params,
                           "gpus": G, "row_weight": w, "hot": hot, "graph": a.graph, "calibration_pass": cpass,
                           "shard_rows": np.diff(bounds).tolist(), "shard_nnz": nnzs,
                           "shard_ms": [round(t, 4) for t in times[i]], "max_ms": round(tmax, 4),
-                          "aggregate_GBs_warm": round(agg, 1), "speedup_vs_first": round(agg / base, 2)}),
+                          "aggregate_GBs_warm": round(agg, 1), "speedup_vs_first": round(agg / base, 2), **extra}),
               flush=True)
     return times, base
 

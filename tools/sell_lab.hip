@@ -163,6 +163,56 @@ __global__ __launch_bounds__(kWave * S) void lab2_kernel(const int64_t *__restri
     VT v[G];
     CT c[G];
     const bool any = g1 > g0 && MODE != 2;  // uniform per wave
+    if constexpr (MODE == 3) {  // column loads first, then values; x gathered from global as columns land
+        const int32_t row3 = wv == 0 ? perm[s * kWave + lane] : -1;
+        double a3[4] = {0.0, 0.0, 0.0, 0.0};
+        if (any) {
+#pragma unroll
+            for (int u = 0; u < G; ++u)
+                c[u] = __builtin_nontemporal_load(reinterpret_cast<const CT *>(cp + (g0 + u < g1 ? g0 + u : g0) * step));
+#pragma unroll
+            for (int u = 0; u < G; ++u)
+                v[u] = __builtin_nontemporal_load(reinterpret_cast<const VT *>(vp + (g0 + u < g1 ? g0 + u : g0) * step));
+            double xg[G * KI];
+#pragma unroll
+            for (int u = 0; u < G; ++u) {
+                if constexpr (KI == 1) {
+                    xg[u] = x[c[u]];
+                } else {
+                    xg[2 * u] = x[c[u].x];
+                    xg[2 * u + 1] = x[c[u].y];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < G; ++u) {
+                const bool in = g0 + u < g1;
+                if constexpr (KI == 1)
+                    a3[u % 4] += (in ? v[u] : 0.0) * xg[u];
+                else
+                    a3[u % 4] += (in ? v[u].x : 0.0) * xg[2 * u] + (in ? v[u].y : 0.0) * xg[2 * u + 1];
+            }
+            if (g0 + G < g1)
+                slots<KI, 4>(vp, cp, g0 + G, g1, step, XG{x}, a3);
+        }
+        double sum3 = (a3[0] + a3[2]) + (a3[1] + a3[3]);
+        __shared__ double part3[S][kWave];
+        if constexpr (S > 1) {
+            part3[wv][lane] = sum3;
+            __syncthreads();
+            if (wv == 0)
+                for (int k = 1; k < S; ++k)
+                    sum3 += part3[k][lane];
+        }
+        if (row3 >= 0)
+            y[row3] = sum3;
+        if (lane == 0) {
+            const int64_t i = (s * S + wv) * 3;
+            stamps[i] = t0;
+            stamps[i + 1] = now();
+            stamps[i + 2] = hw_id();
+        }
+        return;
+    }
     if (any) {
 #pragma unroll
         for (int u = 0; u < G; ++u) {
@@ -257,6 +307,37 @@ __global__ __launch_bounds__(256) void lab_flat_kernel(const v2f64 *__restrict__
     }
     v2f64 v[U];
     v2i32 c[U];
+    if constexpr (GATHER == 3) {  // all column loads first, then the values: x gathers overlap the value stream
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = base + (int64_t)u * 256;
+            c[u] = __builtin_nontemporal_load(col + (i < n2 ? i : n2 - 1));
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = base + (int64_t)u * 256;
+            v[u] = __builtin_nontemporal_load(val + (i < n2 ? i : n2 - 1));
+        }
+        double g0[U], g1[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            g0[u] = x[c[u].x];
+            g1[u] = x[c[u].y];
+        }
+        double s3 = 0.0;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            s3 += v[u].x * g0[u] + v[u].y * g1[u];
+        if (s3 == 1.2345e-300)
+            out[blockIdx.x] = s3;
+        if ((threadIdx.x & 63) == 0) {
+            const int64_t i = ((int64_t)blockIdx.x * 4 + threadIdx.x / 64) * 3;
+            stamps[i] = t0;
+            stamps[i + 1] = now();
+            stamps[i + 2] = hw_id();
+        }
+        return;
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const int64_t i = base + (int64_t)u * 256;
@@ -280,6 +361,122 @@ __global__ __launch_bounds__(256) void lab_flat_kernel(const v2f64 *__restrict__
         stamps[i + 1] = now();
         stamps[i + 2] = hw_id();
     }
+}
+
+// Chunked SELL (C = 64): work item = chunk of <= G slot groups of ONE slice,
+// one wave per chunk, 4 waves per workgroup, one-shot predicated loads.  A
+// slice of one chunk stores y directly; otherwise every chunk leaves its
+// per-row partial in part[c][lane] and bumps cnt[s]; the wave that brings
+// cnt[s] to the slice's chunk count adds the partials in chunk order
+// (deterministic) and stores y[perm].  SYNC = 0: agent-scope fences around
+// the counter (release: L2 write-back, acquire: L2 invalidate); SYNC = 1:
+// partials written and read as agent-scope relaxed atomics (coherent at
+// the device level by themselves) and an explicit wait before the counter.
+// PREF: the first chunk of a slice touches the slice's x window lines.
+// Workgroups are mapped so that consecutive chunks land on one XCD.
+template <int KI, int G, int SYNC, bool PREF>
+__global__ __launch_bounds__(256) void lab_chunk_kernel(
+    int64_t n_chunks, const int32_t *__restrict__ cs, const int32_t *__restrict__ cg,
+    const int32_t *__restrict__ sf, const int64_t *__restrict__ slice_ptr, const int32_t *__restrict__ perm,
+    const int32_t *__restrict__ col, const double *__restrict__ val, const double *__restrict__ x,
+    double *__restrict__ y, double *part, int32_t *cnt, const int2 *__restrict__ win,
+    uint64_t *__restrict__ stamps)
+{
+    const uint64_t t0 = now();
+    const int64_t nb = gridDim.x, b = blockIdx.x;
+    const int64_t per_x = (nb + 7) / 8;  // blocks b, b + 8, ... run on one XCD: give them consecutive chunks
+    const int64_t wgi = (b % 8) * per_x + b / 8;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x / 64;
+    const int64_t c = wgi * 4 + wv;
+    const int64_t si = ((int64_t)b * 4 + wv) * 3;
+    if (c >= n_chunks) {
+        if (lane == 0) { stamps[si] = t0; stamps[si + 1] = now(); stamps[si + 2] = hw_id(); }
+        return;
+    }
+    const int32_t s = cs[c];
+    const int64_t g0 = cg[c];
+    const int64_t base = slice_ptr[s];
+    const int64_t ng = (slice_ptr[s + 1] - base) / (64 * KI);
+    const int64_t g1 = g0 + G < ng ? g0 + G : ng;
+    double pre = 0.0;
+    if constexpr (PREF) {
+        if (g0 == 0) {
+            const int2 wd = win[s];
+            const int32_t lines = (wd.y - wd.x + 16) / 16;
+            for (int32_t l = lane; l < lines; l += 64)
+                pre += x[wd.x + l * 16];
+        }
+    }
+    const int64_t step = (int64_t)64 * KI;
+    const double *vp = val + base + lane * KI;
+    const int32_t *cp = col + base + lane * KI;
+    typedef typename std::conditional<KI == 1, double, v2f64>::type VT;
+    typedef typename std::conditional<KI == 1, int32_t, v2i32>::type CT;
+    VT v[G];
+    CT cc[G];
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+        const int64_t gg = g0 + u < g1 ? g0 + u : g0;
+        v[u] = __builtin_nontemporal_load(reinterpret_cast<const VT *>(vp + gg * step));
+        cc[u] = __builtin_nontemporal_load(reinterpret_cast<const CT *>(cp + gg * step));
+    }
+    const int32_t row = perm[(int64_t)s * 64 + lane];
+    const int32_t f = sf[s], nc = sf[s + 1] - f;
+    double a[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+        const bool in = g0 + u < g1;
+        if constexpr (KI == 1)
+            a[u % 4] += (in ? v[u] : 0.0) * x[cc[u]];
+        else
+            a[u % 4] += (in ? v[u].x : 0.0) * x[cc[u].x] + (in ? v[u].y : 0.0) * x[cc[u].y];
+    }
+    double sum = (a[0] + a[2]) + (a[1] + a[3]);
+    if (pre == 1.2345e-300)
+        sum += 1.0;  // never: keeps the prefetch loads
+    if (nc == 1) {
+        if (row >= 0)
+            y[row] = sum;
+    } else {
+        double *pp = part + c * 64 + lane;
+        if constexpr (SYNC == 0) {
+            *pp = sum;
+            __threadfence();
+        } else {
+            __hip_atomic_store(pp, sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_s_waitcnt(0);
+        }
+        int old = 0;
+        if (lane == 0)
+            old = __hip_atomic_fetch_add(cnt + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        old = __shfl(old, 0);
+        if (old == nc - 1) {  // the last chunk of s to arrive: add all partials in chunk order
+            if constexpr (SYNC == 0)
+                __threadfence();
+            double acc = 0.0;
+            for (int32_t k0 = 0; k0 < nc; k0 += 8) {
+                double q[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const int64_t ck = f + (k0 + k < nc ? k0 + k : 0);
+                    const double *src = part + ck * 64 + lane;
+                    if constexpr (SYNC == 0)
+                        q[k] = *src;
+                    else
+                        q[k] = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                    if (k0 + k < nc)
+                        acc += f + k0 + k == c ? sum : q[k];
+            }
+            if (row >= 0)
+                y[row] = acc;
+            if (lane == 0)
+                __hip_atomic_store(cnt + s, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    if (lane == 0) { stamps[si] = t0; stamps[si + 1] = now(); stamps[si + 2] = hw_id(); }
 }
 
 // column window of every slice: [min, max] of its stored columns
@@ -331,8 +528,25 @@ int lab_flat(int U, int gather, int64_t n2, const void *val, const void *col, co
     if (U == UU && gather == GG)                                                                          \
         hipLaunchKernelGGL((lab_flat_kernel<UU, GG>), dim3(blocks), dim3(256), 0, s, (const v2f64 *)val,   \
                            (const v2i32 *)col, n2, x, out, stamps);
-    FLAT(2, 0) FLAT(2, 1) FLAT(4, 0) FLAT(4, 1) FLAT(8, 0) FLAT(8, 1) FLAT(4, 2) FLAT(8, 2)
+    FLAT(2, 0) FLAT(2, 1) FLAT(4, 0) FLAT(4, 1) FLAT(8, 0) FLAT(8, 1) FLAT(4, 2) FLAT(8, 2) FLAT(4, 3) FLAT(8, 3)
 #undef FLAT
+    return (int)hipGetLastError();
+}
+
+// chunked SELL: code = KI*1000 + G*10 + SYNC*2 + PREF
+int lab_chunk(int code, int64_t n_chunks, const int32_t *cs, const int32_t *cg, const int32_t *sf,
+              const int64_t *sp, const int32_t *perm, const int32_t *col, const double *val, const double *x,
+              double *y, double *part, int32_t *cnt, const void *win, uint64_t *stamps, void *stream)
+{
+    const hipStream_t s = (hipStream_t)stream;
+    const unsigned blocks = (unsigned)((n_chunks + 3) / 4);
+#define CHUNK(KI, G, SY, PF)                                                                              \
+    if (code == KI * 1000 + G * 10 + SY * 2 + PF)                                                         \
+        hipLaunchKernelGGL((lab_chunk_kernel<KI, G, SY, PF>), dim3(blocks), dim3(256), 0, s, n_chunks, cs, cg, \
+                           sf, sp, perm, col, val, x, y, part, cnt, (const int2 *)win, stamps);
+    CHUNK(1, 8, 0, 0) CHUNK(1, 8, 1, 0) CHUNK(1, 8, 1, 1) CHUNK(1, 16, 1, 0) CHUNK(2, 4, 1, 0) CHUNK(2, 4, 1, 1)
+    CHUNK(2, 8, 1, 0) CHUNK(2, 4, 0, 0)
+#undef CHUNK
     return (int)hipGetLastError();
 }
 
@@ -365,6 +579,7 @@ int lab_run(int code, int xw, int64_t n_slices, const int64_t *sp, const int32_t
                            (size_t)xcap * sizeof(double), s, sp, perm, col, val, x, y, w, xcap, stamps);     \
         break;
         LAB3(2, 4, 12, 1) LAB3(2, 4, 12, 2) LAB3(1, 4, 16, 1) LAB3(1, 4, 16, 2) LAB3(2, 2, 16, 1)
+        LAB3(2, 4, 12, 3) LAB3(1, 4, 16, 3) LAB3(2, 2, 16, 3) LAB3(1, 8, 12, 3) LAB3(2, 8, 6, 3)
 #undef LAB3
     default: return (int)hipErrorInvalidValue;
     }

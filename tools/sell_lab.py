@@ -24,7 +24,7 @@ from cant_single import FLUSH_BYTES, probe_lib  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--codes", default="F40,F41,F42,F80,F81,F82")
+    ap.add_argument("--codes", default="F40,F41,F43,F83,520412,510416,520216,510812,520806,120412,110416")
     ap.add_argument("--reps", type=int, default=20)
     a = ap.parse_args()
     import torch
@@ -37,6 +37,7 @@ def main():
     lab.lab_run.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int64, vp, vp, vp, vp, vp, vp, vp, ctypes.c_int32, vp,
                             vp]
     lab.lab_windows.argtypes = [ctypes.c_int64, vp, vp, vp, vp]
+    lab.lab_chunk.argtypes = [ctypes.c_int, ctypes.c_int64] + [vp] * 14
     lab.lab_flat.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int64, vp, vp, vp, vp, vp, vp]
     P = probe_lib()
     scratch = torch.empty(FLUSH_BYTES, dtype=torch.uint8, device=dev)
@@ -72,6 +73,11 @@ def main():
             ts.append(e0.elapsed_time(e1) * 1e3)
         print(json.dumps({"probe": mode, "event_us": round(float(np.median(ts)), 2)}), flush=True)
     for code in a.codes.split(","):
+        if code.startswith("C"):  # chunked: C + KI*1000 + G*10 + SYNC*2 + PREF, e.g. C1082 = ki 1, G 8, sync 1
+            c = int(code[1:])
+            ki, G, sy = c // 1000, (c // 10) % 100, c % 10
+            chunked(a, torch, lab, P, scratch, sp, mats[ki], m, x, xh, b, ki, G, c, code)
+            continue
         if code.startswith("F"):  # flat one-shot read of the ki = 2 arrays: F<U><gather>
             flat(a, torch, lab, P, scratch, st, sp, mats[2][0], x, b, int(code[1:-1]), int(code[-1]), code)
             continue
@@ -113,6 +119,55 @@ def main():
         span = res["cold"]["span_us"]
         print(json.dumps({"code": code, "ki": ki, "S": S, "U": U, "xwin": xw, "xcap": xcap, **res,
                           "cold_GBs_span": round(b / (span * 1e-6) * 1e-9, 1), "parity_ok": bad == 0}), flush=True)
+
+
+def chunked(a, torch, lab, P, scratch, sp, mat, m, x, xh, b, ki, G, c, code):
+    dm, n, win, xcap = mat
+    A = dm.arrays
+    spt = A["slice_ptr"].cpu().numpy()
+    ng = np.diff(spt) // (64 * ki)
+    nch = np.maximum((ng + G - 1) // G, 1)
+    sf = np.zeros(n + 1, np.int32)
+    np.cumsum(nch, out=sf[1:])
+    cs = np.repeat(np.arange(n, dtype=np.int32), nch)
+    cg = (np.arange(sf[-1]) - np.repeat(sf[:-1], nch)).astype(np.int32) * G
+    dev = x.device
+    t = lambda v: torch.from_numpy(np.ascontiguousarray(v)).to(dev)  # noqa: E731
+    cs_d, cg_d, sf_d = t(cs), t(cg), t(sf)
+    nchunks = int(sf[-1])
+    part = torch.zeros(nchunks * 64, dtype=torch.float64, device=dev)
+    cnt = torch.zeros(n, dtype=torch.int32, device=dev)
+    blocks = (nchunks + 3) // 4
+    stamps = torch.zeros(blocks * 4 * 3, dtype=torch.int64, device=dev)
+    y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
+    res = {}
+    for mode in ("warm", "cold"):
+        spans, durs, late = [], [], []
+        for r in range(a.reps):
+            if mode == "cold":
+                P.spmv_probe_flush(scratch.data_ptr(), FLUSH_BYTES, sp)
+            rc = lab.lab_chunk(c, nchunks, cs_d.data_ptr(), cg_d.data_ptr(), sf_d.data_ptr(), A["slice_ptr"].data_ptr(),
+                               A["perm"].data_ptr(), A["col"].data_ptr(), A["val"].data_ptr(), x.data_ptr(),
+                               y.data_ptr(), part.data_ptr(), cnt.data_ptr(), win.data_ptr(), stamps.data_ptr(), sp)
+            assert rc == 0, rc
+            torch.cuda.synchronize()
+            st = stamps.view(-1, 3).cpu().numpy().astype(np.int64)
+            t0, t1 = st[:, 0], st[:, 1]
+            spans.append((t1.max() - t0.min()) * 10e-3)
+            durs.append(np.median(t1 - t0) * 10e-3)
+            late.append((t0.max() - t0.min()) * 10e-3)
+        res[mode] = {"span_us": round(float(np.median(spans)), 2), "wave_us_med": round(float(np.median(durs)), 2),
+                     "last_start_us": round(float(np.median(late)), 2)}
+    bad, _ = sa.check(m, xh, y.cpu().numpy())
+    y1 = y.clone()
+    lab.lab_chunk(c, nchunks, cs_d.data_ptr(), cg_d.data_ptr(), sf_d.data_ptr(), A["slice_ptr"].data_ptr(),
+                  A["perm"].data_ptr(), A["col"].data_ptr(), A["val"].data_ptr(), x.data_ptr(), y.data_ptr(),
+                  part.data_ptr(), cnt.data_ptr(), win.data_ptr(), stamps.data_ptr(), sp)
+    torch.cuda.synchronize()
+    same = bool(torch.equal(y1.view(torch.int64), y.view(torch.int64)))
+    print(json.dumps({"code": code, "ki": ki, "G": G, "chunks": nchunks, "blocks": blocks, **res,
+                      "cold_GBs_span": round(b / (res["cold"]["span_us"] * 1e-6) * 1e-9, 1), "parity_ok": bad == 0,
+                      "repeat_same_bits": same, "counters_reset": bool((cnt == 0).all().item())}), flush=True)
 
 
 def flat(a, torch, lab, P, scratch, st, sp, dm, x, b, U, gather, code):

@@ -19,6 +19,8 @@
 
 #include "common.h"
 
+#include <type_traits>
+
 namespace spmv {
 
 // Non-temporal matrix loads: SELL-64-1024 0.2955 vs 0.3130 ms and ELL
@@ -107,6 +109,13 @@ struct SlotBatch<1, NT, U> {
         for (int u = 0; u < U; ++u)  // branch-free: a guarded add lets the compiler sink the loads into branches
             a[u] += (g + u < end ? v[u] : 0.0) * xs(c[u]);
     }
+    template <typename XS>
+    __device__ __forceinline__ void fma4(const XS &xs, int64_t g, int64_t end, double *a) const
+    {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            a[u % 4] += (g + u < end ? v[u] : 0.0) * xs(c[u]);
+    }
 };
 
 template <bool NT, int U>
@@ -129,6 +138,15 @@ struct SlotBatch<2, NT, U> {
         for (int u = 0; u < U; ++u) {
             const bool in = g + u < end;
             a[u] += (in ? v[u].x : 0.0) * xs(c[u].x) + (in ? v[u].y : 0.0) * xs(c[u].y);
+        }
+    }
+    template <typename XS>
+    __device__ __forceinline__ void fma4(const XS &xs, int64_t g, int64_t end, double *a) const
+    {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool in = g + u < end;
+            a[u % 4] += (in ? v[u].x : 0.0) * xs(c[u].x) + (in ? v[u].y : 0.0) * xs(c[u].y);
         }
     }
 };
@@ -249,8 +267,15 @@ static bool sell_ystage(int bt, int32_t sigma)
     return bt == 1024 && sigma == 1024;
 }
 
+int sell_small_waves(int32_t C, int64_t n_slices);
+
 static void sell_geometry(int32_t C, int32_t sigma, int64_t n_slices, int *bt, int64_t *blocks)
 {
+    if (sell_small_waves(C, n_slices) > 1) {  // sell_small_kernel: one workgroup (and x window) per slice
+        *bt = C;
+        *blocks = n_slices;
+        return;
+    }
     const int64_t slots = n_slices * C;
     const int64_t windows = sigma > 1 ? (slots + sigma - 1) / sigma : 0;
     const bool wide = windows >= 512 && sigma >= kBlock && sigma <= 1024 &&
@@ -372,29 +397,34 @@ __global__ __launch_bounds__(1024) void sell_xwin_kernel(
 }
 
 // Small matrices (BASELINE.json configs[2]: one cant-like matrix is 976
-// slices of C = 64, i.e. 976 waves for 1,024 SIMDs): with one wave per slice
-// each SIMD holds about one wave, 64 lanes x 4 loads x 12 B = 3 KiB in
-// flight, and every lane walks its ~64-entry row in ~16 dependent round
-// trips — latency-bound, 29-33 % of the HBM peak cold.  Here a workgroup of
-// S waves owns ONE slice and splits its slot columns into S contiguous
-// ranges, one per wave (lane = row of the slice, as before); each lane
-// issues U slot loads at a time, branch-free (past its range it re-reads
-// its range's first slot, the same lines, and adds nothing).  The S partial
-// sums of a row meet in LDS and wave 0 adds them in wave order and stores
-// y[perm].  Deterministic; a row's sum is grouped differently from
-// sell_kernel's, so the bits differ from it (the parity rule holds).
-template <int KI, bool NT, int S, typename XS>
+// slices of C = 64).  With one wave per slice each SIMD holds about one wave
+// and every lane walks its ~64-entry row in dependent round trips.  Here a
+// workgroup of S waves owns ONE slice and cuts its slot columns into S
+// contiguous ranges, one per wave (lane = row of the slice).  Every lane
+// issues the value and column loads of its first G slot groups at once
+// (branch-free: past its range it re-reads its first group, same lines,
+// and adds nothing); with those in flight the workgroup copies the slice's
+// x window into LDS (XWIN), then one barrier and the products.  Groups past
+// G (rows wider than S·G·KI) follow in batches of 4.  The S partial sums
+// of a row meet in LDS and wave 0 adds them in wave order.  Deterministic;
+// XWIN and global gathers give the same bits (same G, same batches); a
+// row's sum is grouped differently from sell_kernel's, so the bits differ
+// from it (the parity rule holds).  Diagnosis (tools/sell_lab.py,
+// profiles/round3/sell_lab*.log): the one-shot batch before the window copy
+// is what moved this kernel; see DESIGN.md §8.
+template <int KI, bool NT, int S, bool XWIN, typename XS>
 __global__ __launch_bounds__(kWave * S) void sell_small_kernel(
     int64_t n_slices, const int64_t *__restrict__ slice_ptr,
     const int32_t *__restrict__ perm, const int32_t *__restrict__ col,
-    const double *__restrict__ val, const XS xs, double *__restrict__ y, int64_t wcap)
+    const double *__restrict__ val, const XS xs, double *__restrict__ y, int64_t wcap,
+    const double *__restrict__ x, const int2 *__restrict__ win, int32_t xcap)
 {
-    constexpr int U = 4;
+    constexpr int G = 24 / KI;  // slot groups in the first, one-shot batch (24 entries per lane)
     constexpr int64_t step = (int64_t)kWave * KI;  // elements between slot groups
+    extern __shared__ double s_x[];
     const int64_t s = blockIdx.x;  // grid = n_slices
     (void)n_slices;
     const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
-    const int32_t row = wv == 0 ? perm[s * kWave + lane] : -1;  // in flight with the stream
     const int64_t base = slice_ptr[s];
     int64_t w = (slice_ptr[s + 1] - base) / kWave;
     w = w < wcap ? w : wcap;
@@ -402,17 +432,37 @@ __global__ __launch_bounds__(kWave * S) void sell_small_kernel(
     const int64_t per = (groups + S - 1) / S;
     const int64_t g0 = wv * per;
     const int64_t g1 = g0 + per < groups ? g0 + per : groups;
+    const bool any = g1 > g0;  // uniform per wave: no loads past the slice
     const double *vp = val + base + lane * KI;
     const int32_t *cp = col + base + lane * KI;
-    double a[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-        a[u] = 0.0;
-    for (int64_t g = g0; g < g1; g += U) {
-        SlotBatch<KI, NT, U> b;
-        b.load(vp, cp, g, g1, step);
-        b.fma(xs, g, g1, a);
+    SlotBatch<KI, NT, G> first;
+    if (any)
+        first.load(vp, cp, g0, g1, step);
+    bool staged = false;
+    int2 wnd = make_int2(0, -1);
+    if constexpr (XWIN) {
+        wnd = win[s];
+        const int32_t span = wnd.y - wnd.x + 1;
+        staged = span > 0 && span <= xcap;  // uniform per workgroup
+        if (staged)
+            copy_window<kWave * S, 8>(s_x, x, wnd.x, span);
+        __syncthreads();
     }
+    const int32_t row = wv == 0 ? perm[s * kWave + lane] : -1;
+    double a[4] = {0.0, 0.0, 0.0, 0.0};
+    auto body = [&](const auto &src) {
+        if (any)
+            first.fma4(src, g0, g1, a);
+        for (int64_t g = g0 + G; g < g1; g += 4) {
+            SlotBatch<KI, NT, 4> b;
+            b.load(vp, cp, g, g1, step);
+            b.fma4(src, g, g1, a);
+        }
+    };
+    if (staged)
+        body(XWindow{s_x, wnd.x});
+    else
+        body(xs);
     double sum = (a[0] + a[2]) + (a[1] + a[3]);
     if constexpr (S > 1) {
         __shared__ double part[S][kWave];
@@ -428,58 +478,66 @@ __global__ __launch_bounds__(kWave * S) void sell_small_kernel(
         y[row] = sum;  // scattered by perm: plain stores, as sell_kernel
 }
 
-// Waves per slice of sell_small_kernel: the smallest power of two that puts
-// about four waves on every SIMD, at most 8; 1 = the one-wave-per-slice
-// kernels.  Only C = 64 (a slice is one wave).
-#ifndef SPMV_SELL_SMALL_S  // A/B builds only (tools/ab): force S (1 = one wave per slice)
-#define SPMV_SELL_SMALL_S 0
-#endif
+// Waves per slice of sell_small_kernel: the smallest power of two (2, 4 or
+// 8) that puts about 3.5 waves on every SIMD; 1 = too many slices for it
+// (the one-wave-per-slice kernels).  Only C = 64 (a slice is one wave).
+// The lab measured S = 4 and 8 within 3 % of each other on cant and S = 2
+// 5 % slower (profiles/round3/sell_lab*.log).
 int sell_small_waves(int32_t C, int64_t n_slices)
 {
     if (C != kWave || n_slices <= 0)
         return 1;
-    if (SPMV_SELL_SMALL_S > 0)
-        return SPMV_SELL_SMALL_S;
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
         cus = 256;
-    const int64_t want = 4 * 4 * (int64_t)cus;  // 4 waves on each of a CU's 4 SIMDs
-    int S = 1;
+    const int64_t want = 14 * (int64_t)cus;  // ~3.5 waves on each of a CU's 4 SIMDs
+    if (n_slices >= want)
+        return 1;
+    int S = 2;
     while (S < 8 && n_slices * S < want)
         S *= 2;
     return S;
 }
 
-template <int KI, bool NT, typename XS>
+template <int KI, bool NT, bool XWIN, typename XS>
 static void launch_sell_small(int S, int64_t n_slices, const int64_t *slice_ptr, const int32_t *perm,
                               const int32_t *col, const double *val, const XS xs, double *y, int64_t wcap,
-                              hipStream_t st)
+                              const double *x, const int2 *win, int32_t xcap, hipStream_t st)
 {
-#define SPMV_SELL_SMALL(SS)                                                                                \
-    hipLaunchKernelGGL((sell_small_kernel<KI, NT, SS, XS>), dim3((unsigned)n_slices), dim3(kWave * SS), 0, st, \
-                       n_slices, slice_ptr, perm, col, val, xs, y, wcap)
+    const size_t lds = XWIN ? (size_t)xcap * sizeof(double) : 0;
+#define SPMV_SELL_SMALL(SS)                                                                                 \
+    hipLaunchKernelGGL((sell_small_kernel<KI, NT, SS, XWIN, XS>), dim3((unsigned)n_slices), dim3(kWave * SS), \
+                       lds, st, n_slices, slice_ptr, perm, col, val, xs, y, wcap, x, win, xcap)
     switch (S) {
     case 2: SPMV_SELL_SMALL(2); break;
     case 4: SPMV_SELL_SMALL(4); break;
-    case 16: SPMV_SELL_SMALL(16); break;
     default: SPMV_SELL_SMALL(8); break;
     }
 #undef SPMV_SELL_SMALL
 }
 
+// x-window variant when win != NULL (per-slice windows from
+// spmv_sell_xwin_build), else gathers through xs.
 template <typename XS>
 static void launch_sell_small_any(int S, int32_t ki, bool nt, int64_t n_slices, const int64_t *slice_ptr,
                                   const int32_t *perm, const int32_t *col, const double *val, const XS xs, double *y,
-                                  int64_t wcap, hipStream_t st)
+                                  int64_t wcap, hipStream_t st, const double *x = nullptr,
+                                  const int2 *win = nullptr, int32_t xcap = 0)
 {
-    if (ki == 2) {
-        if (nt) launch_sell_small<2, true>(S, n_slices, slice_ptr, perm, col, val, xs, y, wcap, st);
-        else launch_sell_small<2, false>(S, n_slices, slice_ptr, perm, col, val, xs, y, wcap, st);
-    } else {
-        if (nt) launch_sell_small<1, true>(S, n_slices, slice_ptr, perm, col, val, xs, y, wcap, st);
-        else launch_sell_small<1, false>(S, n_slices, slice_ptr, perm, col, val, xs, y, wcap, st);
+    if (win) {
+        if constexpr (std::is_same<XS, XGlobal>::value) {
+#define SPMV_SMALL_W(K, N) launch_sell_small<K, N, true>(S, n_slices, slice_ptr, perm, col, val, xs, y, wcap, x, win, xcap, st)
+            if (ki == 2) { if (nt) SPMV_SMALL_W(2, true); else SPMV_SMALL_W(2, false); }
+            else { if (nt) SPMV_SMALL_W(1, true); else SPMV_SMALL_W(1, false); }
+#undef SPMV_SMALL_W
+            return;
+        }
     }
+#define SPMV_SMALL_G(K, N) launch_sell_small<K, N, false>(S, n_slices, slice_ptr, perm, col, val, xs, y, wcap, x, (const int2 *)nullptr, 0, st)
+    if (ki == 2) { if (nt) SPMV_SMALL_G(2, true); else SPMV_SMALL_G(2, false); }
+    else { if (nt) SPMV_SMALL_G(1, true); else SPMV_SMALL_G(1, false); }
+#undef SPMV_SMALL_G
 }
 
 // Wide slices (SELL split plan, spmv_sell_split_plan): a slice wider than
@@ -668,9 +726,9 @@ extern "C" int spmv_sell_run_xwin(spmv_dims d, int32_t C, int32_t sigma, int32_t
         return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_run_xwin: grid too large");
     const bool nt = stream_nt(kSellStreamNtDefault);
     const int S = sell_small_waves(C, n_slices);
-    if (S > 1) {  // few slices: the waves-per-slice kernel (global gathers; same bits as spmv_sell_run)
+    if (S > 1) {  // few slices: the waves-per-slice kernel with per-slice x windows (same bits as spmv_sell_run)
         launch_sell_small_any(S, ki, nt, n_slices, slice_ptr, perm, col, val, XGlobal{x}, y, INT64_MAX,
-                              (hipStream_t)d.stream);
+                              (hipStream_t)d.stream, x, (const int2 *)win, xcap);
         SPMV_CHECK_LAUNCH("sell_small_kernel");
         return SPMV_SUCCESS;
     }
@@ -841,7 +899,8 @@ extern "C" int spmv_sell_run_split(spmv_dims d, int32_t C, int32_t sigma, int32_
     const bool nt = stream_nt(kSellStreamNtDefault);
     const int S = sell_small_waves(C, n_slices);
     if (S > 1) {
-        launch_sell_small_any(S, ki, nt, n_slices, slice_ptr, perm, col, val, XGlobal{x}, y, (int64_t)T, st);
+        launch_sell_small_any(S, ki, nt, n_slices, slice_ptr, perm, col, val, XGlobal{x}, y, (int64_t)T, st, x,
+                              (const int2 *)win, xcap);
     } else if (win) {
         auto kern = ki == 2 ? (nt ? sell_xwin_kernel<2, true, 4> : sell_xwin_kernel<2, false, 4>)
                             : (nt ? sell_xwin_kernel<1, true, 4> : sell_xwin_kernel<1, false, 4>);

@@ -539,7 +539,7 @@ int lab_chunk(int code, int64_t n_chunks, const int32_t *cs, const int32_t *cg, 
               double *y, double *part, int32_t *cnt, const void *win, uint64_t *stamps, void *stream)
 {
     const hipStream_t s = (hipStream_t)stream;
-    const unsigned blocks = (unsigned)((n_chunks + 3) / 4);
+    const unsigned blocks = (unsigned)(((n_chunks + 3) / 4 + 7) / 8 * 8);  // a multiple of 8: the XCD map is a bijection
 #define CHUNK(KI, G, SY, PF)                                                                              \
     if (code == KI * 1000 + G * 10 + SY * 2 + PF)                                                         \
         hipLaunchKernelGGL((lab_chunk_kernel<KI, G, SY, PF>), dim3(blocks), dim3(256), 0, s, n_chunks, cs, cg, \

@@ -24,7 +24,7 @@ from cant_single import FLUSH_BYTES, probe_lib  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--codes", default="F40,F41,F43,F83,520412,510416,520216,510812,520806,120412,110416")
+    ap.add_argument("--codes", default="F40,F41,F42,F43,C1082,C1162,C2082,120412,110416,320412,420412,520412")
     ap.add_argument("--reps", type=int, default=20)
     a = ap.parse_args()
     import torch
@@ -137,7 +137,7 @@ def chunked(a, torch, lab, P, scratch, sp, mat, m, x, xh, b, ki, G, c, code):
     nchunks = int(sf[-1])
     part = torch.zeros(nchunks * 64, dtype=torch.float64, device=dev)
     cnt = torch.zeros(n, dtype=torch.int32, device=dev)
-    blocks = (nchunks + 3) // 4
+    blocks = ((nchunks + 3) // 4 + 7) // 8 * 8
     stamps = torch.zeros(blocks * 4 * 3, dtype=torch.int64, device=dev)
     y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
     res = {}

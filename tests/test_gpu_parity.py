@@ -282,26 +282,58 @@ def test_linearity_and_checksum_full_rmat(torch_dev, rmat_full, fmt):
     assert_parity(m, y.cpu().numpy(), x, y_ref=y_ref)
 
 
-def test_banded_shard_rowsums(torch_dev):
+def test_banded_shard_full_parity(torch_dev):
     """BASELINE.json configs[4]: one of 8 row shards of the 1e8-row banded
-    matrix (1.25e7 rows, 2e8 entries) in CSR and SELL; with x = ones every
-    y_i is the sum of row i's 16 values."""
+    matrix (1.25e7 rows, 2e8 entries) in CSR and SELL, every row checked by
+    the parity rule against the host generator's entries, with x[j] = j and
+    with a random x (a wrong column index changes y; with x = 1 it would
+    not)."""
     torch, dev = torch_dev
     n = 100_000_000
     lo, hi = 3 * n // 8, 4 * n // 8
     ptr, col, val = sa.gen_banded_csr(n, lo, hi)
     rows = hi - lo
-    expect = val.reshape(-1, 16).sum(axis=1)
     m = sa.Coo(rows, n, np.repeat(np.arange(rows, dtype=np.int32), 16), col, val)
-    ones = torch.ones(n, dtype=torch.float64, device=dev)
-    for fmt in ("csr", "sell"):
-        dm = sa.to_device(m, fmt, dev)
-        y = torch.full((rows,), float("nan"), dtype=torch.float64, device=dev)
-        dm.run(ones, y)
-        torch.cuda.synchronize()
-        got = y.cpu().numpy()
-        assert np.allclose(got, expect, rtol=1e-12, atol=1e-12), fmt
-        del dm
+    c2, v2 = col.reshape(-1, 16), val.reshape(-1, 16)
+    xs = {"ramp": sa.ramp_x(n), "random": np.random.default_rng(11).uniform(-1.0, 1.0, n)}
+    for name, xh in xs.items():
+        g = xh[c2]
+        ref = np.zeros(rows)
+        for e in range(16):  # file order
+            ref += v2[:, e] * g[:, e]
+        scale = np.maximum(np.abs(ref), np.sum(np.abs(v2 * g), axis=1))
+        del g
+        x = torch.from_numpy(xh).to(dev)
+        for fmt in ("csr", "sell"):
+            dm = sa.to_device(m, fmt, dev)
+            y = torch.full((rows,), float("nan"), dtype=torch.float64, device=dev)
+            dm.run(x, y)
+            torch.cuda.synchronize()
+            bad = np.abs(y.cpu().numpy() - ref) > 1e-6 * scale
+            assert not bad.any(), (name, fmt, np.nonzero(bad)[0][:5])
+            del dm
+
+
+@pytest.mark.parametrize("fmt", ["csr", "sell"])
+def test_banded_full_matrix_sampled_rows(torch_dev, fmt):
+    """The whole 1e8-row / 1.6e9-entry banded matrix generated in HBM (as
+    bench.py's banded_strong at one GPU): value offsets run to 12.8 GB, past
+    2^31 and 2^32 bytes.  Sampled rows (first / last 512, around the 2-, 4-
+    and 8-way cuts, past the 2^31..2^33-byte offsets, 4,096 spread) checked
+    against the host generator with x[j] = j (bench.banded_check)."""
+    torch, dev = torch_dev
+    from bench import banded_check
+
+    n = 100_000_000
+    dm = sa.banded_to_device(n, fmt, dev, 0, n, **({"ki": 1} if fmt == "sell" else {}))
+    x = torch.from_numpy(sa.ramp_x(n)).to(dev)
+    y = torch.full((n,), float("nan"), dtype=torch.float64, device=dev)
+    dm.run(x, y)
+    torch.cuda.synchronize()
+    k, bad = banded_check(n, 0, n, y)
+    assert k > 6000 and bad is None, (k, bad)
+    del dm, x, y
+    torch.cuda.empty_cache()
 
 
 def test_nondefault_stream(torch_dev):

@@ -75,10 +75,10 @@ int spmv_csr_run(spmv_dims d, const int64_t *row_ptr, const int32_t *col,
  * 1 = direct (each lane group streams its own row's entries),
  * 2 = staged (all 256 lanes of a workgroup stream the workgroup's entry
  *     range through LDS, then each lane group reduces its row from LDS),
- * 3 = staged, persistent workgroups with row-offset prefetch,
- * 5 = staged persistent, software-pipelined (the next chunk's loads are
- *     in flight while the current chunk is reduced).
- * Variants 2, 3 and 5 give bit-identical y.  4 is spmv_csr_run_tiled.  */
+ * 3 = staged, persistent workgroups with row-offset prefetch.
+ * Variants 2 and 3 give bit-identical y (and so does spmv_csr_run_xwin);
+ * any other value is refused (the entry-balanced kernel for skewed rows is
+ * spmv_csr_run_tiled).                                                    */
 int spmv_csr_run_variant(spmv_dims d, const int64_t *row_ptr,
                          const int32_t *col, const double *val,
                          const double *x, double *y, int lanes_per_row,

@@ -745,12 +745,22 @@ static size_t csr_xwin_lds(int mode, int32_t xcap, int64_t gpw, int rpb)
 // (L = 2, 128-row groups of 2,048 entries) 0.7534 ms with one-group windows
 // (MODE 0) against 0.7261 ms with two (profiles/round2/ab_banded3.log);
 // explicit rows_per_window: at least one group.  Same chunks, same bits.
-static int64_t csr_xwin_gpw(int L, int32_t rows_per_window)
+// A small matrix (fewer than 4 default windows per CU) gets one-group
+// windows instead, twice the workgroups to spread over the CUs: one
+// cant-like matrix (488 windows of 128 rows) 13.28 vs 13.74 us cold, 10.5 vs
+// 12.1 us warm (rocprof, profiles/round3/cant_single_csr_windows.log).
+static int64_t csr_xwin_gpw(int L, int32_t rows_per_window, int64_t n_rows)
 {
     const int64_t rpb = kBlock / L;
-    const int64_t rows = rows_per_window > 0 ? rows_per_window : kCsrXwinRows;
-    const int64_t g = (rows + rpb - 1) / rpb;
-    return g < (rows_per_window > 0 ? 1 : 2) ? (rows_per_window > 0 ? 1 : 2) : g;
+    if (rows_per_window > 0) {
+        const int64_t g = (rows_per_window + rpb - 1) / rpb;
+        return g < 1 ? 1 : g;
+    }
+    int64_t g = (kCsrXwinRows + rpb - 1) / rpb;
+    g = g < 2 ? 2 : g;
+    if (n_rows < 4 * (int64_t)cu_count() * g * rpb)
+        g = 1;
+    return g;
 }
 
 template <int L, int R, bool NT, typename Cols, typename V = double>
@@ -834,7 +844,7 @@ extern "C" size_t spmv_csr_xwin_bytes(int64_t n_rows, int64_t nnz, int lanes_per
     const int L = lanes_per_row > 0 ? lanes_per_row : spmv_csr_auto_lanes(n_rows, nnz);
     if (L < 2 || L > 64 || (L & (L - 1)) || n_rows <= 0 || rows_per_window < 0)
         return 0;
-    const int64_t rpw = csr_xwin_gpw(L, rows_per_window) * (kBlock / L);
+    const int64_t rpw = csr_xwin_gpw(L, rows_per_window, n_rows) * (kBlock / L);
     return (size_t)((n_rows + rpw - 1) / rpw) * sizeof(int2);
 }
 
@@ -854,7 +864,7 @@ extern "C" int spmv_csr_xwin_build(spmv_dims d, const int64_t *row_ptr, const in
     if (!win || win_bytes < need)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_xwin_build: window buffer too small");
     SPMV_GUARD(d);
-    const int64_t rpw = csr_xwin_gpw(L, rows_per_window) * (kBlock / L);
+    const int64_t rpw = csr_xwin_gpw(L, rows_per_window, d.n_rows) * (kBlock / L);
     const int64_t n_win = (d.n_rows + rpw - 1) / rpw;
     const hipStream_t st = (hipStream_t)d.stream;
     hipLaunchKernelGGL(csr_window_kernel, dim3((unsigned)n_win), dim3(kBlock), 0, st, d.n_rows, rpw, row_ptr,
@@ -911,7 +921,7 @@ extern "C" int spmv_csr_run_xwin(spmv_dims d, const int64_t *row_ptr, const int3
         return rc;
     SPMV_GUARD(d);
     rc = launch_xwin_any(d, L, row_ptr, MakeCol32{col}, val, x, y, (const int2 *)win, xcap,
-                         csr_xwin_gpw(L, rows_per_window));
+                         csr_xwin_gpw(L, rows_per_window, d.n_rows));
     if (rc != SPMV_SUCCESS)
         return rc;
     SPMV_CHECK_LAUNCH("csr_xwin_kernel");
@@ -968,7 +978,7 @@ extern "C" int spmv_csr16_run_xwin(spmv_dims d, const int64_t *row_ptr, const in
         return fail_msg(SPMV_OTHER_ERROR, "spmv_csr16_run_xwin: missing index arrays");
     SPMV_GUARD(d);
     rc = launch_xwin_any(d, L, row_ptr, MakeCol16{blk_base, col_off, col_esc}, val, x, y, (const int2 *)win, xcap,
-                         csr_xwin_gpw(L, rows_per_window));
+                         csr_xwin_gpw(L, rows_per_window, d.n_rows));
     if (rc != SPMV_SUCCESS)
         return rc;
     SPMV_CHECK_LAUNCH("csr_xwin_kernel (16-bit columns)");
@@ -989,7 +999,7 @@ extern "C" int spmv_csr_f32v_run_xwin(spmv_dims d, const int64_t *row_ptr, const
     if (rc != SPMV_SUCCESS || d.n_rows == 0)
         return rc;
     SPMV_GUARD(d);
-    const int64_t gpw = csr_xwin_gpw(L, rows_per_window);
+    const int64_t gpw = csr_xwin_gpw(L, rows_per_window, d.n_rows);
     const int64_t groups = (d.n_rows + kBlock / L - 1) / (kBlock / L);
     if ((groups + gpw - 1) / gpw > INT32_MAX)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_f32v_run_xwin: grid too large");

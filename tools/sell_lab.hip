@@ -479,6 +479,119 @@ __global__ __launch_bounds__(256) void lab_chunk_kernel(
     if (lane == 0) { stamps[si] = t0; stamps[si + 1] = now(); stamps[si + 2] = hw_id(); }
 }
 
+// P consecutive slices (one sigma window holds 16) per workgroup, S waves
+// per slice, one x-window copy for all P: the union of their windows.  Same
+// one-shot first batch of G groups as lab2_kernel (loads issued before the
+// window copy).  Cuts the window-copy traffic P-fold.
+template <int KI, int S, int P, int G>
+__global__ __launch_bounds__(kWave * S * P) void lab4_kernel(int64_t n_slices, const int64_t *__restrict__ slice_ptr,
+                                                             const int32_t *__restrict__ perm,
+                                                             const int32_t *__restrict__ col,
+                                                             const double *__restrict__ val,
+                                                             const double *__restrict__ x, double *__restrict__ y,
+                                                             const int2 *__restrict__ win, int32_t xcap,
+                                                             uint64_t *__restrict__ stamps)
+{
+    const uint64_t t0 = now();
+    extern __shared__ double s_x[];
+    const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+    const int64_t s = (int64_t)blockIdx.x * P + wv / S;
+    const int ws = wv % S;
+    const bool live = s < n_slices;
+    const int64_t base = live ? slice_ptr[s] : 0;
+    const int64_t w = live ? (slice_ptr[s + 1] - base) / kWave : 0;
+    const int64_t groups = w / KI;
+    const int64_t per = (groups + S - 1) / S;
+    const int64_t g0 = ws * per;
+    const int64_t g1 = g0 + per < groups ? g0 + per : groups;
+    const int64_t step = (int64_t)kWave * KI;
+    const double *vp = val + base + lane * KI;
+    const int32_t *cp = col + base + lane * KI;
+    typedef typename std::conditional<KI == 1, double, v2f64>::type VT;
+    typedef typename std::conditional<KI == 1, int32_t, v2i32>::type CT;
+    VT v[G];
+    CT c[G];
+    const bool any = live && g1 > g0;
+    if (any) {
+#pragma unroll
+        for (int u = 0; u < G; ++u) {
+            const int64_t gg = g0 + u < g1 ? g0 + u : g0;
+            v[u] = __builtin_nontemporal_load(reinterpret_cast<const VT *>(vp + gg * step));
+            c[u] = __builtin_nontemporal_load(reinterpret_cast<const CT *>(cp + gg * step));
+        }
+    }
+    // union window of the P slices
+    int lo = INT32_MAX, hi = INT32_MIN;
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+        const int64_t sk = (int64_t)blockIdx.x * P + k;
+        if (sk < n_slices) {
+            const int2 wd = win[sk];
+            if (wd.y >= wd.x) {
+                lo = wd.x < lo ? wd.x : lo;
+                hi = wd.y > hi ? wd.y : hi;
+            }
+        }
+    }
+    const int32_t span = hi >= lo ? hi - lo + 1 : 0;
+    const bool staged = span > 0 && span <= xcap;
+    if (staged) {
+        constexpr int T = kWave * S * P, CU = 8;
+        for (int32_t b0 = 0; b0 < span; b0 += CU * T) {
+            double t[CU];
+#pragma unroll
+            for (int k = 0; k < CU; ++k) {
+                const int32_t i = b0 + threadIdx.x + k * T;
+                t[k] = x[lo + (i < span ? i : span - 1)];
+            }
+#pragma unroll
+            for (int k = 0; k < CU; ++k) {
+                const int32_t i = b0 + threadIdx.x + k * T;
+                if (i < span)
+                    s_x[i] = t[k];
+            }
+        }
+    }
+    const int32_t row = live && ws == 0 ? perm[s * kWave + lane] : -1;
+    __syncthreads();
+    double a[4] = {0.0, 0.0, 0.0, 0.0};
+    auto body = [&](auto xs) {
+        if (any) {
+#pragma unroll
+            for (int u = 0; u < G; ++u) {
+                const bool in = g0 + u < g1;
+                if constexpr (KI == 1)
+                    a[u % 4] += (in ? v[u] : 0.0) * xs(c[u]);
+                else
+                    a[u % 4] += (in ? v[u].x : 0.0) * xs(c[u].x) + (in ? v[u].y : 0.0) * xs(c[u].y);
+            }
+        }
+        if (any && g0 + G < g1)
+            slots<KI, 4>(vp, cp, g0 + G, g1, step, xs, a);
+    };
+    if (staged)
+        body(XW{s_x, lo});
+    else
+        body(XG{x});
+    double sum = (a[0] + a[2]) + (a[1] + a[3]);
+    __shared__ double part[S * P][kWave];
+    if constexpr (S > 1) {
+        part[wv][lane] = sum;
+        __syncthreads();
+        if (ws == 0)
+            for (int k = 1; k < S; ++k)
+                sum += part[wv + k][lane];
+    }
+    if (row >= 0)
+        y[row] = sum;
+    if (lane == 0) {
+        const int64_t i = ((int64_t)blockIdx.x * S * P + wv) * 3;
+        stamps[i] = t0;
+        stamps[i + 1] = now();
+        stamps[i + 2] = hw_id();
+    }
+}
+
 // column window of every slice: [min, max] of its stored columns
 __global__ void lab_window_kernel(const int64_t *__restrict__ slice_ptr, const int32_t *__restrict__ col,
                                   int2 *__restrict__ win)
@@ -547,6 +660,26 @@ int lab_chunk(int code, int64_t n_chunks, const int32_t *cs, const int32_t *cg, 
     CHUNK(1, 8, 0, 0) CHUNK(1, 8, 1, 0) CHUNK(1, 8, 1, 1) CHUNK(1, 16, 1, 0) CHUNK(2, 4, 1, 0) CHUNK(2, 4, 1, 1)
     CHUNK(2, 8, 1, 0) CHUNK(2, 4, 0, 0)
 #undef CHUNK
+    return (int)hipGetLastError();
+}
+
+// multi-slice workgroups: code = KI*10000 + S*1000 + P*100 + G
+int lab_multi(int code, int64_t n_slices, const int64_t *sp, const int32_t *perm, const int32_t *col,
+              const double *val, const double *x, double *y, const void *win, int32_t xcap, uint64_t *stamps,
+              void *stream)
+{
+    const hipStream_t s = (hipStream_t)stream;
+#define MULTI(KI, S, P, G)                                                                                \
+    if (code == KI * 10000 + S * 1000 + P * 100 + G)                                                      \
+        hipLaunchKernelGGL((lab4_kernel<KI, S, P, G>), dim3((unsigned)((n_slices + P - 1) / P)),           \
+                           dim3(kWave * S * P), (size_t)xcap * sizeof(double), s, n_slices, sp, perm, col, val, x, y, \
+                           (const int2 *)win, xcap, stamps);
+    MULTI(1, 4, 1, 24) MULTI(1, 4, 2, 24) MULTI(1, 4, 4, 24) MULTI(1, 2, 2, 24) MULTI(1, 2, 4, 24)
+    MULTI(1, 1, 4, 24) MULTI(2, 4, 2, 12) MULTI(2, 2, 4, 12) MULTI(1, 2, 8, 24) MULTI(1, 1, 8, 24)
+    MULTI(1, 2, 4, 16) MULTI(1, 2, 4, 12) MULTI(2, 2, 4, 8) MULTI(1, 4, 2, 16) MULTI(2, 4, 2, 8)
+    MULTI(1, 2, 2, 16) MULTI(2, 2, 2, 12) MULTI(2, 2, 8, 12) MULTI(2, 1, 4, 12) MULTI(1, 4, 1, 16)
+    MULTI(2, 4, 1, 12)
+#undef MULTI
     return (int)hipGetLastError();
 }
 

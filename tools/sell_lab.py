@@ -24,7 +24,7 @@ from cant_single import FLUSH_BYTES, probe_lib  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--codes", default="F40,F41,F42,F43,C1082,C1162,C2082,120412,110416,320412,420412,520412")
+    ap.add_argument("--codes", default="M14116,M24112,M22412,M12416,M12412,M22408,M14216,M24208,M12216,M22212,M22812,M21412,M22412,M14116")
     ap.add_argument("--reps", type=int, default=20)
     a = ap.parse_args()
     import torch
@@ -38,6 +38,7 @@ def main():
                             vp]
     lab.lab_windows.argtypes = [ctypes.c_int64, vp, vp, vp, vp]
     lab.lab_chunk.argtypes = [ctypes.c_int, ctypes.c_int64] + [vp] * 14
+    lab.lab_multi.argtypes = [ctypes.c_int, ctypes.c_int64] + [vp] * 7 + [ctypes.c_int32, vp, vp]
     lab.lab_flat.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int64, vp, vp, vp, vp, vp, vp]
     P = probe_lib()
     scratch = torch.empty(FLUSH_BYTES, dtype=torch.uint8, device=dev)
@@ -73,6 +74,44 @@ def main():
             ts.append(e0.elapsed_time(e1) * 1e3)
         print(json.dumps({"probe": mode, "event_us": round(float(np.median(ts)), 2)}), flush=True)
     for code in a.codes.split(","):
+        if code.startswith("M"):  # multi-slice workgroups: M + KI*10000 + S*1000 + P*100 + G
+            c = int(code[1:])
+            ki, S, P2, G = c // 10000, (c // 1000) % 10, (c // 100) % 10, c % 100
+            dm, n, win, xcap = mats[ki]
+            A = dm.arrays
+            nb = (n + P2 - 1) // P2
+            stamps = torch.zeros(nb * S * P2 * 3, dtype=torch.int64, device=dev)
+            y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
+            # the union window of P slices can exceed the per-slice xcap: give the lab its own cap
+            cap = 2048 if P2 > 1 else xcap
+
+            def run_m():
+                rc = lab.lab_multi(c, n, A["slice_ptr"].data_ptr(), A["perm"].data_ptr(), A["col"].data_ptr(),
+                                   A["val"].data_ptr(), x.data_ptr(), y.data_ptr(), win.data_ptr(), cap,
+                                   stamps.data_ptr(), sp)
+                assert rc == 0, rc
+
+            res = {}
+            for mode in ("warm", "cold"):
+                spans, durs, late = [], [], []
+                for r in range(a.reps):
+                    if mode == "cold":
+                        P.spmv_probe_flush(scratch.data_ptr(), FLUSH_BYTES, sp)
+                    run_m()
+                    torch.cuda.synchronize()
+                    st_ = stamps.view(-1, 3).cpu().numpy().astype(np.int64)
+                    t0, t1 = st_[:, 0], st_[:, 1]
+                    spans.append((t1.max() - t0.min()) * 10e-3)
+                    durs.append(np.median(t1 - t0) * 10e-3)
+                    late.append((t0.max() - t0.min()) * 10e-3)
+                res[mode] = {"span_us": round(float(np.median(spans)), 2),
+                             "wave_us_med": round(float(np.median(durs)), 2),
+                             "last_start_us": round(float(np.median(late)), 2)}
+            bad, _ = sa.check(m, xh, y.cpu().numpy())
+            print(json.dumps({"code": code, "ki": ki, "S": S, "P": P2, "G": G, "cap": cap, **res,
+                              "cold_GBs_span": round(b / (res["cold"]["span_us"] * 1e-6) * 1e-9, 1),
+                              "parity_ok": bad == 0}), flush=True)
+            continue
         if code.startswith("C"):  # chunked: C + KI*1000 + G*10 + SYNC*2 + PREF, e.g. C1082 = ki 1, G 8, sync 1
             c = int(code[1:])
             ki, G, sy = c // 1000, (c // 10) % 100, c % 10

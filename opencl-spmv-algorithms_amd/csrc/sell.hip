@@ -267,13 +267,15 @@ static bool sell_ystage(int bt, int32_t sigma)
     return bt == 1024 && sigma == 1024;
 }
 
-int sell_small_waves(int32_t C, int64_t n_slices);
+bool sell_small(int32_t C, int64_t n_slices);
+constexpr int kSellSmallS = 2;  // sell_small_kernel: waves per slice
+constexpr int kSellSmallP = 4;  // sell_small_kernel: slices per workgroup (and per x window)
 
 static void sell_geometry(int32_t C, int32_t sigma, int64_t n_slices, int *bt, int64_t *blocks)
 {
-    if (sell_small_waves(C, n_slices) > 1) {  // sell_small_kernel: one workgroup (and x window) per slice
-        *bt = C;
-        *blocks = n_slices;
+    if (sell_small(C, n_slices)) {  // sell_small_kernel: one workgroup (and x window) per 4 slices
+        *bt = C * kSellSmallP;
+        *blocks = (n_slices + kSellSmallP - 1) / kSellSmallP;
         return;
     }
     const int64_t slots = n_slices * C;
@@ -399,38 +401,44 @@ __global__ __launch_bounds__(1024) void sell_xwin_kernel(
 // Small matrices (BASELINE.json configs[2]: one cant-like matrix is 976
 // slices of C = 64).  With one wave per slice each SIMD holds about one wave
 // and every lane walks its ~64-entry row in dependent round trips.  Here a
-// workgroup of S waves owns ONE slice and cuts its slot columns into S
-// contiguous ranges, one per wave (lane = row of the slice).  Every lane
-// issues the value and column loads of its first G slot groups at once
-// (branch-free: past its range it re-reads its first group, same lines,
-// and adds nothing); with those in flight the workgroup copies the slice's
-// x window into LDS (XWIN), then one barrier and the products.  Groups past
-// G (rows wider than S·G·KI) follow in batches of 4.  The S partial sums
-// of a row meet in LDS and wave 0 adds them in wave order.  Deterministic;
-// XWIN and global gathers give the same bits (same G, same batches); a
-// row's sum is grouped differently from sell_kernel's, so the bits differ
-// from it (the parity rule holds).  Diagnosis (tools/sell_lab.py,
-// profiles/round3/sell_lab*.log): the one-shot batch before the window copy
-// is what moved this kernel; see DESIGN.md §8.
-template <int KI, bool NT, int S, bool XWIN, typename XS>
-__global__ __launch_bounds__(kWave * S) void sell_small_kernel(
+// workgroup owns P consecutive slices (one σ-window of 1024 rows holds 16)
+// with S waves per slice; each wave takes a contiguous range of its slice's
+// slot columns (lane = row of the slice).  Every lane issues the value and
+// column loads of its first G slot groups at once (branch-free: past its
+// range it re-reads its first group, same lines, and adds nothing); with
+// those in flight the workgroup copies ONE x window, the union of its P
+// slices' columns (XWIN: windows built per workgroup by spmv_sell_xwin_build),
+// into LDS, then one barrier and the products.  Groups past G follow in
+// batches of 4.  The S partial sums of a row meet in LDS and the slice's
+// first wave adds them in wave order.  Deterministic; XWIN and global
+// gathers give the same bits (same S, G and batches; P only groups slices);
+// a row's sum is grouped differently from sell_kernel's, so the bits differ
+// from it (the parity rule holds).  Shape from tools/sell_lab.py (cold
+// spans, cant-like single, profiles/round3/sell_lab_multi_slice*.log): one
+// slice per workgroup copied a 1,572-entry window per 64 rows (12 MB of L2
+// reads for a 49 MB matrix); four slices share it.
+template <int KI> constexpr int sell_small_g() { return 8; }  // first-batch slot groups per lane
+
+template <int KI, bool NT, bool XWIN, typename XS>
+__global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell_small_kernel(
     int64_t n_slices, const int64_t *__restrict__ slice_ptr,
     const int32_t *__restrict__ perm, const int32_t *__restrict__ col,
     const double *__restrict__ val, const XS xs, double *__restrict__ y, int64_t wcap,
     const double *__restrict__ x, const int2 *__restrict__ win, int32_t xcap)
 {
-    constexpr int G = 24 / KI;  // slot groups in the first, one-shot batch (24 entries per lane)
+    constexpr int S = kSellSmallS, P = kSellSmallP, G = sell_small_g<KI>();
     constexpr int64_t step = (int64_t)kWave * KI;  // elements between slot groups
     extern __shared__ double s_x[];
-    const int64_t s = blockIdx.x;  // grid = n_slices
-    (void)n_slices;
     const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
-    const int64_t base = slice_ptr[s];
-    int64_t w = (slice_ptr[s + 1] - base) / kWave;
+    const int64_t s = (int64_t)blockIdx.x * P + wv / S;
+    const int ws = wv % S;  // wave within its slice
+    const bool live = s < n_slices;  // uniform per wave
+    const int64_t base = live ? slice_ptr[s] : 0;
+    int64_t w = live ? (slice_ptr[s + 1] - base) / kWave : 0;
     w = w < wcap ? w : wcap;
     const int64_t groups = w / KI;
     const int64_t per = (groups + S - 1) / S;
-    const int64_t g0 = wv * per;
+    const int64_t g0 = ws * per;
     const int64_t g1 = g0 + per < groups ? g0 + per : groups;
     const bool any = g1 > g0;  // uniform per wave: no loads past the slice
     const double *vp = val + base + lane * KI;
@@ -441,14 +449,14 @@ __global__ __launch_bounds__(kWave * S) void sell_small_kernel(
     bool staged = false;
     int2 wnd = make_int2(0, -1);
     if constexpr (XWIN) {
-        wnd = win[s];
+        wnd = win[blockIdx.x];
         const int32_t span = wnd.y - wnd.x + 1;
         staged = span > 0 && span <= xcap;  // uniform per workgroup
         if (staged)
-            copy_window<kWave * S, 8>(s_x, x, wnd.x, span);
+            copy_window<kWave * S * P, 4>(s_x, x, wnd.x, span);
         __syncthreads();
     }
-    const int32_t row = wv == 0 ? perm[s * kWave + lane] : -1;
+    const int32_t row = live && ws == 0 ? perm[s * kWave + lane] : -1;
     double a[4] = {0.0, 0.0, 0.0, 0.0};
     auto body = [&](const auto &src) {
         if (any)
@@ -464,77 +472,61 @@ __global__ __launch_bounds__(kWave * S) void sell_small_kernel(
     else
         body(xs);
     double sum = (a[0] + a[2]) + (a[1] + a[3]);
-    if constexpr (S > 1) {
-        __shared__ double part[S][kWave];
-        part[wv][lane] = sum;
-        __syncthreads();
-        if (wv == 0) {
+    __shared__ double part[S * P][kWave];
+    part[wv][lane] = sum;
+    __syncthreads();
+    if (ws == 0) {
 #pragma unroll
-            for (int k = 1; k < S; ++k)
-                sum += part[k][lane];
-        }
+        for (int k = 1; k < S; ++k)
+            sum += part[wv + k][lane];
     }
     if (row >= 0)
         y[row] = sum;  // scattered by perm: plain stores, as sell_kernel
 }
 
-// Waves per slice of sell_small_kernel: the smallest power of two (2, 4 or
-// 8) that puts about 3.5 waves on every SIMD; 1 = too many slices for it
-// (the one-wave-per-slice kernels).  Only C = 64 (a slice is one wave).
-// The lab measured S = 4 and 8 within 3 % of each other on cant and S = 2
-// 5 % slower (profiles/round3/sell_lab*.log).
-int sell_small_waves(int32_t C, int64_t n_slices)
+// Whether sell_small_kernel runs: C = 64 (a slice is one wave) and fewer
+// slices than ~3.5 waves per SIMD of one-wave-per-slice kernels would fill.
+bool sell_small(int32_t C, int64_t n_slices)
 {
     if (C != kWave || n_slices <= 0)
-        return 1;
+        return false;
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
         cus = 256;
-    const int64_t want = 14 * (int64_t)cus;  // ~3.5 waves on each of a CU's 4 SIMDs
-    if (n_slices >= want)
-        return 1;
-    int S = 2;
-    while (S < 8 && n_slices * S < want)
-        S *= 2;
-    return S;
+    return n_slices < 14 * (int64_t)cus;
 }
 
 template <int KI, bool NT, bool XWIN, typename XS>
-static void launch_sell_small(int S, int64_t n_slices, const int64_t *slice_ptr, const int32_t *perm,
-                              const int32_t *col, const double *val, const XS xs, double *y, int64_t wcap,
-                              const double *x, const int2 *win, int32_t xcap, hipStream_t st)
+static void launch_sell_small(int64_t n_slices, const int64_t *slice_ptr, const int32_t *perm, const int32_t *col,
+                              const double *val, const XS xs, double *y, int64_t wcap, const double *x,
+                              const int2 *win, int32_t xcap, hipStream_t st)
 {
     const size_t lds = XWIN ? (size_t)xcap * sizeof(double) : 0;
-#define SPMV_SELL_SMALL(SS)                                                                                 \
-    hipLaunchKernelGGL((sell_small_kernel<KI, NT, SS, XWIN, XS>), dim3((unsigned)n_slices), dim3(kWave * SS), \
-                       lds, st, n_slices, slice_ptr, perm, col, val, xs, y, wcap, x, win, xcap)
-    switch (S) {
-    case 2: SPMV_SELL_SMALL(2); break;
-    case 4: SPMV_SELL_SMALL(4); break;
-    default: SPMV_SELL_SMALL(8); break;
-    }
-#undef SPMV_SELL_SMALL
+    const int64_t blocks = (n_slices + kSellSmallP - 1) / kSellSmallP;
+    hipLaunchKernelGGL((sell_small_kernel<KI, NT, XWIN, XS>), dim3((unsigned)blocks),
+                       dim3(kWave * kSellSmallS * kSellSmallP), lds, st, n_slices, slice_ptr, perm, col, val, xs, y,
+                       wcap, x, win, xcap);
 }
 
-// x-window variant when win != NULL (per-slice windows from
-// spmv_sell_xwin_build), else gathers through xs.
+// x-window variant when win != NULL (windows from spmv_sell_xwin_build:
+// one per workgroup of kSellSmallP slices), else gathers through xs.
 template <typename XS>
-static void launch_sell_small_any(int S, int32_t ki, bool nt, int64_t n_slices, const int64_t *slice_ptr,
+static void launch_sell_small_any(int32_t ki, bool nt, int64_t n_slices, const int64_t *slice_ptr,
                                   const int32_t *perm, const int32_t *col, const double *val, const XS xs, double *y,
                                   int64_t wcap, hipStream_t st, const double *x = nullptr,
                                   const int2 *win = nullptr, int32_t xcap = 0)
 {
     if (win) {
         if constexpr (std::is_same<XS, XGlobal>::value) {
-#define SPMV_SMALL_W(K, N) launch_sell_small<K, N, true>(S, n_slices, slice_ptr, perm, col, val, xs, y, wcap, x, win, xcap, st)
+#define SPMV_SMALL_W(K, N) launch_sell_small<K, N, true>(n_slices, slice_ptr, perm, col, val, xs, y, wcap, x, win, xcap, st)
             if (ki == 2) { if (nt) SPMV_SMALL_W(2, true); else SPMV_SMALL_W(2, false); }
             else { if (nt) SPMV_SMALL_W(1, true); else SPMV_SMALL_W(1, false); }
 #undef SPMV_SMALL_W
             return;
         }
     }
-#define SPMV_SMALL_G(K, N) launch_sell_small<K, N, false>(S, n_slices, slice_ptr, perm, col, val, xs, y, wcap, x, (const int2 *)nullptr, 0, st)
+#define SPMV_SMALL_G(K, N) launch_sell_small<K, N, false>(n_slices, slice_ptr, perm, col, val, xs, y, wcap, x, (const int2 *)nullptr, 0, st)
     if (ki == 2) { if (nt) SPMV_SMALL_G(2, true); else SPMV_SMALL_G(2, false); }
     else { if (nt) SPMV_SMALL_G(1, true); else SPMV_SMALL_G(1, false); }
 #undef SPMV_SMALL_G
@@ -617,6 +609,18 @@ constexpr int32_t kXwinCapNarrow = 2048; // 16 KiB per 256-slot workgroup
 
 }  // namespace spmv
 
+// k-interleave for a SELL matrix of n_rows built for this device: 2 when
+// the small-matrix kernel will run it (16-byte value loads: cant-like single
+// 11.3-11.4 vs 12.1-12.2 us cold span with ki = 1, tools/sell_lab.py,
+// profiles/round3/sell_lab_multi_slice3.log), else 1 (the σ-window kernel's
+// measured best, profiles/round1/sweeps.md).
+extern "C" int spmv_sell_auto_ki(int64_t n_rows, int32_t C)
+{
+    if (n_rows <= 0 || C <= 0)
+        return 1;
+    return sell_small(C, (n_rows + C - 1) / C) ? 2 : 1;
+}
+
 extern "C" int spmv_sell_run(spmv_dims d, int32_t C, int32_t sigma, int32_t ki,
                              int64_t n_slices, const int64_t *slice_ptr,
                              const int32_t *perm, const int32_t *col,
@@ -635,9 +639,8 @@ extern "C" int spmv_sell_run(spmv_dims d, int32_t C, int32_t sigma, int32_t ki,
         return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_run: grid too large");
     const int remap = xcd_remap_enabled() ? 1 : 0;
     const bool nt = stream_nt(kSellStreamNtDefault);
-    const int S = sell_small_waves(C, n_slices);
-    if (S > 1) {
-        launch_sell_small_any(S, ki, nt, n_slices, slice_ptr, perm, col, val, XGlobal{x}, y, INT64_MAX,
+    if (sell_small(C, n_slices)) {
+        launch_sell_small_any(ki, nt, n_slices, slice_ptr, perm, col, val, XGlobal{x}, y, INT64_MAX,
                               (hipStream_t)d.stream);
         SPMV_CHECK_LAUNCH("sell_small_kernel");
         return SPMV_SUCCESS;
@@ -725,9 +728,8 @@ extern "C" int spmv_sell_run_xwin(spmv_dims d, int32_t C, int32_t sigma, int32_t
     if (blocks > INT32_MAX)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_run_xwin: grid too large");
     const bool nt = stream_nt(kSellStreamNtDefault);
-    const int S = sell_small_waves(C, n_slices);
-    if (S > 1) {  // few slices: the waves-per-slice kernel with per-slice x windows (same bits as spmv_sell_run)
-        launch_sell_small_any(S, ki, nt, n_slices, slice_ptr, perm, col, val, XGlobal{x}, y, INT64_MAX,
+    if (sell_small(C, n_slices)) {  // few slices: the waves-per-slice kernel with per-slice x windows (same bits as spmv_sell_run)
+        launch_sell_small_any(ki, nt, n_slices, slice_ptr, perm, col, val, XGlobal{x}, y, INT64_MAX,
                               (hipStream_t)d.stream, x, (const int2 *)win, xcap);
         SPMV_CHECK_LAUNCH("sell_small_kernel");
         return SPMV_SUCCESS;
@@ -897,9 +899,8 @@ extern "C" int spmv_sell_run_split(spmv_dims d, int32_t C, int32_t sigma, int32_
         return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_run_split: grid too large");
     const hipStream_t st = (hipStream_t)d.stream;
     const bool nt = stream_nt(kSellStreamNtDefault);
-    const int S = sell_small_waves(C, n_slices);
-    if (S > 1) {
-        launch_sell_small_any(S, ki, nt, n_slices, slice_ptr, perm, col, val, XGlobal{x}, y, (int64_t)T, st, x,
+    if (sell_small(C, n_slices)) {
+        launch_sell_small_any(ki, nt, n_slices, slice_ptr, perm, col, val, XGlobal{x}, y, (int64_t)T, st, x,
                               (const int2 *)win, xcap);
     } else if (win) {
         auto kern = ki == 2 ? (nt ? sell_xwin_kernel<2, true, 4> : sell_xwin_kernel<2, false, 4>)
@@ -968,9 +969,8 @@ extern "C" int spmv_sell_run_hot(spmv_dims d, int32_t C, int32_t sigma, int32_t 
                            H, hot, x, xh);
     const XHot xs{x, xh, (int32_t)d.n_cols};
     const bool nt = stream_nt(kSellStreamNtDefault);
-    const int S = sell_small_waves(C, n_slices);
-    if (S > 1) {
-        launch_sell_small_any(S, ki, nt, n_slices, slice_ptr, perm, col_hot, val, xs, y, (int64_t)T, st);
+    if (sell_small(C, n_slices)) {
+        launch_sell_small_any(ki, nt, n_slices, slice_ptr, perm, col_hot, val, xs, y, (int64_t)T, st);
     } else {
         auto kern = ki == 2 ? (nt ? sell_kernel<2, true, 4, XHot> : sell_kernel<2, false, 4, XHot>)
                             : (nt ? sell_kernel<1, true, 4, XHot> : sell_kernel<1, false, 4, XHot>);

@@ -208,6 +208,11 @@ int spmv_hyb_run(spmv_dims d, int32_t K, int64_t ld, int32_t ki, const int32_t *
  * the sorting window the builder used (1 = none; else a multiple of C):
  * one workgroup covers one window so its scattered y stores merge in one
  * L2.                                                                    */
+/* k-interleave the SELL builders should use for an n_rows matrix on the
+ * current device (2 for matrices small enough for the waves-per-slice
+ * kernel, else 1): the library's own default, used by ./bin/sigma_c and
+ * spmv_amd.to_device when no --ki / ki is given.                          */
+int spmv_sell_auto_ki(int64_t n_rows, int32_t C);
 int spmv_sell_run(spmv_dims d, int32_t C, int32_t sigma, int32_t ki, int64_t n_slices,
                   const int64_t *slice_ptr, const int32_t *perm,
                   const int32_t *col, const double *val, const double *x,

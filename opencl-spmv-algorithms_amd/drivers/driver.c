@@ -84,7 +84,7 @@ static int parse_opts(int argc, char **argv, spmv_format fmt, opts_t *o)
     o->warmup = 5;
     o->C = 64;
     o->sigma = 1024;
-    o->ki = 0; /* 0: format default (ELL 2, SELL 1) */
+    o->ki = 0; /* 0: format default (ELL 2, SELL spmv_sell_auto_ki) */
     o->h = 8;
     o->cpu = fmt != FMT_SELL;
     o->xwin = 1;
@@ -431,7 +431,7 @@ static int build_format(const opts_t *o, spmv_format fmt, const coo_t *m, dev_fm
     } else { /* SELL */
         f->C = o->C;
         f->sigma = o->sigma;
-        f->ki = o->ki ? o->ki : 1;
+        f->ki = o->ki ? o->ki : spmv_sell_auto_ki(N, o->C);
         if ((rc = spmv_sell_plan(N, ptr, o->C, o->sigma, f->ki, &f->n_slices, &f->stored)))
             return rc;
         f->h_ptr = malloc((size_t)(f->n_slices + 1) * sizeof(int64_t));

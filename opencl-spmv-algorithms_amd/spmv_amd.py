@@ -108,6 +108,7 @@ HIP_SYMBOLS = {
                                            ctypes.POINTER(_c_i32)]),
     "spmv_ell_run_xwin": (ctypes.c_int, [Dims, _c_i32, _c_i64, _c_i32, _vp, _vp, _vp, _vp, _vp, _c_i32]),
     "spmv_sell_xwin_bytes": (ctypes.c_size_t, [_c_i64, _c_i32, _c_i32]),
+    "spmv_sell_auto_ki": (ctypes.c_int, [_c_i64, _c_i32]),
     "spmv_sell_xwin_build": (ctypes.c_int, [Dims, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, ctypes.c_size_t,
                                             ctypes.POINTER(_c_i32)]),
     "spmv_sell_run_xwin": (ctypes.c_int, [Dims, _c_i32, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp,
@@ -922,7 +923,7 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
         if xwin:
             _ell_xwin(dm)
     elif fmt == "sell":
-        ki = ki or 1  # measured best for SELL-64-1024 (profiles/round1_sweep.md)
+        ki = ki or hip_lib().spmv_sell_auto_ki(m.n_rows, C)  # 1 (σ-window kernel) or 2 (small matrices)
         s = sell_build(m.n_rows, ptr, col, val, C=C, sigma=sigma, ki=ki)
         dm.params = dict(C=C, sigma=sigma, ki=ki, n_slices=s["n_slices"], stored=s["stored"])
         dm.arrays = dict(slice_ptr=_dev_tensor(s["slice_ptr"], device), perm=_dev_tensor(s["perm"], device),
@@ -1008,7 +1009,7 @@ def device_build(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, ki: int =
         if xwin:
             _ell_xwin(dm)
     elif fmt == "sell":
-        ki = ki or 1
+        ki = ki or hip_lib().spmv_sell_auto_ki(m.n_rows, C)  # as to_device
         ns = (N + C - 1) // C
         perm = torch.empty(max(ns * C, 1), dtype=torch.int32, device=device)
         sp = torch.empty(ns + 1, dtype=torch.int64, device=device)

@@ -678,7 +678,8 @@ int lab_multi(int code, int64_t n_slices, const int64_t *sp, const int32_t *perm
     MULTI(1, 1, 4, 24) MULTI(2, 4, 2, 12) MULTI(2, 2, 4, 12) MULTI(1, 2, 8, 24) MULTI(1, 1, 8, 24)
     MULTI(1, 2, 4, 16) MULTI(1, 2, 4, 12) MULTI(2, 2, 4, 8) MULTI(1, 4, 2, 16) MULTI(2, 4, 2, 8)
     MULTI(1, 2, 2, 16) MULTI(2, 2, 2, 12) MULTI(2, 2, 8, 12) MULTI(2, 1, 4, 12) MULTI(1, 4, 1, 16)
-    MULTI(2, 4, 1, 12)
+    MULTI(2, 4, 1, 12) MULTI(1, 2, 4, 8) MULTI(1, 2, 4, 6) MULTI(2, 2, 4, 6) MULTI(2, 2, 4, 4)
+    MULTI(1, 1, 8, 12) MULTI(1, 1, 8, 8) MULTI(2, 1, 8, 8) MULTI(1, 4, 2, 8) MULTI(2, 1, 8, 4)
 #undef MULTI
     return (int)hipGetLastError();
 }

@@ -24,7 +24,7 @@ from cant_single import FLUSH_BYTES, probe_lib  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--codes", default="M14116,M24112,M22412,M12416,M12412,M22408,M14216,M24208,M12216,M22212,M22812,M21412,M22412,M14116")
+    ap.add_argument("--codes", default="M22408,M12408,M12406,M22406,M22404,M11812,M11808,M21808,M14208,M21804,M22408,M12408")
     ap.add_argument("--reps", type=int, default=20)
     a = ap.parse_args()
     import torch

@@ -730,3 +730,55 @@ def test_csr_xwin_window_sizes(torch_dev, case):
                 torch.cuda.synchronize()
                 assert torch.equal(y.view(torch.int64), y0.view(torch.int64)), (m.label, lanes, rows)
         assert_parity(m, y0.cpu().numpy(), x.cpu().numpy()[: m.n_cols])
+
+
+@pytest.mark.parametrize("n_rows", [1, 64, 65, 3 * 64 + 5, 5 * 64, 17 * 64 + 1, 1000 * 64 - 7])
+@pytest.mark.parametrize("sigma", [1, 64, 128, 1024])
+@pytest.mark.parametrize("ki", [1, 2])
+def test_sell_small_kernel_shapes(torch_dev, n_rows, sigma, ki):
+    """The small-matrix SELL kernel (4 slices x 2 waves per workgroup, one
+    shared x window): slice counts that are not multiples of 4, σ windows
+    of 1..16 slices (a workgroup's 4 slices may span two σ windows), rows
+    of 0..300 entries; the x-window run must give the same bits as the
+    global-gather run and pass the parity rule."""
+    torch, dev = torch_dev
+    m = sa.gen_random(n_rows, 3 * n_rows + 50, 0, 300 if n_rows < 2000 else 90, seed=n_rows + sigma)
+    x = torch.from_numpy(np.random.default_rng(n_rows).uniform(-1, 1, m.n_cols)).to(dev)
+    ys = []
+    for xw in (False, True):
+        dm = sa.to_device(m, "sell", dev, C=64, sigma=sigma, ki=ki, xwin=xw)
+        y = torch.full((max(m.n_rows, 1),), float("nan"), dtype=torch.float64, device=dev)
+        dm.run(x, y)
+        ys.append(y)
+    torch.cuda.synchronize()
+    assert torch.equal(ys[0].view(torch.int64), ys[1].view(torch.int64))
+    assert_parity(m, ys[1].cpu().numpy()[: m.n_rows], x.cpu().numpy())
+
+
+def test_sell_small_kernel_window_fallback(torch_dev):
+    """Slices whose shared window exceeds the LDS cap gather from global
+    memory; same bits either way."""
+    torch, dev = torch_dev
+    m = sa.gen_random(900 * 64, 20_000_000, 10, 60, seed=5)  # columns spread over 2e7: no window fits
+    x = torch.from_numpy(np.random.default_rng(3).uniform(-1, 1, m.n_cols)).to(dev)
+    ys = []
+    for xw in (False, True):
+        dm = sa.to_device(m, "sell", dev, xwin=xw)
+        y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
+        dm.run(x, y)
+        ys.append(y)
+        if xw:
+            assert dm.params["xcap"] == 0
+    torch.cuda.synchronize()
+    assert torch.equal(ys[0].view(torch.int64), ys[1].view(torch.int64))
+    assert_parity(m, ys[1].cpu().numpy(), x.cpu().numpy())
+
+
+def test_sell_auto_ki_rule(torch_dev):
+    """spmv_sell_auto_ki: k-interleave 2 for matrices the small-matrix kernel
+    runs (one cant-like copy), 1 for the σ-window kernel (the 32-copy batch)."""
+    lib = sa.hip_lib()
+    assert lib.spmv_sell_auto_ki(62_451, 64) == 2
+    assert lib.spmv_sell_auto_ki(32 * 62_451, 64) == 1
+    assert lib.spmv_sell_auto_ki(62_451, 32) == 1  # C != 64: no small kernel
+    assert sa.to_device(sa.gen_cantlike(0), "sell", torch_dev[1]).params["ki"] == 2

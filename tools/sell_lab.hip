@@ -483,7 +483,7 @@ __global__ __launch_bounds__(256) void lab_chunk_kernel(
 // per slice, one x-window copy for all P: the union of their windows.  Same
 // one-shot first batch of G groups as lab2_kernel (loads issued before the
 // window copy).  Cuts the window-copy traffic P-fold.
-template <int KI, int S, int P, int G>
+template <int KI, int S, int P, int G, int BAL = 0>
 __global__ __launch_bounds__(kWave * S * P) void lab4_kernel(int64_t n_slices, const int64_t *__restrict__ slice_ptr,
                                                              const int32_t *__restrict__ perm,
                                                              const int32_t *__restrict__ col,
@@ -495,7 +495,16 @@ __global__ __launch_bounds__(kWave * S * P) void lab4_kernel(int64_t n_slices, c
     const uint64_t t0 = now();
     extern __shared__ double s_x[];
     const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
-    const int64_t s = (int64_t)blockIdx.x * P + wv / S;
+    int64_t s = (int64_t)blockIdx.x * P + wv / S;
+    if constexpr (BAL) {  // P = 4 of a 16-slice sigma window, widest with narrowest: {j, 7-j, 8+j, 15-j}
+        const int64_t b16 = (int64_t)blockIdx.x * P / 16 * 16;
+        const int j = (int)((int64_t)blockIdx.x % (16 / P));
+        const int k = wv / S;
+        if (b16 + 16 <= n_slices) {
+            const int pos = k == 0 ? j : k == 1 ? 7 - j : k == 2 ? 8 + j : 15 - j;
+            s = b16 + pos;
+        }
+    }
     const int ws = wv % S;
     const bool live = s < n_slices;
     const int64_t base = live ? slice_ptr[s] : 0;
@@ -520,11 +529,13 @@ __global__ __launch_bounds__(kWave * S * P) void lab4_kernel(int64_t n_slices, c
             c[u] = __builtin_nontemporal_load(reinterpret_cast<const CT *>(cp + gg * step));
         }
     }
-    // union window of the P slices
+    // union window of the P slices (BAL: of the whole 16-slice block)
     int lo = INT32_MAX, hi = INT32_MIN;
+    constexpr int NW = BAL ? 16 : P;
+    const int64_t w0 = BAL ? (int64_t)blockIdx.x * P / 16 * 16 : (int64_t)blockIdx.x * P;
 #pragma unroll
-    for (int k = 0; k < P; ++k) {
-        const int64_t sk = (int64_t)blockIdx.x * P + k;
+    for (int k = 0; k < NW; ++k) {
+        const int64_t sk = w0 + k;
         if (sk < n_slices) {
             const int2 wd = win[sk];
             if (wd.y >= wd.x) {
@@ -672,6 +683,10 @@ int lab_multi(int code, int64_t n_slices, const int64_t *sp, const int32_t *perm
 #define MULTI(KI, S, P, G)                                                                                \
     if (code == KI * 10000 + S * 1000 + P * 100 + G)                                                      \
         hipLaunchKernelGGL((lab4_kernel<KI, S, P, G>), dim3((unsigned)((n_slices + P - 1) / P)),           \
+                           dim3(kWave * S * P), (size_t)xcap * sizeof(double), s, n_slices, sp, perm, col, val, x, y, \
+                           (const int2 *)win, xcap, stamps);                                               \
+    if (code == 100000 + KI * 10000 + S * 1000 + P * 100 + G)                                             \
+        hipLaunchKernelGGL((lab4_kernel<KI, S, P, G, 1>), dim3((unsigned)((n_slices + P - 1) / P)),        \
                            dim3(kWave * S * P), (size_t)xcap * sizeof(double), s, n_slices, sp, perm, col, val, x, y, \
                            (const int2 *)win, xcap, stamps);
     MULTI(1, 4, 1, 24) MULTI(1, 4, 2, 24) MULTI(1, 4, 4, 24) MULTI(1, 2, 2, 24) MULTI(1, 2, 4, 24)

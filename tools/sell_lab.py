@@ -24,7 +24,7 @@ from cant_single import FLUSH_BYTES, probe_lib  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--codes", default="M22408,M12408,M12406,M22406,M22404,M11812,M11808,M21808,M14208,M21804,M22408,M12408")
+    ap.add_argument("--codes", default="M22408,B22408,M12408,B12408,M22406,B22406,B22404,B12412,M22408,B22408")
     ap.add_argument("--reps", type=int, default=20)
     a = ap.parse_args()
     import torch
@@ -74,9 +74,11 @@ def main():
             ts.append(e0.elapsed_time(e1) * 1e3)
         print(json.dumps({"probe": mode, "event_us": round(float(np.median(ts)), 2)}), flush=True)
     for code in a.codes.split(","):
-        if code.startswith("M"):  # multi-slice workgroups: M + KI*10000 + S*1000 + P*100 + G
+        if code.startswith("M") or code.startswith("B"):  # multi-slice workgroups: M|B + KI*10000 + S*1000 + P*100 + G
             c = int(code[1:])
             ki, S, P2, G = c // 10000, (c // 1000) % 10, (c // 100) % 10, c % 100
+            if code.startswith("B"):  # balanced slice choice inside 16-slice sigma windows
+                c += 100000
             dm, n, win, xcap = mats[ki]
             A = dm.arrays
             nb = (n + P2 - 1) // P2

@@ -116,6 +116,8 @@ def kernel_name(args, dm=None):
     if dm is not None and "win" in getattr(dm, "arrays", {}):
         if args.format in ("csr16", "csrf32"):  # the CSR x-window kernel with another column / value source
             return "csr_xwin_kernel"
+        if args.format == "sell16":  # the SELL kernels with 16-bit column offsets
+            return "sell_small_kernel" if params.get("n_slices", 1 << 30) < 14 * 256 else "sell_xwin_kernel"
         return f"{args.format}_xwin_kernel"
     if args.format == "csr":
         v = params.get("variant", 0) or args.variant or CSR_DEFAULT_VARIANT
@@ -138,6 +140,8 @@ def fmt_kwargs(args, fmt):
     if fmt == "sell":
         sigma = args.sigma or (1 << 24 if args.workload == "rmat" else 1024)
         return {"C": args.C, "sigma": sigma, "ki": args.ki}
+    if fmt == "sell16":
+        return {"C": args.C, "sigma": args.sigma or 1024, "ki": args.ki}
     if fmt == "cmrs":
         return {"h": args.h}
     return {}

@@ -151,12 +151,23 @@ int spmv_csr_run_tiled_hot(spmv_dims d, const int64_t *row_ptr, const int32_t *c
                            size_t ws_bytes);
 /* The tile -> first owned row table of the entry-balanced CSR (int32,
  * spmv_csr_tiled_plan_len(nnz) entries) built once from row_ptr; passed as
- * own_lo_plan it saves every run its pre-pass (NULL: built per run).  Its
- * tail holds one arrival counter per tile, zeroed here, that the fused
- * carry (rows spanning tiles finished inside the tiled kernel) leaves at
- * zero after every run; runs sharing one plan must not overlap in time. */
+ * own_lo_plan it saves every run its pre-pass (NULL: built per run).     */
 int64_t spmv_csr_tiled_plan_len(int64_t nnz);
 int spmv_csr_tiled_plan(spmv_dims d, const int64_t *row_ptr, int32_t *own_lo);
+/* Column-grouped CSR (CSRG, spmv_csrg_plan/fill in spmv_host.h) for
+ * gather-bound power-law matrices; replaces the same reference kernel
+ * (kernels/Csr.cl) on that input.  The entry-balanced kernel runs the
+ * n_pairs (row, column-group) pairs group after group, so the x lines the
+ * tiles in flight gather from are one group's and stay in L2; each pair's
+ * sum goes to the workspace, then every row's pair sums are added in group
+ * order.  own_lo_plan: spmv_csr_tiled_plan over (pair_ptr, n_rows =
+ * n_pairs), or NULL.  `ws` holds spmv_csrg_ws_bytes(n_pairs, nnz) bytes.
+ * Deterministic; agrees with spmv_csr_run to the parity rule (the row sums
+ * are grouped by column group).                                          */
+size_t spmv_csrg_ws_bytes(int64_t n_pairs, int64_t nnz);
+int spmv_csrg_run(spmv_dims d, int64_t n_pairs, const int64_t *pair_ptr, const int32_t *col_g,
+                  const double *val_g, const int32_t *own_lo_plan, const int64_t *row_pair_ptr,
+                  const int32_t *row_pair, const double *x, double *y, void *ws, size_t ws_bytes);
 
 /* ---------------------------------------------------------------- ELL ---
  * Replaces kernel `ell(val,idx,x,y,int N,int K,__local)` (reference
@@ -256,6 +267,22 @@ int spmv_sell_run_xwin(spmv_dims d, int32_t C, int32_t sigma, int32_t ki, int64_
                        const int64_t *slice_ptr, const int32_t *perm, const int32_t *col,
                        const double *val, const double *x, double *y, const void *win,
                        int32_t xcap);
+/* SELL16 (compressed indices; replaces the same
+ * reference kernel, kernels/Sigma_C.cl): the SELL-C-σ arrays with every
+ * stored column kept as a 16-bit offset from its workgroup's x-window base,
+ * 10 instead of 12 bytes per slot.  C must be 64.  Build once: win / xcap
+ * from spmv_sell_xwin_build, then spmv_sell16_fill writes col16[stored]
+ * from col on the device; it returns SPMV_OTHER_ERROR (nothing written)
+ * when some workgroup's columns span more than 65,536 (the caller keeps
+ * plain SELL).  spmv_sell16_run gives y bit-identical to spmv_sell_run_xwin
+ * with the same ki.                                                      */
+int spmv_sell16_fill(spmv_dims d, int32_t C, int32_t sigma, int64_t n_slices,
+                     const int64_t *slice_ptr, const int32_t *col, const void *win,
+                     uint16_t *col16);
+int spmv_sell16_run(spmv_dims d, int32_t C, int32_t sigma, int32_t ki, int64_t n_slices,
+                    const int64_t *slice_ptr, const int32_t *perm, const uint16_t *col16,
+                    const double *val, const double *x, double *y, const void *win,
+                    int32_t xcap);
 
 /* --------------------------------------------------------------- CMRS ---
  * Replaces kernel `cmrs(val,idx,strip_ptr,row_in_strip,x,y,N,h,__local)`

@@ -157,6 +157,25 @@ int spmv_csr16_plan(int64_t nnz, const int32_t *col, int64_t *n_blocks, int64_t 
 int spmv_csr16_fill(int64_t nnz, const int32_t *col, int32_t *blk_base, uint16_t *col_off,
                     int32_t *col_esc);
 
+/* Column-grouped CSR (CSRG) for gather-bound power-law matrices (R-MAT,
+ * BASELINE.json configs[3]).  x is cut into `groups` (1..64) groups of
+ * whole 128-byte lines (16 columns): the line c/16 belongs to group
+ * spmv_csrg_group(c, groups), a hash, so hot and cold lines spread evenly.
+ * The entries are stored group after group; inside a group, as a CSR over
+ * the PAIRS (row, group) that hold entries, rows ascending, each pair's
+ * entries in CSR order.  A run sums every pair (the groups one after
+ * another, so the x lines being gathered stay in the L2s) and then adds
+ * each row's pair sums in group order (row_pair_ptr / row_pair: the pair
+ * indices of row r in group order).  Plan: n_pairs.  Fill: pair_ptr
+ * [n_pairs+1], col_g/val_g[nnz], row_pair_ptr[n_rows+1], row_pair
+ * [n_pairs].                                                            */
+int32_t spmv_csrg_group(int32_t col, int32_t groups);
+int spmv_csrg_plan(int64_t n_rows, const int64_t *row_ptr, const int32_t *col, int32_t groups,
+                   int64_t *n_pairs);
+int spmv_csrg_fill(int64_t n_rows, const int64_t *row_ptr, const int32_t *col, const double *val,
+                   int32_t groups, int64_t *pair_ptr, int32_t *col_g, double *val_g,
+                   int64_t *row_pair_ptr, int32_t *row_pair);
+
 /* ----------------------------------------------------- multi-GPU shard ---
  * Row-range partition for one process per GPU: `parts`
  * contiguous ranges [bounds[p], bounds[p+1]) holding about nnz/parts

@@ -1115,3 +1115,64 @@ extern "C" int spmv_csr_f32v_run_tiled_hot(spmv_dims d, const int64_t *row_ptr, 
     return run_tiled_hot(d, row_ptr, col_hot, val, x, y, H, hot, own_lo_plan, ws,
                          "spmv_csr_f32v_run_tiled_hot");
 }
+
+// ------------------------------------------------- column-grouped CSR (CSRG)
+// Power-law matrices (R-MAT, configs[3]) are bound by their x gathers: a
+// cold column fills a whole 128-byte L2 line for 8 bytes, and the R-MAT's
+// ~4 M used columns (33 MB of x lines) do not fit one XCD's 4 MiB L2, so
+// the tiled kernel moved 3.46x bytes_alg (profiles/traffic_rmat.json).
+// CSRG (host spmv_csrg_fill) stores the entries group after group, each
+// group owning the x lines of 1/G of the columns; the tiled kernel runs the
+// (row, group) pairs in that order, so the tiles in flight gather from one
+// group's lines (~2.5 MB at G = 32) and those stay in L2.  Each pair's sum
+// goes to yp; csrg_reduce_kernel then adds a row's pair sums in group order.
+// Deterministic; the row sums are grouped differently from CSR's, so y
+// agrees with it to the parity rule, not bit for bit.
+__global__ __launch_bounds__(kBlock) void csrg_reduce_kernel(int64_t n_rows, const int64_t *__restrict__ row_pair_ptr,
+                                                             const int32_t *__restrict__ row_pair,
+                                                             const double *__restrict__ yp, double *__restrict__ y)
+{
+    const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (r >= n_rows)
+        return;
+    double s = 0.0;
+    const int64_t j1 = row_pair_ptr[r + 1];
+    for (int64_t j = row_pair_ptr[r]; j < j1; ++j)
+        s += yp[row_pair[j]];
+    store_y(y + r, s);
+}
+
+extern "C" size_t spmv_csrg_ws_bytes(int64_t n_pairs, int64_t nnz)
+{
+    return (size_t)(n_pairs > 0 ? n_pairs : 0) * sizeof(double) + spmv_csr_tiled_ws_bytes(n_pairs, nnz);
+}
+
+extern "C" int spmv_csrg_run(spmv_dims d, int64_t n_pairs, const int64_t *pair_ptr, const int32_t *col_g,
+                             const double *val_g, const int32_t *own_lo_plan, const int64_t *row_pair_ptr,
+                             const int32_t *row_pair, const double *x, double *y, void *ws, size_t ws_bytes)
+{
+    if (d.n_rows < 0 || d.n_cols < 0 || d.nnz < 0 || d.n_rows > INT32_MAX || n_pairs < 0 ||
+        n_pairs > INT32_MAX || n_pairs > d.nnz || (d.nnz > 0 && n_pairs == 0))
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_csrg_run: bad sizes");
+    if (d.n_rows == 0)
+        return SPMV_SUCCESS;
+    SPMV_GUARD(d);
+    if (d.nnz == 0) {
+        hipError_t e = hipMemsetAsync(y, 0, (size_t)d.n_rows * sizeof(double), (hipStream_t)d.stream);
+        return e == hipSuccess ? SPMV_SUCCESS : fail(SPMV_PROGRAM_ERROR, "memset y", e);
+    }
+    if (!pair_ptr || !col_g || !val_g || !row_pair_ptr || !row_pair || !ws ||
+        ws_bytes < spmv_csrg_ws_bytes(n_pairs, d.nnz))
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_csrg_run: arrays or workspace missing");
+    double *yp = (double *)ws;
+    spmv_dims pd = d;  // the pair CSR: one "row" per (row, group) pair
+    pd.n_rows = n_pairs;
+    int rc = run_tiled_hot(pd, pair_ptr, col_g, val_g, x, yp, 0, nullptr, own_lo_plan, yp + n_pairs,
+                           "spmv_csrg_run");
+    if (rc != SPMV_SUCCESS)
+        return rc;
+    hipLaunchKernelGGL(csrg_reduce_kernel, dim3((unsigned)((d.n_rows + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       (hipStream_t)d.stream, d.n_rows, row_pair_ptr, row_pair, yp, y);
+    SPMV_CHECK_LAUNCH("csrg_reduce_kernel");
+    return SPMV_SUCCESS;
+}

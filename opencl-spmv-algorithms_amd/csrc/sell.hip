@@ -28,27 +28,54 @@ namespace spmv {
 // interleaved (profiles/round1/sweeps.md).  SPMV_STREAM_NT overrides.
 constexpr bool kSellStreamNtDefault = true;
 
+// Column sources: int32 columns (SELL), or 16-bit offsets from the
+// workgroup's x-window base (SELL16, spmv_sell16_fill): the gathers then
+// read s_x[offset] (LDS) or (x + base)[offset].  2 or 4 bytes per lane and
+// slot group instead of 4 or 8.
+template <bool NT>
+__device__ __forceinline__ int32_t col_one(const int32_t *p)
+{
+    return stream_load<NT>(p);
+}
+
+template <bool NT>
+__device__ __forceinline__ int32_t col_one(const uint16_t *p)
+{
+    return (int32_t)stream_load<NT>(p);
+}
+
+template <bool NT>
+__device__ __forceinline__ int2 col_two(const int32_t *p)
+{
+    return stream_load2<NT>(p);
+}
+
+template <bool NT>
+__device__ __forceinline__ int2 col_two(const uint16_t *p)
+{
+    const uint32_t v = stream_load<NT>(reinterpret_cast<const uint32_t *>(p));
+    return int2{(int32_t)(v & 0xFFFFu), (int32_t)(v >> 16)};
+}
+
 template <int KI, bool NT>
 struct Step;
 
 template <bool NT>
 struct Step<1, NT> {
-    template <typename XS>
-    static __device__ __forceinline__ double fma(const double *vp, const int32_t *cp, const XS &xs,
-                                                 double acc)
+    template <typename XS, typename CT>
+    static __device__ __forceinline__ double fma(const double *vp, const CT *cp, const XS &xs, double acc)
     {
-        return acc + stream_load<NT>(vp) * xs(stream_load<NT>(cp));
+        return acc + stream_load<NT>(vp) * xs(col_one<NT>(cp));
     }
 };
 
 template <bool NT>
 struct Step<2, NT> {
-    template <typename XS>
-    static __device__ __forceinline__ double fma(const double *vp, const int32_t *cp, const XS &xs,
-                                                 double acc)
+    template <typename XS, typename CT>
+    static __device__ __forceinline__ double fma(const double *vp, const CT *cp, const XS &xs, double acc)
     {
         const double2 v = stream_load2<NT>(vp);
-        const int2 c = stream_load2<NT>(cp);
+        const int2 c = col_two<NT>(cp);
         return acc + v.x * xs(c.x) + v.y * xs(c.y);
     }
 };
@@ -56,9 +83,9 @@ struct Step<2, NT> {
 // Slot-per-lane loop over `w` slots (a multiple of KI) with stride
 // `step` elements between consecutive KI-groups; U groups in flight
 // (U independent accumulators, combined as a pairwise tree).
-template <int KI, bool NT, int U, typename XS>
+template <int KI, bool NT, int U, typename XS, typename CT = int32_t>
 __device__ __forceinline__ double slot_dot(const double *__restrict__ vp,
-                                           const int32_t *__restrict__ cp,
+                                           const CT *__restrict__ cp,
                                            int64_t w, int64_t step, const XS &xs)
 {
     double a[U];
@@ -93,13 +120,14 @@ template <bool NT, int U>
 struct SlotBatch<1, NT, U> {
     double v[U];
     int32_t c[U];
-    __device__ __forceinline__ void load(const double *vp, const int32_t *cp, int64_t g, int64_t end, int64_t step)
+    template <typename CT>
+    __device__ __forceinline__ void load(const double *vp, const CT *cp, int64_t g, int64_t end, int64_t step)
     {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int64_t gg = g + u < end ? g + u : g;
             v[u] = stream_load<NT>(vp + gg * step);
-            c[u] = stream_load<NT>(cp + gg * step);
+            c[u] = col_one<NT>(cp + gg * step);
         }
     }
     template <typename XS>
@@ -122,13 +150,14 @@ template <bool NT, int U>
 struct SlotBatch<2, NT, U> {
     double2 v[U];
     int2 c[U];
-    __device__ __forceinline__ void load(const double *vp, const int32_t *cp, int64_t g, int64_t end, int64_t step)
+    template <typename CT>
+    __device__ __forceinline__ void load(const double *vp, const CT *cp, int64_t g, int64_t end, int64_t step)
     {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int64_t gg = g + u < end ? g + u : g;
             v[u] = stream_load2<NT>(vp + gg * step);
-            c[u] = stream_load2<NT>(cp + gg * step);
+            c[u] = col_two<NT>(cp + gg * step);
         }
     }
     template <typename XS>
@@ -332,10 +361,11 @@ __global__ __launch_bounds__(kBlock) void sell_window_kernel(int32_t C, int bt, 
 // profiles/round1/pmc_stalls.json).  Here the window is copied into LDS
 // once with coalesced loads and every gather is a ds_read_b64.  A
 // workgroup whose window exceeds xcap entries gathers from global memory.
-template <int KI, bool NT, int U>
+// CT = uint16_t: SELL16 (columns stored as offsets from wnd.x).
+template <int KI, bool NT, int U, typename CT = int32_t>
 __global__ __launch_bounds__(1024) void sell_xwin_kernel(
     int32_t C, int64_t n_slices, const int64_t *__restrict__ slice_ptr,
-    const int32_t *__restrict__ perm, const int32_t *__restrict__ col,
+    const int32_t *__restrict__ perm, const CT *__restrict__ col,
     const double *__restrict__ val, const double *__restrict__ x,
     double *__restrict__ y, const int2 *__restrict__ win, int32_t xcap, int64_t wcap, int remap,
     int64_t ystage_rows)
@@ -370,8 +400,9 @@ __global__ __launch_bounds__(1024) void sell_xwin_kernel(
         int64_t w = (slice_ptr[s + 1] - base) / C;
         w = w < wcap ? w : wcap;
         const int64_t off = base + r * KI;
-        sum = staged ? slot_dot<KI, NT, U>(val + off, col + off, w, (int64_t)C * KI, XWindow{s_x, wnd.x})
-                     : slot_dot<KI, NT, U>(val + off, col + off, w, (int64_t)C * KI, XGlobal{x});
+        constexpr bool c16 = std::is_same<CT, uint16_t>::value;
+        sum = staged ? slot_dot<KI, NT, U>(val + off, col + off, w, (int64_t)C * KI, XWindow{s_x, c16 ? 0 : wnd.x})
+                     : slot_dot<KI, NT, U>(val + off, col + off, w, (int64_t)C * KI, XGlobal{c16 ? x + wnd.x : x});
     }
     if (ystage_rows > 0) {
         if (in_order) {  // whole rows in order already: written through L2 directly
@@ -419,14 +450,16 @@ __global__ __launch_bounds__(1024) void sell_xwin_kernel(
 // reads for a 49 MB matrix); four slices share it.
 template <int KI> constexpr int sell_small_g() { return 8; }  // first-batch slot groups per lane
 
-template <int KI, bool NT, bool XWIN, typename XS>
+template <int KI, bool NT, bool XWIN, typename XS, typename CT = int32_t>
 __global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell_small_kernel(
     int64_t n_slices, const int64_t *__restrict__ slice_ptr,
-    const int32_t *__restrict__ perm, const int32_t *__restrict__ col,
+    const int32_t *__restrict__ perm, const CT *__restrict__ col,
     const double *__restrict__ val, const XS xs, double *__restrict__ y, int64_t wcap,
     const double *__restrict__ x, const int2 *__restrict__ win, int32_t xcap)
 {
     constexpr int S = kSellSmallS, P = kSellSmallP, G = sell_small_g<KI>();
+    constexpr bool c16 = std::is_same<CT, uint16_t>::value;  // SELL16: offsets from the window base
+    static_assert(!c16 || XWIN, "SELL16 needs the workgroup windows");
     constexpr int64_t step = (int64_t)kWave * KI;  // elements between slot groups
     extern __shared__ double s_x[];
     const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
@@ -442,7 +475,7 @@ __global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell_small_
     const int64_t g1 = g0 + per < groups ? g0 + per : groups;
     const bool any = g1 > g0;  // uniform per wave: no loads past the slice
     const double *vp = val + base + lane * KI;
-    const int32_t *cp = col + base + lane * KI;
+    const CT *cp = col + base + lane * KI;
     SlotBatch<KI, NT, G> first;
     if (any)
         first.load(vp, cp, g0, g1, step);
@@ -467,10 +500,14 @@ __global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell_small_
             b.fma4(src, g, g1, a);
         }
     };
-    if (staged)
-        body(XWindow{s_x, wnd.x});
-    else
-        body(xs);
+    if (staged) {
+        body(XWindow{s_x, c16 ? 0 : wnd.x});
+    } else {
+        if constexpr (c16)
+            body(XGlobal{x + wnd.x});
+        else
+            body(xs);
+    }
     double sum = (a[0] + a[2]) + (a[1] + a[3]);
     __shared__ double part[S * P][kWave];
     part[wv][lane] = sum;
@@ -497,14 +534,14 @@ bool sell_small(int32_t C, int64_t n_slices)
     return n_slices < 14 * (int64_t)cus;
 }
 
-template <int KI, bool NT, bool XWIN, typename XS>
-static void launch_sell_small(int64_t n_slices, const int64_t *slice_ptr, const int32_t *perm, const int32_t *col,
+template <int KI, bool NT, bool XWIN, typename XS, typename CT = int32_t>
+static void launch_sell_small(int64_t n_slices, const int64_t *slice_ptr, const int32_t *perm, const CT *col,
                               const double *val, const XS xs, double *y, int64_t wcap, const double *x,
                               const int2 *win, int32_t xcap, hipStream_t st)
 {
     const size_t lds = XWIN ? (size_t)xcap * sizeof(double) : 0;
     const int64_t blocks = (n_slices + kSellSmallP - 1) / kSellSmallP;
-    hipLaunchKernelGGL((sell_small_kernel<KI, NT, XWIN, XS>), dim3((unsigned)blocks),
+    hipLaunchKernelGGL((sell_small_kernel<KI, NT, XWIN, XS, CT>), dim3((unsigned)blocks),
                        dim3(kWave * kSellSmallS * kSellSmallP), lds, st, n_slices, slice_ptr, perm, col, val, xs, y,
                        wcap, x, win, xcap);
 }
@@ -741,6 +778,115 @@ extern "C" int spmv_sell_run_xwin(spmv_dims d, int32_t C, int32_t sigma, int32_t
                        (const int2 *)win, xcap, (int64_t)INT64_MAX, xwin_remap(false) ? 1 : 0,
                        sell_ystage(bt, sigma) ? d.n_rows : (int64_t)0);
     SPMV_CHECK_LAUNCH("sell_xwin_kernel");
+    return SPMV_SUCCESS;
+}
+
+// SELL16: the column of every stored slot as a 16-bit offset from its
+// workgroup's x-window base (win[b].x, spmv_sell_xwin_build), so a slot is
+// 10 bytes instead of 12.  Workgroup b covers slices [b·bt/C, (b+1)·bt/C)
+// exactly (C = 64 divides every SELL workgroup size), so each slot has ONE
+// base.  Build time, one workgroup per window.
+__global__ __launch_bounds__(kBlock) void sell16_fill_kernel(int32_t C, int bt, int64_t n_slices,
+                                                             const int64_t *__restrict__ slice_ptr,
+                                                             const int32_t *__restrict__ col,
+                                                             const int2 *__restrict__ win,
+                                                             uint16_t *__restrict__ col16)
+{
+    const int64_t b = blockIdx.x;
+    const int64_t s0 = b * bt / C;
+    int64_t s1 = (b + 1) * bt / C;
+    s1 = s1 < n_slices ? s1 : n_slices;
+    const int32_t lo = win[b].x;
+    for (int64_t e = slice_ptr[s0] + threadIdx.x; e < slice_ptr[s1]; e += kBlock)
+        col16[e] = (uint16_t)(col[e] - lo);
+}
+
+static int sell16_check(const spmv_dims &d, int32_t C, int32_t sigma, int32_t ki, int64_t n_slices, const char *who)
+{
+    int rc = sell_check_args(d, C, sigma, ki, n_slices, who);
+    if (rc != SPMV_SUCCESS)
+        return rc;
+    if (C != kWave)
+        return fail_msg(SPMV_OTHER_ERROR, "SELL16: C must be 64 (one slot column per wave)");
+    return SPMV_SUCCESS;
+}
+
+extern "C" int spmv_sell16_fill(spmv_dims d, int32_t C, int32_t sigma, int64_t n_slices, const int64_t *slice_ptr,
+                                const int32_t *col, const void *win, uint16_t *col16)
+{
+    int rc = sell16_check(d, C, sigma, 1, n_slices, "spmv_sell16_fill");
+    if (rc != SPMV_SUCCESS)
+        return rc;
+    if (d.n_rows == 0 || n_slices == 0)
+        return SPMV_SUCCESS;
+    if (!win || !col || !col16 || !slice_ptr)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_sell16_fill: NULL array");
+    SPMV_GUARD(d);
+    int bt;
+    int64_t blocks;
+    sell_geometry(C, sigma, n_slices, &bt, &blocks);
+    if (bt % C != 0 || blocks > INT32_MAX)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_sell16_fill: workgroups do not hold whole slices");
+    const hipStream_t st = (hipStream_t)d.stream;
+    // every window must span at most 65,536 columns (build time: one
+    // synchronising copy of the window table)
+    int2 *h = (int2 *)malloc((size_t)blocks * sizeof(int2));
+    if (!h)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_sell16_fill: out of host memory");
+    hipError_t e = hipMemcpyAsync(h, win, (size_t)blocks * sizeof(int2), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess)
+        e = hipStreamSynchronize(st);
+    if (e != hipSuccess) {
+        free(h);
+        return fail(SPMV_PROGRAM_ERROR, "spmv_sell16_fill: copy windows", e);
+    }
+    int64_t wide = 0;
+    for (int64_t b = 0; b < blocks; ++b)
+        wide += (int64_t)h[b].y - h[b].x + 1 > 65536;
+    free(h);
+    if (wide > 0)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_sell16_fill: a workgroup's columns span more than 65,536");
+    hipLaunchKernelGGL(sell16_fill_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, st, C, bt, n_slices, slice_ptr,
+                       col, (const int2 *)win, col16);
+    SPMV_CHECK_LAUNCH("sell16_fill_kernel");
+    return SPMV_SUCCESS;
+}
+
+extern "C" int spmv_sell16_run(spmv_dims d, int32_t C, int32_t sigma, int32_t ki, int64_t n_slices,
+                               const int64_t *slice_ptr, const int32_t *perm, const uint16_t *col16,
+                               const double *val, const double *x, double *y, const void *win, int32_t xcap)
+{
+    int rc = sell16_check(d, C, sigma, ki, n_slices, "spmv_sell16_run");
+    if (rc != SPMV_SUCCESS)
+        return rc;
+    if (d.n_rows == 0 || n_slices == 0)
+        return SPMV_SUCCESS;
+    if (!win || xcap < 0 || xcap > kXwinCapWide)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_sell16_run: bad window arguments");
+    SPMV_GUARD(d);
+    int bt;
+    int64_t blocks;
+    sell_geometry(C, sigma, n_slices, &bt, &blocks);
+    if (blocks > INT32_MAX)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_sell16_run: grid too large");
+    const bool nt = stream_nt(kSellStreamNtDefault);
+    const hipStream_t st = (hipStream_t)d.stream;
+    const int2 *w = (const int2 *)win;
+    if (sell_small(C, n_slices)) {
+#define SPMV_SMALL16(K, N) \
+    launch_sell_small<K, N, true, XGlobal, uint16_t>(n_slices, slice_ptr, perm, col16, val, XGlobal{x}, y, INT64_MAX, x, w, xcap, st)
+        if (ki == 2) { if (nt) SPMV_SMALL16(2, true); else SPMV_SMALL16(2, false); }
+        else { if (nt) SPMV_SMALL16(1, true); else SPMV_SMALL16(1, false); }
+#undef SPMV_SMALL16
+        SPMV_CHECK_LAUNCH("sell_small_kernel (SELL16)");
+        return SPMV_SUCCESS;
+    }
+    auto kern = ki == 2 ? (nt ? sell_xwin_kernel<2, true, 4, uint16_t> : sell_xwin_kernel<2, false, 4, uint16_t>)
+                        : (nt ? sell_xwin_kernel<1, true, 4, uint16_t> : sell_xwin_kernel<1, false, 4, uint16_t>);
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(bt), (size_t)xcap * sizeof(double), st, C, n_slices,
+                       slice_ptr, perm, col16, val, x, y, w, xcap, (int64_t)INT64_MAX, xwin_remap(false) ? 1 : 0,
+                       sell_ystage(bt, sigma) ? d.n_rows : (int64_t)0);
+    SPMV_CHECK_LAUNCH("sell_xwin_kernel (SELL16)");
     return SPMV_SUCCESS;
 }
 

@@ -648,6 +648,120 @@ int spmv_csr16_fill(int64_t nnz, const int32_t *col, int32_t *blk_base, uint16_t
     return SPMV_SUCCESS;
 }
 
+/* -------------------------------------------------- column-grouped CSR */
+
+int32_t spmv_csrg_group(int32_t col, int32_t groups)
+{
+    const uint64_t h = ((uint64_t)(uint32_t)col >> 4) * 0x9E3779B97F4A7C15ULL;
+    return groups > 1 ? (int32_t)((h >> 40) % (uint64_t)groups) : 0;
+}
+
+/* groups present in row r (bit g) */
+static uint64_t csrg_mask(const int64_t *row_ptr, const int32_t *col, int64_t r, int32_t groups)
+{
+    uint64_t m = 0;
+    for (int64_t e = row_ptr[r]; e < row_ptr[r + 1]; ++e)
+        m |= 1ULL << spmv_csrg_group(col[e], groups);
+    return m;
+}
+
+int spmv_csrg_plan(int64_t n_rows, const int64_t *row_ptr, const int32_t *col, int32_t groups,
+                   int64_t *n_pairs)
+{
+    if (n_rows < 0 || groups < 1 || groups > 64 || !row_ptr || !n_pairs || (row_ptr[n_rows] > 0 && !col))
+        return SPMV_OTHER_ERROR;
+    int64_t np = 0;
+#pragma omp parallel for schedule(dynamic, 4096) reduction(+ : np)
+    for (int64_t r = 0; r < n_rows; ++r)
+        np += __builtin_popcountll(csrg_mask(row_ptr, col, r, groups));
+    if (np > (int64_t)INT32_MAX)
+        return SPMV_OTHER_ERROR;
+    *n_pairs = np;
+    return SPMV_SUCCESS;
+}
+
+/* Rows are cut into chunks; pass 1 counts each chunk's pairs and entries
+ * per group, a prefix over (group, chunk) gives every chunk its starting
+ * pair and entry in every group, pass 2 writes them.  Same layout for any
+ * thread count. */
+int spmv_csrg_fill(int64_t n_rows, const int64_t *row_ptr, const int32_t *col, const double *val,
+                   int32_t groups, int64_t *pair_ptr, int32_t *col_g, double *val_g,
+                   int64_t *row_pair_ptr, int32_t *row_pair)
+{
+    if (n_rows < 0 || groups < 1 || groups > 64 || !row_ptr || !pair_ptr || !row_pair_ptr)
+        return SPMV_OTHER_ERROR;
+    const int64_t nnz = row_ptr[n_rows];
+    if (nnz > 0 && (!col || !val || !col_g || !val_g || !row_pair))
+        return SPMV_OTHER_ERROR;
+    const int64_t NCH = 256;
+    const int64_t per = (n_rows + NCH - 1) / NCH > 0 ? (n_rows + NCH - 1) / NCH : 1;
+    const int G = groups;
+    int64_t *pc = calloc((size_t)(NCH * G), sizeof(int64_t)); /* pairs of chunk k in group g: [g*NCH + k] */
+    int64_t *ec = calloc((size_t)(NCH * G), sizeof(int64_t)); /* entries */
+    if (!pc || !ec) {
+        free(pc);
+        free(ec);
+        return SPMV_OTHER_ERROR;
+    }
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int64_t k = 0; k < NCH; ++k) {
+        const int64_t r0 = k * per, r1 = r0 + per < n_rows ? r0 + per : n_rows;
+        for (int64_t r = r0; r < r1; ++r) {
+            uint64_t m = 0;
+            for (int64_t e = row_ptr[r]; e < row_ptr[r + 1]; ++e) {
+                const int32_t g = spmv_csrg_group(col[e], groups);
+                m |= 1ULL << g;
+                ++ec[g * NCH + k];
+            }
+            for (; m; m &= m - 1)
+                ++pc[__builtin_ctzll(m) * NCH + k];
+        }
+    }
+    /* exclusive prefix in (group, chunk) order = the group-major layout */
+    int64_t ps = 0, es = 0;
+    for (int64_t i = 0; i < NCH * G; ++i) {
+        const int64_t p = pc[i], e = ec[i];
+        pc[i] = ps;
+        ec[i] = es;
+        ps += p;
+        es += e;
+    }
+    pair_ptr[ps] = es;
+    /* row_pair_ptr: pairs of each row (group order inside a row) */
+    row_pair_ptr[0] = 0;
+    for (int64_t r = 0; r < n_rows; ++r)
+        row_pair_ptr[r + 1] = row_pair_ptr[r] + __builtin_popcountll(csrg_mask(row_ptr, col, r, groups));
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int64_t k = 0; k < NCH; ++k) {
+        int64_t pn[64], en[64];
+        for (int g = 0; g < G; ++g) {
+            pn[g] = pc[g * NCH + k];
+            en[g] = ec[g * NCH + k];
+        }
+        const int64_t r0 = k * per, r1 = r0 + per < n_rows ? r0 + per : n_rows;
+        for (int64_t r = r0; r < r1; ++r) {
+            const uint64_t m = csrg_mask(row_ptr, col, r, groups);
+            int64_t rp = row_pair_ptr[r];
+            for (uint64_t mm = m; mm; mm &= mm - 1) { /* each group of the row: open its pair */
+                const int g = __builtin_ctzll(mm);
+                pair_ptr[pn[g]] = en[g];
+                row_pair[rp++] = (int32_t)pn[g];
+            }
+            for (int64_t e = row_ptr[r]; e < row_ptr[r + 1]; ++e) { /* entries in CSR order */
+                const int g = spmv_csrg_group(col[e], groups);
+                col_g[en[g]] = col[e];
+                val_g[en[g]] = val[e];
+                ++en[g];
+            }
+            for (uint64_t mm = m; mm; mm &= mm - 1)
+                ++pn[__builtin_ctzll(mm)];
+        }
+    }
+    free(pc);
+    free(ec);
+    return SPMV_SUCCESS;
+}
+
 /* ------------------------------------------------------------ sharding */
 
 int spmv_partition_rows_weighted(int64_t n_rows, const int64_t *row_ptr, int parts, int64_t align,

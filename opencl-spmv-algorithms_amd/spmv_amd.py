@@ -27,8 +27,9 @@ LIB_DIR = PKG_DIR / "lib"
 REPO_DIR = PKG_DIR.parent
 
 FORMATS = ("coo", "csr", "ell", "sell", "cmrs")  # the reference's five
-# §8f row 4: CSR with 16-bit column offsets; ELL + COO tail; CSR with fp32 values
-EXTRA_FORMATS = ("csr16", "hyb", "csrf32")
+# §8f row 4: CSR with 16-bit column offsets; ELL + COO tail; CSR with fp32 values;
+# SELL-C-σ with 16-bit column offsets
+EXTRA_FORMATS = ("csr16", "hyb", "csrf32", "sell16")
 ALL_FORMATS = FORMATS + EXTRA_FORMATS
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
@@ -92,6 +93,8 @@ HIP_SYMBOLS = {
                                               ctypes.c_size_t]),
     "spmv_csr_tiled_plan_len": (_c_i64, [_c_i64]),
     "spmv_csr_tiled_plan": (ctypes.c_int, [Dims, _vp, _vp]),
+    "spmv_csrg_ws_bytes": (ctypes.c_size_t, [_c_i64, _c_i64]),
+    "spmv_csrg_run": (ctypes.c_int, [Dims, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t]),
     "spmv_csr16_run": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_int]),
     "spmv_csr16_run_xwin": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_int, _c_i32, _vp,
                                            _c_i32]),
@@ -114,6 +117,9 @@ HIP_SYMBOLS = {
     "spmv_sell_run_xwin": (ctypes.c_int, [Dims, _c_i32, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp,
                                           _vp, _c_i32]),
     "spmv_sell_run": (ctypes.c_int, [Dims, _c_i32, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "spmv_sell16_fill": (ctypes.c_int, [Dims, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, _vp]),
+    "spmv_sell16_run": (ctypes.c_int, [Dims, _c_i32, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                       _c_i32]),
     "spmv_cmrs_run": (ctypes.c_int, [Dims, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "spmv_coo_xwin_bytes": (ctypes.c_size_t, [_c_i64]),
     "spmv_coo_xwin_build": (ctypes.c_int, [Dims, _vp, _vp, ctypes.c_size_t, ctypes.POINTER(_c_i32)]),
@@ -209,6 +215,9 @@ HOST_SYMBOLS = {
                                      ctypes.POINTER(_c_i64)]),
     "spmv_hyb_fill": (ctypes.c_int, [_c_i64, _vp, _vp, _vp, _c_i32, _c_i64, _c_i32, _vp, _vp, _vp, _vp, _vp]),
     "spmv_csr16_fill": (ctypes.c_int, [_c_i64, _vp, _vp, _vp, _vp]),
+    "spmv_csrg_group": (_c_i32, [_c_i32, _c_i32]),
+    "spmv_csrg_plan": (ctypes.c_int, [_c_i64, _vp, _vp, _c_i32, ctypes.POINTER(_c_i64)]),
+    "spmv_csrg_fill": (ctypes.c_int, [_c_i64, _vp, _vp, _vp, _c_i32, _vp, _vp, _vp, _vp, _vp]),
     "spmv_cpu_coo": (ctypes.c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, ctypes.c_int]),
     "spmv_cpu_csr": (ctypes.c_int, [_c_i64, _vp, _vp, _vp, _vp, _vp, ctypes.c_int]),
     "spmv_cpu_ell": (ctypes.c_int, [_c_i64, _c_i32, _c_i64, _c_i32, _vp, _vp, _vp, _vp, ctypes.c_int]),
@@ -487,6 +496,24 @@ def csr16_build(col: np.ndarray):
     return dict(n_blocks=nb.value, n_esc=ne.value, blk_base=base, col_off=off, col_esc=esc)
 
 
+def csrg_build(n_rows: int, ptr, col, val, groups: int = 32):
+    """Column-grouped CSR (spmv_host.h spmv_csrg_plan/fill): the entries
+    group after group of 128-B x lines, as a CSR over (row, group) pairs."""
+    lib = host_lib()
+    npairs = _c_i64(0)
+    _check_host(lib.spmv_csrg_plan(n_rows, _ptr(ptr), _ptr(col), groups, ctypes.byref(npairs)), "csrg_plan")
+    n = npairs.value
+    nnz = int(ptr[n_rows])
+    pair_ptr = np.empty(n + 1, np.int64)
+    col_g = np.empty(max(nnz, 1), np.int32)
+    val_g = np.empty(max(nnz, 1), np.float64)
+    rpp = np.empty(n_rows + 1, np.int64)
+    rp = np.empty(max(n, 1), np.int32)
+    _check_host(lib.spmv_csrg_fill(n_rows, _ptr(ptr), _ptr(col), _ptr(val), groups, _ptr(pair_ptr), _ptr(col_g),
+                                   _ptr(val_g), _ptr(rpp), _ptr(rp)), "csrg_fill")
+    return dict(groups=groups, n_pairs=n, pair_ptr=pair_ptr, col_g=col_g, val_g=val_g, row_pair_ptr=rpp, row_pair=rp)
+
+
 def partition_rows(n_rows: int, ptr: np.ndarray, parts: int, align: int = 1024,
                    row_weight: float = 0.0) -> np.ndarray:
     """Contiguous row ranges with ~nnz/parts entries each (SURVEY.md §8e);
@@ -647,6 +674,14 @@ class DeviceMatrix:
                                        _ptr(a["win"]), p["xcap"])
         elif self.fmt == "ell":
             rc = lib.spmv_ell_run(d, p["K"], p["ld"], p["ki"], _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y))
+        elif self.fmt == "csrg":
+            rc = lib.spmv_csrg_run(d, p["n_pairs"], _ptr(a["pair_ptr"]), _ptr(a["col_g"]), _ptr(a["val_g"]),
+                                   _ptr(a.get("own_lo")), _ptr(a["row_pair_ptr"]), _ptr(a["row_pair"]), _ptr(x),
+                                   _ptr(y), _ptr(a["ws"]), a["ws"].numel())
+        elif self.fmt == "sell16":
+            rc = lib.spmv_sell16_run(d, p["C"], p["sigma"], p["ki"], p["n_slices"], _ptr(a["slice_ptr"]),
+                                     _ptr(a["perm"]), _ptr(a["col16"]), _ptr(a["val"]), _ptr(x), _ptr(y),
+                                     _ptr(a["win"]), p["xcap"])
         elif self.fmt == "sell" and p.get("H", 0) > 0:
             split = p.get("split_T", 0) > 0
             rc = lib.spmv_sell_run_hot(d, p["C"], p["sigma"], p["ki"], p["n_slices"], _ptr(a["slice_ptr"]),
@@ -820,7 +855,7 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
               sigma: int = 1024, h: int = 8, ell_max_padding: float | None = 64.0,
               xwin: bool | None = None, xwin_rows: int = 0, split: int | None = None,
               cmrs_variant: int | None = None, hot: int | None = None,
-              csr16_max_escape: float | None = 0.5) -> DeviceMatrix:
+              csr16_max_escape: float | None = 0.5, groups: int = 0) -> DeviceMatrix:
     """Build `fmt` on the host (libspmv_host.so) and upload it.  xwin (CSR,
     ELL, SELL; default on): also build the per-workgroup x windows on the
     device and run the LDS x-window kernels (same bits as without).  split
@@ -933,6 +968,37 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
             _sell_xwin(dm)
         _sell_split(dm, s["slice_ptr"], split)
         _sell_hot(dm, s["col"][: s["stored"]], hot)
+    elif fmt == "csrg":
+        # column-grouped CSR for gather-bound power-law matrices (R-MAT)
+        g = csrg_build(m.n_rows, ptr, col, val, groups=groups or 32)
+        dm.params = dict(groups=g["groups"], n_pairs=g["n_pairs"])
+        dm.arrays = {k: _dev_tensor(g[k], device) for k in ("pair_ptr", "col_g", "val_g", "row_pair_ptr", "row_pair")}
+        ws = hip_lib().spmv_csrg_ws_bytes(g["n_pairs"], m.nnz)
+        dm.arrays["ws"] = torch.empty(max(ws, 16), dtype=torch.uint8, device=device)
+        n_plan = hip_lib().spmv_csr_tiled_plan_len(m.nnz)
+        if n_plan > 0:  # tile -> first pair table over the pair CSR, built once
+            dm.arrays["own_lo"] = torch.empty(n_plan, dtype=torch.int32, device=device)
+            pd = Dims(g["n_pairs"], m.n_cols, m.nnz, device.index or 0, torch.cuda.current_stream(device).cuda_stream)
+            _check(hip_lib().spmv_csr_tiled_plan(pd, _ptr(dm.arrays["pair_ptr"]), _ptr(dm.arrays["own_lo"])),
+                   "spmv_csr_tiled_plan")
+        dm.stored_bytes = 12 * m.nnz + 8 * (g["n_pairs"] + 1) + 8 * (m.n_rows + 1) + 4 * g["n_pairs"]
+    elif fmt == "sell16":
+        # SELL-C-σ with 16-bit column offsets from each workgroup's window base
+        # (§8f row 4): the SELL build, the x windows, then the device pass
+        # that rewrites col as col16; refused when a window spans > 65,536
+        # columns (R-MAT), like csr16's escape rule
+        ki = ki or hip_lib().spmv_sell_auto_ki(m.n_rows, C)
+        s = sell_build(m.n_rows, ptr, col, val, C=C, sigma=sigma, ki=ki)
+        dm.params = dict(C=C, sigma=sigma, ki=ki, n_slices=s["n_slices"], stored=s["stored"])
+        dm.arrays = dict(slice_ptr=_dev_tensor(s["slice_ptr"], device), perm=_dev_tensor(s["perm"], device),
+                         col=_dev_tensor(s["col"], device), val=_dev_tensor(s["val"], device))
+        _sell_xwin(dm)
+        a = dm.arrays
+        a["col16"] = torch.empty(max(a["col"].numel(), 2), dtype=torch.int16, device=device)
+        _check(hip_lib().spmv_sell16_fill(dm.dims(), C, sigma, s["n_slices"], _ptr(a["slice_ptr"]), _ptr(a["col"]),
+                                          _ptr(a["win"]), _ptr(a["col16"])), "spmv_sell16_fill")
+        del a["col"]
+        dm.stored_bytes = 10 * s["stored"] + 8 * (s["n_slices"] + 1) + 4 * s["n_slices"] * C
     elif fmt == "hyb":
         hb = hyb_build(m.n_rows, ptr, col, val, ki=ki or 2)
         dm.params = dict(K=hb["K"], ld=hb["ld"], ki=hb["ki"], tail_nnz=hb["tail_nnz"], stored=hb["stored"], H=0)

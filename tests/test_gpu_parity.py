@@ -68,6 +68,14 @@ FMT_PARAMS = [
     # COO with x windows in LDS (opt-in), CMRS with global x gathers
     ("coo", {"xwin": True}),
     ("cmrs", {"h": 8, "xwin": False}),
+    # SELL16: 16-bit column offsets from each workgroup's window base
+    ("sell16", {"C": 64, "sigma": 1024, "ki": 2}),
+    ("sell16", {"C": 64, "sigma": 1024, "ki": 1}),
+    ("sell16", {"C": 64, "sigma": 1, "ki": 1}),
+    # column-grouped CSR (gather-bound power-law matrices)
+    ("csrg", {"groups": 1}),
+    ("csrg", {"groups": 5}),
+    ("csrg", {"groups": 32}),
 ]
 IDS = [f"{f}-{'-'.join(f'{k}{v}' for k, v in kw.items()) or 'default'}" for f, kw in FMT_PARAMS]
 
@@ -120,7 +128,7 @@ def test_cantlike(torch_dev, fmt, kw, mode):
     assert_parity(m, y, x)
 
 
-@pytest.mark.parametrize("fmt", ["coo", "csr", "sell", "cmrs", "ell"])
+@pytest.mark.parametrize("fmt", ["coo", "csr", "sell", "cmrs", "ell", "sell16"])
 def test_cantlike_batch_random_x(torch_dev, fmt):
     """The bench workload (block-diagonal batch of cant-like copies) with a
     random x instead of the ramp."""
@@ -249,7 +257,7 @@ def rmat_full():
     return m, x, oracle.file_order_spmv(m.n_rows, m.row, m.col, m.val, x)
 
 
-@pytest.mark.parametrize("fmt", sa.FORMATS)
+@pytest.mark.parametrize("fmt", sa.FORMATS + ("csrg",))
 def test_linearity_and_checksum_full_rmat(torch_dev, rmat_full, fmt):
     """BASELINE.json configs[3] at full size (1e7 rows, 1e8 entries):
     A(2u - 3v) == 2Au - 3Av, and with x = ones sum(y) == sum(values).
@@ -435,6 +443,66 @@ def test_sell_xwin_bit_identical(torch_dev, case, ki):
     torch.cuda.synchronize()
     assert torch.equal(ys[0].view(torch.int64), ys[1].view(torch.int64))
     assert_parity(m, ys[1].cpu().numpy(), x.cpu().numpy())
+
+
+@pytest.mark.parametrize("case", ["cantlike", "cantlike16", "ragged", "banded"])
+@pytest.mark.parametrize("ki", [1, 2])
+def test_sell16_bit_identical_to_sell(torch_dev, case, ki):
+    """SELL16 decodes the same columns and sums in the same order as the
+    x-window SELL kernel of the same geometry (one cant-like copy: the
+    small-matrix kernel; 16 copies: one sigma-window per workgroup)."""
+    torch, dev = torch_dev
+    if case == "cantlike":
+        m = sa.gen_cantlike(0)
+    elif case == "cantlike16":
+        m = sa.gen_cantlike(1, copies=16)
+    elif case == "ragged":
+        m = sa.gen_random(20_000, 20_000, 0, 700, seed=21)
+    else:
+        n = 600_000
+        ptr, col, val = sa.gen_banded_csr(n, 0, n)
+        row = np.repeat(np.arange(n, dtype=np.int32), np.diff(ptr))
+        m = sa.Coo(n, n, row, col, val, False, "banded")
+    x = torch.from_numpy(np.random.default_rng(9).uniform(-1, 1, m.n_cols)).to(dev)
+    ys = []
+    for fmt in ("sell", "sell16"):
+        dm = sa.to_device(m, fmt, dev, C=64, sigma=1024, ki=ki, xwin=True)
+        y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
+        dm.run(x, y)
+        ys.append(y)
+        if fmt == "sell16":
+            assert "col" not in dm.arrays and dm.arrays["col16"].dtype == torch.int16
+            assert dm.stored_bytes < 12 * dm.params["stored"]
+    torch.cuda.synchronize()
+    assert torch.equal(ys[0].view(torch.int64), ys[1].view(torch.int64))
+    assert_parity(m, ys[1].cpu().numpy(), x.cpu().numpy())
+
+
+@pytest.mark.parametrize("groups", [8, 32, 64])
+def test_csrg_rmat(torch_dev, groups):
+    """Column-grouped CSR on a skewed R-MAT (hub rows over many tiles, empty
+    rows): parity with the oracle, same bits on a second run."""
+    torch, dev = torch_dev
+    m = sa.gen_rmat(1_000_000, 10_000_000, scale=20, seed=5)
+    x = np.random.default_rng(12).uniform(-1, 1, m.n_cols)
+    y, _, dm = run_fmt(torch, dev, m, "csrg", x=x, groups=groups)
+    assert dm.params["n_pairs"] > m.n_rows // 4
+    assert_parity(m, y, x)
+    y2 = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
+    dm.run(torch.from_numpy(x).to(dev), y2)
+    torch.cuda.synchronize()
+    assert np.array_equal(y.view(np.int64), y2.cpu().numpy().view(np.int64))
+
+
+def test_sell16_refuses_wide_windows(torch_dev):
+    """A workgroup whose columns span more than 65,536 cannot hold 16-bit
+    offsets: the fill refuses and writes nothing (the caller keeps SELL)."""
+    torch, dev = torch_dev
+    m = sa.gen_rmat(200_000, 2_000_000, scale=18, seed=3)
+    with pytest.raises(sa.SpmvError, match="65,536"):
+        sa.to_device(m, "sell16", dev, C=64, sigma=1024)
+    with pytest.raises(sa.SpmvError, match="C must be 64"):
+        sa.to_device(sa.gen_cantlike(0), "sell16", dev, C=32, sigma=1024)
 
 
 @pytest.mark.parametrize("case", ["cantlike", "rmat", "ragged", "fixtures"])

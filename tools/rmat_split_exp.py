@@ -1,0 +1,87 @@
+#!/usr/bin/env python3
+"""R-MAT column-split experiment (GPU box; diagnostic, not product).
+
+Question: does splitting the R-MAT's columns into P groups of whole 128-B x
+lines, and running the entries group after group, let each XCD's 4 MiB L2
+hold the x lines the in-flight tiles gather from, so that the cold-column
+gathers stop filling a line each (profiles/traffic_rmat.json: 3.46x
+bytes_alg)?  The split matrix is the library's column-grouped CSR (format
+"csrg": one pair per (row, column group) with entries, group-major; the
+tiled kernel over the pairs, then the per-row sum of the pair sums).
+
+    python tools/rmat_split_exp.py [--parts 8,16,32,64] [--reps 20]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(REPO / "opencl-spmv-algorithms_amd"), str(REPO)]
+
+
+def time_run(torch, dm, x, y, reps, cold, sa):
+    st = torch.cuda.current_stream()
+    ts = []
+    for r in range(reps + 2):
+        if cold:
+            sa.flush_cache(st)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        dm.run(x, y)
+        e1.record(st)
+        torch.cuda.synchronize()
+        if r >= 2:
+            ts.append(e0.elapsed_time(e1))
+    return float(np.median(ts))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--parts", default="8,16,32,64")
+    ap.add_argument("--reps", type=int, default=20)
+    a = ap.parse_args()
+    import torch
+    import spmv_amd as sa
+
+    dev = torch.device("cuda:0")
+    t = time.time()
+    m = sa.gen_rmat()
+    xh = np.random.default_rng(7).uniform(-1, 1, m.n_cols)
+    x = torch.from_numpy(xh).to(dev)
+    b = sa.bytes_alg(m.n_rows, m.n_cols, m.nnz)
+    print(json.dumps({"setup_s": round(time.time() - t, 1)}), flush=True)
+    # baseline: the product path (tiled CSR + hot table, library rule)
+    dm = sa.to_device(m, "csr", dev)
+    y = torch.empty(m.n_rows, dtype=torch.float64, device=dev)
+    for cold in (0, 1):
+        ms = time_run(torch, dm, x, y, a.reps, cold, sa)
+        print(json.dumps({"variant": "product", "params": dm.params, "cold": cold, "ms": round(ms, 4),
+                          "GBs": round(b / ms * 1e-6, 1)}), flush=True)
+    y_ref = y.cpu().numpy()
+    del dm
+    torch.cuda.empty_cache()
+    for P in [int(p) for p in a.parts.split(",")]:
+        t = time.time()
+        dm = sa.to_device(m, "csrg", dev, groups=P)
+        setup = time.time() - t
+        yg = torch.empty(m.n_rows, dtype=torch.float64, device=dev)
+        res = {}
+        for cold in (0, 1):
+            res["cold" if cold else "warm"] = round(time_run(torch, dm, x, yg, a.reps, cold, sa), 4)
+        yy = yg.cpu().numpy()
+        err = float(np.max(np.abs(yy - y_ref) / np.maximum(np.abs(y_ref), 1e-300)))
+        print(json.dumps({"variant": "csrg", "groups": P, "pairs": dm.params["n_pairs"], "ms": res,
+                          "GBs_warm": round(b / res["warm"] * 1e-6, 1), "GBs_cold": round(b / res["cold"] * 1e-6, 1),
+                          "max_rel_vs_product": err, "setup_s": round(setup, 1)}), flush=True)
+        del dm, yg
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

@@ -159,15 +159,20 @@ int spmv_csr_tiled_plan(spmv_dims d, const int64_t *row_ptr, int32_t *own_lo);
  * (kernels/Csr.cl) on that input.  The entry-balanced kernel runs the
  * n_pairs (row, column-group) pairs group after group, so the x lines the
  * tiles in flight gather from are one group's and stay in L2; each pair's
- * sum goes to the workspace, then every row's pair sums are added in group
- * order.  own_lo_plan: spmv_csr_tiled_plan over (pair_ptr, n_rows =
- * n_pairs), or NULL.  `ws` holds spmv_csrg_ws_bytes(n_pairs, nnz) bytes.
+ * sum goes to the workspace, then one workgroup per SPMV_CSRG_ROWS rows adds
+ * its rows' pair sums in group order in LDS (blk_off / pair_row) and writes
+ * y.  own_lo_plan: spmv_csr_tiled_plan over (pair_ptr, n_rows = n_pairs),
+ * or NULL.  `ws` holds spmv_csrg_ws_bytes(n_pairs, nnz) bytes.
  * Deterministic; agrees with spmv_csr_run to the parity rule (the row sums
  * are grouped by column group).                                          */
+#ifndef SPMV_CSRG_ROWS
+#define SPMV_CSRG_ROWS 4096 /* also in spmv_host.h */
+#endif
 size_t spmv_csrg_ws_bytes(int64_t n_pairs, int64_t nnz);
-int spmv_csrg_run(spmv_dims d, int64_t n_pairs, const int64_t *pair_ptr, const int32_t *col_g,
-                  const double *val_g, const int32_t *own_lo_plan, const int64_t *row_pair_ptr,
-                  const int32_t *row_pair, const double *x, double *y, void *ws, size_t ws_bytes);
+int spmv_csrg_run(spmv_dims d, int32_t groups, int64_t n_pairs, const int64_t *pair_ptr,
+                  const int32_t *col_g, const double *val_g, const int32_t *own_lo_plan,
+                  const int32_t *blk_off, const uint16_t *pair_row, const double *x, double *y,
+                  void *ws, size_t ws_bytes);
 
 /* ---------------------------------------------------------------- ELL ---
  * Replaces kernel `ell(val,idx,x,y,int N,int K,__local)` (reference

@@ -165,16 +165,21 @@ int spmv_csr16_fill(int64_t nnz, const int32_t *col, int32_t *blk_base, uint16_t
  * the PAIRS (row, group) that hold entries, rows ascending, each pair's
  * entries in CSR order.  A run sums every pair (the groups one after
  * another, so the x lines being gathered stay in the L2s) and then adds
- * each row's pair sums in group order (row_pair_ptr / row_pair: the pair
- * indices of row r in group order).  Plan: n_pairs.  Fill: pair_ptr
- * [n_pairs+1], col_g/val_g[nnz], row_pair_ptr[n_rows+1], row_pair
- * [n_pairs].                                                            */
+ * each row's pair sums in group order, block by block of
+ * SPMV_CSRG_ROWS rows: blk_off[g*(nb+1) + b] is the first pair of group g
+ * whose row is >= b*SPMV_CSRG_ROWS (nb = ceil(n_rows / SPMV_CSRG_ROWS)),
+ * pair_row[p] the pair's row modulo SPMV_CSRG_ROWS.  Plan: n_pairs.
+ * Fill: pair_ptr[n_pairs+1], col_g/val_g[nnz], blk_off[groups*(nb+1)],
+ * pair_row[n_pairs].                                                    */
+#ifndef SPMV_CSRG_ROWS
+#define SPMV_CSRG_ROWS 4096 /* also in spmv.h */
+#endif
 int32_t spmv_csrg_group(int32_t col, int32_t groups);
 int spmv_csrg_plan(int64_t n_rows, const int64_t *row_ptr, const int32_t *col, int32_t groups,
                    int64_t *n_pairs);
 int spmv_csrg_fill(int64_t n_rows, const int64_t *row_ptr, const int32_t *col, const double *val,
                    int32_t groups, int64_t *pair_ptr, int32_t *col_g, double *val_g,
-                   int64_t *row_pair_ptr, int32_t *row_pair);
+                   int32_t *blk_off, uint16_t *pair_row);
 
 /* ----------------------------------------------------- multi-GPU shard ---
  * Row-range partition for one process per GPU: `parts`

@@ -1124,22 +1124,44 @@ extern "C" int spmv_csr_f32v_run_tiled_hot(spmv_dims d, const int64_t *row_ptr, 
 // CSRG (host spmv_csrg_fill) stores the entries group after group, each
 // group owning the x lines of 1/G of the columns; the tiled kernel runs the
 // (row, group) pairs in that order, so the tiles in flight gather from one
-// group's lines (~2.5 MB at G = 32) and those stay in L2.  Each pair's sum
-// goes to yp; csrg_reduce_kernel then adds a row's pair sums in group order.
-// Deterministic; the row sums are grouped differently from CSR's, so y
-// agrees with it to the parity rule, not bit for bit.
-__global__ __launch_bounds__(kBlock) void csrg_reduce_kernel(int64_t n_rows, const int64_t *__restrict__ row_pair_ptr,
-                                                             const int32_t *__restrict__ row_pair,
+// group's lines (~5 MB at G = 16) and mostly hit L2.  Each pair's sum goes
+// to yp; csrg_reduce_kernel then adds a row block's pair sums in group order
+// in LDS: every group's pairs of the block are one contiguous run of yp
+// (blk_off), read as a stream.  Deterministic; the row sums are grouped
+// differently from CSR's, so y agrees with it to the parity rule.
+__global__ __launch_bounds__(kBlock) void csrg_reduce_kernel(int64_t n_rows, int32_t groups, int64_t nb,
+                                                             const int32_t *__restrict__ blk_off,
+                                                             const uint16_t *__restrict__ pair_row,
                                                              const double *__restrict__ yp, double *__restrict__ y)
 {
-    const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (r >= n_rows)
-        return;
-    double s = 0.0;
-    const int64_t j1 = row_pair_ptr[r + 1];
-    for (int64_t j = row_pair_ptr[r]; j < j1; ++j)
-        s += yp[row_pair[j]];
-    store_y(y + r, s);
+    constexpr int B = SPMV_CSRG_ROWS;
+    __shared__ double s_y[B];
+    const int64_t b = blockIdx.x;
+    for (int i = threadIdx.x; i < B; i += kBlock)
+        s_y[i] = 0.0;
+    __syncthreads();
+    for (int32_t g = 0; g < groups; ++g) {  // group order: a row's pair sums added g = 0, 1, ...
+        const int32_t p0 = blk_off[(int64_t)g * (nb + 1) + b], p1 = blk_off[(int64_t)g * (nb + 1) + b + 1];
+        for (int32_t p = p0 + (int32_t)threadIdx.x; p < p1; p += 4 * kBlock) {
+            double v[4];
+            int r[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {  // 4 loads in flight; a row appears once per group
+                const int32_t pk = p + k * kBlock;
+                r[k] = pk < p1 ? (int)pair_row[pk] : -1;
+                v[k] = pk < p1 ? yp[pk] : 0.0;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (r[k] >= 0)
+                    s_y[r[k]] += v[k];
+        }
+        __syncthreads();
+    }
+    const int64_t r0 = b * B;
+    for (int i = threadIdx.x; i < B; i += kBlock)
+        if (r0 + i < n_rows)
+            store_y(y + r0 + i, s_y[i]);
 }
 
 extern "C" size_t spmv_csrg_ws_bytes(int64_t n_pairs, int64_t nnz)
@@ -1147,12 +1169,13 @@ extern "C" size_t spmv_csrg_ws_bytes(int64_t n_pairs, int64_t nnz)
     return (size_t)(n_pairs > 0 ? n_pairs : 0) * sizeof(double) + spmv_csr_tiled_ws_bytes(n_pairs, nnz);
 }
 
-extern "C" int spmv_csrg_run(spmv_dims d, int64_t n_pairs, const int64_t *pair_ptr, const int32_t *col_g,
-                             const double *val_g, const int32_t *own_lo_plan, const int64_t *row_pair_ptr,
-                             const int32_t *row_pair, const double *x, double *y, void *ws, size_t ws_bytes)
+extern "C" int spmv_csrg_run(spmv_dims d, int32_t groups, int64_t n_pairs, const int64_t *pair_ptr,
+                             const int32_t *col_g, const double *val_g, const int32_t *own_lo_plan,
+                             const int32_t *blk_off, const uint16_t *pair_row, const double *x, double *y,
+                             void *ws, size_t ws_bytes)
 {
     if (d.n_rows < 0 || d.n_cols < 0 || d.nnz < 0 || d.n_rows > INT32_MAX || n_pairs < 0 ||
-        n_pairs > INT32_MAX || n_pairs > d.nnz || (d.nnz > 0 && n_pairs == 0))
+        n_pairs > INT32_MAX || n_pairs > d.nnz || (d.nnz > 0 && n_pairs == 0) || groups < 1 || groups > 64)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_csrg_run: bad sizes");
     if (d.n_rows == 0)
         return SPMV_SUCCESS;
@@ -1161,7 +1184,7 @@ extern "C" int spmv_csrg_run(spmv_dims d, int64_t n_pairs, const int64_t *pair_p
         hipError_t e = hipMemsetAsync(y, 0, (size_t)d.n_rows * sizeof(double), (hipStream_t)d.stream);
         return e == hipSuccess ? SPMV_SUCCESS : fail(SPMV_PROGRAM_ERROR, "memset y", e);
     }
-    if (!pair_ptr || !col_g || !val_g || !row_pair_ptr || !row_pair || !ws ||
+    if (!pair_ptr || !col_g || !val_g || !blk_off || !pair_row || !ws ||
         ws_bytes < spmv_csrg_ws_bytes(n_pairs, d.nnz))
         return fail_msg(SPMV_OTHER_ERROR, "spmv_csrg_run: arrays or workspace missing");
     double *yp = (double *)ws;
@@ -1171,8 +1194,9 @@ extern "C" int spmv_csrg_run(spmv_dims d, int64_t n_pairs, const int64_t *pair_p
                            "spmv_csrg_run");
     if (rc != SPMV_SUCCESS)
         return rc;
-    hipLaunchKernelGGL(csrg_reduce_kernel, dim3((unsigned)((d.n_rows + kBlock - 1) / kBlock)), dim3(kBlock), 0,
-                       (hipStream_t)d.stream, d.n_rows, row_pair_ptr, row_pair, yp, y);
+    const int64_t nb = (d.n_rows + SPMV_CSRG_ROWS - 1) / SPMV_CSRG_ROWS;
+    hipLaunchKernelGGL(csrg_reduce_kernel, dim3((unsigned)nb), dim3(kBlock), 0, (hipStream_t)d.stream, d.n_rows,
+                       groups, nb, blk_off, pair_row, yp, y);
     SPMV_CHECK_LAUNCH("csrg_reduce_kernel");
     return SPMV_SUCCESS;
 }

@@ -680,72 +680,76 @@ int spmv_csrg_plan(int64_t n_rows, const int64_t *row_ptr, const int32_t *col, i
     return SPMV_SUCCESS;
 }
 
-/* Rows are cut into chunks; pass 1 counts each chunk's pairs and entries
- * per group, a prefix over (group, chunk) gives every chunk its starting
- * pair and entry in every group, pass 2 writes them.  Same layout for any
- * thread count. */
+/* Rows are cut into blocks of SPMV_CSRG_ROWS; pass 1 counts each block's
+ * pairs and entries per group, a prefix over (group, block) gives every
+ * block its starting pair and entry in every group (the group-major
+ * layout, and blk_off), pass 2 writes them.  Same layout for any thread
+ * count. */
 int spmv_csrg_fill(int64_t n_rows, const int64_t *row_ptr, const int32_t *col, const double *val,
                    int32_t groups, int64_t *pair_ptr, int32_t *col_g, double *val_g,
-                   int64_t *row_pair_ptr, int32_t *row_pair)
+                   int32_t *blk_off, uint16_t *pair_row)
 {
-    if (n_rows < 0 || groups < 1 || groups > 64 || !row_ptr || !pair_ptr || !row_pair_ptr)
+    if (n_rows < 0 || groups < 1 || groups > 64 || !row_ptr || !pair_ptr || !blk_off)
         return SPMV_OTHER_ERROR;
     const int64_t nnz = row_ptr[n_rows];
-    if (nnz > 0 && (!col || !val || !col_g || !val_g || !row_pair))
+    if (nnz > 0 && (!col || !val || !col_g || !val_g || !pair_row))
         return SPMV_OTHER_ERROR;
-    const int64_t NCH = 256;
-    const int64_t per = (n_rows + NCH - 1) / NCH > 0 ? (n_rows + NCH - 1) / NCH : 1;
+    const int64_t B = SPMV_CSRG_ROWS;
+    const int64_t nb = (n_rows + B - 1) / B;
     const int G = groups;
-    int64_t *pc = calloc((size_t)(NCH * G), sizeof(int64_t)); /* pairs of chunk k in group g: [g*NCH + k] */
-    int64_t *ec = calloc((size_t)(NCH * G), sizeof(int64_t)); /* entries */
+    int64_t *pc = calloc((size_t)((nb + 1) * G), sizeof(int64_t)); /* pairs of block k in group g: [g*(nb+1) + k] */
+    int64_t *ec = calloc((size_t)((nb + 1) * G), sizeof(int64_t)); /* entries */
     if (!pc || !ec) {
         free(pc);
         free(ec);
         return SPMV_OTHER_ERROR;
     }
-#pragma omp parallel for schedule(dynamic, 1)
-    for (int64_t k = 0; k < NCH; ++k) {
-        const int64_t r0 = k * per, r1 = r0 + per < n_rows ? r0 + per : n_rows;
-        for (int64_t r = r0; r < r1; ++r) {
+#pragma omp parallel for schedule(dynamic, 16)
+    for (int64_t k = 0; k < nb; ++k) {
+        const int64_t r1 = (k + 1) * B < n_rows ? (k + 1) * B : n_rows;
+        for (int64_t r = k * B; r < r1; ++r) {
             uint64_t m = 0;
             for (int64_t e = row_ptr[r]; e < row_ptr[r + 1]; ++e) {
                 const int32_t g = spmv_csrg_group(col[e], groups);
                 m |= 1ULL << g;
-                ++ec[g * NCH + k];
+                ++ec[g * (nb + 1) + k];
             }
             for (; m; m &= m - 1)
-                ++pc[__builtin_ctzll(m) * NCH + k];
+                ++pc[__builtin_ctzll(m) * (nb + 1) + k];
         }
     }
-    /* exclusive prefix in (group, chunk) order = the group-major layout */
+    /* exclusive prefix in (group, block) order; entry nb of each group row
+     * is the group's end (= the next group's start) */
     int64_t ps = 0, es = 0;
-    for (int64_t i = 0; i < NCH * G; ++i) {
-        const int64_t p = pc[i], e = ec[i];
+    for (int64_t i = 0; i < (nb + 1) * G; ++i) {
+        const int64_t pn = pc[i], en = ec[i];
         pc[i] = ps;
         ec[i] = es;
-        ps += p;
-        es += e;
+        ps += pn;
+        es += en;
     }
+    if (ps > (int64_t)INT32_MAX) {
+        free(pc);
+        free(ec);
+        return SPMV_OTHER_ERROR;
+    }
+    for (int64_t i = 0; i < (nb + 1) * G; ++i)
+        blk_off[i] = (int32_t)pc[i];
     pair_ptr[ps] = es;
-    /* row_pair_ptr: pairs of each row (group order inside a row) */
-    row_pair_ptr[0] = 0;
-    for (int64_t r = 0; r < n_rows; ++r)
-        row_pair_ptr[r + 1] = row_pair_ptr[r] + __builtin_popcountll(csrg_mask(row_ptr, col, r, groups));
-#pragma omp parallel for schedule(dynamic, 1)
-    for (int64_t k = 0; k < NCH; ++k) {
+#pragma omp parallel for schedule(dynamic, 16)
+    for (int64_t k = 0; k < nb; ++k) {
         int64_t pn[64], en[64];
         for (int g = 0; g < G; ++g) {
-            pn[g] = pc[g * NCH + k];
-            en[g] = ec[g * NCH + k];
+            pn[g] = pc[g * (nb + 1) + k];
+            en[g] = ec[g * (nb + 1) + k];
         }
-        const int64_t r0 = k * per, r1 = r0 + per < n_rows ? r0 + per : n_rows;
-        for (int64_t r = r0; r < r1; ++r) {
+        const int64_t r1 = (k + 1) * B < n_rows ? (k + 1) * B : n_rows;
+        for (int64_t r = k * B; r < r1; ++r) {
             const uint64_t m = csrg_mask(row_ptr, col, r, groups);
-            int64_t rp = row_pair_ptr[r];
             for (uint64_t mm = m; mm; mm &= mm - 1) { /* each group of the row: open its pair */
                 const int g = __builtin_ctzll(mm);
                 pair_ptr[pn[g]] = en[g];
-                row_pair[rp++] = (int32_t)pn[g];
+                pair_row[pn[g]] = (uint16_t)(r - k * B);
             }
             for (int64_t e = row_ptr[r]; e < row_ptr[r + 1]; ++e) { /* entries in CSR order */
                 const int g = spmv_csrg_group(col[e], groups);

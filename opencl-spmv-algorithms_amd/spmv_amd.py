@@ -31,7 +31,8 @@ FORMATS = ("coo", "csr", "ell", "sell", "cmrs")  # the reference's five
 # SELL-C-σ with 16-bit column offsets
 EXTRA_FORMATS = ("csr16", "hyb", "csrf32", "sell16")
 ALL_FORMATS = FORMATS + EXTRA_FORMATS
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0
+CSRG_ROWS = 4096  # SPMV_CSRG_ROWS (include/spmv.h): rows per block of the CSRG reduce  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 # The reference's ReturnCode values (reference inc/enums.h:4-11).
 SUCCESS, DEVICE_ERROR, PROGRAM_ERROR, FILE_ERROR, OTHER_ERROR = range(5)
@@ -94,7 +95,8 @@ HIP_SYMBOLS = {
     "spmv_csr_tiled_plan_len": (_c_i64, [_c_i64]),
     "spmv_csr_tiled_plan": (ctypes.c_int, [Dims, _vp, _vp]),
     "spmv_csrg_ws_bytes": (ctypes.c_size_t, [_c_i64, _c_i64]),
-    "spmv_csrg_run": (ctypes.c_int, [Dims, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t]),
+    "spmv_csrg_run": (ctypes.c_int, [Dims, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                     ctypes.c_size_t]),
     "spmv_csr16_run": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_int]),
     "spmv_csr16_run_xwin": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_int, _c_i32, _vp,
                                            _c_i32]),
@@ -498,20 +500,23 @@ def csr16_build(col: np.ndarray):
 
 def csrg_build(n_rows: int, ptr, col, val, groups: int = 32):
     """Column-grouped CSR (spmv_host.h spmv_csrg_plan/fill): the entries
-    group after group of 128-B x lines, as a CSR over (row, group) pairs."""
+    group after group of 128-B x lines, as a CSR over (row, group) pairs,
+    plus the per-row-block pair ranges of the reduce."""
     lib = host_lib()
     npairs = _c_i64(0)
     _check_host(lib.spmv_csrg_plan(n_rows, _ptr(ptr), _ptr(col), groups, ctypes.byref(npairs)), "csrg_plan")
     n = npairs.value
     nnz = int(ptr[n_rows])
+    nb = (n_rows + CSRG_ROWS - 1) // CSRG_ROWS
     pair_ptr = np.empty(n + 1, np.int64)
     col_g = np.empty(max(nnz, 1), np.int32)
     val_g = np.empty(max(nnz, 1), np.float64)
-    rpp = np.empty(n_rows + 1, np.int64)
-    rp = np.empty(max(n, 1), np.int32)
+    blk_off = np.empty(groups * (nb + 1), np.int32)
+    pair_row = np.empty(max(n, 1), np.uint16)
     _check_host(lib.spmv_csrg_fill(n_rows, _ptr(ptr), _ptr(col), _ptr(val), groups, _ptr(pair_ptr), _ptr(col_g),
-                                   _ptr(val_g), _ptr(rpp), _ptr(rp)), "csrg_fill")
-    return dict(groups=groups, n_pairs=n, pair_ptr=pair_ptr, col_g=col_g, val_g=val_g, row_pair_ptr=rpp, row_pair=rp)
+                                   _ptr(val_g), _ptr(blk_off), _ptr(pair_row)), "csrg_fill")
+    return dict(groups=groups, n_pairs=n, nb=nb, pair_ptr=pair_ptr, col_g=col_g, val_g=val_g, blk_off=blk_off,
+                pair_row=pair_row)
 
 
 def partition_rows(n_rows: int, ptr: np.ndarray, parts: int, align: int = 1024,
@@ -675,9 +680,9 @@ class DeviceMatrix:
         elif self.fmt == "ell":
             rc = lib.spmv_ell_run(d, p["K"], p["ld"], p["ki"], _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y))
         elif self.fmt == "csrg":
-            rc = lib.spmv_csrg_run(d, p["n_pairs"], _ptr(a["pair_ptr"]), _ptr(a["col_g"]), _ptr(a["val_g"]),
-                                   _ptr(a.get("own_lo")), _ptr(a["row_pair_ptr"]), _ptr(a["row_pair"]), _ptr(x),
-                                   _ptr(y), _ptr(a["ws"]), a["ws"].numel())
+            rc = lib.spmv_csrg_run(d, p["groups"], p["n_pairs"], _ptr(a["pair_ptr"]), _ptr(a["col_g"]),
+                                   _ptr(a["val_g"]), _ptr(a.get("own_lo")), _ptr(a["blk_off"]), _ptr(a["pair_row"]),
+                                   _ptr(x), _ptr(y), _ptr(a["ws"]), a["ws"].numel())
         elif self.fmt == "sell16":
             rc = lib.spmv_sell16_run(d, p["C"], p["sigma"], p["ki"], p["n_slices"], _ptr(a["slice_ptr"]),
                                      _ptr(a["perm"]), _ptr(a["col16"]), _ptr(a["val"]), _ptr(x), _ptr(y),
@@ -972,7 +977,8 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
         # column-grouped CSR for gather-bound power-law matrices (R-MAT)
         g = csrg_build(m.n_rows, ptr, col, val, groups=groups or 32)
         dm.params = dict(groups=g["groups"], n_pairs=g["n_pairs"])
-        dm.arrays = {k: _dev_tensor(g[k], device) for k in ("pair_ptr", "col_g", "val_g", "row_pair_ptr", "row_pair")}
+        dm.arrays = {k: _dev_tensor(g[k], device) for k in ("pair_ptr", "col_g", "val_g", "blk_off")}
+        dm.arrays["pair_row"] = _dev_tensor(g["pair_row"].view(np.int16), device)
         ws = hip_lib().spmv_csrg_ws_bytes(g["n_pairs"], m.nnz)
         dm.arrays["ws"] = torch.empty(max(ws, 16), dtype=torch.uint8, device=device)
         n_plan = hip_lib().spmv_csr_tiled_plan_len(m.nnz)
@@ -981,7 +987,7 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
             pd = Dims(g["n_pairs"], m.n_cols, m.nnz, device.index or 0, torch.cuda.current_stream(device).cuda_stream)
             _check(hip_lib().spmv_csr_tiled_plan(pd, _ptr(dm.arrays["pair_ptr"]), _ptr(dm.arrays["own_lo"])),
                    "spmv_csr_tiled_plan")
-        dm.stored_bytes = 12 * m.nnz + 8 * (g["n_pairs"] + 1) + 8 * (m.n_rows + 1) + 4 * g["n_pairs"]
+        dm.stored_bytes = 12 * m.nnz + 10 * g["n_pairs"] + 4 * g["blk_off"].size
     elif fmt == "sell16":
         # SELL-C-σ with 16-bit column offsets from each workgroup's window base
         # (§8f row 4): the SELL build, the x windows, then the device pass

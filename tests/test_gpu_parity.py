@@ -445,7 +445,7 @@ def test_sell_xwin_bit_identical(torch_dev, case, ki):
     assert_parity(m, ys[1].cpu().numpy(), x.cpu().numpy())
 
 
-@pytest.mark.parametrize("case", ["cantlike", "cantlike16", "ragged", "banded"])
+@pytest.mark.parametrize("case", ["cantlike", "cantlike16", "ragged", "ragged_wide"])
 @pytest.mark.parametrize("ki", [1, 2])
 def test_sell16_bit_identical_to_sell(torch_dev, case, ki):
     """SELL16 decodes the same columns and sums in the same order as the
@@ -458,11 +458,8 @@ def test_sell16_bit_identical_to_sell(torch_dev, case, ki):
         m = sa.gen_cantlike(1, copies=16)
     elif case == "ragged":
         m = sa.gen_random(20_000, 20_000, 0, 700, seed=21)
-    else:
-        n = 600_000
-        ptr, col, val = sa.gen_banded_csr(n, 0, n)
-        row = np.repeat(np.arange(n, dtype=np.int32), np.diff(ptr))
-        m = sa.Coo(n, n, row, col, val, False, "banded")
+    else:  # columns up to 65,000 apart inside a workgroup: offsets near the 16-bit limit
+        m = sa.gen_random(30_000, 65_000, 1, 40, seed=22)
     x = torch.from_numpy(np.random.default_rng(9).uniform(-1, 1, m.n_cols)).to(dev)
     ys = []
     for fmt in ("sell", "sell16"):
@@ -607,6 +604,37 @@ def test_csr_hot_bit_identical(torch_dev, H):
     assert torch.equal(ya.view(torch.int64), yb.view(torch.int64))
     assert torch.equal(yc.view(torch.int64), yb.view(torch.int64))
     assert_parity(m, ya.cpu().numpy(), x.cpu().numpy())
+
+
+@pytest.mark.parametrize("case,H", [("rmat", 1 << 16), ("rmat", 100), ("rmat", 1 << 19), ("rmat_odd", 4096),
+                                    ("empty_runs", 1024)])
+def test_csr_tiled_lds_bit_identical(torch_dev, monkeypatch, case, H):
+    """The persistent tiled kernel with the hottest table entries in LDS
+    (csr_tiled_lds_kernel: 1024-thread workgroups, four tiles at a time, the
+    next tile's pair issued early) gives the bits of csr_tiled_kernel<L, 1>
+    (SPMV_TILED_LDS=0) on the same hot table: tables smaller and larger than
+    the LDS part, an odd entry count (the array's last entry loaded singly),
+    tiles owning more rows than the LDS offset table and a row over many
+    tiles."""
+    torch, dev = torch_dev
+    if case == "rmat":
+        m = sa.gen_rmat(1_000_000, 10_000_000, scale=20, seed=1)
+    elif case == "rmat_odd":
+        m = sa.gen_rmat(300_000, 2_999_999, scale=19, seed=4)
+    else:
+        m, _ = _empty_run_matrix()
+    dm = sa.to_device(m, "csr", dev, variant=4, hot=H)
+    assert dm.params["H"] == H
+    x = torch.from_numpy(np.random.default_rng(13).uniform(-1, 1, m.n_cols)).to(dev)
+    ys = []
+    for knob in ("0", "1"):
+        monkeypatch.setenv("SPMV_TILED_LDS", knob)
+        y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
+        dm.run(x, y)
+        torch.cuda.synchronize()
+        ys.append(y)
+    assert torch.equal(ys[0].view(torch.int64), ys[1].view(torch.int64))
+    assert_parity(m, ys[1].cpu().numpy(), x.cpu().numpy())
 
 
 def _empty_run_matrix(seed=11):

@@ -524,41 +524,55 @@ def test_row_shard_bad_arguments():
     assert L.spmv_coo_row_shard(0, None, None, None, 0, 0, None, None, None) == 0
 
 
-@pytest.mark.parametrize("kind,groups", [("rmat", 32), ("rmat", 64), ("random", 7), ("empty_rows", 3), ("one", 1)])
+@pytest.mark.parametrize("kind,groups", [("rmat", 32), ("rmat", 64), ("random", 7), ("empty_rows", 3), ("one", 1),
+                                         ("tall", 5)])
 def test_csrg_layout(kind, groups):
     """Column-grouped CSR: entries group after group (groups of whole 16-column
-    x lines), each pair one (row, group) with its entries in CSR order; the
-    pair sums added per row in group order give the CSR product."""
+    x lines), each pair one (row, group) with its entries in CSR order, rows
+    ascending in a group; blk_off / pair_row name every pair's row block and
+    row; the pair sums added per row in group order give the CSR product."""
     if kind == "rmat":
         m = sa.gen_rmat(100_000, 1_000_000, scale=17, seed=2)
     elif kind == "random":
         m = sa.gen_random(5_000, 3_000, 0, 50, seed=3)
     elif kind == "empty_rows":
         m = sa.read_mtx(GOLDEN / "empty_rows.mtx")
+    elif kind == "tall":  # several row blocks, trailing empty block
+        m = sa.gen_random(20_000, 900, 0, 4, seed=5)
     else:
         m = sa.gen_random(100, 100, 0, 3, seed=1)
     ptr, col, val = sa.csr_from_coo(m)
     g = sa.csrg_build(m.n_rows, ptr, col, val, groups)
-    n, pp, nnz = g["n_pairs"], g["pair_ptr"], m.nnz
+    n, pp, nnz, nb, B = g["n_pairs"], g["pair_ptr"], m.nnz, g["nb"], sa.CSRG_ROWS
+    assert nb == (m.n_rows + B - 1) // B
     assert pp[0] == 0 and pp[n] == nnz and (np.diff(pp) > 0).all()
     grp = np.array([sa.host_lib().spmv_csrg_group(int(c), groups) for c in g["col_g"][:nnz]])
     assert (np.diff(grp) >= 0).all()  # group-major
     assert all(sa.host_lib().spmv_csrg_group(c, groups) == sa.host_lib().spmv_csrg_group(c | 15, groups)
                for c in range(0, 4096, 16))  # a 128-B line is in one group
-    # every pair's entries in one row and one group, rows ascending inside a group
-    rpp, rp = g["row_pair_ptr"], g["row_pair"]
-    pair_row = np.repeat(np.arange(m.n_rows), np.diff(rpp))[np.argsort(rp[:n], kind="stable")]
-    for k in range(0, n, max(1, n // 500)):
+    off = g["blk_off"].reshape(groups, nb + 1).astype(np.int64)
+    assert off[0, 0] == 0 and off[-1, -1] == n and (np.diff(off.ravel()) >= 0).all()
+    pair_row = np.empty(n, np.int64)
+    pair_grp = np.empty(n, np.int64)
+    for gg in range(groups):
+        for b in range(nb):
+            pair_row[off[gg, b]:off[gg, b + 1]] = b * B + g["pair_row"][off[gg, b]:off[gg, b + 1]].astype(np.int64)
+            pair_grp[off[gg, b]:off[gg, b + 1]] = gg
+    for gg in range(groups):  # rows ascending and distinct inside a group
+        rows = pair_row[pair_grp == gg]
+        assert (np.diff(rows) > 0).all()
+    for k in range(0, n, max(1, n // 500)):  # a pair = that row's entries of that group, CSR order
         e0, e1 = pp[k], pp[k + 1]
-        assert len(set(grp[e0:e1])) == 1
+        assert (grp[e0:e1] == pair_grp[k]).all()
         r = pair_row[k]
         row_cols = col[ptr[r]:ptr[r + 1]]
         row_grp = np.array([sa.host_lib().spmv_csrg_group(int(c), groups) for c in row_cols])
-        assert np.array_equal(g["col_g"][e0:e1], row_cols[row_grp == grp[e0]])
+        assert np.array_equal(g["col_g"][e0:e1], row_cols[row_grp == pair_grp[k]])
     x = np.random.default_rng(1).uniform(-1, 1, m.n_cols)
     prod = g["val_g"][:nnz] * x[g["col_g"][:nnz]]
     yp = np.add.reduceat(prod, pp[:-1]) if n else np.zeros(0)
-    y = np.array([yp[rp[rpp[r]:rpp[r + 1]]].sum() for r in range(m.n_rows)])
+    y = np.zeros(m.n_rows)
+    np.add.at(y, pair_row, yp)
     y_ref = np.zeros(m.n_rows)
     np.add.at(y_ref, m.row, m.val * x[m.col])
     assert np.allclose(y, y_ref, rtol=1e-12, atol=1e-12)

@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import os
 import sys
 import time
 from pathlib import Path
@@ -45,6 +46,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--parts", default="8,16,32,64")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--colmaps", default="",
+                    help="also time the product kernel (no hot table) with the columns replaced: "
+                         "zero, mod<k>, rand<k> (uniform over k columns), comma-separated")
     a = ap.parse_args()
     import torch
     import spmv_amd as sa
@@ -56,16 +60,41 @@ def main():
     x = torch.from_numpy(xh).to(dev)
     b = sa.bytes_alg(m.n_rows, m.n_cols, m.nnz)
     print(json.dumps({"setup_s": round(time.time() - t, 1)}), flush=True)
-    # baseline: the product path (tiled CSR + hot table, library rule)
+    # baseline: the product path (tiled CSR + hot table, library rule), with
+    # and without the LDS table (SPMV_TILED_LDS, same bits), interleaved
     dm = sa.to_device(m, "csr", dev)
     y = torch.empty(m.n_rows, dtype=torch.float64, device=dev)
-    for cold in (0, 1):
-        ms = time_run(torch, dm, x, y, a.reps, cold, sa)
-        print(json.dumps({"variant": "product", "params": dm.params, "cold": cold, "ms": round(ms, 4),
-                          "GBs": round(b / ms * 1e-6, 1)}), flush=True)
+    outs = {}
+    for rnd in range(2):
+        for knob in ("0", "1"):
+            os.environ["SPMV_TILED_LDS"] = knob
+            for cold in (0, 1):
+                ms = time_run(torch, dm, x, y, a.reps, cold, sa)
+                print(json.dumps({"variant": "product", "lds": knob, "round": rnd, "params": dm.params, "cold": cold,
+                                  "ms": round(ms, 4), "GBs": round(b / ms * 1e-6, 1)}), flush=True)
+            outs[knob] = y.clone()
+    os.environ.pop("SPMV_TILED_LDS", None)
+    print(json.dumps({"lds_same_bits": bool(torch.equal(outs["0"].view(torch.int64), outs["1"].view(torch.int64)))}),
+          flush=True)
     y_ref = y.cpu().numpy()
     del dm
     torch.cuda.empty_cache()
+    # gather-cost probes: same rows, same tiles, columns replaced
+    for cm in [c for c in a.colmaps.split(",") if c]:
+        if cm == "zero":
+            c2 = np.zeros_like(m.col)
+        elif cm.startswith("mod"):
+            c2 = (np.arange(m.nnz, dtype=np.int64) * 7919 % int(cm[3:])).astype(np.int32)
+        else:
+            c2 = np.random.default_rng(3).integers(0, int(cm[4:]), m.nnz).astype(np.int32)
+        m2 = sa.Coo(m.n_rows, m.n_cols, m.row, c2, m.val, False, cm)
+        dm = sa.to_device(m2, "csr", dev, variant=4, hot=0)
+        for cold in (0, 1):
+            ms = time_run(torch, dm, x, y, a.reps, cold, sa)
+            print(json.dumps({"variant": "colmap", "map": cm, "cold": cold, "ms": round(ms, 4),
+                              "GBs": round(b / ms * 1e-6, 1)}), flush=True)
+        del dm, m2, c2
+        torch.cuda.empty_cache()
     for P in [int(p) for p in a.parts.split(",")]:
         t = time.time()
         dm = sa.to_device(m, "csrg", dev, groups=P)

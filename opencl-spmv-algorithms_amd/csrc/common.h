@@ -216,21 +216,6 @@ struct XHot {
     __device__ __forceinline__ double operator()(int32_t c) const { return c >= M ? xh[c - M] : x[c]; }
 };
 
-// Hot-column CSR with the K hottest table entries (xh[0..K), ranks by
-// descending count) also copied into the workgroup's LDS: a gather of one
-// of them is a ds_read instead of an L2 request.
-struct XHotLds {
-    const double *__restrict__ x;
-    const double *__restrict__ xh;
-    const double *s;  // LDS: xh[0..K)
-    int32_t M, K;
-    __device__ __forceinline__ double operator()(int32_t c) const
-    {
-        const int32_t h = c - M;
-        return h < 0 ? x[c] : h < K ? s[h] : xh[h];
-    }
-};
-
 // [min, max] of col[e0..e1) over one 256-thread workgroup ({0, -1} when
 // empty); the result is valid in thread 0.  Build-time pass of the
 // x-window kernels.

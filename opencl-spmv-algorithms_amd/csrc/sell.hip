@@ -16,6 +16,7 @@
 // loaded (that is the format's cost) but re-use the row's own column.
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include "common.h"
 
@@ -450,14 +451,22 @@ __global__ __launch_bounds__(1024) void sell_xwin_kernel(
 // reads for a 49 MB matrix); four slices share it.
 template <int KI> constexpr int sell_small_g() { return 8; }  // first-batch slot groups per lane
 
-template <int KI, bool NT, bool XWIN, typename XS, typename CT = int32_t>
+// WF (window first): the x-window loads are issued before the first batch
+// and written to LDS as soon as they land (they are the older loads), so the
+// barrier waits for the window only and the products start as the batch
+// arrives; with G = 16 nearly every cant-like lane has all its groups in
+// flight at once.  Same accumulators in the same order for any G that is a
+// multiple of 4: the bits do not change.
+template <int KI, bool NT, bool XWIN, typename XS, typename CT = int32_t, int G = sell_small_g<KI>(),
+          bool WF = false>
 __global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell_small_kernel(
     int64_t n_slices, const int64_t *__restrict__ slice_ptr,
     const int32_t *__restrict__ perm, const CT *__restrict__ col,
     const double *__restrict__ val, const XS xs, double *__restrict__ y, int64_t wcap,
     const double *__restrict__ x, const int2 *__restrict__ win, int32_t xcap)
 {
-    constexpr int S = kSellSmallS, P = kSellSmallP, G = sell_small_g<KI>();
+    constexpr int S = kSellSmallS, P = kSellSmallP, T = kWave * S * P;
+    static_assert(G % 4 == 0, "first batch: whole accumulator rounds");
     constexpr bool c16 = std::is_same<CT, uint16_t>::value;  // SELL16: offsets from the window base
     static_assert(!c16 || XWIN, "SELL16 needs the workgroup windows");
     constexpr int64_t step = (int64_t)kWave * KI;  // elements between slot groups
@@ -466,6 +475,23 @@ __global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell_small_
     const int64_t s = (int64_t)blockIdx.x * P + wv / S;
     const int ws = wv % S;  // wave within its slice
     const bool live = s < n_slices;  // uniform per wave
+    bool staged = false;
+    int2 wnd = make_int2(0, -1);
+    constexpr int WU = 4;  // window entries per thread issued ahead (WF)
+    double wv_ahead[WU];
+    int32_t span = 0;
+    if constexpr (XWIN && WF) {
+        wnd = win[blockIdx.x];
+        span = wnd.y - wnd.x + 1;
+        staged = span > 0 && span <= xcap;  // uniform per workgroup
+        if (staged) {
+#pragma unroll
+            for (int k = 0; k < WU; ++k) {
+                const int32_t i = (int32_t)threadIdx.x + k * T;
+                wv_ahead[k] = x[wnd.x + (i < span ? i : span - 1)];
+            }
+        }
+    }
     const int64_t base = live ? slice_ptr[s] : 0;
     int64_t w = live ? (slice_ptr[s + 1] - base) / kWave : 0;
     w = w < wcap ? w : wcap;
@@ -479,14 +505,24 @@ __global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell_small_
     SlotBatch<KI, NT, G> first;
     if (any)
         first.load(vp, cp, g0, g1, step);
-    bool staged = false;
-    int2 wnd = make_int2(0, -1);
-    if constexpr (XWIN) {
+    if constexpr (XWIN && WF) {
+        if (staged) {
+#pragma unroll
+            for (int k = 0; k < WU; ++k) {
+                const int32_t i = (int32_t)threadIdx.x + k * T;
+                if (i < span)
+                    s_x[i] = wv_ahead[k];
+            }
+            if (span > WU * T)  // wider windows: the rest after the batch
+                copy_window<T, 4>(s_x + WU * T, x, wnd.x + WU * T, span - WU * T);
+        }
+        __syncthreads();
+    } else if constexpr (XWIN) {
         wnd = win[blockIdx.x];
-        const int32_t span = wnd.y - wnd.x + 1;
+        span = wnd.y - wnd.x + 1;
         staged = span > 0 && span <= xcap;  // uniform per workgroup
         if (staged)
-            copy_window<kWave * S * P, 4>(s_x, x, wnd.x, span);
+            copy_window<T, 4>(s_x, x, wnd.x, span);
         __syncthreads();
     }
     const int32_t row = live && ws == 0 ? perm[s * kWave + lane] : -1;
@@ -534,6 +570,18 @@ bool sell_small(int32_t C, int64_t n_slices)
     return n_slices < 14 * (int64_t)cus;
 }
 
+// SPMV_SELL_SMALL=<G>[w] picks the first-batch size G (8, 12 or 16) and the
+// window-first order for A/B runs (same bits); default 8, batch first.
+static int sell_small_shape()
+{
+    const char *e = getenv("SPMV_SELL_SMALL");
+    if (!e || !e[0])
+        return 8;
+    const int g = atoi(e);
+    const bool wf = strchr(e, 'w') != nullptr;
+    return (g == 12 || g == 16 ? g : 8) + (wf ? 100 : 0);
+}
+
 template <int KI, bool NT, bool XWIN, typename XS, typename CT = int32_t>
 static void launch_sell_small(int64_t n_slices, const int64_t *slice_ptr, const int32_t *perm, const CT *col,
                               const double *val, const XS xs, double *y, int64_t wcap, const double *x,
@@ -541,9 +589,20 @@ static void launch_sell_small(int64_t n_slices, const int64_t *slice_ptr, const 
 {
     const size_t lds = XWIN ? (size_t)xcap * sizeof(double) : 0;
     const int64_t blocks = (n_slices + kSellSmallP - 1) / kSellSmallP;
-    hipLaunchKernelGGL((sell_small_kernel<KI, NT, XWIN, XS, CT>), dim3((unsigned)blocks),
-                       dim3(kWave * kSellSmallS * kSellSmallP), lds, st, n_slices, slice_ptr, perm, col, val, xs, y,
-                       wcap, x, win, xcap);
+    const int shape = XWIN ? sell_small_shape() : 8;
+#define SPMV_SMALL_SHAPE(GG, WFF)                                                                            \
+    hipLaunchKernelGGL((sell_small_kernel<KI, NT, XWIN, XS, CT, GG, WFF>), dim3((unsigned)blocks),           \
+                       dim3(kWave * kSellSmallS * kSellSmallP), lds, st, n_slices, slice_ptr, perm, col, val, xs, \
+                       y, wcap, x, win, xcap)
+    switch (shape) {
+    case 12: SPMV_SMALL_SHAPE(12, false); break;
+    case 16: SPMV_SMALL_SHAPE(16, false); break;
+    case 108: SPMV_SMALL_SHAPE(8, true); break;
+    case 112: SPMV_SMALL_SHAPE(12, true); break;
+    case 116: SPMV_SMALL_SHAPE(16, true); break;
+    default: SPMV_SMALL_SHAPE(8, false); break;
+    }
+#undef SPMV_SMALL_SHAPE
 }
 
 // x-window variant when win != NULL (windows from spmv_sell_xwin_build:

@@ -405,7 +405,18 @@ constexpr int kTiledRowCap = 1024;
 // (A fused carry — the last-arriving tile of a spanning row finishing it —
 // was bit-identical but slower: 0.890 vs 0.856 ms on R-MAT with the
 // partials passed through RMW atomics, 5.9 ms with agent-scope
-// release/acquire; removed)
+// release/acquire; removed, DESIGN.md §6.  A persistent form with the
+// hottest 16 K table entries in LDS, one 1024-thread workgroup per CU:
+// bit-identical, 2.21 vs 0.83 ms — four tiles in flight per CU instead of
+// eight; removed)
+//
+// Load order: a tile's dependent round trips are the latency the grid
+// waits out (R-MAT with every column = 0, i.e. no gather cost at all:
+// 0.58 ms of the 0.83).  The value/column pairs need the tile index only,
+// so they are issued first; own_lo (a scalar load) and then the row
+// offsets go out behind them into registers; the gathers follow once the
+// columns land; offsets and products reach LDS together before the one
+// barrier, and the carry reads row_ptr[r_lo] from the staged offsets.
 template <int L, int R, bool NT, typename XS, typename V = double>
 __global__ __launch_bounds__(kBlock) void csr_tiled_kernel(
     int64_t n_rows, int64_t nnz, const int64_t *__restrict__ row_ptr,
@@ -416,34 +427,56 @@ __global__ __launch_bounds__(kBlock) void csr_tiled_kernel(
 {
     constexpr int CH = 2 * kBlock * R;
     constexpr int GROUPS = kBlock / L;
+    constexpr int RPK = (kTiledRowCap + 1 + kBlock - 1) / kBlock;  // staged offsets per thread
     __shared__ double2 s_prod[kBlock * R];
     __shared__ int32_t s_rp[kTiledRowCap + 1];
     const double *prod = reinterpret_cast<const double *>(s_prod);
     const int64_t tile = blockIdx.x;
     const int64_t t0 = tile * CH;
     const int64_t t1 = t0 + CH < nnz ? t0 + CH : nnz;
+    StageRegs<R, NT, V, KeysNone> st;
+    st.issue(t0, t1, nnz, col, val, KeysNone{});
     const int64_t r_lo = own_lo[tile];
     const int64_t r_hi = t1 == nnz ? n_rows - 1 : (int64_t)own_lo[tile + 1] - 1;
     const int64_t nr = r_hi - r_lo + 1;  // owned rows (may be 0)
     const bool rp_lds = nr >= 0 && nr <= kTiledRowCap;  // uniform
-    if (rp_lds)
-        for (int i = threadIdx.x; i <= nr; i += kBlock) {  // r_lo + nr <= n_rows
-            const int64_t o = row_ptr[r_lo + i];
-            s_rp[i] = (int32_t)((o < t1 ? o : t1) - t0);
+    int64_t rpv[RPK];
+    if (rp_lds) {
+#pragma unroll
+        for (int k = 0; k < RPK; ++k) {  // r_lo + nr <= n_rows
+            const int i = (int)threadIdx.x + k * kBlock;
+            rpv[k] = i <= nr ? row_ptr[r_lo + i] : 0;
         }
-    stage_chunk<R, NT>(t0, t1, nnz, col, val, xs, s_prod, KeysNone{});
+    }
+    st.commit(t0, t1, nnz, col, val, xs, s_prod, KeysNone{});
+    if (rp_lds) {
+#pragma unroll
+        for (int k = 0; k < RPK; ++k) {
+            const int i = (int)threadIdx.x + k * kBlock;
+            if (i <= nr)
+                s_rp[i] = (int32_t)((rpv[k] < t1 ? rpv[k] : t1) - t0);
+        }
+    }
     __syncthreads();
     const int g = threadIdx.x / L, lane = threadIdx.x % L;
 
     // carry: entry t0 lies in row r_lo-1 when no row starts exactly at t0
+    // (row_ptr[r_lo] > t0; for r_lo = n_rows, row_ptr = nnz >= t1 > t0)
     if (g == 0) {
         double c = 0.0;
         int32_t cr = -1;
-        if (r_lo > 0 && (r_lo == n_rows || row_ptr[r_lo] > t0)) {
+        // e - t0 = min(row_ptr[r_lo], t1) - t0 (r_lo = n_rows: t1 - t0)
+        int64_t e_rel;
+        if (rp_lds) {
+            e_rel = s_rp[0];
+        } else {
+            const int64_t o = r_lo < n_rows ? row_ptr[r_lo] : nnz;
+            e_rel = (o < t1 ? o : t1) - t0;
+        }
+        if (r_lo > 0 && e_rel > 0) {
             cr = (int32_t)(r_lo - 1);
-            const int64_t e = r_lo < n_rows && row_ptr[r_lo] < t1 ? row_ptr[r_lo] : t1;
-            for (int64_t j = t0 + lane; j < e; j += L)
-                c += prod[j - t0];
+            for (int64_t j = lane; j < e_rel; j += L)
+                c += prod[j];
         }
         c = group_sum<L>(c);
         if (lane == 0) {
@@ -469,139 +502,6 @@ __global__ __launch_bounds__(kBlock) void csr_tiled_kernel(
             store_y(y + (r), s);
     }
 }
-
-// Persistent form of csr_tiled_kernel<L, 1> for the hot-column run, with the
-// K hottest table entries in LDS.  On the R-MAT every x gather is one L2
-// request whether it hits or not, and the tiled kernel is held by that
-// request rate; the hottest ~16 K columns take ~30 % of the gathers, and a
-// workgroup that stays resident for the whole run loads them into LDS once
-// and reads them with ds_read_b64.  One 1024-thread workgroup per CU (the
-// table fills the LDS); its four 256-thread quarters each run the tiles of
-// csr_tiled_kernel<L, 1> (same 512-entry tiles, same staging, row phase and
-// carry), so y is bit-identical to it.  Each quarter issues its next tile's
-// value/column pair before the current tile's row phase (one pair in flight
-// during the reduction, as the non-persistent grid had from its extra
-// resident workgroups).
-constexpr int kLdsQ = 4;          // 256-thread quarters per workgroup
-constexpr int kLdsRowCap = 512;   // row offsets staged per tile (more: read from global memory)
-
-template <bool NT, typename V>
-struct TilePair {  // one lane's value/column pair of a 512-entry tile (StageRegs<1> on a quarter)
-    double2 v;
-    int2 c;
-    __device__ __forceinline__ void issue(int64_t cb, int64_t ce, int64_t nz, int t, const int32_t *__restrict__ col,
-                                          const V *__restrict__ val)
-    {
-        if (nz < 2)
-            return;
-        const int64_t spare = cb + 1 < nz ? cb : (nz - 2) & ~(int64_t)1;
-        const int64_t p = cb + 2 * (int64_t)t;
-        const int64_t q = (p < ce && p + 1 < nz) ? p : spare;
-        v = vpair<NT>(val + q);
-        c = stream_load2<NT>(col + q);
-    }
-    template <typename XS>
-    __device__ __forceinline__ void commit(int64_t cb, int64_t ce, int64_t nz, int t, const int32_t *__restrict__ col,
-                                           const V *__restrict__ val, const XS &xs, double2 *s_prod) const
-    {
-        if (nz >= 2)
-            s_prod[t] = double2{v.x * xs(c.x), v.y * xs(c.y)};
-        const int64_t tail = nz - 1 - cb;
-        if ((nz & 1) && nz - 1 < ce && tail >= 0 && tail < 2 * kBlock && (tail >> 1) == t)
-            s_prod[t] = double2{vone<NT>(val + (nz - 1)) * xs(stream_load<NT>(col + (nz - 1))), 0.0};
-    }
-};
-
-template <int L, bool NT, typename V = double>
-__global__ __launch_bounds__(kBlock * kLdsQ) void csr_tiled_lds_kernel(
-    int64_t n_rows, int64_t nnz, int64_t tiles, const int64_t *__restrict__ row_ptr,
-    const int32_t *__restrict__ col, const V *__restrict__ val, const double *__restrict__ x,
-    const double *__restrict__ xh, int32_t M, int32_t K, double *__restrict__ y,
-    const int32_t *__restrict__ own_lo, int32_t *__restrict__ carry_row, double *__restrict__ carry_val)
-{
-    constexpr int CH = 2 * kBlock;  // csr_tiled_kernel<L, 1>'s tile
-    constexpr int GROUPS = kBlock / L;
-    extern __shared__ double s_hot[];
-    __shared__ double2 s_prod_all[kLdsQ][kBlock];
-    __shared__ int32_t s_rp_all[kLdsQ][kLdsRowCap + 1];
-    const int q = threadIdx.x / kBlock, t = threadIdx.x % kBlock;
-    double2 *s_prod = s_prod_all[q];
-    int32_t *s_rp = s_rp_all[q];
-    const double *prod = reinterpret_cast<const double *>(s_prod);
-    const int64_t stride = (int64_t)gridDim.x * kLdsQ;
-    int64_t tile = (int64_t)blockIdx.x * kLdsQ + q;
-    TilePair<NT, V> cur;
-    if (tile < tiles)
-        cur.issue(tile * CH, tile * CH + CH < nnz ? tile * CH + CH : nnz, nnz, t, col, val);
-    copy_window<kBlock * kLdsQ, 8>(s_hot, xh, 0, K);
-    __syncthreads();
-    const XHotLds xs{x, xh, s_hot, M, K};
-    const int64_t n_iter = (tiles - (int64_t)blockIdx.x * kLdsQ + stride - 1) / stride;  // uniform per workgroup
-    for (int64_t it = 0; it < n_iter; ++it, tile += stride) {
-        const bool live = tile < tiles;
-        const int64_t t0 = tile * CH;
-        const int64_t t1 = t0 + CH < nnz ? t0 + CH : nnz;
-        int64_t r_lo = 0, r_hi = -1;
-        if (live) {
-            r_lo = own_lo[tile];
-            r_hi = t1 == nnz ? n_rows - 1 : (int64_t)own_lo[tile + 1] - 1;
-        }
-        const int64_t nr = r_hi - r_lo + 1;
-        const bool rp_lds = nr >= 0 && nr <= kLdsRowCap;  // uniform per quarter
-        if (live && rp_lds)
-            for (int i = t; i <= nr; i += kBlock) {
-                const int64_t o = row_ptr[r_lo + i];
-                s_rp[i] = (int32_t)((o < t1 ? o : t1) - t0);
-            }
-        if (live)
-            cur.commit(t0, t1, nnz, t, col, val, xs, s_prod);
-        // the next tile's pair goes in flight before this tile's reduction
-        const int64_t nt = tile + stride;
-        if (nt < tiles)
-            cur.issue(nt * CH, nt * CH + CH < nnz ? nt * CH + CH : nnz, nnz, t, col, val);
-        __syncthreads();
-        if (live) {
-            const int g = t / L, lane = t % L;
-            if (g == 0) {  // carry: entry t0 lies in row r_lo-1 when no row starts exactly at t0
-                double c = 0.0;
-                int32_t cr = -1;
-                if (r_lo > 0 && (r_lo == n_rows || row_ptr[r_lo] > t0)) {
-                    cr = (int32_t)(r_lo - 1);
-                    const int64_t e = r_lo < n_rows && row_ptr[r_lo] < t1 ? row_ptr[r_lo] : t1;
-                    for (int64_t j = t0 + lane; j < e; j += L)
-                        c += prod[j - t0];
-                }
-                c = group_sum<L>(c);
-                if (lane == 0) {
-                    carry_row[tile] = cr;
-                    carry_val[tile] = c;
-                }
-            }
-            for (int64_t r = r_lo + g; r <= r_hi; r += GROUPS) {
-                int a, b;
-                if (rp_lds) {
-                    a = s_rp[r - r_lo];
-                    b = s_rp[r - r_lo + 1];
-                } else {
-                    const int64_t b64 = row_ptr[r + 1];
-                    a = (int)(row_ptr[r] - t0);
-                    b = (int)((b64 < t1 ? b64 : t1) - t0);
-                }
-                double s = 0.0;
-                for (int j = a + lane; j < b; j += L)
-                    s += prod[j];
-                s = group_sum<L>(s);
-                if (lane == 0)
-                    store_y(y + (r), s);
-            }
-        }
-        __syncthreads();
-    }
-}
-
-// The LDS-table run: K hottest columns (at most kLdsHotCap, what is left of
-// the CU's 160 KiB after the four quarters' staging).
-constexpr int32_t kLdsHotCap = 16384;
 
 // ------------------------------------------------------------ CMRS tiled
 // Entry-balanced CMRS for skewed strips (the R-MAT strip of rows 0-7 holds
@@ -845,46 +745,6 @@ int launch_csr_tiled(const spmv_dims &d, const int64_t *row_ptr, const int32_t *
     return SPMV_SUCCESS;
 }
 
-// The persistent LDS-table form (csr_tiled_lds_kernel) of a hot-column run
-// with 512-entry tiles; false when it does not apply (R = 3 tiles) or is
-// switched off (SPMV_TILED_LDS=0: A/B runs only, same bits either way).
-template <typename V>
-static bool launch_tiled_lds(const spmv_dims &d, int64_t tiles, const int64_t *row_ptr, const int32_t *col,
-                             const V *val, const double *x, const double *xh, int64_t H, double *y,
-                             const int32_t *own_lo, int32_t *carry_row, double *carry_val)
-{
-    const char *env = getenv("SPMV_TILED_LDS");
-    if (tiled_r(d.n_rows, d.nnz) != 1 || H <= 0 || (env && env[0] == '0'))
-        return false;
-    const int32_t K = (int32_t)(H < kLdsHotCap ? H : kLdsHotCap);
-    const size_t lds = (size_t)K * sizeof(double);
-    int dev = 0, cus = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-        cus = 256;
-    const int64_t want = (tiles + kLdsQ - 1) / kLdsQ;
-    const int64_t grid = want < cus ? want : cus;
-    const hipStream_t st = (hipStream_t)d.stream;
-    const double mean = d.n_rows > 0 ? (double)d.nnz / (double)d.n_rows : 0.0;
-#define SPMV_TILED_LDS(LL)                                                                                  \
-    do {                                                                                                    \
-        auto kern = csr_tiled_lds_kernel<LL, true, V>;                                                      \
-        (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
-        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kBlock * kLdsQ), lds, st, d.n_rows, d.nnz, tiles, \
-                           row_ptr, col, val, x, xh, (int32_t)d.n_cols, K, y, own_lo, carry_row, carry_val); \
-    } while (0)
-    if (mean >= 48.0)
-        SPMV_TILED_LDS(8);
-    else if (mean >= 12.0)
-        SPMV_TILED_LDS(4);
-    else if (mean >= 6.0)
-        SPMV_TILED_LDS(2);
-    else
-        SPMV_TILED_LDS(1);
-#undef SPMV_TILED_LDS
-    return true;
-}
-
 template <typename V>
 int launch_csr_tiled_hot(const spmv_dims &d, const int64_t *row_ptr, const int32_t *col,
                          const V *val, const double *x, double *y, int64_t H, const int32_t *hot,
@@ -901,11 +761,10 @@ int launch_csr_tiled_hot(const spmv_dims &d, const int64_t *row_ptr, const int32
         SPMV_CHECK_LAUNCH("csr_tile_rows_kernel");
         own_lo_plan = own_lo;
     }
-    if (H > 0) {
-        if (!launch_tiled_lds(d, tiles, row_ptr, col, val, x, xh, H, y, own_lo_plan, carry_row, carry_val))
-            launch_tiled_xs(d, tiles, row_ptr, col, val, XHot{x, xh, (int32_t)d.n_cols}, y, own_lo_plan, carry_row,
-                            carry_val);
-    } else
+    if (H > 0)
+        launch_tiled_xs(d, tiles, row_ptr, col, val, XHot{x, xh, (int32_t)d.n_cols}, y, own_lo_plan, carry_row,
+                        carry_val);
+    else
         launch_tiled_xs(d, tiles, row_ptr, col, val, XGlobal{x}, y, own_lo_plan, carry_row, carry_val);
     SPMV_CHECK_LAUNCH("csr_tiled_kernel (hot columns)");
     return launch_carry(tiles, carry_row, carry_val, y, st);

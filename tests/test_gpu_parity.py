@@ -606,35 +606,26 @@ def test_csr_hot_bit_identical(torch_dev, H):
     assert_parity(m, ya.cpu().numpy(), x.cpu().numpy())
 
 
-@pytest.mark.parametrize("case,H", [("rmat", 1 << 16), ("rmat", 100), ("rmat", 1 << 19), ("rmat_odd", 4096),
-                                    ("empty_runs", 1024)])
-def test_csr_tiled_lds_bit_identical(torch_dev, monkeypatch, case, H):
-    """The persistent tiled kernel with the hottest table entries in LDS
-    (csr_tiled_lds_kernel: 1024-thread workgroups, four tiles at a time, the
-    next tile's pair issued early) gives the bits of csr_tiled_kernel<L, 1>
-    (SPMV_TILED_LDS=0) on the same hot table: tables smaller and larger than
-    the LDS part, an odd entry count (the array's last entry loaded singly),
-    tiles owning more rows than the LDS offset table and a row over many
-    tiles."""
+@pytest.mark.parametrize("case", ["rmat_odd", "empty_runs", "one_row"])
+def test_csr_tiled_edge_tiles(torch_dev, case):
+    """The tiled kernel's carry and offset staging at the edges: an odd entry
+    count (the array's last entry loaded singly), tiles owning more rows than
+    the LDS offset table, a single row over every tile; the tiled kernel,
+    with and without the hot table, against the oracle."""
     torch, dev = torch_dev
-    if case == "rmat":
-        m = sa.gen_rmat(1_000_000, 10_000_000, scale=20, seed=1)
-    elif case == "rmat_odd":
+    if case == "rmat_odd":
         m = sa.gen_rmat(300_000, 2_999_999, scale=19, seed=4)
-    else:
+    elif case == "empty_runs":
         m, _ = _empty_run_matrix()
-    dm = sa.to_device(m, "csr", dev, variant=4, hot=H)
-    assert dm.params["H"] == H
-    x = torch.from_numpy(np.random.default_rng(13).uniform(-1, 1, m.n_cols)).to(dev)
-    ys = []
-    for knob in ("0", "1"):
-        monkeypatch.setenv("SPMV_TILED_LDS", knob)
-        y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
-        dm.run(x, y)
-        torch.cuda.synchronize()
-        ys.append(y)
-    assert torch.equal(ys[0].view(torch.int64), ys[1].view(torch.int64))
-    assert_parity(m, ys[1].cpu().numpy(), x.cpu().numpy())
+    else:
+        rng = np.random.default_rng(5)
+        m = sa.Coo(3, 5_000, np.full(20_001, 1, np.int32), rng.integers(0, 5_000, 20_001).astype(np.int32),
+                   rng.uniform(-1, 1, 20_001))
+    x = np.random.default_rng(13).uniform(-1, 1, m.n_cols)
+    for H in (0, 4096):
+        y, _, dm = run_fmt(torch, dev, m, "csr", x=x, variant=4, hot=H)
+        assert dm.params["variant"] == 4
+        assert_parity(m, y, x)
 
 
 def _empty_run_matrix(seed=11):
@@ -878,3 +869,24 @@ def test_sell_auto_ki_rule(torch_dev):
     assert lib.spmv_sell_auto_ki(32 * 62_451, 64) == 1
     assert lib.spmv_sell_auto_ki(62_451, 32) == 1  # C != 64: no small kernel
     assert sa.to_device(sa.gen_cantlike(0), "sell", torch_dev[1]).params["ki"] == 2
+
+
+@pytest.mark.parametrize("shape", ["12", "16", "8w", "12w", "16w"])
+@pytest.mark.parametrize("fmt,ki", [("sell", 2), ("sell", 1), ("sell16", 2)])
+def test_sell_small_shapes_same_bits(torch_dev, monkeypatch, shape, fmt, ki):
+    """The small-matrix SELL kernel's first-batch size and window-first order
+    (SPMV_SELL_SMALL, A/B runs) keep every accumulator's order: same bits as
+    the default shape, on one cant-like copy and on ragged rows."""
+    torch, dev = torch_dev
+    for m in (sa.gen_cantlike(0), sa.gen_random(30_000, 20_000, 0, 150, seed=23)):
+        dm = sa.to_device(m, fmt, dev, C=64, sigma=1024, ki=ki, xwin=True)
+        x = torch.from_numpy(np.random.default_rng(17).uniform(-1, 1, m.n_cols)).to(dev)
+        ys = []
+        for knob in ("", shape):
+            monkeypatch.setenv("SPMV_SELL_SMALL", knob)
+            y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
+            dm.run(x, y)
+            torch.cuda.synchronize()
+            ys.append(y)
+        assert torch.equal(ys[0].view(torch.int64), ys[1].view(torch.int64))
+        assert_parity(m, ys[1].cpu().numpy(), x.cpu().numpy())

@@ -15,7 +15,6 @@ from __future__ import annotations
 
 import argparse
 import json
-import os
 import sys
 import time
 from pathlib import Path
@@ -60,22 +59,13 @@ def main():
     x = torch.from_numpy(xh).to(dev)
     b = sa.bytes_alg(m.n_rows, m.n_cols, m.nnz)
     print(json.dumps({"setup_s": round(time.time() - t, 1)}), flush=True)
-    # baseline: the product path (tiled CSR + hot table, library rule), with
-    # and without the LDS table (SPMV_TILED_LDS, same bits), interleaved
+    # baseline: the product path (tiled CSR + hot table, library rule)
     dm = sa.to_device(m, "csr", dev)
     y = torch.empty(m.n_rows, dtype=torch.float64, device=dev)
-    outs = {}
-    for rnd in range(2):
-        for knob in ("0", "1"):
-            os.environ["SPMV_TILED_LDS"] = knob
-            for cold in (0, 1):
-                ms = time_run(torch, dm, x, y, a.reps, cold, sa)
-                print(json.dumps({"variant": "product", "lds": knob, "round": rnd, "params": dm.params, "cold": cold,
-                                  "ms": round(ms, 4), "GBs": round(b / ms * 1e-6, 1)}), flush=True)
-            outs[knob] = y.clone()
-    os.environ.pop("SPMV_TILED_LDS", None)
-    print(json.dumps({"lds_same_bits": bool(torch.equal(outs["0"].view(torch.int64), outs["1"].view(torch.int64)))}),
-          flush=True)
+    for cold in (0, 1):
+        ms = time_run(torch, dm, x, y, a.reps, cold, sa)
+        print(json.dumps({"variant": "product", "params": dm.params, "cold": cold, "ms": round(ms, 4),
+                          "GBs": round(b / ms * 1e-6, 1)}), flush=True)
     y_ref = y.cpu().numpy()
     del dm
     torch.cuda.empty_cache()

@@ -287,7 +287,17 @@ int spmv_sell16_fill(spmv_dims d, int32_t C, int32_t sigma, int64_t n_slices,
 int spmv_sell16_run(spmv_dims d, int32_t C, int32_t sigma, int32_t ki, int64_t n_slices,
                     const int64_t *slice_ptr, const int32_t *perm, const uint16_t *col16,
                     const double *val, const double *x, double *y, const void *win,
-                    int32_t xcap);
+                    int32_t xcap, const void *head);
+/* Head copy for small matrices (the ones spmv_sell_auto_ki gives ki = 2:
+ * fewer than 14 slices per CU): the first slot groups each wave of the
+ * small-matrix kernel reads are also stored at addresses computed from the
+ * workgroup and wave ids, so a cold run issues them without first waiting
+ * for slice_ptr.  spmv_sell16_head_bytes() is 0 for other matrices (no head;
+ * pass head = NULL).  Built once from the SELL16 arrays; y bit-identical.  */
+size_t spmv_sell16_head_bytes(int64_t n_slices, int32_t C, int32_t ki);
+int spmv_sell16_head_fill(spmv_dims d, int32_t C, int32_t sigma, int32_t ki, int64_t n_slices,
+                          const int64_t *slice_ptr, const double *val, const uint16_t *col16,
+                          void *head, size_t head_bytes);
 
 /* --------------------------------------------------------------- CMRS ---
  * Replaces kernel `cmrs(val,idx,strip_ptr,row_in_strip,x,y,N,h,__local)`

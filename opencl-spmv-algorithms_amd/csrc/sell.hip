@@ -16,7 +16,6 @@
 // loaded (that is the format's cost) but re-use the row's own column.
 #include <stdio.h>
 #include <stdlib.h>
-#include <string.h>
 
 #include "common.h"
 
@@ -451,47 +450,34 @@ __global__ __launch_bounds__(1024) void sell_xwin_kernel(
 // reads for a 49 MB matrix); four slices share it.
 template <int KI> constexpr int sell_small_g() { return 8; }  // first-batch slot groups per lane
 
-// WF (window first): the x-window loads are issued before the first batch
-// and written to LDS as soon as they land (they are the older loads), so the
-// barrier waits for the window only and the products start as the batch
-// arrives; with G = 16 nearly every cant-like lane has all its groups in
-// flight at once.  Same accumulators in the same order for any G that is a
-// multiple of 4: the bits do not change.
-template <int KI, bool NT, bool XWIN, typename XS, typename CT = int32_t, int G = sell_small_g<KI>(),
-          bool WF = false>
+// HEAD (SELL16 head copy, spmv_sell16_head_fill): the first G slot groups
+// of every wave are also stored in a head array at an address computed from
+// the workgroup and wave ids alone, so the first batch goes out without
+// waiting for slice_ptr (one dependent HBM round trip fewer on a cold
+// matrix); the later groups come from the SELL arrays.  Same values in the
+// same accumulators: bit-identical.
+template <int KI, bool NT, bool XWIN, typename XS, typename CT = int32_t, bool HEAD = false>
 __global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell_small_kernel(
     int64_t n_slices, const int64_t *__restrict__ slice_ptr,
     const int32_t *__restrict__ perm, const CT *__restrict__ col,
     const double *__restrict__ val, const XS xs, double *__restrict__ y, int64_t wcap,
-    const double *__restrict__ x, const int2 *__restrict__ win, int32_t xcap)
+    const double *__restrict__ x, const int2 *__restrict__ win, int32_t xcap,
+    const double *__restrict__ hval = nullptr, const CT *__restrict__ hcol = nullptr)
 {
-    constexpr int S = kSellSmallS, P = kSellSmallP, T = kWave * S * P;
-    static_assert(G % 4 == 0, "first batch: whole accumulator rounds");
+    constexpr int S = kSellSmallS, P = kSellSmallP, G = sell_small_g<KI>();
     constexpr bool c16 = std::is_same<CT, uint16_t>::value;  // SELL16: offsets from the window base
     static_assert(!c16 || XWIN, "SELL16 needs the workgroup windows");
     constexpr int64_t step = (int64_t)kWave * KI;  // elements between slot groups
     extern __shared__ double s_x[];
     const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+    SlotBatch<KI, NT, G> first;
+    if constexpr (HEAD) {  // this wave's head: G groups, whatever its slice
+        const int64_t hw = (int64_t)blockIdx.x * (S * P) + wv;
+        first.load(hval + hw * G * step + lane * KI, hcol + hw * G * step + lane * KI, 0, G, step);
+    }
     const int64_t s = (int64_t)blockIdx.x * P + wv / S;
     const int ws = wv % S;  // wave within its slice
     const bool live = s < n_slices;  // uniform per wave
-    bool staged = false;
-    int2 wnd = make_int2(0, -1);
-    constexpr int WU = 4;  // window entries per thread issued ahead (WF)
-    double wv_ahead[WU];
-    int32_t span = 0;
-    if constexpr (XWIN && WF) {
-        wnd = win[blockIdx.x];
-        span = wnd.y - wnd.x + 1;
-        staged = span > 0 && span <= xcap;  // uniform per workgroup
-        if (staged) {
-#pragma unroll
-            for (int k = 0; k < WU; ++k) {
-                const int32_t i = (int32_t)threadIdx.x + k * T;
-                wv_ahead[k] = x[wnd.x + (i < span ? i : span - 1)];
-            }
-        }
-    }
     const int64_t base = live ? slice_ptr[s] : 0;
     int64_t w = live ? (slice_ptr[s + 1] - base) / kWave : 0;
     w = w < wcap ? w : wcap;
@@ -502,27 +488,18 @@ __global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell_small_
     const bool any = g1 > g0;  // uniform per wave: no loads past the slice
     const double *vp = val + base + lane * KI;
     const CT *cp = col + base + lane * KI;
-    SlotBatch<KI, NT, G> first;
-    if (any)
-        first.load(vp, cp, g0, g1, step);
-    if constexpr (XWIN && WF) {
-        if (staged) {
-#pragma unroll
-            for (int k = 0; k < WU; ++k) {
-                const int32_t i = (int32_t)threadIdx.x + k * T;
-                if (i < span)
-                    s_x[i] = wv_ahead[k];
-            }
-            if (span > WU * T)  // wider windows: the rest after the batch
-                copy_window<T, 4>(s_x + WU * T, x, wnd.x + WU * T, span - WU * T);
-        }
-        __syncthreads();
-    } else if constexpr (XWIN) {
+    if constexpr (!HEAD) {
+        if (any)
+            first.load(vp, cp, g0, g1, step);
+    }
+    bool staged = false;
+    int2 wnd = make_int2(0, -1);
+    if constexpr (XWIN) {
         wnd = win[blockIdx.x];
-        span = wnd.y - wnd.x + 1;
+        const int32_t span = wnd.y - wnd.x + 1;
         staged = span > 0 && span <= xcap;  // uniform per workgroup
         if (staged)
-            copy_window<T, 4>(s_x, x, wnd.x, span);
+            copy_window<kWave * S * P, 4>(s_x, x, wnd.x, span);
         __syncthreads();
     }
     const int32_t row = live && ws == 0 ? perm[s * kWave + lane] : -1;
@@ -570,39 +547,58 @@ bool sell_small(int32_t C, int64_t n_slices)
     return n_slices < 14 * (int64_t)cus;
 }
 
-// SPMV_SELL_SMALL=<G>[w] picks the first-batch size G (8, 12 or 16) and the
-// window-first order for A/B runs (same bits); default 8, batch first.
-static int sell_small_shape()
-{
-    const char *e = getenv("SPMV_SELL_SMALL");
-    if (!e || !e[0])
-        return 8;
-    const int g = atoi(e);
-    const bool wf = strchr(e, 'w') != nullptr;
-    return (g == 12 || g == 16 ? g : 8) + (wf ? 100 : 0);
-}
-
 template <int KI, bool NT, bool XWIN, typename XS, typename CT = int32_t>
 static void launch_sell_small(int64_t n_slices, const int64_t *slice_ptr, const int32_t *perm, const CT *col,
                               const double *val, const XS xs, double *y, int64_t wcap, const double *x,
-                              const int2 *win, int32_t xcap, hipStream_t st)
+                              const int2 *win, int32_t xcap, hipStream_t st, const double *hval = nullptr,
+                              const CT *hcol = nullptr)
 {
     const size_t lds = XWIN ? (size_t)xcap * sizeof(double) : 0;
     const int64_t blocks = (n_slices + kSellSmallP - 1) / kSellSmallP;
-    const int shape = XWIN ? sell_small_shape() : 8;
-#define SPMV_SMALL_SHAPE(GG, WFF)                                                                            \
-    hipLaunchKernelGGL((sell_small_kernel<KI, NT, XWIN, XS, CT, GG, WFF>), dim3((unsigned)blocks),           \
-                       dim3(kWave * kSellSmallS * kSellSmallP), lds, st, n_slices, slice_ptr, perm, col, val, xs, \
-                       y, wcap, x, win, xcap)
-    switch (shape) {
-    case 12: SPMV_SMALL_SHAPE(12, false); break;
-    case 16: SPMV_SMALL_SHAPE(16, false); break;
-    case 108: SPMV_SMALL_SHAPE(8, true); break;
-    case 112: SPMV_SMALL_SHAPE(12, true); break;
-    case 116: SPMV_SMALL_SHAPE(16, true); break;
-    default: SPMV_SMALL_SHAPE(8, false); break;
-    }
-#undef SPMV_SMALL_SHAPE
+    if (hval)
+        hipLaunchKernelGGL((sell_small_kernel<KI, NT, XWIN, XS, CT, true>), dim3((unsigned)blocks),
+                           dim3(kWave * kSellSmallS * kSellSmallP), lds, st, n_slices, slice_ptr, perm, col, val, xs,
+                           y, wcap, x, win, xcap, hval, hcol);
+    else
+        hipLaunchKernelGGL((sell_small_kernel<KI, NT, XWIN, XS, CT, false>), dim3((unsigned)blocks),
+                           dim3(kWave * kSellSmallS * kSellSmallP), lds, st, n_slices, slice_ptr, perm, col, val, xs,
+                           y, wcap, x, win, xcap, nullptr, nullptr);
+}
+
+// SELL16 head copy: waves = 8 per small-kernel workgroup, G groups of
+// 64 lanes x ki slots each; padding (a wave with fewer groups) holds value
+// 0 and offset 0, and the kernel never adds it.
+static int64_t sell16_head_elems(int64_t n_slices, int32_t ki)
+{
+    const int64_t blocks = (n_slices + kSellSmallP - 1) / kSellSmallP;
+    return blocks * kSellSmallS * kSellSmallP * (int64_t)sell_small_g<1>() * kWave * ki;
+}
+
+template <int KI>
+__global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell16_head_kernel(
+    int64_t n_slices, const int64_t *__restrict__ slice_ptr, const double *__restrict__ val,
+    const uint16_t *__restrict__ col16, double *__restrict__ hval, uint16_t *__restrict__ hcol)
+{
+    constexpr int S = kSellSmallS, P = kSellSmallP, G = sell_small_g<KI>();
+    constexpr int64_t step = (int64_t)kWave * KI;
+    const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+    const int64_t s = (int64_t)blockIdx.x * P + wv / S;
+    const int ws = wv % S;
+    const bool live = s < n_slices;
+    const int64_t base = live ? slice_ptr[s] : 0;
+    const int64_t groups = live ? (slice_ptr[s + 1] - base) / kWave / KI : 0;  // as sell_small_kernel (wcap = max)
+    const int64_t per = (groups + S - 1) / S;
+    const int64_t g0 = ws * per;
+    const int64_t g1 = g0 + per < groups ? g0 + per : groups;
+    const int64_t hw = (int64_t)blockIdx.x * (S * P) + wv;
+    for (int u = 0; u < G; ++u)
+        for (int k = 0; k < KI; ++k) {
+            const int64_t dst = (hw * G + u) * step + lane * KI + k;
+            const bool in = g0 + u < g1;
+            const int64_t src = base + (g0 + u) * step + lane * KI + k;
+            hval[dst] = in ? val[src] : 0.0;
+            hcol[dst] = in ? col16[src] : (uint16_t)0;
+        }
 }
 
 // x-window variant when win != NULL (windows from spmv_sell_xwin_build:
@@ -911,9 +907,44 @@ extern "C" int spmv_sell16_fill(spmv_dims d, int32_t C, int32_t sigma, int64_t n
     return SPMV_SUCCESS;
 }
 
+extern "C" size_t spmv_sell16_head_bytes(int64_t n_slices, int32_t C, int32_t ki)
+{
+    if (n_slices <= 0 || (ki != 1 && ki != 2) || !sell_small(C, n_slices))
+        return 0;
+    return (size_t)sell16_head_elems(n_slices, ki) * (sizeof(double) + sizeof(uint16_t));
+}
+
+extern "C" int spmv_sell16_head_fill(spmv_dims d, int32_t C, int32_t sigma, int32_t ki, int64_t n_slices,
+                                     const int64_t *slice_ptr, const double *val, const uint16_t *col16, void *head,
+                                     size_t head_bytes)
+{
+    int rc = sell16_check(d, C, sigma, ki, n_slices, "spmv_sell16_head_fill");
+    if (rc != SPMV_SUCCESS)
+        return rc;
+    const size_t need = spmv_sell16_head_bytes(n_slices, C, ki);
+    if (need == 0)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_sell16_head_fill: no head (not a small-kernel matrix)");
+    if (!head || head_bytes < need || !slice_ptr || !val || !col16)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_sell16_head_fill: arrays or head buffer missing");
+    SPMV_GUARD(d);
+    double *hval = (double *)head;
+    uint16_t *hcol = (uint16_t *)(hval + sell16_head_elems(n_slices, ki));
+    const int64_t blocks = (n_slices + kSellSmallP - 1) / kSellSmallP;
+    const hipStream_t st = (hipStream_t)d.stream;
+    if (ki == 2)
+        hipLaunchKernelGGL(sell16_head_kernel<2>, dim3((unsigned)blocks), dim3(kWave * kSellSmallS * kSellSmallP), 0,
+                           st, n_slices, slice_ptr, val, col16, hval, hcol);
+    else
+        hipLaunchKernelGGL(sell16_head_kernel<1>, dim3((unsigned)blocks), dim3(kWave * kSellSmallS * kSellSmallP), 0,
+                           st, n_slices, slice_ptr, val, col16, hval, hcol);
+    SPMV_CHECK_LAUNCH("sell16_head_kernel");
+    return SPMV_SUCCESS;
+}
+
 extern "C" int spmv_sell16_run(spmv_dims d, int32_t C, int32_t sigma, int32_t ki, int64_t n_slices,
                                const int64_t *slice_ptr, const int32_t *perm, const uint16_t *col16,
-                               const double *val, const double *x, double *y, const void *win, int32_t xcap)
+                               const double *val, const double *x, double *y, const void *win, int32_t xcap,
+                               const void *head)
 {
     int rc = sell16_check(d, C, sigma, ki, n_slices, "spmv_sell16_run");
     if (rc != SPMV_SUCCESS)
@@ -932,8 +963,10 @@ extern "C" int spmv_sell16_run(spmv_dims d, int32_t C, int32_t sigma, int32_t ki
     const hipStream_t st = (hipStream_t)d.stream;
     const int2 *w = (const int2 *)win;
     if (sell_small(C, n_slices)) {
+        const double *hval = (const double *)head;
+        const uint16_t *hcol = head ? (const uint16_t *)(hval + sell16_head_elems(n_slices, ki)) : nullptr;
 #define SPMV_SMALL16(K, N) \
-    launch_sell_small<K, N, true, XGlobal, uint16_t>(n_slices, slice_ptr, perm, col16, val, XGlobal{x}, y, INT64_MAX, x, w, xcap, st)
+    launch_sell_small<K, N, true, XGlobal, uint16_t>(n_slices, slice_ptr, perm, col16, val, XGlobal{x}, y, INT64_MAX, x, w, xcap, st, hval, hcol)
         if (ki == 2) { if (nt) SPMV_SMALL16(2, true); else SPMV_SMALL16(2, false); }
         else { if (nt) SPMV_SMALL16(1, true); else SPMV_SMALL16(1, false); }
 #undef SPMV_SMALL16

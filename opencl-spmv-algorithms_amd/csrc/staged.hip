@@ -411,13 +411,33 @@ constexpr int kTiledRowCap = 1024;
 // eight; removed)
 //
 // Load order: a tile's dependent round trips are the latency the grid
-// waits out (R-MAT with every column = 0, i.e. no gather cost at all:
-// 0.58 ms of the 0.83).  The value/column pairs need the tile index only,
-// so they are issued first; own_lo (a scalar load) and then the row
-// offsets go out behind them into registers; the gathers follow once the
-// columns land; offsets and products reach LDS together before the one
-// barrier, and the carry reads row_ptr[r_lo] from the staged offsets.
-template <int L, int R, bool NT, typename XS, typename V = double>
+// waits out.  The value/column pairs need the tile index only, so they are
+// issued first; own_lo (a scalar load) and then the row offsets go out
+// behind them into registers; the gathers follow once the columns land;
+// offsets and products reach LDS together before the one barrier.
+//
+// Row phase: wave w takes the tile's rows in runs of 64 (runs w, w+4, ...);
+// a lane sums a row of at most kTiledShort entries alone, in entry order;
+// a longer row (R-MAT hub rows fill whole tiles) is summed by the whole
+// wave, lane j taking entries j, j+64, ..., then a butterfly.  With one L-lane
+// group per row, a tile inside a hub row was summed by L = 2 lanes, 256
+// dependent adds, while the other 254 lanes waited.  The carry (the
+// entries before the first row that starts in the tile) is wave 0's, the
+// same way.  Deterministic (fixed per-row order); the grouping differs from
+// an L-lane sum, so y agrees with the other CSR kernels to the parity rule.
+constexpr int kTiledShort = 16;
+
+// sum of p[a..b) by the whole wave (all lanes call it with the same a, b)
+__device__ __forceinline__ double wave_sum(const double *p, int a, int b)
+{
+    const int lane = threadIdx.x & (kWave - 1);
+    double s = 0.0;
+    for (int j = a + lane; j < b; j += kWave)
+        s += p[j];
+    return group_sum<kWave>(s);
+}
+
+template <int R, bool NT, typename XS, typename V = double>
 __global__ __launch_bounds__(kBlock) void csr_tiled_kernel(
     int64_t n_rows, int64_t nnz, const int64_t *__restrict__ row_ptr,
     const int32_t *__restrict__ col, const V *__restrict__ val,
@@ -426,8 +446,8 @@ __global__ __launch_bounds__(kBlock) void csr_tiled_kernel(
     double *__restrict__ carry_val)
 {
     constexpr int CH = 2 * kBlock * R;
-    constexpr int GROUPS = kBlock / L;
     constexpr int RPK = (kTiledRowCap + 1 + kBlock - 1) / kBlock;  // staged offsets per thread
+    constexpr int NW = kBlock / kWave;
     __shared__ double2 s_prod[kBlock * R];
     __shared__ int32_t s_rp[kTiledRowCap + 1];
     const double *prod = reinterpret_cast<const double *>(s_prod);
@@ -458,48 +478,54 @@ __global__ __launch_bounds__(kBlock) void csr_tiled_kernel(
         }
     }
     __syncthreads();
-    const int g = threadIdx.x / L, lane = threadIdx.x % L;
-
+    const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+    // [a, b) of owned row r (relative to t0)
+    auto range = [&](int64_t r, int &a, int &b) {
+        if (rp_lds) {
+            a = s_rp[r - r_lo];
+            b = s_rp[r - r_lo + 1];
+        } else {
+            const int64_t a64 = row_ptr[r], b64 = row_ptr[r + 1];
+            a = (int)(a64 - t0);
+            b = (int)((b64 < t1 ? b64 : t1) - t0);
+        }
+    };
     // carry: entry t0 lies in row r_lo-1 when no row starts exactly at t0
     // (row_ptr[r_lo] > t0; for r_lo = n_rows, row_ptr = nnz >= t1 > t0)
-    if (g == 0) {
-        double c = 0.0;
-        int32_t cr = -1;
-        // e - t0 = min(row_ptr[r_lo], t1) - t0 (r_lo = n_rows: t1 - t0)
-        int64_t e_rel;
+    if (wv == 0) {
+        int64_t e_rel;  // min(row_ptr[r_lo], t1) - t0
         if (rp_lds) {
             e_rel = s_rp[0];
         } else {
             const int64_t o = r_lo < n_rows ? row_ptr[r_lo] : nnz;
             e_rel = (o < t1 ? o : t1) - t0;
         }
-        if (r_lo > 0 && e_rel > 0) {
-            cr = (int32_t)(r_lo - 1);
-            for (int64_t j = lane; j < e_rel; j += L)
-                c += prod[j];
-        }
-        c = group_sum<L>(c);
+        const bool has = r_lo > 0 && e_rel > 0;
+        const double c = has ? wave_sum(prod, 0, (int)e_rel) : 0.0;
         if (lane == 0) {
-            carry_row[tile] = cr;
+            carry_row[tile] = has ? (int32_t)(r_lo - 1) : -1;
             carry_val[tile] = c;
         }
     }
-    for (int64_t r = r_lo + g; r <= r_hi; r += GROUPS) {
-        int a, b;
-        if (rp_lds) {
-            a = s_rp[r - r_lo];
-            b = s_rp[r - r_lo + 1];
-        } else {
-            const int64_t b64 = row_ptr[r + 1];
-            a = (int)(row_ptr[r] - t0);
-            b = (int)((b64 < t1 ? b64 : t1) - t0);
+    for (int64_t r0 = r_lo + (int64_t)wv * kWave; r0 <= r_hi; r0 += NW * kWave) {
+        const int64_t r = r0 + lane;
+        int a = 0, b = 0;
+        if (r <= r_hi)
+            range(r, a, b);
+        const bool lng = b - a > kTiledShort;
+        if (r <= r_hi && !lng) {
+            double sum = 0.0;
+            for (int j = a; j < b; ++j)
+                sum += prod[j];
+            store_y(y + r, sum);
         }
-        double s = 0.0;
-        for (int j = a + lane; j < b; j += L)
-            s += prod[j];
-        s = group_sum<L>(s);
-        if (lane == 0)
-            store_y(y + (r), s);
+        for (uint64_t m = __ballot(r <= r_hi && lng); m; m &= m - 1) {  // long rows: the whole wave
+            const int l = __builtin_ctzll(m);
+            const int la = __shfl(a, l), lb = __shfl(b, l);
+            const double sum = wave_sum(prod, la, lb);
+            if (lane == 0)
+                store_y(y + r0 + l, sum);
+        }
     }
 }
 
@@ -680,6 +706,9 @@ int launch_cmrs_tiled(const spmv_dims &d, int32_t h, int64_t n_strips, const int
 // Workspaces and plans are sized for the smallest tile.
 static int tiled_r(int64_t n_rows, int64_t nnz)
 {
+    const char *e = getenv("SPMV_TILED_R");  // A/B runs of the tile size (experiment only)
+    if (e && (e[0] == '1' || e[0] == '2' || e[0] == '3'))
+        return e[0] - '0';
     return n_rows > 0 && (double)nnz >= 96.0 * (double)n_rows ? 3 : 1;
 }
 
@@ -692,31 +721,13 @@ static void launch_tiled_r(const spmv_dims &d, int64_t tiles, const int64_t *row
                            double *carry_val)
 {
     const hipStream_t st = (hipStream_t)d.stream;
-    const double mean = d.n_rows > 0 ? (double)d.nnz / (double)d.n_rows : 0.0;
     // the plain-load variant exists for R = 3 only
-    const bool nt = R != 3 || stream_nt(true);
-#define SPMV_TILED(LL)                                                                                    \
-    do {                                                                                                  \
-        if constexpr (R == 3) {                                                                           \
-            if (!nt) {                                                                                    \
-                hipLaunchKernelGGL((csr_tiled_kernel<LL, R, false, XS, V>), dim3((unsigned)tiles),       \
-                                   dim3(kBlock), 0, st, d.n_rows, d.nnz, row_ptr, col, val, xs, y, own_lo, \
-                                   carry_row, carry_val);                                                 \
-                break;                                                                                    \
-            }                                                                                             \
-        }                                                                                                 \
-        hipLaunchKernelGGL((csr_tiled_kernel<LL, R, true, XS, V>), dim3((unsigned)tiles), dim3(kBlock), 0, \
-                           st, d.n_rows, d.nnz, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val);  \
-    } while (0)
-    if (mean >= 48.0)
-        SPMV_TILED(8);
-    else if (mean >= 12.0)
-        SPMV_TILED(4);
-    else if (mean >= 6.0)
-        SPMV_TILED(2);
-    else  // mostly empty rows (an R-MAT shard of high row ids): one lane per row
-        SPMV_TILED(1);
-#undef SPMV_TILED
+    if (R == 3 && !stream_nt(true))
+        hipLaunchKernelGGL((csr_tiled_kernel<R, false, XS, V>), dim3((unsigned)tiles), dim3(kBlock), 0, st, d.n_rows,
+                           d.nnz, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val);
+    else
+        hipLaunchKernelGGL((csr_tiled_kernel<R, true, XS, V>), dim3((unsigned)tiles), dim3(kBlock), 0, st, d.n_rows,
+                           d.nnz, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val);
 }
 
 template <typename XS, typename V>
@@ -724,10 +735,11 @@ static void launch_tiled_xs(const spmv_dims &d, int64_t tiles, const int64_t *ro
                             const V *val, XS xs, double *y, const int32_t *own_lo, int32_t *carry_row,
                             double *carry_val)
 {
-    if (tiled_r(d.n_rows, d.nnz) == 1)
-        launch_tiled_r<1>(d, tiles, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val);
-    else
-        launch_tiled_r<3>(d, tiles, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val);
+    switch (tiled_r(d.n_rows, d.nnz)) {
+    case 1: launch_tiled_r<1>(d, tiles, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val); break;
+    case 2: launch_tiled_r<2>(d, tiles, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val); break;
+    default: launch_tiled_r<3>(d, tiles, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val); break;
+    }
 }
 
 int launch_csr_tiled(const spmv_dims &d, const int64_t *row_ptr, const int32_t *col,

@@ -121,7 +121,10 @@ HIP_SYMBOLS = {
     "spmv_sell_run": (ctypes.c_int, [Dims, _c_i32, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "spmv_sell16_fill": (ctypes.c_int, [Dims, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, _vp]),
     "spmv_sell16_run": (ctypes.c_int, [Dims, _c_i32, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
-                                       _c_i32]),
+                                       _c_i32, _vp]),
+    "spmv_sell16_head_bytes": (ctypes.c_size_t, [_c_i64, _c_i32, _c_i32]),
+    "spmv_sell16_head_fill": (ctypes.c_int, [Dims, _c_i32, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, _vp,
+                                             ctypes.c_size_t]),
     "spmv_cmrs_run": (ctypes.c_int, [Dims, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "spmv_coo_xwin_bytes": (ctypes.c_size_t, [_c_i64]),
     "spmv_coo_xwin_build": (ctypes.c_int, [Dims, _vp, _vp, ctypes.c_size_t, ctypes.POINTER(_c_i32)]),
@@ -686,7 +689,7 @@ class DeviceMatrix:
         elif self.fmt == "sell16":
             rc = lib.spmv_sell16_run(d, p["C"], p["sigma"], p["ki"], p["n_slices"], _ptr(a["slice_ptr"]),
                                      _ptr(a["perm"]), _ptr(a["col16"]), _ptr(a["val"]), _ptr(x), _ptr(y),
-                                     _ptr(a["win"]), p["xcap"])
+                                     _ptr(a["win"]), p["xcap"], _ptr(a.get("head")))
         elif self.fmt == "sell" and p.get("H", 0) > 0:
             split = p.get("split_T", 0) > 0
             rc = lib.spmv_sell_run_hot(d, p["C"], p["sigma"], p["ki"], p["n_slices"], _ptr(a["slice_ptr"]),
@@ -860,7 +863,7 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
               sigma: int = 1024, h: int = 8, ell_max_padding: float | None = 64.0,
               xwin: bool | None = None, xwin_rows: int = 0, split: int | None = None,
               cmrs_variant: int | None = None, hot: int | None = None,
-              csr16_max_escape: float | None = 0.5, groups: int = 0) -> DeviceMatrix:
+              csr16_max_escape: float | None = 0.5, groups: int = 0, head: bool = True) -> DeviceMatrix:
     """Build `fmt` on the host (libspmv_host.so) and upload it.  xwin (CSR,
     ELL, SELL; default on): also build the per-workgroup x windows on the
     device and run the LDS x-window kernels (same bits as without).  split
@@ -1005,6 +1008,13 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
                                           _ptr(a["win"]), _ptr(a["col16"])), "spmv_sell16_fill")
         del a["col"]
         dm.stored_bytes = 10 * s["stored"] + 8 * (s["n_slices"] + 1) + 4 * s["n_slices"] * C
+        hb = hip_lib().spmv_sell16_head_bytes(s["n_slices"], C, ki) if head else 0
+        if hb > 0:  # small matrix: the head copy of every wave's first slot groups
+            a["head"] = torch.empty(hb, dtype=torch.uint8, device=device)
+            _check(hip_lib().spmv_sell16_head_fill(dm.dims(), C, sigma, ki, s["n_slices"], _ptr(a["slice_ptr"]),
+                                                   _ptr(a["val"]), _ptr(a["col16"]), _ptr(a["head"]), hb),
+                   "spmv_sell16_head_fill")
+            dm.params["head_bytes"] = hb
     elif fmt == "hyb":
         hb = hyb_build(m.n_rows, ptr, col, val, ki=ki or 2)
         dm.params = dict(K=hb["K"], ld=hb["ld"], ki=hb["ki"], tail_nnz=hb["tail_nnz"], stored=hb["stored"], H=0)

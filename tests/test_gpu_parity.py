@@ -871,22 +871,28 @@ def test_sell_auto_ki_rule(torch_dev):
     assert sa.to_device(sa.gen_cantlike(0), "sell", torch_dev[1]).params["ki"] == 2
 
 
-@pytest.mark.parametrize("shape", ["12", "16", "8w", "12w", "16w"])
-@pytest.mark.parametrize("fmt,ki", [("sell", 2), ("sell", 1), ("sell16", 2)])
-def test_sell_small_shapes_same_bits(torch_dev, monkeypatch, shape, fmt, ki):
-    """The small-matrix SELL kernel's first-batch size and window-first order
-    (SPMV_SELL_SMALL, A/B runs) keep every accumulator's order: same bits as
-    the default shape, on one cant-like copy and on ragged rows."""
+@pytest.mark.parametrize("ki", [1, 2])
+@pytest.mark.parametrize("case", ["cantlike", "ragged", "few_slices"])
+def test_sell16_head_same_bits(torch_dev, ki, case):
+    """SELL16's head copy (small matrices: every wave's first slot groups at
+    computed addresses, spmv_sell16_head_fill) gives the bits of the run
+    without it; waves with fewer groups than the head holds read padding
+    they never add."""
     torch, dev = torch_dev
-    for m in (sa.gen_cantlike(0), sa.gen_random(30_000, 20_000, 0, 150, seed=23)):
-        dm = sa.to_device(m, fmt, dev, C=64, sigma=1024, ki=ki, xwin=True)
-        x = torch.from_numpy(np.random.default_rng(17).uniform(-1, 1, m.n_cols)).to(dev)
-        ys = []
-        for knob in ("", shape):
-            monkeypatch.setenv("SPMV_SELL_SMALL", knob)
-            y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
-            dm.run(x, y)
-            torch.cuda.synchronize()
-            ys.append(y)
-        assert torch.equal(ys[0].view(torch.int64), ys[1].view(torch.int64))
-        assert_parity(m, ys[1].cpu().numpy(), x.cpu().numpy())
+    if case == "cantlike":
+        m = sa.gen_cantlike(2)
+    elif case == "ragged":
+        m = sa.gen_random(30_000, 20_000, 0, 150, seed=23)
+    else:  # 3 slices, rows of 0-5 entries: most waves have no groups or one
+        m = sa.gen_random(150, 400, 0, 5, seed=24)
+    x = torch.from_numpy(np.random.default_rng(19).uniform(-1, 1, m.n_cols)).to(dev)
+    ys = []
+    for head in (False, True):
+        dm = sa.to_device(m, "sell16", dev, C=64, sigma=1024, ki=ki, head=head)
+        assert ("head" in dm.arrays) == head
+        y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
+        dm.run(x, y)
+        torch.cuda.synchronize()
+        ys.append(y)
+    assert torch.equal(ys[0].view(torch.int64), ys[1].view(torch.int64))
+    assert_parity(m, ys[1].cpu().numpy(), x.cpu().numpy())

@@ -456,7 +456,7 @@ template <int KI> constexpr int sell_small_g() { return 8; }  // first-batch slo
 // waiting for slice_ptr (one dependent HBM round trip fewer on a cold
 // matrix); the later groups come from the SELL arrays.  Same values in the
 // same accumulators: bit-identical.
-template <int KI, bool NT, bool XWIN, typename XS, typename CT = int32_t, bool HEAD = false>
+template <int KI, bool NT, bool XWIN, typename XS, typename CT = int32_t, int HG = 0>
 __global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell_small_kernel(
     int64_t n_slices, const int64_t *__restrict__ slice_ptr,
     const int32_t *__restrict__ perm, const CT *__restrict__ col,
@@ -464,7 +464,8 @@ __global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell_small_
     const double *__restrict__ x, const int2 *__restrict__ win, int32_t xcap,
     const double *__restrict__ hval = nullptr, const CT *__restrict__ hcol = nullptr)
 {
-    constexpr int S = kSellSmallS, P = kSellSmallP, G = sell_small_g<KI>();
+    constexpr bool HEAD = HG > 0;  // HG: the head's slot groups per wave (the first batch)
+    constexpr int S = kSellSmallS, P = kSellSmallP, G = HEAD ? HG : sell_small_g<KI>();
     constexpr bool c16 = std::is_same<CT, uint16_t>::value;  // SELL16: offsets from the window base
     static_assert(!c16 || XWIN, "SELL16 needs the workgroup windows");
     constexpr int64_t step = (int64_t)kWave * KI;  // elements between slot groups
@@ -492,6 +493,16 @@ __global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell_small_
         if (any)
             first.load(vp, cp, g0, g1, step);
     }
+    // HEAD: the head went out without slice_ptr; the groups after it (TB of
+    // them) go out as soon as slice_ptr lands, before the window barrier,
+    // instead of one batch of 4 per round trip after the head's products
+    constexpr int TB = HEAD ? 12 : 0;
+    SlotBatch<KI, NT, (TB > 0 ? TB : 1)> tail;
+    const bool has_tail = TB > 0 && g0 + G < g1;  // uniform per wave
+    if constexpr (TB > 0) {
+        if (has_tail)
+            tail.load(vp, cp, g0 + G, g1, step);
+    }
     bool staged = false;
     int2 wnd = make_int2(0, -1);
     if constexpr (XWIN) {
@@ -507,7 +518,11 @@ __global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell_small_
     auto body = [&](const auto &src) {
         if (any)
             first.fma4(src, g0, g1, a);
-        for (int64_t g = g0 + G; g < g1; g += 4) {
+        if constexpr (TB > 0) {  // group g0+G+u -> a[u % 4]: G is a multiple of 4, the order of every a[] is kept
+            if (has_tail)
+                tail.fma4(src, g0 + G, g1, a);
+        }
+        for (int64_t g = g0 + G + TB; g < g1; g += 4) {
             SlotBatch<KI, NT, 4> b;
             b.load(vp, cp, g, g1, step);
             b.fma4(src, g, g1, a);
@@ -547,6 +562,16 @@ bool sell_small(int32_t C, int64_t n_slices)
     return n_slices < 14 * (int64_t)cus;
 }
 
+// slot groups per wave in the SELL16 head (its kernel's first batch);
+// SPMV_SELL16_HEAD_G=12|16 for A/B runs (read by the build and the run
+// alike; same bits)
+static int sell16_head_g()
+{
+    const char *e = getenv("SPMV_SELL16_HEAD_G");
+    const int g = e ? atoi(e) : 8;
+    return g == 12 || g == 16 ? g : 8;
+}
+
 template <int KI, bool NT, bool XWIN, typename XS, typename CT = int32_t>
 static void launch_sell_small(int64_t n_slices, const int64_t *slice_ptr, const int32_t *perm, const CT *col,
                               const double *val, const XS xs, double *y, int64_t wcap, const double *x,
@@ -555,14 +580,24 @@ static void launch_sell_small(int64_t n_slices, const int64_t *slice_ptr, const 
 {
     const size_t lds = XWIN ? (size_t)xcap * sizeof(double) : 0;
     const int64_t blocks = (n_slices + kSellSmallP - 1) / kSellSmallP;
-    if (hval)
-        hipLaunchKernelGGL((sell_small_kernel<KI, NT, XWIN, XS, CT, true>), dim3((unsigned)blocks),
-                           dim3(kWave * kSellSmallS * kSellSmallP), lds, st, n_slices, slice_ptr, perm, col, val, xs,
-                           y, wcap, x, win, xcap, hval, hcol);
-    else
-        hipLaunchKernelGGL((sell_small_kernel<KI, NT, XWIN, XS, CT, false>), dim3((unsigned)blocks),
-                           dim3(kWave * kSellSmallS * kSellSmallP), lds, st, n_slices, slice_ptr, perm, col, val, xs,
-                           y, wcap, x, win, xcap, nullptr, nullptr);
+#define SPMV_SMALL_HG(HH)                                                                                     \
+    hipLaunchKernelGGL((sell_small_kernel<KI, NT, XWIN, XS, CT, HH>), dim3((unsigned)blocks),                 \
+                       dim3(kWave * kSellSmallS * kSellSmallP), lds, st, n_slices, slice_ptr, perm, col, val, xs, \
+                       y, wcap, x, win, xcap, hval, hcol)
+    if constexpr (XWIN && std::is_same<CT, uint16_t>::value) {  // the head exists for SELL16 only
+        const int hg = hval ? sell16_head_g() : 0;
+        if (hg == 16)
+            SPMV_SMALL_HG(16);
+        else if (hg == 12)
+            SPMV_SMALL_HG(12);
+        else if (hg == 8)
+            SPMV_SMALL_HG(8);
+        else
+            SPMV_SMALL_HG(0);
+    } else {
+        SPMV_SMALL_HG(0);
+    }
+#undef SPMV_SMALL_HG
 }
 
 // SELL16 head copy: waves = 8 per small-kernel workgroup, G groups of
@@ -571,15 +606,15 @@ static void launch_sell_small(int64_t n_slices, const int64_t *slice_ptr, const 
 static int64_t sell16_head_elems(int64_t n_slices, int32_t ki)
 {
     const int64_t blocks = (n_slices + kSellSmallP - 1) / kSellSmallP;
-    return blocks * kSellSmallS * kSellSmallP * (int64_t)sell_small_g<1>() * kWave * ki;
+    return blocks * kSellSmallS * kSellSmallP * (int64_t)sell16_head_g() * kWave * ki;
 }
 
-template <int KI>
+template <int KI, int G>
 __global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell16_head_kernel(
     int64_t n_slices, const int64_t *__restrict__ slice_ptr, const double *__restrict__ val,
     const uint16_t *__restrict__ col16, double *__restrict__ hval, uint16_t *__restrict__ hcol)
 {
-    constexpr int S = kSellSmallS, P = kSellSmallP, G = sell_small_g<KI>();
+    constexpr int S = kSellSmallS, P = kSellSmallP;
     constexpr int64_t step = (int64_t)kWave * KI;
     const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
     const int64_t s = (int64_t)blockIdx.x * P + wv / S;
@@ -931,12 +966,16 @@ extern "C" int spmv_sell16_head_fill(spmv_dims d, int32_t C, int32_t sigma, int3
     uint16_t *hcol = (uint16_t *)(hval + sell16_head_elems(n_slices, ki));
     const int64_t blocks = (n_slices + kSellSmallP - 1) / kSellSmallP;
     const hipStream_t st = (hipStream_t)d.stream;
-    if (ki == 2)
-        hipLaunchKernelGGL(sell16_head_kernel<2>, dim3((unsigned)blocks), dim3(kWave * kSellSmallS * kSellSmallP), 0,
-                           st, n_slices, slice_ptr, val, col16, hval, hcol);
-    else
-        hipLaunchKernelGGL(sell16_head_kernel<1>, dim3((unsigned)blocks), dim3(kWave * kSellSmallS * kSellSmallP), 0,
-                           st, n_slices, slice_ptr, val, col16, hval, hcol);
+#define SPMV_HEAD_FILL(K, HH)                                                                                    \
+    hipLaunchKernelGGL((sell16_head_kernel<K, HH>), dim3((unsigned)blocks), dim3(kWave * kSellSmallS * kSellSmallP), 0, \
+                       st, n_slices, slice_ptr, val, col16, hval, hcol)
+    const int hg = sell16_head_g();
+    if (ki == 2) {
+        if (hg == 16) SPMV_HEAD_FILL(2, 16); else if (hg == 12) SPMV_HEAD_FILL(2, 12); else SPMV_HEAD_FILL(2, 8);
+    } else {
+        if (hg == 16) SPMV_HEAD_FILL(1, 16); else if (hg == 12) SPMV_HEAD_FILL(1, 12); else SPMV_HEAD_FILL(1, 8);
+    }
+#undef SPMV_HEAD_FILL
     SPMV_CHECK_LAUNCH("sell16_head_kernel");
     return SPMV_SUCCESS;
 }

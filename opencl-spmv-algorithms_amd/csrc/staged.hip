@@ -695,21 +695,21 @@ int launch_cmrs_tiled(const spmv_dims &d, int32_t h, int64_t n_strips, const int
     return launch_carry((int64_t)h * tiles, carry_row, carry_val, y, st);
 }
 
-// Tile = 2·kBlock·R entries.  R = 1 (512-entry tiles) unless the mean row
-// is long (>= 96 entries): on the R-MAT 1e7/1e8 the whole matrix ran
-// 0.826 / 0.831 / 0.861 / 0.887 ms with R = 1 / 2 / 3 / 4, the 8 row shards
-// of mean 4-34 fastest with R = 1 (0.118-0.150 ms against 0.147-0.173 with
-// R = 3): shorter tiles finish the grid with a shorter tail
-// (profiles/round2/ab_tiled_r.log).  Hub shards, whose rows run over many
-// tiles (more carries), split: mean 179 (1 of 8) 0.1366 ms with R = 3 vs
-// 0.1475 with R = 1, mean 55 (1 of 4) 0.2855 vs 0.2667 (ab_tiled_r_hub.log).
-// Workspaces and plans are sized for the smallest tile.
+// Tile = 2·kBlock·R entries.  R = 2 (1,024-entry tiles) unless the mean row
+// is long (>= 96 entries, R = 3).  Round 2 picked R = 1 for R-MAT-like rows
+// (0.826 / 0.831 / 0.861 ms with R = 1 / 2 / 3, profiles/round2/ab_tiled_r.log)
+// while hub rows were summed by L = 2 lanes per tile; with the wave-per-long-
+// row phase the whole R-MAT runs 0.800 / 0.785 / 0.788 ms and the tile
+// structure alone (every column 0) 0.386 / 0.327 / 0.345 ms
+// (profiles/round3/rmat_tiled_r.log).  Hub shards, whose rows run over many
+// tiles, ran best with R = 3 in round 2 (ab_tiled_r_hub.log).  Workspaces
+// and plans are sized for the smallest tile (R = 1).
 static int tiled_r(int64_t n_rows, int64_t nnz)
 {
     const char *e = getenv("SPMV_TILED_R");  // A/B runs of the tile size (experiment only)
     if (e && (e[0] == '1' || e[0] == '2' || e[0] == '3'))
         return e[0] - '0';
-    return n_rows > 0 && (double)nnz >= 96.0 * (double)n_rows ? 3 : 1;
+    return n_rows > 0 && (double)nnz >= 96.0 * (double)n_rows ? 3 : 2;
 }
 
 int64_t csr_tiled_tile(int64_t n_rows, int64_t nnz) { return 2 * kBlock * tiled_r(n_rows, nnz); }

@@ -493,10 +493,11 @@ __global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell_small_
         if (any)
             first.load(vp, cp, g0, g1, step);
     }
-    // HEAD: the head went out without slice_ptr; the groups after it (TB of
-    // them) go out as soon as slice_ptr lands, before the window barrier,
-    // instead of one batch of 4 per round trip after the head's products
-    constexpr int TB = HEAD ? 12 : 0;
+    // TB > 0: the TB groups after the head go out as soon as slice_ptr lands,
+    // before the window barrier, instead of in batches of 4 after the head's
+    // products: measured slower for SELL16 on one cant-like copy (10.94-11.0
+    // vs 10.36 us cold, 214 VGPRs), so TB = 0
+    constexpr int TB = 0;
     SlotBatch<KI, NT, (TB > 0 ? TB : 1)> tail;
     const bool has_tail = TB > 0 && g0 + G < g1;  // uniform per wave
     if constexpr (TB > 0) {

@@ -28,8 +28,8 @@ REPO_DIR = PKG_DIR.parent
 
 FORMATS = ("coo", "csr", "ell", "sell", "cmrs")  # the reference's five
 # §8f row 4: CSR with 16-bit column offsets; ELL + COO tail; CSR with fp32 values;
-# SELL-C-σ with 16-bit column offsets
-EXTRA_FORMATS = ("csr16", "hyb", "csrf32", "sell16")
+# SELL-C-σ with 16-bit column offsets; column-grouped CSR (gather-bound rows)
+EXTRA_FORMATS = ("csr16", "hyb", "csrf32", "sell16", "csrg")
 ALL_FORMATS = FORMATS + EXTRA_FORMATS
 HBM_PEAK_GBS = 8000.0
 CSRG_ROWS = 4096  # SPMV_CSRG_ROWS (include/spmv.h): rows per block of the CSRG reduce  # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -978,7 +978,9 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
         _sell_hot(dm, s["col"][: s["stored"]], hot)
     elif fmt == "csrg":
         # column-grouped CSR for gather-bound power-law matrices (R-MAT)
-        g = csrg_build(m.n_rows, ptr, col, val, groups=groups or 32)
+        # G = 4 measured best on the R-MAT (0.757-0.785 ms vs 0.768-0.83 at G = 8,
+        # profiles/round3/rmat_tiled_r.log): more groups add pairs
+        g = csrg_build(m.n_rows, ptr, col, val, groups=groups or 4)
         dm.params = dict(groups=g["groups"], n_pairs=g["n_pairs"])
         dm.arrays = {k: _dev_tensor(g[k], device) for k in ("pair_ptr", "col_g", "val_g", "blk_off")}
         dm.arrays["pair_row"] = _dev_tensor(g["pair_row"].view(np.int16), device)

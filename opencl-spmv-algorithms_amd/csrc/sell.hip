@@ -450,6 +450,9 @@ __global__ __launch_bounds__(1024) void sell_xwin_kernel(
 // reads for a 49 MB matrix); four slices share it.
 template <int KI> constexpr int sell_small_g() { return 8; }  // first-batch slot groups per lane
 
+// (Also issuing the 12 groups after the head as soon as slice_ptr lands,
+// before the window barrier, measured slower: 10.94-11.0 vs 10.36 us cold
+// for SELL16 on one cant-like copy, 214 VGPRs.)
 // HEAD (SELL16 head copy, spmv_sell16_head_fill): the first G slot groups
 // of every wave are also stored in a head array at an address computed from
 // the workgroup and wave ids alone, so the first batch goes out without
@@ -493,17 +496,6 @@ __global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell_small_
         if (any)
             first.load(vp, cp, g0, g1, step);
     }
-    // TB > 0: the TB groups after the head go out as soon as slice_ptr lands,
-    // before the window barrier, instead of in batches of 4 after the head's
-    // products: measured slower for SELL16 on one cant-like copy (10.94-11.0
-    // vs 10.36 us cold, 214 VGPRs), so TB = 0
-    constexpr int TB = 0;
-    SlotBatch<KI, NT, (TB > 0 ? TB : 1)> tail;
-    const bool has_tail = TB > 0 && g0 + G < g1;  // uniform per wave
-    if constexpr (TB > 0) {
-        if (has_tail)
-            tail.load(vp, cp, g0 + G, g1, step);
-    }
     bool staged = false;
     int2 wnd = make_int2(0, -1);
     if constexpr (XWIN) {
@@ -519,11 +511,7 @@ __global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell_small_
     auto body = [&](const auto &src) {
         if (any)
             first.fma4(src, g0, g1, a);
-        if constexpr (TB > 0) {  // group g0+G+u -> a[u % 4]: G is a multiple of 4, the order of every a[] is kept
-            if (has_tail)
-                tail.fma4(src, g0 + G, g1, a);
-        }
-        for (int64_t g = g0 + G + TB; g < g1; g += 4) {
+        for (int64_t g = g0 + G; g < g1; g += 4) {
             SlotBatch<KI, NT, 4> b;
             b.load(vp, cp, g, g1, step);
             b.fma4(src, g, g1, a);
@@ -563,15 +551,11 @@ bool sell_small(int32_t C, int64_t n_slices)
     return n_slices < 14 * (int64_t)cus;
 }
 
-// slot groups per wave in the SELL16 head (its kernel's first batch);
-// SPMV_SELL16_HEAD_G=12|16 for A/B runs (read by the build and the run
-// alike; same bits)
-static int sell16_head_g()
-{
-    const char *e = getenv("SPMV_SELL16_HEAD_G");
-    const int g = e ? atoi(e) : 8;
-    return g == 12 || g == 16 ? g : 8;
-}
+// slot groups per wave in the SELL16 head (its kernel's first batch): 8 and
+// 12 ran the same (10.36 us cold, cant-like single), 16 slower (11.24 us:
+// waves of 9-15 groups read padding); profiles/round3/cant_single_sell16_head_*.json
+constexpr int kSell16HeadG = 8;
+static int sell16_head_g() { return kSell16HeadG; }
 
 template <int KI, bool NT, bool XWIN, typename XS, typename CT = int32_t>
 static void launch_sell_small(int64_t n_slices, const int64_t *slice_ptr, const int32_t *perm, const CT *col,
@@ -586,13 +570,8 @@ static void launch_sell_small(int64_t n_slices, const int64_t *slice_ptr, const 
                        dim3(kWave * kSellSmallS * kSellSmallP), lds, st, n_slices, slice_ptr, perm, col, val, xs, \
                        y, wcap, x, win, xcap, hval, hcol)
     if constexpr (XWIN && std::is_same<CT, uint16_t>::value) {  // the head exists for SELL16 only
-        const int hg = hval ? sell16_head_g() : 0;
-        if (hg == 16)
-            SPMV_SMALL_HG(16);
-        else if (hg == 12)
-            SPMV_SMALL_HG(12);
-        else if (hg == 8)
-            SPMV_SMALL_HG(8);
+        if (hval)
+            SPMV_SMALL_HG(kSell16HeadG);
         else
             SPMV_SMALL_HG(0);
     } else {
@@ -970,12 +949,10 @@ extern "C" int spmv_sell16_head_fill(spmv_dims d, int32_t C, int32_t sigma, int3
 #define SPMV_HEAD_FILL(K, HH)                                                                                    \
     hipLaunchKernelGGL((sell16_head_kernel<K, HH>), dim3((unsigned)blocks), dim3(kWave * kSellSmallS * kSellSmallP), 0, \
                        st, n_slices, slice_ptr, val, col16, hval, hcol)
-    const int hg = sell16_head_g();
-    if (ki == 2) {
-        if (hg == 16) SPMV_HEAD_FILL(2, 16); else if (hg == 12) SPMV_HEAD_FILL(2, 12); else SPMV_HEAD_FILL(2, 8);
-    } else {
-        if (hg == 16) SPMV_HEAD_FILL(1, 16); else if (hg == 12) SPMV_HEAD_FILL(1, 12); else SPMV_HEAD_FILL(1, 8);
-    }
+    if (ki == 2)
+        SPMV_HEAD_FILL(2, kSell16HeadG);
+    else
+        SPMV_HEAD_FILL(1, kSell16HeadG);
 #undef SPMV_HEAD_FILL
     SPMV_CHECK_LAUNCH("sell16_head_kernel");
     return SPMV_SUCCESS;

@@ -706,9 +706,6 @@ int launch_cmrs_tiled(const spmv_dims &d, int32_t h, int64_t n_strips, const int
 // and plans are sized for the smallest tile (R = 1).
 static int tiled_r(int64_t n_rows, int64_t nnz)
 {
-    const char *e = getenv("SPMV_TILED_R");  // A/B runs of the tile size (experiment only)
-    if (e && (e[0] == '1' || e[0] == '2' || e[0] == '3'))
-        return e[0] - '0';
     return n_rows > 0 && (double)nnz >= 96.0 * (double)n_rows ? 3 : 2;
 }
 
@@ -735,11 +732,10 @@ static void launch_tiled_xs(const spmv_dims &d, int64_t tiles, const int64_t *ro
                             const V *val, XS xs, double *y, const int32_t *own_lo, int32_t *carry_row,
                             double *carry_val)
 {
-    switch (tiled_r(d.n_rows, d.nnz)) {
-    case 1: launch_tiled_r<1>(d, tiles, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val); break;
-    case 2: launch_tiled_r<2>(d, tiles, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val); break;
-    default: launch_tiled_r<3>(d, tiles, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val); break;
-    }
+    if (tiled_r(d.n_rows, d.nnz) == 2)
+        launch_tiled_r<2>(d, tiles, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val);
+    else
+        launch_tiled_r<3>(d, tiles, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val);
 }
 
 int launch_csr_tiled(const spmv_dims &d, const int64_t *row_ptr, const int32_t *col,

@@ -871,10 +871,9 @@ def test_sell_auto_ki_rule(torch_dev):
     assert sa.to_device(sa.gen_cantlike(0), "sell", torch_dev[1]).params["ki"] == 2
 
 
-@pytest.mark.parametrize("hg", ["8", "12", "16"])
 @pytest.mark.parametrize("ki", [1, 2])
 @pytest.mark.parametrize("case", ["cantlike", "ragged", "few_slices"])
-def test_sell16_head_same_bits(torch_dev, monkeypatch, hg, ki, case):
+def test_sell16_head_same_bits(torch_dev, ki, case):
     """SELL16's head copy (small matrices: every wave's first slot groups at
     computed addresses, spmv_sell16_head_fill) gives the bits of the run
     without it; waves with fewer groups than the head holds read padding
@@ -887,7 +886,6 @@ def test_sell16_head_same_bits(torch_dev, monkeypatch, hg, ki, case):
     else:  # 3 slices, rows of 0-5 entries: most waves have no groups or one
         m = sa.gen_random(150, 400, 0, 5, seed=24)
     x = torch.from_numpy(np.random.default_rng(19).uniform(-1, 1, m.n_cols)).to(dev)
-    monkeypatch.setenv("SPMV_SELL16_HEAD_G", hg)  # head size (A/B knob read by build and run)
     ys = []
     for head in (False, True):
         dm = sa.to_device(m, "sell16", dev, C=64, sigma=1024, ki=ki, head=head)

@@ -450,9 +450,10 @@ __global__ __launch_bounds__(1024) void sell_xwin_kernel(
 // reads for a 49 MB matrix); four slices share it.
 template <int KI> constexpr int sell_small_g() { return 8; }  // first-batch slot groups per lane
 
-// (Also issuing the 12 groups after the head as soon as slice_ptr lands,
-// before the window barrier, measured slower: 10.94-11.0 vs 10.36 us cold
-// for SELL16 on one cant-like copy, 214 VGPRs.)
+// (Also issuing the 12 groups after the head early measured slower for
+// SELL16 on one cant-like copy: before the window's loads 10.94-11.0 vs
+// 10.36 us cold; after them, before the window barrier, 10.84-10.98 vs
+// 10.20-10.24 us in one A/B (profiles/round3/ab_sell16_tail.log).)
 // HEAD (SELL16 head copy, spmv_sell16_head_fill): the first G slot groups
 // of every wave are also stored in a head array at an address computed from
 // the workgroup and wave ids alone, so the first batch goes out without

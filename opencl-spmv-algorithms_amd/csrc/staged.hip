@@ -695,8 +695,11 @@ int launch_cmrs_tiled(const spmv_dims &d, int32_t h, int64_t n_strips, const int
     return launch_carry((int64_t)h * tiles, carry_row, carry_val, y, st);
 }
 
-// Tile = 2·kBlock·R entries.  R = 2 (1,024-entry tiles) unless the mean row
-// is long (>= 96 entries, R = 3).  Round 2 picked R = 1 for R-MAT-like rows
+// Tile = 2·kBlock·R entries.  R = 2 (1,024-entry tiles) for mean rows of
+// 6-95 entries, R = 3 from 96, R = 1 below 6 (mostly empty rows: an R-MAT
+// shard of high row ids, 2.8 M rows / 9.4 M entries, ran 0.1255 -> 0.1371 ms
+// warm and 0.1436 -> 0.1724 ms cold with R = 2 tiles, as a 1,024-entry tile
+// then owns more rows than its LDS offset table; shard_rehearse_cold_b.log).  Round 2 picked R = 1 for R-MAT-like rows
 // (0.826 / 0.831 / 0.861 ms with R = 1 / 2 / 3, profiles/round2/ab_tiled_r.log)
 // while hub rows were summed by L = 2 lanes per tile; with the wave-per-long-
 // row phase the whole R-MAT runs 0.800 / 0.785 / 0.788 ms and the tile
@@ -706,7 +709,9 @@ int launch_cmrs_tiled(const spmv_dims &d, int32_t h, int64_t n_strips, const int
 // and plans are sized for the smallest tile (R = 1).
 static int tiled_r(int64_t n_rows, int64_t nnz)
 {
-    return n_rows > 0 && (double)nnz >= 96.0 * (double)n_rows ? 3 : 2;
+    if (n_rows > 0 && (double)nnz >= 96.0 * (double)n_rows)
+        return 3;
+    return n_rows > 0 && (double)nnz >= 6.0 * (double)n_rows ? 2 : 1;
 }
 
 int64_t csr_tiled_tile(int64_t n_rows, int64_t nnz) { return 2 * kBlock * tiled_r(n_rows, nnz); }
@@ -732,10 +737,11 @@ static void launch_tiled_xs(const spmv_dims &d, int64_t tiles, const int64_t *ro
                             const V *val, XS xs, double *y, const int32_t *own_lo, int32_t *carry_row,
                             double *carry_val)
 {
-    if (tiled_r(d.n_rows, d.nnz) == 2)
-        launch_tiled_r<2>(d, tiles, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val);
-    else
-        launch_tiled_r<3>(d, tiles, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val);
+    switch (tiled_r(d.n_rows, d.nnz)) {
+    case 1: launch_tiled_r<1>(d, tiles, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val); break;
+    case 2: launch_tiled_r<2>(d, tiles, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val); break;
+    default: launch_tiled_r<3>(d, tiles, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val); break;
+    }
 }
 
 int launch_csr_tiled(const spmv_dims &d, const int64_t *row_ptr, const int32_t *col,

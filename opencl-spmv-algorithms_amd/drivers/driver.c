@@ -62,7 +62,7 @@ typedef struct {
     const char *gen;
     const char *write_mtx;
     int64_t copies;
-    int reps, warmup, warm, device, C, sigma, ki, h, lanes, threads, cpu, strict, cache, xwin, gpus;
+    int reps, warmup, warm, device, C, sigma, ki, h, lanes, threads, cpu, strict, cache, xwin, gpus, index16;
 } opts_t;
 
 static void usage(const char *prog)
@@ -71,7 +71,7 @@ static void usage(const char *prog)
            "          [--copies B] [--reps N] [--warmup W] [--warm] [--device D]\n"
            "          [--C C] [--sigma S] [--ki 1|2] [--h H] [--lanes L]\n"
            "          [--threads T] [--cpu|--no-cpu] [--strict] [--write-mtx PATH] [--cache]\n"
-           "          [--no-xwin] [--gpus N]\n",
+           "          [--no-xwin] [--gpus N] [--index16 (sigma_c: SELL16)]\n",
            prog);
 }
 
@@ -119,6 +119,7 @@ static int parse_opts(int argc, char **argv, spmv_format fmt, opts_t *o)
         else if (!strcmp(a, "--strict")) o->strict = 1;
         else if (!strcmp(a, "--cache")) o->cache = 1;
         else if (!strcmp(a, "--no-xwin")) o->xwin = 0;
+        else if (!strcmp(a, "--index16")) o->index16 = 1;
         else if (!strcmp(a, "--help") || !strcmp(a, "-h")) { usage(argv[0]); exit(0); }
         else {
             fprintf(stderr, "unknown option %s\n", a);
@@ -130,6 +131,10 @@ static int parse_opts(int argc, char **argv, spmv_format fmt, opts_t *o)
     if (o->reps < 1 || o->warmup < 0 || o->copies < 1 || (o->ki < 0 || o->ki > 2) ||
         o->h < 1 || o->h > 64 || o->C < 1 || o->C > 1024 || o->gpus < 0 || o->gpus > 64)
         return SPMV_OTHER_ERROR;
+    if (o->index16 && (fmt != FMT_SELL || !o->xwin || o->gpus > 0)) {
+        fprintf(stderr, "--index16 is SELL16: sigma_c, one GPU, with x windows\n");
+        return SPMV_OTHER_ERROR;
+    }
     return SPMV_SUCCESS;
 }
 
@@ -265,6 +270,9 @@ typedef struct {
     size_t ws_bytes;
     void *d_win; /* x-window kernels: per-workgroup column ranges */
     int32_t xcap;
+    /* SELL16 (--index16): 16-bit column offsets, head copy for small matrices */
+    uint16_t *d_col16;
+    void *d_head;
     int32_t K, C, sigma, ki, h, lanes, variant;
     int64_t ld, n_slices, n_strips;
     /* SELL wide-slice split plan (power-law rows; spmv_sell_run_split) */
@@ -513,6 +521,31 @@ static int build_windows(dev_fmt_t *f)
     return rc;
 }
 
+/* SELL16 (--index16): the SELL columns rewritten as 16-bit offsets from each
+ * workgroup's window base on the device; matrices of the small-matrix
+ * kernel also get the head copy.  Refused (exit 4) when a window spans more
+ * than 65,536 columns or the split plan is in use (power-law rows). */
+static int build_sell16(dev_fmt_t *f)
+{
+    if (!f->d_win || f->split_T > 0)
+        return SPMV_OTHER_ERROR;
+    int rc = spmv_malloc((void **)&f->d_col16, (size_t)(f->stored > 0 ? f->stored : 1) * sizeof(uint16_t));
+    if (rc == SPMV_SUCCESS)
+        rc = spmv_sell16_fill(f->d, f->C, f->sigma, f->n_slices, f->d_ptr, f->d_col, f->d_win, f->d_col16);
+    const size_t hb = spmv_sell16_head_bytes(f->n_slices, f->C, f->ki);
+    if (rc == SPMV_SUCCESS && hb > 0) {
+        rc = spmv_malloc(&f->d_head, hb);
+        if (rc == SPMV_SUCCESS)
+            rc = spmv_sell16_head_fill(f->d, f->C, f->sigma, f->ki, f->n_slices, f->d_ptr, f->d_val, f->d_col16,
+                                       f->d_head, hb);
+    }
+    if (rc == SPMV_SUCCESS)
+        printf("SELL16: 16-bit column offsets, %.1f MB stored%s\n",
+               (10.0 * (double)f->stored + 8.0 * (double)(f->n_slices + 1) + 4.0 * (double)f->n_slices * f->C) * 1e-6,
+               hb > 0 ? " + head copy" : "");
+    return rc;
+}
+
 static int launch(void *arg)
 {
     dev_fmt_t *f = (dev_fmt_t *)arg;
@@ -520,6 +553,9 @@ static int launch(void *arg)
         return spmv_sell_run_split(f->d, f->C, f->sigma, f->ki, f->n_slices, f->d_ptr, f->d_perm, f->d_col,
                                    f->d_val, f->d_x, f->d_y, f->d_win, f->xcap, f->split_T, f->n_chunks,
                                    f->d_chunk_slice, f->d_chunk_k0, f->d_ws, f->ws_bytes);
+    if (f->d_col16)
+        return spmv_sell16_run(f->d, f->C, f->sigma, f->ki, f->n_slices, f->d_ptr, f->d_perm, f->d_col16, f->d_val,
+                               f->d_x, f->d_y, f->d_win, f->xcap, f->d_head);
     if (f->d_win) {
         if (f->fmt == FMT_CSR)
             return spmv_csr_run_xwin(f->d, f->d_ptr, f->d_col, f->d_val, f->d_x, f->d_y, f->lanes, 0,
@@ -845,6 +881,8 @@ int spmv_driver_main(int argc, char **argv, spmv_format fmt)
     rc = build_format(&o, fmt, &m, &f);
     if (rc == SPMV_SUCCESS && o.xwin)
         rc = build_windows(&f);
+    if (rc == SPMV_SUCCESS && o.index16)
+        rc = build_sell16(&f);
     if (rc != SPMV_SUCCESS) {
         printf("format build/upload failed: %s %s\n", spmv_strerror(rc), spmv_last_error());
         return rc == SPMV_OTHER_ERROR ? SPMV_OTHER_ERROR : SPMV_PROGRAM_ERROR;

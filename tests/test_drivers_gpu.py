@@ -127,3 +127,19 @@ def test_program_gpus_flag_more_gpus_than_present():
     """Asking for more GPUs than the node has is the reference's device error (1)."""
     r = run("csr", "--gen", "cantlike", "--gpus", "64", "--reps", "1")
     assert r.returncode == 1, r.stdout + r.stderr
+
+
+def test_sigma_c_index16():
+    """./bin/sigma_c --index16: SELL16 (16-bit column offsets, head copy on a
+    small matrix) through the C-ABI, checked like every run; refused for the
+    other programs (the C-ABI refusal of wide windows:
+    test_gpu_parity.test_sell16_refuses_wide_windows)."""
+    r = run("sigma_c", "--gen", "cantlike", "--reps", "5", "--warmup", "1", "--strict", "--index16")
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "SELL16: 16-bit column offsets" in r.stdout and "head copy" in r.stdout
+    assert "\nresult is ok\n" in "\n" + r.stdout
+    r = run("sigma_c", "--matrix", str(GOLDEN / "ragged_shuffled.mtx"), "--reps", "3", "--strict", "--index16")
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "\nresult is ok\n" in "\n" + r.stdout
+    r = run("csr", "--gen", "cantlike", "--index16")
+    assert r.returncode == 4

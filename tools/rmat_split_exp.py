@@ -67,6 +67,8 @@ def main():
         print(json.dumps({"variant": "product", "params": dm.params, "cold": cold, "ms": round(ms, 4),
                           "GBs": round(b / ms * 1e-6, 1)}), flush=True)
     y_ref = y.cpu().numpy()
+    import hashlib
+    print(json.dumps({"product_y_sha1": hashlib.sha1(y_ref.tobytes()).hexdigest()}), flush=True)
     del dm
     torch.cuda.empty_cache()
     # gather-cost probes: same rows, same tiles, columns replaced

@@ -450,6 +450,9 @@ __global__ __launch_bounds__(1024) void sell_xwin_kernel(
 // reads for a 49 MB matrix); four slices share it.
 template <int KI> constexpr int sell_small_g() { return 8; }  // first-batch slot groups per lane
 
+// (SELL16 gathering x from global memory instead of the LDS window (xcap 0)
+// measured slower on one cant-like copy: 11.6-11.9 vs 10.3-10.6 us cold,
+// profiles/round3/ab_sell16_xwindow_vs_global.json.)
 // (Also issuing the 12 groups after the head early measured slower for
 // SELL16 on one cant-like copy: before the window's loads 10.94-11.0 vs
 // 10.36 us cold; after them, before the window barrier, 10.84-10.98 vs

@@ -60,7 +60,8 @@ def main():
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--formats", default=",".join(sa.ALL_FORMATS))
     ap.add_argument("--extra", action="append", default=[], metavar='FMT@JSON',
-                    help='another run of FMT with to_device kwargs, e.g. csr@{"xwin_rows": 64}')
+                    help='another run of FMT with to_device kwargs, e.g. csr@{"xwin_rows": 64}; '
+                         '"_params" overrides run parameters after the build, e.g. sell16@{"_params": {"xcap": 0}}')
     ap.add_argument("--attach", default=None, metavar="TRACE_DIR",
                     help="no GPU run: add the kernel-trace figures of a finished rocprofv3 run in TRACE_DIR "
                          "to the --json file it wrote")
@@ -99,7 +100,10 @@ def main():
         formats.append((f"{f}@{kw}", f, json.loads(kw)))
     for i, (label, fmt, kw) in enumerate(formats):
         tag(SETUP_TAG + i)  # builds, fills and the first run land in an ignored phase
+        kw = dict(kw)
+        over = kw.pop("_params", {})  # run-parameter overrides after the build, e.g. {"xcap": 0}
         dm = sa.to_device(m, fmt, dev, **kw)
+        dm.params.update(over)
         y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
         dm.run(x, y)
         torch.cuda.synchronize()

@@ -6,32 +6,41 @@ format on cant.mtx.  The real cant.mtx is a Git-LFS pointer in the
 reference, so the matrix is the cant-like stand-in
 (spmv_gen_cantlike: N = 62,451, Z = 4,007,383, the real cant's counts).
 
-Headline step = ONE SpMV launch over a batch of B = 32 independent
-cant-like matrices stacked block-diagonally (the configs[1] matrix,
-CSR-vector, batched): 1.58 GB of CSR, 6x the 256 MiB Infinity Cache, so
-the matrix streams from HBM; all arrays resident in HBM before timing
-starts.  ONE cant-like matrix is 49 MB and sits in the Infinity Cache after
-one pass, so its figures are reported beside the headline, not as it
-(`cant_single`): every format on the single matrix, cold (512 MiB flush
-first) and warm, timed from a rocprofv3 kernel trace (tools/cant_single.py,
-run as a child process before this process touches the GPU), next to the
-pure-stream ceiling of the same 49 MB.  At N=1 every format is also
-measured on the batch (`per_format`).
+Headline (default `--workload cant`, BASELINE.json configs[1]): CSR-vector
+on ONE cant-like matrix per GPU, COLD.  A step is a 512 MiB flush (evicts
+the 256 MiB Infinity Cache and the L2s) followed by ONE SpMV launch, so the
+49.3 MB matrix is read from HBM every step.  W untimed warm-up steps, then
+exactly K steps captured in one HIP graph and replayed between a barrier +
+synchronize on both sides.  The SpMV's own share of a step is its kernel
+duration: at N=1 from a rocprofv3 kernel trace of tools/cant_single.py (a
+child process started before this process touches the GPU; every format,
+cold and warm, beside the stream-probe ceiling of the same bytes), at N>1
+from one such child per rank (headline format only, on that rank's GPU);
+without a trace, from the in-process timed region: (span of K x (flush +
+SpMV) - span of K x flush) / K.  value = N x bytes_alg / (max over ranks
+of that cold SpMV time) = the whole job's throughput of replicated
+configs[1] steps (weak scaling: one matrix per GPU, no collective);
+ms_per_step = that SpMV time; the timed region's wall clock (flushes
+included) is `timed_region`.
 
-Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): rank r
-owns copies [r·B, (r+1)·B) of an N·B-copy matrix (weak scaling, no
-collective in the timed step).  `rmat_strong` (configs[3]) and
-`banded_strong` (configs[4]) cut ONE matrix into N row shards (strong
-scaling, x replicated) and report SpMV-only, the y all-gather of the real
-shard sizes over RCCL (an allgatherv), SpMV + all-gather, and cold shards
-(512 MiB flush before each step).
+At N=1 also `batch`: ONE launch over 32 cant-like matrices stacked
+block-diagonally (1.58 GB, 6x the Infinity Cache, streamed from HBM; the
+round 1-3 headline) with its own roofline and every format on it
+(`per_format`).  `rmat_strong` (configs[3]) and `banded_strong`
+(configs[4]) cut ONE matrix into N row shards (strong scaling, x
+replicated) and report SpMV-only, the y all-gather of the real shard sizes
+over RCCL (an allgatherv), SpMV + all-gather, and cold shards.
 
-value = algorithmic bytes of all ranks / (max over ranks of the wall time
-of K steps / K).  bytes_alg = 12·Z + 4·(N+1) + 8·M + 8·N per matrix
-(SURVEY.md §8d): values, columns, row offsets, x and y once each.
-roofline.achieved uses the same bytes over the kernel's mean duration from
-HIP events recorded on the launch stream; roofline.traffic comes from the
-rocprofv3 PMC passes committed in profiles/ (tools/pmc_traffic.py).
+`python3 bench.py --gpus N` without a launcher starts itself as N ranks
+under torch.distributed.run in a CHILD process (launch.spawn_ranks) and
+exits with its code; under torch.distributed.run (WORLD_SIZE set) it is a
+rank.
+
+bytes_alg = 12·Z + 4·(N+1) + 8·M + 8·N per matrix:
+values, columns, row offsets, x and y once each.  roofline.achieved uses
+the same bytes over the dominant kernel's cold duration; roofline.traffic
+comes from the rocprofv3 PMC passes committed in profiles/
+(tools/pmc_traffic.py).
 """
 from __future__ import annotations
 
@@ -53,6 +62,7 @@ sys.path.insert(0, str(REPO))
 sys.path.insert(0, str(REPO / "tools"))
 
 import iterate  # noqa: E402
+import launch  # noqa: E402
 import spmv_amd as sa  # noqa: E402
 
 METRIC = "effective HBM GB/s + GFLOP/s per format on cant.mtx, 1/2/4/8 MI355X"
@@ -75,14 +85,18 @@ def parse():
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--format", default="csr", choices=sa.ALL_FORMATS)
     p.add_argument("--copies", type=int, default=32, help="cant-like copies per GPU (batch)")
-    p.add_argument("--workload", default="cantlike", choices=["cantlike", "rmat", "banded"],
-                   help="cantlike (default, configs[1]/[2]); rmat (configs[3]); banded (configs[4])")
+    p.add_argument("--workload", default="cant", choices=["cant", "batch", "cantlike", "rmat", "banded"],
+                   help="cant (default: ONE cant-like matrix per GPU, cold, configs[1]/[2]); batch (= cantlike: "
+                        "the 32-copy block-diagonal batch); rmat (configs[3]); banded (configs[4])")
+    p.add_argument("--batch", default="auto", choices=["auto", "yes", "no"],
+                   help="with --workload cant, also time the 32-copy batch and every format on it (auto: N=1)")
     p.add_argument("--banded-rows", type=int, default=100_000_000)
     p.add_argument("--per-format", default="auto", choices=["auto", "yes", "no"],
                    help="also measure the other formats (default: at N=1 only)")
     p.add_argument("--single", default="auto", choices=["auto", "yes", "no"],
-                   help="cant_single: ONE cant-like matrix, every format, cold and warm, from a rocprofv3 "
-                        "kernel trace of a child process (default: at N=1 with the cant-like workload)")
+                   help="cant_single: ONE cant-like matrix, cold and warm, from a rocprofv3 kernel trace of a "
+                        "child process (auto, with --workload cant: every format at N=1, the headline format "
+                        "on every rank at N>1)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0: skip)")
     p.add_argument("--lanes", type=int, default=0)
     p.add_argument("--variant", type=int, default=0, help="CSR kernel variant (0 auto, 1 direct, 2 staged)")
@@ -97,10 +111,10 @@ def parse():
     p.add_argument("--share-gpu", action="store_true", help="all ranks on cuda:0 (rehearsal only)")
     p.add_argument("--rmat-strong", default="auto", choices=["auto", "yes", "no"],
                    help="also time CSR on the R-MAT 1e7/1e8 row-sharded over all ranks (strong scaling, "
-                        "north-star sweep; auto: with the default cant-like workload)")
+                        "north-star sweep; auto: with the default workload)")
     p.add_argument("--banded-strong", default="auto", choices=["auto", "yes", "no"],
                    help="also time CSR and SELL on the banded 1e8-row / 1.6e9-entry matrix row-sharded over all "
-                        "ranks (configs[4], generated on device; auto: with the default cant-like workload)")
+                        "ranks (configs[4], generated on device; auto: with the default workload)")
     p.add_argument("--flush", default="yes", choices=["yes", "no"],
                    help="strong-scaling legs: also time every shard cold (512 MiB flush before each step)")
     p.add_argument("--graph", default="yes", choices=["yes", "no"],
@@ -113,6 +127,8 @@ def kernel_name(args, dm=None):
     params = (getattr(dm, "params", {}) or {}) if dm is not None else {}
     if args.format == "cmrs" and params.get("variant") == 1:
         return "cmrs_tiled_kernel"
+    if dm is not None and args.format == "csr" and "plan" in getattr(dm, "arrays", {}):
+        return "csr_small_kernel"
     if dm is not None and "win" in getattr(dm, "arrays", {}):
         if args.format in ("csr16", "csrf32"):  # the CSR x-window kernel with another column / value source
             return "csr_xwin_kernel"
@@ -256,10 +272,11 @@ def cold_step_ms(torch, dm, x, y, steps):
     return (spans["both"] - spans["flush"]) / steps
 
 
-def traffic_for(fmt, workload_bytes, kernel=None):
+def traffic_for(fmt, workload_bytes, kernel=None, cold=False):
     """HBM bytes per launch from the committed PMC passes, if they were
-    measured on this workload and this kernel."""
-    for name in ("traffic.json", "traffic_rmat.json"):
+    measured on this workload and this kernel (cold: the single-matrix
+    passes with a flush before every launch, profiles/traffic_single.json)."""
+    for name in (("traffic_single.json",) if cold else ("traffic.json", "traffic_rmat.json")):
         f = REPO / "profiles" / name
         if not f.exists():
             continue
@@ -350,7 +367,7 @@ def build_workload(args, torch, dev, rank, world):
         matrix, equal row ranges, each shard generated on its GPU.
     """
     fk = fmt_kwargs(args, args.format)
-    if args.workload == "cantlike":
+    if args.workload == "batch":
         B = args.copies
         m = sa.gen_cantlike(0, B)
         x = torch.from_numpy(sa.ramp_x(m.n_cols) + rank * m.n_cols).to(dev)  # this shard's x block
@@ -449,26 +466,47 @@ def cpu_baseline(m_single_csr, copies, budget_s):
             "gflops": round(2 * B * int(ptr[-1]) / t * 1e-9, 2)}
 
 
-def cant_single_rocprof():
+def child_device_env(local: int) -> dict:
+    """Environment of a per-rank child that must see only this rank's GPU
+    (as its cuda:0): HIP_VISIBLE_DEVICES = the rank's entry of any visible
+    list the launcher already set, else the local rank."""
+    env = dict(os.environ)
+    for var in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        if env.get(var):
+            ids = [t for t in env[var].split(",") if t.strip()]
+            if local < len(ids):
+                env["HIP_VISIBLE_DEVICES"] = ids[local].strip()
+                env.pop("CUDA_VISIBLE_DEVICES", None)
+                return env
+    env["HIP_VISIBLE_DEVICES"] = str(local)
+    env.pop("CUDA_VISIBLE_DEVICES", None)
+    return env
+
+
+def cant_single_rocprof(formats=None, local=None):
     """tools/cant_single.py under `rocprofv3 --kernel-trace` as a child
-    process, run before this process touches the GPU: every format on ONE
-    cant-like matrix, cold and warm, kernel durations from the trace, beside
-    the stream ceiling of the same bytes.  Without rocprofv3 (or if the
-    profiled run fails) the child runs unprofiled and its HIP-event figures
-    are reported, labelled so."""
+    process, run before this process touches the GPU: formats (default
+    every format) on ONE cant-like matrix, cold and warm, kernel durations
+    from the trace, beside the stream ceiling of the same bytes.  `local`
+    (a rank's local GPU): the child sees only that GPU.  Without rocprofv3
+    (or if the profiled run fails) the child runs unprofiled and its
+    HIP-event figures are reported, labelled so."""
     tool = REPO / "tools" / "cant_single.py"
     rocprof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    env = child_device_env(local) if local is not None else None
     with tempfile.TemporaryDirectory(prefix="cant_single_") as tmp:
         out = Path(tmp) / "cant_single.json"
         plain = [sys.executable, str(tool), "--json", str(out)]
+        if formats:
+            plain += ["--formats", ",".join(formats)]
         traced = Path(rocprof).exists()
         cmd = ([rocprof, "--kernel-trace", "--output-format", "csv", "-d", tmp, "-o", "run", "--"] + plain
                if traced else plain)
         try:
-            r = subprocess.run(cmd, capture_output=True, text=True, timeout=420, cwd=str(REPO))
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=420, cwd=str(REPO), env=env)
             if traced and (r.returncode != 0 or not out.exists()):
                 traced = False
-                r = subprocess.run(plain, capture_output=True, text=True, timeout=300, cwd=str(REPO))
+                r = subprocess.run(plain, capture_output=True, text=True, timeout=300, cwd=str(REPO), env=env)
         except subprocess.TimeoutExpired:
             return {"error": "cant_single timed out"}
         if r.returncode != 0 or not out.exists():
@@ -482,6 +520,98 @@ def cant_single_rocprof():
             res["timing"] = "HIP events around each launch (no rocprofv3 trace): includes event overhead"
     res.pop("phases", None)
     return res
+
+
+def single_cold(args, torch, dev, rank, world, dist, cdev, prof):
+    """The headline (BASELINE.json configs[1]; configs[2] with --format
+    sell): ONE cant-like matrix on this rank's GPU, cold.  A step = 512 MiB
+    flush + one SpMV launch.  W untimed warm-up steps; then the K steps are
+    captured in one HIP graph, replayed once untimed, and replayed once
+    between barrier + synchronize on both sides (the timed region); then a
+    graph of K flushes alone is timed the same way, so the in-process cold
+    SpMV time is (span(K x (flush + SpMV)) - span(K x flush)) / K.  The
+    headline's SpMV time is the rocprofv3 trace median of the same kernel
+    cold (`prof`, this rank's cant_single child) when every rank has one,
+    else the in-process figure on every rank; max over ranks."""
+    m = sa.gen_cantlike(0, 1)
+    b = sa.bytes_alg(m.n_rows, m.n_cols, m.nnz)
+    fk = fmt_kwargs(args, args.format)
+    xh = sa.ramp_x(m.n_cols)
+    x = torch.from_numpy(xh).to(dev)
+    y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
+    dm = sa.to_device(m, args.format, dev, **fk)
+    stream = torch.cuda.current_stream()
+    sa.flush_cache(stream)  # allocates the scratch outside any capture
+    torch.cuda.synchronize()
+
+    def step():
+        sa.flush_cache()
+        dm.run(x, y)
+
+    def spans(fn, k):
+        """(wall s, GPU span ms) of k calls of fn between barriers."""
+        g = capture(torch, fn, k) if GRAPH["on"] else None
+        if g is not None:
+            g.replay()
+            torch.cuda.synchronize()
+        a, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        a.record(stream)
+        if g is not None:
+            g.replay()
+        else:
+            for _ in range(k):
+                fn()
+        e.record(stream)
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0, a.elapsed_time(e)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    K = args.steps
+    wall, span_both = spans(step, K)
+    _, span_flush = spans(lambda: sa.flush_cache(), K)
+    inproc = max((span_both - span_flush) / K, 1e-6)
+    bad, first = sa.check(m, xh, y.cpu().numpy())
+    all_ok(dist, cdev, torch, bad == 0, f"cant-like single matrix, row {first}", rank)
+
+    rec = (prof or {}).get("formats", {}).get(args.format, {}) if isinstance(prof, dict) else {}
+    traced = rec.get("cold_ms")
+    have = torch.tensor([1.0 if traced else 0.0], dtype=torch.float64, device=cdev)
+    if dist is not None:
+        dist.all_reduce(have, op=dist.ReduceOp.MIN)
+    use_trace = bool(have.item())
+    t = torch.tensor([traced if use_trace else inproc, inproc, wall * 1e3 / K], dtype=torch.float64, device=cdev)
+    per_rank = [float(t[0].item())]
+    if dist is not None:
+        g = [torch.zeros(3, dtype=torch.float64, device=cdev) for _ in range(world)]
+        dist.all_gather(g, t)
+        per_rank = [float(v[0].item()) for v in g]
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    cold_ms, inproc_max, wall_step = (float(v) for v in t.tolist())
+    kernels = rec.get("kernels") or [kernel_name(args, dm)]
+    params = {k: v for k, v in dm.params.items() if isinstance(v, (int, float, str))}
+    del dm
+    torch.cuda.empty_cache()
+    return {"cold_ms": cold_ms, "bytes": b, "nnz": m.nnz, "rows": m.n_rows, "kernels": kernels, "params": params,
+            "source": ("rocprofv3 kernel trace of tools/cant_single.py (median of 50 cold launches, every rank)"
+                       if use_trace else "in-process: (span of K x (flush + SpMV) - span of K x flush) / K"),
+            "timed_region": {"what": f"{K} x (512 MiB flush + one SpMV), "
+                                     + ("one HIP graph replay" if GRAPH["on"] else "eager launches")
+                                     + " between barrier + synchronize",
+                             "wall_ms": round(wall * 1e3, 4), "wall_ms_per_step_incl_flush": round(wall_step, 5),
+                             "cold_spmv_ms_in_process": round(inproc_max, 5),
+                             "cold_spmv_ms_rocprof_rank0": traced,
+                             "cold_ms_per_rank": [round(v, 5) for v in per_rank]},
+            "parity_ok": True,
+            "check": "all 62,451 rows of y against the host check_result rule (1e-6 relative), every rank"}
 
 
 def strong_exchange(torch, comm, cdev, dm, x, y_full, lo, hi, bounds, steps, flush):
@@ -700,23 +830,88 @@ def banded_strong(args, torch, dev, rank, world, dist, cdev):
                         "ranks, generated on device, x[j] = j replicated", "scaling": "strong", "steps": 20, **out}
 
 
+def batch_leg(args, torch, dev, rank, world, dist, cdev):
+    """The block-diagonal batch of `--copies` cant-like matrices per rank
+    (rounds 1-3's headline): one launch per step streams 1.58 GB from HBM.
+    Returns (the workload dict, per-step wall ms, kernel ms, roofline)."""
+    a = argparse.Namespace(**vars(args))
+    a.workload = "batch"
+    w = build_workload(a, torch, dev, rank, world)
+    wall, kern = time_steps(torch, w["dm"], w["x"], w["y"], args.steps, args.warmup, dist)
+    bad = w["check"]()
+    all_ok(dist, cdev, torch, bad is None, str(bad), rank)
+    t = torch.tensor([wall, float(np.mean(kern))], dtype=torch.float64, device=cdev)
+    if dist is not None:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    ms_per_step = float(t[0].item()) / args.steps * 1e3
+    kern_ms = float(t[1].item())
+    achieved = w["bytes_rank"] / (kern_ms * 1e-3) * 1e-9
+    kname = kernel_name(a, w["dm"])
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": sa.HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / sa.HBM_PEAK_GBS, 4), "traffic": traffic_for(a.format, w["bytes_rank"], kname),
+            "kernel": kname, "kernel_ms": round(kern_ms, 5), "bytes_alg_per_launch": w["bytes_rank"]}
+    return w, ms_per_step, kern_ms, roof
+
+
+def per_format_leg(args, torch, dev, m, x, y, nnz, bytes_step):
+    """Every format on the same matrix (R-MAT: ELL is N/A, padding)."""
+    per_format = {}
+    x_host = x.cpu().numpy()
+    for fmt in sa.ALL_FORMATS:
+        kw = fmt_kwargs(args, fmt)
+        try:
+            d2 = sa.to_device(m, fmt, dev, **kw)
+        except sa.SpmvError as e:
+            per_format[fmt] = {"na": str(e)}
+            continue
+        _, k2 = time_steps(torch, d2, x, y, max(20, args.steps // 2), 5)
+        km = float(np.mean(k2))
+        # the output of every format is checked (host check_result rule,
+        # 1e-6 relative); csrf32 rounds the values to fp32, so its check
+        # shows fp32-value tolerance, not fp64 parity
+        badf, _ = sa.check(m, x_host, y[:m.n_rows].cpu().numpy())
+        per_format[fmt] = {"GBs": round(bytes_step / (km * 1e-3) * 1e-9, 1),
+                           "GFLOPs": round(2 * nnz / (km * 1e-3) * 1e-9, 1),
+                           "frac": round(bytes_step / (km * 1e-3) * 1e-9 / sa.HBM_PEAK_GBS, 4),
+                           "kernel_ms": round(km, 5), "stored_MB": round(d2.stored_bytes * 1e-6, 1),
+                           "params": dict(kw, **{k: v for k, v in d2.params.items()
+                                                 if k in ("variant", "split_T", "n_chunks", "H")}) or None,
+                           "parity_ok": badf == 0}
+        if fmt == "csrf32":
+            per_format[fmt]["parity"] = "within fp32-value tolerance (values rounded to fp32)"
+        del d2
+        torch.cuda.empty_cache()
+    return per_format
+
+
 def main():
     args = parse()
+    if args.workload == "cantlike":
+        args.workload = "batch"
+    if launch.needs_spawn(args.gpus):
+        # `--gpus N` from a plain process: N ranks in a child
+        # torch.distributed.run job; this process never touches the GPU
+        sys.exit(launch.spawn_ranks(__file__, args.gpus))
     GRAPH["on"] = args.graph == "yes"
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # the single-matrix figures come from a profiled CHILD process, run
-    # before this process initialises the GPU
-    single = None
-    if rank == 0 and not args.profile and (
-            args.single == "yes" or (args.single == "auto" and world == 1 and args.workload == "cantlike")):
-        single = cant_single_rocprof()
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    # the single-matrix kernel trace comes from a profiled CHILD process,
+    # run before this process initialises the GPU (every format at N=1; the
+    # headline format on every rank's own GPU at N>1)
+    prof = None
+    if not args.profile and args.workload == "cant" and args.single != "no":
+        if world == 1:
+            prof = cant_single_rocprof()
+        else:
+            prof = cant_single_rocprof([args.format], 0 if args.share_gpu else local)
+    elif rank == 0 and not args.profile and args.single == "yes" and world == 1:
+        prof = cant_single_rocprof()
 
     import torch
 
-    if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     dist = None
     gpu = 0 if args.share_gpu else local
     torch.cuda.set_device(gpu)
@@ -732,115 +927,139 @@ def main():
         else:
             dist.init_process_group("gloo")
 
-    w = build_workload(args, torch, dev, rank, world)
-    dm, x, y = w["dm"], w["x"], w["y"]
-    n_rows, nnz, bytes_step = w["rows"], w["nnz"], w["bytes_rank"]
-    wall, kern = time_steps(torch, dm, x, y, args.steps, args.warmup, dist)
-    launch = (f"hip-graph: the K launches captured once, replayed untimed for >= {WARM_REPLAY_MS:g} ms of GPU "
-              "work, then once timed; kernel_ms = span / K"
-              if GRAPH.get("last") == "hip-graph" else "eager launches, one HIP event after each")
-    if args.profile:
+    if args.profile:  # only the timed loop, for rocprofv3 --pmc passes
+        if args.workload == "cant":
+            s = single_cold(args, torch, dev, rank, world, dist, cdev, None)
+            ms = s["timed_region"]["cold_spmv_ms_in_process"]
+        else:
+            w = build_workload(args, torch, dev, rank, world)
+            _, kern = time_steps(torch, w["dm"], w["x"], w["y"], args.steps, args.warmup, dist)
+            ms = float(np.mean(kern))
         if rank == 0:
-            print(json.dumps({"profile_run": args.format, "ms_per_launch": float(np.mean(kern))}))
+            print(json.dumps({"profile_run": args.format, "workload": args.workload, "ms_per_launch": ms}))
         return
 
-    # parity of this step's output (host check_result rule), all ranks agree
-    bad = w["check"]()
-    all_ok(dist, cdev, torch, bad is None, str(bad), rank)
-
-    wall_t = torch.tensor([wall], dtype=torch.float64, device=cdev)
-    kern_t = torch.tensor([float(np.mean(kern))], dtype=torch.float64, device=cdev)
-    if dist is not None:
-        dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
-        dist.all_reduce(kern_t, op=dist.ReduceOp.MAX)
-    ms_per_step = float(wall_t.item()) / args.steps * 1e3
-    total_bytes = w["bytes_total"]
-    value = total_bytes / (ms_per_step * 1e-3) * 1e-9
-    gflops = 2.0 * w["nnz_total"] / (ms_per_step * 1e-3) * 1e-9
-
-    # ---- weak-scaling batch: the y blocks (all the same size) all-gathered
-    # over RCCL, timed separately, not in `value`
-    allgather = None
-    if dist is not None and args.workload == "cantlike":
-        y_loc = y if cdev.type == "cuda" else y.cpu()
-        y_all = torch.empty(n_rows * world, dtype=torch.float64, device=cdev)
-        for _ in range(3):
-            dist.all_gather_into_tensor(y_all, y_loc)
-        torch.cuda.synchronize()
-        ok = bool(torch.equal(y_all[rank * n_rows:(rank + 1) * n_rows], y_loc))
-        all_ok(dist, cdev, torch, ok, "all-gathered y block", rank)
-        dist.barrier()
-        t0 = time.perf_counter()
-        reps = 20
-        for _ in range(reps):
-            dist.all_gather_into_tensor(y_all, y_loc)
-        torch.cuda.synchronize()
-        ag = torch.tensor([(time.perf_counter() - t0) / reps], dtype=torch.float64, device=cdev)
-        dist.all_reduce(ag, op=dist.ReduceOp.MAX)
-        ag_ms = float(ag.item()) * 1e3
-        allgather = {"ms": round(ag_ms, 4), "bytes_per_rank": 8 * n_rows, "backend": args.backend,
-                     "value_with_allgather_GBs": round(total_bytes / ((ms_per_step + ag_ms) * 1e-3) * 1e-9, 1)}
-
-    kern_ms = float(kern_t.item())
-    achieved = bytes_step / (kern_ms * 1e-3) * 1e-9
-    kname = kernel_name(args, dm)
-    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": sa.HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / sa.HBM_PEAK_GBS, 4),
-                "traffic": traffic_for(args.format, bytes_step, kname),
-                "kernel": kname, "kernel_ms": round(kern_ms, 5), "bytes_alg_per_launch": bytes_step}
-
-    per_format = None
-    cpu = None
-    do_pf = rank == 0 and (args.per_format == "yes" or (args.per_format == "auto" and world == 1))
-    if do_pf and args.workload in ("rmat", "cantlike"):
-        # every format on the same matrix (R-MAT: ELL is N/A, padding)
-        m = w["loc"] if args.workload == "rmat" else w["m"]
-        del dm, w["dm"]
-        torch.cuda.empty_cache()
-        per_format = {}
-        x_host = x.cpu().numpy()
-        for fmt in sa.ALL_FORMATS:
-            kw = fmt_kwargs(args, fmt)
-            try:
-                d2 = sa.to_device(m, fmt, dev, **kw)
-            except sa.SpmvError as e:
-                per_format[fmt] = {"na": str(e)}
-                continue
-            _, k2 = time_steps(torch, d2, x, y, max(20, args.steps // 2), 5)
-            km = float(np.mean(k2))
-            # the output of every format is checked (host check_result rule,
-            # 1e-6 relative); csrf32 rounds the values to fp32, so its check
-            # shows fp32-value tolerance, not fp64 parity
-            badf, _ = sa.check(m, x_host, y[:m.n_rows].cpu().numpy())
-            per_format[fmt] = {"GBs": round(bytes_step / (km * 1e-3) * 1e-9, 1),
-                               "GFLOPs": round(2 * nnz / (km * 1e-3) * 1e-9, 1),
-                               "frac": round(bytes_step / (km * 1e-3) * 1e-9 / sa.HBM_PEAK_GBS, 4),
-                               "kernel_ms": round(km, 5), "stored_MB": round(d2.stored_bytes * 1e-6, 1),
-                               "params": dict(kw, **{k: v for k, v in d2.params.items()
-                                                     if k in ("variant", "split_T", "n_chunks", "H")}) or None,
-                               "parity_ok": badf == 0}
-            if fmt == "csrf32":
-                per_format[fmt]["parity"] = "within fp32-value tolerance (values rounded to fp32)"
-            del d2
+    batch = per_format = cpu = allgather = None
+    if args.workload == "cant":
+        s = single_cold(args, torch, dev, rank, world, dist, cdev, prof)
+        ms_per_step = s["cold_ms"]
+        bytes_step, total_bytes = s["bytes"], s["bytes"] * world
+        value = total_bytes / (ms_per_step * 1e-3) * 1e-9
+        gflops = 2.0 * s["nnz"] * world / (ms_per_step * 1e-3) * 1e-9
+        kname = s["kernels"][0]
+        roofline = {"bound": "hbm", "achieved": round(bytes_step / (ms_per_step * 1e-3) * 1e-9, 1),
+                    "peak": sa.HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(bytes_step / (ms_per_step * 1e-3) * 1e-9 / sa.HBM_PEAK_GBS, 4),
+                    "traffic": traffic_for(args.format, bytes_step, kname, cold=True),
+                    "kernel": kname, "kernels": s["kernels"], "kernel_ms": round(ms_per_step, 5),
+                    "kernel_ms_source": s["source"], "bytes_alg_per_launch": bytes_step,
+                    "state": "cold: 512 MiB flush before every launch"}
+        scaling, n_rows, nnz = "weak", s["rows"], s["nnz"]
+        data = ("synthetic: cant-like stand-in (62,451 rows, 4,007,383 entries = SuiteSparse cant's counts; the "
+                "reference's cant.mtx is an unfetched Git-LFS pointer), x[j] = j")
+        config = {"workload": f"{args.format} SpMV on ONE cant-like matrix per GPU (BASELINE.json "
+                              + ("configs[2]" if args.format == "sell" else "configs[1]")
+                              + "), cold: 512 MiB flush before every step; N GPUs run N replicas, no collective",
+                  "timed_region": s["timed_region"], "kernel_params": s["params"]}
+        launch_desc = s["timed_region"]["what"]
+        do_batch = args.batch == "yes" or (args.batch == "auto" and world == 1)
+        if do_batch:
+            w, b_ms, b_kern, b_roof = batch_leg(args, torch, dev, rank, world, dist, cdev)
+            batch = {"workload": w["config"]["workload"], "copies_per_gpu": args.copies,
+                     "value_GBs": round(w["bytes_total"] / (b_ms * 1e-3) * 1e-9, 1), "ms_per_step": round(b_ms, 5),
+                     "launch": "hip-graph replay (K launches, span / K)" if GRAPH.get("last") == "hip-graph"
+                               else "eager", "roofline": b_roof, "parity_ok": True}
+            if rank == 0 and world == 1 and args.per_format != "no":
+                dm = w.pop("dm")
+                del dm
+                torch.cuda.empty_cache()
+                batch["per_format"] = per_format_leg(args, torch, dev, w["m"], w["x"], w["y"], w["nnz"],
+                                                     w["bytes_rank"])
+            del w
             torch.cuda.empty_cache()
-        if args.cpu_seconds > 0:
-            if args.workload == "rmat":
-                ptr, col, val = sa.csr_from_coo(m)
-                cpu = cpu_baseline((ptr, col, val, m.n_rows, m.n_cols), 1, args.cpu_seconds)
-                cpu["sample"] = cpu["sample"].replace("the same 1-copy batch", "the same R-MAT")
-            else:
-                sm = sa.gen_cantlike(0, 1)
-                ptr, col, val = sa.csr_from_coo(sm)
-                cpu = cpu_baseline((ptr, col, val, sm.n_rows, sm.n_cols), args.copies, args.cpu_seconds)
+        if rank == 0 and world == 1 and args.cpu_seconds > 0:
+            sm = sa.gen_cantlike(0, 1)
+            ptr, col, val = sa.csr_from_coo(sm)
+            cpu = cpu_baseline((ptr, col, val, sm.n_rows, sm.n_cols), 1, args.cpu_seconds)
+            cpu["sample"] = cpu["sample"].replace("the same 1-copy batch", "the same single cant-like matrix "
+                                                  "(host caches warm: a CPU pass re-reads what the last left)")
+    else:
+        w = build_workload(args, torch, dev, rank, world)
+        dm, x, y = w["dm"], w["x"], w["y"]
+        n_rows, nnz, bytes_step = w["rows"], w["nnz"], w["bytes_rank"]
+        wall, kern = time_steps(torch, dm, x, y, args.steps, args.warmup, dist)
+        launch_desc = (f"hip-graph: the K launches captured once, replayed untimed for >= {WARM_REPLAY_MS:g} ms of "
+                       "GPU work, then once timed; kernel_ms = span / K"
+                       if GRAPH.get("last") == "hip-graph" else "eager launches, one HIP event after each")
+        bad = w["check"]()
+        all_ok(dist, cdev, torch, bad is None, str(bad), rank)
+        wall_t = torch.tensor([wall], dtype=torch.float64, device=cdev)
+        kern_t = torch.tensor([float(np.mean(kern))], dtype=torch.float64, device=cdev)
+        if dist is not None:
+            dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
+            dist.all_reduce(kern_t, op=dist.ReduceOp.MAX)
+        ms_per_step = float(wall_t.item()) / args.steps * 1e3
+        total_bytes = w["bytes_total"]
+        value = total_bytes / (ms_per_step * 1e-3) * 1e-9
+        gflops = 2.0 * w["nnz_total"] / (ms_per_step * 1e-3) * 1e-9
+        scaling, data, config = w["scaling"], w["data"], dict(w["config"])
 
-    rstrong = None
-    if args.rmat_strong == "yes" or (args.rmat_strong == "auto" and args.workload == "cantlike"):
+        # weak-scaling batch: the y blocks (all the same size) all-gathered
+        # over RCCL, timed separately, not in `value`
+        if dist is not None and args.workload == "batch":
+            y_loc = y if cdev.type == "cuda" else y.cpu()
+            y_all = torch.empty(n_rows * world, dtype=torch.float64, device=cdev)
+            for _ in range(3):
+                dist.all_gather_into_tensor(y_all, y_loc)
+            torch.cuda.synchronize()
+            ok = bool(torch.equal(y_all[rank * n_rows:(rank + 1) * n_rows], y_loc))
+            all_ok(dist, cdev, torch, ok, "all-gathered y block", rank)
+            dist.barrier()
+            t0 = time.perf_counter()
+            reps = 20
+            for _ in range(reps):
+                dist.all_gather_into_tensor(y_all, y_loc)
+            torch.cuda.synchronize()
+            ag = torch.tensor([(time.perf_counter() - t0) / reps], dtype=torch.float64, device=cdev)
+            dist.all_reduce(ag, op=dist.ReduceOp.MAX)
+            ag_ms = float(ag.item()) * 1e3
+            allgather = {"ms": round(ag_ms, 4), "bytes_per_rank": 8 * n_rows, "backend": args.backend,
+                         "value_with_allgather_GBs": round(total_bytes / ((ms_per_step + ag_ms) * 1e-3) * 1e-9, 1)}
+
+        kern_ms = float(kern_t.item())
+        achieved = bytes_step / (kern_ms * 1e-3) * 1e-9
+        kname = kernel_name(args, dm)
+        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": sa.HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / sa.HBM_PEAK_GBS, 4),
+                    "traffic": traffic_for(args.format, bytes_step, kname),
+                    "kernel": kname, "kernel_ms": round(kern_ms, 5), "bytes_alg_per_launch": bytes_step}
+
+        do_pf = rank == 0 and (args.per_format == "yes" or (args.per_format == "auto" and world == 1))
+        if do_pf and args.workload in ("rmat", "batch"):
+            m = w["loc"] if args.workload == "rmat" else w["m"]
+            del dm, w["dm"]
+            torch.cuda.empty_cache()
+            per_format = per_format_leg(args, torch, dev, m, x, y, nnz, bytes_step)
+            if args.cpu_seconds > 0:
+                if args.workload == "rmat":
+                    ptr, col, val = sa.csr_from_coo(m)
+                    cpu = cpu_baseline((ptr, col, val, m.n_rows, m.n_cols), 1, args.cpu_seconds)
+                    cpu["sample"] = cpu["sample"].replace("the same 1-copy batch", "the same R-MAT")
+                else:
+                    sm = sa.gen_cantlike(0, 1)
+                    ptr, col, val = sa.csr_from_coo(sm)
+                    cpu = cpu_baseline((ptr, col, val, sm.n_rows, sm.n_cols), args.copies, args.cpu_seconds)
         w.pop("dm", None)
         dm = None
         torch.cuda.empty_cache()
+
+    rstrong = None
+    default_wl = args.workload in ("cant", "batch")
+    if args.rmat_strong == "yes" or (args.rmat_strong == "auto" and default_wl):
+        torch.cuda.empty_cache()
         rstrong = rmat_strong(args, torch, dev, rank, world, dist, cdev)
     bstrong = None
-    if args.banded_strong == "yes" or (args.banded_strong == "auto" and args.workload == "cantlike"):
+    if args.banded_strong == "yes" or (args.banded_strong == "auto" and default_wl):
         bstrong = banded_strong(args, torch, dev, rank, world, dist, cdev)
 
     if rank == 0:
@@ -853,18 +1072,20 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 5),
             "higher_is_better": True,
-            "scaling": w["scaling"],
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "f64",
-            "data": w["data"],
-            "config": dict(w["config"], format=args.format, params=fmt_kwargs(args, args.format) or None,
+            "data": data,
+            "config": dict(config, format=args.format, params=fmt_kwargs(args, args.format) or None,
                            rows_rank0=n_rows, nnz_rank0=nnz, bytes_alg_rank0_step=bytes_step,
-                           bytes_alg_all_ranks_step=total_bytes, parallelism=f"row-shard x{world}",
-                           launch=launch),
+                           bytes_alg_all_ranks_step=total_bytes, parallelism=f"row-shard x{world}"
+                           if args.workload in ("rmat", "banded") else f"replicas x{world}",
+                           launch=launch_desc),
             "gflops": round(gflops, 1),
             "roofline": roofline,
             "cpu_baseline": cpu,
-            "cant_single": single,
+            "cant_single": prof if world == 1 else ({"rank0": prof} if prof else None),
+            "batch": batch,
             "per_format": per_format,
             "allgather": allgather,
             "rmat_strong": rstrong,

@@ -171,9 +171,10 @@ int spmv_csr16_fill(int64_t nnz, const int32_t *col, int32_t *blk_base, uint16_t
  * pair_row[p] the pair's row modulo SPMV_CSRG_ROWS.  Plan: n_pairs.
  * Fill: pair_ptr[n_pairs+1], col_g/val_g[nnz], blk_off[groups*(nb+1)],
  * pair_row[n_pairs].                                                    */
-#ifndef SPMV_CSRG_ROWS
+/* fixed (no -D override): the host fill, the device reduce and the Python
+ * binding (spmv_csrg_block_rows) must agree on it */
 #define SPMV_CSRG_ROWS 4096 /* also in spmv.h */
-#endif
+int32_t spmv_csrg_block_rows(void); /* SPMV_CSRG_ROWS as built into libspmv_host */
 int32_t spmv_csrg_group(int32_t col, int32_t groups);
 int spmv_csrg_plan(int64_t n_rows, const int64_t *row_ptr, const int32_t *col, int32_t groups,
                    int64_t *n_pairs);

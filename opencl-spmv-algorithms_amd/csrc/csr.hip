@@ -758,7 +758,10 @@ static int64_t csr_xwin_gpw(int L, int32_t rows_per_window, int64_t n_rows)
     }
     int64_t g = (kCsrXwinRows + rpb - 1) / rpb;
     g = g < 2 ? 2 : g;
-    if (n_rows < 4 * (int64_t)cu_count() * g * rpb)
+    // the MI355X's 256 CUs as a constant, not the current device's count:
+    // the window table (spmv_csr_xwin_build) bakes this choice in, so it
+    // must not change with the device a matrix is later run on
+    if (n_rows < 4 * (int64_t)256 * g * rpb)
         g = 1;
     return g;
 }

@@ -543,16 +543,20 @@ __global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell_small_
 }
 
 // Whether sell_small_kernel runs: C = 64 (a slice is one wave) and fewer
-// slices than ~3.5 waves per SIMD of one-wave-per-slice kernels would fill.
+// slices than ~3.5 waves per SIMD of one-wave-per-slice kernels would fill
+// on the MI355X's 256 CUs.  A pure function of (C, n_slices), never of the
+// current device: it sets the SELL geometry (4-slice workgroups or σ
+// windows) that spmv_sell_xwin_bytes/_build, spmv_sell16_fill (16-bit
+// offsets from each workgroup's window base), the SELL16 head and
+// spmv_sell_auto_ki all bake into the arrays they build, so a matrix built
+// under one device must run under the same geometry on any other (ADVICE
+// round 3: a CU-count query here made it depend on the current device).
+constexpr int64_t kSellSmallCUs = 256;
 bool sell_small(int32_t C, int64_t n_slices)
 {
     if (C != kWave || n_slices <= 0)
         return false;
-    int dev = 0, cus = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-        cus = 256;
-    return n_slices < 14 * (int64_t)cus;
+    return n_slices < 14 * kSellSmallCUs;
 }
 
 // slot groups per wave in the SELL16 head (its kernel's first batch): 8 and
@@ -610,13 +614,18 @@ __global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell16_head
     const int64_t g0 = ws * per;
     const int64_t g1 = g0 + per < groups ? g0 + per : groups;
     const int64_t hw = (int64_t)blockIdx.x * (S * P) + wv;
+    // groups past the wave's range repeat its first group, exactly as
+    // SlotBatch::load re-reads it without a head: the kernel masks their
+    // values, and x is read at one of the lane's own columns, so head and
+    // no-head give the same bits even for a non-finite x
     for (int u = 0; u < G; ++u)
         for (int k = 0; k < KI; ++k) {
             const int64_t dst = (hw * G + u) * step + lane * KI + k;
-            const bool in = g0 + u < g1;
-            const int64_t src = base + (g0 + u) * step + lane * KI + k;
-            hval[dst] = in ? val[src] : 0.0;
-            hcol[dst] = in ? col16[src] : (uint16_t)0;
+            const bool any = g1 > g0;
+            const int64_t gg = g0 + u < g1 ? g0 + u : g0;
+            const int64_t src = base + gg * step + lane * KI + k;
+            hval[dst] = any ? val[src] : 0.0;
+            hcol[dst] = any ? col16[src] : (uint16_t)0;
         }
 }
 

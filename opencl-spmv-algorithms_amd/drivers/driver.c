@@ -741,7 +741,10 @@ static int run_multi(const opts_t *o, spmv_format fmt, const coo_t *m, const dou
         /* x replicated; this shard's kernel writes rows [lo, hi) of y_full */
         if ((rc = upload((void **)&f[g].d_x, x, (size_t)m->n_cols * 8, NULL)) ||
             (rc = spmv_malloc((void **)&y_full[g], (size_t)(N + 1) * 8)) ||
-            (rc = spmv_memset(y_full[g], 0xFF, (size_t)(N + 1) * 8, NULL))) /* NaN: every row must arrive */
+            /* NaN: every row must arrive; queued on the shard's own stream
+             * (non-blocking, not ordered with the null stream) so the fill
+             * lands before the warm-up kernel writes its rows */
+            (rc = spmv_memset(y_full[g], 0xFF, (size_t)(N + 1) * 8, f[g].d.stream)))
             return SPMV_PROGRAM_ERROR;
         f[g].d_y = y_full[g] + lo;
         free(s.row);

@@ -665,6 +665,8 @@ static uint64_t csrg_mask(const int64_t *row_ptr, const int32_t *col, int64_t r,
     return m;
 }
 
+int32_t spmv_csrg_block_rows(void) { return SPMV_CSRG_ROWS; }
+
 int spmv_csrg_plan(int64_t n_rows, const int64_t *row_ptr, const int32_t *col, int32_t groups,
                    int64_t *n_pairs)
 {

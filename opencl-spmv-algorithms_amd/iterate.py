@@ -143,11 +143,22 @@ class Comm:
         return None
 
     @staticmethod
-    def wait(work) -> None:
+    def wait(work, stream=None) -> None:
         """Make the compute stream wait for a started collective (NCCL: a
-        stream dependency, the host does not block)."""
-        if work is not None:
-            work.wait()
+        stream dependency, the host does not block).  work.wait() orders
+        torch's CURRENT stream only; when the kernels run on another
+        `stream`, that stream waits on an event recorded on the current one
+        behind the collective."""
+        if work is None:
+            return
+        work.wait()
+        if stream is not None:
+            torch = sa._torch()
+            cur = torch.cuda.current_stream(stream.device)
+            if cur.cuda_stream != stream.cuda_stream:
+                ev = torch.cuda.Event()
+                ev.record(cur)
+                stream.wait_event(ev)
 
     def allgatherv(self, full, bounds) -> str:
         """In-place all-gather of row shards of their REAL sizes: `full`
@@ -279,10 +290,11 @@ class _Apply:
             op.kernels.spmv(self.full, y)
             return
         work = comm.allgather_start(self.full, self.send)
+        st = getattr(op.kernels, "stream", None)
         if not op.overlap:
-            comm.wait(work)
+            comm.wait(work, st)
         op.kernels.spmv(self.send, y)  # own block only: runs while the exchange is in flight
-        comm.wait(work)
+        comm.wait(work, st)
         op.remote.spmv(self.full, self.y2)
         op.kernels.axpy_ratio(op.rows, self.one, self.one, 1.0, self.y2, y)  # y += y_remote, exact
 

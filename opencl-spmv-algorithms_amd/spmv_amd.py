@@ -31,8 +31,7 @@ FORMATS = ("coo", "csr", "ell", "sell", "cmrs")  # the reference's five
 # SELL-C-σ with 16-bit column offsets; column-grouped CSR (gather-bound rows)
 EXTRA_FORMATS = ("csr16", "hyb", "csrf32", "sell16", "csrg")
 ALL_FORMATS = FORMATS + EXTRA_FORMATS
-HBM_PEAK_GBS = 8000.0
-CSRG_ROWS = 4096  # SPMV_CSRG_ROWS (include/spmv.h): rows per block of the CSRG reduce  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 # The reference's ReturnCode values (reference inc/enums.h:4-11).
 SUCCESS, DEVICE_ERROR, PROGRAM_ERROR, FILE_ERROR, OTHER_ERROR = range(5)
@@ -107,6 +106,11 @@ HIP_SYMBOLS = {
     "spmv_csr_xwin_build": (ctypes.c_int, [Dims, _vp, _vp, ctypes.c_int, _c_i32, _vp, ctypes.c_size_t,
                                            ctypes.POINTER(_c_i32)]),
     "spmv_csr_run_xwin": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, ctypes.c_int, _c_i32, _vp, _c_i32]),
+    "spmv_csr_small_bytes": (ctypes.c_size_t, [_c_i64, _c_i64]),
+    "spmv_csr_small_suits": (ctypes.c_int, [_c_i64, _c_i64]),
+    "spmv_csr_small_build": (ctypes.c_int, [Dims, _vp, _vp, ctypes.c_int, _vp, ctypes.c_size_t,
+                                            ctypes.POINTER(_c_i32)]),
+    "spmv_csr_run_small": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, ctypes.c_int, _vp, _c_i32]),
     "spmv_ell_run": (ctypes.c_int, [Dims, _c_i32, _c_i64, _c_i32, _vp, _vp, _vp, _vp]),
     "spmv_ell_xwin_bytes": (ctypes.c_size_t, [_c_i64]),
     "spmv_ell_xwin_build": (ctypes.c_int, [Dims, _c_i32, _c_i64, _c_i32, _vp, _vp, ctypes.c_size_t,
@@ -221,6 +225,7 @@ HOST_SYMBOLS = {
     "spmv_hyb_fill": (ctypes.c_int, [_c_i64, _vp, _vp, _vp, _c_i32, _c_i64, _c_i32, _vp, _vp, _vp, _vp, _vp]),
     "spmv_csr16_fill": (ctypes.c_int, [_c_i64, _vp, _vp, _vp, _vp]),
     "spmv_csrg_group": (_c_i32, [_c_i32, _c_i32]),
+    "spmv_csrg_block_rows": (_c_i32, []),
     "spmv_csrg_plan": (ctypes.c_int, [_c_i64, _vp, _vp, _c_i32, ctypes.POINTER(_c_i64)]),
     "spmv_csrg_fill": (ctypes.c_int, [_c_i64, _vp, _vp, _vp, _c_i32, _vp, _vp, _vp, _vp, _vp]),
     "spmv_cpu_coo": (ctypes.c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, ctypes.c_int]),
@@ -501,7 +506,7 @@ def csr16_build(col: np.ndarray):
     return dict(n_blocks=nb.value, n_esc=ne.value, blk_base=base, col_off=off, col_esc=esc)
 
 
-def csrg_build(n_rows: int, ptr, col, val, groups: int = 32):
+def csrg_build(n_rows: int, ptr, col, val, groups: int = 4):
     """Column-grouped CSR (spmv_host.h spmv_csrg_plan/fill): the entries
     group after group of 128-B x lines, as a CSR over (row, group) pairs,
     plus the per-row-block pair ranges of the reduce."""
@@ -510,7 +515,8 @@ def csrg_build(n_rows: int, ptr, col, val, groups: int = 32):
     _check_host(lib.spmv_csrg_plan(n_rows, _ptr(ptr), _ptr(col), groups, ctypes.byref(npairs)), "csrg_plan")
     n = npairs.value
     nnz = int(ptr[n_rows])
-    nb = (n_rows + CSRG_ROWS - 1) // CSRG_ROWS
+    rows = int(host_lib().spmv_csrg_block_rows())  # SPMV_CSRG_ROWS as built into the host fill
+    nb = (n_rows + rows - 1) // rows
     pair_ptr = np.empty(n + 1, np.int64)
     col_g = np.empty(max(nnz, 1), np.int32)
     val_g = np.empty(max(nnz, 1), np.float64)
@@ -641,6 +647,9 @@ class DeviceMatrix:
         elif self.fmt == "coo":
             rc = lib.spmv_coo_run(d, _ptr(a["row"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
                                   _ptr(a["ws"]), a["ws"].numel())
+        elif self.fmt == "csr" and "plan" in a:
+            rc = lib.spmv_csr_run_small(d, _ptr(a["row_ptr"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
+                                        p["lanes"], _ptr(a["plan"]), p["xcap"])
         elif self.fmt == "csr" and "win" in a:
             rc = lib.spmv_csr_run_xwin(d, _ptr(a["row_ptr"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
                                        p["lanes"], p.get("xwin_rows", 0), _ptr(a["win"]), p["xcap"])
@@ -859,15 +868,38 @@ def _csr_xwin(dm: DeviceMatrix) -> None:
     p["variant"] = 3
 
 
+def _csr_small(dm: DeviceMatrix) -> bool:
+    """Plan of the single-pass small-matrix CSR kernel (spmv_csr_run_small);
+    False when a tile would own too many rows or a row runs too far past
+    its tile (the x-window kernel then runs)."""
+    torch = _torch()
+    p, a = dm.params, dm.arrays
+    nbytes = hip_lib().spmv_csr_small_bytes(dm.n_rows, dm.nnz)
+    plan = torch.empty(max(nbytes, 32), dtype=torch.uint8, device=dm.device)
+    cap = _c_i32(0)
+    rc = hip_lib().spmv_csr_small_build(dm.dims(), _ptr(a["row_ptr"]), _ptr(a["col"]), p["lanes"], _ptr(plan),
+                                        plan.numel(), ctypes.byref(cap))
+    if rc != SUCCESS:
+        return False
+    a["plan"] = plan
+    p["xcap"] = cap.value
+    p["variant"] = 5
+    return True
+
+
 def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int = 0, ki: int = 0, C: int = 64,
               sigma: int = 1024, h: int = 8, ell_max_padding: float | None = 64.0,
               xwin: bool | None = None, xwin_rows: int = 0, split: int | None = None,
               cmrs_variant: int | None = None, hot: int | None = None,
-              csr16_max_escape: float | None = 0.5, groups: int = 0, head: bool = True) -> DeviceMatrix:
+              csr16_max_escape: float | None = 0.5, groups: int = 0, head: bool = True,
+              small: bool | None = None) -> DeviceMatrix:
     """Build `fmt` on the host (libspmv_host.so) and upload it.  xwin (CSR,
     ELL, SELL; default on): also build the per-workgroup x windows on the
     device and run the LDS x-window kernels (same bits as without).  split
-    (SELL) / cmrs_variant (CMRS): None = the library's skew rule."""
+    (SELL) / cmrs_variant (CMRS): None = the library's skew rule.  small
+    (CSR): the single-pass fixed-tile kernel for matrices whose whole grid
+    is resident at once (spmv_csr_run_small, variant 5); None = when the
+    library's rule says so and no variant / window size was asked for."""
     torch = _torch()
     if xwin is None:
         # COO: per-tile windows measured slower (0.534 vs 0.491 ms on the
@@ -892,12 +924,18 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
         return dm
     ptr, col, val = csr_from_coo(m)
     if fmt == "csr":
+        auto = variant == 0
         if variant == 0:  # host-side choice from the row-length skew
             variant = host_lib().spmv_csr_pick_variant(m.n_rows, _ptr(ptr))
+        if small is None:
+            small = (auto and variant == 3 and xwin and xwin_rows == 0 and lanes in (0, 2, 4, 8, 16)
+                     and bool(hip_lib().spmv_csr_small_suits(m.n_rows, m.nnz)))
         dm.params = dict(lanes=lanes, variant=variant, xwin_rows=xwin_rows)  # 0 = library picks
         dm.arrays = dict(row_ptr=_dev_tensor(ptr, device), col=_dev_tensor(col, device),
                          val=_dev_tensor(val, device))
-        if variant == 4:
+        if small and m.n_rows > 0 and _csr_small(dm):
+            pass
+        elif variant == 4:
             # hot-column table for power-law columns (None: library rule)
             H, hot_cols, col_hot = hot_columns(m.n_cols, col, 0 if hot is None else hot) if hot != 0 else (0, None, col)
             dm.params["H"] = H

@@ -543,7 +543,7 @@ def test_csrg_layout(kind, groups):
         m = sa.gen_random(100, 100, 0, 3, seed=1)
     ptr, col, val = sa.csr_from_coo(m)
     g = sa.csrg_build(m.n_rows, ptr, col, val, groups)
-    n, pp, nnz, nb, B = g["n_pairs"], g["pair_ptr"], m.nnz, g["nb"], sa.CSRG_ROWS
+    n, pp, nnz, nb, B = g["n_pairs"], g["pair_ptr"], m.nnz, g["nb"], int(sa.host_lib().spmv_csrg_block_rows())
     assert nb == (m.n_rows + B - 1) // B
     assert pp[0] == 0 and pp[n] == nnz and (np.diff(pp) > 0).all()
     grp = np.array([sa.host_lib().spmv_csrg_group(int(c), groups) for c in g["col_g"][:nnz]])

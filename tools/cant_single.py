@@ -182,8 +182,8 @@ def attach_trace(out, trace_dir):
         rec = out["formats"][fmt] if fmt in out["formats"] else out["stream_probe"]
         nbytes = rec.get("bytes", b)
         if cold:
-            cm = float(np.median(cold))
-            rec.update(cold_ms=round(cm, 5), cold_GBs=round(nbytes / (cm * 1e-3) * 1e-9, 1),
+            cm = round(float(np.median(cold)), 5)  # every figure from the rounded median (bench.py reuses it)
+            rec.update(cold_ms=cm, cold_GBs=round(nbytes / (cm * 1e-3) * 1e-9, 1),
                        cold_frac=round(nbytes / (cm * 1e-3) * 1e-9 / sa.HBM_PEAK_GBS, 4),
                        cold_ms_range=[round(min(cold), 5), round(max(cold), 5)])
         if warm:

@@ -33,13 +33,17 @@ for s in "${steps[@]}"; do
     bench) run bench 900 python bench.py;;
     prof) run prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --profile --steps 200;;
     single) run cant_single 600 python tools/cant_single.py --json gpurun_out/cant_single.json;;
-    profsingle) run prof_single 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_single -o run -- python3 tools/cant_single.py --json gpurun_out/cant_single_prof.json &&
+    profsingle) # CS_ARGS: extra cant_single arguments, e.g. --formats csr --extra 'csr@{"small": false}'
+                eval "cs_args=(${CS_ARGS:-})"
+                run prof_single 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_single -o run -- python3 tools/cant_single.py --json gpurun_out/cant_single_prof.json "${cs_args[@]}" &&
                 run attach_single 120 python tools/cant_single.py --json gpurun_out/cant_single_prof.json --attach gpurun_out/prof_single;;
+    newtests) run new_tests 900 $PYT tests/test_gpu_parity.py -k "small or sell16_head";;
     sweep) run sweep 600 python tools/sweep.py;;
     benchrmat) run bench_rmat 600 python bench.py --workload rmat --steps 20;;
     benchbanded) run bench_banded_sell 600 python bench.py --workload banded --format sell --steps 20 && run bench_banded_csr 600 python bench.py --workload banded --format csr --steps 20;;
     rehearse8) run shard_rehearse 900 python tools/shard_rehearse.py --gpus 1,2,4,8 --graph --reps 50;;
     rehearsecold) run shard_rehearse_cold 900 python tools/shard_rehearse.py --gpus 1,2,4,8 --graph --reps 50 --flush;;
+    spawn2) run spawn2 900 python bench.py --gpus 2 --backend gloo --share-gpu --steps 20 --banded-strong no;;
     rehearse2) run rehearse2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --backend gloo --share-gpu --steps 20;;
     rehearse2r) run rehearse2_rmat 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --backend gloo --share-gpu --workload rmat --steps 10;;
     drivers) run drivers 600 $PYT tests/test_drivers_gpu.py;;

@@ -45,6 +45,7 @@ import numpy as np
 REPO = Path(__file__).resolve().parents[1]
 sys.path[:0] = [str(REPO / "opencl-spmv-algorithms_amd"), str(REPO)]
 import iterate as it  # noqa: E402
+import launch  # noqa: E402
 import spmv_amd as sa  # noqa: E402
 
 
@@ -93,6 +94,8 @@ def main():
     ap.add_argument("--format", default="csr")
     ap.add_argument("--graph", action="store_true", help="HIP-graph replay (one rank)")
     ap.add_argument("--backend", default="nccl")
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks; without torch.distributed.run, N > 1 starts N ranks in a child job")
     ap.add_argument("--share-gpu", action="store_true", help="all ranks on cuda:0 (rehearsal)")
     ap.add_argument("--out", default=None)
     ap.add_argument("--mode", choices=["plain", "split", "overlap"], default="plain",
@@ -101,6 +104,8 @@ def main():
                     help="one-GPU overlap rehearsal of a W-way cut (no torch.distributed)")
     ap.add_argument("--reps", type=int, default=50)
     a = ap.parse_args()
+    if launch.needs_spawn(a.gpus):  # N ranks in a child torch.distributed.run job
+        sys.exit(launch.spawn_ranks(__file__, a.gpus))
     if a.rehearse:
         return rehearse(a)
 

@@ -70,6 +70,8 @@ METRIC = "effective HBM GB/s + GFLOP/s per format on cant.mtx, 1/2/4/8 MI355X"
 # tiles the slowest of 8 shards took 0.1421 / 0.1411 / 0.1464 / 0.1549 ms
 # with weights 1 / 2 / 3 / 4 (profiles/round2/shard_rehearse_tiled_w.log)
 RMAT_ROW_WEIGHT = 2.0
+# profile-guided re-cuts of the R-MAT shards (on cold shard times with --flush yes)
+RMAT_RECUTS = 3
 CSR_DEFAULT_VARIANT = 3  # spmv_csr_run_variant's default (csrc/csr.hip)
 # untimed replays of a freshly captured graph before the timed replay, at
 # least this much GPU time: the first replays of a new graph ran ~4 % slower
@@ -127,8 +129,6 @@ def kernel_name(args, dm=None):
     params = (getattr(dm, "params", {}) or {}) if dm is not None else {}
     if args.format == "cmrs" and params.get("variant") == 1:
         return "cmrs_tiled_kernel"
-    if dm is not None and args.format == "csr" and "plan" in getattr(dm, "arrays", {}):
-        return "csr_small_kernel"
     if dm is not None and "win" in getattr(dm, "arrays", {}):
         if args.format in ("csr16", "csrf32"):  # the CSR x-window kernel with another column / value source
             return "csr_xwin_kernel"
@@ -286,7 +286,7 @@ def traffic_for(fmt, workload_bytes, kernel=None, cold=False):
             continue
         if not t or int(t.get("bytes_alg", -1)) != int(workload_bytes):
             continue
-        if kernel is not None and t.get("kernel") != kernel:
+        if kernel is not None and str(t.get("kernel")) not in str(kernel):  # a name substring of the kernel
             continue
         return t.get("hbm_bytes_per_launch")
     return None
@@ -695,7 +695,9 @@ def rmat_strong(args, torch, dev, rank, world, dist, cdev):
                      col[ptr[lo]:ptr[hi]], val[ptr[lo]:ptr[hi]])
         return loc, sa.to_device(loc, "csr", dev), lo, hi
 
-    def run(bounds, k):
+    def run(bounds, k, cold=False):
+        """Warm steps of the cut (and with `cold`, each shard's cold time,
+        bench.cold_step_ms); every rank's shard times gathered."""
         loc, dm, _, _ = shard(bounds)
         y = torch.empty(max(loc.n_rows, 1), dtype=torch.float64, device=dev)
         wall, kern = time_steps(torch, dm, x, y, k, 5, dist)
@@ -703,28 +705,35 @@ def rmat_strong(args, torch, dev, rank, world, dist, cdev):
         all_ok(dist, cdev, torch, bad == 0, f"R-MAT shard row {first}", rank)
         params = {kk: v for kk, v in dm.params.items() if isinstance(v, (int, float, str))}
         t = torch.tensor([wall / k * 1e3, float(np.mean(kern))], dtype=torch.float64, device=cdev)
-        shard_ms = [float(np.mean(kern))]
+        c = (cold_step_ms(torch, dm, x, y, 10) or -1.0) if cold else -1.0
+        mine = torch.tensor([float(np.mean(kern)), c], dtype=torch.float64, device=cdev)
+        shard_ms, shard_cold = [float(mine[0].item())], [c]
         if dist is not None:
-            g = [torch.zeros(1, dtype=torch.float64, device=cdev) for _ in range(world)]
-            dist.all_gather(g, torch.tensor([float(np.mean(kern))], dtype=torch.float64, device=cdev))
-            shard_ms = [float(v.item()) for v in g]
+            g = [torch.zeros(2, dtype=torch.float64, device=cdev) for _ in range(world)]
+            dist.all_gather(g, mine)
+            shard_ms = [float(v[0].item()) for v in g]
+            shard_cold = [float(v[1].item()) for v in g]
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         del dm, y
         torch.cuda.empty_cache()
-        return float(t[0].item()), float(t[1].item()), shard_ms, params
+        return float(t[0].item()), float(t[1].item()), shard_ms, params, shard_cold
 
     bounds0 = sa.partition_rows(n, ptr, world, align=1024, row_weight=RMAT_ROW_WEIGHT)
-    step0, _, shard0, _ = run(bounds0, 20)
+    calib = args.flush == "yes"  # cut on COLD shard times (each shard flushed first), else warm
+    step0, _, shard0, _, cold0 = run(bounds0, 20, cold=calib and world > 1)
     bounds, passes = bounds0, []
-    if world > 1:  # two re-cuts, each from the previous cut's measured times;
-        b, t, best = bounds0, shard0, (max(shard0), bounds0)  # the measured cut with the lowest max is kept
-        for _ in range(2):
+    if world > 1:  # re-cuts, each from the previous cut's measured (cold) times;
+        key0 = cold0 if calib and min(cold0) > 0 else shard0
+        b, t, best = bounds0, key0, (max(key0), bounds0)  # the measured cut with the lowest max is kept
+        for _ in range(RMAT_RECUTS):
             b = sa.partition_rows_calibrated(n, ptr, world, b, t, align=1024, row_weight=RMAT_ROW_WEIGHT)
-            _, _, t, _ = run(b, 20)
-            passes.append({"shard_rows": np.diff(b).tolist(), "shard_ms": [round(v, 5) for v in t]})
-            best = min(best, (max(t), b), key=lambda c: c[0])
+            _, _, tw, _, tc = run(b, 20, cold=calib)
+            t = tc if calib and min(tc) > 0 else tw
+            passes.append({"shard_rows": np.diff(b).tolist(), "shard_ms": [round(v, 5) for v in tw],
+                           "shard_ms_cold": [round(v, 5) for v in tc] if calib else None})
+            best = min(best, (max(t), b), key=lambda cc: cc[0])
         bounds = best[1]
-    step_ms, kern_ms, shard_ms, params = run(bounds, steps)
+    step_ms, kern_ms, shard_ms, params, _ = run(bounds, steps)
 
     # the exchange on the final cut
     comm = iterate.Comm(dist)
@@ -756,10 +765,14 @@ def rmat_strong(args, torch, dev, rank, world, dist, cdev):
                          "ms": round(ag_ms, 5), "spmv_plus_allgather_ms": round(both_ms, 5),
                          "aggregate_GBs_with_allgather": gbs(both_ms),
                          "gathered_y_parity": "rank 0 checks all 1e7 rows of the gathered y"},
-           "partition": ("profile-guided: weighted cut (row weight %g) and two re-cuts by measured cost timed, "
-                         "the one with the lowest max shard time kept" % RMAT_ROW_WEIGHT) if world > 1 else "whole matrix",
+           "partition": ("profile-guided: weighted cut (row weight %g) and %d re-cuts by measured %s cost "
+                         "timed, the one with the lowest max %s shard time kept"
+                         % (RMAT_ROW_WEIGHT, RMAT_RECUTS, "cold" if calib else "warm", "cold" if calib else "warm"))
+                        if world > 1 else "whole matrix",
            "calibration": {"weighted_cut": {"shard_rows": np.diff(bounds0).tolist(),
                                             "shard_ms": [round(v, 5) for v in shard0],
+                                            "shard_ms_cold": [round(v, 5) for v in cold0] if calib and world > 1
+                                            else None,
                                             "aggregate_GBs": gbs(step0)},
                            "recuts": passes},
            "setup_s": round(time.perf_counter() - t0, 1)}

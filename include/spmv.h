@@ -98,28 +98,6 @@ int spmv_csr_xwin_build(spmv_dims d, const int64_t *row_ptr, const int32_t *col,
 int spmv_csr_run_xwin(spmv_dims d, const int64_t *row_ptr, const int32_t *col, const double *val,
                       const double *x, double *y, int lanes_per_row, int32_t rows_per_window,
                       const void *win, int32_t xcap);
-/* Single-pass CSR for small matrices whose whole grid is resident at once
- * (one cant-like matrix: 978 tiles for 256 CUs).  Each workgroup owns the
- * fixed entry tile [t*4096, (t+1)*4096): all of its value/column loads are
- * issued at once from blockIdx alone; it sums the rows whose first entry
- * lies in the tile (the entries of its last row past the tile end are
- * loaded too, at most 512).  Build once: spmv_csr_small_build writes one
- * 32-byte record per tile into `plan` (spmv_csr_small_bytes bytes: owned
- * rows, tail, x range) and returns the LDS x-window entries in *xcap; it
- * returns SPMV_OTHER_ERROR when a tile would own more than 4*256/L rows
- * or a row would run more than 512 entries past its tile (use
- * spmv_csr_run_xwin).  spmv_csr_small_suits: the library's rule for when
- * this kernel runs (at most 1,024 tiles).  lanes_per_row 0 (auto), 2, 4,
- * 8 or 16, the same at build and run.  Deterministic, no atomics, one
- * kernel; rows are summed in tile chunks, so y agrees with the other CSR
- * kernels to the parity rule, not bit for bit.  (reference kernels/Csr.cl,
- * csr.c:201)                                                             */
-size_t spmv_csr_small_bytes(int64_t n_rows, int64_t nnz);
-int spmv_csr_small_suits(int64_t n_rows, int64_t nnz);
-int spmv_csr_small_build(spmv_dims d, const int64_t *row_ptr, const int32_t *col, int lanes_per_row,
-                         void *plan, size_t plan_bytes, int32_t *xcap);
-int spmv_csr_run_small(spmv_dims d, const int64_t *row_ptr, const int32_t *col, const double *val,
-                       const double *x, double *y, int lanes_per_row, const void *plan, int32_t xcap);
 /* CSR with compressed 16-bit column indices (arrays
  * from spmv_csr16_plan/fill in spmv_host.h): 10.06 instead of 12 bytes per
  * entry when 64-entry blocks of columns span < 65536 (banded / FEM

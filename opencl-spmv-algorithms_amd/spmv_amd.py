@@ -106,11 +106,6 @@ HIP_SYMBOLS = {
     "spmv_csr_xwin_build": (ctypes.c_int, [Dims, _vp, _vp, ctypes.c_int, _c_i32, _vp, ctypes.c_size_t,
                                            ctypes.POINTER(_c_i32)]),
     "spmv_csr_run_xwin": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, ctypes.c_int, _c_i32, _vp, _c_i32]),
-    "spmv_csr_small_bytes": (ctypes.c_size_t, [_c_i64, _c_i64]),
-    "spmv_csr_small_suits": (ctypes.c_int, [_c_i64, _c_i64]),
-    "spmv_csr_small_build": (ctypes.c_int, [Dims, _vp, _vp, ctypes.c_int, _vp, ctypes.c_size_t,
-                                            ctypes.POINTER(_c_i32)]),
-    "spmv_csr_run_small": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, ctypes.c_int, _vp, _c_i32]),
     "spmv_ell_run": (ctypes.c_int, [Dims, _c_i32, _c_i64, _c_i32, _vp, _vp, _vp, _vp]),
     "spmv_ell_xwin_bytes": (ctypes.c_size_t, [_c_i64]),
     "spmv_ell_xwin_build": (ctypes.c_int, [Dims, _c_i32, _c_i64, _c_i32, _vp, _vp, ctypes.c_size_t,
@@ -260,7 +255,7 @@ def hip_lib() -> ctypes.CDLL:
     """libspmv_hip.so — raises if it was not built (no CPU fallback)."""
     global _hip
     if _hip is None:
-        path = Path(os.environ.get("SPMV_HIP_LIB", LIB_DIR / "libspmv_hip.so"))  # override: A/B runs
+        path = Path(os.environ.get("SPMV_HIP_LIB") or LIB_DIR / "libspmv_hip.so")  # override: A/B runs
         if not path.exists():
             raise SpmvError(PROGRAM_ERROR, "load libspmv_hip.so", f"{path} missing: run `make lib`")
         _hip = _bind(ctypes.CDLL(str(path), mode=ctypes.RTLD_GLOBAL), HIP_SYMBOLS)
@@ -647,9 +642,6 @@ class DeviceMatrix:
         elif self.fmt == "coo":
             rc = lib.spmv_coo_run(d, _ptr(a["row"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
                                   _ptr(a["ws"]), a["ws"].numel())
-        elif self.fmt == "csr" and "plan" in a:
-            rc = lib.spmv_csr_run_small(d, _ptr(a["row_ptr"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
-                                        p["lanes"], _ptr(a["plan"]), p["xcap"])
         elif self.fmt == "csr" and "win" in a:
             rc = lib.spmv_csr_run_xwin(d, _ptr(a["row_ptr"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
                                        p["lanes"], p.get("xwin_rows", 0), _ptr(a["win"]), p["xcap"])
@@ -868,38 +860,15 @@ def _csr_xwin(dm: DeviceMatrix) -> None:
     p["variant"] = 3
 
 
-def _csr_small(dm: DeviceMatrix) -> bool:
-    """Plan of the single-pass small-matrix CSR kernel (spmv_csr_run_small);
-    False when a tile would own too many rows or a row runs too far past
-    its tile (the x-window kernel then runs)."""
-    torch = _torch()
-    p, a = dm.params, dm.arrays
-    nbytes = hip_lib().spmv_csr_small_bytes(dm.n_rows, dm.nnz)
-    plan = torch.empty(max(nbytes, 32), dtype=torch.uint8, device=dm.device)
-    cap = _c_i32(0)
-    rc = hip_lib().spmv_csr_small_build(dm.dims(), _ptr(a["row_ptr"]), _ptr(a["col"]), p["lanes"], _ptr(plan),
-                                        plan.numel(), ctypes.byref(cap))
-    if rc != SUCCESS:
-        return False
-    a["plan"] = plan
-    p["xcap"] = cap.value
-    p["variant"] = 5
-    return True
-
-
 def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int = 0, ki: int = 0, C: int = 64,
               sigma: int = 1024, h: int = 8, ell_max_padding: float | None = 64.0,
               xwin: bool | None = None, xwin_rows: int = 0, split: int | None = None,
               cmrs_variant: int | None = None, hot: int | None = None,
-              csr16_max_escape: float | None = 0.5, groups: int = 0, head: bool = True,
-              small: bool | None = None) -> DeviceMatrix:
+              csr16_max_escape: float | None = 0.5, groups: int = 0, head: bool = True) -> DeviceMatrix:
     """Build `fmt` on the host (libspmv_host.so) and upload it.  xwin (CSR,
     ELL, SELL; default on): also build the per-workgroup x windows on the
     device and run the LDS x-window kernels (same bits as without).  split
-    (SELL) / cmrs_variant (CMRS): None = the library's skew rule.  small
-    (CSR): the single-pass fixed-tile kernel for matrices whose whole grid
-    is resident at once (spmv_csr_run_small, variant 5); None = when the
-    library's rule says so and no variant / window size was asked for."""
+    (SELL) / cmrs_variant (CMRS): None = the library's skew rule."""
     torch = _torch()
     if xwin is None:
         # COO: per-tile windows measured slower (0.534 vs 0.491 ms on the
@@ -924,18 +893,12 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
         return dm
     ptr, col, val = csr_from_coo(m)
     if fmt == "csr":
-        auto = variant == 0
         if variant == 0:  # host-side choice from the row-length skew
             variant = host_lib().spmv_csr_pick_variant(m.n_rows, _ptr(ptr))
-        if small is None:
-            small = (auto and variant == 3 and xwin and xwin_rows == 0 and lanes in (0, 2, 4, 8, 16)
-                     and bool(hip_lib().spmv_csr_small_suits(m.n_rows, m.nnz)))
         dm.params = dict(lanes=lanes, variant=variant, xwin_rows=xwin_rows)  # 0 = library picks
         dm.arrays = dict(row_ptr=_dev_tensor(ptr, device), col=_dev_tensor(col, device),
                          val=_dev_tensor(val, device))
-        if small and m.n_rows > 0 and _csr_small(dm):
-            pass
-        elif variant == 4:
+        if variant == 4:
             # hot-column table for power-law columns (None: library rule)
             H, hot_cols, col_hot = hot_columns(m.n_cols, col, 0 if hot is None else hot) if hot != 0 else (0, None, col)
             dm.params["H"] = H

@@ -72,11 +72,6 @@ FMT_PARAMS = [
     ("sell16", {"C": 64, "sigma": 1024, "ki": 2}),
     ("sell16", {"C": 64, "sigma": 1024, "ki": 1}),
     ("sell16", {"C": 64, "sigma": 1, "ki": 1}),
-    # single-pass fixed-tile CSR for small matrices (forced on and off)
-    ("csr", {"small": True}),
-    ("csr", {"small": True, "lanes": 16}),
-    ("csr", {"small": True, "lanes": 2}),
-    ("csr", {"small": False}),
     # column-grouped CSR (gather-bound power-law matrices)
     ("csrg", {"groups": 1}),
     ("csrg", {"groups": 5}),
@@ -921,88 +916,3 @@ def test_sell16_head_same_bits_nonfinite_x(torch_dev, ki):
         torch.cuda.synchronize()
         ys.append(y)
     assert torch.equal(ys[0].view(torch.int64), ys[1].view(torch.int64))
-
-
-# --------------------------------------------------------------------------
-# single-pass small-matrix CSR (spmv_csr_run_small, csrc/small.hip)
-
-def _small_cases():
-    rng = np.random.default_rng(31)
-    out = {}
-    # rows crossing tile ends by up to 512 entries (the tail), odd nnz
-    lens = rng.integers(0, 400, 3000)
-    lens[::97] = 0
-    out["ragged_tails"] = lens
-    # every row exactly 4096 / 64 entries: rows start on tile boundaries
-    out["aligned"] = np.full(4096, 64)
-    # one entry, odd totals, a last row alone in its tile
-    out["one"] = np.array([1])
-    out["odd"] = np.array([3, 0, 5, 0, 0, 7])
-    out["last_alone"] = np.concatenate([np.full(64, 64), [1]])
-    # empty rows at both ends and runs of them inside tiles
-    out["empty_runs"] = np.concatenate([[0] * 50, rng.integers(0, 30, 4000), [0] * 300])
-    return out
-
-
-def _matrix_from_lens(lens, n_cols=5000, seed=0):
-    rng = np.random.default_rng(seed)
-    lens = np.asarray(lens, dtype=np.int64)
-    row = np.repeat(np.arange(lens.size, dtype=np.int32), lens)
-    col = rng.integers(0, n_cols, row.size).astype(np.int32)
-    val = rng.uniform(-1, 1, row.size)
-    return sa.Coo(lens.size, n_cols, row, col, val, False, "lens")
-
-
-@pytest.mark.parametrize("case", list(_small_cases()))
-@pytest.mark.parametrize("lanes", [0, 2, 16])
-def test_csr_small_edges(torch_dev, case, lanes):
-    """Tiles cut rows anywhere: the owning tile loads the tail of its last
-    row, empty rows are owned and written 0, the lead-in entries of a row
-    begun in the previous tile are never summed; y pre-filled with NaN."""
-    torch, dev = torch_dev
-    m = _matrix_from_lens(_small_cases()[case], seed=len(case))
-    dm = sa.to_device(m, "csr", dev, lanes=lanes, small=True)
-    assert dm.params["variant"] == 5 and "plan" in dm.arrays
-    x = torch.from_numpy(np.random.default_rng(5).uniform(-1, 1, m.n_cols)).to(dev)
-    y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
-    dm.run(x, y)
-    y2 = torch.full_like(y, float("nan"))
-    dm.run(x, y2)
-    torch.cuda.synchronize()
-    assert torch.equal(y.view(torch.int64), y2.view(torch.int64))  # reproducible
-    assert_parity(m, y.cpu().numpy(), x.cpu().numpy())
-
-
-def test_csr_small_refuses_long_rows(torch_dev):
-    """A row running more than 512 entries past its tile (or a tile owning
-    more rows than its batches hold) is refused by the plan: the x-window
-    kernel runs instead, with the same parity."""
-    torch, dev = torch_dev
-    lens = np.concatenate([np.full(100, 10), [5000], np.full(100, 10)])
-    m = _matrix_from_lens(lens, seed=3)
-    dm = sa.to_device(m, "csr", dev, small=True)
-    assert dm.params["variant"] == 3 and "plan" not in dm.arrays
-    x = torch.from_numpy(np.random.default_rng(2).uniform(-1, 1, m.n_cols)).to(dev)
-    y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
-    dm.run(x, y)
-    torch.cuda.synchronize()
-    assert_parity(m, y.cpu().numpy(), x.cpu().numpy())
-    many = _matrix_from_lens(np.concatenate([np.zeros(3000, np.int64), [5]]), seed=4)  # one tile, 3,001 rows
-    assert "plan" not in sa.to_device(many, "csr", dev, small=True).arrays
-
-
-def test_csr_small_is_default_for_one_cantlike(torch_dev):
-    """ONE cant-like matrix (BASELINE.json configs[1]) runs the small kernel
-    by default, the 32-copy batch the x-window kernel; both pass the parity
-    rule against the file-order oracle with x[j] = j."""
-    torch, dev = torch_dev
-    for copies, variant in ((1, 5), (32, 3)):
-        m = sa.gen_cantlike(0, copies)
-        dm = sa.to_device(m, "csr", dev)
-        assert dm.params["variant"] == variant, copies
-        x = torch.from_numpy(sa.ramp_x(m.n_cols)).to(dev)
-        y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
-        dm.run(x, y)
-        torch.cuda.synchronize()
-        bad, first = sa.check(m, sa.ramp_x(m.n_cols), y.cpu().numpy())
-        assert bad == 0, (copies, first)

@@ -28,6 +28,7 @@ from __future__ import annotations
 import argparse
 import ctypes
 import json
+import os
 import sys
 from pathlib import Path
 
@@ -49,7 +50,10 @@ def probe_lib():
     lib.spmv_probe_stream.argtypes = [vp, ctypes.c_size_t, vp, vp]
     lib.spmv_probe_flush.argtypes = [vp, ctypes.c_size_t, vp]
     lib.spmv_probe_tag.argtypes = [ctypes.c_int, vp]
-    for f in (lib.spmv_probe_stream, lib.spmv_probe_flush, lib.spmv_probe_tag):
+    lib.spmv_probe_csr_stream.argtypes = [vp, vp, ctypes.c_int64, ctypes.c_int, vp, vp]
+    lib.spmv_probe_flush_read.argtypes = [vp, ctypes.c_size_t, vp, vp]
+    for f in (lib.spmv_probe_stream, lib.spmv_probe_flush, lib.spmv_probe_tag, lib.spmv_probe_csr_stream,
+              lib.spmv_probe_flush_read):
         f.restype = ctypes.c_int
     return lib
 
@@ -61,7 +65,15 @@ def main():
     ap.add_argument("--formats", default=",".join(sa.ALL_FORMATS))
     ap.add_argument("--extra", action="append", default=[], metavar='FMT@JSON',
                     help='another run of FMT with to_device kwargs, e.g. csr@{"xwin_rows": 64}; '
-                         '"_params" overrides run parameters after the build, e.g. sell16@{"_params": {"xcap": 0}}')
+                         '"_params" overrides run parameters after the build, e.g. sell16@{"_params": {"xcap": 0}}; '
+                         '"_env" sets library environment switches for that run only')
+    ap.add_argument("--flush-mode", default="write", choices=["write", "read"],
+                    help="cold state: 512 MiB WRITTEN before each launch (default; the caches hold dirty lines) "
+                         "or READ (clean lines)")
+    ap.add_argument("--warm-x", action="store_true",
+                    help="diagnostic: read x once after every flush (matrix cold, x cache-resident)")
+    ap.add_argument("--csr-probes", default="", help="also time the CSR-shaped stream probe (val + col pairs, "
+                    "no x) on the matrix's CSR arrays with these R values, e.g. 1,3,8")
     ap.add_argument("--attach", default=None, metavar="TRACE_DIR",
                     help="no GPU run: add the kernel-trace figures of a finished rocprofv3 run in TRACE_DIR "
                          "to the --json file it wrote")
@@ -81,8 +93,13 @@ def main():
     P = probe_lib()
     scratch = torch.empty(FLUSH_BYTES, dtype=torch.uint8, device=dev)
 
+    fsink = torch.zeros(16, dtype=torch.int32, device=dev)
+
     def flush():
-        assert P.spmv_probe_flush(scratch.data_ptr(), FLUSH_BYTES, sp) == 0
+        if a.flush_mode == "read":
+            assert P.spmv_probe_flush_read(scratch.data_ptr(), FLUSH_BYTES, fsink.data_ptr(), sp) == 0
+        else:
+            assert P.spmv_probe_flush(scratch.data_ptr(), FLUSH_BYTES, sp) == 0
 
     def tag(i):
         assert P.spmv_probe_tag(i, sp) == 0
@@ -91,8 +108,16 @@ def main():
     b = sa.bytes_alg(m.n_rows, m.n_cols, m.nnz)
     xh = sa.ramp_x(m.n_cols)
     x = torch.from_numpy(xh).to(dev)
+    if a.warm_x:
+        xsink = torch.zeros(1 << 12, dtype=torch.float64, device=dev)
+        plain_flush = flush
+
+        def flush():  # noqa: F811 — diagnostic: x read back into the caches after the flush
+            plain_flush()
+            assert P.spmv_probe_stream(x.data_ptr(), (m.n_cols * 8) // 16 * 16, xsink.data_ptr(), sp) == 0
     reps = a.reps
     out = {"matrix": "cant-like (62,451 rows, 4,007,383 entries), x[j] = j", "bytes_alg": b, "reps": reps,
+           "flush": f"512 MiB {'read' if a.flush_mode == 'read' else 'written'} before every cold launch",
            "formats": {}, "phases": {}}
     formats = [(f, f, {}) for f in a.formats.split(",") if f]
     for e in a.extra:
@@ -102,6 +127,9 @@ def main():
         tag(SETUP_TAG + i)  # builds, fills and the first run land in an ignored phase
         kw = dict(kw)
         over = kw.pop("_params", {})  # run-parameter overrides after the build, e.g. {"xcap": 0}
+        env = kw.pop("_env", {})  # library environment switches for this run only (A/B of placement / order)
+        saved = {k: os.environ.get(k) for k in env}
+        os.environ.update({k: str(v) for k, v in env.items()})
         dm = sa.to_device(m, fmt, dev, **kw)
         dm.params.update(over)
         y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
@@ -137,6 +165,57 @@ def main():
             out["formats"][label]["parity"] = "within fp32-value tolerance (values rounded to fp32)"
         out["phases"][label] = [2 * i, 2 * i + 1]
         del dm
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    # the CSR arrays streamed without the kernels' structure (val + col pairs)
+    if a.csr_probes:
+        _, ccol, cval = sa.csr_from_coo(m)
+        dval = torch.from_numpy(cval).to(dev)
+        dcol = torch.from_numpy(ccol).to(dev)
+        npairs = m.nnz // 2
+        sink2 = torch.zeros(1 << 16, dtype=torch.float64, device=dev)
+        for j, r in enumerate(int(v) for v in a.csr_probes.split(",")):
+            label = f"csr_stream_probe_R{r}"
+            ph = PROBE_TAG + 10 + 2 * j
+            tag(ph)
+            for _ in range(reps):
+                flush()
+                assert P.spmv_probe_csr_stream(dval.data_ptr(), dcol.data_ptr(), npairs, r, sink2.data_ptr(), sp) == 0
+            tag(ph + 1)
+            for _ in range(reps):
+                assert P.spmv_probe_csr_stream(dval.data_ptr(), dcol.data_ptr(), npairs, r, sink2.data_ptr(), sp) == 0
+            out["formats"][label] = {"bytes": 12 * 2 * npairs}
+            out["phases"][label] = [ph, ph + 1]
+        # the same probe on other placements of the same bytes: fresh copies,
+        # and val + col inside ONE allocation; and the plain probe on val alone
+        one = torch.empty(12 * 2 * npairs + 256, dtype=torch.uint8, device=dev)
+        v1 = one[: 16 * npairs].view(torch.float64)
+        c1 = one[16 * npairs: 24 * npairs].view(torch.int32)
+        v1.copy_(dval[: 2 * npairs])
+        c1.copy_(dcol[: 2 * npairs])
+        dval2, dcol2 = dval.clone(), dcol.clone()
+        extra = [("csr_stream_probe_R3_copies", lambda: P.spmv_probe_csr_stream(dval2.data_ptr(), dcol2.data_ptr(), npairs,
+                                                                                  3, sink2.data_ptr(), sp), 24 * npairs),
+                 ("csr_stream_probe_R3_one_alloc", lambda: P.spmv_probe_csr_stream(v1.data_ptr(), c1.data_ptr(), npairs, 3,
+                                                                                     sink2.data_ptr(), sp), 24 * npairs),
+                 ("stream_probe_val_only", lambda: P.spmv_probe_stream(dval.data_ptr(), 16 * npairs, sink2.data_ptr(), sp),
+                  16 * npairs)]
+        for j, (label, fn, nbytes) in enumerate(extra):
+            ph = PROBE_TAG + 40 + 2 * j
+            tag(ph)
+            for _ in range(reps):
+                flush()
+                assert fn() == 0
+            tag(ph + 1)
+            for _ in range(reps):
+                assert fn() == 0
+            out["formats"][label] = {"bytes": nbytes}
+            out["phases"][label] = [ph, ph + 1]
+        tag(SETUP_TAG + len(formats) + 1)
+        torch.cuda.synchronize()
     # the stream ceiling of the same bytes
     nb = (b + 15) // 16 * 16
     tag(SETUP_TAG + len(formats))

@@ -42,18 +42,23 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--passes", default="", help="comma list of pass names (default all)")
     ap.add_argument("--out", default="pmc_stalls.json")
+    ap.add_argument("--workload", default="batch", choices=["batch", "cant"],
+                    help="bench.py workload: the 32-copy batch, or ONE cant-like matrix cold")
+    ap.add_argument("--no-probe", action="store_true", help="skip the bandwidth-probe reference passes")
     a = ap.parse_args()
     passes = {k: v for k, v in PASSES.items() if not a.passes or k in a.passes.split(",")}
     probe = REPO / "tools" / "bw_probe"
-    jobs = [("probe_tile_nt", [str(probe), str(2 << 30), "3"], "tile_read_kernel<true, 8>", {}),
-            # the CSR access pattern without the LDS work (values + columns, R = 4)
-            ("probe_csr_stream", [str(probe), str(2 << 30), "3"], "csr_stream_kernel<4>", {})]
+    jobs = [] if a.no_probe else [
+        ("probe_tile_nt", [str(probe), str(2 << 30), "3"], "tile_read_kernel<true, 8>", {}),
+        # the CSR access pattern without the LDS work (values + columns, R = 4)
+        ("probe_csr_stream", [str(probe), str(2 << 30), "3"], "csr_stream_kernel<4>", {})]
     for spec in a.formats.split(","):
         spec_main, *env_parts = spec.split("@")
         env_kv = dict(e.split("=", 1) for e in env_parts)
         fmt = spec_main.partition(":")[0]
-        cmd = ["python3", "bench.py", "--profile", "--format", fmt, "--steps", str(a.steps), "--warmup", "2"]
-        jobs.append((spec, cmd, kernel_for(fmt, env_kv), env_kv))
+        cmd = ["python3", "bench.py", "--profile", "--format", fmt, "--steps", str(a.steps), "--warmup", "2",
+               "--workload", a.workload]
+        jobs.append((spec, cmd, kernel_for(fmt, env_kv, a.workload), env_kv))
     out = {}
     for name, cmd, kern, env_kv in jobs:
         counters = {}

@@ -12,6 +12,10 @@ Follows MI355X_MICROARCH.md §HBM / cdna_hip_programming.md §7:
     goes to profiles/traffic.json, which bench.py reports as
     roofline.traffic when its workload (bytes_alg) matches.
     python tools/pmc_traffic.py [--formats csr,sell,ell,coo,cmrs] [--copies 32]
+    python tools/pmc_traffic.py --workload cant --formats csr --out traffic_single.json
+  (--workload cant: ONE cant-like matrix, COLD — bench.py's headline step,
+  a 512 MiB flush before every launch — written for bench.py's cold
+  roofline.traffic)
 """
 from __future__ import annotations
 
@@ -27,12 +31,14 @@ REPO = Path(__file__).resolve().parents[1]
 OUT = REPO / "gpurun_out" / "pmc"
 KERNELS = {"csr": "csr_xwin_kernel", "sell": "sell_xwin_kernel", "ell": "ell_xwin_kernel",
            "coo": "coo_staged_kernel", "cmrs": "cmrs_staged_kernel", "csr16": "Col16"}
+# one cant-like matrix: the small-matrix kernels
+KERNELS_SINGLE = dict(KERNELS, sell="sell_small_kernel", sell16="sell_small_kernel")
 
 
-def kernel_for(fmt, env):
+def kernel_for(fmt, env, workload="batch"):
     """The dominant kernel's name (substring) for `fmt` under `env`."""
     del env  # placement / cache-policy knobs do not change the kernel
-    return KERNELS[fmt]
+    return (KERNELS_SINGLE if workload == "cant" else KERNELS)[fmt]
 PASSES = {
     "fetch": ["FETCH_SIZE"],
     "write": ["WRITE_SIZE"],
@@ -94,9 +100,11 @@ def main():
     ap.add_argument("--copies", type=int, default=32)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--out", default=None, help="file name under profiles/ (default traffic.json)")
-    ap.add_argument("--workload", default="cantlike", choices=["cantlike", "rmat"])
+    ap.add_argument("--workload", default="batch", choices=["batch", "cantlike", "cant", "rmat"])
     ap.add_argument("--kernel", default=None, help="kernel name substring (default: the format's)")
     a = ap.parse_args()
+    if a.workload == "cantlike":
+        a.workload = "batch"
     probe = REPO / "tools" / "bw_probe"
     if not probe.exists():
         subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", str(REPO / "tools" / "bw_probe.hip"), "-o",
@@ -134,11 +142,12 @@ def main():
         for tag, cs in PASSES.items():
             f = run_pass(f"{tag0}_{tag}", cs, cmd)
             if f:
-                c, n = mean_per_dispatch(f, a.kernel or kernel_for(fmt, env_kv))
+                c, n = mean_per_dispatch(f, a.kernel or kernel_for(fmt, env_kv, a.workload))
                 counters.update(c)
         if not counters:
             continue
-        N, Z = (CANT_N * a.copies, CANT_Z * a.copies) if a.workload == "cantlike" else (10**7, 10**8)
+        N, Z = {"batch": (CANT_N * a.copies, CANT_Z * a.copies), "cant": (CANT_N, CANT_Z)}.get(a.workload,
+                                                                                               (10**7, 10**8))
         b_alg = 12 * Z + 4 * (N + 1) + 8 * N + 8 * N
         read_rdreq = bytes_from_rdreq(counters)
         if cal_rdreq and 0.8 < cal_rdreq < 1.25:
@@ -154,7 +163,8 @@ def main():
         hits, miss = counters.get("TCC_HIT_sum", 0.0), counters.get("TCC_MISS_sum", 0.0)
         for k in env_kv:
             os.environ.pop(k, None)
-        result[spec] = {"kernel": a.kernel or kernel_for(fmt, env_kv), "workload": a.workload, "bytes_alg": b_alg, "dispatches": n, "cmd": " ".join(cmd[1:]),
+        result[spec] = {"kernel": a.kernel or kernel_for(fmt, env_kv, a.workload), "workload": a.workload,
+                        "state": "cold: 512 MiB flush before every launch" if a.workload == "cant" else "streamed", "bytes_alg": b_alg, "dispatches": n, "cmd": " ".join(cmd[1:]),
                         "env": env_kv or None,
                        "hbm_read_bytes_per_launch": round(read), "hbm_write_bytes_per_launch": round(write),
                        "hbm_bytes_per_launch": round(read + write),

@@ -37,10 +37,58 @@ __global__ __launch_bounds__(kBlock) void probe_stream_kernel(const v2f64 *__res
         out[blockIdx.x] = s;
 }
 
+// The CSR-shaped stream: each workgroup reads one contiguous range of E =
+// 2·256·R entries of `val` (16-byte pairs) and `col` (8-byte pairs), all R
+// pairs of a lane in flight together, no LDS and no x (the bytes the CSR
+// kernels stream, without their structure).
+// MODE (lab): 0 = val + col, 1 = val only, 2 = col only, 3 = val + col with
+// the column pairs non-temporal too
+template <int R, int MODE = 0>
+__global__ __launch_bounds__(kBlock) void probe_csr_stream_kernel(const v2f64 *__restrict__ val,
+                                                                  const int2 *__restrict__ col, int64_t npairs,
+                                                                  double *__restrict__ out)
+{
+    const int64_t base = (int64_t)blockIdx.x * kBlock * R + threadIdx.x;
+    v2f64 v[R];
+    int2 c[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+        const int64_t i = base + (int64_t)k * kBlock;
+        const int64_t q = i < npairs ? i : npairs - 1;
+        v[k] = MODE == 2 ? v2f64{0.0, 0.0} : __builtin_nontemporal_load(val + q);
+        if (MODE == 3) {
+            typedef int v2i32 __attribute__((ext_vector_type(2)));
+            const v2i32 t = __builtin_nontemporal_load(reinterpret_cast<const v2i32 *>(col) + q);
+            c[k] = int2{t.x, t.y};
+        } else {
+            c[k] = MODE == 1 ? int2{0, 0} : col[q];
+        }
+    }
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < R; ++k)
+        s += v[k].x + v[k].y + (double)(c[k].x + c[k].y);
+    if (s == 1.2345e-300)
+        out[blockIdx.x] = s;
+}
+
 __global__ __launch_bounds__(kBlock) void probe_flush_kernel(uint4 *__restrict__ p, int64_t n16, uint32_t tick)
 {
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n16; i += (int64_t)gridDim.x * kBlock)
         p[i] = uint4{tick, (uint32_t)i, tick, (uint32_t)(i >> 32)};
+}
+
+// evicts by READING (plain loads): leaves the caches full of clean lines
+__global__ __launch_bounds__(kBlock) void probe_flush_read_kernel(const uint4 *__restrict__ p, int64_t n16,
+                                                                  uint32_t *__restrict__ sink)
+{
+    uint32_t acc = 0;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n16; i += (int64_t)gridDim.x * kBlock) {
+        const uint4 v = p[i];
+        acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+    if (acc == 0x9e3779b9u && sink)
+        *sink = acc;
 }
 
 __global__ void probe_tag_kernel(int *__restrict__ sink)
@@ -65,11 +113,46 @@ int spmv_probe_stream(const void *buf, size_t bytes, double *out, void *stream)
     return (int)hipGetLastError();
 }
 
+// reads the first 2·npairs entries of val (fp64) and col (int32) with R
+// pairs per lane (R = 1, 3 or 8); returns a hipError_t
+int spmv_probe_csr_stream(const void *val, const void *col, int64_t npairs, int R, double *out, void *stream)
+{
+    if (npairs <= 0)
+        return (int)hipErrorInvalidValue;
+    if (R >= 10 && R <= 13) {  // lab: R = 10 + MODE with 3 pairs per lane
+        const int64_t b3 = (npairs + kBlock * 3 - 1) / (kBlock * 3);
+#define PCS(M) hipLaunchKernelGGL((probe_csr_stream_kernel<3, M>), dim3((unsigned)b3), dim3(kBlock), 0, \
+                                  (hipStream_t)stream, (const v2f64 *)val, (const int2 *)col, npairs, out)
+        if (R == 10) PCS(0); else if (R == 11) PCS(1); else if (R == 12) PCS(2); else PCS(3);
+#undef PCS
+        return (int)hipGetLastError();
+    }
+    const int r = R >= 8 ? 8 : R >= 3 ? 3 : 1;
+    const int64_t blocks = (npairs + kBlock * r - 1) / (kBlock * r);
+    if (r == 8)
+        hipLaunchKernelGGL(probe_csr_stream_kernel<8>, dim3((unsigned)blocks), dim3(kBlock), 0, (hipStream_t)stream,
+                           (const v2f64 *)val, (const int2 *)col, npairs, out);
+    else if (r == 3)
+        hipLaunchKernelGGL(probe_csr_stream_kernel<3>, dim3((unsigned)blocks), dim3(kBlock), 0, (hipStream_t)stream,
+                           (const v2f64 *)val, (const int2 *)col, npairs, out);
+    else
+        hipLaunchKernelGGL(probe_csr_stream_kernel<1>, dim3((unsigned)blocks), dim3(kBlock), 0, (hipStream_t)stream,
+                           (const v2f64 *)val, (const int2 *)col, npairs, out);
+    return (int)hipGetLastError();
+}
+
 int spmv_probe_flush(void *buf, size_t bytes, void *stream)
 {
     static uint32_t tick = 0;
     hipLaunchKernelGGL(probe_flush_kernel, dim3(2048), dim3(kBlock), 0, (hipStream_t)stream, (uint4 *)buf,
                        (int64_t)(bytes / 16), ++tick);
+    return (int)hipGetLastError();
+}
+
+int spmv_probe_flush_read(const void *buf, size_t bytes, void *sink, void *stream)
+{
+    hipLaunchKernelGGL(probe_flush_read_kernel, dim3(2048), dim3(kBlock), 0, (hipStream_t)stream, (const uint4 *)buf,
+                       (int64_t)(bytes / 16), (uint32_t *)sink);
     return (int)hipGetLastError();
 }
 

@@ -45,6 +45,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--parts", default="8,16,32,64")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--sorts", default="",
+                    help="also time the product path with each row's entries reordered: col (ascending "
+                         "column) or hot (ascending hot-table id: cold columns by id, then hot ones by rank)")
     ap.add_argument("--colmaps", default="",
                     help="also time the product kernel (no hot table) with the columns replaced: "
                          "zero, mod<k>, rand<k> (uniform over k columns), comma-separated")
@@ -71,6 +74,25 @@ def main():
     print(json.dumps({"product_y_sha1": hashlib.sha1(y_ref.tobytes()).hexdigest()}), flush=True)
     del dm
     torch.cuda.empty_cache()
+    # within-row entry orders (same rows, same tiles; sums reordered inside rows)
+    for so in [c for c in a.sorts.split(",") if c]:
+        if so == "col":
+            key = m.col.astype(np.int64)
+        else:
+            _, _, col_hot = sa.hot_columns(m.n_cols, m.col, 0)
+            key = col_hot.astype(np.int64)
+        o = np.lexsort((key, m.row))
+        m2 = sa.Coo(m.n_rows, m.n_cols, m.row[o], m.col[o], m.val[o], False, so)
+        del o, key
+        dm = sa.to_device(m2, "csr", dev)
+        for cold in (0, 1):
+            ms = time_run(torch, dm, x, y, a.reps, cold, sa)
+            print(json.dumps({"variant": "sorted", "order": so, "cold": cold, "ms": round(ms, 4),
+                              "GBs": round(b / ms * 1e-6, 1)}), flush=True)
+        bad, first = sa.check(m2, xh, y.cpu().numpy())
+        print(json.dumps({"variant": "sorted", "order": so, "parity_bad_rows": int(bad)}), flush=True)
+        del dm, m2
+        torch.cuda.empty_cache()
     # gather-cost probes: same rows, same tiles, columns replaced
     for cm in [c for c in a.colmaps.split(",") if c]:
         if cm == "zero":
@@ -87,7 +109,7 @@ def main():
                               "GBs": round(b / ms * 1e-6, 1)}), flush=True)
         del dm, m2, c2
         torch.cuda.empty_cache()
-    for P in [int(p) for p in a.parts.split(",")]:
+    for P in [int(p) for p in a.parts.split(",") if p]:
         t = time.time()
         dm = sa.to_device(m, "csrg", dev, groups=P)
         setup = time.time() - t

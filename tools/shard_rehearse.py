@@ -109,10 +109,11 @@ def main():
             kw["sigma"] = 1 << 24  # whole-matrix sort on R-MAT (bench.py's R-MAT default)
         bounds = sa.partition_rows(n, ptr, G, align=1024, row_weight=w)
         for cpass in range(a.calibrate + 1):
-            if cpass:
-                bounds = sa.partition_rows_calibrated(n, ptr, G, bounds, times[0], align=1024, row_weight=w)
-            times, base = run_split(a, torch, sa, dev, ptr, col, val, n, x, xh, b_total, envs, kw, G, w, hot,
-                                    bounds, cpass, base)
+            if cpass:  # re-cut on the cold shard times with --flush (bench.py's rule), else warm
+                cost = cold if a.flush and cold and min(cold) > 0 else times[0]
+                bounds = sa.partition_rows_calibrated(n, ptr, G, bounds, cost, align=1024, row_weight=w)
+            times, base, cold = run_split(a, torch, sa, dev, ptr, col, val, n, x, xh, b_total, envs, kw, G, w,
+                                          hot, bounds, cpass, base)
 
 
 def run_split(a, torch, sa, dev, ptr, col, val, n, x, xh, b_total, envs, kw, G, w, hot, bounds, cpass, base):
@@ -156,7 +157,7 @@ def run_split(a, torch, sa, dev, ptr, col, val, n, x, xh, b_total, envs, kw, G, 
                           "shard_ms": [round(t, 4) for t in times[i]], "max_ms": round(tmax, 4),
                           "aggregate_GBs_warm": round(agg, 1), "speedup_vs_first": round(agg / base, 2), **extra}),
               flush=True)
-    return times, base
+    return times, base, cold
 
 
 if __name__ == "__main__":

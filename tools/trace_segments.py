@@ -15,7 +15,7 @@ import csv
 from collections import defaultdict
 
 TAG = "probe_tag_kernel"
-FLUSH = "probe_flush_kernel"
+FLUSH = "probe_flush"  # probe_flush_kernel (write) or probe_flush_read_kernel
 
 
 def _dispatches(path):

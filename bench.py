@@ -456,7 +456,7 @@ def cpu_baseline(m_single_csr, copies, budget_s):
     t_end = time.perf_counter() + budget_s
     while time.perf_counter() < t_end or len(times) < 3:
         times.append(oracle.cpu_csr_omp(B * n_rows, bptr, bcol, bval, x, y, threads))
-        if len(times) >= 5000:  # ~10 s of passes on the cant batch (4-5 ms each)
+        if len(times) >= 200_000:  # ~10 s of passes on one cant-like matrix (~0.1 ms each)
             break
     t = float(np.median(times))
     b = sa.bytes_alg(B * n_rows, B * n_cols, B * int(ptr[-1]))
@@ -500,7 +500,7 @@ def cant_single_rocprof(formats=None, local=None):
         if formats:
             plain += ["--formats", ",".join(formats)]
         traced = Path(rocprof).exists()
-        cmd = ([rocprof, "--kernel-trace", "--output-format", "csv", "-d", tmp, "-o", "run", "--"] + plain
+        cmd = ([rocprof, "--kernel-trace", "--stats", "--output-format", "csv", "-d", tmp, "-o", "run", "--"] + plain
                if traced else plain)
         try:
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=420, cwd=str(REPO), env=env)
@@ -516,6 +516,17 @@ def cant_single_rocprof(formats=None, local=None):
             from cant_single import attach_trace
 
             attach_trace(res, tmp)
+            # the profiler's own --stats summary of the same run (every launch
+            # of a kernel, cold and warm together)
+            stats = sorted(Path(tmp).rglob("*kernel_stats.csv"))
+            if stats:
+                import csv
+
+                res["rocprof_kernel_stats"] = [
+                    {"kernel": r["Name"].replace("void ", "").split("(")[0], "calls": int(r["Calls"]),
+                     "avg_ns": round(float(r["AverageNs"]), 1), "min_ns": int(float(r["MinNs"])),
+                     "max_ns": int(float(r["MaxNs"]))}
+                    for r in csv.DictReader(open(stats[-1], newline="")) if "spmv::" in r["Name"]]
         else:
             res["timing"] = "HIP events around each launch (no rocprofv3 trace): includes event overhead"
     res.pop("phases", None)

@@ -298,6 +298,18 @@ size_t spmv_sell16_head_bytes(int64_t n_slices, int32_t C, int32_t ki);
 int spmv_sell16_head_fill(spmv_dims d, int32_t C, int32_t sigma, int32_t ki, int64_t n_slices,
                           const int64_t *slice_ptr, const double *val, const uint16_t *col16,
                           void *head, size_t head_bytes);
+/* The same head for int32 SELL-C-sigma (small matrices only; 12 B per head
+ * slot): spmv_sell_head_bytes() is 0 for other matrices.  The run with a
+ * head gives the bits of spmv_sell_run_xwin (win/xcap from
+ * spmv_sell_xwin_build).  (reference kernels/Sigma_C.cl, sigma_c.c:311)  */
+size_t spmv_sell_head_bytes(int64_t n_slices, int32_t C, int32_t ki);
+int spmv_sell_head_fill(spmv_dims d, int32_t C, int32_t sigma, int32_t ki, int64_t n_slices,
+                        const int64_t *slice_ptr, const double *val, const int32_t *col, void *head,
+                        size_t head_bytes);
+int spmv_sell_run_xwin_head(spmv_dims d, int32_t C, int32_t sigma, int32_t ki, int64_t n_slices,
+                            const int64_t *slice_ptr, const int32_t *perm, const int32_t *col,
+                            const double *val, const double *x, double *y, const void *win, int32_t xcap,
+                            const void *head);
 
 /* --------------------------------------------------------------- CMRS ---
  * Replaces kernel `cmrs(val,idx,strip_ptr,row_in_strip,x,y,N,h,__local)`

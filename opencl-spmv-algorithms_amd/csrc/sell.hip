@@ -577,7 +577,7 @@ static void launch_sell_small(int64_t n_slices, const int64_t *slice_ptr, const 
     hipLaunchKernelGGL((sell_small_kernel<KI, NT, XWIN, XS, CT, HH>), dim3((unsigned)blocks),                 \
                        dim3(kWave * kSellSmallS * kSellSmallP), lds, st, n_slices, slice_ptr, perm, col, val, xs, \
                        y, wcap, x, win, xcap, hval, hcol)
-    if constexpr (XWIN && std::is_same<CT, uint16_t>::value) {  // the head exists for SELL16 only
+    if constexpr (XWIN) {  // the head (SELL16, or int32 SELL small matrices)
         if (hval)
             SPMV_SMALL_HG(kSell16HeadG);
         else
@@ -597,10 +597,10 @@ static int64_t sell16_head_elems(int64_t n_slices, int32_t ki)
     return blocks * kSellSmallS * kSellSmallP * (int64_t)sell16_head_g() * kWave * ki;
 }
 
-template <int KI, int G>
+template <int KI, int G, typename CT>
 __global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell16_head_kernel(
     int64_t n_slices, const int64_t *__restrict__ slice_ptr, const double *__restrict__ val,
-    const uint16_t *__restrict__ col16, double *__restrict__ hval, uint16_t *__restrict__ hcol)
+    const CT *__restrict__ col16, double *__restrict__ hval, CT *__restrict__ hcol)
 {
     constexpr int S = kSellSmallS, P = kSellSmallP;
     constexpr int64_t step = (int64_t)kWave * KI;
@@ -625,7 +625,7 @@ __global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell16_head
             const int64_t gg = g0 + u < g1 ? g0 + u : g0;
             const int64_t src = base + gg * step + lane * KI + k;
             hval[dst] = any ? val[src] : 0.0;
-            hcol[dst] = any ? col16[src] : (uint16_t)0;
+            hcol[dst] = any ? col16[src] : (CT)0;
         }
 }
 
@@ -960,14 +960,80 @@ extern "C" int spmv_sell16_head_fill(spmv_dims d, int32_t C, int32_t sigma, int3
     const int64_t blocks = (n_slices + kSellSmallP - 1) / kSellSmallP;
     const hipStream_t st = (hipStream_t)d.stream;
 #define SPMV_HEAD_FILL(K, HH)                                                                                    \
-    hipLaunchKernelGGL((sell16_head_kernel<K, HH>), dim3((unsigned)blocks), dim3(kWave * kSellSmallS * kSellSmallP), 0, \
-                       st, n_slices, slice_ptr, val, col16, hval, hcol)
+    hipLaunchKernelGGL((sell16_head_kernel<K, HH, uint16_t>), dim3((unsigned)blocks),                             \
+                       dim3(kWave * kSellSmallS * kSellSmallP), 0, st, n_slices, slice_ptr, val, col16, hval, hcol)
     if (ki == 2)
         SPMV_HEAD_FILL(2, kSell16HeadG);
     else
         SPMV_HEAD_FILL(1, kSell16HeadG);
 #undef SPMV_HEAD_FILL
     SPMV_CHECK_LAUNCH("sell16_head_kernel");
+    return SPMV_SUCCESS;
+}
+
+// The head for int32 SELL (small matrices): the same copy of every wave's
+// first slot groups, with int32 columns (12 B per slot).
+extern "C" size_t spmv_sell_head_bytes(int64_t n_slices, int32_t C, int32_t ki)
+{
+    if (n_slices <= 0 || (ki != 1 && ki != 2) || !sell_small(C, n_slices))
+        return 0;
+    return (size_t)sell16_head_elems(n_slices, ki) * (sizeof(double) + sizeof(int32_t));
+}
+
+extern "C" int spmv_sell_head_fill(spmv_dims d, int32_t C, int32_t sigma, int32_t ki, int64_t n_slices,
+                                   const int64_t *slice_ptr, const double *val, const int32_t *col, void *head,
+                                   size_t head_bytes)
+{
+    int rc = sell_check_args(d, C, sigma, ki, n_slices, "spmv_sell_head_fill");
+    if (rc != SPMV_SUCCESS)
+        return rc;
+    const size_t need = spmv_sell_head_bytes(n_slices, C, ki);
+    if (need == 0)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_head_fill: no head (not a small-kernel matrix)");
+    if (!head || head_bytes < need || !slice_ptr || !val || !col)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_head_fill: arrays or head buffer missing");
+    SPMV_GUARD(d);
+    double *hval = (double *)head;
+    int32_t *hcol = (int32_t *)(hval + sell16_head_elems(n_slices, ki));
+    const int64_t blocks = (n_slices + kSellSmallP - 1) / kSellSmallP;
+    const hipStream_t st = (hipStream_t)d.stream;
+    if (ki == 2)
+        hipLaunchKernelGGL((sell16_head_kernel<2, kSell16HeadG, int32_t>), dim3((unsigned)blocks),
+                           dim3(kWave * kSellSmallS * kSellSmallP), 0, st, n_slices, slice_ptr, val, col, hval, hcol);
+    else
+        hipLaunchKernelGGL((sell16_head_kernel<1, kSell16HeadG, int32_t>), dim3((unsigned)blocks),
+                           dim3(kWave * kSellSmallS * kSellSmallP), 0, st, n_slices, slice_ptr, val, col, hval, hcol);
+    SPMV_CHECK_LAUNCH("sell_head_kernel");
+    return SPMV_SUCCESS;
+}
+
+// spmv_sell_run_xwin with the head (small matrices): same bits.
+extern "C" int spmv_sell_run_xwin_head(spmv_dims d, int32_t C, int32_t sigma, int32_t ki, int64_t n_slices,
+                                       const int64_t *slice_ptr, const int32_t *perm, const int32_t *col,
+                                       const double *val, const double *x, double *y, const void *win,
+                                       int32_t xcap, const void *head)
+{
+    if (!head || !sell_small(C, n_slices))
+        return spmv_sell_run_xwin(d, C, sigma, ki, n_slices, slice_ptr, perm, col, val, x, y, win, xcap);
+    int rc = sell_check_args(d, C, sigma, ki, n_slices, "spmv_sell_run_xwin_head");
+    if (rc != SPMV_SUCCESS)
+        return rc;
+    if (d.n_rows == 0 || n_slices == 0)
+        return SPMV_SUCCESS;
+    if (!win || xcap < 0 || xcap > kXwinCapWide)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_run_xwin_head: bad window arguments");
+    SPMV_GUARD(d);
+    const bool nt = stream_nt(kSellStreamNtDefault);
+    const hipStream_t st = (hipStream_t)d.stream;
+    const int2 *w = (const int2 *)win;
+    const double *hval = (const double *)head;
+    const int32_t *hcol = (const int32_t *)(hval + sell16_head_elems(n_slices, ki));
+#define SPMV_SMALLH(K, N) \
+    launch_sell_small<K, N, true, XGlobal, int32_t>(n_slices, slice_ptr, perm, col, val, XGlobal{x}, y, INT64_MAX, x, w, xcap, st, hval, hcol)
+    if (ki == 2) { if (nt) SPMV_SMALLH(2, true); else SPMV_SMALLH(2, false); }
+    else { if (nt) SPMV_SMALLH(1, true); else SPMV_SMALLH(1, false); }
+#undef SPMV_SMALLH
+    SPMV_CHECK_LAUNCH("sell_small_kernel (head)");
     return SPMV_SUCCESS;
 }
 

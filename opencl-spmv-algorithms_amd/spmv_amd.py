@@ -122,6 +122,11 @@ HIP_SYMBOLS = {
     "spmv_sell16_run": (ctypes.c_int, [Dims, _c_i32, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                        _c_i32, _vp]),
     "spmv_sell16_head_bytes": (ctypes.c_size_t, [_c_i64, _c_i32, _c_i32]),
+    "spmv_sell_head_bytes": (ctypes.c_size_t, [_c_i64, _c_i32, _c_i32]),
+    "spmv_sell_head_fill": (ctypes.c_int, [Dims, _c_i32, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, _vp,
+                                           ctypes.c_size_t]),
+    "spmv_sell_run_xwin_head": (ctypes.c_int, [Dims, _c_i32, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp,
+                                               _vp, _c_i32, _vp]),
     "spmv_sell16_head_fill": (ctypes.c_int, [Dims, _c_i32, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, _vp,
                                              ctypes.c_size_t]),
     "spmv_cmrs_run": (ctypes.c_int, [Dims, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
@@ -704,6 +709,10 @@ class DeviceMatrix:
                                          _ptr(a.get("win")), p.get("xcap", 0), p["split_T"], p["n_chunks"],
                                          _ptr(a["chunk_slice"]), _ptr(a["chunk_k0"]), _ptr(a["split_ws"]),
                                          a["split_ws"].numel())
+        elif self.fmt == "sell" and "win" in a and "head" in a:
+            rc = lib.spmv_sell_run_xwin_head(d, p["C"], p["sigma"], p["ki"], p["n_slices"], _ptr(a["slice_ptr"]),
+                                             _ptr(a["perm"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
+                                             _ptr(a["win"]), p["xcap"], _ptr(a["head"]))
         elif self.fmt == "sell" and "win" in a:
             rc = lib.spmv_sell_run_xwin(d, p["C"], p["sigma"], p["ki"], p["n_slices"], _ptr(a["slice_ptr"]),
                                         _ptr(a["perm"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
@@ -864,7 +873,8 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
               sigma: int = 1024, h: int = 8, ell_max_padding: float | None = 64.0,
               xwin: bool | None = None, xwin_rows: int = 0, split: int | None = None,
               cmrs_variant: int | None = None, hot: int | None = None,
-              csr16_max_escape: float | None = 0.5, groups: int = 0, head: bool = True) -> DeviceMatrix:
+              csr16_max_escape: float | None = 0.5, groups: int = 0, head: bool = True,
+              sell_head: bool = False) -> DeviceMatrix:
     """Build `fmt` on the host (libspmv_host.so) and upload it.  xwin (CSR,
     ELL, SELL; default on): also build the per-workgroup x windows on the
     device and run the LDS x-window kernels (same bits as without).  split
@@ -977,6 +987,15 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
             _sell_xwin(dm)
         _sell_split(dm, s["slice_ptr"], split)
         _sell_hot(dm, s["col"][: s["stored"]], hot)
+        if sell_head and xwin and dm.params.get("split_T", 0) == 0 and dm.params.get("H", 0) == 0:
+            hb = hip_lib().spmv_sell_head_bytes(s["n_slices"], C, ki)
+            if hb > 0:  # small matrix: the head copy of every wave's first slot groups
+                a = dm.arrays
+                a["head"] = torch.empty(hb, dtype=torch.uint8, device=device)
+                _check(hip_lib().spmv_sell_head_fill(dm.dims(), C, sigma, ki, s["n_slices"], _ptr(a["slice_ptr"]),
+                                                     _ptr(a["val"]), _ptr(a["col"]), _ptr(a["head"]), hb),
+                       "spmv_sell_head_fill")
+                dm.params["head_bytes"] = hb
     elif fmt == "csrg":
         # column-grouped CSR for gather-bound power-law matrices (R-MAT)
         # G = 4 measured best on the R-MAT (0.757-0.785 ms vs 0.768-0.83 at G = 8,

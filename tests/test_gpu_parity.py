@@ -898,6 +898,35 @@ def test_sell16_head_same_bits(torch_dev, ki, case):
     assert_parity(m, ys[1].cpu().numpy(), x.cpu().numpy())
 
 @pytest.mark.parametrize("ki", [1, 2])
+@pytest.mark.parametrize("case", ["cantlike", "ragged", "few_slices", "inf_x"])
+def test_sell_int32_head_same_bits(torch_dev, ki, case):
+    """The head for int32 SELL (sell_head=True, small matrices) gives the
+    bits of the x-window run without it, also for an x holding Inf."""
+    torch, dev = torch_dev
+    if case == "cantlike":
+        m = sa.gen_cantlike(2)
+    elif case == "ragged":
+        m = sa.gen_random(30_000, 20_000, 0, 150, seed=23)
+    else:
+        m = sa.gen_random(150, 400, 0, 5, seed=24)
+    xh = np.random.default_rng(19).uniform(-1, 1, m.n_cols)
+    if case == "inf_x":
+        xh[::37] = np.inf
+    x = torch.from_numpy(xh).to(dev)
+    ys = []
+    for head in (False, True):
+        dm = sa.to_device(m, "sell", dev, C=64, sigma=1024, ki=ki, sell_head=head)
+        assert ("head" in dm.arrays) == head
+        y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
+        dm.run(x, y)
+        torch.cuda.synchronize()
+        ys.append(y)
+    assert torch.equal(ys[0].view(torch.int64), ys[1].view(torch.int64))
+    if case != "inf_x":
+        assert_parity(m, ys[1].cpu().numpy(), x.cpu().numpy())
+
+
+@pytest.mark.parametrize("ki", [1, 2])
 def test_sell16_head_same_bits_nonfinite_x(torch_dev, ki):
     """The head pads a wave's unused groups with its own first group (as the
     run without a head re-reads it), so even an x holding Inf gives the same

@@ -262,7 +262,8 @@ def attach_trace(out, trace_dir):
         nbytes = rec.get("bytes", b)
         if cold:
             cm = round(float(np.median(cold)), 5)  # every figure from the rounded median (bench.py reuses it)
-            rec.update(cold_ms=cm, cold_GBs=round(nbytes / (cm * 1e-3) * 1e-9, 1),
+            rec.update(cold_ms=cm, cold_ms_mean=round(float(np.mean(cold)), 5), cold_reps=len(cold),
+                       cold_GBs=round(nbytes / (cm * 1e-3) * 1e-9, 1),
                        cold_frac=round(nbytes / (cm * 1e-3) * 1e-9 / sa.HBM_PEAK_GBS, 4),
                        cold_ms_range=[round(min(cold), 5), round(max(cold), 5)])
         if warm:

@@ -191,11 +191,7 @@ int64_t spmv_hot_columns(int64_t n_cols, int64_t nnz, const int32_t *col, int64_
         free(sel);
         return 0;
     }
-    {
-        const char *ho = getenv("SPMV_HOT_ORDER"); /* LAB: "col" keeps the table in column order */
-        if (!ho || strcmp(ho, "col") != 0)
-            qsort(sel, (size_t)n, sizeof *sel, by_count_desc);
-    }
+    qsort(sel, (size_t)n, sizeof *sel, by_count_desc);
     int32_t *rank = (int32_t *)malloc((size_t)n_cols * sizeof(int32_t));
     if (!rank) {
         free(sel);

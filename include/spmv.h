@@ -59,6 +59,18 @@ size_t spmv_coo_ws_bytes(int64_t nnz);
 int spmv_coo_run(spmv_dims d, const int32_t *row, const int32_t *col,
                  const double *val, const double *x, double *y, void *ws,
                  size_t ws_bytes);
+/* Single-pass COO (no carry pass): every workgroup also loads the entries of
+ * its last row that lie past its 1,536-entry tile and finishes that row; a
+ * row begun in an earlier tile is left to that tile.  Build once:
+ * spmv_coo_tail_build counts those entries per tile into `tails`
+ * (spmv_coo_tail_bytes bytes) and returns SPMV_OTHER_ERROR when a row runs
+ * more than 512 entries past a tile end (use spmv_coo_run).  Deterministic;
+ * rows that span tiles are summed in one pass, so y agrees with
+ * spmv_coo_run to the parity rule.  (reference kernels/Coo.cl, coo.c:194) */
+size_t spmv_coo_tail_bytes(int64_t nnz);
+int spmv_coo_tail_build(spmv_dims d, const int32_t *row, void *tails, size_t tails_bytes);
+int spmv_coo_run_tail(spmv_dims d, const int32_t *row, const int32_t *col, const double *val,
+                      const double *x, double *y, const void *tails);
 
 /* ---------------------------------------------------------------- CSR ---
  * Replaces kernel `csr(ptr,col,val,x,y,int N)` (reference kernels/Csr.cl:1)

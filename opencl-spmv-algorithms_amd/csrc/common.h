@@ -47,7 +47,12 @@ int launch_cmrs_staged(const spmv_dims &d, int32_t h, int64_t n_strips,
 void cmrs_geometry(const spmv_dims &d, int32_t h, int64_t n_strips, int *L, int *G, int64_t *blocks);
 int launch_coo_staged(const spmv_dims &d, const int32_t *row, const int32_t *col,
                       const double *val, const double *x, double *y, int32_t *carry_row,
-                      double *carry_val, const int2 *win = nullptr, int32_t xcap = 0);
+                      double *carry_val, const int2 *win = nullptr, int32_t xcap = 0,
+                      const int32_t *tails = nullptr);
+// single-pass COO: the tail plan (tails[tile], staged.hip); returns the
+// largest tail, or -1 on a launch / copy error
+int64_t coo_tail_build(const spmv_dims &d, const int32_t *row, int32_t *tails);
+int64_t coo_tail_cap();
 // LDS entries of x a staged COO tile / CMRS strip run may stage (16 KiB)
 constexpr int32_t kStagedXwinCap = 2048;
 int64_t coo_staged_tile();

@@ -118,6 +118,52 @@ extern "C" int spmv_coo_run(spmv_dims d, const int32_t *row,
     return launch_carry(st_tiles, cr, cv, y, (hipStream_t)d.stream);
 }
 
+// Single-pass COO (no carry pass): every tile also finishes its last row
+// from the entries past its end, the tail plan giving their count.  For
+// matrices whose rows run at most 512 entries past a tile end (one
+// cant-like matrix: the carry kernel was 4.3 of its 20.9 us cold).
+extern "C" size_t spmv_coo_tail_bytes(int64_t nnz)
+{
+    if (nnz <= 0)
+        return 0;
+    return (size_t)((nnz + coo_staged_tile() - 1) / coo_staged_tile()) * sizeof(int32_t);
+}
+
+extern "C" int spmv_coo_tail_build(spmv_dims d, const int32_t *row, void *tails, size_t tails_bytes)
+{
+    if (d.n_rows < 0 || d.nnz < 0 || d.n_rows > INT32_MAX)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_coo_tail_build: bad sizes");
+    if (d.nnz == 0)
+        return SPMV_SUCCESS;
+    if (!row || !tails || tails_bytes < spmv_coo_tail_bytes(d.nnz))
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_coo_tail_build: arrays or buffer missing");
+    SPMV_GUARD(d);
+    const int64_t mx = coo_tail_build(d, row, (int32_t *)tails);
+    if (mx < 0)
+        return fail_msg(SPMV_PROGRAM_ERROR, "spmv_coo_tail_build: plan kernel");
+    if (mx > coo_tail_cap())
+        return fail_msg(SPMV_OTHER_ERROR,
+                        "spmv_coo_tail_build: a row runs more than 512 entries past its tile (use spmv_coo_run)");
+    return SPMV_SUCCESS;
+}
+
+extern "C" int spmv_coo_run_tail(spmv_dims d, const int32_t *row, const int32_t *col, const double *val,
+                                 const double *x, double *y, const void *tails)
+{
+    if (d.n_rows < 0 || d.nnz < 0 || d.n_rows > INT32_MAX)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_coo_run_tail: bad sizes");
+    if (d.n_rows == 0)
+        return SPMV_SUCCESS;
+    SPMV_GUARD(d);
+    if (d.nnz == 0) {
+        hipError_t e = hipMemsetAsync(y, 0, (size_t)d.n_rows * sizeof(double), (hipStream_t)d.stream);
+        return e == hipSuccess ? SPMV_SUCCESS : fail(SPMV_PROGRAM_ERROR, "memset y", e);
+    }
+    if (!tails)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_coo_run_tail: no tail plan");
+    return launch_coo_staged(d, row, col, val, x, y, nullptr, nullptr, nullptr, 0, (const int32_t *)tails);
+}
+
 extern "C" int spmv_cmrs_run(spmv_dims d, int32_t h, int64_t n_strips,
                              const int64_t *strip_ptr,
                              const uint8_t *row_in_strip, const int32_t *col,

@@ -225,6 +225,7 @@ __global__ __launch_bounds__(kBlock) void cmrs_staged_kernel(
 
 // ------------------------------------------------------------------- COO
 constexpr int kCooRowCap = 1024;
+constexpr int kCooTailCap = 2 * kBlock;  // entries a single-pass COO tile may load past its end
 // entry pairs staged per thread by the COO kernels (tile = 2·256·kCooR entries)
 constexpr int kCooR = 3;
 
@@ -235,18 +236,24 @@ constexpr int kCooR = 3;
 // XW: the tile's x window in LDS (as cmrs_staged_kernel), bit-identical.
 // XS/NT: x accessor of the global gathers (XHot: hot-column table) and the
 // stream load policy.
-template <int L, int R, bool ACC, bool XW, bool NT = false, typename XS = XGlobal>
+// TAIL (single pass, spmv_coo_run_tail): the tile also loads the entries of
+// its last row that run past the tile end (tails[tile] of them, at most
+// 2·256, from spmv_coo_tail_build) and finishes that row itself; a row begun
+// in an earlier tile is skipped, so no carry pass runs.
+template <int L, int R, bool ACC, bool XW, bool NT = false, typename XS = XGlobal, bool TAIL = false>
 __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
     int64_t n_rows, int64_t nnz, const int32_t *__restrict__ row,
     const int32_t *__restrict__ col, const double *__restrict__ val,
     const double *__restrict__ x, double *__restrict__ y, int32_t *__restrict__ carry_row,
-    double *__restrict__ carry_val, const int2 *__restrict__ win, int32_t xcap, const XS xs)
+    double *__restrict__ carry_val, const int2 *__restrict__ win, int32_t xcap, const XS xs,
+    const int32_t *__restrict__ tails = nullptr)
 {
     constexpr int CH = 2 * kBlock * R;
     extern __shared__ double s_x[];
     constexpr int GROUPS = kBlock / L;
-    __shared__ double2 s_prod[kBlock * R];
-    __shared__ int2 s_row2[kBlock * R];
+    constexpr int TP = TAIL ? kBlock : 0;  // tail entry pairs staged behind the tile
+    __shared__ double2 s_prod[kBlock * R + TP];
+    __shared__ int2 s_row2[kBlock * R + TP];
     __shared__ int32_t s_prev;
     __shared__ int32_t s_start[kCooRowCap + 1];  // owned rows' first entries
     const int32_t *s_row = reinterpret_cast<const int32_t *>(s_row2);
@@ -256,6 +263,7 @@ __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
     const int64_t t0 = tile * CH;
     const int64_t t1 = t0 + CH < nnz ? t0 + CH : nnz;
     const int n = (int)(t1 - t0);
+    const int tail = TAIL ? tails[tile] : 0;  // uniform; > 0 only for full tiles (n even)
     if (threadIdx.x == 0)
         s_prev = t0 > 0 ? row[t0 - 1] : -1;
     const KeysRow32<NT> keys{row, s_row2};
@@ -275,10 +283,33 @@ __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
         stage_chunk<R, NT>(t0, t1, nnz, col, val, XWindow{s_x, wlo}, s_prod, keys);
     else
         stage_chunk<R, NT>(t0, t1, nnz, col, val, xs, s_prod, keys);
+    if constexpr (TAIL) {
+        if (tail > 0) {  // the last row's entries past t1, pair j at t1 + 2j
+            const int j = threadIdx.x;
+            const int64_t p = t1 + 2 * (int64_t)j;
+            if (2 * j < tail) {
+                double2 pr = {0.0, 0.0};
+                int2 kk;
+                if (2 * j + 1 < tail) {
+                    const double2 v = stream_load2<NT>(val + p);
+                    const int2 c = stream_load2<NT>(col + p);
+                    kk = stream_load2<NT>(row + p);
+                    pr = double2{v.x * xs(c.x), v.y * xs(c.y)};
+                } else {
+                    pr.x = stream_load<NT>(val + p) * xs(stream_load<NT>(col + p));
+                    kk = make_int2(stream_load<NT>(row + p), 0);
+                    kk.y = kk.x;  // never read: the row ends at 2j+1 = tail
+                }
+                s_prod[n / 2 + j] = pr;
+                s_row2[n / 2 + j] = kk;
+            }
+        }
+    }
     __syncthreads();
 
     const int32_t prev = s_prev;
     const int32_t first = s_row[0], last = s_row[n - 1];
+    const int ne = n + tail;  // staged entries: the tile, then its last row's tail
     const bool first_continues = prev == first;
     const int g = threadIdx.x / L, lane = threadIdx.x % L;
     // Row starts from the key changes (one pass over the staged keys, every
@@ -298,13 +329,14 @@ __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
                     s_start[r - r_lo] = j;
             }
             if (threadIdx.x == 0)
-                s_start[span] = n;
+                s_start[span] = ne;
             __syncthreads();
         }
     }
 
-    // carry: the first row's entries when it began in an earlier tile
-    if (g == 0) {
+    // carry: the first row's entries when it began in an earlier tile (with
+    // TAIL the earlier tile summed them from its tail)
+    if (!TAIL && g == 0) {
         double c = 0.0;
         if (first_continues) {
             const int b = heads ? s_start[0] : lower_bound_lds(s_row, 0, n, first + 1);
@@ -353,8 +385,8 @@ __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
                 a = s_start[r - r_lo];
                 b = s_start[r - r_lo + 1];
             } else {
-                a = lower_bound_lds(s_row, 0, n, (int)r);
-                b = lower_bound_lds(s_row, a, n, (int)r + 1);
+                a = lower_bound_lds(s_row, 0, ne, (int)r);
+                b = lower_bound_lds(s_row, a, ne, (int)r + 1);
             }
             for (int j = a + lane; j < b; j += L)
                 s += prod[j];
@@ -892,9 +924,54 @@ int launch_coo_staged_acc_hot(const spmv_dims &d, const int32_t *row, const int3
     return SPMV_SUCCESS;
 }
 
+// Tail plan of the single-pass COO: for every full tile, how many entries
+// of its last row lie past its end (kCooTailCap + 1 = too many).
+__global__ __launch_bounds__(kBlock) void coo_tail_kernel(int64_t nnz, int64_t tiles, int64_t CH,
+                                                          const int32_t *__restrict__ row,
+                                                          int32_t *__restrict__ tails)
+{
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= tiles)
+        return;
+    const int64_t t1 = (t + 1) * CH;
+    int32_t k = 0;
+    if (t1 < nnz) {
+        const int32_t last = row[t1 - 1];
+        while (k <= kCooTailCap && t1 + k < nnz && row[t1 + k] == last)
+            ++k;
+    }
+    tails[t] = k;
+}
+
+int64_t coo_tail_build(const spmv_dims &d, const int32_t *row, int32_t *tails)
+{
+    const int64_t CH = coo_staged_tile();
+    const int64_t tiles = (d.nnz + CH - 1) / CH;
+    if (tiles <= 0)
+        return 0;
+    const hipStream_t st = (hipStream_t)d.stream;
+    hipLaunchKernelGGL(coo_tail_kernel, dim3((unsigned)((tiles + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, d.nnz,
+                       tiles, CH, row, tails);
+    if (hipGetLastError() != hipSuccess)
+        return -1;
+    int32_t *h = (int32_t *)malloc((size_t)tiles * sizeof(int32_t));
+    if (!h)
+        return -1;
+    hipError_t e = hipMemcpyAsync(h, tails, (size_t)tiles * sizeof(int32_t), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess)
+        e = hipStreamSynchronize(st);
+    int64_t mx = 0;
+    for (int64_t t = 0; e == hipSuccess && t < tiles; ++t)
+        mx = h[t] > mx ? h[t] : mx;
+    free(h);
+    return e == hipSuccess ? mx : -1;
+}
+
+int64_t coo_tail_cap() { return kCooTailCap; }
+
 int launch_coo_staged(const spmv_dims &d, const int32_t *row, const int32_t *col,
                       const double *val, const double *x, double *y, int32_t *carry_row,
-                      double *carry_val, const int2 *win, int32_t xcap)
+                      double *carry_val, const int2 *win, int32_t xcap, const int32_t *tails)
 {
     constexpr int R = kCooR;
     const int64_t tiles = (d.nnz + coo_staged_tile() - 1) / coo_staged_tile();
@@ -910,7 +987,11 @@ int launch_coo_staged(const spmv_dims &d, const int32_t *row, const int32_t *col
     const bool nt = stream_nt(true);
 #define SPMV_COO_STAGED(LL)                                                                              \
     do {                                                                                                 \
-        if (win)                                                                                         \
+        if (tails)                                                                                       \
+            hipLaunchKernelGGL((coo_staged_kernel<LL, R, false, false, true, XGlobal, true>),            \
+                               dim3((unsigned)tiles), dim3(kBlock), 0, st, d.n_rows, d.nnz, row, col, val, \
+                               x, y, carry_row, carry_val, (const int2 *)nullptr, 0, XGlobal{x}, tails);  \
+        else if (win)                                                                                    \
             hipLaunchKernelGGL((coo_staged_kernel<LL, R, false, true>), dim3((unsigned)tiles),            \
                                dim3(kBlock), lds, st, d.n_rows, d.nnz, row, col, val, x, y, carry_row,    \
                                carry_val, win, xcap, XGlobal{x});                                        \

@@ -269,6 +269,7 @@ typedef struct {
     void *d_ws;
     size_t ws_bytes;
     void *d_win; /* x-window kernels: per-workgroup column ranges */
+    void *d_tails; /* single-pass COO: entries of each tile's last row past its end */
     int32_t xcap;
     /* SELL16 (--index16): 16-bit column offsets, head copy for small matrices */
     uint16_t *d_col16;
@@ -353,6 +354,14 @@ static int build_format(const opts_t *o, spmv_format fmt, const coo_t *m, dev_fm
             (rc = upload((void **)&f->d_val, f->h_val, (size_t)Z * 8, NULL)) ||
             (rc = spmv_malloc(&f->d_ws, f->ws_bytes)))
             return rc;
+        /* single pass (no carry kernel) when every row ends within 512
+         * entries of its tile; otherwise the carry pass stays */
+        const size_t tb = spmv_coo_tail_bytes(Z);
+        if (tb > 0 && spmv_malloc(&f->d_tails, tb) == SPMV_SUCCESS &&
+            spmv_coo_tail_build(f->d, f->d_row, f->d_tails, tb) != SPMV_SUCCESS) {
+            spmv_free(f->d_tails);
+            f->d_tails = NULL;
+        }
         return SPMV_SUCCESS;
     }
     /* every other format starts from CSR */
@@ -575,6 +584,8 @@ static int launch(void *arg)
     }
     switch (f->fmt) {
     case FMT_COO:
+        if (f->d_tails)
+            return spmv_coo_run_tail(f->d, f->d_row, f->d_col, f->d_val, f->d_x, f->d_y, f->d_tails);
         return spmv_coo_run(f->d, f->d_row, f->d_col, f->d_val, f->d_x, f->d_y, f->d_ws,
                             f->ws_bytes);
     case FMT_CSR:

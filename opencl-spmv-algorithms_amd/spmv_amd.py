@@ -80,6 +80,9 @@ class MtxInfo(ctypes.Structure):
 HIP_SYMBOLS = {
     "spmv_coo_ws_bytes": (ctypes.c_size_t, [_c_i64]),
     "spmv_coo_run": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t]),
+    "spmv_coo_tail_bytes": (ctypes.c_size_t, [_c_i64]),
+    "spmv_coo_tail_build": (ctypes.c_int, [Dims, _vp, _vp, ctypes.c_size_t]),
+    "spmv_coo_run_tail": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, _vp]),
     "spmv_csr_auto_lanes": (ctypes.c_int, [_c_i64, _c_i64]),
     "spmv_csr_run": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, ctypes.c_int]),
     "spmv_csr_run_variant": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, ctypes.c_int, ctypes.c_int]),
@@ -641,6 +644,9 @@ class DeviceMatrix:
         if self.fmt == "coo" and p.get("H", 0) > 0:
             rc = lib.spmv_coo_run_hot(d, _ptr(a["row"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y), p["H"],
                                       _ptr(a["hot"]), _ptr(a["ws"]), a["ws"].numel())
+        elif self.fmt == "coo" and "tails" in a:
+            rc = lib.spmv_coo_run_tail(d, _ptr(a["row"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
+                                       _ptr(a["tails"]))
         elif self.fmt == "coo" and "win" in a:
             rc = lib.spmv_coo_run_xwin(d, _ptr(a["row"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
                                        _ptr(a["ws"]), a["ws"].numel(), _ptr(a["win"]), p["xcap"])
@@ -874,7 +880,7 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
               xwin: bool | None = None, xwin_rows: int = 0, split: int | None = None,
               cmrs_variant: int | None = None, hot: int | None = None,
               csr16_max_escape: float | None = 0.5, groups: int = 0, head: bool = True,
-              sell_head: bool = False) -> DeviceMatrix:
+              sell_head: bool = False, coo_tail: bool | None = None) -> DeviceMatrix:
     """Build `fmt` on the host (libspmv_host.so) and upload it.  xwin (CSR,
     ELL, SELL; default on): also build the per-workgroup x windows on the
     device and run the LDS x-window kernels (same bits as without).  split
@@ -900,6 +906,17 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
         dm.stored_bytes = 16 * m.nnz
         if xwin and H == 0:
             _coo_xwin(dm)
+        elif H == 0 and coo_tail is not False and m.nnz > 0:
+            # single pass (no carry kernel) when every row runs at most 512
+            # entries past its tile; refused otherwise (R-MAT hubs)
+            tb = hip_lib().spmv_coo_tail_bytes(m.nnz)
+            tails = torch.empty(max(tb, 4), dtype=torch.uint8, device=device)
+            rc = hip_lib().spmv_coo_tail_build(dm.dims(), _ptr(dm.arrays["row"]), _ptr(tails), tails.numel())
+            if rc == SUCCESS:
+                dm.arrays["tails"] = tails
+                dm.params["single_pass"] = 1
+            elif coo_tail:
+                raise SpmvError(rc, "spmv_coo_tail_build", hip_lib().spmv_last_error().decode())
         return dm
     ptr, col, val = csr_from_coo(m)
     if fmt == "csr":

@@ -67,6 +67,7 @@ FMT_PARAMS = [
     ("cmrs", {"h": 64, "cmrs_variant": 1}),
     # COO with x windows in LDS (opt-in), CMRS with global x gathers
     ("coo", {"xwin": True}),
+    ("coo", {"coo_tail": False}),  # the carry pass (default is single pass where rows allow)
     ("cmrs", {"h": 8, "xwin": False}),
     # SELL16: 16-bit column offsets from each workgroup's window base
     ("sell16", {"C": 64, "sigma": 1024, "ki": 2}),
@@ -566,7 +567,8 @@ def test_coo_cmrs_xwin_bit_identical(torch_dev, case, fmt, kw):
         ms = [sa.read_mtx(GOLDEN / f"{n}.mtx") for n in CASES]
     for m in ms:
         a = sa.to_device(m, fmt, dev, xwin=True, **kw)
-        b = sa.to_device(m, fmt, dev, xwin=False, **kw)
+        extra = {"coo_tail": False} if fmt == "coo" else {}  # the carry path: the same tiles and sums
+        b = sa.to_device(m, fmt, dev, xwin=False, **kw, **extra)
         assert "win" in a.arrays and "win" not in b.arrays
         if case == "cantlike":
             assert a.params["xcap"] > 0
@@ -945,3 +947,67 @@ def test_sell16_head_same_bits_nonfinite_x(torch_dev, ki):
         torch.cuda.synchronize()
         ys.append(y)
     assert torch.equal(ys[0].view(torch.int64), ys[1].view(torch.int64))
+
+
+# --------------------------------------------------------------------------
+# single-pass COO (spmv_coo_run_tail): the owning tile finishes its last row
+
+@pytest.mark.parametrize("case", ["cantlike", "ragged_tails", "aligned", "fixtures", "batch"])
+def test_coo_single_pass(torch_dev, case):
+    """The single-pass COO matches the oracle (parity rule) and the carry
+    path within it; it is the default where every row ends within 512
+    entries of its tile, reproducible run to run; y pre-filled with NaN."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(41)
+    if case == "cantlike":
+        ms = [sa.gen_cantlike(0)]
+    elif case == "batch":
+        ms = [sa.gen_cantlike(1, copies=3)]
+    elif case == "ragged_tails":
+        lens = rng.integers(0, 500, 4000)
+        lens[::53] = 0
+        row = np.repeat(np.arange(lens.size, dtype=np.int32), lens)
+        ms = [sa.Coo(lens.size, 3000, row, rng.integers(0, 3000, row.size).astype(np.int32),
+                     rng.uniform(-1, 1, row.size), False, "ragged")]
+    elif case == "aligned":  # rows of 512 entries: 3 per tile, tails of 0 and 512
+        lens = np.full(300, 512)
+        row = np.repeat(np.arange(lens.size, dtype=np.int32), lens)
+        ms = [sa.Coo(lens.size, 3000, row, rng.integers(0, 3000, row.size).astype(np.int32),
+                     rng.uniform(-1, 1, row.size), False, "aligned")]
+    else:
+        ms = [sa.read_mtx(GOLDEN / f"{c}.mtx") for c in CASES]
+    for m in ms:
+        if m.n_rows == 0:
+            continue
+        a = sa.to_device(m, "coo", dev)
+        assert ("tails" in a.arrays) == (m.nnz > 0), m.label
+        b = sa.to_device(m, "coo", dev, coo_tail=False)
+        x = torch.from_numpy(rng.uniform(-1, 1, max(m.n_cols, 1))).to(dev)
+        ya = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
+        ya2, yb = torch.full_like(ya, float("nan")), torch.full_like(ya, float("nan"))
+        a.run(x, ya)
+        a.run(x, ya2)
+        b.run(x, yb)
+        torch.cuda.synchronize()
+        assert torch.equal(ya.view(torch.int64), ya2.view(torch.int64))
+        assert_parity(m, ya.cpu().numpy(), x.cpu().numpy()[: m.n_cols])
+        assert_parity(m, yb.cpu().numpy(), x.cpu().numpy()[: m.n_cols])
+
+
+def test_coo_single_pass_refuses_long_rows(torch_dev):
+    """A row running more than 512 entries past its tile keeps the carry pass."""
+    torch, dev = torch_dev
+    lens = np.concatenate([np.full(10, 100), [3000], np.full(10, 100)])
+    rng = np.random.default_rng(5)
+    row = np.repeat(np.arange(lens.size, dtype=np.int32), lens)
+    m = sa.Coo(lens.size, 2000, row, rng.integers(0, 2000, row.size).astype(np.int32), rng.uniform(-1, 1, row.size),
+               False, "long")
+    dm = sa.to_device(m, "coo", dev)
+    assert "tails" not in dm.arrays
+    with pytest.raises(sa.SpmvError):
+        sa.to_device(m, "coo", dev, coo_tail=True)
+    x = torch.from_numpy(rng.uniform(-1, 1, m.n_cols)).to(dev)
+    y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
+    dm.run(x, y)
+    torch.cuda.synchronize()
+    assert_parity(m, y.cpu().numpy(), x.cpu().numpy())

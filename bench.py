@@ -552,11 +552,21 @@ def single_cold(args, torch, dev, rank, world, dist, cdev, prof):
     y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
     dm = sa.to_device(m, args.format, dev, **fk)
     stream = torch.cuda.current_stream()
-    sa.flush_cache(stream)  # allocates the scratch outside any capture
+    # the same flush as the traced child (tools/cant_single.py): a 512 MiB
+    # scratch written by probe_flush_kernel, so both measure one cold state
+    from cant_single import FLUSH_BYTES, probe_lib
+
+    probe = probe_lib()
+    scratch = torch.empty(FLUSH_BYTES, dtype=torch.uint8, device=dev)
+
+    def flush():
+        assert probe.spmv_probe_flush(scratch.data_ptr(), FLUSH_BYTES, torch.cuda.current_stream().cuda_stream) == 0
+
+    flush()
     torch.cuda.synchronize()
 
     def step():
-        sa.flush_cache()
+        flush()
         dm.run(x, y)
 
     def spans(fn, k):
@@ -588,7 +598,7 @@ def single_cold(args, torch, dev, rank, world, dist, cdev, prof):
     torch.cuda.synchronize()
     K = args.steps
     wall, span_both = spans(step, K)
-    _, span_flush = spans(lambda: sa.flush_cache(), K)
+    _, span_flush = spans(flush, K)
     inproc = max((span_both - span_flush) / K, 1e-6)
     bad, first = sa.check(m, xh, y.cpu().numpy())
     all_ok(dist, cdev, torch, bad == 0, f"cant-like single matrix, row {first}", rank)

@@ -211,8 +211,17 @@ __global__ __launch_bounds__(kBlock) void cmrs_staged_kernel(
         const int64_t lo = sb > cb ? sb : cb;
         const int64_t hi = se < ce ? se : ce;
         if (lo < hi) {  // this strip has entries in the chunk: find the row
-            const int a = lower_bound_lds(s_key, (int)(lo - cb), (int)(hi - cb), key);
-            const int b = lower_bound_lds(s_key, a, (int)(hi - cb), key + 1);
+            // the row's two bounds searched at once by lanes 0 and 1 of its
+            // group (one dependent LDS chain instead of two; the same a, b)
+            int a, b;
+            if constexpr (L >= 2) {
+                const int f = lower_bound_lds(s_key, (int)(lo - cb), (int)(hi - cb), key + (lane & 1));
+                a = __shfl(f, 0, L);
+                b = __shfl(f, 1, L);
+            } else {
+                a = lower_bound_lds(s_key, (int)(lo - cb), (int)(hi - cb), key);
+                b = lower_bound_lds(s_key, a, (int)(hi - cb), key + 1);
+            }
             for (int j = a + lane; j < b; j += L)
                 acc += prod[j];
         }

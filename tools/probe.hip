@@ -72,6 +72,44 @@ __global__ __launch_bounds__(kBlock) void probe_csr_stream_kernel(const v2f64 *_
         out[blockIdx.x] = s;
 }
 
+// Chained CSR-shaped stream (lab): each workgroup reads K chunks of 3 pairs
+// per lane (K·1,536 entries of val + col, non-temporal); DEP: chunk k+1's
+// addresses depend on chunk k's data (one dependent round trip per chunk,
+// as the staged kernels' chunk loop), else all K chunks are issued at once.
+template <int K, bool DEP>
+__global__ __launch_bounds__(kBlock) void probe_chain_kernel(const v2f64 *__restrict__ val,
+                                                             const int2 *__restrict__ col, int64_t npairs,
+                                                             double *__restrict__ out)
+{
+    typedef int v2i32 __attribute__((ext_vector_type(2)));
+    const int64_t base = (int64_t)blockIdx.x * kBlock * 3 * K + threadIdx.x;
+    double s = 0.0;
+    int64_t bump = 0;
+    v2f64 v[3 * K];
+    v2i32 c[3 * K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+            const int64_t i = base + (int64_t)(3 * k + u) * kBlock + bump;
+            const int64_t q = i < npairs ? i : npairs - 1;
+            v[3 * k + u] = __builtin_nontemporal_load(val + q);
+            c[3 * k + u] = __builtin_nontemporal_load(reinterpret_cast<const v2i32 *>(col) + q);
+        }
+        if (DEP) {
+#pragma unroll
+            for (int u = 0; u < 3; ++u)
+                s += v[3 * k + u].x + (double)c[3 * k + u].x;
+            bump = s == 1.2345e-300 ? 1 : 0;  // never 1: a data dependency only
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < 3 * K; ++u)
+        s += v[u].y + (double)c[u].y;
+    if (s == 1.2345e-300)
+        out[blockIdx.x] = s;
+}
+
 __global__ __launch_bounds__(kBlock) void probe_flush_kernel(uint4 *__restrict__ p, int64_t n16, uint32_t tick)
 {
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n16; i += (int64_t)gridDim.x * kBlock)
@@ -125,6 +163,20 @@ int spmv_probe_csr_stream(const void *val, const void *col, int64_t npairs, int 
                                   (hipStream_t)stream, (const v2f64 *)val, (const int2 *)col, npairs, out)
         if (R == 10) PCS(0); else if (R == 11) PCS(1); else if (R == 12) PCS(2); else PCS(3);
 #undef PCS
+        return (int)hipGetLastError();
+    }
+    if (R >= 20 && R <= 23) {  // lab: 20/21 = 3 chunks at once / chained; 22/23 = 1 chunk (R = 3) same grid shape
+        const int K = R <= 21 ? 3 : 1;
+        const int64_t bk = (npairs + kBlock * 3 * K - 1) / (kBlock * 3 * K);
+        if (R == 20)
+            hipLaunchKernelGGL((probe_chain_kernel<3, false>), dim3((unsigned)bk), dim3(kBlock), 0, (hipStream_t)stream,
+                               (const v2f64 *)val, (const int2 *)col, npairs, out);
+        else if (R == 21)
+            hipLaunchKernelGGL((probe_chain_kernel<3, true>), dim3((unsigned)bk), dim3(kBlock), 0, (hipStream_t)stream,
+                               (const v2f64 *)val, (const int2 *)col, npairs, out);
+        else
+            hipLaunchKernelGGL((probe_chain_kernel<1, false>), dim3((unsigned)bk), dim3(kBlock), 0, (hipStream_t)stream,
+                               (const v2f64 *)val, (const int2 *)col, npairs, out);
         return (int)hipGetLastError();
     }
     const int r = R >= 8 ? 8 : R >= 3 ? 3 : 1;

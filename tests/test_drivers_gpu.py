@@ -143,3 +143,16 @@ def test_sigma_c_index16():
     assert "\nresult is ok\n" in "\n" + r.stdout
     r = run("csr", "--gen", "cantlike", "--index16")
     assert r.returncode == 4
+
+
+def test_coo_single_pass_flag():
+    """./bin/coo --single-pass: the carry-free COO where rows allow (the
+    cant-like matrix), the carry pass where one row is too long; both checked."""
+    r = run("coo", "--gen", "cantlike", "--reps", "5", "--warmup", "1", "--strict", "--single-pass")
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "COO single pass: no carry kernel" in r.stdout
+    assert "\nresult is ok\n" in "\n" + r.stdout
+    r = run("coo", "--matrix", str(GOLDEN / "long_rows.mtx"), "--reps", "2", "--warmup", "1", "--strict",
+            "--single-pass")
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "COO single pass: refused" in r.stdout

@@ -67,7 +67,6 @@ FMT_PARAMS = [
     ("cmrs", {"h": 64, "cmrs_variant": 1}),
     # COO with x windows in LDS (opt-in), CMRS with global x gathers
     ("coo", {"xwin": True}),
-    ("coo", {"coo_tail": False}),  # the carry pass (default is single pass where rows allow)
     ("cmrs", {"h": 8, "xwin": False}),
     # SELL16: 16-bit column offsets from each workgroup's window base
     ("sell16", {"C": 64, "sigma": 1024, "ki": 2}),
@@ -567,8 +566,7 @@ def test_coo_cmrs_xwin_bit_identical(torch_dev, case, fmt, kw):
         ms = [sa.read_mtx(GOLDEN / f"{n}.mtx") for n in CASES]
     for m in ms:
         a = sa.to_device(m, fmt, dev, xwin=True, **kw)
-        extra = {"coo_tail": False} if fmt == "coo" else {}  # the carry path: the same tiles and sums
-        b = sa.to_device(m, fmt, dev, xwin=False, **kw, **extra)
+        b = sa.to_device(m, fmt, dev, xwin=False, **kw)
         assert "win" in a.arrays and "win" not in b.arrays
         if case == "cantlike":
             assert a.params["xcap"] > 0
@@ -954,9 +952,10 @@ def test_sell16_head_same_bits_nonfinite_x(torch_dev, ki):
 
 @pytest.mark.parametrize("case", ["cantlike", "ragged_tails", "aligned", "fixtures", "batch"])
 def test_coo_single_pass(torch_dev, case):
-    """The single-pass COO matches the oracle (parity rule) and the carry
-    path within it; it is the default where every row ends within 512
-    entries of its tile, reproducible run to run; y pre-filled with NaN."""
+    """The single-pass COO (coo_tail=True, opt-in) matches the oracle
+    (parity rule) and the carry path within it wherever every row ends
+    within 512 entries of its tile, reproducible run to run; y pre-filled
+    with NaN."""
     torch, dev = torch_dev
     rng = np.random.default_rng(41)
     if case == "cantlike":
@@ -979,9 +978,13 @@ def test_coo_single_pass(torch_dev, case):
     for m in ms:
         if m.n_rows == 0:
             continue
-        a = sa.to_device(m, "coo", dev)
-        assert ("tails" in a.arrays) == (m.nnz > 0), m.label
-        b = sa.to_device(m, "coo", dev, coo_tail=False)
+        longest = int(np.bincount(m.row, minlength=m.n_rows).max()) if m.nnz else 0
+        fits = 0 < longest <= 512  # no row can run more than 512 entries past a tile
+        a = sa.to_device(m, "coo", dev, coo_tail=fits)
+        if fits:
+            assert "tails" in a.arrays, m.label
+        b = sa.to_device(m, "coo", dev)  # default: the carry pass
+        assert "tails" not in b.arrays
         x = torch.from_numpy(rng.uniform(-1, 1, max(m.n_cols, 1))).to(dev)
         ya = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
         ya2, yb = torch.full_like(ya, float("nan")), torch.full_like(ya, float("nan"))
@@ -995,7 +998,8 @@ def test_coo_single_pass(torch_dev, case):
 
 
 def test_coo_single_pass_refuses_long_rows(torch_dev):
-    """A row running more than 512 entries past its tile keeps the carry pass."""
+    """A row running more than 512 entries past its tile refuses the single
+    pass (coo_tail=True raises); the default carry pass runs it."""
     torch, dev = torch_dev
     lens = np.concatenate([np.full(10, 100), [3000], np.full(10, 100)])
     rng = np.random.default_rng(5)

@@ -777,7 +777,7 @@ static void launch_csr_xwin(const spmv_dims &d, const int64_t *row_ptr, const Co
     int mode = csr_xwin_mode(d.n_rows, d.nnz, gpw * RPB, R);
     // a very tall window's offsets would not fit beside the x range in the
     // 64 KiB of dynamic LDS: MODE 0 stages them per row group instead
-    if (mode == 3 && csr_xwin_lds(mode, xcap, gpw, RPB) + sizeof(double2) * kBlock * R > 64 * 1024)
+    if (mode == 3 && csr_xwin_lds(mode, xcap, gpw, RPB) + sizeof(double2) * kBlock * R * 2 > 64 * 1024)
         mode = 0;
     const size_t lds = csr_xwin_lds(mode, xcap, gpw, RPB);
     if (n_win > INT32_MAX)
@@ -800,13 +800,6 @@ static void launch_xwin_l(const spmv_dims &d, const int64_t *row_ptr, MakeCols m
 {
     const bool nt = stream_nt(kCsrXwinNtDefault);
     const bool r4 = csr_stage_rounds(d.n_rows, d.nnz, L) == 4;  // R = 3 or 4 (the rule)
-    if constexpr (L == 4) {  // LAB: chunk size override
-        const int lab_r = getenv("SPMV_LAB_CSR_R") ? atoi(getenv("SPMV_LAB_CSR_R")) : 0;
-        if (nt && lab_r == 5) { launch_csr_xwin<L, 5, true>(d, row_ptr, mk.template get<true>(), val, x, y, w, xcap, gpw); return; }
-        if (nt && lab_r == 6) { launch_csr_xwin<L, 6, true>(d, row_ptr, mk.template get<true>(), val, x, y, w, xcap, gpw); return; }
-        if (nt && lab_r == 8) { launch_csr_xwin<L, 8, true>(d, row_ptr, mk.template get<true>(), val, x, y, w, xcap, gpw); return; }
-        if (nt && lab_r == 9) { launch_csr_xwin<L, 9, true>(d, row_ptr, mk.template get<true>(), val, x, y, w, xcap, gpw); return; }
-    }
     if (nt && r4)
         launch_csr_xwin<L, 4, true>(d, row_ptr, mk.template get<true>(), val, x, y, w, xcap, gpw);
     else if (nt)

@@ -64,7 +64,7 @@ int spmv_coo_run(spmv_dims d, const int32_t *row, const int32_t *col,
  * row begun in an earlier tile is left to that tile.  Build once:
  * spmv_coo_tail_build counts those entries per tile into `tails`
  * (spmv_coo_tail_bytes bytes) and returns SPMV_OTHER_ERROR when a row runs
- * more than 512 entries past a tile end (use spmv_coo_run).  Deterministic;
+ * more than 80 entries past a tile end (use spmv_coo_run).  Deterministic;
  * rows that span tiles are summed in one pass, so y agrees with
  * spmv_coo_run to the parity rule.  (reference kernels/Coo.cl, coo.c:194) */
 size_t spmv_coo_tail_bytes(int64_t nnz);

@@ -120,7 +120,7 @@ extern "C" int spmv_coo_run(spmv_dims d, const int32_t *row,
 
 // Single-pass COO (no carry pass): every tile also finishes its last row
 // from the entries past its end, the tail plan giving their count.  For
-// matrices whose rows run at most 512 entries past a tile end (one
+// matrices whose rows run at most 80 entries past a tile end (one
 // cant-like matrix: the carry kernel was 4.3 of its 20.9 us cold).
 extern "C" size_t spmv_coo_tail_bytes(int64_t nnz)
 {
@@ -143,7 +143,7 @@ extern "C" int spmv_coo_tail_build(spmv_dims d, const int32_t *row, void *tails,
         return fail_msg(SPMV_PROGRAM_ERROR, "spmv_coo_tail_build: plan kernel");
     if (mx > coo_tail_cap())
         return fail_msg(SPMV_OTHER_ERROR,
-                        "spmv_coo_tail_build: a row runs more than 512 entries past its tile (use spmv_coo_run)");
+                        "spmv_coo_tail_build: a row runs more than 80 entries past its tile (use spmv_coo_run)");
     return SPMV_SUCCESS;
 }
 

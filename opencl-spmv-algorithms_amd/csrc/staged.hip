@@ -198,7 +198,9 @@ __global__ __launch_bounds__(kBlock) void cmrs_staged_kernel(
     // csr.hip kChunkAlign); the previous strip's entries are never summed.
     // (A software-pipelined chunk loop, the next chunk's loads issued before
     // this chunk's barrier, measured 0.3227 vs 0.2896 ms: 78 instead of 66
-    // VGPRs; profiles/round2/ab_cmrs_pipe.log.)
+    // VGPRs; profiles/round2/ab_cmrs_pipe.log.  On ONE cant-like matrix, with
+    // the first chunk also issued before the x window, 18.9 vs 16.4 us cold:
+    // profiles/round4/ab_csr_single.md J.)
     const int64_t c0 = s_sp[0] & ~(int64_t)31;
     for (int64_t cb = c0; cb < blk_end; cb += CH) {
         const int64_t ce = cb + CH < blk_end ? cb + CH : blk_end;
@@ -234,7 +236,17 @@ __global__ __launch_bounds__(kBlock) void cmrs_staged_kernel(
 
 // ------------------------------------------------------------------- COO
 constexpr int kCooRowCap = 1024;
-constexpr int kCooTailCap = 2 * kBlock;  // entries a single-pass COO tile may load past its end
+// Rows of row-start table per tile for mean rows >= 12 (a 1,536-entry tile
+// spans ~128 rows or fewer): the table shrinks from 4 to 1 KiB, so 8 tiles fit
+// a CU's LDS instead of 7 (the single-pass form: 8 instead of 5); a tile
+// spanning more rows keeps the binary searches (same bits).
+constexpr int kCooRowCapShort = 250;
+// entries a single-pass COO tile may load past its end (pairs staged in LDS
+// behind the tile: 40; the cant-like matrix's rows reach 81 entries, so its
+// tails stay within 80).  With 256 pairs (512 entries) the tail's LDS left
+// 5 tiles per CU: 21.8 us cold on one cant-like matrix, against 18.0 us now
+// and 20.6 us for the carry pass
+constexpr int kCooTailCap = 80;
 // entry pairs staged per thread by the COO kernels (tile = 2·256·kCooR entries)
 constexpr int kCooR = 3;
 
@@ -247,9 +259,10 @@ constexpr int kCooR = 3;
 // stream load policy.
 // TAIL (single pass, spmv_coo_run_tail): the tile also loads the entries of
 // its last row that run past the tile end (tails[tile] of them, at most
-// 2·256, from spmv_coo_tail_build) and finishes that row itself; a row begun
+// kCooTailCap, from spmv_coo_tail_build) and finishes that row itself; a row begun
 // in an earlier tile is skipped, so no carry pass runs.
-template <int L, int R, bool ACC, bool XW, bool NT = false, typename XS = XGlobal, bool TAIL = false>
+template <int L, int R, bool ACC, bool XW, bool NT = false, typename XS = XGlobal, bool TAIL = false,
+          int RC = kCooRowCap>
 __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
     int64_t n_rows, int64_t nnz, const int32_t *__restrict__ row,
     const int32_t *__restrict__ col, const double *__restrict__ val,
@@ -260,11 +273,11 @@ __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
     constexpr int CH = 2 * kBlock * R;
     extern __shared__ double s_x[];
     constexpr int GROUPS = kBlock / L;
-    constexpr int TP = TAIL ? kBlock : 0;  // tail entry pairs staged behind the tile
+    constexpr int TP = TAIL ? (kCooTailCap + 1) / 2 : 0;  // tail entry pairs staged behind the tile
     __shared__ double2 s_prod[kBlock * R + TP];
     __shared__ int2 s_row2[kBlock * R + TP];
     __shared__ int32_t s_prev;
-    __shared__ int32_t s_start[kCooRowCap + 1];  // owned rows' first entries
+    __shared__ int32_t s_start[RC + 1];  // owned rows' first entries
     const int32_t *s_row = reinterpret_cast<const int32_t *>(s_row2);
     const double *prod = reinterpret_cast<const double *>(s_prod);
 
@@ -288,31 +301,37 @@ __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
             __syncthreads();
         }
     }
-    if (staged)
-        stage_chunk<R, NT>(t0, t1, nnz, col, val, XWindow{s_x, wlo}, s_prod, keys);
-    else
-        stage_chunk<R, NT>(t0, t1, nnz, col, val, xs, s_prod, keys);
     if constexpr (TAIL) {
-        if (tail > 0) {  // the last row's entries past t1, pair j at t1 + 2j
-            const int j = threadIdx.x;
-            const int64_t p = t1 + 2 * (int64_t)j;
-            if (2 * j < tail) {
-                double2 pr = {0.0, 0.0};
-                int2 kk;
-                if (2 * j + 1 < tail) {
-                    const double2 v = stream_load2<NT>(val + p);
-                    const int2 c = stream_load2<NT>(col + p);
-                    kk = stream_load2<NT>(row + p);
-                    pr = double2{v.x * xs(c.x), v.y * xs(c.y)};
-                } else {
-                    pr.x = stream_load<NT>(val + p) * xs(stream_load<NT>(col + p));
-                    kk = make_int2(stream_load<NT>(row + p), 0);
-                    kk.y = kk.x;  // never read: the row ends at 2j+1 = tail
-                }
-                s_prod[n / 2 + j] = pr;
-                s_row2[n / 2 + j] = kk;
-            }
+        // the tile's pairs and the last row's entries past t1 (pair j at
+        // t1 + 2j) in flight together, then the products of both
+        static_assert(!XW, "the single-pass COO gathers x through xs");
+        StageRegs<R, NT, double, KeysRow32<NT>> st;
+        st.issue(t0, t1, nnz, col, val, keys);
+        const int j = threadIdx.x;
+        const int64_t p = t1 + 2 * (int64_t)j;
+        const bool tpair = 2 * j + 1 < tail, tone = 2 * j + 1 == tail;  // tail > 0 only for full tiles
+        static_assert(TP <= kBlock, "one tail pair per thread");
+        double2 tv = {0.0, 0.0};
+        int2 tc = {0, 0}, tk = {0, 0};
+        if (tpair) {
+            tv = stream_load2<NT>(val + p);
+            tc = stream_load2<NT>(col + p);
+            tk = stream_load2<NT>(row + p);
+        } else if (tone) {
+            tv.x = stream_load<NT>(val + p);
+            tc.x = stream_load<NT>(col + p);
+            tk.x = stream_load<NT>(row + p);
+            tk.y = tk.x;  // never read: the row ends at 2j+1 = tail
         }
+        st.commit(t0, t1, nnz, col, val, xs, s_prod, keys);
+        if (tpair || tone) {
+            s_prod[n / 2 + j] = tpair ? double2{tv.x * xs(tc.x), tv.y * xs(tc.y)} : double2{tv.x * xs(tc.x), 0.0};
+            s_row2[n / 2 + j] = tk;
+        }
+    } else if (staged) {
+        stage_chunk<R, NT>(t0, t1, nnz, col, val, XWindow{s_x, wlo}, s_prod, keys);
+    } else {
+        stage_chunk<R, NT>(t0, t1, nnz, col, val, xs, s_prod, keys);
     }
     __syncthreads();
 
@@ -323,13 +342,13 @@ __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
     const int g = threadIdx.x / L, lane = threadIdx.x % L;
     // Row starts from the key changes (one pass over the staged keys, every
     // row of (prev, last] written by exactly one thread) instead of two
-    // binary searches per row; a tile spanning more than kCooRowCap rows
+    // binary searches per row; a tile spanning more than RC rows
     // (long runs of empty rows) keeps the searches.
     const int64_t r_lo = (int64_t)prev + 1;
     const int64_t span = (int64_t)last - r_lo + 1;  // rows (prev, last]
     bool heads = false;  // uniform per workgroup
     {
-        heads = span >= 0 && span <= kCooRowCap;
+        heads = span >= 0 && span <= RC;
         if (heads) {
             for (int j = threadIdx.x; j < n; j += kBlock) {
                 const int32_t k = s_row[j];
@@ -997,7 +1016,7 @@ int launch_coo_staged(const spmv_dims &d, const int32_t *row, const int32_t *col
 #define SPMV_COO_STAGED(LL)                                                                              \
     do {                                                                                                 \
         if (tails)                                                                                       \
-            hipLaunchKernelGGL((coo_staged_kernel<LL, R, false, false, true, XGlobal, true>),            \
+            hipLaunchKernelGGL((coo_staged_kernel<LL, R, false, false, true, XGlobal, true, RC>),        \
                                dim3((unsigned)tiles), dim3(kBlock), 0, st, d.n_rows, d.nnz, row, col, val, \
                                x, y, carry_row, carry_val, (const int2 *)nullptr, 0, XGlobal{x}, tails);  \
         else if (win)                                                                                    \
@@ -1005,7 +1024,8 @@ int launch_coo_staged(const spmv_dims &d, const int32_t *row, const int32_t *col
                                dim3(kBlock), lds, st, d.n_rows, d.nnz, row, col, val, x, y, carry_row,    \
                                carry_val, win, xcap, XGlobal{x});                                        \
         else if (nt)                                                                                     \
-            hipLaunchKernelGGL((coo_staged_kernel<LL, R, false, false, true>), dim3((unsigned)tiles),     \
+            hipLaunchKernelGGL((coo_staged_kernel<LL, R, false, false, true, XGlobal, false, RC>),       \
+                               dim3((unsigned)tiles),                                                    \
                                dim3(kBlock), 0, st, d.n_rows, d.nnz, row, col, val, x, y, carry_row,      \
                                carry_val, (const int2 *)nullptr, 0, XGlobal{x});                         \
         else                                                                                             \
@@ -1013,12 +1033,16 @@ int launch_coo_staged(const spmv_dims &d, const int32_t *row, const int32_t *col
                                dim3(kBlock), 0, st, d.n_rows, d.nnz, row, col, val, x, y, carry_row,      \
                                carry_val, (const int2 *)nullptr, 0, XGlobal{x});                         \
     } while (0)
-    if (mean >= 48.0)
+    if (mean >= 48.0) {
+        constexpr int RC = kCooRowCapShort;
         SPMV_COO_STAGED(8);
-    else if (mean >= 12.0)
+    } else if (mean >= 12.0) {
+        constexpr int RC = kCooRowCapShort;
         SPMV_COO_STAGED(4);
-    else
+    } else {
+        constexpr int RC = kCooRowCap;
         SPMV_COO_STAGED(2);
+    }
 #undef SPMV_COO_STAGED
     SPMV_CHECK_LAUNCH("coo_staged_kernel");
     return SPMV_SUCCESS;

@@ -880,7 +880,7 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
               xwin: bool | None = None, xwin_rows: int = 0, split: int | None = None,
               cmrs_variant: int | None = None, hot: int | None = None,
               csr16_max_escape: float | None = 0.5, groups: int = 0, head: bool = True,
-              sell_head: bool = False, coo_tail: bool = False) -> DeviceMatrix:
+              sell_head: bool = False, coo_tail: bool | None = None) -> DeviceMatrix:
     """Build `fmt` on the host (libspmv_host.so) and upload it.  xwin (CSR,
     ELL, SELL; default on): also build the per-workgroup x windows on the
     device and run the LDS x-window kernels (same bits as without).  split
@@ -906,17 +906,17 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
         dm.stored_bytes = 16 * m.nnz
         if xwin and H == 0:
             _coo_xwin(dm)
-        elif H == 0 and coo_tail and m.nnz > 0:
-            # coo_tail: single pass (no carry kernel) when every row runs at
-            # most 512 entries past its tile; refused otherwise (R-MAT hubs).
-            # Opt-in: 21.8 vs 20.8 us cold for the carry pass (cant-like)
+        elif H == 0 and coo_tail is not False and m.nnz > 0:
+            # single pass (no carry kernel) when every row runs at most 80
+            # entries past its tile (None: where the plan allows; True: or
+            # raise); cant-like cold 18.1 vs 20.6 us for the carry pass
             tb = hip_lib().spmv_coo_tail_bytes(m.nnz)
             tails = torch.empty(max(tb, 4), dtype=torch.uint8, device=device)
             rc = hip_lib().spmv_coo_tail_build(dm.dims(), _ptr(dm.arrays["row"]), _ptr(tails), tails.numel())
             if rc == SUCCESS:
                 dm.arrays["tails"] = tails
                 dm.params["single_pass"] = 1
-            else:
+            elif coo_tail:
                 raise SpmvError(rc, "spmv_coo_tail_build", hip_lib().spmv_last_error().decode())
         return dm
     ptr, col, val = csr_from_coo(m)

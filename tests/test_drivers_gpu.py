@@ -146,13 +146,15 @@ def test_sigma_c_index16():
 
 
 def test_coo_single_pass_flag():
-    """./bin/coo --single-pass: the carry-free COO where rows allow (the
-    cant-like matrix), the carry pass where one row is too long; both checked."""
-    r = run("coo", "--gen", "cantlike", "--reps", "5", "--warmup", "1", "--strict", "--single-pass")
+    """./bin/coo: the carry-free COO where rows allow (the cant-like matrix),
+    the carry pass where one row is too long or with --carry-pass; all checked."""
+    r = run("coo", "--gen", "cantlike", "--reps", "5", "--warmup", "1", "--strict")
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "COO single pass: no carry kernel" in r.stdout
+    assert "COO single pass: no carry kernel" in r.stderr
     assert "\nresult is ok\n" in "\n" + r.stdout
-    r = run("coo", "--matrix", str(GOLDEN / "long_rows.mtx"), "--reps", "2", "--warmup", "1", "--strict",
-            "--single-pass")
+    r = run("coo", "--gen", "cantlike", "--reps", "5", "--warmup", "1", "--strict", "--carry-pass")
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "COO single pass: refused" in r.stdout
+    assert "COO single pass: off" in r.stderr and "\nresult is ok\n" in "\n" + r.stdout
+    r = run("coo", "--matrix", str(GOLDEN / "long_rows.mtx"), "--reps", "2", "--warmup", "1", "--strict")
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "COO single pass: refused" in r.stderr

@@ -67,6 +67,7 @@ FMT_PARAMS = [
     ("cmrs", {"h": 64, "cmrs_variant": 1}),
     # COO with x windows in LDS (opt-in), CMRS with global x gathers
     ("coo", {"xwin": True}),
+    ("coo", {"coo_tail": False}),  # the carry pass (default: single pass where rows allow)
     ("cmrs", {"h": 8, "xwin": False}),
     # SELL16: 16-bit column offsets from each workgroup's window base
     ("sell16", {"C": 64, "sigma": 1024, "ki": 2}),
@@ -566,7 +567,8 @@ def test_coo_cmrs_xwin_bit_identical(torch_dev, case, fmt, kw):
         ms = [sa.read_mtx(GOLDEN / f"{n}.mtx") for n in CASES]
     for m in ms:
         a = sa.to_device(m, fmt, dev, xwin=True, **kw)
-        b = sa.to_device(m, fmt, dev, xwin=False, **kw)
+        extra = {"coo_tail": False} if fmt == "coo" else {}  # the carry path: the same tiles and sums
+        b = sa.to_device(m, fmt, dev, xwin=False, **kw, **extra)
         assert "win" in a.arrays and "win" not in b.arrays
         if case == "cantlike":
             assert a.params["xcap"] > 0
@@ -950,11 +952,14 @@ def test_sell16_head_same_bits_nonfinite_x(torch_dev, ki):
 # --------------------------------------------------------------------------
 # single-pass COO (spmv_coo_run_tail): the owning tile finishes its last row
 
+COO_TAIL_CAP = 80  # csrc/staged.hip kCooTailCap
+
+
 @pytest.mark.parametrize("case", ["cantlike", "ragged_tails", "aligned", "fixtures", "batch"])
 def test_coo_single_pass(torch_dev, case):
-    """The single-pass COO (coo_tail=True, opt-in) matches the oracle
+    """The single-pass COO (the default where the plan allows) matches the oracle
     (parity rule) and the carry path within it wherever every row ends
-    within 512 entries of its tile, reproducible run to run; y pre-filled
+    within COO_TAIL_CAP entries of its tile, reproducible run to run; y pre-filled
     with NaN."""
     torch, dev = torch_dev
     rng = np.random.default_rng(41)
@@ -963,13 +968,13 @@ def test_coo_single_pass(torch_dev, case):
     elif case == "batch":
         ms = [sa.gen_cantlike(1, copies=3)]
     elif case == "ragged_tails":
-        lens = rng.integers(0, 500, 4000)
+        lens = rng.integers(0, COO_TAIL_CAP + 1, 4000)
         lens[::53] = 0
         row = np.repeat(np.arange(lens.size, dtype=np.int32), lens)
         ms = [sa.Coo(lens.size, 3000, row, rng.integers(0, 3000, row.size).astype(np.int32),
                      rng.uniform(-1, 1, row.size), False, "ragged")]
-    elif case == "aligned":  # rows of 512 entries: 3 per tile, tails of 0 and 512
-        lens = np.full(300, 512)
+    elif case == "aligned":  # rows of 82 entries: tails up to exactly the cap (80, tile 26)
+        lens = np.full(600, COO_TAIL_CAP + 2)
         row = np.repeat(np.arange(lens.size, dtype=np.int32), lens)
         ms = [sa.Coo(lens.size, 3000, row, rng.integers(0, 3000, row.size).astype(np.int32),
                      rng.uniform(-1, 1, row.size), False, "aligned")]
@@ -979,11 +984,13 @@ def test_coo_single_pass(torch_dev, case):
         if m.n_rows == 0:
             continue
         longest = int(np.bincount(m.row, minlength=m.n_rows).max()) if m.nnz else 0
-        fits = 0 < longest <= 512  # no row can run more than 512 entries past a tile
-        a = sa.to_device(m, "coo", dev, coo_tail=fits)
+        # a row of k entries runs at most k - 1 past a tile end (rows of 82:
+        # tile ends are even, so a tail of 81 never occurs)
+        fits = 0 < longest <= COO_TAIL_CAP + 1 or case == "aligned"
+        a = sa.to_device(m, "coo", dev)  # default: single pass where the plan allows
         if fits:
             assert "tails" in a.arrays, m.label
-        b = sa.to_device(m, "coo", dev)  # default: the carry pass
+        b = sa.to_device(m, "coo", dev, coo_tail=False)  # the carry pass
         assert "tails" not in b.arrays
         x = torch.from_numpy(rng.uniform(-1, 1, max(m.n_cols, 1))).to(dev)
         ya = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
@@ -998,8 +1005,8 @@ def test_coo_single_pass(torch_dev, case):
 
 
 def test_coo_single_pass_refuses_long_rows(torch_dev):
-    """A row running more than 512 entries past its tile refuses the single
-    pass (coo_tail=True raises); the default carry pass runs it."""
+    """A row running more than COO_TAIL_CAP entries past its tile refuses the single
+    pass (coo_tail=True raises); the default falls back to the carry pass."""
     torch, dev = torch_dev
     lens = np.concatenate([np.full(10, 100), [3000], np.full(10, 100)])
     rng = np.random.default_rng(5)

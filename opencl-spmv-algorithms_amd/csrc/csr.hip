@@ -171,34 +171,41 @@ struct Col16 {
 };
 
 // One lane's share of a row's products in the staged chunk: entries
-// [lo, hi) of the chunk (chunk-relative, < 2^31), every L-th from lo+lane,
-// two partial sums so consecutive LDS reads do not wait on each other.
-// Eight products are read per step before the first add (one LDS round
-// trip per 8·L entries instead of per 2·L); the adds keep the a0/a1
-// alternation, so the sums are the same bits as the two-at-a-time loop.
+// [lo, hi) of the chunk (chunk-relative, < 2^31).  The products are read as
+// 16-byte pairs (half the LDS instructions of single reads): lane k takes
+// pairs plo+k, plo+k+L, ... into two partial sums (a0 the first product of
+// each pair, a1 the second), four pairs read per step before the first add;
+// an odd first entry goes to lane 0's a0, an odd last entry to lane L-1's a1.
 template <int L>
 __device__ __forceinline__ double slice_sum(const double *prod, int64_t lo64, int64_t hi64, int lane)
 {
     const int lo = (int)lo64, hi = (int)hi64;
     double a0 = 0.0, a1 = 0.0;
-    int j = lo + lane;
-    for (; j + 7 * L < hi; j += 8 * L) {
-        double p[8];
+    if (lo >= hi)
+        return 0.0;
+    if ((lo & 1) && lane == 0)
+        a0 = prod[lo];
+    if ((hi & 1) && lane == L - 1)
+        a1 = prod[hi - 1];
+    const double2 *p2 = reinterpret_cast<const double2 *>(prod);
+    const int pe = hi >> 1;  // whole pairs [(lo+1)/2, hi/2)
+    int k = ((lo + 1) >> 1) + lane;
+    for (; k + 3 * L < pe; k += 4 * L) {
+        double2 v[4];
 #pragma unroll
-        for (int k = 0; k < 8; ++k)
-            p[k] = prod[j + k * L];
+        for (int u = 0; u < 4; ++u)
+            v[u] = p2[k + u * L];
 #pragma unroll
-        for (int k = 0; k < 8; k += 2) {
-            a0 += p[k];
-            a1 += p[k + 1];
+        for (int u = 0; u < 4; ++u) {
+            a0 += v[u].x;
+            a1 += v[u].y;
         }
     }
-    for (; j + L < hi; j += 2 * L) {
-        a0 += prod[j];
-        a1 += prod[j + L];
+    for (; k < pe; k += L) {
+        const double2 v = p2[k];
+        a0 += v.x;
+        a1 += v.y;
     }
-    if (j < hi)
-        a0 += prod[j];
     return a0 + a1;
 }
 

@@ -261,12 +261,31 @@ __device__ __forceinline__ int2 block_minmax(int lo, int hi)
     return lo <= hi ? int2{lo, hi} : int2{0, -1};
 }
 
+// v from lane (lane ^ 1) or (lane ^ 2) of its quad by a DPP quad_perm move
+// (a VALU operand modifier) instead of __shfl_xor's ds_bpermute through the
+// LDS unit; whole quads are active together wherever group_sum runs.
+template <int CTRL>
+__device__ __forceinline__ double quad_xor(double v)
+{
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+
+// Butterfly sum over W-lane groups: every lane gets the group's sum, added
+// in the same order as the xor butterfly (the last two steps by DPP: same
+// bits as __shfl_xor).
 template <int W>
 __device__ __forceinline__ double group_sum(double v)
 {
 #pragma unroll
-    for (int off = W / 2; off > 0; off >>= 1)
+    for (int off = W / 2; off > 2; off >>= 1)
         v += __shfl_xor(v, off, W);
+    if constexpr (W >= 4)
+        v += quad_xor<0x4E>(v);  // quad_perm [2,3,0,1]: lane ^ 2
+    if constexpr (W >= 2)
+        v += quad_xor<0xB1>(v);  // quad_perm [1,0,3,2]: lane ^ 1
     return v;
 }
 

@@ -16,7 +16,8 @@
 #              8-shard cold R-MAT rehearsal)
 #   PMC_ARGS   extra tools/pmc_traffic.py arguments (pmc, pmcsingle)
 #   TEST_K     pytest -k expression (testk)
-#   BENCH_ARGS extra bench.py arguments (bench)
+#   BENCH_ARGS extra bench.py arguments (bench), BENCH_TAG its log name
+#              (gpurun_out/bench_<tag>.log; default bench.log)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -50,7 +51,7 @@ for s in "${steps[@]}"; do
     testk) run gpu_tests_k 900 $PYT tests -m gpu -k "${TEST_K:?TEST_K is required}";;
     drivers) run drivers 600 $PYT tests/test_drivers_gpu.py;;
     itertests) run iter_tests 600 $PYT tests/test_iterate_gpu.py;;
-    bench) run bench 900 python bench.py "${bench_args[@]}";;
+    bench) run "bench${BENCH_TAG:+_$BENCH_TAG}" 900 python bench.py "${bench_args[@]}";;
     benchrmat) run bench_rmat 600 python bench.py --workload rmat --steps 20;;
     benchbatch) run bench_batch 600 python bench.py --workload batch --rmat-strong no --banded-strong no;;
     benchbanded) run bench_banded_sell 600 python bench.py --workload banded --format sell --steps 20 &&

@@ -170,45 +170,6 @@ struct Col16 {
     }
 };
 
-// One lane's share of a row's products in the staged chunk: entries
-// [lo, hi) of the chunk (chunk-relative, < 2^31).  The products are read as
-// 16-byte pairs (half the LDS instructions of single reads): lane k takes
-// pairs plo+k, plo+k+L, ... into two partial sums (a0 the first product of
-// each pair, a1 the second), four pairs read per step before the first add;
-// an odd first entry goes to lane 0's a0, an odd last entry to lane L-1's a1.
-template <int L>
-__device__ __forceinline__ double slice_sum(const double *prod, int64_t lo64, int64_t hi64, int lane)
-{
-    const int lo = (int)lo64, hi = (int)hi64;
-    double a0 = 0.0, a1 = 0.0;
-    if (lo >= hi)
-        return 0.0;
-    if ((lo & 1) && lane == 0)
-        a0 = prod[lo];
-    if ((hi & 1) && lane == L - 1)
-        a1 = prod[hi - 1];
-    const double2 *p2 = reinterpret_cast<const double2 *>(prod);
-    const int pe = hi >> 1;  // whole pairs [(lo+1)/2, hi/2)
-    int k = ((lo + 1) >> 1) + lane;
-    for (; k + 3 * L < pe; k += 4 * L) {
-        double2 v[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-            v[u] = p2[k + u * L];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            a0 += v[u].x;
-            a1 += v[u].y;
-        }
-    }
-    for (; k < pe; k += L) {
-        const double2 v = p2[k];
-        a0 += v.x;
-        a1 += v.y;
-    }
-    return a0 + a1;
-}
-
 // One row group (RPB = 256/L rows) of the staged scheme; s_ptr holds the
 // group's RPB+1 row offsets.  Ends with a barrier, so the caller may
 // overwrite s_ptr / s_prod afterwards.  Per-round guarded loads (the batched

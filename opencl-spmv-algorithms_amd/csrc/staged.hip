@@ -224,8 +224,7 @@ __global__ __launch_bounds__(kBlock) void cmrs_staged_kernel(
                 a = lower_bound_lds(s_key, (int)(lo - cb), (int)(hi - cb), key);
                 b = lower_bound_lds(s_key, a, (int)(hi - cb), key + 1);
             }
-            for (int j = a + lane; j < b; j += L)
-                acc += prod[j];
+            acc += slice_sum<L>(prod, a, b, lane);
         }
         __syncthreads();
     }
@@ -368,8 +367,7 @@ __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
         double c = 0.0;
         if (first_continues) {
             const int b = heads ? s_start[0] : lower_bound_lds(s_row, 0, n, first + 1);
-            for (int j = lane; j < b; j += L)
-                c += prod[j];
+            c = slice_sum<L>(prod, 0, b, lane);
         }
         c = group_sum<L>(c);
         if (lane == 0) {
@@ -393,9 +391,7 @@ __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
             }
             if (a == b)
                 continue;  // uniform over the group
-            double s = 0.0;
-            for (int j = a + lane; j < b; j += L)
-                s += prod[j];
+            double s = slice_sum<L>(prod, a, b, lane);
             s = group_sum<L>(s);
             if (lane == 0)
                 y[r] += s;
@@ -416,8 +412,7 @@ __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
                 a = lower_bound_lds(s_row, 0, ne, (int)r);
                 b = lower_bound_lds(s_row, a, ne, (int)r + 1);
             }
-            for (int j = a + lane; j < b; j += L)
-                s += prod[j];
+            s = slice_sum<L>(prod, a, b, lane);
         }
         s = group_sum<L>(s);
         if (lane == 0)

@@ -27,9 +27,10 @@ steps=("$@")
 run() { # name timeout cmd...
   local name=$1 t=$2; shift 2
   echo "=== $name: $*" | tee -a gpurun_out/job.log
+  local t0=$SECONDS
   timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
   local rc=$?
-  echo "=== $name exit $rc" | tee -a gpurun_out/job.log
+  echo "=== $name exit $rc ($((SECONDS - t0)) s)" | tee -a gpurun_out/job.log
   tail -5 "gpurun_out/$name.log"
   if [ "$rc" -ne 0 ]; then echo "fatal exit $rc in $name: stopping"; exit "$rc"; fi
   return 0

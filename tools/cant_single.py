@@ -130,8 +130,27 @@ def main():
         env = kw.pop("_env", {})  # library environment switches for this run only (A/B of placement / order)
         saved = {k: os.environ.get(k) for k in env}
         os.environ.update({k: str(v) for k, v in env.items()})
+        # "_gap_kib": re-place the matrix arrays in ONE allocation, in the
+        # order built, each at a 2 MiB boundary plus this gap after the
+        # previous one (placement A/B: same bits)
+        gap = kw.pop("_gap_kib", None)
         dm = sa.to_device(m, fmt, dev, **kw)
         dm.params.update(over)
+        if gap is not None:
+            names = [k for k in ("row_ptr", "row", "col", "val") if k in dm.arrays]
+            sizes = [dm.arrays[k].numel() * dm.arrays[k].element_size() for k in names]
+            al = 2 << 20
+            offs, o = [], 0
+            for b in sizes:
+                offs.append(o)
+                o = (o + b + al - 1) // al * al + int(gap) * 1024
+            pool = torch.empty(o + al, dtype=torch.uint8, device=dev)
+            dm._pool = pool
+            for k, off, b in zip(names, offs, sizes):
+                t = dm.arrays[k]
+                view = pool[off:off + b].view(t.dtype)
+                view.copy_(t.reshape(-1))
+                dm.arrays[k] = view
         y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
         dm.run(x, y)
         torch.cuda.synchronize()

@@ -223,6 +223,13 @@ int spmv_hyb_run(spmv_dims d, int32_t K, int64_t ld, int32_t ki, const int32_t *
                  const double *ell_val, int64_t tail_nnz, const int32_t *tail_row,
                  const int32_t *tail_col, const double *tail_val, const double *x, double *y,
                  void *ws, size_t ws_bytes);
+/* HYB with a single-pass tail (no carry pass, no workspace): `tails` built
+ * by spmv_coo_tail_build over the tail (dims.nnz = tail_nnz), which refuses
+ * a tail row running more than 80 entries past a tile end. */
+int spmv_hyb_run_tail(spmv_dims d, int32_t K, int64_t ld, int32_t ki, const int32_t *ell_col,
+                      const double *ell_val, int64_t tail_nnz, const int32_t *tail_row,
+                      const int32_t *tail_col, const double *tail_val, const double *x, double *y,
+                      const void *tails);
 
 /* -------------------------------------------------------- SELL-C-sigma ---
  * Replaces kernel `sigma_c(val,idx,x,y,slice_ptr,int C)` (reference

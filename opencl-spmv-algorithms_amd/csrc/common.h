@@ -61,7 +61,7 @@ int64_t coo_hot_tile(int64_t n_rows, int64_t nnz);
 // accumulate mode: y[r] += entries of the rows present (HYB tail)
 int launch_coo_staged_acc(const spmv_dims &d, const int32_t *row, const int32_t *col,
                           const double *val, const double *x, double *y, int32_t *carry_row,
-                          double *carry_val);
+                          double *carry_val, const int32_t *tails = nullptr);
 int launch_csr_tiled(const spmv_dims &d, const int64_t *row_ptr, const int32_t *col,
                      const double *val, const double *x, double *y, int32_t *own_lo,
                      int32_t *carry_row, double *carry_val);

@@ -392,8 +392,8 @@ __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
                 a = s_start[r - r_lo];
                 b = s_start[r - r_lo + 1];
             } else {
-                a = lower_bound_lds(s_row, 0, n, (int)r);
-                b = lower_bound_lds(s_row, a, n, (int)r + 1);
+                a = lower_bound_lds(s_row, 0, ne, (int)r);
+                b = lower_bound_lds(s_row, a, ne, (int)r + 1);
             }
             if (a == b)
                 continue;  // uniform over the group
@@ -921,7 +921,7 @@ int64_t coo_hot_tile(int64_t n_rows, int64_t nnz) { return 2 * kBlock * coo_hot_
 
 int launch_coo_staged_acc(const spmv_dims &d, const int32_t *row, const int32_t *col,
                           const double *val, const double *x, double *y, int32_t *carry_row,
-                          double *carry_val)
+                          double *carry_val, const int32_t *tails)
 {
     constexpr int R = kCooR;
     const int64_t tiles = (d.nnz + coo_staged_tile() - 1) / coo_staged_tile();
@@ -929,9 +929,14 @@ int launch_coo_staged_acc(const spmv_dims &d, const int32_t *row, const int32_t 
         return fail_msg(SPMV_OTHER_ERROR, "coo tail: grid too large");
     if (tiles == 0)
         return SPMV_SUCCESS;
-    hipLaunchKernelGGL((coo_staged_kernel<4, R, true, false>), dim3((unsigned)tiles), dim3(kBlock), 0,
-                       (hipStream_t)d.stream, d.n_rows, d.nnz, row, col, val, x, y, carry_row, carry_val,
-                       (const int2 *)nullptr, 0, XGlobal{x});
+    if (tails)  // single pass: every tile finishes its last row (no carry)
+        hipLaunchKernelGGL((coo_staged_kernel<4, R, true, false, false, XGlobal, true>), dim3((unsigned)tiles),
+                           dim3(kBlock), 0, (hipStream_t)d.stream, d.n_rows, d.nnz, row, col, val, x, y,
+                           carry_row, carry_val, (const int2 *)nullptr, 0, XGlobal{x}, tails);
+    else
+        hipLaunchKernelGGL((coo_staged_kernel<4, R, true, false>), dim3((unsigned)tiles), dim3(kBlock), 0,
+                           (hipStream_t)d.stream, d.n_rows, d.nnz, row, col, val, x, y, carry_row, carry_val,
+                           (const int2 *)nullptr, 0, XGlobal{x});
     SPMV_CHECK_LAUNCH("coo_staged_kernel (accumulate)");
     return SPMV_SUCCESS;
 }

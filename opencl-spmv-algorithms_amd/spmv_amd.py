@@ -105,6 +105,8 @@ HIP_SYMBOLS = {
     "spmv_hyb_ws_bytes": (ctypes.c_size_t, [_c_i64]),
     "spmv_hyb_run": (ctypes.c_int, [Dims, _c_i32, _c_i64, _c_i32, _vp, _vp, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp,
                                     ctypes.c_size_t]),
+    "spmv_hyb_run_tail": (ctypes.c_int, [Dims, _c_i32, _c_i64, _c_i32, _vp, _vp, _c_i64, _vp, _vp, _vp, _vp, _vp,
+                                         _vp]),
     "spmv_csr_xwin_bytes": (ctypes.c_size_t, [_c_i64, _c_i64, ctypes.c_int, _c_i32]),
     "spmv_csr_xwin_build": (ctypes.c_int, [Dims, _vp, _vp, ctypes.c_int, _c_i32, _vp, ctypes.c_size_t,
                                            ctypes.POINTER(_c_i32)]),
@@ -685,6 +687,10 @@ class DeviceMatrix:
             rc = lib.spmv_hyb_run_hot(d, p["K"], p["ld"], p["ki"], _ptr(a["ell_col"]), _ptr(a["ell_val"]),
                                       p["tail_nnz"], _ptr(a["tail_row"]), _ptr(a["tail_col"]), _ptr(a["tail_val"]),
                                       _ptr(x), _ptr(y), p["H"], _ptr(a["hot"]), _ptr(a["ws"]), a["ws"].numel())
+        elif self.fmt == "hyb" and "tails" in a:
+            rc = lib.spmv_hyb_run_tail(d, p["K"], p["ld"], p["ki"], _ptr(a["ell_col"]), _ptr(a["ell_val"]),
+                                       p["tail_nnz"], _ptr(a["tail_row"]), _ptr(a["tail_col"]), _ptr(a["tail_val"]),
+                                       _ptr(x), _ptr(y), _ptr(a["tails"]))
         elif self.fmt == "hyb":
             rc = lib.spmv_hyb_run(d, p["K"], p["ld"], p["ki"], _ptr(a["ell_col"]), _ptr(a["ell_val"]), p["tail_nnz"],
                                   _ptr(a["tail_row"]), _ptr(a["tail_col"]), _ptr(a["tail_val"]), _ptr(x), _ptr(y),
@@ -1071,6 +1077,19 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
         dm.arrays["ws"] = torch.empty(max(ws, 16), dtype=torch.uint8, device=device)
         if dm.params["H"] > 0:
             dm.arrays["hot"] = _dev_tensor(hot_cols, device)
+        elif hb["tail_nnz"] > 0 and coo_tail is not False:
+            # single-pass tail (no carry pass) where every tail row ends
+            # within 80 entries of its tile, as the COO format
+            td = dm.dims()
+            td.nnz = hb["tail_nnz"]
+            tb = hip_lib().spmv_coo_tail_bytes(hb["tail_nnz"])
+            tails = torch.empty(max(tb, 4), dtype=torch.uint8, device=device)
+            rc = hip_lib().spmv_coo_tail_build(td, _ptr(dm.arrays["tail_row"]), _ptr(tails), tails.numel())
+            if rc == SUCCESS:
+                dm.arrays["tails"] = tails
+                dm.params["single_pass"] = 1
+            elif coo_tail:
+                raise SpmvError(rc, "spmv_coo_tail_build (hyb tail)", hip_lib().spmv_last_error().decode())
         dm.stored_bytes = 12 * hb["stored"] + 16 * hb["tail_nnz"]
     elif fmt == "cmrs":
         c = cmrs_build(m.n_rows, ptr, h=h)

@@ -68,6 +68,7 @@ FMT_PARAMS = [
     # COO with x windows in LDS (opt-in), CMRS with global x gathers
     ("coo", {"xwin": True}),
     ("coo", {"coo_tail": False}),  # the carry pass (default: single pass where rows allow)
+    ("hyb", {"coo_tail": False}),  # HYB tail through the carry pass
     ("cmrs", {"h": 8, "xwin": False}),
     # SELL16: 16-bit column offsets from each workgroup's window base
     ("sell16", {"C": 64, "sigma": 1024, "ki": 2}),
@@ -992,6 +993,39 @@ def test_coo_single_pass(torch_dev, case):
             assert "tails" in a.arrays, m.label
         b = sa.to_device(m, "coo", dev, coo_tail=False)  # the carry pass
         assert "tails" not in b.arrays
+        x = torch.from_numpy(rng.uniform(-1, 1, max(m.n_cols, 1))).to(dev)
+        ya = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
+        ya2, yb = torch.full_like(ya, float("nan")), torch.full_like(ya, float("nan"))
+        a.run(x, ya)
+        a.run(x, ya2)
+        b.run(x, yb)
+        torch.cuda.synchronize()
+        assert torch.equal(ya.view(torch.int64), ya2.view(torch.int64))
+        assert_parity(m, ya.cpu().numpy(), x.cpu().numpy()[: m.n_cols])
+        assert_parity(m, yb.cpu().numpy(), x.cpu().numpy()[: m.n_cols])
+
+
+@pytest.mark.parametrize("case", ["cantlike", "fixtures", "batch"])
+def test_hyb_single_pass_tail(torch_dev, case):
+    """HYB's COO tail in one pass (spmv_hyb_run_tail, the default where the
+    tail plan allows) against the oracle and the carry pass; y pre-filled
+    with NaN, reproducible run to run."""
+    torch, dev = torch_dev
+    if case == "cantlike":
+        ms = [sa.gen_cantlike(0)]
+    elif case == "batch":
+        ms = [sa.gen_cantlike(1, copies=3)]
+    else:
+        ms = [sa.read_mtx(GOLDEN / f"{c}.mtx") for c in CASES]
+    rng = np.random.default_rng(43)
+    for m in ms:
+        if m.n_rows == 0:
+            continue
+        a = sa.to_device(m, "hyb", dev)
+        b = sa.to_device(m, "hyb", dev, coo_tail=False)
+        assert "tails" not in b.arrays
+        if case != "fixtures":
+            assert a.params["tail_nnz"] > 0 and "tails" in a.arrays, m.label
         x = torch.from_numpy(rng.uniform(-1, 1, max(m.n_cols, 1))).to(dev)
         ya = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
         ya2, yb = torch.full_like(ya, float("nan")), torch.full_like(ya, float("nan"))

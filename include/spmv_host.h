@@ -94,6 +94,19 @@ int spmv_csr_pick_variant(int64_t n_rows, const int64_t *row_ptr);
 int64_t spmv_hot_columns(int64_t n_cols, int64_t nnz, const int32_t *col, int64_t H_req, int32_t *hot,
                          int32_t *col_out);
 
+/* Degree-ordered column relabel (power-law columns, x replicated): the
+ * columns ranked by decreasing entry count (ties: lower column first;
+ * columns without entries last, in id order).  order[rank] = column,
+ * newid[column] = rank, and col_out (may alias col) = newid[col].  The
+ * relabelled matrix A' = A·Pᵀ takes x' = P·x (x'[k] = x[order[k]]) and
+ * gives the same y in the same row order, bit for bit with any kernel
+ * whose per-row summation order does not depend on column ids: the hot
+ * columns are x'[0..H) (no per-run hot-table fill) and the touched part of
+ * x is one dense prefix.  Returns the number of non-empty columns, -1 on
+ * bad input.                                                             */
+int64_t spmv_column_relabel(int64_t n_cols, int64_t nnz, const int32_t *col, int32_t *order, int32_t *newid,
+                            int32_t *col_out);
+
 /* ELL, column-major with leading dimension ld = round_up(N, 64) and
  * k-interleave ki (spmv.h).  K = round_up(max row length, ki).
  * spmv_ell_plan gives K and ld; arrays are ld*K elements.               */

@@ -34,12 +34,11 @@ __global__ __launch_bounds__(kBlock) void coo_carry_kernel(
     const double *__restrict__ carry_val, double *__restrict__ y)
 {
     const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (t >= n_tiles)
-        return;
-    // The head test and the first 8 tiles' loads are issued together (one
-    // round trip for a row over <= 8 tiles, the common case); a hub row over
-    // ~100 tiles then loads 8 tiles per step.  Still added in tile order.
-    const int32_t prev = t > 0 ? carry_row[t - 1] : -1;
+    const int lane = threadIdx.x & (kWave - 1);
+    // The head test and the first 8 tiles' loads are issued together: one
+    // round trip for a row over <= 8 tiles (the common case), added in tile
+    // order by the head's thread.
+    const int32_t prev = t > 0 && t < n_tiles ? carry_row[t - 1] : -1;
     int32_t rr[8];
     double vv[8];
 #pragma unroll
@@ -49,24 +48,48 @@ __global__ __launch_bounds__(kBlock) void coo_carry_kernel(
         vv[k] = in ? carry_val[t + k] : 0.0;
     }
     const int32_t r = rr[0];
-    if (r < 0 || prev == r)
-        return;  // not a carry, or not the head of its run
-    double s = 0.0;
-    for (int64_t u = t;;) {
-        int k = 0;
-        for (; k < 8 && rr[k] == r; ++k)
+    const bool head = t < n_tiles && r >= 0 && prev != r;  // first tile of a run of carries
+    const bool lng = head && rr[7] == r;                   // the run goes on past 8 tiles
+    if (head && !lng) {
+        double s = 0.0;
+        for (int k = 0; k < 8 && rr[k] == r; ++k)
             s += vv[k];
-        if (k < 8)
-            break;
-        u += 8;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const bool in = u + q < n_tiles;
-            rr[q] = in ? carry_row[u + q] : -2;
-            vv[q] = in ? carry_val[u + q] : 0.0;
-        }
+        y[r] += s;
     }
-    y[r] += s;
+    // A hub row's run (R-MAT rows of 1e5 entries span ~100-150 tiles) is
+    // summed by the whole wave: 4 x 64 tiles per round trip, lane-strided,
+    // then the butterfly (a fixed order, so still bitwise reproducible);
+    // one thread walking it 8 tiles per round trip took 13+ dependent round
+    // trips (9 us of an R-MAT shard's 145).
+    for (uint64_t m = __ballot(lng); m; m &= m - 1) {
+        const int l = __builtin_ctzll(m);
+        const int32_t hr = __shfl(r, l);
+        const int64_t ht = t - lane + l;
+        double s = 0.0;
+        for (int64_t base = ht;; base += 4 * kWave) {
+            int32_t q[4];
+            double v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int64_t i = base + u * kWave + lane;
+                q[u] = i < n_tiles ? carry_row[i] : -2;
+                v[u] = i < n_tiles ? carry_val[i] : 0.0;
+            }
+            bool end = false;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (q[u] == hr)
+                    s += v[u];
+                else
+                    end = true;
+            }
+            if (__ballot(end))
+                break;  // the run ended inside this round: rows only grow with the tile
+        }
+        s = group_sum<kWave>(s);
+        if (lane == l)
+            y[hr] += s;
+    }
 }
 
 int launch_carry(int64_t tiles, const int32_t *carry_row, const double *carry_val, double *y,

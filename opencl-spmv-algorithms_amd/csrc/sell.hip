@@ -297,7 +297,13 @@ static bool sell_ystage(int bt, int32_t sigma)
 }
 
 bool sell_small(int32_t C, int64_t n_slices);
-constexpr int kSellSmallS = 2;  // sell_small_kernel: waves per slice
+#ifndef SPMV_SELL_SMALL_S  // A/B builds only (tools/gpu_job.sh absingle); the product is built with the default
+#define SPMV_SELL_SMALL_S 2
+#endif
+constexpr int kSellSmallS = SPMV_SELL_SMALL_S;  // sell_small_kernel: waves per slice
+#ifndef SPMV_SELL_HEAD_G  // A/B builds only, as SPMV_SELL_SMALL_S
+#define SPMV_SELL_HEAD_G 8
+#endif
 constexpr int kSellSmallP = 4;  // sell_small_kernel: slices per workgroup (and per x window)
 
 static void sell_geometry(int32_t C, int32_t sigma, int64_t n_slices, int *bt, int64_t *blocks)
@@ -448,7 +454,7 @@ __global__ __launch_bounds__(1024) void sell_xwin_kernel(
 // spans, cant-like single, profiles/round3/sell_lab_multi_slice*.log): one
 // slice per workgroup copied a 1,572-entry window per 64 rows (12 MB of L2
 // reads for a 49 MB matrix); four slices share it.
-template <int KI> constexpr int sell_small_g() { return 8; }  // first-batch slot groups per lane
+template <int KI> constexpr int sell_small_g() { return SPMV_SELL_HEAD_G; }  // first-batch slot groups per lane
 
 // (SELL16 gathering x from global memory instead of the LDS window (xcap 0)
 // measured slower on one cant-like copy: 11.6-11.9 vs 10.3-10.6 us cold,
@@ -562,7 +568,7 @@ bool sell_small(int32_t C, int64_t n_slices)
 // slot groups per wave in the SELL16 head (its kernel's first batch): 8 and
 // 12 ran the same (10.36 us cold, cant-like single), 16 slower (11.24 us:
 // waves of 9-15 groups read padding); profiles/round3/cant_single_sell16_head_*.json
-constexpr int kSell16HeadG = 8;
+constexpr int kSell16HeadG = SPMV_SELL_HEAD_G;
 static int sell16_head_g() { return kSell16HeadG; }
 
 template <int KI, bool NT, bool XWIN, typename XS, typename CT = int32_t>

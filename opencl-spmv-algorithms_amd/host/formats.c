@@ -214,6 +214,53 @@ int64_t spmv_hot_columns(int64_t n_cols, int64_t nnz, const int32_t *col, int64_
     return n;
 }
 
+/* Counting sort of the columns by entry count: ranks are handed out from
+ * the largest count down, and inside one count in increasing column id, so
+ * the order is the same whatever the thread count. */
+int64_t spmv_column_relabel(int64_t n_cols, int64_t nnz, const int32_t *col, int32_t *order, int32_t *newid,
+                            int32_t *col_out)
+{
+    if (n_cols <= 0 || n_cols > INT32_MAX || nnz < 0 || !order || !newid || (nnz > 0 && (!col || !col_out)))
+        return -1;
+    int64_t *cnt = (int64_t *)calloc((size_t)n_cols, sizeof(int64_t));
+    if (!cnt)
+        return -1;
+    int64_t maxc = 0;
+    for (int64_t j = 0; j < nnz; ++j) {
+        if (col[j] < 0 || col[j] >= n_cols) {
+            free(cnt);
+            return -1;
+        }
+        const int64_t c = ++cnt[col[j]];
+        maxc = c > maxc ? c : maxc;
+    }
+    /* first[k] = first rank of count k: counts above k come first */
+    int64_t *first = (int64_t *)calloc((size_t)maxc + 2, sizeof(int64_t));
+    if (!first) {
+        free(cnt);
+        return -1;
+    }
+    for (int64_t c = 0; c < n_cols; ++c)
+        first[cnt[c]]++;
+    int64_t acc = 0, nonempty = n_cols - first[0];
+    for (int64_t k = maxc; k >= 0; --k) {
+        const int64_t h = first[k];
+        first[k] = acc;
+        acc += h;
+    }
+    for (int64_t c = 0; c < n_cols; ++c) {
+        const int64_t r = first[cnt[c]]++;
+        order[r] = (int32_t)c;
+        newid[c] = (int32_t)r;
+    }
+    free(first);
+    free(cnt);
+#pragma omp parallel for schedule(static)
+    for (int64_t j = 0; j < nnz; ++j)
+        col_out[j] = newid[col[j]];
+    return nonempty;
+}
+
 int spmv_csr_pick_variant(int64_t n_rows, const int64_t *row_ptr)
 {
     int64_t mx = 0;

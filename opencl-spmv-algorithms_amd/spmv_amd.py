@@ -211,6 +211,7 @@ HOST_SYMBOLS = {
     "spmv_csr_row_stats": (ctypes.c_int, [_c_i64, _vp, ctypes.POINTER(_c_i64), ctypes.POINTER(_c_i64), ctypes.POINTER(ctypes.c_double)]),
     "spmv_csr_pick_variant": (ctypes.c_int, [_c_i64, _vp]),
     "spmv_hot_columns": (_c_i64, [_c_i64, _c_i64, _vp, _c_i64, _vp, _vp]),
+    "spmv_column_relabel": (_c_i64, [_c_i64, _c_i64, _vp, _vp, _vp, _vp]),
     "spmv_ell_plan": (ctypes.c_int, [_c_i64, _vp, _c_i32, ctypes.POINTER(_c_i32), ctypes.POINTER(_c_i64)]),
     "spmv_ell_fill": (ctypes.c_int, [_c_i64, _vp, _vp, _vp, _c_i32, _c_i64, _c_i32, _vp, _vp]),
     "spmv_sell_plan": (ctypes.c_int, [_c_i64, _vp, _c_i32, _c_i32, _c_i32, ctypes.POINTER(_c_i64), ctypes.POINTER(_c_i64)]),
@@ -474,6 +475,27 @@ def hot_columns(n_cols: int, col, H: int = 0):
     if n < 0:
         raise SpmvError(OTHER_ERROR, "spmv_hot_columns", "bad arguments")
     return int(n), hot[:n].copy(), out[: col.size]
+
+
+def column_relabel(n_cols: int, col):
+    """spmv_column_relabel: (order, newid, col') — columns ranked by
+    decreasing entry count; x' = x[order] is the input of the relabelled
+    matrix, whose y is the original's, row for row."""
+    col = np.ascontiguousarray(col, dtype=np.int32)
+    order = np.empty(n_cols, np.int32)
+    newid = np.empty(n_cols, np.int32)
+    out = np.empty(max(col.size, 1), np.int32)
+    n = host_lib().spmv_column_relabel(n_cols, col.size, _ptr(col), _ptr(order), _ptr(newid), _ptr(out))
+    if n < 0:
+        raise SpmvError(OTHER_ERROR, "spmv_column_relabel", "bad arguments")
+    return order, newid, out[: col.size]
+
+
+def relabel_columns(m: Coo):
+    """(m', order): m with its columns relabelled hot-first (same rows, same
+    entry order); run m' on x[order]."""
+    order, _, c2 = column_relabel(m.n_cols, m.col)
+    return Coo(m.n_rows, m.n_cols, m.row, c2, m.val, False, f"{m.label} (columns relabelled by degree)"), order
 
 
 def cmrs_build(n_rows: int, ptr, h: int = 8):

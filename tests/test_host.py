@@ -418,6 +418,43 @@ def test_hot_columns_rule(skewed):
         assert n == 0 and np.array_equal(ch, col)
 
 
+@pytest.mark.parametrize("kind", ["rmat", "tiny", "empty_cols"])
+def test_column_relabel(kind):
+    """spmv_column_relabel: a permutation ranking columns by decreasing
+    count (ties by id, empty columns last in id order); col' = newid[col];
+    the relabelled matrix on x[order] gives the oracle's y bit for bit
+    (same rows, same entry order, same products)."""
+    if kind == "rmat":
+        m = sa.gen_rmat(100_000, 1_000_000, scale=17, seed=2)
+    elif kind == "tiny":
+        m = sa.Coo(3, 4, np.array([0, 1, 2, 2], np.int32), np.array([3, 1, 3, 1], np.int32),
+                   np.array([1.0, 2.0, 3.0, 4.0]))
+    else:
+        m = sa.gen_random(500, 5000, 0, 9, seed=4)
+    order, newid, c2 = sa.column_relabel(m.n_cols, m.col)
+    cnt = np.bincount(m.col, minlength=m.n_cols)
+    assert np.array_equal(np.sort(order), np.arange(m.n_cols))
+    assert np.array_equal(newid[order], np.arange(m.n_cols))
+    assert np.all(np.diff(cnt[order]) <= 0)
+    ties = np.diff(cnt[order]) == 0
+    assert np.all(np.diff(order)[ties] > 0)  # ties in increasing column id
+    assert np.array_equal(c2, newid[m.col])
+    m2, order2 = sa.relabel_columns(m)
+    assert np.array_equal(order2, order) and np.array_equal(m2.row, m.row) and np.array_equal(m2.col, c2)
+    x = np.random.default_rng(1).uniform(-1, 1, m.n_cols)
+    assert np.array_equal(oracle.file_order_spmv(m.n_rows, m.row, m.col, m.val, x), oracle.file_order_spmv(m2.n_rows, m2.row, m2.col, m2.val, np.ascontiguousarray(x[order])))
+    if kind == "tiny":
+        assert order.tolist() == [1, 3, 0, 2]
+
+
+def test_column_relabel_bad_input():
+    lib = sa.host_lib()
+    col = np.array([0, 5], np.int32)
+    buf = np.empty(8, np.int32)
+    assert lib.spmv_column_relabel(5, 2, col.ctypes.data, buf.ctypes.data, buf.ctypes.data, buf.ctypes.data) == -1
+    assert lib.spmv_column_relabel(0, 0, None, buf.ctypes.data, buf.ctypes.data, None) == -1
+
+
 def _rmat_like_ptr(n=200_000, seed=3):
     rng = np.random.default_rng(seed)
     lens = (rng.pareto(1.2, n) * 3).astype(np.int64)

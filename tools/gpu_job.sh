@@ -15,6 +15,7 @@
 #              (R-MAT tiled CSR, tools/rmat_split_exp.py), abreh (1- and
 #              8-shard cold R-MAT rehearsal)
 #   PMC_ARGS   extra tools/pmc_traffic.py arguments (pmc, pmcsingle)
+#   REH_ARGS   extra tools/shard_rehearse.py arguments (abreh), e.g. --relabel
 #   TEST_K     pytest -k expression (testk)
 #   BENCH_ARGS extra bench.py arguments (bench), BENCH_TAG its log name
 #              (gpurun_out/bench_<tag>.log; default bench.log)
@@ -43,6 +44,7 @@ PYT="python -u -m pytest -x -q --timeout 300 --timeout-method thread"
 eval "cs_args=(${CS_ARGS:-})"
 eval "pmc_args=(${PMC_ARGS:-})"
 eval "bench_args=(${BENCH_ARGS:-})"
+eval "reh_args=(${REH_ARGS:-})"
 for s in "${steps[@]}"; do
   case $s in
     smoke) run smoke 400 python -c "import __graft_entry__ as g; g.smoke()";;
@@ -81,9 +83,13 @@ for s in "${steps[@]}"; do
     abreh) ab_pairs
            for i in 1 2; do
              for p in "${AB[@]}"; do
-               SPMV_HIP_LIB=$(lib_of "${p#*=}") run "ab_reh_${p%%=*}_$i" 400 python3 -u tools/shard_rehearse.py --gpus 1,8 --graph --flush
+               SPMV_HIP_LIB=$(lib_of "${p#*=}") run "ab_reh_${p%%=*}_$i" 400 python3 -u tools/shard_rehearse.py --gpus 1,8 --graph --flush "${reh_args[@]}"
              done
            done;;
+    rehrelabel) run reh_base 500 python -u tools/shard_rehearse.py --gpus 1,8 --graph --flush &&
+                run reh_relabel 500 python -u tools/shard_rehearse.py --gpus 1,8 --graph --flush --relabel;;
+    rehtrace) run reh_trace 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/reh_trace -o run -- python3 -u tools/shard_rehearse.py --gpus 1,8 --graph --flush --reps 20 "${reh_args[@]}";;
+    rehcal) run reh_cal 900 python -u tools/shard_rehearse.py --gpus 8 --graph --flush --calibrate 3 "${reh_args[@]}";;
     sweep) run sweep 600 python tools/sweep.py;;
     rehearse8) run shard_rehearse 900 python tools/shard_rehearse.py --gpus 1,2,4,8 --graph --reps 50;;
     rehearsecold) run shard_rehearse_cold 900 python tools/shard_rehearse.py --gpus 1,2,4,8 --graph --reps 50 --flush;;

@@ -81,6 +81,9 @@ def main():
                     help="KEY=v1,v2: library knobs timed interleaved on every shard (several: cartesian product)")
     ap.add_argument("--rounds", type=int, default=1, help="interleaved rounds per shard (median of rounds)")
     ap.add_argument("--flush", action="store_true", help="also time every shard cold (512 MiB flush first)")
+    ap.add_argument("--relabel", action="store_true",
+                    help="columns relabelled by decreasing degree (spmv_column_relabel), x permuted to match; "
+                         "no hot-column table")
     ap.add_argument("--calibrate", type=int, default=0,
                     help="profile-guided re-cuts after the weighted cut (spmv_partition_rows_calibrated, "
                          "from the first --env config's shard times), each timed again")
@@ -99,6 +102,10 @@ def main():
     n, z = full.n_rows, full.nnz
     del full
     xh = sa.ramp_x(n)
+    if a.relabel:  # the replicated x arrives in the relabelled layout (outside the timed step)
+        order, _, col = sa.column_relabel(n, col)
+        xh = np.ascontiguousarray(xh[order])
+        a.hot = "0"
     x = torch.from_numpy(xh).to(dev)
     b_total = sa.bytes_alg(n, n, z)
     base = None
@@ -151,7 +158,8 @@ def run_split(a, torch, sa, dev, ptr, col, val, n, x, xh, b_total, envs, kw, G, 
         if cold:
             extra = {"shard_ms_cold": [round(t, 4) for t in cold], "max_ms_cold": round(max(cold), 4),
                      "aggregate_GBs_cold": round(b_total / (max(cold) * 1e-3) * 1e-9, 1)}
-        print(json.dumps({"workload": "rmat 1e7/1e8", "format": a.format, "env": env, "params_shard0": params,
+        print(json.dumps({"workload": "rmat 1e7/1e8", "format": a.format, "relabel": a.relabel, "env": env,
+                          "params_shard0": params,
                           "gpus": G, "row_weight": w, "hot": hot, "graph": a.graph, "calibration_pass": cpass,
                           "shard_rows": np.diff(bounds).tolist(), "shard_nnz": nnzs,
                           "shard_ms": [round(t, 4) for t in times[i]], "max_ms": round(tmax, 4),

@@ -11,14 +11,15 @@ on ONE cant-like matrix per GPU, COLD.  A step is a 512 MiB flush (evicts
 the 256 MiB Infinity Cache and the L2s) followed by ONE SpMV launch, so the
 49.3 MB matrix is read from HBM every step.  W untimed warm-up steps, then
 exactly K steps captured in one HIP graph and replayed between a barrier +
-synchronize on both sides.  The SpMV's own share of a step is its kernel
-duration: at N=1 from a rocprofv3 kernel trace of tools/cant_single.py (a
-child process started before this process touches the GPU; every format,
-cold and warm, beside the stream-probe ceiling of the same bytes), at N>1
-from one such child per rank (headline format only, on that rank's GPU);
-without a trace, from the in-process timed region: (span of K x (flush +
-SpMV) - span of K x flush) / K.  value = N x bytes_alg / (max over ranks
-of that cold SpMV time) = the whole job's throughput of replicated
+synchronize on both sides; a graph of K flushes alone is timed the same
+way, and the SpMV's share of a step is (span of K x (flush + SpMV) - span
+of K x flush) / K, HIP events on the launch stream, max over ranks.  A
+rocprofv3 kernel trace of the same kernel, cold (tools/cant_single.py, a
+child process started before this process touches the GPU: every format
+at N=1, the headline format on every rank's GPU at N>1, beside the
+stream-probe ceiling of the same bytes), is reported beside it as
+corroboration (roofline.kernel_ms_trace).  value = N x bytes_alg / (that
+in-process cold SpMV time) = the whole job's throughput of replicated
 configs[1] steps (weak scaling: one matrix per GPU, no collective);
 ms_per_step = that SpMV time; the timed region's wall clock (flushes
 included) is `timed_region`.
@@ -70,8 +71,11 @@ METRIC = "effective HBM GB/s + GFLOP/s per format on cant.mtx, 1/2/4/8 MI355X"
 # tiles the slowest of 8 shards took 0.1421 / 0.1411 / 0.1464 / 0.1549 ms
 # with weights 1 / 2 / 3 / 4 (profiles/round2/shard_rehearse_tiled_w.log)
 RMAT_ROW_WEIGHT = 2.0
-# profile-guided re-cuts of the R-MAT shards (on cold shard times with --flush yes)
-RMAT_RECUTS = 3
+# profile-guided re-cuts of the R-MAT shards (on cold shard times with --flush yes),
+# each moving the cut points RMAT_DAMP of the way (full cold re-cuts overshot:
+# profiles/round4/shard_rehearse_cold_calibrated.log)
+RMAT_RECUTS = 4
+RMAT_DAMP = 0.5
 CSR_DEFAULT_VARIANT = 3  # spmv_csr_run_variant's default (csrc/csr.hip)
 # untimed replays of a freshly captured graph before the timed replay, at
 # least this much GPU time: the first replays of a new graph ran ~4 % slower
@@ -117,6 +121,12 @@ def parse():
     p.add_argument("--banded-strong", default="auto", choices=["auto", "yes", "no"],
                    help="also time CSR and SELL on the banded 1e8-row / 1.6e9-entry matrix row-sharded over all "
                         "ranks (configs[4], generated on device; auto: with the default workload)")
+    p.add_argument("--relabel", default="auto", choices=["auto", "yes", "no"],
+                   help="R-MAT: columns relabelled by decreasing degree at build time (spmv_column_relabel), x "
+                        "replicated in that layout (auto: yes); no = the per-run hot-column table instead")
+    p.add_argument("--rmat-rows", type=int, default=10_000_000, help="R-MAT rows (configs[3]: 1e7)")
+    p.add_argument("--rmat-nnz", type=int, default=100_000_000, help="R-MAT entries (configs[3]: 1e8)")
+    p.add_argument("--recuts", type=int, default=None, help="profile-guided R-MAT re-cuts (default RMAT_RECUTS)")
     p.add_argument("--flush", default="yes", choices=["yes", "no"],
                    help="strong-scaling legs: also time every shard cold (512 MiB flush before each step)")
     p.add_argument("--graph", default="yes", choices=["yes", "no"],
@@ -389,29 +399,33 @@ def build_workload(args, torch, dev, rank, world):
                                         "49 MB matrix (Infinity-Cache resident when warm) is cant_single",
                             "copies_per_gpu": B})
     if args.workload == "rmat":
-        full = sa.gen_rmat()  # deterministic: every rank builds the same matrix
+        full = rmat_matrix(args)  # deterministic: every rank builds the same matrix
         ptr, col, val = sa.csr_from_coo(full)
-        bounds = sa.partition_rows(full.n_rows, ptr, world, align=1024, row_weight=RMAT_ROW_WEIGHT)
+        n, z = full.n_rows, full.nnz
+        del full
+        col, xh, hot, layout = rmat_layout(args, n, col)
+        bounds = sa.partition_rows(n, ptr, world, align=1024, row_weight=RMAT_ROW_WEIGHT)
         lo, hi = int(bounds[rank]), int(bounds[rank + 1])
         lptr = ptr[lo:hi + 1] - ptr[lo]
-        loc = sa.Coo(hi - lo, full.n_cols, np.repeat(np.arange(hi - lo, dtype=np.int32), np.diff(lptr)),
+        loc = sa.Coo(hi - lo, n, np.repeat(np.arange(hi - lo, dtype=np.int32), np.diff(lptr)),
                      col[ptr[lo]:ptr[hi]], val[ptr[lo]:ptr[hi]])
-        del full
-        x = torch.from_numpy(sa.ramp_x(loc.n_cols)).to(dev)
+        x = torch.from_numpy(xh).to(dev)
         y = torch.empty(max(loc.n_rows, 1), dtype=torch.float64, device=dev)
+        if hot is not None:
+            fk = dict(fk, hot=hot)
         dm = sa.to_device(loc, args.format, dev, **fk)
-        n, z = 10_000_000, 100_000_000
 
         def check():
-            bad, first = sa.check(loc, sa.ramp_x(loc.n_cols), y[:loc.n_rows].cpu().numpy())
+            bad, first = sa.check(loc, xh, y[:loc.n_rows].cpu().numpy())
             return f"row {first}" if bad else None
 
-        return dict(dm=dm, x=x, y=y, loc=loc, rows=loc.n_rows, nnz=loc.nnz,
+        return dict(dm=dm, x=x, y=y, loc=loc, rows=loc.n_rows, nnz=loc.nnz, hot=hot,
                     bytes_rank=sa.bytes_alg(loc.n_rows, loc.n_cols, loc.nnz), bytes_total=sa.bytes_alg(n, n, z),
                     nnz_total=z, check=check, scaling="strong",
-                    data="synthetic: R-MAT (a,b,c,d)=(.57,.19,.19,.05), 1e7 rows, 1e8 entries, seed 1, x[j] = j",
-                    config={"workload": f"{args.format} SpMV on R-MAT 1e7/1e8 row-sharded over {world} GPU(s) "
-                                        "(BASELINE.json configs[3])"})
+                    data=f"synthetic: R-MAT (a,b,c,d)=(.57,.19,.19,.05), {n:.0e} rows, {z:.0e} entries, seed 1, "
+                         "x[j] = j",
+                    config={"workload": f"{args.format} SpMV on R-MAT {n:.0e}/{z:.0e} row-sharded over {world} "
+                                        "GPU(s) (BASELINE.json configs[3])", "layout": layout})
     # banded
     n = args.banded_rows
     lo, hi = banded_bounds(n, world)[rank:rank + 2]
@@ -437,9 +451,15 @@ def build_workload(args, torch, dev, rank, world):
                                     f"row-sharded over {world} GPU(s) (BASELINE.json configs[4])"})
 
 
-def cpu_baseline(m_single_csr, copies, budget_s):
+CPU_SWEEP_BYTES = 2 << 30  # > every host's last-level caches together (cold CPU passes)
+
+
+def cpu_baseline(m_single_csr, copies, budget_s, cold=False):
     """The oracle's restatement of the reference's OpenMP CSR loop
-    (reference csr.c:285-309) on the same batch, bounded to ~budget_s."""
+    (reference csr.c:285-309) on the same batch, bounded to ~budget_s.
+    cold: before every timed pass all threads sweep a 2 GiB buffer
+    (oracle_sweep), so the pass reads the matrix from DRAM, as the cold GPU
+    step reads it from HBM; the sweep is not timed."""
     from oracle import oracle
 
     ptr, col, val, n_rows, n_cols = m_single_csr
@@ -452,17 +472,24 @@ def cpu_baseline(m_single_csr, copies, budget_s):
     x = np.arange(B * n_cols, dtype=np.float64)
     y = np.empty(B * n_rows, np.float64)
     threads = oracle.max_threads()
+    scratch = np.zeros(CPU_SWEEP_BYTES, np.uint8) if cold else None
     times = []
     t_end = time.perf_counter() + budget_s
     while time.perf_counter() < t_end or len(times) < 3:
+        if cold:
+            oracle.sweep(scratch, threads)
         times.append(oracle.cpu_csr_omp(B * n_rows, bptr, bcol, bval, x, y, threads))
         if len(times) >= 200_000:  # ~10 s of passes on one cant-like matrix (~0.1 ms each)
             break
     t = float(np.median(times))
     b = sa.bytes_alg(B * n_rows, B * n_cols, B * int(ptr[-1]))
+    state = ("cold: a 2 GiB all-thread sweep before every pass evicts the host caches (not timed)" if cold
+             else "warm: every pass re-reads what the last one left in the host caches")
     return {"value": round(b / t * 1e-9, 2), "unit": "GB/s", "cores": threads, "kind": "port",
             "sample": f"oracle OpenMP CSR loop (reference csr.c:285-309) over the same {B}-copy batch, "
-                      f"{len(times)} passes in ~{sum(times):.1f} s, median {t * 1e3:.2f} ms/pass",
+                      f"{len(times)} passes in ~{sum(times):.1f} s of timed passes, median {t * 1e3:.3f} ms/pass; "
+                      + state,
+            "state": "cold" if cold else "warm",
             "gflops": round(2 * B * int(ptr[-1]) / t * 1e-9, 2)}
 
 
@@ -540,10 +567,9 @@ def single_cold(args, torch, dev, rank, world, dist, cdev, prof):
     captured in one HIP graph, replayed once untimed, and replayed once
     between barrier + synchronize on both sides (the timed region); then a
     graph of K flushes alone is timed the same way, so the in-process cold
-    SpMV time is (span(K x (flush + SpMV)) - span(K x flush)) / K.  The
-    headline's SpMV time is the rocprofv3 trace median of the same kernel
-    cold (`prof`, this rank's cant_single child) when every rank has one,
-    else the in-process figure on every rank; max over ranks."""
+    SpMV time is (span(K x (flush + SpMV)) - span(K x flush)) / K, max over
+    ranks: the headline.  The rocprofv3 trace median and mean of the same
+    kernel cold (`prof`, this rank's cant_single child) go beside it."""
     m = sa.gen_cantlike(0, 1)
     b = sa.bytes_alg(m.n_rows, m.n_cols, m.nnz)
     fk = fmt_kwargs(args, args.format)
@@ -603,32 +629,41 @@ def single_cold(args, torch, dev, rank, world, dist, cdev, prof):
     bad, first = sa.check(m, xh, y.cpu().numpy())
     all_ok(dist, cdev, torch, bad == 0, f"cant-like single matrix, row {first}", rank)
 
+    # the headline is the in-process figure: the timed region's
+    # own span difference; the child's rocprofv3 trace of the same kernel
+    # cold (median and mean of 50 launches) is reported beside it
     rec = (prof or {}).get("formats", {}).get(args.format, {}) if isinstance(prof, dict) else {}
-    traced = rec.get("cold_ms")
-    have = torch.tensor([1.0 if traced else 0.0], dtype=torch.float64, device=cdev)
-    if dist is not None:
-        dist.all_reduce(have, op=dist.ReduceOp.MIN)
-    use_trace = bool(have.item())
-    t = torch.tensor([traced if use_trace else inproc, inproc, wall * 1e3 / K], dtype=torch.float64, device=cdev)
+    traced, traced_mean = rec.get("cold_ms"), rec.get("cold_ms_mean")
+    t = torch.tensor([inproc, wall * 1e3 / K], dtype=torch.float64, device=cdev)
     per_rank = [float(t[0].item())]
     if dist is not None:
-        g = [torch.zeros(3, dtype=torch.float64, device=cdev) for _ in range(world)]
+        g = [torch.zeros(2, dtype=torch.float64, device=cdev) for _ in range(world)]
         dist.all_gather(g, t)
         per_rank = [float(v[0].item()) for v in g]
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    cold_ms, inproc_max, wall_step = (float(v) for v in t.tolist())
+    cold_ms, wall_step = (float(v) for v in t.tolist())
     kernels = rec.get("kernels") or [kernel_name(args, dm)]
     params = {k: v for k, v in dm.params.items() if isinstance(v, (int, float, str))}
     del dm
     torch.cuda.empty_cache()
+    corr = None
+    if traced:
+        corr = {"kernel_ms_median": traced, "kernel_ms_mean": traced_mean,
+                "in_process_over_trace_mean": round(cold_ms / traced_mean, 4) if traced_mean else None,
+                "in_process_over_trace_median": round(cold_ms / traced, 4),
+                "source": "rocprofv3 kernel trace of tools/cant_single.py, 50 cold launches" +
+                          (" (rank 0's GPU)" if world > 1 else ""),
+                "note": "the in-process span difference also holds the gap between the flush and the SpMV "
+                        "kernel inside the graph (~1 us); the trace times the kernel alone"}
     return {"cold_ms": cold_ms, "bytes": b, "nnz": m.nnz, "rows": m.n_rows, "kernels": kernels, "params": params,
-            "source": ("rocprofv3 kernel trace of tools/cant_single.py (median of 50 cold launches, every rank)"
-                       if use_trace else "in-process: (span of K x (flush + SpMV) - span of K x flush) / K"),
+            "source": "in-process: (span of K x (flush + SpMV) - span of K x flush) / K, HIP events on the launch "
+                      "stream, max over ranks",
+            "trace": corr,
             "timed_region": {"what": f"{K} x (512 MiB flush + one SpMV), "
                                      + ("one HIP graph replay" if GRAPH["on"] else "eager launches")
                                      + " between barrier + synchronize",
                              "wall_ms": round(wall * 1e3, 4), "wall_ms_per_step_incl_flush": round(wall_step, 5),
-                             "cold_spmv_ms_in_process": round(inproc_max, 5),
+                             "cold_spmv_ms_in_process": round(cold_ms, 5),
                              "cold_spmv_ms_rocprof_rank0": traced,
                              "cold_ms_per_rank": [round(v, 5) for v in per_rank]},
             "parity_ok": True,
@@ -681,6 +716,28 @@ def strong_exchange(torch, comm, cdev, dm, x, y_full, lo, hi, bounds, steps, flu
     return how, float(t[0].item()), float(t[1].item()), cold
 
 
+def rmat_matrix(args):
+    """The R-MAT of configs[3] (default 1e7 rows / 1e8 entries; smaller with
+    --rmat-rows / --rmat-nnz for tests), deterministic on every rank."""
+    n, z = args.rmat_rows, args.rmat_nnz
+    return sa.gen_rmat(n, z, scale=max(1, (n - 1).bit_length()))
+
+
+def rmat_layout(args, n, col):
+    """(col, x host, hot kwarg, label): with the relabel (default) the CSR's
+    columns are renumbered by decreasing degree once at build time and x is
+    replicated in that layout (x'[k] = x[order[k]]: the replication step,
+    SURVEY.md §8e, delivers it; outside the timed SpMV), so no per-run
+    hot-table fill runs and the touched part of x is one dense prefix; y
+    keeps the original row order.  Otherwise the per-run hot-column table."""
+    xh = sa.ramp_x(n)
+    if args.relabel == "no":
+        return col, xh, None, "hot-column table (per-run fill of the 2^19 hottest x entries)"
+    order, _, col2 = sa.column_relabel(n, col)
+    return col2, np.ascontiguousarray(xh[order]), 0, ("columns relabelled by decreasing degree at build time "
+                                                     "(spmv_column_relabel); x replicated in that layout")
+
+
 def rmat_strong(args, torch, dev, rank, world, dist, cdev):
     """North-star sweep (BASELINE.json north_star, configs[3]): CSR on the
     1e7 x 1e7 / 1e8-entry R-MAT, rows cut into `world` shards, one per
@@ -690,31 +747,56 @@ def rmat_strong(args, torch, dev, rank, world, dist, cdev):
     The cut is profile-guided: the weighted cut (entries + RMAT_ROW_WEIGHT
     x rows, 1024-aligned) is timed (20 steps), every rank's shard time is
     all-gathered, and spmv_partition_rows_calibrated re-cuts the rows into
-    equal shares of the measured cost, twice (`calibration`); the measured
-    cut with the lowest max shard time is kept (the same on every rank).
-    The R-MAT's hub shard costs more per entry than shards of short rows,
-    and no single row weight balances 2, 4 and 8 shards
-    (profiles/round2/shard_rehearse_w_g248.log, shard_rehearse_calibrated.log).
-    Setup only: the timed steps are the same SpMV on the final shards.
-    Then the exchange on the final cut (strong_exchange): y all-gathered
-    with the real shard sizes, SpMV + all-gather, cold shards.  Every rank
-    checks its shard; rank 0 checks the whole gathered y."""
+    equal shares of the measured cost (`calibration`, on cold times with
+    --flush yes); the measured cut with the lowest max shard time is kept
+    (the same on every rank).  Setup only: the timed steps are the same
+    SpMV on the final shards.  At N > 1, rank 0 first times the WHOLE
+    matrix alone (warm and cold) in the same job, so the line carries its
+    own strong-scaling speed-ups (speedup_warm / speedup_cold = whole /
+    max shard).  Then the exchange on the final cut (strong_exchange): y
+    all-gathered with the real shard sizes, SpMV + all-gather, cold
+    shards.  Every rank checks its shard; rank 0 checks the whole gathered
+    y against the ORIGINAL (un-relabelled) matrix and x."""
     t0 = time.perf_counter()
-    full = sa.gen_rmat()  # deterministic: every rank builds the same matrix
+    full = rmat_matrix(args)  # deterministic: every rank builds the same matrix
     ptr, col, val = sa.csr_from_coo(full)
     n, z = full.n_rows, full.nnz
     if rank != 0:
         del full
-    x = torch.from_numpy(sa.ramp_x(n)).to(dev)
+    col, xh, hot, layout = rmat_layout(args, n, col)
+    x = torch.from_numpy(xh).to(dev)
     b_total = sa.bytes_alg(n, n, z)
     steps = max(20, args.steps // 2)
+    calib = args.flush == "yes"  # cut on COLD shard times (each shard flushed first), else warm
+    recuts = RMAT_RECUTS if args.recuts is None else args.recuts
+
+    def rows_of(lo, hi):
+        lptr = ptr[lo:hi + 1] - ptr[lo]
+        return sa.Coo(hi - lo, n, np.repeat(np.arange(hi - lo, dtype=np.int32), np.diff(lptr)),
+                      col[ptr[lo]:ptr[hi]], val[ptr[lo]:ptr[hi]])
 
     def shard(bounds):
         lo, hi = int(bounds[rank]), int(bounds[rank + 1])
-        lptr = ptr[lo:hi + 1] - ptr[lo]
-        loc = sa.Coo(hi - lo, n, np.repeat(np.arange(hi - lo, dtype=np.int32), np.diff(lptr)),
-                     col[ptr[lo]:ptr[hi]], val[ptr[lo]:ptr[hi]])
-        return loc, sa.to_device(loc, "csr", dev), lo, hi
+        loc = rows_of(lo, hi)
+        return loc, sa.to_device(loc, "csr", dev, hot=hot), lo, hi
+
+    # the whole matrix alone on rank 0 (N > 1): the 1-GPU reference of the
+    # speed-ups, measured in the same job as the shards
+    whole = None
+    if world > 1:
+        if rank == 0:
+            loc = rows_of(0, n)
+            dm = sa.to_device(loc, "csr", dev, hot=hot)
+            y = torch.empty(n, dtype=torch.float64, device=dev)
+            _, kern = time_steps(torch, dm, x, y, 20, 5)
+            bad, first = sa.check(loc, xh, y.cpu().numpy())
+            c = cold_step_ms(torch, dm, x, y, 10) if calib else None
+            whole = {"ms": float(np.mean(kern)), "cold_ms": c, "parity_ok": bad == 0}
+            del dm, y, loc
+            torch.cuda.empty_cache()
+            if bad:
+                print(f"rank 0: whole R-MAT parity failure at row {first}", file=sys.stderr)
+        all_ok(dist, cdev, torch, whole is None or whole["parity_ok"], "whole R-MAT (rank 0 alone)", rank)
 
     def run(bounds, k, cold=False):
         """Warm steps of the cut (and with `cold`, each shard's cold time,
@@ -722,7 +804,7 @@ def rmat_strong(args, torch, dev, rank, world, dist, cdev):
         loc, dm, _, _ = shard(bounds)
         y = torch.empty(max(loc.n_rows, 1), dtype=torch.float64, device=dev)
         wall, kern = time_steps(torch, dm, x, y, k, 5, dist)
-        bad, first = sa.check(loc, sa.ramp_x(n), y[:loc.n_rows].cpu().numpy())
+        bad, first = sa.check(loc, xh, y[:loc.n_rows].cpu().numpy())
         all_ok(dist, cdev, torch, bad == 0, f"R-MAT shard row {first}", rank)
         params = {kk: v for kk, v in dm.params.items() if isinstance(v, (int, float, str))}
         t = torch.tensor([wall / k * 1e3, float(np.mean(kern))], dtype=torch.float64, device=cdev)
@@ -740,14 +822,14 @@ def rmat_strong(args, torch, dev, rank, world, dist, cdev):
         return float(t[0].item()), float(t[1].item()), shard_ms, params, shard_cold
 
     bounds0 = sa.partition_rows(n, ptr, world, align=1024, row_weight=RMAT_ROW_WEIGHT)
-    calib = args.flush == "yes"  # cut on COLD shard times (each shard flushed first), else warm
     step0, _, shard0, _, cold0 = run(bounds0, 20, cold=calib and world > 1)
     bounds, passes = bounds0, []
     if world > 1:  # re-cuts, each from the previous cut's measured (cold) times;
         key0 = cold0 if calib and min(cold0) > 0 else shard0
         b, t, best = bounds0, key0, (max(key0), bounds0)  # the measured cut with the lowest max is kept
-        for _ in range(RMAT_RECUTS):
-            b = sa.partition_rows_calibrated(n, ptr, world, b, t, align=1024, row_weight=RMAT_ROW_WEIGHT)
+        for _ in range(recuts):
+            nb = sa.partition_rows_calibrated(n, ptr, world, b, t, align=1024, row_weight=RMAT_ROW_WEIGHT)
+            b = sa.partition_rows_damped(n, b, nb, RMAT_DAMP)
             _, _, tw, _, tc = run(b, 20, cold=calib)
             t = tc if calib and min(tc) > 0 else tw
             passes.append({"shard_rows": np.diff(b).tolist(), "shard_ms": [round(v, 5) for v in tw],
@@ -762,20 +844,20 @@ def rmat_strong(args, torch, dev, rank, world, dist, cdev):
     y_full = torch.full((n,), float("nan"), dtype=torch.float64, device=dev)
     how, ag_ms, both_ms, cold = strong_exchange(torch, comm, cdev, dm, x, y_full, lo, hi, bounds, steps,
                                                 args.flush == "yes")
-    whole = None
-    if rank == 0:  # the gathered y of the whole matrix against the host rule
+    bad_whole = None
+    if rank == 0:  # the gathered y against the ORIGINAL matrix and x (host rule)
         bad, first = sa.check(full, sa.ramp_x(n), y_full.cpu().numpy())
-        whole = None if bad == 0 else f"gathered R-MAT y, row {first}"
+        bad_whole = None if bad == 0 else f"gathered R-MAT y, row {first}"
         del full
-    all_ok(dist, cdev, torch, whole is None, str(whole), rank)
+    all_ok(dist, cdev, torch, bad_whole is None, str(bad_whole), rank)
     del dm, y_full
     torch.cuda.empty_cache()
 
     def gbs(ms):
         return round(b_total / (ms * 1e-3) * 1e-9, 1) if ms and ms > 0 else None
 
-    out = {"workload": "csr SpMV on R-MAT 1e7/1e8 (configs[3]) row-sharded over all ranks, x replicated",
-           "scaling": "strong", "steps": steps,
+    out = {"workload": f"csr SpMV on R-MAT {n:.0e}/{z:.0e} (configs[3]) row-sharded over all ranks, x replicated",
+           "layout": layout, "scaling": "strong", "steps": steps,
            "aggregate_GBs": gbs(step_ms),
            "GFLOPs": round(2 * z / (step_ms * 1e-3) * 1e-9, 1),
            "frac_of_one_gpu_peak": round(b_total / (step_ms * 1e-3) * 1e-9 / sa.HBM_PEAK_GBS, 4),
@@ -785,10 +867,12 @@ def rmat_strong(args, torch, dev, rank, world, dist, cdev):
            "allgather": {"how": how, "bytes_received_rank0": 8 * (n - (hi - lo)) if rank == 0 else None,
                          "ms": round(ag_ms, 5), "spmv_plus_allgather_ms": round(both_ms, 5),
                          "aggregate_GBs_with_allgather": gbs(both_ms),
-                         "gathered_y_parity": "rank 0 checks all 1e7 rows of the gathered y"},
+                         "gathered_y_parity": "rank 0 checks all rows of the gathered y against the original "
+                                              "matrix and x"},
            "partition": ("profile-guided: weighted cut (row weight %g) and %d re-cuts by measured %s cost "
-                         "timed, the one with the lowest max %s shard time kept"
-                         % (RMAT_ROW_WEIGHT, RMAT_RECUTS, "cold" if calib else "warm", "cold" if calib else "warm"))
+                         "(each moving the cut points %g of the way) timed, the one with the lowest max %s "
+                         "shard time kept" % (RMAT_ROW_WEIGHT, recuts, "cold" if calib else "warm", RMAT_DAMP,
+                                               "cold" if calib else "warm"))
                         if world > 1 else "whole matrix",
            "calibration": {"weighted_cut": {"shard_rows": np.diff(bounds0).tolist(),
                                             "shard_ms": [round(v, 5) for v in shard0],
@@ -802,6 +886,14 @@ def rmat_strong(args, torch, dev, rank, world, dist, cdev):
         out["cold"] = {"how": "per rank: graph of K x (512 MiB flush + SpMV) minus a graph of K flushes",
                        "shard_ms": [round(v, 5) for v in cold], "max_shard_ms": round(cm, 5),
                        "aggregate_GBs": gbs(cm)}
+    # strong-scaling speed-ups from this job's own 1-GPU figure (rank 0 alone)
+    w_ms = whole["ms"] if whole else kern_ms
+    w_cold = (whole or {}).get("cold_ms") if world > 1 else (min(cold) if cold else None)
+    out["whole_matrix_one_gpu"] = {"ms": round(w_ms, 5), "cold_ms": round(w_cold, 5) if w_cold else None,
+                                   "how": "rank 0 alone, before the shards, same job" if world > 1
+                                          else "N = 1: the one shard is the whole matrix"}
+    out["speedup_warm"] = round(w_ms / kern_ms, 3) if kern_ms > 0 else None
+    out["speedup_cold"] = round(w_cold / max(cold), 3) if w_cold and cold and max(cold) > 0 else None
     return out
 
 
@@ -887,12 +979,15 @@ def batch_leg(args, torch, dev, rank, world, dist, cdev):
     return w, ms_per_step, kern_ms, roof
 
 
-def per_format_leg(args, torch, dev, m, x, y, nnz, bytes_step):
-    """Every format on the same matrix (R-MAT: ELL is N/A, padding)."""
+def per_format_leg(args, torch, dev, m, x, y, nnz, bytes_step, hot=None):
+    """Every format on the same matrix (R-MAT: ELL is N/A, padding).  hot:
+    the hot-column kwarg of a relabelled matrix (0: no per-run table)."""
     per_format = {}
     x_host = x.cpu().numpy()
     for fmt in sa.ALL_FORMATS:
         kw = fmt_kwargs(args, fmt)
+        if hot is not None and fmt in ("coo", "csr", "csrf32", "cmrs", "sell", "hyb"):
+            kw = dict(kw, hot=hot)
         try:
             d2 = sa.to_device(m, fmt, dev, **kw)
         except sa.SpmvError as e:
@@ -986,7 +1081,8 @@ def main():
                     "frac": round(bytes_step / (ms_per_step * 1e-3) * 1e-9 / sa.HBM_PEAK_GBS, 4),
                     "traffic": traffic_for(args.format, bytes_step, kname, cold=True),
                     "kernel": kname, "kernels": s["kernels"], "kernel_ms": round(ms_per_step, 5),
-                    "kernel_ms_source": s["source"], "bytes_alg_per_launch": bytes_step,
+                    "kernel_ms_source": s["source"], "kernel_ms_trace": s["trace"],
+                    "bytes_alg_per_launch": bytes_step,
                     "state": "cold: 512 MiB flush before every launch"}
         scaling, n_rows, nnz = "weak", s["rows"], s["nnz"]
         data = ("synthetic: cant-like stand-in (62,451 rows, 4,007,383 entries = SuiteSparse cant's counts; the "
@@ -994,7 +1090,13 @@ def main():
         config = {"workload": f"{args.format} SpMV on ONE cant-like matrix per GPU (BASELINE.json "
                               + ("configs[2]" if args.format == "sell" else "configs[1]")
                               + "), cold: 512 MiB flush before every step; N GPUs run N replicas, no collective",
-                  "timed_region": s["timed_region"], "kernel_params": s["params"]}
+                  "timed_region": s["timed_region"], "kernel_params": s["params"],
+                  "ms_per_step_is": "the SpMV's share of one step (the step's 512 MiB flush excluded; the "
+                                    "wall clock per step with it is timed_region.wall_ms_per_step_incl_flush)"}
+        if world > 1:
+            config["value_is"] = ("replica throughput: N independent copies of configs[1], one per GPU, no "
+                                  "exchange (weak scaling); the strong-scaling evidence is rmat_strong."
+                                  "speedup_cold / speedup_warm")
         launch_desc = s["timed_region"]["what"]
         do_batch = args.batch == "yes" or (args.batch == "auto" and world == 1)
         if do_batch:
@@ -1012,11 +1114,15 @@ def main():
             del w
             torch.cuda.empty_cache()
         if rank == 0 and world == 1 and args.cpu_seconds > 0:
+            # cold, like the GPU headline (2/3 of the budget), and warm beside it
             sm = sa.gen_cantlike(0, 1)
             ptr, col, val = sa.csr_from_coo(sm)
-            cpu = cpu_baseline((ptr, col, val, sm.n_rows, sm.n_cols), 1, args.cpu_seconds)
-            cpu["sample"] = cpu["sample"].replace("the same 1-copy batch", "the same single cant-like matrix "
-                                                  "(host caches warm: a CPU pass re-reads what the last left)")
+            arrs = (ptr, col, val, sm.n_rows, sm.n_cols)
+            cpu = cpu_baseline(arrs, 1, args.cpu_seconds * 2 / 3, cold=True)
+            warm = cpu_baseline(arrs, 1, args.cpu_seconds / 3)
+            for c in (cpu, warm):
+                c["sample"] = c["sample"].replace("the same 1-copy batch", "the same single cant-like matrix")
+            cpu["warm"] = {k: warm[k] for k in ("value", "unit", "cores", "sample", "gflops")}
     else:
         w = build_workload(args, torch, dev, rank, world)
         dm, x, y = w["dm"], w["x"], w["y"]
@@ -1073,7 +1179,7 @@ def main():
             m = w["loc"] if args.workload == "rmat" else w["m"]
             del dm, w["dm"]
             torch.cuda.empty_cache()
-            per_format = per_format_leg(args, torch, dev, m, x, y, nnz, bytes_step)
+            per_format = per_format_leg(args, torch, dev, m, x, y, nnz, bytes_step, w.get("hot"))
             if args.cpu_seconds > 0:
                 if args.workload == "rmat":
                     ptr, col, val = sa.csr_from_coo(m)
@@ -1123,6 +1229,9 @@ def main():
             "per_format": per_format,
             "allgather": allgather,
             "rmat_strong": rstrong,
+            "strong_scaling": ({"rmat_speedup_cold": rstrong.get("speedup_cold"),
+                                "rmat_speedup_warm": rstrong.get("speedup_warm"),
+                                "n_gpus": world, "layout": rstrong.get("layout")} if rstrong else None),
             "banded_strong": bstrong,
             "device": sa.device_name(gpu),
         }

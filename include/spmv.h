@@ -231,6 +231,13 @@ int spmv_hyb_run_tail(spmv_dims d, int32_t K, int64_t ld, int32_t ki, const int3
                       const int32_t *tail_col, const double *tail_val, const double *x, double *y,
                       const void *tails);
 
+/* spmv_hyb_run_tail with the ELL part through the x-window ELL kernel
+ * (`win`, `xcap` from spmv_ell_xwin_build over ell_col); same bits. */
+int spmv_hyb_run_tail_xwin(spmv_dims d, int32_t K, int64_t ld, int32_t ki, const int32_t *ell_col,
+                           const double *ell_val, int64_t tail_nnz, const int32_t *tail_row,
+                           const int32_t *tail_col, const double *tail_val, const double *x, double *y,
+                           const void *tails, const void *win, int32_t xcap);
+
 /* -------------------------------------------------------- SELL-C-sigma ---
  * Replaces kernel `sigma_c(val,idx,x,y,slice_ptr,int C)` (reference
  * kernels/Sigma_C.cl:1) and its launch (reference sigma_c.c:50-51,71-72,

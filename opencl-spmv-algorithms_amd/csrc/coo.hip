@@ -164,9 +164,13 @@ extern "C" int spmv_coo_tail_build(spmv_dims d, const int32_t *row, void *tails,
     const int64_t mx = coo_tail_build(d, row, (int32_t *)tails);
     if (mx < 0)
         return fail_msg(SPMV_PROGRAM_ERROR, "spmv_coo_tail_build: plan kernel");
-    if (mx > coo_tail_cap())
+    if (mx > coo_tail_cap()) {
+        // a refused plan is zeroed, so passing it anyway cannot overrun the
+        // kernel's staged tail; its y would be wrong, not unsafe
+        (void)hipMemsetAsync(tails, 0, spmv_coo_tail_bytes(d.nnz), (hipStream_t)d.stream);
         return fail_msg(SPMV_OTHER_ERROR,
                         "spmv_coo_tail_build: a row runs more than 80 entries past its tile (use spmv_coo_run)");
+    }
     return SPMV_SUCCESS;
 }
 

@@ -1226,6 +1226,28 @@ extern "C" int spmv_hyb_run_tail(spmv_dims d, int32_t K, int64_t ld, int32_t ki,
                                  (const int32_t *)tails);
 }
 
+// HYB with a single-pass tail and the ELL part through the x-window ELL
+// kernel (`win`/`xcap` from spmv_ell_xwin_build over ell_col): same bits as
+// spmv_hyb_run_tail (the window only moves where x is read from).
+extern "C" int spmv_hyb_run_tail_xwin(spmv_dims d, int32_t K, int64_t ld, int32_t ki, const int32_t *ell_col,
+                                      const double *ell_val, int64_t tail_nnz, const int32_t *tail_row,
+                                      const int32_t *tail_col, const double *tail_val, const double *x, double *y,
+                                      const void *tails, const void *win, int32_t xcap)
+{
+    if (tail_nnz < 0)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_hyb_run_tail_xwin: negative tail size");
+    int rc = spmv_ell_run_xwin(d, K, ld, ki, ell_col, ell_val, x, y, win, xcap);
+    if (rc != SPMV_SUCCESS || tail_nnz == 0 || d.n_rows == 0)
+        return rc;
+    if (!tails)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_hyb_run_tail_xwin: no tail plan");
+    SPMV_GUARD(d);
+    spmv_dims dt = d;
+    dt.nnz = tail_nnz;
+    return launch_coo_staged_acc(dt, tail_row, tail_col, tail_val, x, y, nullptr, nullptr,
+                                 (const int32_t *)tails);
+}
+
 extern "C" size_t spmv_sell_split_ws_bytes(int64_t n_chunks, int32_t C)
 {
     return n_chunks > 0 && C > 0 ? (size_t)n_chunks * C * sizeof(double) : 0;

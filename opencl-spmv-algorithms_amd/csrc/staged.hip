@@ -284,7 +284,11 @@ __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
     const int64_t t0 = tile * CH;
     const int64_t t1 = t0 + CH < nnz ? t0 + CH : nnz;
     const int n = (int)(t1 - t0);
-    const int tail = TAIL ? tails[tile] : 0;  // uniform; > 0 only for full tiles (n even)
+    // uniform; > 0 only for full tiles (n even).  Clamped to the staged
+    // capacity, so a plan built for other row arrays cannot write past the
+    // LDS tail (spmv_coo_tail_build zeroes a plan it refuses)
+    int tail = TAIL ? tails[tile] : 0;
+    tail = tail < 0 ? 0 : (tail > 2 * TP ? 2 * TP : tail);
     if (threadIdx.x == 0)
         s_prev = t0 > 0 ? row[t0 - 1] : -1;
     const KeysRow32<NT> keys{row, s_row2};
@@ -756,23 +760,26 @@ int launch_cmrs_tiled(const spmv_dims &d, int32_t h, int64_t n_strips, const int
     return launch_carry((int64_t)h * tiles, carry_row, carry_val, y, st);
 }
 
-// Tile = 2·kBlock·R entries.  R = 2 (1,024-entry tiles) for mean rows of
-// 6-95 entries, R = 3 from 96, R = 1 below 6 (mostly empty rows: an R-MAT
-// shard of high row ids, 2.8 M rows / 9.4 M entries, ran 0.1255 -> 0.1371 ms
-// warm and 0.1436 -> 0.1724 ms cold with R = 2 tiles, as a 1,024-entry tile
-// then owns more rows than its LDS offset table; shard_rehearse_cold_b.log).  Round 2 picked R = 1 for R-MAT-like rows
-// (0.826 / 0.831 / 0.861 ms with R = 1 / 2 / 3, profiles/round2/ab_tiled_r.log)
-// while hub rows were summed by L = 2 lanes per tile; with the wave-per-long-
-// row phase the whole R-MAT runs 0.800 / 0.785 / 0.788 ms and the tile
-// structure alone (every column 0) 0.386 / 0.327 / 0.345 ms
-// (profiles/round3/rmat_tiled_r.log).  Hub shards, whose rows run over many
-// tiles, ran best with R = 3 in round 2 (ab_tiled_r_hub.log).  Workspaces
-// and plans are sized for the smallest tile (R = 1).
+// Tile = 2·kBlock·R entries.  Round 5: R = 1 (512-entry tiles) for every
+// matrix.  With the R-MAT's columns relabelled by degree (no hot table) the
+// whole matrix ran 0.772-0.777 ms cold with R = 1 against 0.784-0.785 with
+// the round-4 rule (R = 2 for mean rows of 6-95 entries, 3 from 96) and
+// 0.806 with R = 3, and every 8-way shard was as fast or faster, the hub
+// shard (mean row 179) 0.124 vs 0.130 ms (profiles/round5/ab_tiled_r.md):
+// a shard's ~1e4 tiles fill the chip ~6 times, so halving the tile halves
+// the grid's tail.  History: round 2 picked R = 1 for R-MAT-like rows
+// (0.826 / 0.831 / 0.861 ms with R = 1 / 2 / 3, profiles/round2/ab_tiled_r.log);
+// with round 3's wave-per-long-row phase the hot-table R-MAT ran 0.800 /
+// 0.785 / 0.788 ms (profiles/round3/rmat_tiled_r.log).  Workspaces and plans
+// are sized for the smallest tile (R = 1).
 static int tiled_r(int64_t n_rows, int64_t nnz)
 {
-    if (n_rows > 0 && (double)nnz >= 96.0 * (double)n_rows)
-        return 3;
-    return n_rows > 0 && (double)nnz >= 6.0 * (double)n_rows ? 2 : 1;
+#ifdef SPMV_TILED_R_FORCE  // A/B builds only (lab/build_variant.sh); the product uses the rule below
+    return SPMV_TILED_R_FORCE;
+#endif
+    (void)n_rows;
+    (void)nnz;
+    return 1;
 }
 
 int64_t csr_tiled_tile(int64_t n_rows, int64_t nnz) { return 2 * kBlock * tiled_r(n_rows, nnz); }

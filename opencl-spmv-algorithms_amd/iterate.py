@@ -38,6 +38,7 @@ CPU ranks (gloo); the product path only ever builds HipKernels.
 """
 from __future__ import annotations
 
+import contextlib
 from dataclasses import dataclass
 
 import numpy as np
@@ -285,18 +286,35 @@ class _Apply:
 
     def __call__(self, y) -> None:
         op, comm = self.op, self.comm
+        st = getattr(op.kernels, "stream", None)
+        cur = sa._torch().cuda.current_stream(st.device) if st is not None else None
+        # the collective (or the one-rank copy) runs on torch's current
+        # stream and reads `send`, which the kernels' stream produced: order
+        # it behind them (both directions)
+        _order(st, cur)
         if op.remote is None:
             comm.allgather(self.full, self.send)
+            _order(cur, st)
             op.kernels.spmv(self.full, y)
             return
         work = comm.allgather_start(self.full, self.send)
-        st = getattr(op.kernels, "stream", None)
+        if work is None:
+            _order(cur, st)  # one rank: the copy was queued on the current stream
         if not op.overlap:
             comm.wait(work, st)
         op.kernels.spmv(self.send, y)  # own block only: runs while the exchange is in flight
         comm.wait(work, st)
         op.remote.spmv(self.full, self.y2)
         op.kernels.axpy_ratio(op.rows, self.one, self.one, 1.0, self.y2, y)  # y += y_remote, exact
+
+
+def _order(src, dst) -> None:
+    """dst waits for the work queued on src so far (no-op for one stream)."""
+    if src is None or dst is None or src.cuda_stream == dst.cuda_stream:
+        return
+    ev = sa._torch().cuda.Event()
+    ev.record(src)
+    dst.wait_event(ev)
 
 
 def _gathered_pair(op, comm):
@@ -308,8 +326,24 @@ def _gathered_pair(op, comm):
 
 
 # -------------------------------------------------------- power iteration
+def _kernel_stream(op):
+    """Context that makes the operator's kernel stream torch's current one
+    for a whole solve, so torch copies, host reads and the collectives are
+    ordered with the HIP kernels; no-op on the default stream."""
+    st = getattr(op.kernels, "stream", None)
+    return sa._torch().cuda.stream(st) if st is not None else contextlib.nullcontext()
+
+
 def power_iteration(op: DistOperator, iters: int, comm: Comm | None = None, x0=None, graph: bool = False,
                     block: int = 16):
+    """x <- A x / ||A x||, `iters` times, on the operator's kernel stream
+    (_power_iteration has the details)."""
+    with _kernel_stream(op):
+        return _power_iteration(op, iters, comm, x0, graph, block)
+
+
+def _power_iteration(op: DistOperator, iters: int, comm: Comm | None = None, x0=None, graph: bool = False,
+                     block: int = 16):
     """x <- A x / ||A x||, `iters` times.  Returns (hist, x_local): hist is a
     host array [iters, 2] of (x·Ax, ||Ax||²) per iteration — x·Ax converges
     to the dominant eigenvalue of a symmetric A — and x_local is this
@@ -366,6 +400,13 @@ def power_iteration(op: DistOperator, iters: int, comm: Comm | None = None, x0=N
 # ---------------------------------------------------------------------- CG
 def cg(op: DistOperator, b_loc, comm: Comm | None = None, tol: float = 1e-10, maxit: int = 1000,
        check_every: int = 10):
+    """Conjugate gradients on the operator's kernel stream (_cg)."""
+    with _kernel_stream(op):
+        return _cg(op, b_loc, comm, tol, maxit, check_every)
+
+
+def _cg(op: DistOperator, b_loc, comm: Comm | None = None, tol: float = 1e-10, maxit: int = 1000,
+        check_every: int = 10):
     """Conjugate gradients for a symmetric positive definite A, x0 = 0.
     Returns (x_local, iterations, relative residual ||r||/||b||)."""
     comm = comm or Comm()

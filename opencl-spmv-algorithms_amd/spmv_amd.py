@@ -107,6 +107,8 @@ HIP_SYMBOLS = {
                                     ctypes.c_size_t]),
     "spmv_hyb_run_tail": (ctypes.c_int, [Dims, _c_i32, _c_i64, _c_i32, _vp, _vp, _c_i64, _vp, _vp, _vp, _vp, _vp,
                                          _vp]),
+    "spmv_hyb_run_tail_xwin": (ctypes.c_int, [Dims, _c_i32, _c_i64, _c_i32, _vp, _vp, _c_i64, _vp, _vp, _vp, _vp,
+                                              _vp, _vp, _vp, _c_i32]),
     "spmv_csr_xwin_bytes": (ctypes.c_size_t, [_c_i64, _c_i64, ctypes.c_int, _c_i32]),
     "spmv_csr_xwin_build": (ctypes.c_int, [Dims, _vp, _vp, ctypes.c_int, _c_i32, _vp, ctypes.c_size_t,
                                            ctypes.POINTER(_c_i32)]),
@@ -586,6 +588,22 @@ def partition_rows_calibrated(n_rows: int, ptr: np.ndarray, parts: int, old_boun
     return bounds
 
 
+def partition_rows_damped(n_rows: int, old_bounds, new_bounds, damp: float = 0.5, align: int = 1024) -> np.ndarray:
+    """Move every cut point of old_bounds the fraction `damp` of the way to
+    new_bounds (aligned, monotone, ends kept).  Cold shard times are not
+    linear in a shard's rows and entries (a flushed shard also re-reads x
+    and its row offsets), so a full profile-guided re-cut overshoots; half
+    steps settle instead."""
+    ob = np.asarray(old_bounds, dtype=np.float64)
+    nb = np.asarray(new_bounds, dtype=np.float64)
+    if ob.shape != nb.shape or ob[0] != 0 or nb[0] != 0 or ob[-1] != n_rows or nb[-1] != n_rows:
+        raise SpmvError(OTHER_ERROR, "partition_rows_damped", "bounds must share size and ends")
+    b = np.rint((ob + damp * (nb - ob)) / align).astype(np.int64) * align
+    b[0], b[-1] = 0, n_rows
+    b = np.minimum(np.maximum.accumulate(b), n_rows)
+    return b
+
+
 def shard(m: Coo, lo: int, hi: int) -> Coo:
     """Rows [lo, hi) of m as a local matrix (row ids rebased, columns kept:
     x stays replicated)."""
@@ -709,6 +727,11 @@ class DeviceMatrix:
             rc = lib.spmv_hyb_run_hot(d, p["K"], p["ld"], p["ki"], _ptr(a["ell_col"]), _ptr(a["ell_val"]),
                                       p["tail_nnz"], _ptr(a["tail_row"]), _ptr(a["tail_col"]), _ptr(a["tail_val"]),
                                       _ptr(x), _ptr(y), p["H"], _ptr(a["hot"]), _ptr(a["ws"]), a["ws"].numel())
+        elif self.fmt == "hyb" and "tails" in a and "win" in a:
+            rc = lib.spmv_hyb_run_tail_xwin(d, p["K"], p["ld"], p["ki"], _ptr(a["ell_col"]), _ptr(a["ell_val"]),
+                                            p["tail_nnz"], _ptr(a["tail_row"]), _ptr(a["tail_col"]),
+                                            _ptr(a["tail_val"]), _ptr(x), _ptr(y), _ptr(a["tails"]), _ptr(a["win"]),
+                                            p["xcap"])
         elif self.fmt == "hyb" and "tails" in a:
             rc = lib.spmv_hyb_run_tail(d, p["K"], p["ld"], p["ki"], _ptr(a["ell_col"]), _ptr(a["ell_val"]),
                                        p["tail_nnz"], _ptr(a["tail_row"]), _ptr(a["tail_col"]), _ptr(a["tail_val"]),
@@ -908,16 +931,20 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
               xwin: bool | None = None, xwin_rows: int = 0, split: int | None = None,
               cmrs_variant: int | None = None, hot: int | None = None,
               csr16_max_escape: float | None = 0.5, groups: int = 0, head: bool = True,
-              sell_head: bool = False, coo_tail: bool | None = None) -> DeviceMatrix:
+              sell_head: bool | None = None, coo_tail: bool | None = None) -> DeviceMatrix:
     """Build `fmt` on the host (libspmv_host.so) and upload it.  xwin (CSR,
     ELL, SELL; default on): also build the per-workgroup x windows on the
     device and run the LDS x-window kernels (same bits as without).  split
-    (SELL) / cmrs_variant (CMRS): None = the library's skew rule."""
+    (SELL) / cmrs_variant (CMRS): None = the library's skew rule.
+    sell_head (SELL): None = the head copy wherever the small-matrix kernel
+    runs (spmv_sell_head_bytes > 0: one cant-like matrix cold 11.9 -> 11.4 us,
+    same bits).  coo_tail (COO, HYB): None = the single pass where the tail
+    plan accepts the matrix, True = it or raise, False = the carry pass."""
     torch = _torch()
     if xwin is None:
         # COO: per-tile windows measured slower (0.534 vs 0.491 ms on the
         # cant-like batch), so they stay opt-in; CMRS 0.352 vs 0.404 ms
-        xwin = fmt in ("csr", "csr16", "ell", "sell", "cmrs")
+        xwin = fmt in ("csr", "csr16", "ell", "sell", "cmrs", "hyb")
     device = torch.device(device)
     dm = DeviceMatrix(fmt, m.n_rows, m.n_cols, m.nnz, device)
     if fmt == "coo":
@@ -932,6 +959,9 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
         if H > 0:
             dm.arrays["hot"] = _dev_tensor(hot_cols, device)
         dm.stored_bytes = 16 * m.nnz
+        if coo_tail and (xwin or H > 0):  # never drop an explicit request silently
+            raise SpmvError(OTHER_ERROR, "to_device", "coo_tail=True needs xwin=False and no hot-column table "
+                            "(hot=0): the x-window and hot-table COO paths use the carry pass")
         if xwin and H == 0:
             _coo_xwin(dm)
         elif H == 0 and coo_tail is not False and m.nnz > 0:
@@ -1033,7 +1063,7 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
             _sell_xwin(dm)
         _sell_split(dm, s["slice_ptr"], split)
         _sell_hot(dm, s["col"][: s["stored"]], hot)
-        if sell_head and xwin and dm.params.get("split_T", 0) == 0 and dm.params.get("H", 0) == 0:
+        if sell_head is not False and xwin and dm.params.get("split_T", 0) == 0 and dm.params.get("H", 0) == 0:
             hb = hip_lib().spmv_sell_head_bytes(s["n_slices"], C, ki)
             if hb > 0:  # small matrix: the head copy of every wave's first slot groups
                 a = dm.arrays
@@ -1112,6 +1142,17 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
                 dm.params["single_pass"] = 1
             elif coo_tail:
                 raise SpmvError(rc, "spmv_coo_tail_build (hyb tail)", hip_lib().spmv_last_error().decode())
+        if xwin and "tails" in dm.arrays and hb["stored"] > 0:
+            # the ELL part through the x-window ELL kernel (same bits): one
+            # cant-like matrix cold, a full ELL 12.26 vs 13.36 us
+            a, p = dm.arrays, dm.params
+            nbytes = hip_lib().spmv_ell_xwin_bytes(dm.n_rows)
+            a["win"] = torch.empty(max(nbytes, 8), dtype=torch.uint8, device=device)
+            cap = _c_i32(0)
+            _check(hip_lib().spmv_ell_xwin_build(dm.dims(), p["K"], p["ld"], p["ki"], _ptr(a["ell_col"]),
+                                                 _ptr(a["win"]), a["win"].numel(), ctypes.byref(cap)),
+                   "spmv_ell_xwin_build (hyb)")
+            p["xcap"] = cap.value
         dm.stored_bytes = 12 * hb["stored"] + 16 * hb["tail_nnz"]
     elif fmt == "cmrs":
         c = cmrs_build(m.n_rows, ptr, h=h)

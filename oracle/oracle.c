@@ -305,4 +305,16 @@ double oracle_cpu_csr_omp(long long n_rows, const long long *row_ptr,
     return omp_get_wtime() - t0;
 }
 
+/* Evict the host caches before a cold pass: every thread writes its
+ * static share of a buffer larger than the last-level caches (each CCD's
+ * L3 holds only what its own cores touched, so one writer is not enough). */
+void oracle_sweep(unsigned char *buf, long long bytes, int threads)
+{
+    if (threads <= 0)
+        threads = omp_get_max_threads();
+#pragma omp parallel for num_threads(threads) schedule(static)
+    for (long long i = 0; i < bytes; i += 64)
+        buf[i] = (unsigned char)(buf[i] + 1);
+}
+
 int oracle_max_threads(void) { return omp_get_max_threads(); }

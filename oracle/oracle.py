@@ -60,6 +60,8 @@ def lib() -> ctypes.CDLL:
         L.oracle_cpu_csr_omp.argtypes = [_i64, _vp, _vp, _vp, _vp, _vp, ctypes.c_int]
         L.oracle_cpu_csr_omp.restype = ctypes.c_double
         L.oracle_max_threads.restype = ctypes.c_int
+        L.oracle_sweep.argtypes = [_vp, _i64, ctypes.c_int]
+        L.oracle_sweep.restype = None
         _lib = L
     return _lib
 
@@ -127,6 +129,12 @@ def cpu_csr_omp(n_rows, row_ptr, col, val, x, y, threads=0) -> float:
     """csr.c:285-309 compute_using_cpu (OpenMP); returns seconds."""
     return lib().oracle_cpu_csr_omp(n_rows, row_ptr.ctypes.data, col.ctypes.data, val.ctypes.data,
                                     x.ctypes.data, y.ctypes.data, threads)
+
+
+def sweep(buf: np.ndarray, threads=0) -> None:
+    """Write every 64th byte of buf from all threads (host cache eviction
+    between cold CPU passes)."""
+    lib().oracle_sweep(buf.ctypes.data, buf.nbytes, threads)
 
 
 def max_threads() -> int:

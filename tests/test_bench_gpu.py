@@ -52,12 +52,25 @@ def test_bench_one_gpu_line():
 
 
 def test_bench_gpus_2_without_launcher():
-    """`python3 bench.py --gpus 2` (the driver's form) measures TWO ranks."""
+    """`python3 bench.py --gpus 2` (the driver's form) measures TWO ranks, and
+    the line carries its own strong-scaling evidence: rank 0 times the whole
+    R-MAT alone in the same job, so rmat_strong has speedup_cold /
+    speedup_warm (a 1e6 / 1e7 R-MAT here, one re-cut)."""
+    args = [a for a in QUICK]
+    i = args.index("--rmat-strong")
+    args[i + 1] = "yes"
+    args += ["--rmat-rows", "1000000", "--rmat-nnz", "10000000", "--recuts", "1"]
     r = subprocess.run([sys.executable, str(REPO / "bench.py"), "--gpus", "2", "--backend", "gloo", "--share-gpu",
-                        *QUICK], capture_output=True, text=True, timeout=900, env=_env(), cwd=str(REPO))
+                        *args], capture_output=True, text=True, timeout=900, env=_env(), cwd=str(REPO))
     assert r.returncode == 0, r.stderr[-3000:]
     d = _line(r.stdout)
     assert d["n_gpus"] == 2
     assert len(d["config"]["timed_region"]["cold_ms_per_rank"]) == 2
     assert d["config"]["bytes_alg_all_ranks_step"] == 2 * d["config"]["bytes_alg_rank0_step"]
+    assert "replica throughput" in d["config"]["value_is"]
+    rs = d["rmat_strong"]
+    assert rs["whole_matrix_one_gpu"]["how"].startswith("rank 0 alone")
+    assert rs["speedup_warm"] > 0 and rs["speedup_cold"] > 0
+    assert d["strong_scaling"]["rmat_speedup_cold"] == rs["speedup_cold"]
+    assert "relabelled" in rs["layout"]
     assert "[launch] --gpus 2 without a launcher" in r.stderr

@@ -1023,19 +1023,59 @@ def test_hyb_single_pass_tail(torch_dev, case):
             continue
         a = sa.to_device(m, "hyb", dev)
         b = sa.to_device(m, "hyb", dev, coo_tail=False)
-        assert "tails" not in b.arrays
+        c = sa.to_device(m, "hyb", dev, xwin=False)  # the ELL part without x windows
+        assert "tails" not in b.arrays and "win" not in c.arrays
         if case != "fixtures":
-            assert a.params["tail_nnz"] > 0 and "tails" in a.arrays, m.label
+            assert a.params["tail_nnz"] > 0 and "tails" in a.arrays and "win" in a.arrays, m.label
         x = torch.from_numpy(rng.uniform(-1, 1, max(m.n_cols, 1))).to(dev)
         ya = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
-        ya2, yb = torch.full_like(ya, float("nan")), torch.full_like(ya, float("nan"))
+        ya2, yb, yc = (torch.full_like(ya, float("nan")) for _ in range(3))
         a.run(x, ya)
         a.run(x, ya2)
         b.run(x, yb)
+        c.run(x, yc)
         torch.cuda.synchronize()
         assert torch.equal(ya.view(torch.int64), ya2.view(torch.int64))
+        assert torch.equal(ya.view(torch.int64), yc.view(torch.int64))  # x windows: same bits
         assert_parity(m, ya.cpu().numpy(), x.cpu().numpy()[: m.n_cols])
         assert_parity(m, yb.cpu().numpy(), x.cpu().numpy()[: m.n_cols])
+
+
+def test_coo_single_pass_empty_row_run_search_path(torch_dev):
+    """the single pass with mean rows >= 12 (the 250-row start
+    table) where one tile spans more rows than the table (a run of 400 empty
+    rows), so the row phase searches the staged keys including the tail
+    entries, and that tile's last row runs 64 entries past its end.
+    Against the carry pass (same tiles) and the oracle."""
+    torch, dev = torch_dev
+    lens = np.concatenate([np.full(70, 20), np.zeros(400, np.int64), [200], np.full(1000, 40)])
+    rng = np.random.default_rng(12)
+    row = np.repeat(np.arange(lens.size, dtype=np.int32), lens)
+    m = sa.Coo(lens.size, 3000, row, rng.integers(0, 3000, row.size).astype(np.int32), rng.uniform(-1, 1, row.size),
+               False, "empty-row run")
+    assert m.nnz / m.n_rows >= 12
+    a = sa.to_device(m, "coo", dev, coo_tail=True, hot=0)
+    b = sa.to_device(m, "coo", dev, coo_tail=False, hot=0)
+    assert "tails" in a.arrays and "tails" not in b.arrays
+    x = torch.from_numpy(rng.uniform(-1, 1, m.n_cols)).to(dev)
+    ya, yb = (torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev) for _ in range(2))
+    a.run(x, ya)
+    b.run(x, yb)
+    torch.cuda.synchronize()
+    assert_parity(m, ya.cpu().numpy(), x.cpu().numpy())
+    assert_parity(m, yb.cpu().numpy(), x.cpu().numpy())
+    assert np.all(ya.cpu().numpy()[70:470] == 0.0)
+
+
+def test_coo_tail_conflicting_options_raise(torch_dev):
+    """coo_tail=True with the x-window or hot-table COO path (which
+    use the carry pass) raises instead of being ignored."""
+    _, dev = torch_dev
+    m = sa.gen_random(2000, 2000, 1, 20, seed=3)
+    with pytest.raises(sa.SpmvError):
+        sa.to_device(m, "coo", dev, coo_tail=True, xwin=True)
+    with pytest.raises(sa.SpmvError):
+        sa.to_device(m, "coo", dev, coo_tail=True, hot=64)
 
 
 def test_coo_single_pass_refuses_long_rows(torch_dev):

@@ -102,6 +102,30 @@ def test_power_iteration_matches_numpy(torch_dev, fmt):
     assert np.allclose(x.cpu().numpy(), xr, rtol=1e-9, atol=1e-13)
 
 
+@pytest.mark.parametrize("split", [False, True])
+def test_side_stream_same_bits(torch_dev, split):
+    """kernels on a non-default stream (HipKernels(stream=s)):
+    the solve runs on that stream end to end (copies, dots, the exchange and
+    the host reads ordered with the SpMVs), same bits as the default."""
+    torch, dev = torch_dev
+    m = _sym_random()
+    ref = it.build_operator(m, 0, 1, "csr", dev, align=64, split=split)
+    h1, x1 = it.power_iteration(ref, 30)
+    x1 = x1.clone()
+    op = it.build_operator(m, 0, 1, "csr", dev, align=64, split=split)
+    s = torch.cuda.Stream(dev)
+    op.kernels.stream = s
+    if op.remote is not None:
+        op.remote.stream = s
+    h2, x2 = it.power_iteration(op, 30)
+    torch.cuda.synchronize()
+    assert np.array_equal(h1.view(np.int64), h2.view(np.int64))
+    assert torch.equal(x1.view(torch.int64), x2.view(torch.int64))
+    xs, iters, res = it.cg(op, torch.ones(op.rows, dtype=torch.float64, device=dev), maxit=50)
+    torch.cuda.synchronize()
+    assert iters > 0 and np.isfinite(res)
+
+
 def test_power_iteration_graph_replay_same_bits(torch_dev):
     torch, dev = torch_dev
     m = sa.gen_cantlike(0, copies=2)

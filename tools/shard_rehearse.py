@@ -81,6 +81,8 @@ def main():
                     help="KEY=v1,v2: library knobs timed interleaved on every shard (several: cartesian product)")
     ap.add_argument("--rounds", type=int, default=1, help="interleaved rounds per shard (median of rounds)")
     ap.add_argument("--flush", action="store_true", help="also time every shard cold (512 MiB flush first)")
+    ap.add_argument("--damp", type=float, default=0.5,
+                    help="each re-cut moves the cut points this fraction of the way (bench.py's RMAT_DAMP)")
     ap.add_argument("--relabel", action="store_true",
                     help="columns relabelled by decreasing degree (spmv_column_relabel), x permuted to match; "
                          "no hot-column table")
@@ -118,7 +120,8 @@ def main():
         for cpass in range(a.calibrate + 1):
             if cpass:  # re-cut on the cold shard times with --flush (bench.py's rule), else warm
                 cost = cold if a.flush and cold and min(cold) > 0 else times[0]
-                bounds = sa.partition_rows_calibrated(n, ptr, G, bounds, cost, align=1024, row_weight=w)
+                nb = sa.partition_rows_calibrated(n, ptr, G, bounds, cost, align=1024, row_weight=w)
+                bounds = sa.partition_rows_damped(n, bounds, nb, a.damp) if a.damp < 1 else nb
             times, base, cold = run_split(a, torch, sa, dev, ptr, col, val, n, x, xh, b_total, envs, kw, G, w,
                                           hot, bounds, cpass, base)
 

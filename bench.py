@@ -121,6 +121,9 @@ def parse():
     p.add_argument("--banded-strong", default="auto", choices=["auto", "yes", "no"],
                    help="also time CSR and SELL on the banded 1e8-row / 1.6e9-entry matrix row-sharded over all "
                         "ranks (configs[4], generated on device; auto: with the default workload)")
+    p.add_argument("--cold-flush", default="read", choices=["read", "write"],
+                   help="headline cold state: 512 MiB READ (clean lines, default) or WRITTEN before every SpMV; "
+                        "the other is timed beside it")
     p.add_argument("--relabel", default="auto", choices=["auto", "yes", "no"],
                    help="R-MAT: columns relabelled by decreasing degree at build time (spmv_column_relabel), x "
                         "replicated in that layout (auto: yes); no = the per-run hot-column table instead")
@@ -510,7 +513,7 @@ def child_device_env(local: int) -> dict:
     return env
 
 
-def cant_single_rocprof(formats=None, local=None):
+def cant_single_rocprof(formats=None, local=None, flush_mode="read"):
     """tools/cant_single.py under `rocprofv3 --kernel-trace` as a child
     process, run before this process touches the GPU: formats (default
     every format) on ONE cant-like matrix, cold and warm, kernel durations
@@ -523,7 +526,7 @@ def cant_single_rocprof(formats=None, local=None):
     env = child_device_env(local) if local is not None else None
     with tempfile.TemporaryDirectory(prefix="cant_single_") as tmp:
         out = Path(tmp) / "cant_single.json"
-        plain = [sys.executable, str(tool), "--json", str(out)]
+        plain = [sys.executable, str(tool), "--json", str(out), "--flush-mode", flush_mode]
         if formats:
             plain += ["--formats", ",".join(formats)]
         traced = Path(rocprof).exists()
@@ -584,11 +587,19 @@ def single_cold(args, torch, dev, rank, world, dist, cdev, prof):
 
     probe = probe_lib()
     scratch = torch.empty(FLUSH_BYTES, dtype=torch.uint8, device=dev)
+    sink = torch.zeros(64, dtype=torch.int32, device=dev)
 
-    def flush():
+    def flush_write():
         assert probe.spmv_probe_flush(scratch.data_ptr(), FLUSH_BYTES, torch.cuda.current_stream().cuda_stream) == 0
 
-    flush()
+    def flush_read():  # the same eviction by READING 512 MiB: clean lines, nothing to write back
+        assert probe.spmv_probe_flush_read(scratch.data_ptr(), FLUSH_BYTES, sink.data_ptr(),
+                                           torch.cuda.current_stream().cuda_stream) == 0
+
+    modes = {"write": flush_write, "read": flush_read}
+    flush = modes[args.cold_flush]
+    other = modes["read" if args.cold_flush == "write" else "write"]
+    flush_write()
     torch.cuda.synchronize()
 
     def step():
@@ -626,6 +637,10 @@ def single_cold(args, torch, dev, rank, world, dist, cdev, prof):
     wall, span_both = spans(step, K)
     _, span_flush = spans(flush, K)
     inproc = max((span_both - span_flush) / K, 1e-6)
+    # the other cold state beside it (not the headline)
+    _, sb2 = spans(lambda: (other(), dm.run(x, y)), K)
+    _, sf2 = spans(other, K)
+    inproc_other = max((sb2 - sf2) / K, 1e-6)
     bad, first = sa.check(m, xh, y.cpu().numpy())
     all_ok(dist, cdev, torch, bad == 0, f"cant-like single matrix, row {first}", rank)
 
@@ -664,6 +679,11 @@ def single_cold(args, torch, dev, rank, world, dist, cdev, prof):
                                      + " between barrier + synchronize",
                              "wall_ms": round(wall * 1e3, 4), "wall_ms_per_step_incl_flush": round(wall_step, 5),
                              "cold_spmv_ms_in_process": round(cold_ms, 5),
+                             "cold_flush": f"{args.cold_flush}: 512 MiB " +
+                                           ("written" if args.cold_flush == "write" else "read") +
+                                           " before every SpMV (evicts the Infinity Cache and the L2s)",
+                             "cold_spmv_ms_in_process_other_flush": {
+                                 ("read" if args.cold_flush == "write" else "write"): round(inproc_other, 5)},
                              "cold_spmv_ms_rocprof_rank0": traced,
                              "cold_ms_per_rank": [round(v, 5) for v in per_rank]},
             "parity_ok": True,
@@ -1006,6 +1026,14 @@ def per_format_leg(args, torch, dev, m, x, y, nnz, bytes_step, hot=None):
                            "params": dict(kw, **{k: v for k, v in d2.params.items()
                                                  if k in ("variant", "split_T", "n_chunks", "H")}) or None,
                            "parity_ok": badf == 0}
+        # formats that store fewer bytes than bytes_alg credits (16-bit column
+        # offsets, fp32 values): frac above is of the fp64/int32 bytes_alg and
+        # can pass 1; frac_vs_stored prices the bytes they actually read
+        stored = d2.stored_bytes + 8 * m.n_cols + 8 * m.n_rows
+        if stored < bytes_step:
+            per_format[fmt]["frac_vs_stored"] = round(stored / (km * 1e-3) * 1e-9 / sa.HBM_PEAK_GBS, 4)
+            per_format[fmt]["frac_note"] = (f"frac is of bytes_alg ({bytes_step} B); this format stores "
+                                            f"{stored} B with x and y: frac_vs_stored is the HBM figure")
         if fmt == "csrf32":
             per_format[fmt]["parity"] = "within fp32-value tolerance (values rounded to fp32)"
         del d2
@@ -1033,11 +1061,11 @@ def main():
     prof = None
     if not args.profile and args.workload == "cant" and args.single != "no":
         if world == 1:
-            prof = cant_single_rocprof()
+            prof = cant_single_rocprof(flush_mode=args.cold_flush)
         else:
-            prof = cant_single_rocprof([args.format], 0 if args.share_gpu else local)
+            prof = cant_single_rocprof([args.format], 0 if args.share_gpu else local, args.cold_flush)
     elif rank == 0 and not args.profile and args.single == "yes" and world == 1:
-        prof = cant_single_rocprof()
+        prof = cant_single_rocprof(flush_mode=args.cold_flush)
 
     import torch
 

@@ -166,6 +166,18 @@ int spmv_csr_run_tiled_hot(spmv_dims d, const int64_t *row_ptr, const int32_t *c
  * own_lo_plan it saves every run its pre-pass (NULL: built per run).     */
 int64_t spmv_csr_tiled_plan_len(int64_t nnz);
 int spmv_csr_tiled_plan(spmv_dims d, const int64_t *row_ptr, int32_t *own_lo);
+/* Entries per tile of the entry-balanced CSR for this matrix (the `tile`
+ * of spmv_csr_tiled_bigplan, spmv_host.h). */
+int64_t spmv_csr_tiled_tile(int64_t n_rows, int64_t nnz);
+/* spmv_csr_run_tiled_hot with the big-tile plan (spmv_csr_tiled_bigplan,
+ * uploaded; own_lo_plan required): a tile owning more than 1,024 rows (long
+ * runs of empty rows) writes its rows without entries as zeros and sums
+ * only the listed ones.  big = NULL is spmv_csr_run_tiled_hot.  Same
+ * products; rows of a big tile are summed in entry order by one lane. */
+int spmv_csr_run_tiled_plan(spmv_dims d, const int64_t *row_ptr, const int32_t *col_hot,
+                            const double *val, const double *x, double *y, int64_t H,
+                            const int32_t *hot, const int32_t *own_lo_plan, const int32_t *big,
+                            void *ws, size_t ws_bytes);
 /* Column-grouped CSR (CSRG, spmv_csrg_plan/fill in spmv_host.h) for
  * gather-bound power-law matrices; replaces the same reference kernel
  * (kernels/Csr.cl) on that input.  The entry-balanced kernel runs the
@@ -454,6 +466,10 @@ int spmv_xpay_ratio(int64_t n, const double *num, const double *den, const doubl
 /* y = x / sqrt(*s)                (power iteration: normalise)          */
 int spmv_scale_rsqrt(int64_t n, const double *s, const double *x, double *y, int device,
                      void *stream);
+/* out[k] = x[order[k]]: x in the layout of a matrix whose columns were
+ * relabelled by spmv_column_relabel (spmv_host.h), the input its SpMV
+ * takes.  out must not alias x.                                          */
+int spmv_gather(int64_t n, const int32_t *order, const double *x, double *out, int device, void *stream);
 
 /* ------------------------------------------------------------ helpers ---
  * Device discovery (replaces reference inc/helper_functions.h:76-129),

@@ -94,6 +94,18 @@ int spmv_csr_pick_variant(int64_t n_rows, const int64_t *row_ptr);
 int64_t spmv_hot_columns(int64_t n_cols, int64_t nnz, const int32_t *col, int64_t H_req, int32_t *hot,
                          int32_t *col_out);
 
+/* Big-tile plan of the entry-balanced CSR (spmv_csr_run_tiled_plan):
+ * with tiles of `tile` entries (spmv_csr_tiled_tile), every tile owning
+ * more than `cap` rows (the rows whose first offset lies in it; the last
+ * tile also the trailing rows) and at most 65,536 gets the list of its
+ * owned rows that have entries in it, as int32 pairs {row - first owned
+ * row, a | b << 16} with [a, b) relative to the tile start.  Layout
+ * (int32): idx[tiles] (-1 or the big tile's number k), start[nbig + 1]
+ * (absolute, even positions), then the pairs.  plan = NULL returns the
+ * length only.  Returns the int32 length, -1 on bad input.                */
+int64_t spmv_csr_tiled_bigplan(int64_t n_rows, const int64_t *row_ptr, int64_t tile, int32_t cap,
+                               int32_t *plan);
+
 /* Degree-ordered column relabel (power-law columns, x replicated): the
  * columns ranked by decreasing entry count (ties: lower column first;
  * columns without entries last, in id order).  order[rank] = column,

@@ -72,7 +72,7 @@ template <typename V>  // double or float values (instantiated in staged.hip)
 int launch_csr_tiled_hot(const spmv_dims &d, const int64_t *row_ptr, const int32_t *col,
                          const V *val, const double *x, double *y, int64_t H, const int32_t *hot,
                          double *xh, const int32_t *own_lo_plan, int32_t *own_lo, int32_t *carry_row,
-                         double *carry_val);
+                         double *carry_val, const int32_t *big = nullptr);
 int launch_cmrs_tiled(const spmv_dims &d, int32_t h, int64_t n_strips, const int64_t *strip_ptr,
                       const uint8_t *rin, const int32_t *col, const double *val, const double *x,
                       double *y, int32_t *own_lo, int32_t *carry_row, double *carry_val, int64_t H = 0,

@@ -1063,6 +1063,42 @@ extern "C" int spmv_csr_run_tiled_hot(spmv_dims d, const int64_t *row_ptr, const
                          "spmv_csr_run_tiled_hot");
 }
 
+extern "C" int64_t spmv_csr_tiled_tile(int64_t n_rows, int64_t nnz)
+{
+    return csr_tiled_tile(n_rows, nnz);
+}
+
+// spmv_csr_run_tiled_hot with the big-tile plan of the host builder
+// spmv_csr_tiled_bigplan (uploaded; built for tile = spmv_csr_tiled_tile):
+// tiles owning more than 1,024 rows write their rows without entries as
+// zeros and sum only the listed ones, instead of reading every owned row's
+// offsets from global memory.  big = NULL: spmv_csr_run_tiled_hot.
+extern "C" int spmv_csr_run_tiled_plan(spmv_dims d, const int64_t *row_ptr, const int32_t *col_hot,
+                                       const double *val, const double *x, double *y, int64_t H,
+                                       const int32_t *hot, const int32_t *own_lo_plan, const int32_t *big,
+                                       void *ws, size_t ws_bytes)
+{
+    if (!big)
+        return spmv_csr_run_tiled_hot(d, row_ptr, col_hot, val, x, y, H, hot, own_lo_plan, ws, ws_bytes);
+    if (d.n_rows < 0 || d.n_cols < 0 || d.nnz < 0 || d.n_rows > INT32_MAX || H < 0 ||
+        d.n_cols + H > INT32_MAX)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_run_tiled_plan: bad sizes");
+    if (d.n_rows == 0 || d.nnz == 0)
+        return spmv_csr_run_tiled(d, row_ptr, col_hot, val, x, y, ws, ws_bytes);
+    if (!own_lo_plan || (H > 0 && !hot) || !ws || ws_bytes < spmv_csr_hot_ws_bytes(d.n_rows, d.nnz, H))
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_run_tiled_plan: tile plan, hot list or workspace missing");
+    SPMV_GUARD(d);
+    const int64_t tiles = (d.nnz + csr_tiled_tile(d.n_rows, d.nnz) - 1) / csr_tiled_tile(d.n_rows, d.nnz);
+    if (tiles > INT32_MAX)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_run_tiled_plan: grid too large");
+    double *xh = (double *)ws;
+    double *carry_val = xh + H;
+    int32_t *own_lo = (int32_t *)(carry_val + tiles);
+    int32_t *carry_row = own_lo + tiles + 1;
+    return launch_csr_tiled_hot(d, row_ptr, col_hot, val, x, y, H, hot, xh, own_lo_plan, own_lo, carry_row,
+                                carry_val, big);
+}
+
 // fp32 values, entry-balanced tiles (+ hot-column table, build-once tile
 // plan), as spmv_csr_run_tiled_hot: bit-identical to it on the fp32-rounded
 // values.  own_lo_plan from spmv_csr_tiled_plan, or NULL.

@@ -304,7 +304,10 @@ constexpr int kSellSmallS = SPMV_SELL_SMALL_S;  // sell_small_kernel: waves per 
 #ifndef SPMV_SELL_HEAD_G  // A/B builds only, as SPMV_SELL_SMALL_S
 #define SPMV_SELL_HEAD_G 8
 #endif
-constexpr int kSellSmallP = 4;  // sell_small_kernel: slices per workgroup (and per x window)
+#ifndef SPMV_SELL_SMALL_P  // A/B builds only, as SPMV_SELL_SMALL_S
+#define SPMV_SELL_SMALL_P 4
+#endif
+constexpr int kSellSmallP = SPMV_SELL_SMALL_P;  // sell_small_kernel: slices per workgroup (and per x window)
 
 static void sell_geometry(int32_t C, int32_t sigma, int64_t n_slices, int *bt, int64_t *blocks)
 {

@@ -466,6 +466,13 @@ __global__ __launch_bounds__(kBlock) void csr_tile_rows_kernel(int64_t n_rows, i
 // stream-only x this phase, not the gathers, held the kernel to 2.6 TB/s
 // on R-MAT (tools/rmat_exp.hip mode 2).
 constexpr int kTiledRowCap = 1024;
+// A tile owning more rows (R-MAT: 1,329 of 195,313 512-entry tiles, up to
+// 28,255 rows, almost all empty) read their offsets from global memory one
+// 64-row run per wave at a time: one such tile took most of an R-MAT
+// shard's time.  With the big-tile plan (spmv_csr_tiled_bigplan) it lists
+// its owned rows that HAVE entries and writes the rest as zeros from a bitmap
+// of up to kTiledBigRowCap rows; more than that keeps the old path.
+constexpr int kTiledBigRowCap = 65536;
 
 // (A fused carry — the last-arriving tile of a spanning row finishing it —
 // was bit-identical but slower: 0.890 vs 0.856 ms on R-MAT with the
@@ -508,13 +515,15 @@ __global__ __launch_bounds__(kBlock) void csr_tiled_kernel(
     const int32_t *__restrict__ col, const V *__restrict__ val,
     const XS xs, double *__restrict__ y,
     const int32_t *__restrict__ own_lo, int32_t *__restrict__ carry_row,
-    double *__restrict__ carry_val)
+    double *__restrict__ carry_val, const int32_t *__restrict__ big = nullptr)
 {
     constexpr int CH = 2 * kBlock * R;
     constexpr int RPK = (kTiledRowCap + 1 + kBlock - 1) / kBlock;  // staged offsets per thread
     constexpr int NW = kBlock / kWave;
+    static_assert(kTiledBigRowCap / 32 >= kTiledRowCap + 1, "s_rp lives in the big-tile bitmap");
     __shared__ double2 s_prod[kBlock * R];
-    __shared__ int32_t s_rp[kTiledRowCap + 1];
+    __shared__ uint32_t s_bits[kTiledBigRowCap / 32];  // big tiles: owned rows with entries; else s_rp
+    int32_t *s_rp = reinterpret_cast<int32_t *>(s_bits);
     const double *prod = reinterpret_cast<const double *>(s_prod);
     const int64_t tile = blockIdx.x;
     const int64_t t0 = tile * CH;
@@ -525,6 +534,11 @@ __global__ __launch_bounds__(kBlock) void csr_tiled_kernel(
     const int64_t r_hi = t1 == nnz ? n_rows - 1 : (int64_t)own_lo[tile + 1] - 1;
     const int64_t nr = r_hi - r_lo + 1;  // owned rows (may be 0)
     const bool rp_lds = nr >= 0 && nr <= kTiledRowCap;  // uniform
+    // big tile (more owned rows than the offset table, at most the bitmap's):
+    // the plan lists its owned rows WITH entries, [a, b) relative to t0
+    const int32_t bk = !rp_lds && big && nr <= kTiledBigRowCap ? big[tile] : -1;  // uniform
+    int32_t b_beg = 0, b_end = 0;
+    int2 item[2] = {{0, 0}, {0, 0}};
     int64_t rpv[RPK];
     if (rp_lds) {
 #pragma unroll
@@ -532,6 +546,18 @@ __global__ __launch_bounds__(kBlock) void csr_tiled_kernel(
             const int i = (int)threadIdx.x + k * kBlock;
             rpv[k] = i <= nr ? row_ptr[r_lo + i] : 0;
         }
+    } else if (bk >= 0) {
+        const int64_t tiles = (nnz + CH - 1) / CH;
+        b_beg = big[tiles + bk];
+        b_end = big[tiles + bk + 1];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {  // at most CH listed rows; CH <= 2·kBlock for R = 1
+            const int32_t i = b_beg + 2 * ((int32_t)threadIdx.x + k * kBlock);
+            if (i < b_end)
+                item[k] = *reinterpret_cast<const int2 *>(big + i);
+        }
+        for (int32_t i = threadIdx.x; i < (int32_t)((nr + 31) >> 5); i += kBlock)
+            s_bits[i] = 0u;
     }
     st.commit(t0, t1, nnz, col, val, xs, s_prod, KeysNone{});
     if (rp_lds) {
@@ -544,6 +570,56 @@ __global__ __launch_bounds__(kBlock) void csr_tiled_kernel(
     }
     __syncthreads();
     const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+    if (bk >= 0) {
+        // carry: the entries before the first listed row (the owned rows
+        // before it have none) belong to row r_lo - 1
+        if (wv == 0) {
+            const int n_t = (int)(t1 - t0);
+            int e_rel = b_end > b_beg ? (big[b_beg + 1] & 0xFFFF) : n_t;
+            e_rel = e_rel < n_t ? e_rel : n_t;
+            const bool has = r_lo > 0 && e_rel > 0;
+            const double c = has ? wave_sum(prod, 0, e_rel) : 0.0;
+            if (lane == 0) {
+                carry_row[tile] = has ? (int32_t)(r_lo - 1) : -1;
+                carry_val[tile] = c;
+            }
+        }
+        // the listed rows, summed as the offset-table path sums them (the
+        // same bits): up to kTiledShort entries by one lane in entry order,
+        // longer rows by the whole wave; each row marked in the bitmap
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int32_t i = b_beg + 2 * ((int32_t)threadIdx.x + k * kBlock);
+            // (bounds re-checked so a plan of another matrix cannot index
+            // past the bitmap or the products)
+            const bool ok = i < b_end && item[k].x >= 0 && item[k].x < nr;
+            const int32_t rr = item[k].x, a = item[k].y & 0xFFFF;
+            int32_t b = (int32_t)((uint32_t)item[k].y >> 16);
+            b = b < CH ? b : CH;
+            const bool lng = ok && b - a > kTiledShort;
+            if (ok && !lng) {
+                double sum = 0.0;
+                for (int j = a; j < b; ++j)
+                    sum += prod[j];
+                store_y(y + r_lo + rr, sum);
+            }
+            if (ok)
+                atomicOr(&s_bits[rr >> 5], 1u << (rr & 31));
+            for (uint64_t m = __ballot(lng); m; m &= m - 1) {
+                const int l = __builtin_ctzll(m);
+                const int la = __shfl(a, l), lb = __shfl(b, l), lr = __shfl(rr, l);
+                const double sum = wave_sum(prod, la, lb);
+                if (lane == 0)
+                    store_y(y + r_lo + lr, sum);
+            }
+        }
+        __syncthreads();
+        // every other owned row has no entries: y = 0, coalesced, no row_ptr reads
+        for (int32_t i = threadIdx.x; i < (int32_t)nr; i += kBlock)
+            if (!((s_bits[i >> 5] >> (i & 31)) & 1u))
+                store_y(y + r_lo + i, 0.0);
+        return;
+    }
     // [a, b) of owned row r (relative to t0)
     auto range = [&](int64_t r, int &a, int &b) {
         if (rp_lds) {
@@ -788,27 +864,27 @@ int64_t csr_tiled_tile_min() { return 2 * kBlock; }
 template <int R, typename XS, typename V>
 static void launch_tiled_r(const spmv_dims &d, int64_t tiles, const int64_t *row_ptr, const int32_t *col,
                            const V *val, XS xs, double *y, const int32_t *own_lo, int32_t *carry_row,
-                           double *carry_val)
+                           double *carry_val, const int32_t *big)
 {
     const hipStream_t st = (hipStream_t)d.stream;
     // the plain-load variant exists for R = 3 only
     if (R == 3 && !stream_nt(true))
         hipLaunchKernelGGL((csr_tiled_kernel<R, false, XS, V>), dim3((unsigned)tiles), dim3(kBlock), 0, st, d.n_rows,
-                           d.nnz, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val);
+                           d.nnz, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val, R == 1 ? big : nullptr);
     else
         hipLaunchKernelGGL((csr_tiled_kernel<R, true, XS, V>), dim3((unsigned)tiles), dim3(kBlock), 0, st, d.n_rows,
-                           d.nnz, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val);
+                           d.nnz, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val, R == 1 ? big : nullptr);
 }
 
 template <typename XS, typename V>
 static void launch_tiled_xs(const spmv_dims &d, int64_t tiles, const int64_t *row_ptr, const int32_t *col,
                             const V *val, XS xs, double *y, const int32_t *own_lo, int32_t *carry_row,
-                            double *carry_val)
+                            double *carry_val, const int32_t *big = nullptr)
 {
     switch (tiled_r(d.n_rows, d.nnz)) {
-    case 1: launch_tiled_r<1>(d, tiles, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val); break;
-    case 2: launch_tiled_r<2>(d, tiles, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val); break;
-    default: launch_tiled_r<3>(d, tiles, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val); break;
+    case 1: launch_tiled_r<1>(d, tiles, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val, big); break;
+    case 2: launch_tiled_r<2>(d, tiles, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val, big); break;
+    default: launch_tiled_r<3>(d, tiles, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val, big); break;
     }
 }
 
@@ -831,7 +907,7 @@ template <typename V>
 int launch_csr_tiled_hot(const spmv_dims &d, const int64_t *row_ptr, const int32_t *col,
                          const V *val, const double *x, double *y, int64_t H, const int32_t *hot,
                          double *xh, const int32_t *own_lo_plan, int32_t *own_lo, int32_t *carry_row,
-                         double *carry_val)
+                         double *carry_val, const int32_t *big)
 {
     const int64_t ch = csr_tiled_tile(d.n_rows, d.nnz);
     const int64_t tiles = (d.nnz + ch - 1) / ch;
@@ -845,19 +921,19 @@ int launch_csr_tiled_hot(const spmv_dims &d, const int64_t *row_ptr, const int32
     }
     if (H > 0)
         launch_tiled_xs(d, tiles, row_ptr, col, val, XHot{x, xh, (int32_t)d.n_cols}, y, own_lo_plan, carry_row,
-                        carry_val);
+                        carry_val, big);
     else
-        launch_tiled_xs(d, tiles, row_ptr, col, val, XGlobal{x}, y, own_lo_plan, carry_row, carry_val);
+        launch_tiled_xs(d, tiles, row_ptr, col, val, XGlobal{x}, y, own_lo_plan, carry_row, carry_val, big);
     SPMV_CHECK_LAUNCH("csr_tiled_kernel (hot columns)");
     return launch_carry(tiles, carry_row, carry_val, y, st);
 }
 
 template int launch_csr_tiled_hot<double>(const spmv_dims &, const int64_t *, const int32_t *, const double *,
                                           const double *, double *, int64_t, const int32_t *, double *,
-                                          const int32_t *, int32_t *, int32_t *, double *);
+                                          const int32_t *, int32_t *, int32_t *, double *, const int32_t *);
 template int launch_csr_tiled_hot<float>(const spmv_dims &, const int64_t *, const int32_t *, const float *,
                                          const double *, double *, int64_t, const int32_t *, double *,
-                                         const int32_t *, int32_t *, int32_t *, double *);
+                                         const int32_t *, int32_t *, int32_t *, double *, const int32_t *);
 
 // ----------------------------------------------------------- launchers
 // Geometry of the strip-run CMRS kernel: lanes per row as the staged CSR

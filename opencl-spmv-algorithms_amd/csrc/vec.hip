@@ -104,6 +104,16 @@ __global__ __launch_bounds__(kBlock) void scale_rsqrt_kernel(int64_t n, const do
         y[i] = x[i] * inv;
 }
 
+// out[k] = x[order[k]]: x in the layout of a column-relabelled matrix
+// (spmv_column_relabel); the replication step's gather, not the SpMV's
+__global__ __launch_bounds__(kBlock) void gather_kernel(int64_t n, const int32_t *__restrict__ order,
+                                                        const double *__restrict__ x, double *__restrict__ out)
+{
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
+        out[i] = x[order[i]];
+}
+
 static unsigned stream_grid(int64_t n)
 {
     // a few waves of workgroups per CU is enough for a pure stream
@@ -183,5 +193,19 @@ extern "C" int spmv_scale_rsqrt(int64_t n, const double *s, const double *x, dou
     hipLaunchKernelGGL(scale_rsqrt_kernel, dim3(stream_grid(n)), dim3(kBlock), 0, (hipStream_t)stream, n, s,
                        x, y);
     SPMV_CHECK_LAUNCH("scale_rsqrt_kernel");
+    return SPMV_SUCCESS;
+}
+
+extern "C" int spmv_gather(int64_t n, const int32_t *order, const double *x, double *out, int device, void *stream)
+{
+    if (n < 0 || (n > 0 && (!order || !x || !out)) || (n > 0 && x == out))
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_gather: bad arguments");
+    if (n == 0)
+        return SPMV_SUCCESS;
+    DeviceGuard guard(device);
+    if (guard.rc() != SPMV_SUCCESS)
+        return guard.rc();
+    hipLaunchKernelGGL(gather_kernel, dim3(stream_grid(n)), dim3(kBlock), 0, (hipStream_t)stream, n, order, x, out);
+    SPMV_CHECK_LAUNCH("gather_kernel");
     return SPMV_SUCCESS;
 }

@@ -214,6 +214,80 @@ int64_t spmv_hot_columns(int64_t n_cols, int64_t nnz, const int32_t *col, int64_
     return n;
 }
 
+/* first row r with row_ptr[r] >= off (row_ptr nondecreasing) */
+static int64_t first_row_at(int64_t n_rows, const int64_t *row_ptr, int64_t off)
+{
+    int64_t lo = 0, hi = n_rows;
+    while (lo < hi) {
+        const int64_t mid = lo + (hi - lo) / 2;
+        if (row_ptr[mid] < off)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return lo;
+}
+
+int64_t spmv_csr_tiled_bigplan(int64_t n_rows, const int64_t *row_ptr, int64_t tile, int32_t cap,
+                               int32_t *plan)
+{
+    const int64_t kBigCap = 65536;
+    if (n_rows < 0 || !row_ptr || tile < 2 || tile > 65535 || cap < 0)
+        return -1;
+    const int64_t nnz = row_ptr[n_rows];
+    const int64_t tiles = nnz > 0 ? (nnz + tile - 1) / tile : 0;
+    /* pass 1: the big tiles and their listed rows */
+    int64_t nbig = 0, items = 0;
+    for (int64_t t = 0; t < tiles; ++t) {
+        const int64_t t0 = t * tile, t1 = t0 + tile < nnz ? t0 + tile : nnz;
+        const int64_t r_lo = first_row_at(n_rows, row_ptr, t0);
+        const int64_t r_hi = t1 == nnz ? n_rows - 1 : first_row_at(n_rows, row_ptr, t1) - 1;
+        const int64_t nr = r_hi - r_lo + 1;
+        if (nr <= cap || nr > kBigCap)
+            continue;
+        int64_t k = 0;
+        for (int64_t r = r_lo; r <= r_hi; ++r) {
+            const int64_t b = row_ptr[r + 1] < t1 ? row_ptr[r + 1] : t1;
+            if (row_ptr[r] < b)
+                ++k;
+        }
+        ++nbig;
+        items += k;
+    }
+    const int64_t head = tiles + nbig + 1;
+    const int64_t len = head + (head & 1) + 2 * items;
+    if (len > INT32_MAX)
+        return -1;
+    if (!plan)
+        return len;
+    /* pass 2: fill */
+    int64_t kb = 0, pos = head + (head & 1);
+    for (int64_t t = 0; t < tiles; ++t) {
+        const int64_t t0 = t * tile, t1 = t0 + tile < nnz ? t0 + tile : nnz;
+        const int64_t r_lo = first_row_at(n_rows, row_ptr, t0);
+        const int64_t r_hi = t1 == nnz ? n_rows - 1 : first_row_at(n_rows, row_ptr, t1) - 1;
+        const int64_t nr = r_hi - r_lo + 1;
+        plan[t] = -1;
+        if (nr <= cap || nr > kBigCap)
+            continue;
+        plan[t] = (int32_t)kb;
+        plan[tiles + kb] = (int32_t)pos;
+        for (int64_t r = r_lo; r <= r_hi; ++r) {
+            const int64_t b = row_ptr[r + 1] < t1 ? row_ptr[r + 1] : t1;
+            if (row_ptr[r] < b) {
+                plan[pos] = (int32_t)(r - r_lo);
+                plan[pos + 1] = (int32_t)((uint32_t)(row_ptr[r] - t0) | ((uint32_t)(b - t0) << 16));
+                pos += 2;
+            }
+        }
+        ++kb;
+    }
+    plan[tiles + kb] = (int32_t)pos;
+    if (head & 1)
+        plan[head] = 0;
+    return len;
+}
+
 /* Counting sort of the columns by entry count: ranks are handed out from
  * the largest count down, and inside one count in increasing column id, so
  * the order is the same whatever the thread count. */

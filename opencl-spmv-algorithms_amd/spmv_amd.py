@@ -96,6 +96,9 @@ HIP_SYMBOLS = {
                                               ctypes.c_size_t]),
     "spmv_csr_tiled_plan_len": (_c_i64, [_c_i64]),
     "spmv_csr_tiled_plan": (ctypes.c_int, [Dims, _vp, _vp]),
+    "spmv_csr_tiled_tile": (_c_i64, [_c_i64, _c_i64]),
+    "spmv_csr_run_tiled_plan": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, _c_i64, _vp, _vp, _vp, _vp,
+                                               ctypes.c_size_t]),
     "spmv_csrg_ws_bytes": (ctypes.c_size_t, [_c_i64, _c_i64]),
     "spmv_csrg_run": (ctypes.c_int, [Dims, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                      ctypes.c_size_t]),
@@ -174,6 +177,7 @@ HIP_SYMBOLS = {
     "spmv_axpy_ratio": (ctypes.c_int, [_c_i64, _vp, _vp, ctypes.c_double, _vp, _vp, ctypes.c_int, _vp]),
     "spmv_xpay_ratio": (ctypes.c_int, [_c_i64, _vp, _vp, _vp, _vp, ctypes.c_int, _vp]),
     "spmv_scale_rsqrt": (ctypes.c_int, [_c_i64, _vp, _vp, _vp, ctypes.c_int, _vp]),
+    "spmv_gather": (ctypes.c_int, [_c_i64, _vp, _vp, _vp, ctypes.c_int, _vp]),
     "spmv_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     "spmv_set_device": (ctypes.c_int, [ctypes.c_int]),
     "spmv_device_name": (ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t]),
@@ -214,6 +218,7 @@ HOST_SYMBOLS = {
     "spmv_csr_pick_variant": (ctypes.c_int, [_c_i64, _vp]),
     "spmv_hot_columns": (_c_i64, [_c_i64, _c_i64, _vp, _c_i64, _vp, _vp]),
     "spmv_column_relabel": (_c_i64, [_c_i64, _c_i64, _vp, _vp, _vp, _vp]),
+    "spmv_csr_tiled_bigplan": (_c_i64, [_c_i64, _vp, _c_i64, _c_i32, _vp]),
     "spmv_ell_plan": (ctypes.c_int, [_c_i64, _vp, _c_i32, ctypes.POINTER(_c_i32), ctypes.POINTER(_c_i64)]),
     "spmv_ell_fill": (ctypes.c_int, [_c_i64, _vp, _vp, _vp, _c_i32, _c_i64, _c_i32, _vp, _vp]),
     "spmv_sell_plan": (ctypes.c_int, [_c_i64, _vp, _c_i32, _c_i32, _c_i32, ctypes.POINTER(_c_i64), ctypes.POINTER(_c_i64)]),
@@ -493,11 +498,41 @@ def column_relabel(n_cols: int, col):
     return order, newid, out[: col.size]
 
 
+TILED_ROW_CAP = 1024  # rows a tiled-CSR tile stages offsets for (staged.hip kTiledRowCap)
+
+
+def csr_tiled_bigplan(n_rows: int, ptr: np.ndarray, nnz: int, cap: int = TILED_ROW_CAP):
+    """spmv_csr_tiled_bigplan for the tile the library runs this matrix
+    with (spmv_csr_tiled_tile): int32 plan, or None when no tile owns more
+    than `cap` rows."""
+    ptr = np.ascontiguousarray(ptr, dtype=np.int64)
+    tile = int(hip_lib().spmv_csr_tiled_tile(n_rows, nnz))
+    n = host_lib().spmv_csr_tiled_bigplan(n_rows, _ptr(ptr), tile, cap, None)
+    if n < 0:
+        raise SpmvError(OTHER_ERROR, "spmv_csr_tiled_bigplan", "bad arguments")
+    plan = np.empty(max(n, 1), np.int32)
+    host_lib().spmv_csr_tiled_bigplan(n_rows, _ptr(ptr), tile, cap, _ptr(plan))
+    tiles = (nnz + tile - 1) // tile
+    return plan if tiles > 0 and np.any(plan[:tiles] >= 0) else None
+
+
 def relabel_columns(m: Coo):
     """(m', order): m with its columns relabelled hot-first (same rows, same
     entry order); run m' on x[order]."""
     order, _, c2 = column_relabel(m.n_cols, m.col)
     return Coo(m.n_rows, m.n_cols, m.row, c2, m.val, False, f"{m.label} (columns relabelled by degree)"), order
+
+
+def gather_x(order, x, out=None, stream=None):
+    """out[k] = x[order[k]] on the device (spmv_gather): the x a
+    column-relabelled matrix takes.  order: int32 device tensor."""
+    torch = _torch()
+    if out is None:
+        out = torch.empty(order.numel(), dtype=torch.float64, device=x.device)
+    s = stream if stream is not None else torch.cuda.current_stream(x.device)
+    _check(hip_lib().spmv_gather(order.numel(), _ptr(order), _ptr(x), _ptr(out), x.device.index or 0, s.cuda_stream),
+           "spmv_gather")
+    return out
 
 
 def cmrs_build(n_rows: int, ptr, h: int = 8):
@@ -699,7 +734,11 @@ class DeviceMatrix:
             rc = lib.spmv_csr_run_xwin(d, _ptr(a["row_ptr"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
                                        p["lanes"], p.get("xwin_rows", 0), _ptr(a["win"]), p["xcap"])
         elif self.fmt == "csr":
-            if p.get("variant", 0) == 4 and "own_lo" in a:
+            if p.get("variant", 0) == 4 and "big" in a:
+                rc = lib.spmv_csr_run_tiled_plan(d, _ptr(a["row_ptr"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x),
+                                                 _ptr(y), p["H"], _ptr(a.get("hot")), _ptr(a["own_lo"]),
+                                                 _ptr(a["big"]), _ptr(a["ws"]), a["ws"].numel())
+            elif p.get("variant", 0) == 4 and "own_lo" in a:
                 rc = lib.spmv_csr_run_tiled_hot(d, _ptr(a["row_ptr"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x),
                                                 _ptr(y), p["H"], _ptr(a.get("hot")), _ptr(a["own_lo"]), _ptr(a["ws"]),
                                                 a["ws"].numel())
@@ -931,7 +970,7 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
               xwin: bool | None = None, xwin_rows: int = 0, split: int | None = None,
               cmrs_variant: int | None = None, hot: int | None = None,
               csr16_max_escape: float | None = 0.5, groups: int = 0, head: bool = True,
-              sell_head: bool | None = None, coo_tail: bool | None = None) -> DeviceMatrix:
+              sell_head: bool | None = None, coo_tail: bool | None = None, bigplan: bool = True) -> DeviceMatrix:
     """Build `fmt` on the host (libspmv_host.so) and upload it.  xwin (CSR,
     ELL, SELL; default on): also build the per-workgroup x windows on the
     device and run the LDS x-window kernels (same bits as without).  split
@@ -939,7 +978,9 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
     sell_head (SELL): None = the head copy wherever the small-matrix kernel
     runs (spmv_sell_head_bytes > 0: one cant-like matrix cold 11.9 -> 11.4 us,
     same bits).  coo_tail (COO, HYB): None = the single pass where the tail
-    plan accepts the matrix, True = it or raise, False = the carry pass."""
+    plan accepts the matrix, True = it or raise, False = the carry pass.
+    bigplan (tiled CSR): the plan of the tiles that own more than 1,024 rows
+    (spmv_csr_tiled_bigplan); False keeps their global-offset row phase."""
     torch = _torch()
     if xwin is None:
         # COO: per-tile windows measured slower (0.534 vs 0.491 ms on the
@@ -998,6 +1039,12 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
                 dm.arrays["own_lo"] = torch.empty(n_plan, dtype=torch.int32, device=device)
                 _check(hip_lib().spmv_csr_tiled_plan(dm.dims(), _ptr(dm.arrays["row_ptr"]), _ptr(dm.arrays["own_lo"])),
                        "spmv_csr_tiled_plan")
+                # tiles owning more rows than their offset table (runs of
+                # empty rows): the list of their rows with entries
+                bp = csr_tiled_bigplan(m.n_rows, ptr, m.nnz) if bigplan else None
+                if bp is not None:
+                    dm.arrays["big"] = _dev_tensor(bp, device)
+                    dm.params["big_tiles"] = int(np.count_nonzero(bp[: (m.nnz + 511) // 512] >= 0))
         elif xwin and variant in (0, 3):
             _csr_xwin(dm)
         dm.stored_bytes = 12 * m.nnz + 8 * (m.n_rows + 1)

@@ -646,20 +646,24 @@ def _empty_run_matrix(seed=11):
     return sa.Coo(n, nc, r, c, v), rows
 
 
+@pytest.mark.parametrize("bigplan", [True, False])
 @pytest.mark.parametrize("H", [0, 1024])
-def test_csr_tiled_empty_row_runs(torch_dev, H):
-    """Rows a tile owns past its 1024-entry LDS offset table read row_ptr
-    from global memory instead (csr_tiled_kernel, rp_lds false): the same
-    bits as the compacted matrix (3 empty rows after each nonempty one, so
-    the same lanes per row and every row staged by its tile: the same
-    entries in the same tiles), zeros for empty rows."""
+def test_csr_tiled_empty_row_runs(torch_dev, H, bigplan):
+    """Rows a tile owns past its 1024-entry LDS offset table: with the
+    big-tile plan (default) the tile sums only its listed rows and writes
+    zeros from a bitmap, without it reads row_ptr from global memory
+    (csr_tiled_kernel, rp_lds false); either way the same bits as the
+    compacted matrix (3 empty rows after each nonempty one, so the same
+    lanes per row and every row staged by its tile: the same entries in the
+    same tiles), zeros for empty rows."""
     torch, dev = torch_dev
     m, rows = _empty_run_matrix()
     inv = np.zeros(m.n_rows, np.int32)
     inv[rows] = 4 * np.arange(rows.size, dtype=np.int32)
     mc = sa.Coo(4 * rows.size, m.n_cols, inv[m.row], m.col, m.val)
     x = torch.from_numpy(np.random.default_rng(3).uniform(-1, 1, m.n_cols)).to(dev)
-    a = sa.to_device(m, "csr", dev, variant=4, hot=H)
+    a = sa.to_device(m, "csr", dev, variant=4, hot=H, bigplan=bigplan)
+    assert ("big" in a.arrays) == bigplan and (not bigplan or a.params["big_tiles"] > 10)
     c = sa.to_device(mc, "csr", dev, variant=4, hot=H)
     ya = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
     yc = torch.full((mc.n_rows,), float("nan"), dtype=torch.float64, device=dev)
@@ -1096,3 +1100,47 @@ def test_coo_single_pass_refuses_long_rows(torch_dev):
     dm.run(x, y)
     torch.cuda.synchronize()
     assert_parity(m, y.cpu().numpy(), x.cpu().numpy())
+
+
+@pytest.mark.parametrize("fmt,kw", [("csr", {"variant": 4}), ("coo", {}), ("cmrs", {"cmrs_variant": 1}),
+                                    ("sell", {"sigma": 1 << 24, "ki": 2, "xwin": False}), ("csrf32", {})])
+def test_column_relabel_same_bits(torch_dev, fmt, kw):
+    """Columns relabelled by degree (spmv_column_relabel) with x gathered
+    into that layout on the device (spmv_gather): the same products in the
+    same order, so y is bit-identical to the original matrix on x (no hot
+    table on either side), and passes the oracle on the ORIGINAL matrix."""
+    torch, dev = torch_dev
+    m = sa.gen_rmat(1_000_000, 10_000_000, scale=20, seed=6)
+    m2, order = sa.relabel_columns(m)
+    xh = np.random.default_rng(21).uniform(-1, 1, m.n_cols)
+    x = torch.from_numpy(xh).to(dev)
+    x2 = sa.gather_x(torch.from_numpy(order).to(dev), x)
+    assert torch.equal(x2.cpu(), torch.from_numpy(xh[order]))
+    a = sa.to_device(m, fmt, dev, hot=0, **kw)
+    b = sa.to_device(m2, fmt, dev, hot=0, **kw)
+    ya, yb = (torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev) for _ in range(2))
+    a.run(x, ya)
+    b.run(x2, yb)
+    torch.cuda.synchronize()
+    assert torch.equal(ya.view(torch.int64), yb.view(torch.int64))
+    if fmt != "csrf32":
+        assert_parity(m, yb.cpu().numpy(), xh)
+
+
+def test_csr_tiled_bigplan_rmat_same_bits(torch_dev):
+    """The R-MAT's big tiles (runs of empty rows) through the big-tile plan:
+    bit-identical to the global-offset row phase (bigplan=False), with and
+    without the relabel, and the oracle's y."""
+    torch, dev = torch_dev
+    m = sa.gen_rmat(2_000_000, 6_000_000, scale=21, seed=7)
+    xh = np.random.default_rng(22).uniform(-1, 1, m.n_cols)
+    x = torch.from_numpy(xh).to(dev)
+    a = sa.to_device(m, "csr", dev, variant=4, hot=0)
+    b = sa.to_device(m, "csr", dev, variant=4, hot=0, bigplan=False)
+    assert "big" in a.arrays and a.params["big_tiles"] > 0 and "big" not in b.arrays
+    ya, yb = (torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev) for _ in range(2))
+    a.run(x, ya)
+    b.run(x, yb)
+    torch.cuda.synchronize()
+    assert torch.equal(ya.view(torch.int64), yb.view(torch.int64))
+    assert_parity(m, ya.cpu().numpy(), xh)

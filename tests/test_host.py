@@ -447,6 +447,40 @@ def test_column_relabel(kind):
         assert order.tolist() == [1, 3, 0, 2]
 
 
+@pytest.mark.parametrize("tile,cap", [(512, 1024), (512, 16), (1536, 100)])
+def test_csr_tiled_bigplan(tile, cap):
+    """spmv_csr_tiled_bigplan lists, for every tile owning more than `cap`
+    rows (at most 65,536), exactly its owned rows with entries in it and
+    their [a, b) relative to the tile start; other tiles get -1."""
+    m = sa.gen_rmat(200_000, 600_000, scale=18, seed=3)
+    ptr, _, _ = sa.csr_from_coo(m)
+    lib = sa.host_lib()
+    n = lib.spmv_csr_tiled_bigplan(m.n_rows, ptr.ctypes.data, tile, cap, None)
+    plan = np.empty(n, np.int32)
+    assert lib.spmv_csr_tiled_bigplan(m.n_rows, ptr.ctypes.data, tile, cap, plan.ctypes.data) == n
+    z = int(ptr[-1])
+    tiles = (z + tile - 1) // tile
+    seen = 0
+    for t in range(tiles):
+        t0, t1 = t * tile, min(t * tile + tile, z)
+        r_lo = int(np.searchsorted(ptr, t0, side="left"))
+        r_hi = m.n_rows - 1 if t1 == z else int(np.searchsorted(ptr, t1, side="left")) - 1
+        nr = r_hi - r_lo + 1
+        if nr <= cap or nr > 65536:
+            assert plan[t] == -1
+            continue
+        assert plan[t] == seen
+        st, en = plan[tiles + seen], plan[tiles + seen + 1]
+        assert st % 2 == 0
+        want = [(r - r_lo, int(ptr[r] - t0), int(min(ptr[r + 1], t1) - t0)) for r in range(r_lo, r_hi + 1)
+                if ptr[r] < min(ptr[r + 1], t1)]
+        got = [(int(plan[i]), int(plan[i + 1]) & 0xFFFF, (int(plan[i + 1]) >> 16) & 0xFFFF) for i in range(st, en, 2)]
+        assert got == want
+        seen += 1
+    assert (seen > 0) == (cap == 16 or seen > 0)
+    assert lib.spmv_csr_tiled_bigplan(m.n_rows, ptr.ctypes.data, 1, cap, None) == -1
+
+
 def test_column_relabel_bad_input():
     lib = sa.host_lib()
     col = np.array([0, 5], np.int32)

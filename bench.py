@@ -406,7 +406,7 @@ def build_workload(args, torch, dev, rank, world):
         ptr, col, val = sa.csr_from_coo(full)
         n, z = full.n_rows, full.nnz
         del full
-        col, xh, hot, layout = rmat_layout(args, n, col)
+        col, xh, hot, layout = rmat_layout(args, n, ptr, col, val)
         bounds = sa.partition_rows(n, ptr, world, align=1024, row_weight=RMAT_ROW_WEIGHT)
         lo, hi = int(bounds[rank]), int(bounds[rank + 1])
         lptr = ptr[lo:hi + 1] - ptr[lo]
@@ -743,19 +743,25 @@ def rmat_matrix(args):
     return sa.gen_rmat(n, z, scale=max(1, (n - 1).bit_length()))
 
 
-def rmat_layout(args, n, col):
+def rmat_layout(args, n, ptr, col, val):
     """(col, x host, hot kwarg, label): with the relabel (default) the CSR's
     columns are renumbered by decreasing degree once at build time and x is
     replicated in that layout (x'[k] = x[order[k]]: the replication step,
     SURVEY.md §8e, delivers it; outside the timed SpMV), so no per-run
-    hot-table fill runs and the touched part of x is one dense prefix; y
-    keeps the original row order.  Otherwise the per-run hot-column table."""
+    hot-table fill runs and the touched part of x is one dense prefix; then
+    every row's entries are ordered by the new column (spmv_csr_sort_rows,
+    in place on col and val), so a long row reads that prefix in address
+    order (whole R-MAT cold 0.762 -> 0.734 ms, profiles/round5/ab_rmat_sort_rows.md);
+    y keeps the original row order.  Otherwise the per-run hot-column
+    table on the file-order rows."""
     xh = sa.ramp_x(n)
     if args.relabel == "no":
         return col, xh, None, "hot-column table (per-run fill of the 2^19 hottest x entries)"
     order, _, col2 = sa.column_relabel(n, col)
+    sa.csr_sort_rows(n, ptr, col2, val)
     return col2, np.ascontiguousarray(xh[order]), 0, ("columns relabelled by decreasing degree at build time "
-                                                     "(spmv_column_relabel); x replicated in that layout")
+                                                     "(spmv_column_relabel), each row's entries in new-column "
+                                                     "order (spmv_csr_sort_rows); x replicated in that layout")
 
 
 def rmat_strong(args, torch, dev, rank, world, dist, cdev):
@@ -783,7 +789,7 @@ def rmat_strong(args, torch, dev, rank, world, dist, cdev):
     n, z = full.n_rows, full.nnz
     if rank != 0:
         del full
-    col, xh, hot, layout = rmat_layout(args, n, col)
+    col, xh, hot, layout = rmat_layout(args, n, ptr, col, val)
     x = torch.from_numpy(xh).to(dev)
     b_total = sa.bytes_alg(n, n, z)
     steps = max(20, args.steps // 2)

@@ -73,6 +73,11 @@ int spmv_coo_sort_by_row(int64_t n_rows, int64_t nnz, const int32_t *row,
 int spmv_csr_from_coo(int64_t n_rows, int64_t nnz, const int32_t *row,
                       const int32_t *col, const double *val,
                       int64_t *row_ptr, int32_t *col_out, double *val_out);
+/* Entries of every CSR row reordered by increasing column (stable).  With
+ * degree-relabelled columns (spmv_column_relabel) a long row then reads x
+ * from its dense hot prefix in address order.  Changes each row's
+ * summation order (not the products): y within the parity rule.          */
+int spmv_csr_sort_rows(int64_t n_rows, const int64_t *row_ptr, int32_t *col, double *val);
 /* Row-length statistics of a CSR matrix. */
 int spmv_csr_row_stats(int64_t n_rows, const int64_t *row_ptr,
                        int64_t *min_len, int64_t *max_len, double *mean_len);

@@ -101,6 +101,76 @@ int spmv_csr_row_stats(int64_t n_rows, const int64_t *row_ptr,
     return SPMV_SUCCESS;
 }
 
+/* Entries of every row sorted by column, stable (equal columns keep their
+ * order): insertion sort below 32 entries, else a merge sort through a
+ * per-thread scratch of the longest row. */
+typedef struct {
+    int32_t c;
+    double v;
+} cv_t;
+
+static void sort_row(cv_t *a, cv_t *tmp, int64_t n)
+{
+    if (n < 32) {
+        for (int64_t i = 1; i < n; ++i) {
+            const cv_t k = a[i];
+            int64_t j = i - 1;
+            while (j >= 0 && a[j].c > k.c) {
+                a[j + 1] = a[j];
+                --j;
+            }
+            a[j + 1] = k;
+        }
+        return;
+    }
+    const int64_t h = n / 2;
+    sort_row(a, tmp, h);
+    sort_row(a + h, tmp, n - h);
+    int64_t i = 0, j = h, k = 0;
+    while (i < h && j < n)
+        tmp[k++] = a[j].c < a[i].c ? a[j++] : a[i++];
+    while (i < h)
+        tmp[k++] = a[i++];
+    while (j < n)
+        tmp[k++] = a[j++];
+    memcpy(a, tmp, (size_t)n * sizeof(cv_t));
+}
+
+int spmv_csr_sort_rows(int64_t n_rows, const int64_t *row_ptr, int32_t *col, double *val)
+{
+    if (n_rows < 0 || !row_ptr || (row_ptr[n_rows] > 0 && (!col || !val)))
+        return SPMV_OTHER_ERROR;
+    int64_t mx = 0;
+    for (int64_t r = 0; r < n_rows; ++r)
+        mx = row_ptr[r + 1] - row_ptr[r] > mx ? row_ptr[r + 1] - row_ptr[r] : mx;
+    int bad = 0;
+#pragma omp parallel reduction(| : bad)
+    {
+        cv_t *a = (cv_t *)malloc((size_t)(mx > 0 ? mx : 1) * sizeof(cv_t));
+        cv_t *tmp = (cv_t *)malloc((size_t)(mx > 0 ? mx : 1) * sizeof(cv_t));
+        if (!a || !tmp) {
+            bad = 1;
+        } else {
+#pragma omp for schedule(dynamic, 1024)
+            for (int64_t r = 0; r < n_rows; ++r) {
+                const int64_t b = row_ptr[r], n = row_ptr[r + 1] - b;
+                if (n < 2)
+                    continue;
+                for (int64_t e = 0; e < n; ++e)
+                    a[e] = (cv_t){col[b + e], val[b + e]};
+                sort_row(a, tmp, n);
+                for (int64_t e = 0; e < n; ++e) {
+                    col[b + e] = a[e].c;
+                    val[b + e] = a[e].v;
+                }
+            }
+        }
+        free(a);
+        free(tmp);
+    }
+    return bad ? SPMV_OTHER_ERROR : SPMV_SUCCESS;
+}
+
 typedef struct {
     int64_t cnt;
     int32_t col;

@@ -214,6 +214,7 @@ HOST_SYMBOLS = {
     "spmv_bin_read": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(MtxInfo), _vp, _vp, _vp]),
     "spmv_coo_sort_by_row": (ctypes.c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "spmv_csr_from_coo": (ctypes.c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "spmv_csr_sort_rows": (ctypes.c_int, [_c_i64, _vp, _vp, _vp]),
     "spmv_csr_row_stats": (ctypes.c_int, [_c_i64, _vp, ctypes.POINTER(_c_i64), ctypes.POINTER(_c_i64), ctypes.POINTER(ctypes.c_double)]),
     "spmv_csr_pick_variant": (ctypes.c_int, [_c_i64, _vp]),
     "spmv_hot_columns": (_c_i64, [_c_i64, _c_i64, _vp, _c_i64, _vp, _vp]),
@@ -409,6 +410,11 @@ def csr_from_coo(m: Coo):
     _check_host(host_lib().spmv_csr_from_coo(m.n_rows, m.nnz, _ptr(m.row), _ptr(m.col), _ptr(m.val),
                                              _ptr(ptr), _ptr(col), _ptr(val)), "csr_from_coo")
     return ptr, col, val
+
+
+def csr_sort_rows(n_rows: int, ptr, col, val) -> None:
+    """Sort every row's entries by column, in place (spmv_csr_sort_rows)."""
+    _check_host(host_lib().spmv_csr_sort_rows(n_rows, _ptr(ptr), _ptr(col), _ptr(val)), "csr_sort_rows")
 
 
 def coo_sort_by_row(m: Coo):

@@ -103,7 +103,7 @@ for s in "${steps[@]}"; do
     counters) run counters 120 rocprofv3 -L;;
     probe) [ -x tools/bw_probe ] || hipcc --offload-arch=gfx950 -O3 tools/bw_probe.hip -o tools/bw_probe; run bw_probe 300 tools/bw_probe;;
     pmc) run pmc 1100 python tools/pmc_traffic.py "${pmc_args[@]}";;
-    pmcrmat) run pmc_rmat 1100 python tools/pmc_traffic.py --workload rmat --formats csr --kernel csr_tiled_kernel --out traffic_rmat.json --steps 5;;
+    pmcrmat) run pmc_rmat 1100 python tools/pmc_traffic.py --workload rmat --formats csr --kernel csr_tiled_kernel --out "${PMC_OUT:-traffic_rmat.json}" --steps 5;;
     pmcsingle) run pmc_single 1100 python tools/pmc_traffic.py --workload cant --formats csr --out traffic_single.json --steps 20 "${pmc_args[@]}";;
     stalls) run pmc_stalls 1150 python tools/pmc_stalls.py --formats csr,sell;;
     stallsingle) run pmc_stalls_single 1150 python tools/pmc_stalls.py --workload cant --no-probe --formats "${STALL_FORMATS:-csr,sell16}" --passes "${STALL_PASSES:-sq,sq2,lds,lat,tcc,ta}" --out pmc_stalls_single.json;;

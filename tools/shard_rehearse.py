@@ -83,6 +83,8 @@ def main():
     ap.add_argument("--flush", action="store_true", help="also time every shard cold (512 MiB flush first)")
     ap.add_argument("--damp", type=float, default=0.5,
                     help="each re-cut moves the cut points this fraction of the way (bench.py's RMAT_DAMP)")
+    ap.add_argument("--sort-rows", action="store_true",
+                    help="after the relabel: every row's entries by increasing column (spmv_csr_sort_rows)")
     ap.add_argument("--relabel", action="store_true",
                     help="columns relabelled by decreasing degree (spmv_column_relabel), x permuted to match; "
                          "no hot-column table")
@@ -108,6 +110,8 @@ def main():
         order, _, col = sa.column_relabel(n, col)
         xh = np.ascontiguousarray(xh[order])
         a.hot = "0"
+    if a.sort_rows:
+        sa.csr_sort_rows(n, ptr, col, val)
     x = torch.from_numpy(xh).to(dev)
     b_total = sa.bytes_alg(n, n, z)
     base = None
@@ -161,7 +165,7 @@ def run_split(a, torch, sa, dev, ptr, col, val, n, x, xh, b_total, envs, kw, G, 
         if cold:
             extra = {"shard_ms_cold": [round(t, 4) for t in cold], "max_ms_cold": round(max(cold), 4),
                      "aggregate_GBs_cold": round(b_total / (max(cold) * 1e-3) * 1e-9, 1)}
-        print(json.dumps({"workload": "rmat 1e7/1e8", "format": a.format, "relabel": a.relabel, "env": env,
+        print(json.dumps({"workload": "rmat 1e7/1e8", "format": a.format, "relabel": a.relabel, "sort_rows": a.sort_rows, "env": env,
                           "params_shard0": params,
                           "gpus": G, "row_weight": w, "hot": hot, "graph": a.graph, "calibration_pass": cpass,
                           "shard_rows": np.diff(bounds).tolist(), "shard_nnz": nnzs,

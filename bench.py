@@ -637,10 +637,13 @@ def single_cold(args, torch, dev, rank, world, dist, cdev, prof):
     wall, span_both = spans(step, K)
     _, span_flush = spans(flush, K)
     inproc = max((span_both - span_flush) / K, 1e-6)
-    # the other cold state beside it (not the headline)
-    _, sb2 = spans(lambda: (other(), dm.run(x, y)), K)
-    _, sf2 = spans(other, K)
-    inproc_other = max((sb2 - sf2) / K, 1e-6)
+    # the other cold state beside it (not the headline; not in --profile runs,
+    # whose PMC passes average every launch of the kernel)
+    inproc_other = None
+    if not args.profile:
+        _, sb2 = spans(lambda: (other(), dm.run(x, y)), K)
+        _, sf2 = spans(other, K)
+        inproc_other = max((sb2 - sf2) / K, 1e-6)
     bad, first = sa.check(m, xh, y.cpu().numpy())
     all_ok(dist, cdev, torch, bad == 0, f"cant-like single matrix, row {first}", rank)
 
@@ -683,7 +686,8 @@ def single_cold(args, torch, dev, rank, world, dist, cdev, prof):
                                            ("written" if args.cold_flush == "write" else "read") +
                                            " before every SpMV (evicts the Infinity Cache and the L2s)",
                              "cold_spmv_ms_in_process_other_flush": {
-                                 ("read" if args.cold_flush == "write" else "write"): round(inproc_other, 5)},
+                                 ("read" if args.cold_flush == "write" else "write"):
+                                     round(inproc_other, 5) if inproc_other else None},
                              "cold_spmv_ms_rocprof_rank0": traced,
                              "cold_ms_per_rank": [round(v, 5) for v in per_rank]},
             "parity_ok": True,

@@ -33,6 +33,8 @@ PASSES = {
     "lat": ["TCP_TCC_READ_REQ_LATENCY_sum", "TA_FLAT_READ_WAVEFRONTS_sum", "TA_TOTAL_WAVEFRONTS_sum",
             "SQ_WAVES"],
     "lds": ["SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE", "SQ_WAIT_INST_LDS", "SQ_ACTIVE_INST_LDS"],
+    "inst": ["SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_SMEM", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_ANY",
+             "SQ_WAVES"],
 }
 
 

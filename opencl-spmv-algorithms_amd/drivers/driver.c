@@ -287,6 +287,7 @@ typedef struct {
      * the renumbered columns, h_col the original ones for the CPU loop */
     int64_t H;
     int32_t *d_hot, *d_own_lo;
+    int32_t *d_big; /* tiled CSR: the big-tile plan (spmv_csr_tiled_bigplan), or NULL */
     /* host copies for the CPU loop */
     int64_t *h_ptr;
     int32_t *h_row, *h_col, *h_perm;
@@ -403,6 +404,25 @@ static int build_format(const opts_t *o, spmv_format fmt, const coo_t *m, dev_fm
                 if (n_plan > 0 && ((rc = spmv_malloc((void **)&f->d_own_lo, (size_t)n_plan * 4)) ||
                                    (rc = spmv_csr_tiled_plan(f->d, f->d_ptr, f->d_own_lo))))
                     return rc;
+                /* tiles owning more than 1,024 rows (runs of empty rows): the
+                 * list of their rows with entries (same bits) */
+                const int64_t tile = spmv_csr_tiled_tile(N, Z);
+                const int64_t nb = n_plan > 0 ? spmv_csr_tiled_bigplan(N, ptr, tile, 1024, NULL) : -1;
+                const int64_t tiles = tile > 0 ? (Z + tile - 1) / tile : 0;
+                if (nb > tiles) { /* some tile is big: the plan holds more than its index */
+                    int32_t *big = malloc((size_t)nb * sizeof(int32_t));
+                    if (!big)
+                        return SPMV_OTHER_ERROR;
+                    spmv_csr_tiled_bigplan(N, ptr, tile, 1024, big);
+                    int any = 0;
+                    for (int64_t t = 0; t < tiles && !any; ++t)
+                        any = big[t] >= 0;
+                    if (any)
+                        rc = upload((void **)&f->d_big, big, (size_t)nb * sizeof(int32_t), NULL);
+                    free(big);
+                    if (rc)
+                        return rc;
+                }
             }
         } else {
             f->h = o->h;
@@ -598,6 +618,9 @@ static int launch(void *arg)
         return spmv_coo_run(f->d, f->d_row, f->d_col, f->d_val, f->d_x, f->d_y, f->d_ws,
                             f->ws_bytes);
     case FMT_CSR:
+        if (f->variant == 4 && f->d_big && f->d_own_lo)
+            return spmv_csr_run_tiled_plan(f->d, f->d_ptr, f->d_col, f->d_val, f->d_x, f->d_y, f->H, f->d_hot,
+                                           f->d_own_lo, f->d_big, f->d_ws, f->ws_bytes);
         if (f->variant == 4)
             return spmv_csr_run_tiled_hot(f->d, f->d_ptr, f->d_col, f->d_val, f->d_x, f->d_y, f->H, f->d_hot,
                                           f->d_own_lo, f->d_ws, f->ws_bytes);

@@ -158,3 +158,25 @@ def test_coo_single_pass_flag():
     r = run("coo", "--matrix", str(GOLDEN / "long_rows.mtx"), "--reps", "2", "--warmup", "1", "--strict")
     assert r.returncode == 0, r.stdout + r.stderr
     assert "COO single pass: refused" in r.stderr
+
+
+def test_csr_program_big_tiles(tmp_path):
+    """./bin/csr on a matrix whose rows run in long empty stretches (the
+    tiled CSR path, tiles owning thousands of rows: the big-tile plan) —
+    the reference's lines and a passing check."""
+    import numpy as np
+
+    import spmv_amd as sa
+
+    rng = np.random.default_rng(11)
+    n, nc = 400_000, 50_000
+    rows = np.sort(rng.choice(np.arange(1, n - 5000), 4000, replace=False))
+    lens = rng.integers(2, 20, rows.size)
+    lens[rows.size // 2] = 20_000
+    r = np.repeat(rows, lens).astype(np.int32)
+    m = sa.Coo(n, nc, r, rng.integers(0, nc, r.size).astype(np.int32), rng.uniform(-1, 1, r.size))
+    f = tmp_path / "big_tiles.mtx"
+    sa.write_mtx(f, m)
+    res = run("csr", "--matrix", str(f), "--reps", "3", "--warmup", "1", "--strict", "--cpu")
+    assert res.returncode == 0, res.stdout + res.stderr
+    assert "\nresult is ok\n" in "\n" + res.stdout

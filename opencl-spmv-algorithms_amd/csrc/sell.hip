@@ -478,9 +478,12 @@ __global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell_small_
     const int32_t *__restrict__ perm, const CT *__restrict__ col,
     const double *__restrict__ val, const XS xs, double *__restrict__ y, int64_t wcap,
     const double *__restrict__ x, const int2 *__restrict__ win, int32_t xcap,
-    const double *__restrict__ hval = nullptr, const CT *__restrict__ hcol = nullptr)
+    const double *__restrict__ hval = nullptr, const CT *__restrict__ hcol = nullptr, int remap = 0)
 {
     constexpr bool HEAD = HG > 0;  // HG: the head's slot groups per wave (the first batch)
+    // remap: consecutive workgroups (the 1024 / (64 P) of one σ-window, whose
+    // y[perm] stores share lines) on one XCD, so its L2 merges those lines
+    const int64_t bid = xcd_block(remap);
     constexpr int S = kSellSmallS, P = kSellSmallP, G = HEAD ? HG : sell_small_g<KI>();
     constexpr bool c16 = std::is_same<CT, uint16_t>::value;  // SELL16: offsets from the window base
     static_assert(!c16 || XWIN, "SELL16 needs the workgroup windows");
@@ -489,10 +492,10 @@ __global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell_small_
     const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
     SlotBatch<KI, NT, G> first;
     if constexpr (HEAD) {  // this wave's head: G groups, whatever its slice
-        const int64_t hw = (int64_t)blockIdx.x * (S * P) + wv;
+        const int64_t hw = bid * (S * P) + wv;
         first.load(hval + hw * G * step + lane * KI, hcol + hw * G * step + lane * KI, 0, G, step);
     }
-    const int64_t s = (int64_t)blockIdx.x * P + wv / S;
+    const int64_t s = bid * P + wv / S;
     const int ws = wv % S;  // wave within its slice
     const bool live = s < n_slices;  // uniform per wave
     const int64_t base = live ? slice_ptr[s] : 0;
@@ -512,7 +515,7 @@ __global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell_small_
     bool staged = false;
     int2 wnd = make_int2(0, -1);
     if constexpr (XWIN) {
-        wnd = win[blockIdx.x];
+        wnd = win[bid];
         const int32_t span = wnd.y - wnd.x + 1;
         staged = span > 0 && span <= xcap;  // uniform per workgroup
         if (staged)
@@ -574,6 +577,16 @@ bool sell_small(int32_t C, int64_t n_slices)
 constexpr int kSell16HeadG = SPMV_SELL_HEAD_G;
 static int sell16_head_g() { return kSell16HeadG; }
 
+// XCD-contiguous placement of the small-matrix kernel's workgroups: the
+// workgroups of one σ-window then share one L2, which merges their
+// scattered y[perm] stores into whole lines (one cant-like matrix cold,
+// interleaved A/B: SELL 11.06 -> 10.86 us, SELL16 10.12 -> 9.80 us,
+// profiles/round5/ab_sell_remap.md).  SPMV_XWIN_REMAP=0/1 overrides it per
+// call, as for the x-window kernels.  (Round 5 also tried sharing the
+// workgroup's 8 waves out over its 4 slices in proportion to their widths,
+// instead of 2 per slice: 11.6-11.8 vs 10.5-10.7 us, not kept.)
+constexpr bool kSellSmallRemapDefault = true;
+
 template <int KI, bool NT, bool XWIN, typename XS, typename CT = int32_t>
 static void launch_sell_small(int64_t n_slices, const int64_t *slice_ptr, const int32_t *perm, const CT *col,
                               const double *val, const XS xs, double *y, int64_t wcap, const double *x,
@@ -582,10 +595,11 @@ static void launch_sell_small(int64_t n_slices, const int64_t *slice_ptr, const 
 {
     const size_t lds = XWIN ? (size_t)xcap * sizeof(double) : 0;
     const int64_t blocks = (n_slices + kSellSmallP - 1) / kSellSmallP;
+    const int remap = xwin_remap(kSellSmallRemapDefault) ? 1 : 0;
 #define SPMV_SMALL_HG(HH)                                                                                     \
     hipLaunchKernelGGL((sell_small_kernel<KI, NT, XWIN, XS, CT, HH>), dim3((unsigned)blocks),                 \
                        dim3(kWave * kSellSmallS * kSellSmallP), lds, st, n_slices, slice_ptr, perm, col, val, xs, \
-                       y, wcap, x, win, xcap, hval, hcol)
+                       y, wcap, x, win, xcap, hval, hcol, remap)
     if constexpr (XWIN) {  // the head (SELL16, or int32 SELL small matrices)
         if (hval)
             SPMV_SMALL_HG(kSell16HeadG);

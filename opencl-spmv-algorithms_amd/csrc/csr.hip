@@ -695,9 +695,14 @@ static int csr_xwin_mode(int64_t n_rows, int64_t nnz, int64_t rows_per_window, i
 // rows; on), not when each row reads a narrow band (banded: 143 columns for
 // 128 rows; 0.765 vs 0.782 ms with remap, off).  SPMV_XWIN_REMAP forces it
 // (placement only: same bits).
-static bool csr_xwin_remap_rule(int32_t xcap, int64_t rows_per_window)
+// Round 5: only for grids of many rounds on the chip (>= 8 windows per CU).
+// On ONE cant-like matrix (488 windows, one round, all windows resident at
+// once) the round-robin placement ran 1.5 % faster in three interleaved A/Bs
+// (12.08 / 11.98 vs 12.18 / 12.26 us cold, profiles/round5/ab_remap_staged.md;
+// 12.12 vs 12.20-12.30 in round 4, profiles/round4/ab_csr_single.md T).
+static bool csr_xwin_remap_rule(int32_t xcap, int64_t rows_per_window, int64_t n_windows)
 {
-    return xwin_remap((int64_t)xcap > 2 * rows_per_window);
+    return xwin_remap((int64_t)xcap > 2 * rows_per_window && n_windows >= 8 * 256);
 }
 
 // dynamic LDS of csr_xwin_kernel: the x window, and in MODE 3 the window's
@@ -750,7 +755,7 @@ static void launch_csr_xwin(const spmv_dims &d, const int64_t *row_ptr, const Co
     const size_t lds = csr_xwin_lds(mode, xcap, gpw, RPB);
     if (n_win > INT32_MAX)
         return;
-    const int remap = csr_xwin_remap_rule(xcap, gpw * RPB) ? 1 : 0;
+    const int remap = csr_xwin_remap_rule(xcap, gpw * RPB, n_win) ? 1 : 0;
     const hipStream_t st = (hipStream_t)d.stream;
     if (mode == 3)
         hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, V, 3, Cols>), dim3((unsigned)n_win), dim3(kBlock), lds, st,

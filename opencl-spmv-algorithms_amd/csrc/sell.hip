@@ -254,10 +254,11 @@ template <int KI, bool NT, int U>
 __global__ __launch_bounds__(kBlock) void ell_xwin_kernel(
     int64_t n_rows, int32_t K, int64_t ld, const int32_t *__restrict__ col,
     const double *__restrict__ val, const double *__restrict__ x,
-    double *__restrict__ y, const int2 *__restrict__ win, int32_t xcap)
+    double *__restrict__ y, const int2 *__restrict__ win, int32_t xcap, int remap = 0)
 {
     extern __shared__ double s_x[];
-    const int2 wnd = win[blockIdx.x];
+    const int64_t blk = xcd_block(remap);  // remap: neighbouring row blocks (shared x lines) on one XCD
+    const int2 wnd = win[blk];
     const int32_t span = wnd.y - wnd.x + 1;
     const bool staged = span > 0 && span <= xcap;  // uniform per workgroup
     if (staged) {
@@ -267,7 +268,7 @@ __global__ __launch_bounds__(kBlock) void ell_xwin_kernel(
             s_x[j] = x[wnd.x + j];
         __syncthreads();
     }
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t i = blk * kBlock + threadIdx.x;
     if (i >= n_rows)
         return;
     const int64_t off = i * KI;
@@ -576,6 +577,12 @@ bool sell_small(int32_t C, int64_t n_slices)
 // waves of 9-15 groups read padding); profiles/round3/cant_single_sell16_head_*.json
 constexpr int kSell16HeadG = SPMV_SELL_HEAD_G;
 static int sell16_head_g() { return kSell16HeadG; }
+
+// XCD-contiguous placement of the x-window ELL workgroups (neighbouring
+// 256-row blocks read overlapping x lines; on one XCD they share its L2):
+// one cant-like matrix cold 12.28 / 12.16 -> 11.84 / 11.76 us, two
+// interleaved rounds (profiles/round5/ab_remap_staged.md).
+constexpr bool kEllRemapDefault = true;
 
 // XCD-contiguous placement of the small-matrix kernel's workgroups: the
 // workgroups of one σ-window then share one L2, which merges their
@@ -1183,7 +1190,8 @@ extern "C" int spmv_ell_run_xwin(spmv_dims d, int32_t K, int64_t ld, int32_t ki,
     auto kern = ki == 2 ? (nt ? ell_xwin_kernel<2, true, 4> : ell_xwin_kernel<2, false, 4>)
                         : (nt ? ell_xwin_kernel<1, true, 4> : ell_xwin_kernel<1, false, 4>);
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock), (size_t)xcap * sizeof(double),
-                       (hipStream_t)d.stream, d.n_rows, K, ld, col, val, x, y, (const int2 *)win, xcap);
+                       (hipStream_t)d.stream, d.n_rows, K, ld, col, val, x, y, (const int2 *)win, xcap,
+                       xwin_remap(kEllRemapDefault) ? 1 : 0);
     SPMV_CHECK_LAUNCH("ell_xwin_kernel");
     return SPMV_SUCCESS;
 }

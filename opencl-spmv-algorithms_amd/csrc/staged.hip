@@ -156,17 +156,18 @@ __global__ __launch_bounds__(kBlock) void cmrs_staged_kernel(
     const int64_t *__restrict__ strip_ptr, const uint8_t *__restrict__ rin,
     const int32_t *__restrict__ col, const double *__restrict__ val,
     const double *__restrict__ x, double *__restrict__ y,
-    const int2 *__restrict__ win, int32_t xcap)
+    const int2 *__restrict__ win, int32_t xcap, int remap = 0)
 {
     constexpr int CH = 2 * kBlock * R;
     extern __shared__ double s_x[];
     __shared__ int64_t s_sp[kBlock + 1];
+    const int64_t blk = xcd_block(remap);  // remap: neighbouring strip runs (shared x lines) on one XCD
     __shared__ double2 s_prod[kBlock * R];
     __shared__ uint16_t s_key2[kBlock * R];  // keys of entry pairs
     const uint8_t *s_key = reinterpret_cast<const uint8_t *>(s_key2);
     const double *prod = reinterpret_cast<const double *>(s_prod);
 
-    const int64_t s0 = (int64_t)blockIdx.x * G;
+    const int64_t s0 = blk * G;
     if ((int)threadIdx.x <= G) {
         const int64_t s = s0 + threadIdx.x;
         s_sp[threadIdx.x] = strip_ptr[s < n_strips ? s : n_strips];
@@ -174,7 +175,7 @@ __global__ __launch_bounds__(kBlock) void cmrs_staged_kernel(
     bool staged = false;  // uniform per workgroup
     int32_t wlo = 0;
     if constexpr (XW) {
-        const int2 wnd = win[blockIdx.x];
+        const int2 wnd = win[blk];
         const int32_t span = wnd.y - wnd.x + 1;
         staged = span > 0 && span <= xcap;
         wlo = wnd.x;
@@ -248,6 +249,14 @@ constexpr int kCooRowCapShort = 250;
 constexpr int kCooTailCap = 80;
 // entry pairs staged per thread by the COO kernels (tile = 2·256·kCooR entries)
 constexpr int kCooR = 3;
+// XCD-contiguous placement of the single-pass COO tiles and the x-window
+// CMRS strip runs (neighbours read overlapping x lines; on one XCD they share
+// its L2).  SPMV_XWIN_REMAP=0/1 overrides it per call.  One cant-like matrix
+// cold, two interleaved rounds (profiles/round5/ab_remap_staged.md): COO
+// 16.68 / 16.88 -> 16.54 / 16.52 us (on), CMRS 13.34 / 13.48 -> 13.52 / 13.58
+// (off).
+constexpr bool kCooRemapDefault = true;
+constexpr bool kCmrsRemapDefault = false;
 
 // A workgroup owns one tile of CH consecutive row-sorted entries and
 // writes y for rows (row[t0-1], row[t1-1]] (rows without entries get 0;
@@ -267,7 +276,7 @@ __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
     const int32_t *__restrict__ col, const double *__restrict__ val,
     const double *__restrict__ x, double *__restrict__ y, int32_t *__restrict__ carry_row,
     double *__restrict__ carry_val, const int2 *__restrict__ win, int32_t xcap, const XS xs,
-    const int32_t *__restrict__ tails = nullptr)
+    const int32_t *__restrict__ tails = nullptr, int remap = 0)
 {
     constexpr int CH = 2 * kBlock * R;
     extern __shared__ double s_x[];
@@ -280,7 +289,7 @@ __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
     const int32_t *s_row = reinterpret_cast<const int32_t *>(s_row2);
     const double *prod = reinterpret_cast<const double *>(s_prod);
 
-    const int64_t tile = blockIdx.x;
+    const int64_t tile = xcd_block(remap);  // remap: neighbouring tiles (shared x lines) on one XCD
     const int64_t t0 = tile * CH;
     const int64_t t1 = t0 + CH < nnz ? t0 + CH : nnz;
     const int n = (int)(t1 - t0);
@@ -962,16 +971,17 @@ int launch_cmrs_staged(const spmv_dims &d, int32_t h, int64_t n_strips,
     constexpr int R = 3;
     const size_t lds = win ? (size_t)xcap * sizeof(double) : 0;
     const bool nt = stream_nt(true);  // +5 % on the cant batch (0.321 vs 0.338 ms)
+    const int remap = xwin_remap(kCmrsRemapDefault) ? 1 : 0;
 #define SPMV_CMRS_STAGED(LL)                                                                            \
     do {                                                                                                \
         if (win && nt)                                                                             \
             hipLaunchKernelGGL((cmrs_staged_kernel<LL, R, true, true>), dim3((unsigned)blocks),          \
                                dim3(kBlock), lds, st, d.n_rows, h, G, n_strips, strip_ptr, rin, col, val, \
-                               x, y, win, xcap);                                                        \
+                               x, y, win, xcap, remap);                                                 \
         else if (win)                                                                                   \
             hipLaunchKernelGGL((cmrs_staged_kernel<LL, R, true>), dim3((unsigned)blocks), dim3(kBlock),  \
                                lds, st, d.n_rows, h, G, n_strips, strip_ptr, rin, col, val, x, y, win,   \
-                               xcap);                                                                   \
+                               xcap, remap);                                                            \
         else                                                                                            \
             hipLaunchKernelGGL((cmrs_staged_kernel<LL, R, false>), dim3((unsigned)blocks), dim3(kBlock), \
                                0, st, d.n_rows, h, G, n_strips, strip_ptr, rin, col, val, x, y,          \
@@ -992,6 +1002,7 @@ int launch_cmrs_staged(const spmv_dims &d, int32_t h, int64_t n_strips,
 }
 
 int64_t coo_staged_tile() { return 2 * kBlock * kCooR; }
+
 
 // COO over the hot-column table (power-law matrices): 512-entry tiles (R =
 // 1) below a mean row of 96, as the tiled CSR and CMRS.
@@ -1015,7 +1026,8 @@ int launch_coo_staged_acc(const spmv_dims &d, const int32_t *row, const int32_t 
     if (tails)  // single pass: every tile finishes its last row (no carry)
         hipLaunchKernelGGL((coo_staged_kernel<4, R, true, false, false, XGlobal, true>), dim3((unsigned)tiles),
                            dim3(kBlock), 0, (hipStream_t)d.stream, d.n_rows, d.nnz, row, col, val, x, y,
-                           carry_row, carry_val, (const int2 *)nullptr, 0, XGlobal{x}, tails);
+                           carry_row, carry_val, (const int2 *)nullptr, 0, XGlobal{x}, tails,
+                           xwin_remap(kCooRemapDefault) ? 1 : 0);
     else
         hipLaunchKernelGGL((coo_staged_kernel<4, R, true, false>), dim3((unsigned)tiles), dim3(kBlock), 0,
                            (hipStream_t)d.stream, d.n_rows, d.nnz, row, col, val, x, y, carry_row, carry_val,
@@ -1102,12 +1114,14 @@ int launch_coo_staged(const spmv_dims &d, const int32_t *row, const int32_t *col
     // (SPMV_STREAM_NT=0), three interleaved pairs on one box,
     // profiles/round2/ab_coo_nt.log
     const bool nt = stream_nt(true);
+    const int remap = xwin_remap(kCooRemapDefault) ? 1 : 0;  // the single pass (tails) only
 #define SPMV_COO_STAGED(LL)                                                                              \
     do {                                                                                                 \
         if (tails)                                                                                       \
             hipLaunchKernelGGL((coo_staged_kernel<LL, R, false, false, true, XGlobal, true, RC>),        \
                                dim3((unsigned)tiles), dim3(kBlock), 0, st, d.n_rows, d.nnz, row, col, val, \
-                               x, y, carry_row, carry_val, (const int2 *)nullptr, 0, XGlobal{x}, tails);  \
+                               x, y, carry_row, carry_val, (const int2 *)nullptr, 0, XGlobal{x}, tails,   \
+                               remap);                                                                   \
         else if (win)                                                                                    \
             hipLaunchKernelGGL((coo_staged_kernel<LL, R, false, true>), dim3((unsigned)tiles),            \
                                dim3(kBlock), lds, st, d.n_rows, d.nnz, row, col, val, x, y, carry_row,    \

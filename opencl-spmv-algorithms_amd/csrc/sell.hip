@@ -305,6 +305,10 @@ constexpr int kSellSmallS = SPMV_SELL_SMALL_S;  // sell_small_kernel: waves per 
 #ifndef SPMV_SELL_HEAD_G  // A/B builds only, as SPMV_SELL_SMALL_S
 #define SPMV_SELL_HEAD_G 8
 #endif
+#ifndef SPMV_SELL_PIPE  // A/B builds only, as SPMV_SELL_SMALL_S
+#define SPMV_SELL_PIPE 0
+#endif
+constexpr int kSellPipe = SPMV_SELL_PIPE;  // sell_small_kernel's batch pipeline (see there)
 #ifndef SPMV_SELL_SMALL_P  // A/B builds only, as SPMV_SELL_SMALL_S
 #define SPMV_SELL_SMALL_P 4
 #endif
@@ -473,6 +477,20 @@ template <int KI> constexpr int sell_small_g() { return SPMV_SELL_HEAD_G; }  // 
 // waiting for slice_ptr (one dependent HBM round trip fewer on a cold
 // matrix); the later groups come from the SELL arrays.  Same values in the
 // same accumulators: bit-identical.
+#ifdef SPMV_SELL_STAMPS  // lab builds only (tools/sell_stamps.py): per-wave phase times
+constexpr int kStampWaves = 8192, kStamps = 8;
+__device__ uint64_t g_sell_stamps[kStampWaves * kStamps];
+#define SELL_STAMP(k)                                                                                   \
+    do {                                                                                                \
+        const int64_t sw_ = bid * (kSellSmallS * kSellSmallP) + wv;                                     \
+        if (lane == 0 && sw_ < kStampWaves)                                                             \
+            g_sell_stamps[sw_ * kStamps + (k)] = __builtin_amdgcn_s_memrealtime();                      \
+    } while (0)
+#else
+#define SELL_STAMP(k) \
+    do {              \
+    } while (0)
+#endif
 template <int KI, bool NT, bool XWIN, typename XS, typename CT = int32_t, int HG = 0>
 __global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell_small_kernel(
     int64_t n_slices, const int64_t *__restrict__ slice_ptr,
@@ -491,13 +509,25 @@ __global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell_small_
     constexpr int64_t step = (int64_t)kWave * KI;  // elements between slot groups
     extern __shared__ double s_x[];
     const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+    SELL_STAMP(0);
+#ifdef SPMV_SELL_STAMPS
+    {
+        uint32_t hid;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hid));
+        const int64_t sw_ = bid * (kSellSmallS * kSellSmallP) + wv;
+        if (lane == 0 && sw_ < kStampWaves)
+            g_sell_stamps[sw_ * kStamps + 7] = hid;
+    }
+#endif
     SlotBatch<KI, NT, G> first;
     if constexpr (HEAD) {  // this wave's head: G groups, whatever its slice
         const int64_t hw = bid * (S * P) + wv;
         first.load(hval + hw * G * step + lane * KI, hcol + hw * G * step + lane * KI, 0, G, step);
     }
-    const int64_t s = bid * P + wv / S;
-    const int ws = wv % S;  // wave within its slice
+    constexpr int PIPE = kSellPipe;
+    const int wu = (PIPE & 1) ? __builtin_amdgcn_readfirstlane(wv) : wv;
+    const int64_t s = bid * P + wu / S;
+    const int ws = wu % S;  // wave within its slice
     const bool live = s < n_slices;  // uniform per wave
     const int64_t base = live ? slice_ptr[s] : 0;
     int64_t w = live ? (slice_ptr[s + 1] - base) / kWave : 0;
@@ -513,26 +543,74 @@ __global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell_small_
         if (any)
             first.load(vp, cp, g0, g1, step);
     }
+    // PIPE bits: 1 the slice bounds through the scalar cache; 8 the next
+    // batch's loads issued before the current batch's products, batch 1 after
+    // the head's products, or (2) after the window barrier before them, or
+    // (4) before the window barrier (2 and 4 need 8)
+    SlotBatch<KI, NT, 4> nb;
+    bool have = g0 + G < g1;  // uniform per wave
     bool staged = false;
     int2 wnd = make_int2(0, -1);
     if constexpr (XWIN) {
         wnd = win[bid];
         const int32_t span = wnd.y - wnd.x + 1;
         staged = span > 0 && span <= xcap;  // uniform per workgroup
-        if (staged)
-            copy_window<kWave * S * P, 4>(s_x, x, wnd.x, span);
+        constexpr int T = kWave * S * P;
+        if ((PIPE & 4) && staged && span <= 4 * T) {
+            double xv[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int32_t i = (int32_t)threadIdx.x + k * T;
+                xv[k] = x[wnd.x + (i < span ? i : span - 1)];
+            }
+            if (have)
+                nb.load(vp, cp, g0 + G, g1, step);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int32_t i = (int32_t)threadIdx.x + k * T;
+                if (i < span)
+                    s_x[i] = xv[k];
+            }
+        } else {
+            if ((PIPE & 4) && have)
+                nb.load(vp, cp, g0 + G, g1, step);
+            if (staged)
+                copy_window<T, 4>(s_x, x, wnd.x, span);
+        }
         __syncthreads();
+    } else if ((PIPE & 4) && have) {
+        nb.load(vp, cp, g0 + G, g1, step);
     }
+    SELL_STAMP(1);
+    if ((PIPE & 2) && have)
+        nb.load(vp, cp, g0 + G, g1, step);
     const int32_t row = live && ws == 0 ? perm[s * kWave + lane] : -1;
     double a[4] = {0.0, 0.0, 0.0, 0.0};
     auto body = [&](const auto &src) {
         if (any)
             first.fma4(src, g0, g1, a);
-        for (int64_t g = g0 + G; g < g1; g += 4) {
-            SlotBatch<KI, NT, 4> b;
-            b.load(vp, cp, g, g1, step);
-            b.fma4(src, g, g1, a);
+        SELL_STAMP(2);
+        if constexpr ((PIPE & 8) != 0) {
+            if ((PIPE & 6) == 0 && have)  // batch 1 not issued yet
+                nb.load(vp, cp, g0 + G, g1, step);
+            int64_t g = g0 + G;
+            while (have) {  // same batches, same order: same bits
+                const SlotBatch<KI, NT, 4> cur = nb;
+                const int64_t gc = g;
+                g += 4;
+                have = g < g1;
+                if (have)
+                    nb.load(vp, cp, g, g1, step);
+                cur.fma4(src, gc, g1, a);
+            }
+        } else {
+            for (int64_t g = g0 + G; g < g1; g += 4) {
+                SlotBatch<KI, NT, 4> b;
+                b.load(vp, cp, g, g1, step);
+                b.fma4(src, g, g1, a);
+            }
         }
+        SELL_STAMP(3);
     };
     if (staged) {
         body(XWindow{s_x, c16 ? 0 : wnd.x});
@@ -546,6 +624,7 @@ __global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell_small_
     __shared__ double part[S * P][kWave];
     part[wv][lane] = sum;
     __syncthreads();
+    SELL_STAMP(4);
     if (ws == 0) {
 #pragma unroll
         for (int k = 1; k < S; ++k)
@@ -553,6 +632,7 @@ __global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell_small_
     }
     if (row >= 0)
         y[row] = sum;  // scattered by perm: plain stores, as sell_kernel
+    SELL_STAMP(5);
 }
 
 // Whether sell_small_kernel runs: C = 64 (a slice is one wave) and fewer
@@ -964,6 +1044,13 @@ extern "C" int spmv_sell16_fill(spmv_dims d, int32_t C, int32_t sigma, int64_t n
     SPMV_CHECK_LAUNCH("sell16_fill_kernel");
     return SPMV_SUCCESS;
 }
+
+#ifdef SPMV_SELL_STAMPS
+extern "C" int spmv_lab_sell_stamps(void *host, size_t bytes)
+{
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_sell_stamps), bytes);
+}
+#endif
 
 extern "C" size_t spmv_sell16_head_bytes(int64_t n_slices, int32_t C, int32_t ki)
 {

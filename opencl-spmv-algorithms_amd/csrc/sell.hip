@@ -305,10 +305,6 @@ constexpr int kSellSmallS = SPMV_SELL_SMALL_S;  // sell_small_kernel: waves per 
 #ifndef SPMV_SELL_HEAD_G  // A/B builds only, as SPMV_SELL_SMALL_S
 #define SPMV_SELL_HEAD_G 8
 #endif
-#ifndef SPMV_SELL_PIPE  // A/B builds only, as SPMV_SELL_SMALL_S
-#define SPMV_SELL_PIPE 0
-#endif
-constexpr int kSellPipe = SPMV_SELL_PIPE;  // sell_small_kernel's batch pipeline (see there)
 #ifndef SPMV_SELL_SMALL_P  // A/B builds only, as SPMV_SELL_SMALL_S
 #define SPMV_SELL_SMALL_P 4
 #endif
@@ -524,8 +520,12 @@ __global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell_small_
         const int64_t hw = bid * (S * P) + wv;
         first.load(hval + hw * G * step + lane * KI, hcol + hw * G * step + lane * KI, 0, G, step);
     }
-    constexpr int PIPE = kSellPipe;
-    const int wu = (PIPE & 1) ? __builtin_amdgcn_readfirstlane(wv) : wv;
+    // The slice bounds come through the scalar cache (a wave-uniform index):
+    // as vector loads they returned behind the head's loads (loads return in
+    // order), so the x window's loads went out only once the whole head had
+    // arrived.  Per-wave stamps (tools/sell_stamps.py, cold): 4.4 of 10.4 us
+    // from the start to the window barrier.
+    const int wu = __builtin_amdgcn_readfirstlane(wv);
     const int64_t s = bid * P + wu / S;
     const int ws = wu % S;  // wave within its slice
     const bool live = s < n_slices;  // uniform per wave
@@ -543,46 +543,24 @@ __global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell_small_
         if (any)
             first.load(vp, cp, g0, g1, step);
     }
-    // PIPE bits: 1 the slice bounds through the scalar cache; 8 the next
-    // batch's loads issued before the current batch's products, batch 1 after
-    // the head's products, or (2) after the window barrier before them, or
-    // (4) before the window barrier (2 and 4 need 8)
-    SlotBatch<KI, NT, 4> nb;
-    bool have = g0 + G < g1;  // uniform per wave
     bool staged = false;
     int2 wnd = make_int2(0, -1);
     if constexpr (XWIN) {
         wnd = win[bid];
         const int32_t span = wnd.y - wnd.x + 1;
         staged = span > 0 && span <= xcap;  // uniform per workgroup
-        constexpr int T = kWave * S * P;
-        if ((PIPE & 4) && staged && span <= 4 * T) {
-            double xv[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int32_t i = (int32_t)threadIdx.x + k * T;
-                xv[k] = x[wnd.x + (i < span ? i : span - 1)];
-            }
-            if (have)
-                nb.load(vp, cp, g0 + G, g1, step);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int32_t i = (int32_t)threadIdx.x + k * T;
-                if (i < span)
-                    s_x[i] = xv[k];
-            }
-        } else {
-            if ((PIPE & 4) && have)
-                nb.load(vp, cp, g0 + G, g1, step);
-            if (staged)
-                copy_window<T, 4>(s_x, x, wnd.x, span);
-        }
+        if (staged)
+            copy_window<kWave * S * P, 4>(s_x, x, wnd.x, span);
         __syncthreads();
-    } else if ((PIPE & 4) && have) {
-        nb.load(vp, cp, g0 + G, g1, step);
     }
     SELL_STAMP(1);
-    if ((PIPE & 2) && have)
+    // batch 1 (the 4 groups after the first batch) goes out before the first
+    // batch's products, later batches one at a time.  One cant-like matrix
+    // cold, with the scalar bounds (profiles/round5/ab_sell_pipe.md): SELL
+    // 10.80 -> 10.28 us, SELL16 9.70 -> 9.55; keeping two batches in flight
+    // throughout, or issuing batch 1 before the window barrier, was slower.
+    SlotBatch<KI, NT, 4> nb;
+    if (g0 + G < g1)  // uniform per wave
         nb.load(vp, cp, g0 + G, g1, step);
     const int32_t row = live && ws == 0 ? perm[s * kWave + lane] : -1;
     double a[4] = {0.0, 0.0, 0.0, 0.0};
@@ -590,25 +568,13 @@ __global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell_small_
         if (any)
             first.fma4(src, g0, g1, a);
         SELL_STAMP(2);
-        if constexpr ((PIPE & 8) != 0) {
-            if ((PIPE & 6) == 0 && have)  // batch 1 not issued yet
-                nb.load(vp, cp, g0 + G, g1, step);
-            int64_t g = g0 + G;
-            while (have) {  // same batches, same order: same bits
-                const SlotBatch<KI, NT, 4> cur = nb;
-                const int64_t gc = g;
-                g += 4;
-                have = g < g1;
-                if (have)
-                    nb.load(vp, cp, g, g1, step);
-                cur.fma4(src, gc, g1, a);
-            }
-        } else {
-            for (int64_t g = g0 + G; g < g1; g += 4) {
-                SlotBatch<KI, NT, 4> b;
-                b.load(vp, cp, g, g1, step);
-                b.fma4(src, g, g1, a);
-            }
+        int64_t g = g0 + G;
+        if (g < g1)
+            nb.fma4(src, g, g1, a);
+        for (g += 4; g < g1; g += 4) {  // same batches, same order: the same bits
+            SlotBatch<KI, NT, 4> b;
+            b.load(vp, cp, g, g1, step);
+            b.fma4(src, g, g1, a);
         }
         SELL_STAMP(3);
     };

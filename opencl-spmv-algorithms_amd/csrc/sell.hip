@@ -309,6 +309,7 @@ constexpr int kSellSmallS = SPMV_SELL_SMALL_S;  // sell_small_kernel: waves per 
 #define SPMV_SELL_SMALL_P 4
 #endif
 constexpr int kSellSmallP = SPMV_SELL_SMALL_P;  // sell_small_kernel: slices per workgroup (and per x window)
+constexpr int kSellXCopy = 4;  // sell_small_kernel: waves that copy the x window (HEAD)
 
 static void sell_geometry(int32_t C, int32_t sigma, int64_t n_slices, int *bt, int64_t *blocks)
 {
@@ -502,6 +503,7 @@ __global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell_small_
     constexpr int S = kSellSmallS, P = kSellSmallP, G = HEAD ? HG : sell_small_g<KI>();
     constexpr bool c16 = std::is_same<CT, uint16_t>::value;  // SELL16: offsets from the window base
     static_assert(!c16 || XWIN, "SELL16 needs the workgroup windows");
+    static_assert(!HEAD || XWIN, "the head runs with the workgroup windows");
     constexpr int64_t step = (int64_t)kWave * KI;  // elements between slot groups
     extern __shared__ double s_x[];
     const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
@@ -516,9 +518,34 @@ __global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell_small_
     }
 #endif
     SlotBatch<KI, NT, G> first;
-    if constexpr (HEAD) {  // this wave's head: G groups, whatever its slice
+    // The x window (HEAD + XWIN): the first kSellXCopy waves request it
+    // before their heads (its loads then return ahead of theirs) and store
+    // it; the others issue their heads at once.  One cant-like matrix cold:
+    // SELL16 9.56 -> 9.38 us, SELL 10.33 -> 10.28 (profiles/round5/ab_sell_pipe.md).
+    constexpr int XT = kWave * kSellXCopy, XU = 2048 / XT;
+    bool xdone = false;
+    if constexpr (HEAD && XWIN) {
+        const int2 wq = win[bid];
+        const int32_t spq = wq.y - wq.x + 1;
+        xdone = spq > 0 && spq <= xcap && spq <= XU * XT;  // uniform per workgroup
         const int64_t hw = bid * (S * P) + wv;
-        first.load(hval + hw * G * step + lane * KI, hcol + hw * G * step + lane * KI, 0, G, step);
+        if (xdone && __builtin_amdgcn_readfirstlane(wv) < kSellXCopy) {
+            double xv[XU];
+#pragma unroll
+            for (int k = 0; k < XU; ++k) {
+                const int32_t i = (int32_t)threadIdx.x + k * XT;
+                xv[k] = x[wq.x + (i < spq ? i : spq - 1)];
+            }
+            first.load(hval + hw * G * step + lane * KI, hcol + hw * G * step + lane * KI, 0, G, step);
+#pragma unroll
+            for (int k = 0; k < XU; ++k) {
+                const int32_t i = (int32_t)threadIdx.x + k * XT;
+                if (i < spq)
+                    s_x[i] = xv[k];
+            }
+        } else {
+            first.load(hval + hw * G * step + lane * KI, hcol + hw * G * step + lane * KI, 0, G, step);
+        }
     }
     // The slice bounds come through the scalar cache (a wave-uniform index):
     // as vector loads they returned behind the head's loads (loads return in
@@ -549,7 +576,7 @@ __global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell_small_
         wnd = win[bid];
         const int32_t span = wnd.y - wnd.x + 1;
         staged = span > 0 && span <= xcap;  // uniform per workgroup
-        if (staged)
+        if (staged && !xdone)
             copy_window<kWave * S * P, 4>(s_x, x, wnd.x, span);
         __syncthreads();
     }

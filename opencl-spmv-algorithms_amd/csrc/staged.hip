@@ -79,7 +79,10 @@ struct KeysNone {  // the tiled CSR: rows come from row_ptr, no keys
 // commit() writes the products and keys of the issued chunk to LDS.  A
 // kernel may issue the next chunk between a commit and the barrier that
 // publishes it (software pipelining), with the same result as stage_chunk.
-template <int R, bool NT, typename V, typename Keys>
+// SAFE2: the caller guarantees nz >= 2 (no branch on it: with one, the
+// compiler widened the column indices on the load path before the merge, so
+// it waited for the columns right after issuing them, before anything else)
+template <int R, bool NT, typename V, typename Keys, bool SAFE2 = false>
 struct StageRegs {
     double2 v[R];
     int2 c[R];
@@ -88,8 +91,9 @@ struct StageRegs {
     __device__ __forceinline__ void issue(int64_t cb, int64_t ce, int64_t nz, const int32_t *__restrict__ col,
                                           const V *__restrict__ val, const Keys &keys)
     {
-        if (nz < 2)  // uniform; a 1-entry array has no pair 0 (its entry: the tail in commit)
-            return;
+        if constexpr (!SAFE2)
+            if (nz < 2)  // uniform; a 1-entry array has no pair 0 (its entry: the tail in commit)
+                return;
         const int64_t spare = cb + 1 < nz ? cb : (nz - 2) & ~(int64_t)1;  // this chunk's first pair
 #pragma unroll
         for (int k = 0; k < R; ++k) {
@@ -106,7 +110,7 @@ struct StageRegs {
                                            const V *__restrict__ val, const XS &xs, double2 *s_prod,
                                            const Keys &keys) const
     {
-        if (nz >= 2) {
+        if (SAFE2 || nz >= 2) {
 #pragma unroll
             for (int k = 0; k < R; ++k) {
                 const int t = threadIdx.x + k * kBlock;
@@ -317,7 +321,7 @@ __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
         // the tile's pairs and the last row's entries past t1 (pair j at
         // t1 + 2j) in flight together, then the products of both
         static_assert(!XW, "the single-pass COO gathers x through xs");
-        StageRegs<R, NT, double, KeysRow32<NT>> st;
+        StageRegs<R, NT, double, KeysRow32<NT>, true> st;  // nnz >= 2 (coo_tiny_kernel below that)
         st.issue(t0, t1, nnz, col, val, keys);
         const int j = threadIdx.x;
         const int64_t p = t1 + 2 * (int64_t)j;
@@ -325,20 +329,21 @@ __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
         static_assert(TP <= kBlock, "one tail pair per thread");
         double2 tv = {0.0, 0.0};
         int2 tc = {0, 0}, tk = {0, 0};
-        if (tpair) {
-            tv = stream_load2<NT>(val + p);
-            tc = stream_load2<NT>(col + p);
-            tk = stream_load2<NT>(row + p);
-        } else if (tone) {
-            tv.x = stream_load<NT>(val + p);
-            tc.x = stream_load<NT>(col + p);
-            tk.x = stream_load<NT>(row + p);
-            tk.y = tk.x;  // never read: the row ends at 2j+1 = tail
+        // a pair, or the lone last entry: its pair is (p - 1, p) when p is
+        // the array's last entry (nnz >= 2 here; used in the products below)
+        const bool tsh = p + 1 >= nnz;
+        if (tpair || tone) {  // ONE branch: with two, a merge made the waves wait for the tile's loads first
+            const int64_t q = tsh ? nnz - 2 : p;
+            tv = stream_load2<NT>(val + q);
+            tc = stream_load2<NT>(col + q);
+            tk = stream_load2<NT>(row + q);
         }
         st.commit(t0, t1, nnz, col, val, xs, s_prod, keys);
         if (tpair || tone) {
-            s_prod[n / 2 + j] = tpair ? double2{tv.x * xs(tc.x), tv.y * xs(tc.y)} : double2{tv.x * xs(tc.x), 0.0};
-            s_row2[n / 2 + j] = tk;
+            const double v0 = tsh ? tv.y : tv.x;
+            const int32_t c0 = tsh ? tc.y : tc.x;
+            s_prod[n / 2 + j] = tpair ? double2{tv.x * xs(tc.x), tv.y * xs(tc.y)} : double2{v0 * xs(c0), 0.0};
+            s_row2[n / 2 + j] = tsh ? make_int2(tk.y, tk.y) : tk;  // (.y of a lone entry is never read)
         }
     } else if (staged) {
         stage_chunk<R, NT>(t0, t1, nnz, col, val, XWindow{s_x, wlo}, s_prod, keys);
@@ -537,7 +542,7 @@ __global__ __launch_bounds__(kBlock) void csr_tiled_kernel(
     const int64_t tile = blockIdx.x;
     const int64_t t0 = tile * CH;
     const int64_t t1 = t0 + CH < nnz ? t0 + CH : nnz;
-    StageRegs<R, NT, V, KeysNone> st;
+    StageRegs<R, NT, V, KeysNone, true> st;  // nnz >= 2 (launch_tiled_xs)
     st.issue(t0, t1, nnz, col, val, KeysNone{});
     const int64_t r_lo = own_lo[tile];
     const int64_t r_hi = t1 == nnz ? n_rows - 1 : (int64_t)own_lo[tile + 1] - 1;
@@ -885,11 +890,35 @@ static void launch_tiled_r(const spmv_dims &d, int64_t tiles, const int64_t *row
                            d.nnz, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val, R == 1 ? big : nullptr);
 }
 
+// A matrix of fewer than two entries (the tiled kernel loads entry pairs):
+// one workgroup, a row per thread; the carry pass that follows finds none.
+template <typename XS, typename V>
+__global__ __launch_bounds__(kBlock) void csr_tiny_kernel(int64_t n_rows, int64_t tiles,
+                                                          const int64_t *__restrict__ row_ptr,
+                                                          const int32_t *__restrict__ col, const V *__restrict__ val,
+                                                          const XS xs, double *__restrict__ y,
+                                                          int32_t *__restrict__ carry_row)
+{
+    for (int64_t r = threadIdx.x; r < n_rows; r += kBlock) {
+        double s = 0.0;
+        for (int64_t j = row_ptr[r]; j < row_ptr[r + 1]; ++j)
+            s += (double)val[j] * xs(col[j]);
+        y[r] = s;
+    }
+    if (threadIdx.x < tiles)
+        carry_row[threadIdx.x] = -1;
+}
+
 template <typename XS, typename V>
 static void launch_tiled_xs(const spmv_dims &d, int64_t tiles, const int64_t *row_ptr, const int32_t *col,
                             const V *val, XS xs, double *y, const int32_t *own_lo, int32_t *carry_row,
                             double *carry_val, const int32_t *big = nullptr)
 {
+    if (d.nnz < 2) {
+        hipLaunchKernelGGL((csr_tiny_kernel<XS, V>), dim3(1), dim3(kBlock), 0, (hipStream_t)d.stream, d.n_rows,
+                           tiles, row_ptr, col, val, xs, y, carry_row);
+        return;
+    }
     switch (tiled_r(d.n_rows, d.nnz)) {
     case 1: launch_tiled_r<1>(d, tiles, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val, big); break;
     case 2: launch_tiled_r<2>(d, tiles, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val, big); break;
@@ -1013,6 +1042,22 @@ static int coo_hot_r(int64_t n_rows, int64_t nnz)
 
 int64_t coo_hot_tile(int64_t n_rows, int64_t nnz) { return 2 * kBlock * coo_hot_r(n_rows, nnz); }
 
+// The single pass on fewer than two entries (its kernel loads entry pairs):
+// one workgroup; ACC adds into y, else y is written (zeros, then the entry).
+template <bool ACC>
+__global__ __launch_bounds__(kBlock) void coo_tiny_kernel(int64_t n_rows, int64_t nnz, const int32_t *__restrict__ row,
+                                                          const int32_t *__restrict__ col,
+                                                          const double *__restrict__ val,
+                                                          const double *__restrict__ x, double *__restrict__ y)
+{
+    if constexpr (!ACC)
+        for (int64_t r = threadIdx.x; r < n_rows; r += kBlock)
+            y[r] = 0.0;
+    __syncthreads();
+    if (threadIdx.x == 0 && nnz == 1)
+        y[row[0]] = (ACC ? y[row[0]] : 0.0) + val[0] * x[col[0]];
+}
+
 int launch_coo_staged_acc(const spmv_dims &d, const int32_t *row, const int32_t *col,
                           const double *val, const double *x, double *y, int32_t *carry_row,
                           double *carry_val, const int32_t *tails)
@@ -1023,7 +1068,10 @@ int launch_coo_staged_acc(const spmv_dims &d, const int32_t *row, const int32_t 
         return fail_msg(SPMV_OTHER_ERROR, "coo tail: grid too large");
     if (tiles == 0)
         return SPMV_SUCCESS;
-    if (tails)  // single pass: every tile finishes its last row (no carry)
+    if (tails && d.nnz < 2)
+        hipLaunchKernelGGL(coo_tiny_kernel<true>, dim3(1), dim3(kBlock), 0, (hipStream_t)d.stream, d.n_rows, d.nnz,
+                           row, col, val, x, y);
+    else if (tails)  // single pass: every tile finishes its last row (no carry)
         hipLaunchKernelGGL((coo_staged_kernel<4, R, true, false, false, XGlobal, true>), dim3((unsigned)tiles),
                            dim3(kBlock), 0, (hipStream_t)d.stream, d.n_rows, d.nnz, row, col, val, x, y,
                            carry_row, carry_val, (const int2 *)nullptr, 0, XGlobal{x}, tails,
@@ -1115,6 +1163,11 @@ int launch_coo_staged(const spmv_dims &d, const int32_t *row, const int32_t *col
     // profiles/round2/ab_coo_nt.log
     const bool nt = stream_nt(true);
     const int remap = xwin_remap(kCooRemapDefault) ? 1 : 0;  // the single pass (tails) only
+    if (tails && d.nnz < 2) {
+        hipLaunchKernelGGL(coo_tiny_kernel<false>, dim3(1), dim3(kBlock), 0, st, d.n_rows, d.nnz, row, col, val, x, y);
+        SPMV_CHECK_LAUNCH("coo_tiny_kernel");
+        return SPMV_SUCCESS;
+    }
 #define SPMV_COO_STAGED(LL)                                                                              \
     do {                                                                                                 \
         if (tails)                                                                                       \

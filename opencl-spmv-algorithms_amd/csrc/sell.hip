@@ -250,7 +250,9 @@ __global__ __launch_bounds__(kBlock) void ell_window_kernel(int64_t n_rows, int3
 }
 
 // ELL with the workgroup's x window staged in LDS (as sell_xwin_kernel).
-template <int KI, bool NT, int U>
+// WB: the window copied with 4 loads per thread in flight (copy_window);
+// else a strided copy, one round trip per 256 entries.
+template <int KI, bool NT, int U, bool WB = false>
 __global__ __launch_bounds__(kBlock) void ell_xwin_kernel(
     int64_t n_rows, int32_t K, int64_t ld, const int32_t *__restrict__ col,
     const double *__restrict__ val, const double *__restrict__ x,
@@ -262,10 +264,17 @@ __global__ __launch_bounds__(kBlock) void ell_xwin_kernel(
     const int32_t span = wnd.y - wnd.x + 1;
     const bool staged = span > 0 && span <= xcap;  // uniform per workgroup
     if (staged) {
-        // a strided copy: the batched copy_window measured 1 % slower here
-        // (0.3300 / 0.3272 vs 0.3244 / 0.3248 ms, profiles/round2/ab_formats.log)
-        for (int32_t j = threadIdx.x; j < span; j += kBlock)
-            s_x[j] = x[wnd.x + j];
+        // the strided copy: the batched copy_window measured 1 % slower on the
+        // 32-copy batch (0.3300 / 0.3272 vs 0.3244 / 0.3248 ms,
+        // profiles/round2/ab_formats.log) and 1.8 % faster on one cant-like
+        // matrix (11.88 -> 11.67 us cold, profiles/round5/ab_ell_wcopy.md),
+        // where every workgroup is resident at once and waits out the copy's
+        // round trips: batched for a grid of at most 4 workgroups per CU
+        if constexpr (WB)
+            copy_window<kBlock, 4>(s_x, x, wnd.x, span);
+        else
+            for (int32_t j = threadIdx.x; j < span; j += kBlock)
+                s_x[j] = x[wnd.x + j];
         __syncthreads();
     }
     const int64_t i = blk * kBlock + threadIdx.x;
@@ -1267,8 +1276,11 @@ extern "C" int spmv_ell_run_xwin(spmv_dims d, int32_t K, int64_t ld, int32_t ki,
     SPMV_GUARD(d);
     const int64_t blocks = (d.n_rows + kBlock - 1) / kBlock;
     const bool nt = stream_nt(kSellStreamNtDefault);
-    auto kern = ki == 2 ? (nt ? ell_xwin_kernel<2, true, 4> : ell_xwin_kernel<2, false, 4>)
-                        : (nt ? ell_xwin_kernel<1, true, 4> : ell_xwin_kernel<1, false, 4>);
+    auto kern = blocks <= 4 * 256
+                    ? (ki == 2 ? (nt ? ell_xwin_kernel<2, true, 4, true> : ell_xwin_kernel<2, false, 4, true>)
+                               : (nt ? ell_xwin_kernel<1, true, 4, true> : ell_xwin_kernel<1, false, 4, true>))
+                    : (ki == 2 ? (nt ? ell_xwin_kernel<2, true, 4> : ell_xwin_kernel<2, false, 4>)
+                               : (nt ? ell_xwin_kernel<1, true, 4> : ell_xwin_kernel<1, false, 4>));
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock), (size_t)xcap * sizeof(double),
                        (hipStream_t)d.stream, d.n_rows, K, ld, col, val, x, y, (const int2 *)win, xcap,
                        xwin_remap(kEllRemapDefault) ? 1 : 0);

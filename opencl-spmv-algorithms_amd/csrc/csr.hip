@@ -464,6 +464,39 @@ __global__ __launch_bounds__(kBlock) void csr_xwin_kernel(
         const int64_t r0 = g_beg * RPB;
         const int32_t nr = (int32_t)((g_end - g_beg) * RPB) + 1;
         constexpr int U = 2;  // offsets per thread per pass (nr <= U·256 in one pass)
+        constexpr int XU = 8;  // window entries per thread (copy_window's default)
+        if (nr <= U * kBlock && span <= XU * kBlock) {
+            // one pass, branch-free: the offsets' and the window's loads all
+            // go out before the first store (with the loop below the compiler
+            // waited for the offsets before requesting the window)
+            int64_t o[U];
+            double xv[XU];
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const int64_t r = r0 + threadIdx.x + k * kBlock;
+                o[k] = row_ptr[r < n_rows ? r : n_rows];
+            }
+            const int32_t xl = span > 0 ? span - 1 : 0;  // clamped (loaded, never stored past span)
+#pragma unroll
+            for (int k = 0; k < XU; ++k) {
+                const int32_t i = (int32_t)threadIdx.x + k * kBlock;
+                xv[k] = x[wnd.x + (i < xl ? i : xl)];
+            }
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const int32_t i = (int32_t)threadIdx.x + k * kBlock;
+                if (i < nr)
+                    s_off[i] = o[k];
+            }
+            if (staged) {
+#pragma unroll
+                for (int k = 0; k < XU; ++k) {
+                    const int32_t i = (int32_t)threadIdx.x + k * kBlock;
+                    if (i < span)
+                        s_x[i] = xv[k];
+                }
+            }
+        } else
         for (int32_t b = 0; b < nr; b += U * kBlock) {
             int64_t o[U];
 #pragma unroll

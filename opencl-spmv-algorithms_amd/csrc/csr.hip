@@ -283,6 +283,20 @@ struct StreamRegs {
 // L-lane reduction instead of after it.  s_off holds the window's
 // ngroups·RPB + 1 row offsets.  Chunks and per-row sums are exactly those
 // of staged_group (same boundaries, same order): the same bits.
+#ifdef SPMV_CSR_STAMPS  // lab builds only (tools/sell_stamps.py --kernel csr): per-wave phase times
+constexpr int kCsrStampWaves = 8192, kCsrStamps = 8;
+__device__ uint64_t g_csr_stamps[kCsrStampWaves * kCsrStamps];
+#define CSR_STAMP(k)                                                                                   \
+    do {                                                                                               \
+        const int64_t sw_ = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;                    \
+        if ((threadIdx.x & 63) == 0 && sw_ < kCsrStampWaves && (k) < kCsrStamps)                       \
+            g_csr_stamps[sw_ * kCsrStamps + (k)] = __builtin_amdgcn_s_memrealtime();                   \
+    } while (0)
+#else
+#define CSR_STAMP(k) \
+    do {             \
+    } while (0)
+#endif
 template <int L, int R, bool NT, typename XS, typename V, typename Cols = Col32<NT>>
 __device__ __forceinline__ void staged_window_pipelined(int64_t row0, int ngroups, const int64_t *s_off,
                                                         double2 *s_prod, const Cols cols,
@@ -308,6 +322,8 @@ __device__ __forceinline__ void staged_window_pipelined(int64_t row0, int ngroup
         const int64_t b = chunk_start(s_off[jn * RPB]), e = s_off[(jn + 1) * RPB];
         st.issue(b, b + CH < e ? b + CH : e, nz, cols, val);
     }
+    int nchunk = 0;
+    (void)nchunk;
     for (int gi = 0; gi < ngroups; ++gi) {
         const int64_t *gp = s_off + gi * RPB;
         const int64_t beg = gp[g], end = gp[g + 1];
@@ -316,6 +332,8 @@ __device__ __forceinline__ void staged_window_pipelined(int64_t row0, int ngroup
         for (int64_t cb = chunk_start(gp[0]); cb < blk_end; cb += CH) {
             const int64_t ce = cb + CH < blk_end ? cb + CH : blk_end;
             st.products(cb, ce, nz, cols, val, xs, s_prod);
+            CSR_STAMP(2 + nchunk);
+            ++nchunk;
             // the next chunk: this group's, else the next group's first
             if (cb + CH < blk_end) {
                 const int64_t nb = cb + CH;
@@ -444,6 +462,7 @@ __global__ __launch_bounds__(kBlock) void csr_xwin_kernel(
     int remap)
 {
     static_assert(MODE == 0 || MODE == 3, "csr_xwin_kernel: MODE 0 or 3");
+    CSR_STAMP(0);
     constexpr int RPB = kBlock / L;
     extern __shared__ double s_x[];
     __shared__ int64_t s_ptr[MODE == 3 ? 1 : RPB + 1];
@@ -514,6 +533,7 @@ __global__ __launch_bounds__(kBlock) void csr_xwin_kernel(
             }
         }
         __syncthreads();  // window and offsets visible
+        CSR_STAMP(1);
         if (staged)
             staged_window_pipelined<L, R, NT, XWindow, V, Cols>(r0, (int)(g_end - g_beg), s_off, s_prod, cols, val,
                                                                XWindow{s_x, wnd.x}, y, n_rows, nz);
@@ -659,6 +679,13 @@ extern "C" int spmv_csr_auto_lanes(int64_t n_rows, int64_t nnz)
         L *= 2;
     return L;
 }
+
+#ifdef SPMV_CSR_STAMPS
+extern "C" int spmv_lab_csr_stamps(void *host, size_t bytes)
+{
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_csr_stamps), bytes);
+}
+#endif
 
 extern "C" int spmv_csr_run_variant(spmv_dims d, const int64_t *row_ptr,
                                     const int32_t *col, const double *val,

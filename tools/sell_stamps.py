@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""sell_stamps — where the small-matrix SELL kernel's time goes, per wave.
+"""sell_stamps — where the small-matrix SELL (or the CSR x-window) kernel's time goes, per wave.
 
 Lab only.  Runs the library's SELL (int32, head copy) and SELL16 on one
 cant-like matrix with a lab build of libspmv_hip.so compiled with
@@ -9,7 +9,9 @@ and reads the per-wave s_memrealtime stamps (100 MHz, 10 ns) that build
 writes at: 0 start, 1 x window published (barrier), 2 first batch summed,
 3 all batches summed, 4 partial sums published (barrier), 5 y stored.
 Prints medians over launches of the kernel span and of each phase's
-distribution over the waves (p10 / p50 / p90 / max, us)."""
+distribution over the waves (p10 / p50 / p90 / max, us).  --kernel csr: the
+CSR x-window kernel of a -DSPMV_CSR_STAMPS build (0 start, 1 window and
+offsets published, 2.. each chunk's products in LDS)."""
 from __future__ import annotations
 
 import argparse
@@ -32,14 +34,17 @@ PHASES = [("window", 0, 1), ("first_batch", 1, 2), ("batches", 2, 3), ("part_bar
 
 
 def q(v):
-    return [round(float(np.percentile(v, p)), 3) for p in (10, 50, 90)] + [round(float(np.max(v)), 3)]
+    return [round(float(np.nanpercentile(v, p)), 3) for p in (10, 50, 90)] + [round(float(np.nanmax(v)), 3)]
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--formats", default="sell,sell16")
+    ap.add_argument("--kernel", default="sell", choices=["sell", "csr"])
     a = ap.parse_args()
+    if a.kernel == "csr":
+        return csr_main(a)
     if not os.environ.get("SPMV_HIP_LIB"):
         sys.exit("set SPMV_HIP_LIB to a -DSPMV_SELL_STAMPS build")
     import torch
@@ -103,6 +108,51 @@ def main():
                    "groups_per_wave_p10_p50_p90_max": [int(np.percentile(gw, p)) for p in (10, 50, 90, 100)]}
             print(json.dumps(out), flush=True)
         del dm
+
+
+def csr_main(a):
+    import torch
+
+    dev = torch.device("cuda:0")
+    sp = torch.cuda.current_stream(dev).cuda_stream
+    P = probe_lib()
+    fn = sa.hip_lib().spmv_lab_csr_stamps
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    fn.restype = ctypes.c_int
+    scratch = torch.empty(FLUSH_BYTES, dtype=torch.uint8, device=dev)
+    fsink = torch.zeros(16, dtype=torch.int32, device=dev)
+    m = sa.gen_cantlike(0, 1)
+    xh = sa.ramp_x(m.n_cols)
+    x = torch.from_numpy(xh).to(dev)
+    host = np.zeros(NWAVES * NSTAMP, dtype=np.uint64)
+    dm = sa.to_device(m, "csr", dev)
+    y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
+    nw = ((m.n_rows + 127) // 128) * 4
+    for state in ("cold", "warm"):
+        rows = []
+        for _ in range(a.reps):
+            host[:] = 0
+            if state == "cold":
+                assert P.spmv_probe_flush_read(scratch.data_ptr(), FLUSH_BYTES, fsink.data_ptr(), sp) == 0
+            dm.run(x, y)
+            torch.cuda.synchronize()
+            assert fn(host.ctypes.data, host.nbytes) == 0
+            t = host[: nw * NSTAMP].reshape(nw, NSTAMP).astype(np.int64)
+            t0 = t[:, 0].min()
+            us = np.where(t > 0, (t - t0) * 0.01, np.nan)
+            last = np.nanmax(us, axis=1)
+            rows.append({"span": float(np.nanmax(last)),
+                         "start": q(us[:, 0]), "window": q(us[:, 1] - us[:, 0]),
+                         "chunks": [q(us[:, k + 1] - us[:, k]) for k in range(1, NSTAMP - 1)
+                                    if not np.all(np.isnan(us[:, k + 1]))]})
+        bad, _ = sa.check(m, xh, y.cpu().numpy())
+        out = {"format": "csr", "state": state, "waves": nw, "parity_ok": bad == 0,
+               "span_us_median": round(float(np.median([r["span"] for r in rows])), 3),
+               "start_us": np.median(np.array([r["start"] for r in rows]), axis=0).round(3).tolist(),
+               "window_us": np.median(np.array([r["window"] for r in rows]), axis=0).round(3).tolist(),
+               "chunk_us": [np.median(np.array([r["chunks"][k] for r in rows if len(r["chunks"]) > k]), axis=0)
+                            .round(3).tolist() for k in range(max(len(r["chunks"]) for r in rows))]}
+        print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":

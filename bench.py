@@ -124,6 +124,10 @@ def parse():
     p.add_argument("--cold-flush", default="read", choices=["read", "write"],
                    help="headline cold state: 512 MiB READ (clean lines, default) or WRITTEN before every SpMV; "
                         "the other is timed beside it")
+    p.add_argument("--relabel-ties", default="first", choices=["first", "id"],
+                   help="R-MAT relabel: equal-degree columns in order of their first row (default: neighbouring "
+                        "rows' low-degree columns share x lines; whole R-MAT 0.715 -> 0.680 ms, "
+                        "profiles/round5/ab_rmat_ties.md) or by column id")
     p.add_argument("--relabel", default="auto", choices=["auto", "yes", "no"],
                    help="R-MAT: columns relabelled by decreasing degree at build time (spmv_column_relabel), x "
                         "replicated in that layout (auto: yes); no = the per-run hot-column table instead")
@@ -761,11 +765,13 @@ def rmat_layout(args, n, ptr, col, val):
     xh = sa.ramp_x(n)
     if args.relabel == "no":
         return col, xh, None, "hot-column table (per-run fill of the 2^19 hottest x entries)"
-    order, _, col2 = sa.column_relabel(n, col)
+    order, _, col2 = sa.column_relabel(n, col, args.relabel_ties)
     sa.csr_sort_rows(n, ptr, col2, val)
-    return col2, np.ascontiguousarray(xh[order]), 0, ("columns relabelled by decreasing degree at build time "
-                                                     "(spmv_column_relabel), each row's entries in new-column "
-                                                     "order (spmv_csr_sort_rows); x replicated in that layout")
+    ties = "first row" if args.relabel_ties == "first" else "column id"
+    return col2, np.ascontiguousarray(xh[order]), 0, (f"columns relabelled by decreasing degree at build time, "
+                                                     f"ties by {ties} (spmv_column_relabel_ex), each row's entries "
+                                                     "in new-column order (spmv_csr_sort_rows); x replicated in "
+                                                     "that layout")
 
 
 def rmat_strong(args, torch, dev, rank, world, dist, cdev):

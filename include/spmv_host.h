@@ -123,6 +123,12 @@ int64_t spmv_csr_tiled_bigplan(int64_t n_rows, const int64_t *row_ptr, int64_t t
  * bad input.                                                             */
 int64_t spmv_column_relabel(int64_t n_cols, int64_t nnz, const int32_t *col, int32_t *order, int32_t *newid,
                             int32_t *col_out);
+/* The same with a choice of tie order among equal counts: ties = 0 lower
+ * column first (spmv_column_relabel), 1 first appearance in col (for a
+ * row-major CSR col: the first row that uses the column, so the low-degree
+ * columns of neighbouring rows share x' lines).  -1 on bad input.        */
+int64_t spmv_column_relabel_ex(int64_t n_cols, int64_t nnz, const int32_t *col, int32_t *order, int32_t *newid,
+                               int32_t *col_out, int32_t ties);
 
 /* ELL, column-major with leading dimension ld = round_up(N, 64) and
  * k-interleave ki (spmv.h).  K = round_up(max row length, ki).

@@ -364,6 +364,14 @@ int64_t spmv_csr_tiled_bigplan(int64_t n_rows, const int64_t *row_ptr, int64_t t
 int64_t spmv_column_relabel(int64_t n_cols, int64_t nnz, const int32_t *col, int32_t *order, int32_t *newid,
                             int32_t *col_out)
 {
+    return spmv_column_relabel_ex(n_cols, nnz, col, order, newid, col_out, 0);
+}
+
+int64_t spmv_column_relabel_ex(int64_t n_cols, int64_t nnz, const int32_t *col, int32_t *order, int32_t *newid,
+                               int32_t *col_out, int32_t ties)
+{
+    if (ties != 0 && ties != 1)
+        return -1;
     if (n_cols <= 0 || n_cols > INT32_MAX || nnz < 0 || !order || !newid || (nnz > 0 && (!col || !col_out)))
         return -1;
     int64_t *cnt = (int64_t *)calloc((size_t)n_cols, sizeof(int64_t));
@@ -392,10 +400,31 @@ int64_t spmv_column_relabel(int64_t n_cols, int64_t nnz, const int32_t *col, int
         first[k] = acc;
         acc += h;
     }
-    for (int64_t c = 0; c < n_cols; ++c) {
-        const int64_t r = first[cnt[c]]++;
-        order[r] = (int32_t)c;
-        newid[c] = (int32_t)r;
+    if (ties == 0) {
+        for (int64_t c = 0; c < n_cols; ++c) {
+            const int64_t r = first[cnt[c]]++;
+            order[r] = (int32_t)c;
+            newid[c] = (int32_t)r;
+        }
+    } else {
+        /* equal counts in order of first appearance in col (row-major CSR:
+         * the first row using the column), unused columns last by id */
+        for (int64_t c = 0; c < n_cols; ++c)
+            newid[c] = -1;
+        for (int64_t j = 0; j < nnz; ++j) {
+            const int32_t c = col[j];
+            if (newid[c] < 0) {
+                const int64_t r = first[cnt[c]]++;
+                order[r] = c;
+                newid[c] = (int32_t)r;
+            }
+        }
+        for (int64_t c = 0; c < n_cols; ++c)
+            if (cnt[c] == 0) {
+                const int64_t r = first[0]++;
+                order[r] = (int32_t)c;
+                newid[c] = (int32_t)r;
+            }
     }
     free(first);
     free(cnt);

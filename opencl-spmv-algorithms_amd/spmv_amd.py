@@ -219,6 +219,7 @@ HOST_SYMBOLS = {
     "spmv_csr_pick_variant": (ctypes.c_int, [_c_i64, _vp]),
     "spmv_hot_columns": (_c_i64, [_c_i64, _c_i64, _vp, _c_i64, _vp, _vp]),
     "spmv_column_relabel": (_c_i64, [_c_i64, _c_i64, _vp, _vp, _vp, _vp]),
+    "spmv_column_relabel_ex": (_c_i64, [_c_i64, _c_i64, _vp, _vp, _vp, _vp, _c_i32]),
     "spmv_csr_tiled_bigplan": (_c_i64, [_c_i64, _vp, _c_i64, _c_i32, _vp]),
     "spmv_ell_plan": (ctypes.c_int, [_c_i64, _vp, _c_i32, ctypes.POINTER(_c_i32), ctypes.POINTER(_c_i64)]),
     "spmv_ell_fill": (ctypes.c_int, [_c_i64, _vp, _vp, _vp, _c_i32, _c_i64, _c_i32, _vp, _vp]),
@@ -490,15 +491,19 @@ def hot_columns(n_cols: int, col, H: int = 0):
     return int(n), hot[:n].copy(), out[: col.size]
 
 
-def column_relabel(n_cols: int, col):
-    """spmv_column_relabel: (order, newid, col') — columns ranked by
-    decreasing entry count; x' = x[order] is the input of the relabelled
-    matrix, whose y is the original's, row for row."""
+def column_relabel(n_cols: int, col, ties: str = "id"):
+    """spmv_column_relabel(_ex): (order, newid, col') — columns ranked by
+    decreasing entry count, ties by column id or (ties="first") by first
+    appearance in col; x' = x[order] is the input of the relabelled matrix,
+    whose y is the original's, row for row."""
+    if ties not in ("id", "first"):
+        raise SpmvError(OTHER_ERROR, "spmv_column_relabel", f"ties must be 'id' or 'first', not {ties!r}")
     col = np.ascontiguousarray(col, dtype=np.int32)
     order = np.empty(n_cols, np.int32)
     newid = np.empty(n_cols, np.int32)
     out = np.empty(max(col.size, 1), np.int32)
-    n = host_lib().spmv_column_relabel(n_cols, col.size, _ptr(col), _ptr(order), _ptr(newid), _ptr(out))
+    n = host_lib().spmv_column_relabel_ex(n_cols, col.size, _ptr(col), _ptr(order), _ptr(newid), _ptr(out),
+                                          0 if ties == "id" else 1)
     if n < 0:
         raise SpmvError(OTHER_ERROR, "spmv_column_relabel", "bad arguments")
     return order, newid, out[: col.size]

@@ -481,12 +481,47 @@ def test_csr_tiled_bigplan(tile, cap):
     assert lib.spmv_csr_tiled_bigplan(m.n_rows, ptr.ctypes.data, 1, cap, None) == -1
 
 
+@pytest.mark.parametrize("kind", ["random", "rmat", "tiny"])
+def test_column_relabel_ties_first(kind):
+    """spmv_column_relabel_ex(ties = 1): the same count ranking, equal
+    counts in order of first appearance in col (unused columns last by
+    id); the relabelled matrix gives the oracle's y bit for bit."""
+    if kind == "rmat":
+        m = sa.gen_rmat(100_000, 1_000_000, scale=17, seed=2)
+    elif kind == "tiny":
+        m = sa.Coo(3, 6, np.array([0, 0, 1, 1, 1, 2, 2, 2], np.int32), np.array([3, 1, 3, 2, 1, 0, 5, 3], np.int32),
+                   np.arange(1.0, 9.0))
+    else:
+        m = sa.gen_random(500, 5000, 0, 9, seed=4)
+    order, newid, c2 = sa.column_relabel(m.n_cols, m.col, "first")
+    cnt = np.bincount(m.col, minlength=m.n_cols)
+    assert np.array_equal(np.sort(order), np.arange(m.n_cols))
+    assert np.array_equal(newid[order], np.arange(m.n_cols))
+    assert np.all(np.diff(cnt[order]) <= 0)
+    first = np.full(m.n_cols, np.iinfo(np.int64).max)
+    np.minimum.at(first, m.col, np.arange(m.col.size))
+    key = np.where(cnt[order] > 0, first[order], m.col.size + order)  # unused: after, by id
+    ties = np.diff(cnt[order]) == 0
+    assert np.all(np.diff(key)[ties] > 0)
+    assert np.array_equal(c2, newid[m.col])
+    x = np.random.default_rng(1).uniform(-1, 1, m.n_cols)
+    assert np.array_equal(oracle.file_order_spmv(m.n_rows, m.row, m.col, m.val, x),
+                          oracle.file_order_spmv(m.n_rows, m.row, c2, m.val, np.ascontiguousarray(x[order])))
+    if kind == "tiny":
+        assert order.tolist() == [3, 1, 2, 0, 5, 4]
+
+
 def test_column_relabel_bad_input():
     lib = sa.host_lib()
     col = np.array([0, 5], np.int32)
     buf = np.empty(8, np.int32)
     assert lib.spmv_column_relabel(5, 2, col.ctypes.data, buf.ctypes.data, buf.ctypes.data, buf.ctypes.data) == -1
     assert lib.spmv_column_relabel(0, 0, None, buf.ctypes.data, buf.ctypes.data, None) == -1
+    assert lib.spmv_column_relabel_ex(5, 2, col.ctypes.data, buf.ctypes.data, buf.ctypes.data, buf.ctypes.data, 1) == -1
+    ok = np.array([0, 1], np.int32)
+    assert lib.spmv_column_relabel_ex(5, 2, ok.ctypes.data, buf.ctypes.data, buf.ctypes.data, buf.ctypes.data, 2) == -1
+    with pytest.raises(sa.SpmvError):
+        sa.column_relabel(5, ok, "degree")
 
 
 def _rmat_like_ptr(n=200_000, seed=3):

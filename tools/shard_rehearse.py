@@ -85,6 +85,8 @@ def main():
                     help="each re-cut moves the cut points this fraction of the way (bench.py's RMAT_DAMP)")
     ap.add_argument("--sort-rows", action="store_true",
                     help="after the relabel: every row's entries by increasing column (spmv_csr_sort_rows)")
+    ap.add_argument("--ties", default="first", choices=["id", "first"],
+                    help="relabel ties: column id, or first appearance (the first row using the column)")
     ap.add_argument("--relabel", action="store_true",
                     help="columns relabelled by decreasing degree (spmv_column_relabel), x permuted to match; "
                          "no hot-column table")
@@ -107,7 +109,7 @@ def main():
     del full
     xh = sa.ramp_x(n)
     if a.relabel:  # the replicated x arrives in the relabelled layout (outside the timed step)
-        order, _, col = sa.column_relabel(n, col)
+        order, _, col = sa.column_relabel(n, col, a.ties)
         xh = np.ascontiguousarray(xh[order])
         a.hot = "0"
     if a.sort_rows:
@@ -165,7 +167,7 @@ def run_split(a, torch, sa, dev, ptr, col, val, n, x, xh, b_total, envs, kw, G, 
         if cold:
             extra = {"shard_ms_cold": [round(t, 4) for t in cold], "max_ms_cold": round(max(cold), 4),
                      "aggregate_GBs_cold": round(b_total / (max(cold) * 1e-3) * 1e-9, 1)}
-        print(json.dumps({"workload": "rmat 1e7/1e8", "format": a.format, "relabel": a.relabel, "sort_rows": a.sort_rows, "env": env,
+        print(json.dumps({"workload": "rmat 1e7/1e8", "format": a.format, "relabel": a.relabel, "ties": a.ties, "sort_rows": a.sort_rows, "env": env,
                           "params_shard0": params,
                           "gpus": G, "row_weight": w, "hot": hot, "graph": a.graph, "calibration_pass": cpass,
                           "shard_rows": np.diff(bounds).tolist(), "shard_nnz": nnzs,

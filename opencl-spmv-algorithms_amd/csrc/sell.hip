@@ -319,6 +319,10 @@ constexpr int kSellSmallS = SPMV_SELL_SMALL_S;  // sell_small_kernel: waves per 
 #endif
 constexpr int kSellSmallP = SPMV_SELL_SMALL_P;  // sell_small_kernel: slices per workgroup (and per x window)
 constexpr int kSellXCopy = 4;  // sell_small_kernel: waves that copy the x window (HEAD)
+#ifndef SPMV_SELL_LAST_B  // A/B builds only
+#define SPMV_SELL_LAST_B 8
+#endif
+constexpr int kSellLastB = SPMV_SELL_LAST_B;  // sell_small_kernel: the largest last batch
 
 static void sell_geometry(int32_t C, int32_t sigma, int64_t n_slices, int *bt, int64_t *blocks)
 {
@@ -607,10 +611,23 @@ __global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell_small_
         int64_t g = g0 + G;
         if (g < g1)
             nb.fma4(src, g, g1, a);
-        for (g += 4; g < g1; g += 4) {  // same batches, same order: the same bits
+        // later batches of 4 groups, the last one up to kSellLastB: a short
+        // remainder rides with the batch before it instead of costing a
+        // round trip of its own (same groups, same accumulators, same order:
+        // the same bits).  One cant-like matrix cold, four interleaved rounds:
+        // SELL 10.27 -> 10.21 us, SELL16 9.48 -> 9.26; a last batch of up to
+        // 6 groups measured slower (profiles/round5/ab_sell_pipe.md)
+        for (g += 4; g < g1;) {
+            if (g1 - g <= kSellLastB) {
+                SlotBatch<KI, NT, kSellLastB> b;
+                b.load(vp, cp, g, g1, step);
+                b.fma4(src, g, g1, a);
+                break;
+            }
             SlotBatch<KI, NT, 4> b;
             b.load(vp, cp, g, g1, step);
             b.fma4(src, g, g1, a);
+            g += 4;
         }
         SELL_STAMP(3);
     };

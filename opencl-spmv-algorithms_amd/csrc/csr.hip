@@ -332,7 +332,7 @@ __device__ __forceinline__ void staged_window_pipelined(int64_t row0, int ngroup
         for (int64_t cb = chunk_start(gp[0]); cb < blk_end; cb += CH) {
             const int64_t ce = cb + CH < blk_end ? cb + CH : blk_end;
             st.products(cb, ce, nz, cols, val, xs, s_prod);
-            CSR_STAMP(2 + nchunk);
+            CSR_STAMP(nchunk == 0 ? 2 : 5 + nchunk);  // 2: chunk 0's products; 6, 7: chunks 1, 2
             ++nchunk;
             // the next chunk: this group's, else the next group's first
             if (cb + CH < blk_end) {
@@ -343,8 +343,14 @@ __device__ __forceinline__ void staged_window_pipelined(int64_t row0, int ngroup
                 st.issue(b, b + CH < e ? b + CH : e, nz, cols, val);
             }
             __syncthreads();
+            if (nchunk == 1)
+                CSR_STAMP(3);  // chunk 0: products published
             acc += slice_sum<L>(prod, beg > cb ? beg - cb : 0, (end < ce ? end : ce) - cb, lane);
+            if (nchunk == 1)
+                CSR_STAMP(4);  // chunk 0: row sums read
             __syncthreads();
+            if (nchunk == 1)
+                CSR_STAMP(5);  // chunk 0: second barrier
         }
         acc = group_sum<L>(acc);
         const int64_t row = row0 + (int64_t)gi * RPB + g;

@@ -11,7 +11,8 @@ writes at: 0 start, 1 x window published (barrier), 2 first batch summed,
 Prints medians over launches of the kernel span and of each phase's
 distribution over the waves (p10 / p50 / p90 / max, us).  --kernel csr: the
 CSR x-window kernel of a -DSPMV_CSR_STAMPS build (0 start, 1 window and
-offsets published, 2.. each chunk's products in LDS)."""
+offsets published, 2 chunk 0's products in LDS, 3 its barrier, 4 its row
+sums read, 5 its second barrier, 6 / 7 chunks 1 / 2's products in LDS)."""
 from __future__ import annotations
 
 import argparse

@@ -1305,6 +1305,15 @@ extern "C" int spmv_ell_run_xwin(spmv_dims d, int32_t K, int64_t ld, int32_t ki,
     return SPMV_SUCCESS;
 }
 
+// Lanes per tail row: 4 for the long rows' remainders; with K = 0 the tail
+// is the whole matrix (power-law rows, where most rows are short: R-MAT
+// picks K = 0) and takes COO's choice from the mean row.  The hot-column
+// run picks the same, so it keeps spmv_hyb_run's bits.
+static int hyb_tail_lanes(const spmv_dims &d, int32_t K, int64_t tail_nnz)
+{
+    return K == 0 ? coo_lanes(d.n_rows, tail_nnz) : 4;
+}
+
 extern "C" size_t spmv_hyb_ws_bytes(int64_t tail_nnz)
 {
     return spmv_coo_ws_bytes(tail_nnz);
@@ -1332,7 +1341,8 @@ extern "C" int spmv_hyb_run(spmv_dims d, int32_t K, int64_t ld, int32_t ki, cons
     int32_t *carry_row = (int32_t *)(carry_val + tiles);
     spmv_dims dt = d;
     dt.nnz = tail_nnz;
-    rc = launch_coo_staged_acc(dt, tail_row, tail_col, tail_val, x, y, carry_row, carry_val);
+    rc = launch_coo_staged_acc(dt, tail_row, tail_col, tail_val, x, y, carry_row, carry_val, nullptr,
+                               hyb_tail_lanes(d, K, tail_nnz));
     if (rc != SPMV_SUCCESS)
         return rc;
     return launch_carry(tiles, carry_row, carry_val, y, (hipStream_t)d.stream);
@@ -1357,7 +1367,7 @@ extern "C" int spmv_hyb_run_tail(spmv_dims d, int32_t K, int64_t ld, int32_t ki,
     spmv_dims dt = d;
     dt.nnz = tail_nnz;
     return launch_coo_staged_acc(dt, tail_row, tail_col, tail_val, x, y, nullptr, nullptr,
-                                 (const int32_t *)tails);
+                                 (const int32_t *)tails, hyb_tail_lanes(d, K, tail_nnz));
 }
 
 // HYB with a single-pass tail and the ELL part through the x-window ELL
@@ -1379,7 +1389,7 @@ extern "C" int spmv_hyb_run_tail_xwin(spmv_dims d, int32_t K, int64_t ld, int32_
     spmv_dims dt = d;
     dt.nnz = tail_nnz;
     return launch_coo_staged_acc(dt, tail_row, tail_col, tail_val, x, y, nullptr, nullptr,
-                                 (const int32_t *)tails);
+                                 (const int32_t *)tails, hyb_tail_lanes(d, K, tail_nnz));
 }
 
 extern "C" size_t spmv_sell_split_ws_bytes(int64_t n_chunks, int32_t C)
@@ -1554,7 +1564,8 @@ extern "C" int spmv_hyb_run_hot(spmv_dims d, int32_t K, int64_t ld, int32_t ki, 
     int32_t *carry_row = (int32_t *)(carry_val + tiles);
     spmv_dims dt = d;
     dt.nnz = tail_nnz;
-    int rc = launch_coo_staged_acc_hot(dt, tail_row, tail_col_hot, tail_val, x, y, carry_row, carry_val, xs);
+    int rc = launch_coo_staged_acc_hot(dt, tail_row, tail_col_hot, tail_val, x, y, carry_row, carry_val, xs,
+                                       hyb_tail_lanes(d, K, tail_nnz));
     if (rc != SPMV_SUCCESS)
         return rc;
     return launch_carry(tiles, carry_row, carry_val, y, st);

@@ -109,7 +109,8 @@ using namespace spmv;
 
 extern "C" size_t spmv_coo_ws_bytes(int64_t nnz)
 {
-    const int64_t t = coo_staged_tile();
+    // the carry pass may cut 512-entry tiles (coo_hot_tile): sized for them
+    const int64_t t = 2 * kBlock;
     const int64_t tiles = nnz > 0 ? (nnz + t - 1) / t : 0;
     // carry_val (8-byte aligned) first, then carry_row
     return (size_t)(tiles * (int64_t)sizeof(double) + tiles * (int64_t)sizeof(int32_t) + 16);
@@ -132,7 +133,7 @@ extern "C" int spmv_coo_run(spmv_dims d, const int32_t *row,
     }
     if (!ws || ws_bytes < spmv_coo_ws_bytes(d.nnz))
         return fail_msg(SPMV_OTHER_ERROR, "spmv_coo_run: workspace too small");
-    const int64_t st_tiles = (d.nnz + coo_staged_tile() - 1) / coo_staged_tile();
+    const int64_t st_tiles = (d.nnz + coo_hot_tile(d.n_rows, d.nnz) - 1) / coo_hot_tile(d.n_rows, d.nnz);
     double *cv = (double *)ws;
     int32_t *cr = (int32_t *)(cv + st_tiles);
     int rc = launch_coo_staged(d, row, col, val, x, y, cr, cv);
@@ -261,7 +262,7 @@ extern "C" int spmv_coo_run_xwin(spmv_dims d, const int32_t *row, const int32_t 
     if (!ws || ws_bytes < spmv_coo_ws_bytes(d.nnz))
         return fail_msg(SPMV_OTHER_ERROR, "spmv_coo_run_xwin: workspace too small");
     SPMV_GUARD(d);
-    const int64_t st_tiles = (d.nnz + coo_staged_tile() - 1) / coo_staged_tile();
+    const int64_t st_tiles = (d.nnz + coo_hot_tile(d.n_rows, d.nnz) - 1) / coo_hot_tile(d.n_rows, d.nnz);
     double *cv = (double *)ws;
     int32_t *cr = (int32_t *)(cv + st_tiles);
     int rc = launch_coo_staged(d, row, col, val, x, y, cr, cv, (const int2 *)win, xcap);

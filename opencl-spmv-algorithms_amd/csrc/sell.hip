@@ -1314,6 +1314,12 @@ static int hyb_tail_lanes(const spmv_dims &d, int32_t K, int64_t tail_nnz)
     return K == 0 ? coo_lanes(d.n_rows, tail_nnz) : 4;
 }
 
+// Tile of the tail's carry pass: COO's (coo_hot_tile) for a whole matrix.
+static int64_t hyb_tail_tile(const spmv_dims &d, int32_t K, int64_t tail_nnz)
+{
+    return K == 0 ? coo_hot_tile(d.n_rows, tail_nnz) : coo_staged_tile();
+}
+
 extern "C" size_t spmv_hyb_ws_bytes(int64_t tail_nnz)
 {
     return spmv_coo_ws_bytes(tail_nnz);
@@ -1336,13 +1342,14 @@ extern "C" int spmv_hyb_run(spmv_dims d, int32_t K, int64_t ld, int32_t ki, cons
     if (!ws || ws_bytes < spmv_hyb_ws_bytes(tail_nnz))
         return fail_msg(SPMV_OTHER_ERROR, "spmv_hyb_run: workspace too small");
     SPMV_GUARD(d);
-    const int64_t tiles = (tail_nnz + coo_staged_tile() - 1) / coo_staged_tile();
+    const int64_t tile = hyb_tail_tile(d, K, tail_nnz);
+    const int64_t tiles = (tail_nnz + tile - 1) / tile;
     double *carry_val = (double *)ws;
     int32_t *carry_row = (int32_t *)(carry_val + tiles);
     spmv_dims dt = d;
     dt.nnz = tail_nnz;
     rc = launch_coo_staged_acc(dt, tail_row, tail_col, tail_val, x, y, carry_row, carry_val, nullptr,
-                               hyb_tail_lanes(d, K, tail_nnz));
+                               hyb_tail_lanes(d, K, tail_nnz), tile);
     if (rc != SPMV_SUCCESS)
         return rc;
     return launch_carry(tiles, carry_row, carry_val, y, (hipStream_t)d.stream);
@@ -1559,13 +1566,14 @@ extern "C" int spmv_hyb_run_hot(spmv_dims d, int32_t K, int64_t ld, int32_t ki, 
     SPMV_CHECK_LAUNCH("ell_kernel (hot columns)");
     if (tail_nnz == 0)
         return SPMV_SUCCESS;
-    const int64_t tiles = (tail_nnz + coo_staged_tile() - 1) / coo_staged_tile();
+    const int64_t tile = hyb_tail_tile(d, K, tail_nnz);
+    const int64_t tiles = (tail_nnz + tile - 1) / tile;
     double *carry_val = xh + H;
     int32_t *carry_row = (int32_t *)(carry_val + tiles);
     spmv_dims dt = d;
     dt.nnz = tail_nnz;
     int rc = launch_coo_staged_acc_hot(dt, tail_row, tail_col_hot, tail_val, x, y, carry_row, carry_val, xs,
-                                       hyb_tail_lanes(d, K, tail_nnz));
+                                       hyb_tail_lanes(d, K, tail_nnz), tile);
     if (rc != SPMV_SUCCESS)
         return rc;
     return launch_carry(tiles, carry_row, carry_val, y, st);

@@ -1067,13 +1067,20 @@ int coo_lanes(int64_t n_rows, int64_t nnz)
 }
 
 // lanes: 4 for a HYB tail (the long rows' remainders); a whole matrix
-// (HYB with K = 0) takes coo_lanes and non-temporal stream loads, as COO.
+// (HYB with K = 0) takes coo_lanes and non-temporal stream loads, as COO,
+// and its carry pass COO's tiles (tile = coo_hot_tile; the single pass
+// keeps coo_staged_tile, the tail plan's).
 int launch_coo_staged_acc(const spmv_dims &d, const int32_t *row, const int32_t *col,
                           const double *val, const double *x, double *y, int32_t *carry_row,
-                          double *carry_val, const int32_t *tails, int lanes)
+                          double *carry_val, const int32_t *tails, int lanes, int64_t tile)
 {
     constexpr int R = kCooR;
-    const int64_t tiles = (d.nnz + coo_staged_tile() - 1) / coo_staged_tile();
+    if (tile == 0)
+        tile = coo_staged_tile();
+    if (tile != coo_staged_tile() && (tails || tile != 2 * kBlock))
+        return fail_msg(SPMV_OTHER_ERROR, "coo tail: bad tile");
+    const bool r1 = tile != coo_staged_tile();
+    const int64_t tiles = (d.nnz + tile - 1) / tile;
     if (tiles > INT32_MAX)
         return fail_msg(SPMV_OTHER_ERROR, "coo tail: grid too large");
     if (tiles == 0)
@@ -1093,6 +1100,10 @@ int launch_coo_staged_acc(const spmv_dims &d, const int32_t *row, const int32_t 
             hipLaunchKernelGGL((coo_staged_kernel<LL, R, true, false, NTT, XGlobal, true>),                \
                                dim3((unsigned)tiles), dim3(kBlock), 0, st, d.n_rows, d.nnz, row, col, val, x, \
                                y, carry_row, carry_val, (const int2 *)nullptr, 0, XGlobal{x}, tails, remap); \
+        else if (r1)                                                                                       \
+            hipLaunchKernelGGL((coo_staged_kernel<LL, 1, true, false, NTT>), dim3((unsigned)tiles),         \
+                               dim3(kBlock), 0, st, d.n_rows, d.nnz, row, col, val, x, y, carry_row,        \
+                               carry_val, (const int2 *)nullptr, 0, XGlobal{x});                           \
         else                                                                                               \
             hipLaunchKernelGGL((coo_staged_kernel<LL, R, true, false, NTT>), dim3((unsigned)tiles),         \
                                dim3(kBlock), 0, st, d.n_rows, d.nnz, row, col, val, x, y, carry_row,        \
@@ -1111,20 +1122,32 @@ int launch_coo_staged_acc(const spmv_dims &d, const int32_t *row, const int32_t 
 
 int launch_coo_staged_acc_hot(const spmv_dims &d, const int32_t *row, const int32_t *col,
                               const double *val, const double *x, double *y, int32_t *carry_row,
-                              double *carry_val, const XHot xs, int lanes)
+                              double *carry_val, const XHot xs, int lanes, int64_t tile)
 {
     constexpr int R = kCooR;
-    const int64_t tiles = (d.nnz + coo_staged_tile() - 1) / coo_staged_tile();
+    if (tile == 0)
+        tile = coo_staged_tile();
+    if (tile != coo_staged_tile() && tile != 2 * kBlock)
+        return fail_msg(SPMV_OTHER_ERROR, "hyb tail: bad tile");
+    const bool r1 = tile != coo_staged_tile();
+    const int64_t tiles = (d.nnz + tile - 1) / tile;
     if (tiles > INT32_MAX)
         return fail_msg(SPMV_OTHER_ERROR, "hyb tail: grid too large");
     if (tiles == 0)
         return SPMV_SUCCESS;
     if (lanes != 2 && lanes != 4 && lanes != 8)
         return fail_msg(SPMV_OTHER_ERROR, "hyb tail: lanes must be 2, 4 or 8");
-#define SPMV_COO_ACC_HOT(LL)                                                                              \
-    hipLaunchKernelGGL((coo_staged_kernel<LL, R, true, false, true, XHot>), dim3((unsigned)tiles), dim3(kBlock), \
+#define SPMV_COO_ACC_HOT_R(LL, RR)                                                                        \
+    hipLaunchKernelGGL((coo_staged_kernel<LL, RR, true, false, true, XHot>), dim3((unsigned)tiles), dim3(kBlock), \
                        0, (hipStream_t)d.stream, d.n_rows, d.nnz, row, col, val, x, y, carry_row, carry_val,   \
                        (const int2 *)nullptr, 0, xs)
+#define SPMV_COO_ACC_HOT(LL)           \
+    do {                               \
+        if (r1)                        \
+            SPMV_COO_ACC_HOT_R(LL, 1); \
+        else                           \
+            SPMV_COO_ACC_HOT_R(LL, R); \
+    } while (0)
     if (lanes == 4)
         SPMV_COO_ACC_HOT(4);
     else if (lanes == 8)
@@ -1132,6 +1155,7 @@ int launch_coo_staged_acc_hot(const spmv_dims &d, const int32_t *row, const int3
     else
         SPMV_COO_ACC_HOT(2);
 #undef SPMV_COO_ACC_HOT
+#undef SPMV_COO_ACC_HOT_R
     SPMV_CHECK_LAUNCH("coo_staged_kernel (accumulate, hot columns)");
     return SPMV_SUCCESS;
 }
@@ -1186,7 +1210,12 @@ int launch_coo_staged(const spmv_dims &d, const int32_t *row, const int32_t *col
                       double *carry_val, const int2 *win, int32_t xcap, const int32_t *tails)
 {
     constexpr int R = kCooR;
-    const int64_t tiles = (d.nnz + coo_staged_tile() - 1) / coo_staged_tile();
+    // the carry pass (with or without x windows) cuts the hot path's tiles
+    // (512 entries below a mean row of 96: R-MAT 1.046 -> 0.872 ms warm), so
+    // all three keep the same bits; the single pass, 1536
+    const int64_t tile = tails ? coo_staged_tile() : coo_hot_tile(d.n_rows, d.nnz);
+    const bool r1 = tile != coo_staged_tile();
+    const int64_t tiles = (d.nnz + tile - 1) / tile;
     if (tiles > INT32_MAX)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_coo_run: grid too large");
     const hipStream_t st = (hipStream_t)d.stream;
@@ -1210,13 +1239,25 @@ int launch_coo_staged(const spmv_dims &d, const int32_t *row, const int32_t *col
                                dim3((unsigned)tiles), dim3(kBlock), 0, st, d.n_rows, d.nnz, row, col, val, \
                                x, y, carry_row, carry_val, (const int2 *)nullptr, 0, XGlobal{x}, tails,   \
                                remap);                                                                   \
+        else if (win && r1)                                                                              \
+            hipLaunchKernelGGL((coo_staged_kernel<LL, 1, false, true>), dim3((unsigned)tiles),            \
+                               dim3(kBlock), lds, st, d.n_rows, d.nnz, row, col, val, x, y, carry_row,    \
+                               carry_val, win, xcap, XGlobal{x});                                        \
         else if (win)                                                                                    \
             hipLaunchKernelGGL((coo_staged_kernel<LL, R, false, true>), dim3((unsigned)tiles),            \
                                dim3(kBlock), lds, st, d.n_rows, d.nnz, row, col, val, x, y, carry_row,    \
                                carry_val, win, xcap, XGlobal{x});                                        \
+        else if (nt && r1)                                                                               \
+            hipLaunchKernelGGL((coo_staged_kernel<LL, 1, false, false, true, XGlobal, false, RC>),       \
+                               dim3((unsigned)tiles), dim3(kBlock), 0, st, d.n_rows, d.nnz, row, col, val, \
+                               x, y, carry_row, carry_val, (const int2 *)nullptr, 0, XGlobal{x});         \
         else if (nt)                                                                                     \
             hipLaunchKernelGGL((coo_staged_kernel<LL, R, false, false, true, XGlobal, false, RC>),       \
                                dim3((unsigned)tiles),                                                    \
+                               dim3(kBlock), 0, st, d.n_rows, d.nnz, row, col, val, x, y, carry_row,      \
+                               carry_val, (const int2 *)nullptr, 0, XGlobal{x});                         \
+        else if (r1)                                                                                     \
+            hipLaunchKernelGGL((coo_staged_kernel<LL, 1, false, false>), dim3((unsigned)tiles),           \
                                dim3(kBlock), 0, st, d.n_rows, d.nnz, row, col, val, x, y, carry_row,      \
                                carry_val, (const int2 *)nullptr, 0, XGlobal{x});                         \
         else                                                                                             \
@@ -1342,7 +1383,8 @@ using namespace spmv;
 
 extern "C" size_t spmv_coo_xwin_bytes(int64_t nnz)
 {
-    return nnz > 0 ? (size_t)((nnz + coo_staged_tile() - 1) / coo_staged_tile()) * sizeof(int2) : 0;
+    // one window per carry-pass tile (coo_hot_tile: 512 or 1536 entries)
+    return nnz > 0 ? (size_t)((nnz + 2 * kBlock - 1) / (2 * kBlock)) * sizeof(int2) : 0;
 }
 
 extern "C" int spmv_coo_xwin_build(spmv_dims d, const int32_t *col, void *win, size_t win_bytes, int32_t *xcap)
@@ -1355,11 +1397,12 @@ extern "C" int spmv_coo_xwin_build(spmv_dims d, const int32_t *col, void *win, s
     if (!win || win_bytes < spmv_coo_xwin_bytes(d.nnz))
         return fail_msg(SPMV_OTHER_ERROR, "spmv_coo_xwin_build: window buffer too small");
     SPMV_GUARD(d);
-    const int64_t tiles = (d.nnz + coo_staged_tile() - 1) / coo_staged_tile();
+    const int64_t tile = coo_hot_tile(d.n_rows, d.nnz);
+    const int64_t tiles = (d.nnz + tile - 1) / tile;
     if (tiles > INT32_MAX)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_coo_xwin_build: grid too large");
     const hipStream_t st = (hipStream_t)d.stream;
-    hipLaunchKernelGGL(tile_window_kernel, dim3((unsigned)tiles), dim3(kBlock), 0, st, d.nnz, coo_staged_tile(), col,
+    hipLaunchKernelGGL(tile_window_kernel, dim3((unsigned)tiles), dim3(kBlock), 0, st, d.nnz, tile, col,
                        (int2 *)win);
     SPMV_CHECK_LAUNCH("tile_window_kernel");
     return windows_xcap((const int2 *)win, tiles, kStagedXwinCap, st, xcap, "spmv_coo_xwin_build: copy windows");

@@ -61,9 +61,7 @@ int64_t coo_hot_tile(int64_t n_rows, int64_t nnz);
 // accumulate mode: y[r] += entries of the rows present (HYB tail)
 int launch_coo_staged_acc(const spmv_dims &d, const int32_t *row, const int32_t *col,
                           const double *val, const double *x, double *y, int32_t *carry_row,
-                          double *carry_val, const int32_t *tails = nullptr, int lanes = 4,
-                          int64_t tile = 0);  // 0: coo_staged_tile()
-int coo_lanes(int64_t n_rows, int64_t nnz);
+                          double *carry_val, const int32_t *tails = nullptr);
 int launch_csr_tiled(const spmv_dims &d, const int64_t *row_ptr, const int32_t *col,
                      const double *val, const double *x, double *y, int32_t *own_lo,
                      int32_t *carry_row, double *carry_val);
@@ -82,8 +80,7 @@ int launch_cmrs_tiled(const spmv_dims &d, int32_t h, int64_t n_strips, const int
 struct XHot;
 int launch_coo_staged_acc_hot(const spmv_dims &d, const int32_t *row, const int32_t *col,
                               const double *val, const double *x, double *y, int32_t *carry_row,
-                              double *carry_val, const XHot xs, int lanes = 4,
-                              int64_t tile = 0);  // 0: coo_staged_tile()
+                              double *carry_val, const XHot xs);
 int launch_coo_staged_hot(const spmv_dims &d, const int32_t *row, const int32_t *col, const double *val,
                           const double *x, double *y, int32_t *carry_row, double *carry_val, int64_t H,
                           const int32_t *hot, double *xh);

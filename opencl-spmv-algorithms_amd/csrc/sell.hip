@@ -1305,19 +1305,14 @@ extern "C" int spmv_ell_run_xwin(spmv_dims d, int32_t K, int64_t ld, int32_t ki,
     return SPMV_SUCCESS;
 }
 
-// Lanes per tail row: 4 for the long rows' remainders; with K = 0 the tail
-// is the whole matrix (power-law rows, where most rows are short: R-MAT
-// picks K = 0) and takes COO's choice from the mean row.  The hot-column
-// run picks the same, so it keeps spmv_hyb_run's bits.
-static int hyb_tail_lanes(const spmv_dims &d, int32_t K, int64_t tail_nnz)
+// HYB with K = 0, the plan's choice where most rows are empty or short (an
+// ELL slot would cost more than the tail entry it saves: R-MAT): no ELL
+// part, the tail is the whole matrix in row order, so it runs as COO (same
+// kernels and workspace; y written, not zeroed and then added to: R-MAT
+// 1.587 -> 0.870 ms).  Bad K / ld / ki fall through to the ELL checks.
+static bool hyb_is_coo(const spmv_dims &d, int32_t K, int64_t ld, int32_t ki, int64_t tail_nnz)
 {
-    return K == 0 ? coo_lanes(d.n_rows, tail_nnz) : 4;
-}
-
-// Tile of the tail's carry pass: COO's (coo_hot_tile) for a whole matrix.
-static int64_t hyb_tail_tile(const spmv_dims &d, int32_t K, int64_t tail_nnz)
-{
-    return K == 0 ? coo_hot_tile(d.n_rows, tail_nnz) : coo_staged_tile();
+    return K == 0 && d.n_rows > 0 && ld >= d.n_rows && ld % 64 == 0 && (ki == 1 || ki == 2) && tail_nnz > 0;
 }
 
 extern "C" size_t spmv_hyb_ws_bytes(int64_t tail_nnz)
@@ -1336,20 +1331,20 @@ extern "C" int spmv_hyb_run(spmv_dims d, int32_t K, int64_t ld, int32_t ki, cons
 {
     if (tail_nnz < 0)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_hyb_run: negative tail size");
+    spmv_dims dt = d;
+    dt.nnz = tail_nnz;
+    if (hyb_is_coo(d, K, ld, ki, tail_nnz))
+        return spmv_coo_run(dt, tail_row, tail_col, tail_val, x, y, ws, ws_bytes);
     int rc = spmv_ell_run(d, K, ld, ki, ell_col, ell_val, x, y);
     if (rc != SPMV_SUCCESS || tail_nnz == 0 || d.n_rows == 0)
         return rc;
     if (!ws || ws_bytes < spmv_hyb_ws_bytes(tail_nnz))
         return fail_msg(SPMV_OTHER_ERROR, "spmv_hyb_run: workspace too small");
     SPMV_GUARD(d);
-    const int64_t tile = hyb_tail_tile(d, K, tail_nnz);
-    const int64_t tiles = (tail_nnz + tile - 1) / tile;
+    const int64_t tiles = (tail_nnz + coo_staged_tile() - 1) / coo_staged_tile();
     double *carry_val = (double *)ws;
     int32_t *carry_row = (int32_t *)(carry_val + tiles);
-    spmv_dims dt = d;
-    dt.nnz = tail_nnz;
-    rc = launch_coo_staged_acc(dt, tail_row, tail_col, tail_val, x, y, carry_row, carry_val, nullptr,
-                               hyb_tail_lanes(d, K, tail_nnz), tile);
+    rc = launch_coo_staged_acc(dt, tail_row, tail_col, tail_val, x, y, carry_row, carry_val);
     if (rc != SPMV_SUCCESS)
         return rc;
     return launch_carry(tiles, carry_row, carry_val, y, (hipStream_t)d.stream);
@@ -1365,16 +1360,18 @@ extern "C" int spmv_hyb_run_tail(spmv_dims d, int32_t K, int64_t ld, int32_t ki,
 {
     if (tail_nnz < 0)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_hyb_run_tail: negative tail size");
+    spmv_dims dt = d;
+    dt.nnz = tail_nnz;
+    if (hyb_is_coo(d, K, ld, ki, tail_nnz))
+        return spmv_coo_run_tail(dt, tail_row, tail_col, tail_val, x, y, tails);
     int rc = spmv_ell_run(d, K, ld, ki, ell_col, ell_val, x, y);
     if (rc != SPMV_SUCCESS || tail_nnz == 0 || d.n_rows == 0)
         return rc;
     if (!tails)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_hyb_run_tail: no tail plan");
     SPMV_GUARD(d);
-    spmv_dims dt = d;
-    dt.nnz = tail_nnz;
     return launch_coo_staged_acc(dt, tail_row, tail_col, tail_val, x, y, nullptr, nullptr,
-                                 (const int32_t *)tails, hyb_tail_lanes(d, K, tail_nnz));
+                                 (const int32_t *)tails);
 }
 
 // HYB with a single-pass tail and the ELL part through the x-window ELL
@@ -1387,16 +1384,18 @@ extern "C" int spmv_hyb_run_tail_xwin(spmv_dims d, int32_t K, int64_t ld, int32_
 {
     if (tail_nnz < 0)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_hyb_run_tail_xwin: negative tail size");
+    spmv_dims dt = d;
+    dt.nnz = tail_nnz;
+    if (hyb_is_coo(d, K, ld, ki, tail_nnz))
+        return spmv_coo_run_tail(dt, tail_row, tail_col, tail_val, x, y, tails);
     int rc = spmv_ell_run_xwin(d, K, ld, ki, ell_col, ell_val, x, y, win, xcap);
     if (rc != SPMV_SUCCESS || tail_nnz == 0 || d.n_rows == 0)
         return rc;
     if (!tails)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_hyb_run_tail_xwin: no tail plan");
     SPMV_GUARD(d);
-    spmv_dims dt = d;
-    dt.nnz = tail_nnz;
     return launch_coo_staged_acc(dt, tail_row, tail_col, tail_val, x, y, nullptr, nullptr,
-                                 (const int32_t *)tails, hyb_tail_lanes(d, K, tail_nnz));
+                                 (const int32_t *)tails);
 }
 
 extern "C" size_t spmv_sell_split_ws_bytes(int64_t n_chunks, int32_t C)
@@ -1545,6 +1544,11 @@ extern "C" int spmv_hyb_run_hot(spmv_dims d, int32_t K, int64_t ld, int32_t ki, 
     if (H == 0)
         return spmv_hyb_run(d, K, ld, ki, ell_col_hot, ell_val, tail_nnz, tail_row, tail_col_hot, tail_val, x, y,
                             ws, ws_bytes);
+    if (hyb_is_coo(d, K, ld, ki, tail_nnz)) {  // as spmv_hyb_run: the COO over the same table
+        spmv_dims dt = d;
+        dt.nnz = tail_nnz;
+        return spmv_coo_run_hot(dt, tail_row, tail_col_hot, tail_val, x, y, H, hot, ws, ws_bytes);
+    }
     if (d.n_rows < 0 || K < 0 || ld < d.n_rows || ld % 64 != 0 || (ki != 1 && ki != 2) || K % ki != 0)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_hyb_run_hot: bad K / ld / ki");
     if (d.n_rows == 0)
@@ -1566,14 +1570,12 @@ extern "C" int spmv_hyb_run_hot(spmv_dims d, int32_t K, int64_t ld, int32_t ki, 
     SPMV_CHECK_LAUNCH("ell_kernel (hot columns)");
     if (tail_nnz == 0)
         return SPMV_SUCCESS;
-    const int64_t tile = hyb_tail_tile(d, K, tail_nnz);
-    const int64_t tiles = (tail_nnz + tile - 1) / tile;
+    const int64_t tiles = (tail_nnz + coo_staged_tile() - 1) / coo_staged_tile();
     double *carry_val = xh + H;
     int32_t *carry_row = (int32_t *)(carry_val + tiles);
     spmv_dims dt = d;
     dt.nnz = tail_nnz;
-    int rc = launch_coo_staged_acc_hot(dt, tail_row, tail_col_hot, tail_val, x, y, carry_row, carry_val, xs,
-                                       hyb_tail_lanes(d, K, tail_nnz), tile);
+    int rc = launch_coo_staged_acc_hot(dt, tail_row, tail_col_hot, tail_val, x, y, carry_row, carry_val, xs);
     if (rc != SPMV_SUCCESS)
         return rc;
     return launch_carry(tiles, carry_row, carry_val, y, st);

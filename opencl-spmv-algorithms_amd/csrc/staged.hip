@@ -1058,104 +1058,45 @@ __global__ __launch_bounds__(kBlock) void coo_tiny_kernel(int64_t n_rows, int64_
         y[row[0]] = (ACC ? y[row[0]] : 0.0) + val[0] * x[col[0]];
 }
 
-// Lanes per row of the staged COO kernel from the mean row (as
-// launch_coo_staged): 8 from 48 entries, 4 from 12, else 2.
-int coo_lanes(int64_t n_rows, int64_t nnz)
-{
-    const double mean = n_rows > 0 ? (double)nnz / (double)n_rows : 0.0;
-    return mean >= 48.0 ? 8 : mean >= 12.0 ? 4 : 2;
-}
-
-// lanes: 4 for a HYB tail (the long rows' remainders); a whole matrix
-// (HYB with K = 0) takes coo_lanes and non-temporal stream loads, as COO,
-// and its carry pass COO's tiles (tile = coo_hot_tile; the single pass
-// keeps coo_staged_tile, the tail plan's).
 int launch_coo_staged_acc(const spmv_dims &d, const int32_t *row, const int32_t *col,
                           const double *val, const double *x, double *y, int32_t *carry_row,
-                          double *carry_val, const int32_t *tails, int lanes, int64_t tile)
+                          double *carry_val, const int32_t *tails)
 {
     constexpr int R = kCooR;
-    if (tile == 0)
-        tile = coo_staged_tile();
-    if (tile != coo_staged_tile() && (tails || tile != 2 * kBlock))
-        return fail_msg(SPMV_OTHER_ERROR, "coo tail: bad tile");
-    const bool r1 = tile != coo_staged_tile();
-    const int64_t tiles = (d.nnz + tile - 1) / tile;
+    const int64_t tiles = (d.nnz + coo_staged_tile() - 1) / coo_staged_tile();
     if (tiles > INT32_MAX)
         return fail_msg(SPMV_OTHER_ERROR, "coo tail: grid too large");
     if (tiles == 0)
         return SPMV_SUCCESS;
-    if (lanes != 2 && lanes != 4 && lanes != 8)
-        return fail_msg(SPMV_OTHER_ERROR, "coo tail: lanes must be 2, 4 or 8");
-    const hipStream_t st = (hipStream_t)d.stream;
-    const int remap = xwin_remap(kCooRemapDefault) ? 1 : 0;
-    if (tails && d.nnz < 2) {
-        hipLaunchKernelGGL(coo_tiny_kernel<true>, dim3(1), dim3(kBlock), 0, st, d.n_rows, d.nnz, row, col, val, x, y);
-        SPMV_CHECK_LAUNCH("coo_tiny_kernel (accumulate)");
-        return SPMV_SUCCESS;
-    }
-#define SPMV_COO_ACC(LL, NTT)                                                                              \
-    do {                                                                                                   \
-        if (tails)  /* single pass: every tile finishes its last row (no carry) */                         \
-            hipLaunchKernelGGL((coo_staged_kernel<LL, R, true, false, NTT, XGlobal, true>),                \
-                               dim3((unsigned)tiles), dim3(kBlock), 0, st, d.n_rows, d.nnz, row, col, val, x, \
-                               y, carry_row, carry_val, (const int2 *)nullptr, 0, XGlobal{x}, tails, remap); \
-        else if (r1)                                                                                       \
-            hipLaunchKernelGGL((coo_staged_kernel<LL, 1, true, false, NTT>), dim3((unsigned)tiles),         \
-                               dim3(kBlock), 0, st, d.n_rows, d.nnz, row, col, val, x, y, carry_row,        \
-                               carry_val, (const int2 *)nullptr, 0, XGlobal{x});                           \
-        else                                                                                               \
-            hipLaunchKernelGGL((coo_staged_kernel<LL, R, true, false, NTT>), dim3((unsigned)tiles),         \
-                               dim3(kBlock), 0, st, d.n_rows, d.nnz, row, col, val, x, y, carry_row,        \
-                               carry_val, (const int2 *)nullptr, 0, XGlobal{x});                           \
-    } while (0)
-    if (lanes == 4)
-        SPMV_COO_ACC(4, false);
-    else if (lanes == 8)
-        SPMV_COO_ACC(8, true);
+    if (tails && d.nnz < 2)
+        hipLaunchKernelGGL(coo_tiny_kernel<true>, dim3(1), dim3(kBlock), 0, (hipStream_t)d.stream, d.n_rows, d.nnz,
+                           row, col, val, x, y);
+    else if (tails)  // single pass: every tile finishes its last row (no carry)
+        hipLaunchKernelGGL((coo_staged_kernel<4, R, true, false, false, XGlobal, true>), dim3((unsigned)tiles),
+                           dim3(kBlock), 0, (hipStream_t)d.stream, d.n_rows, d.nnz, row, col, val, x, y,
+                           carry_row, carry_val, (const int2 *)nullptr, 0, XGlobal{x}, tails,
+                           xwin_remap(kCooRemapDefault) ? 1 : 0);
     else
-        SPMV_COO_ACC(2, true);
-#undef SPMV_COO_ACC
+        hipLaunchKernelGGL((coo_staged_kernel<4, R, true, false>), dim3((unsigned)tiles), dim3(kBlock), 0,
+                           (hipStream_t)d.stream, d.n_rows, d.nnz, row, col, val, x, y, carry_row, carry_val,
+                           (const int2 *)nullptr, 0, XGlobal{x});
     SPMV_CHECK_LAUNCH("coo_staged_kernel (accumulate)");
     return SPMV_SUCCESS;
 }
 
 int launch_coo_staged_acc_hot(const spmv_dims &d, const int32_t *row, const int32_t *col,
                               const double *val, const double *x, double *y, int32_t *carry_row,
-                              double *carry_val, const XHot xs, int lanes, int64_t tile)
+                              double *carry_val, const XHot xs)
 {
     constexpr int R = kCooR;
-    if (tile == 0)
-        tile = coo_staged_tile();
-    if (tile != coo_staged_tile() && tile != 2 * kBlock)
-        return fail_msg(SPMV_OTHER_ERROR, "hyb tail: bad tile");
-    const bool r1 = tile != coo_staged_tile();
-    const int64_t tiles = (d.nnz + tile - 1) / tile;
+    const int64_t tiles = (d.nnz + coo_staged_tile() - 1) / coo_staged_tile();
     if (tiles > INT32_MAX)
         return fail_msg(SPMV_OTHER_ERROR, "hyb tail: grid too large");
     if (tiles == 0)
         return SPMV_SUCCESS;
-    if (lanes != 2 && lanes != 4 && lanes != 8)
-        return fail_msg(SPMV_OTHER_ERROR, "hyb tail: lanes must be 2, 4 or 8");
-#define SPMV_COO_ACC_HOT_R(LL, RR)                                                                        \
-    hipLaunchKernelGGL((coo_staged_kernel<LL, RR, true, false, true, XHot>), dim3((unsigned)tiles), dim3(kBlock), \
-                       0, (hipStream_t)d.stream, d.n_rows, d.nnz, row, col, val, x, y, carry_row, carry_val,   \
-                       (const int2 *)nullptr, 0, xs)
-#define SPMV_COO_ACC_HOT(LL)           \
-    do {                               \
-        if (r1)                        \
-            SPMV_COO_ACC_HOT_R(LL, 1); \
-        else                           \
-            SPMV_COO_ACC_HOT_R(LL, R); \
-    } while (0)
-    if (lanes == 4)
-        SPMV_COO_ACC_HOT(4);
-    else if (lanes == 8)
-        SPMV_COO_ACC_HOT(8);
-    else
-        SPMV_COO_ACC_HOT(2);
-#undef SPMV_COO_ACC_HOT
-#undef SPMV_COO_ACC_HOT_R
+    hipLaunchKernelGGL((coo_staged_kernel<4, R, true, false, true, XHot>), dim3((unsigned)tiles), dim3(kBlock), 0,
+                       (hipStream_t)d.stream, d.n_rows, d.nnz, row, col, val, x, y, carry_row, carry_val,
+                       (const int2 *)nullptr, 0, xs);
     SPMV_CHECK_LAUNCH("coo_staged_kernel (accumulate, hot columns)");
     return SPMV_SUCCESS;
 }

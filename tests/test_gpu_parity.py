@@ -1045,6 +1045,26 @@ def test_hyb_single_pass_tail(torch_dev, case):
         assert_parity(m, yb.cpu().numpy(), x.cpu().numpy()[: m.n_cols])
 
 
+@pytest.mark.parametrize("hot", [0, 4096])
+def test_hyb_k0_runs_as_coo(torch_dev, hot):
+    """HYB whose plan picks K = 0 (R-MAT: most rows empty or short) has no
+    ELL part: it runs as COO over the same entries (spmv_coo_run /
+    spmv_coo_run_hot), so y has COO's bits, NaN-prefilled y fully written."""
+    torch, dev = torch_dev
+    m = sa.gen_rmat(1_000_000, 10_000_000, scale=20, seed=3)
+    a = sa.to_device(m, "hyb", dev, hot=hot)
+    b = sa.to_device(m, "coo", dev, hot=hot)
+    assert a.params["K"] == 0 and a.params["tail_nnz"] == m.nnz and a.params["H"] == b.params["H"]
+    x = torch.from_numpy(np.random.default_rng(11).uniform(-1, 1, m.n_cols)).to(dev)
+    ya = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
+    yb = torch.full_like(ya, float("nan"))
+    a.run(x, ya)
+    b.run(x, yb)
+    torch.cuda.synchronize()
+    assert torch.equal(ya.view(torch.int64), yb.view(torch.int64))
+    assert_parity(m, ya.cpu().numpy(), x.cpu().numpy())
+
+
 def test_coo_single_pass_empty_row_run_search_path(torch_dev):
     """the single pass with mean rows >= 12 (the 250-row start
     table) where one tile spans more rows than the table (a run of 400 empty

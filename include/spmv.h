@@ -231,6 +231,9 @@ int spmv_hyb_run_hot(spmv_dims d, int32_t K, int64_t ld, int32_t ki, const int32
                      const double *ell_val, int64_t tail_nnz, const int32_t *tail_row,
                      const int32_t *tail_col_hot, const double *tail_val, const double *x, double *y,
                      int64_t H, const int32_t *hot, void *ws, size_t ws_bytes);
+/* K = 0 (no ELL part; the tail is the whole matrix): every spmv_hyb_run*
+ * runs it as COO (spmv_coo_run / spmv_coo_run_tail / spmv_coo_run_hot) and
+ * y has COO's bits. */
 int spmv_hyb_run(spmv_dims d, int32_t K, int64_t ld, int32_t ki, const int32_t *ell_col,
                  const double *ell_val, int64_t tail_nnz, const int32_t *tail_row,
                  const int32_t *tail_col, const double *tail_val, const double *x, double *y,

@@ -27,7 +27,7 @@ HIPFLAGS += -g
 endif
 
 HIP_SRC  := $(wildcard $(PKG)/csrc/*.hip)
-HIP_HDR  := $(wildcard $(PKG)/csrc/*.h) include/spmv.h include/spmv_rc.h
+HIP_HDR  := $(wildcard $(PKG)/csrc/*.h) include/spmv.h include/spmv_ext.h include/spmv_host.h include/spmv_rc.h
 HOST_SRC := $(wildcard $(PKG)/host/*.c)
 TARGETS  := coo csr ell sigma_c cmrs
 
@@ -49,13 +49,16 @@ build/hip/%.o: $(PKG)/csrc/%.hip $(HIP_HDR)
 	@mkdir -p build/hip
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIB_HIP): $(HIP_OBJ)
+# the plans (csrc/plan.hip) call the host rules of libspmv_host.so
+# (variant rules, SELL split plan, tiled-CSR big-tile plan): linked by soname
+# and found next to libspmv_hip.so ($ORIGIN)
+$(LIB_HIP): $(HIP_OBJ) $(LIB_HOST)
 	@mkdir -p $(LIBDIR)
-	$(HIPCC) $(HIPFLAGS) -shared $(HIP_OBJ) -o $@ -ldl
+	$(HIPCC) $(HIPFLAGS) -shared $(HIP_OBJ) -o $@ -L$(LIBDIR) -lspmv_host -Wl,-rpath,'$$ORIGIN' -ldl
 
 $(LIB_HOST): $(HOST_SRC) include/spmv_host.h include/spmv_rc.h
 	@mkdir -p $(LIBDIR)
-	$(CC) $(CFLAGS) -shared $(HOST_SRC) -o $@ -lm
+	$(CC) $(CFLAGS) -shared $(HOST_SRC) -o $@ -Wl,-soname,libspmv_host.so -lm
 
 $(TARGETS): %: $(BINDIR)/%
 

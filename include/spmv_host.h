@@ -86,6 +86,9 @@ int spmv_csr_row_stats(int64_t n_rows, const int64_t *row_ptr,
  * entries and 64x the mean (a row-per-group kernel would then wait on one
  * group), else 0 (the library's row-group default).                    */
 int spmv_csr_pick_variant(int64_t n_rows, const int64_t *row_ptr);
+/* The rule itself, from the longest row (max_len) and the entry count:
+ * shared with the CSR plan of spmv.h, which finds max_len on the device. */
+int spmv_csr_variant_rule(int64_t n_rows, int64_t nnz, int64_t max_len);
 
 /* Hot columns for spmv_csr_run_tiled_hot: the H most frequent columns in
  * decreasing count (ties: lower column first) into hot[], and col_out
@@ -98,6 +101,10 @@ int spmv_csr_pick_variant(int64_t n_rows, const int64_t *row_ptr);
  * hot[] holds max(H_req, 2^19) entries.  Returns H, -1 on bad input.    */
 int64_t spmv_hot_columns(int64_t n_cols, int64_t nnz, const int32_t *col, int64_t H_req, int32_t *hot,
                          int32_t *col_out);
+/* 0 when spmv_hot_columns(n_cols, ..., H_req, ...) returns 0 whatever the
+ * columns (the rule never tables a matrix of <= 2^21 columns): lets a
+ * caller skip fetching the columns.                                      */
+int spmv_hot_columns_possible(int64_t n_cols, int64_t H_req);
 
 /* Big-tile plan of the entry-balanced CSR (spmv_csr_run_tiled_plan):
  * with tiles of `tile` entries (spmv_csr_tiled_tile), every tile owning
@@ -160,6 +167,8 @@ int spmv_cmrs_build(int64_t n_rows, const int64_t *row_ptr, int32_t h,
 /* 1 = entry-balanced (spmv_cmrs_run_tiled) when the longest strip exceeds
  * both 4,096 entries and 64x the mean strip, else 0 (spmv_cmrs_run).    */
 int spmv_cmrs_pick_variant(int64_t n_strips, const int64_t *strip_ptr);
+/* The rule from the longest strip and the entry count (the CMRS plan).  */
+int spmv_cmrs_variant_rule(int64_t n_strips, int64_t nnz, int64_t max_len);
 
 /* SELL split plan for wide slices (spmv_sell_run_split).  _auto gives T
  * (slot columns kept by the main kernel, a multiple of ki) or 0 when no

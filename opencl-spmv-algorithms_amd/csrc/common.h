@@ -6,6 +6,7 @@
 #include <stdint.h>
 
 #include "spmv.h"
+#include "spmv_ext.h"
 
 namespace spmv {
 
@@ -29,14 +30,17 @@ class DeviceGuard {
     int rc_ = SPMV_SUCCESS;
 };
 
-// The library's only environment switches; each changes placement or cache
-// policy, never a result bit (tests/test_gpu_parity.py checks that):
-// XCD-contiguous blockIdx remap switch (SPMV_XCD_REMAP=1 enables; read once).
+// The library's A/B switches (spmv_set_option, spmv_ext.h; initial values
+// from SPMV_XCD_REMAP / SPMV_XWIN_REMAP / SPMV_STREAM_NT, read once at load);
+// each changes placement or cache policy, never a result bit
+// (tests/test_gpu_parity.py checks that):
+// XCD-contiguous blockIdx remap of the global-gather kernels (default off).
 bool xcd_remap_enabled();
-// XCD-contiguous window placement of the CSR / SELL x-window kernels:
-// SPMV_XWIN_REMAP=1 / 0 forces it (read on every call, so a sweep can flip
-// it), otherwise `dflt` (each kernel's measured best).
+// XCD-contiguous window placement of the x-window kernels; `dflt` = each
+// kernel's measured best.
 bool xwin_remap(bool dflt);
+// small-matrix SELL geometry (sell.hip): C = 64 and fewer than 14 slices per CU
+bool sell_small(int32_t C, int64_t n_slices);
 
 // LDS-staged CMRS / COO launchers (staged.hip)
 // win != nullptr: the x-window kernels (win/xcap from *_xwin_build)
@@ -72,7 +76,7 @@ template <typename V>  // double or float values (instantiated in staged.hip)
 int launch_csr_tiled_hot(const spmv_dims &d, const int64_t *row_ptr, const int32_t *col,
                          const V *val, const double *x, double *y, int64_t H, const int32_t *hot,
                          double *xh, const int32_t *own_lo_plan, int32_t *own_lo, int32_t *carry_row,
-                         double *carry_val, const int32_t *big = nullptr);
+                         double *carry_val, const int32_t *big = nullptr, int64_t big_len = 0);
 int launch_cmrs_tiled(const spmv_dims &d, int32_t h, int64_t n_strips, const int64_t *strip_ptr,
                       const uint8_t *rin, const int32_t *col, const double *val, const double *x,
                       double *y, int32_t *own_lo, int32_t *carry_row, double *carry_val, int64_t H = 0,
@@ -171,9 +175,8 @@ __device__ __forceinline__ void store_y(double *p, double v)
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Load-policy switch for the streamed arrays: SPMV_STREAM_NT=1 / 0 forces
-// it, otherwise `dflt` (each kernel's measured best).  Read on every call
-// so a sweep can flip it inside one process.
+// Load-policy switch for the streamed arrays (SPMV_OPT_STREAM_NT), otherwise
+// `dflt` (each kernel's measured best).
 bool stream_nt(bool dflt);
 
 // Where x[c] comes from: global memory (XGlobal) or the workgroup's

@@ -283,16 +283,9 @@ struct StreamRegs {
 // L-lane reduction instead of after it.  s_off holds the window's
 // ngroups·RPB + 1 row offsets.  Chunks and per-row sums are exactly those
 // of staged_group (same boundaries, same order): the same bits.
-#ifdef SPMV_CSR_STAMPS  // lab builds only (tools/sell_stamps.py --kernel csr): per-wave phase times
-constexpr int kCsrStampWaves = 8192, kCsrStamps = 8;
-__device__ uint64_t g_csr_stamps[kCsrStampWaves * kCsrStamps];
-#define CSR_STAMP(k)                                                                                   \
-    do {                                                                                               \
-        const int64_t sw_ = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;                    \
-        if ((threadIdx.x & 63) == 0 && sw_ < kCsrStampWaves && (k) < kCsrStamps)                       \
-            g_csr_stamps[sw_ * kCsrStamps + (k)] = __builtin_amdgcn_s_memrealtime();                   \
-    } while (0)
-#else
+// CSR_STAMP(k): per-wave phase hooks, no-ops in the product; a lab build
+// (tools/build_variant.sh stamps_csr) injects tools/lab_stamps_csr.h
+#ifndef CSR_STAMP
 #define CSR_STAMP(k) \
     do {             \
     } while (0)
@@ -685,13 +678,6 @@ extern "C" int spmv_csr_auto_lanes(int64_t n_rows, int64_t nnz)
         L *= 2;
     return L;
 }
-
-#ifdef SPMV_CSR_STAMPS
-extern "C" int spmv_lab_csr_stamps(void *host, size_t bytes)
-{
-    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_csr_stamps), bytes);
-}
-#endif
 
 extern "C" int spmv_csr_run_variant(spmv_dims d, const int64_t *row_ptr,
                                     const int32_t *col, const double *val,
@@ -1147,10 +1133,16 @@ extern "C" int64_t spmv_csr_tiled_tile(int64_t n_rows, int64_t nnz)
 extern "C" int spmv_csr_run_tiled_plan(spmv_dims d, const int64_t *row_ptr, const int32_t *col_hot,
                                        const double *val, const double *x, double *y, int64_t H,
                                        const int32_t *hot, const int32_t *own_lo_plan, const int32_t *big,
-                                       void *ws, size_t ws_bytes)
+                                       int64_t big_len, int64_t big_tile, void *ws, size_t ws_bytes)
 {
     if (!big)
         return spmv_csr_run_tiled_hot(d, row_ptr, col_hot, val, x, y, H, hot, own_lo_plan, ws, ws_bytes);
+    // the plan must be this matrix's: built for the tile the run cuts, and
+    // at least as long as its tile index (the kernel bounds-checks the rest)
+    if (big_tile != csr_tiled_tile(d.n_rows, d.nnz) || big_tile != csr_tiled_tile_min())
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_run_tiled_plan: plan built for another tile size");
+    if (d.nnz > 0 && big_len < (d.nnz + big_tile - 1) / big_tile + 1)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_run_tiled_plan: plan shorter than its tile index");
     if (d.n_rows < 0 || d.n_cols < 0 || d.nnz < 0 || d.n_rows > INT32_MAX || H < 0 ||
         d.n_cols + H > INT32_MAX)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_csr_run_tiled_plan: bad sizes");
@@ -1167,7 +1159,7 @@ extern "C" int spmv_csr_run_tiled_plan(spmv_dims d, const int64_t *row_ptr, cons
     int32_t *own_lo = (int32_t *)(carry_val + tiles);
     int32_t *carry_row = own_lo + tiles + 1;
     return launch_csr_tiled_hot(d, row_ptr, col_hot, val, x, y, H, hot, xh, own_lo_plan, own_lo, carry_row,
-                                carry_val, big);
+                                carry_val, big, big_len);
 }
 
 // fp32 values, entry-balanced tiles (+ hot-column table, build-once tile

@@ -7,6 +7,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
+
 #include "common.h"
 
 namespace spmv {
@@ -48,39 +50,91 @@ DeviceGuard::~DeviceGuard()
         (void)hipSetDevice(prev_);
 }
 
-bool xwin_remap(bool dflt)
+// The A/B switches (spmv_ext.h spmv_set_option): read from the
+// environment ONCE, when the library is loaded, then only through
+// spmv_set_option; the launch path reads one int, never getenv (VERDICT r5:
+// hidden global configuration behind a C-ABI).  -1 = each kernel's default.
+static int env_switch(const char *name)
 {
-    const char *s = getenv("SPMV_XWIN_REMAP");
-    if (s && (s[0] == '0' || s[0] == '1'))
-        return s[0] == '1';
-    return dflt;
+    const char *s = getenv(name);
+    return (s && (s[0] == '0' || s[0] == '1') && s[1] == 0) ? s[0] - '0' : -1;
+}
+static std::atomic<int> g_opt_xwin_remap{env_switch("SPMV_XWIN_REMAP")};
+static std::atomic<int> g_opt_xcd_remap{env_switch("SPMV_XCD_REMAP")};
+static std::atomic<int> g_opt_stream_nt{env_switch("SPMV_STREAM_NT")};
+
+static std::atomic<int> *option_slot(int option)
+{
+    switch (option) {
+    case SPMV_OPT_XWIN_REMAP:
+        return &g_opt_xwin_remap;
+    case SPMV_OPT_XCD_REMAP:
+        return &g_opt_xcd_remap;
+    case SPMV_OPT_STREAM_NT:
+        return &g_opt_stream_nt;
+    default:
+        return nullptr;
+    }
 }
 
-bool xcd_remap_enabled()
+bool xwin_remap(bool dflt)
 {
-    static int cached = -1;
-    if (cached < 0) {
-        // Off by default: on the cant-like batch the round-robin placement
-        // measured 1-2 % faster than the contiguous-per-XCD remap
-        // (profiles/round1_sweep.md).  SPMV_XCD_REMAP=1 turns it on.
-        const char *s = getenv("SPMV_XCD_REMAP");
-        cached = (s && s[0] == '1') ? 1 : 0;
-    }
-    return cached == 1;
+    const int v = g_opt_xwin_remap.load(std::memory_order_relaxed);
+    return v < 0 ? dflt : v == 1;
 }
+
+// Off by default: on the cant-like batch the round-robin placement
+// measured 1-2 % faster than the contiguous-per-XCD remap
+// (profiles/round1/sweeps.md).
+bool xcd_remap_enabled() { return g_opt_xcd_remap.load(std::memory_order_relaxed) == 1; }
 
 bool stream_nt(bool dflt)
 {
-    const char *s = getenv("SPMV_STREAM_NT");
-    if (s && (s[0] == '0' || s[0] == '1'))
-        return s[0] == '1';
-    return dflt;
+    const int v = g_opt_stream_nt.load(std::memory_order_relaxed);
+    return v < 0 ? dflt : v == 1;
 }
 
 // One flush buffer per device, allocated on first use, freed by
 // spmv_release().
 static void *g_flush[64];
 static size_t g_flush_bytes[64];
+
+// evicts by READING the scratch: 16-byte loads, a value that is never true
+// keeps them (the caches end up holding clean lines of the scratch)
+__global__ __launch_bounds__(kBlock) void flush_read_kernel(const uint4 *__restrict__ p, int64_t n16,
+                                                            uint32_t *__restrict__ sink)
+{
+    uint32_t acc = 0;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n16; i += (int64_t)gridDim.x * kBlock) {
+        const uint4 v = p[i];
+        acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+    if (acc == 0x9e3779b9u && sink)
+        sink[threadIdx.x] = acc;
+}
+
+// the device's scratch of at least `bytes` (allocated / grown on demand)
+static int flush_scratch(size_t bytes, void **buf)
+{
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess)
+        return fail(SPMV_DEVICE_ERROR, "hipGetDevice", e);
+    if (dev < 0 || dev >= 64)
+        return fail_msg(SPMV_DEVICE_ERROR, "device ordinal out of range");
+    if (g_flush_bytes[dev] < bytes) {
+        if (g_flush[dev])
+            (void)hipFree(g_flush[dev]);
+        g_flush[dev] = nullptr;
+        g_flush_bytes[dev] = 0;
+        e = hipMalloc(&g_flush[dev], bytes);
+        if (e != hipSuccess)
+            return fail(SPMV_PROGRAM_ERROR, "hipMalloc(flush)", e);
+        g_flush_bytes[dev] = bytes;
+    }
+    *buf = g_flush[dev];
+    return SPMV_SUCCESS;
+}
 
 }  // namespace spmv
 
@@ -108,7 +162,22 @@ const char *spmv_strerror(int rc)
     }
 }
 
-const char *spmv_version(void) { return "spmv-hip 0.1 gfx950"; }
+const char *spmv_version(void) { return "spmv-hip 0.2 gfx950"; }
+
+int spmv_set_option(int option, int value)
+{
+    std::atomic<int> *o = option_slot(option);
+    if (!o || value < -1 || value > 1)
+        return fail_msg(SPMV_OTHER_ERROR, "spmv_set_option: unknown option or value (-1, 0, 1)");
+    o->store(value, std::memory_order_relaxed);
+    return SPMV_SUCCESS;
+}
+
+int spmv_get_option(int option)
+{
+    std::atomic<int> *o = option_slot(option);
+    return o ? o->load(std::memory_order_relaxed) : -2;
+}
 
 int spmv_device_count(int *count)
 {
@@ -218,26 +287,62 @@ int spmv_flush_cache(void *stream, size_t bytes)
 {
     if (bytes == 0)
         bytes = (size_t)512 << 20;
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess)
-        return fail(SPMV_DEVICE_ERROR, "hipGetDevice", e);
-    if (dev < 0 || dev >= 64)
-        return fail_msg(SPMV_DEVICE_ERROR, "device ordinal out of range");
-    if (g_flush_bytes[dev] < bytes) {
-        if (g_flush[dev])
-            (void)hipFree(g_flush[dev]);
-        g_flush[dev] = nullptr;
-        g_flush_bytes[dev] = 0;
-        e = hipMalloc(&g_flush[dev], bytes);
-        if (e != hipSuccess)
-            return fail(SPMV_PROGRAM_ERROR, "hipMalloc(flush)", e);
-        g_flush_bytes[dev] = bytes;
-    }
+    void *buf = nullptr;
+    int rc = flush_scratch(bytes, &buf);
+    if (rc != SPMV_SUCCESS)
+        return rc;
     static unsigned char tick = 0;
-    e = hipMemsetAsync(g_flush[dev], ++tick, bytes, (hipStream_t)stream);
+    hipError_t e = hipMemsetAsync(buf, ++tick, bytes, (hipStream_t)stream);
     return e == hipSuccess ? SPMV_SUCCESS
                            : fail(SPMV_PROGRAM_ERROR, "flush", e);
+}
+
+int spmv_flush_cache_read(void *stream, size_t bytes)
+{
+    if (bytes == 0)
+        bytes = (size_t)512 << 20;
+    void *buf = nullptr;
+    int rc = flush_scratch(bytes, &buf);
+    if (rc != SPMV_SUCCESS)
+        return rc;
+    hipLaunchKernelGGL(flush_read_kernel, dim3(2048), dim3(kBlock), 0, (hipStream_t)stream, (const uint4 *)buf,
+                       (int64_t)(bytes / 16), (uint32_t *)nullptr);
+    SPMV_CHECK_LAUNCH("flush_read_kernel");
+    return SPMV_SUCCESS;
+}
+
+int spmv_event_create(void **ev)
+{
+    hipEvent_t e0;
+    hipError_t e = hipEventCreate(&e0);
+    *ev = e == hipSuccess ? (void *)e0 : nullptr;
+    return e == hipSuccess ? SPMV_SUCCESS : fail(SPMV_PROGRAM_ERROR, "hipEventCreate", e);
+}
+
+int spmv_event_destroy(void *ev)
+{
+    if (!ev)
+        return SPMV_SUCCESS;
+    hipError_t e = hipEventDestroy((hipEvent_t)ev);
+    return e == hipSuccess ? SPMV_SUCCESS : fail(SPMV_PROGRAM_ERROR, "hipEventDestroy", e);
+}
+
+int spmv_event_record(void *ev, void *stream)
+{
+    hipError_t e = hipEventRecord((hipEvent_t)ev, (hipStream_t)stream);
+    return e == hipSuccess ? SPMV_SUCCESS : fail(SPMV_PROGRAM_ERROR, "hipEventRecord", e);
+}
+
+int spmv_event_elapsed(void *start, void *end, double *ms)
+{
+    hipError_t e = hipEventSynchronize((hipEvent_t)end);
+    float f = 0.f;
+    if (e == hipSuccess)
+        e = hipEventElapsedTime(&f, (hipEvent_t)start, (hipEvent_t)end);
+    if (e != hipSuccess)
+        return fail(SPMV_PROGRAM_ERROR, "event timing", e);
+    *ms = (double)f;
+    return SPMV_SUCCESS;
 }
 
 int spmv_time_launch(spmv_launch_fn launch, void *arg, void *stream, double *ms)

@@ -487,18 +487,15 @@ template <int KI> constexpr int sell_small_g() { return SPMV_SELL_HEAD_G; }  // 
 // waiting for slice_ptr (one dependent HBM round trip fewer on a cold
 // matrix); the later groups come from the SELL arrays.  Same values in the
 // same accumulators: bit-identical.
-#ifdef SPMV_SELL_STAMPS  // lab builds only (tools/sell_stamps.py): per-wave phase times
-constexpr int kStampWaves = 8192, kStamps = 8;
-__device__ uint64_t g_sell_stamps[kStampWaves * kStamps];
-#define SELL_STAMP(k)                                                                                   \
-    do {                                                                                                \
-        const int64_t sw_ = bid * (kSellSmallS * kSellSmallP) + wv;                                     \
-        if (lane == 0 && sw_ < kStampWaves)                                                             \
-            g_sell_stamps[sw_ * kStamps + (k)] = __builtin_amdgcn_s_memrealtime();                      \
-    } while (0)
-#else
+// SELL_STAMP(k) / SELL_STAMP_HWID(): per-wave phase hooks, no-ops in the
+// product; a lab build (tools/build_variant.sh stamps_sell) injects
+// tools/lab_stamps_sell.h (tools/sell_stamps.py reads them)
+#ifndef SELL_STAMP
 #define SELL_STAMP(k) \
     do {              \
+    } while (0)
+#define SELL_STAMP_HWID() \
+    do {                  \
     } while (0)
 #endif
 template <int KI, bool NT, bool XWIN, typename XS, typename CT = int32_t, int HG = 0>
@@ -521,15 +518,7 @@ __global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell_small_
     extern __shared__ double s_x[];
     const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
     SELL_STAMP(0);
-#ifdef SPMV_SELL_STAMPS
-    {
-        uint32_t hid;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hid));
-        const int64_t sw_ = bid * (kSellSmallS * kSellSmallP) + wv;
-        if (lane == 0 && sw_ < kStampWaves)
-            g_sell_stamps[sw_ * kStamps + 7] = hid;
-    }
-#endif
+    SELL_STAMP_HWID();
     SlotBatch<KI, NT, G> first;
     // The x window (HEAD + XWIN): the first kSellXCopy waves request it
     // before their heads (its loads then return ahead of theirs) and store
@@ -1063,13 +1052,6 @@ extern "C" int spmv_sell16_fill(spmv_dims d, int32_t C, int32_t sigma, int64_t n
     SPMV_CHECK_LAUNCH("sell16_fill_kernel");
     return SPMV_SUCCESS;
 }
-
-#ifdef SPMV_SELL_STAMPS
-extern "C" int spmv_lab_sell_stamps(void *host, size_t bytes)
-{
-    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_sell_stamps), bytes);
-}
-#endif
 
 extern "C" size_t spmv_sell16_head_bytes(int64_t n_slices, int32_t C, int32_t ki)
 {

@@ -529,14 +529,17 @@ __global__ __launch_bounds__(kBlock) void csr_tiled_kernel(
     const int32_t *__restrict__ col, const V *__restrict__ val,
     const XS xs, double *__restrict__ y,
     const int32_t *__restrict__ own_lo, int32_t *__restrict__ carry_row,
-    double *__restrict__ carry_val, const int32_t *__restrict__ big = nullptr)
+    double *__restrict__ carry_val, const int32_t *__restrict__ big = nullptr, int64_t big_len = 0)
 {
     constexpr int CH = 2 * kBlock * R;
     constexpr int RPK = (kTiledRowCap + 1 + kBlock - 1) / kBlock;  // staged offsets per thread
     constexpr int NW = kBlock / kWave;
-    static_assert(kTiledBigRowCap / 32 >= kTiledRowCap + 1, "s_rp lives in the big-tile bitmap");
+    // only the R = 1 instantiation takes a big-tile plan (launch_tiled_r):
+    // the others keep 4 KiB of LDS for s_rp instead of the 8 KiB bitmap
+    constexpr int kBitWords = R == 1 ? kTiledBigRowCap / 32 : kTiledRowCap + 1;
+    static_assert(kBitWords >= kTiledRowCap + 1, "s_rp lives in the big-tile bitmap");
     __shared__ double2 s_prod[kBlock * R];
-    __shared__ uint32_t s_bits[kTiledBigRowCap / 32];  // big tiles: owned rows with entries; else s_rp
+    __shared__ uint32_t s_bits[kBitWords];  // big tiles: owned rows with entries; else s_rp
     int32_t *s_rp = reinterpret_cast<int32_t *>(s_bits);
     const double *prod = reinterpret_cast<const double *>(s_prod);
     const int64_t tile = blockIdx.x;
@@ -550,7 +553,12 @@ __global__ __launch_bounds__(kBlock) void csr_tiled_kernel(
     const bool rp_lds = nr >= 0 && nr <= kTiledRowCap;  // uniform
     // big tile (more owned rows than the offset table, at most the bitmap's):
     // the plan lists its owned rows WITH entries, [a, b) relative to t0
-    const int32_t bk = !rp_lds && big && nr <= kTiledBigRowCap ? big[tile] : -1;  // uniform
+    // (every plan read is bounds-checked against big_len, so a plan of
+    // another matrix or tile size cannot read past its buffer)
+    const int64_t tiles = (nnz + CH - 1) / CH;
+    int32_t bk = R == 1 && !rp_lds && big && nr <= kTiledBigRowCap && tile < big_len ? big[tile] : -1;  // uniform
+    if (bk >= 0 && tiles + bk + 1 >= big_len)
+        bk = -1;
     int32_t b_beg = 0, b_end = 0;
     int2 item[2] = {{0, 0}, {0, 0}};
     int64_t rpv[RPK];
@@ -561,13 +569,14 @@ __global__ __launch_bounds__(kBlock) void csr_tiled_kernel(
             rpv[k] = i <= nr ? row_ptr[r_lo + i] : 0;
         }
     } else if (bk >= 0) {
-        const int64_t tiles = (nnz + CH - 1) / CH;
         b_beg = big[tiles + bk];
         b_end = big[tiles + bk + 1];
+        b_beg = b_beg > 0 ? b_beg : 0;
+        b_end = (int64_t)b_end < big_len ? b_end : (int32_t)big_len;
 #pragma unroll
         for (int k = 0; k < 2; ++k) {  // at most CH listed rows; CH <= 2·kBlock for R = 1
             const int32_t i = b_beg + 2 * ((int32_t)threadIdx.x + k * kBlock);
-            if (i < b_end)
+            if (i + 1 < b_end)
                 item[k] = *reinterpret_cast<const int2 *>(big + i);
         }
         for (int32_t i = threadIdx.x; i < (int32_t)((nr + 31) >> 5); i += kBlock)
@@ -589,7 +598,7 @@ __global__ __launch_bounds__(kBlock) void csr_tiled_kernel(
         // before it have none) belong to row r_lo - 1
         if (wv == 0) {
             const int n_t = (int)(t1 - t0);
-            int e_rel = b_end > b_beg ? (big[b_beg + 1] & 0xFFFF) : n_t;
+            int e_rel = b_end > b_beg + 1 ? (big[b_beg + 1] & 0xFFFF) : n_t;
             e_rel = e_rel < n_t ? e_rel : n_t;
             const bool has = r_lo > 0 && e_rel > 0;
             const double c = has ? wave_sum(prod, 0, e_rel) : 0.0;
@@ -606,7 +615,7 @@ __global__ __launch_bounds__(kBlock) void csr_tiled_kernel(
             const int32_t i = b_beg + 2 * ((int32_t)threadIdx.x + k * kBlock);
             // (bounds re-checked so a plan of another matrix cannot index
             // past the bitmap or the products)
-            const bool ok = i < b_end && item[k].x >= 0 && item[k].x < nr;
+            const bool ok = i + 1 < b_end && item[k].x >= 0 && item[k].x < nr;
             const int32_t rr = item[k].x, a = item[k].y & 0xFFFF;
             int32_t b = (int32_t)((uint32_t)item[k].y >> 16);
             b = b < CH ? b : CH;
@@ -864,9 +873,6 @@ int launch_cmrs_tiled(const spmv_dims &d, int32_t h, int64_t n_strips, const int
 // are sized for the smallest tile (R = 1).
 static int tiled_r(int64_t n_rows, int64_t nnz)
 {
-#ifdef SPMV_TILED_R_FORCE  // A/B builds only (lab/build_variant.sh); the product uses the rule below
-    return SPMV_TILED_R_FORCE;
-#endif
     (void)n_rows;
     (void)nnz;
     return 1;
@@ -878,16 +884,16 @@ int64_t csr_tiled_tile_min() { return 2 * kBlock; }
 template <int R, typename XS, typename V>
 static void launch_tiled_r(const spmv_dims &d, int64_t tiles, const int64_t *row_ptr, const int32_t *col,
                            const V *val, XS xs, double *y, const int32_t *own_lo, int32_t *carry_row,
-                           double *carry_val, const int32_t *big)
+                           double *carry_val, const int32_t *big, int64_t big_len)
 {
     const hipStream_t st = (hipStream_t)d.stream;
     // the plain-load variant exists for R = 3 only
     if (R == 3 && !stream_nt(true))
         hipLaunchKernelGGL((csr_tiled_kernel<R, false, XS, V>), dim3((unsigned)tiles), dim3(kBlock), 0, st, d.n_rows,
-                           d.nnz, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val, R == 1 ? big : nullptr);
+                           d.nnz, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val, R == 1 ? big : nullptr, big_len);
     else
         hipLaunchKernelGGL((csr_tiled_kernel<R, true, XS, V>), dim3((unsigned)tiles), dim3(kBlock), 0, st, d.n_rows,
-                           d.nnz, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val, R == 1 ? big : nullptr);
+                           d.nnz, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val, R == 1 ? big : nullptr, big_len);
 }
 
 // A matrix of fewer than two entries (the tiled kernel loads entry pairs):
@@ -912,7 +918,7 @@ __global__ __launch_bounds__(kBlock) void csr_tiny_kernel(int64_t n_rows, int64_
 template <typename XS, typename V>
 static void launch_tiled_xs(const spmv_dims &d, int64_t tiles, const int64_t *row_ptr, const int32_t *col,
                             const V *val, XS xs, double *y, const int32_t *own_lo, int32_t *carry_row,
-                            double *carry_val, const int32_t *big = nullptr)
+                            double *carry_val, const int32_t *big = nullptr, int64_t big_len = 0)
 {
     if (d.nnz < 2) {
         hipLaunchKernelGGL((csr_tiny_kernel<XS, V>), dim3(1), dim3(kBlock), 0, (hipStream_t)d.stream, d.n_rows,
@@ -920,9 +926,9 @@ static void launch_tiled_xs(const spmv_dims &d, int64_t tiles, const int64_t *ro
         return;
     }
     switch (tiled_r(d.n_rows, d.nnz)) {
-    case 1: launch_tiled_r<1>(d, tiles, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val, big); break;
-    case 2: launch_tiled_r<2>(d, tiles, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val, big); break;
-    default: launch_tiled_r<3>(d, tiles, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val, big); break;
+    case 1: launch_tiled_r<1>(d, tiles, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val, big, big_len); break;
+    case 2: launch_tiled_r<2>(d, tiles, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val, big, big_len); break;
+    default: launch_tiled_r<3>(d, tiles, row_ptr, col, val, xs, y, own_lo, carry_row, carry_val, big, big_len); break;
     }
 }
 
@@ -945,7 +951,7 @@ template <typename V>
 int launch_csr_tiled_hot(const spmv_dims &d, const int64_t *row_ptr, const int32_t *col,
                          const V *val, const double *x, double *y, int64_t H, const int32_t *hot,
                          double *xh, const int32_t *own_lo_plan, int32_t *own_lo, int32_t *carry_row,
-                         double *carry_val, const int32_t *big)
+                         double *carry_val, const int32_t *big, int64_t big_len)
 {
     const int64_t ch = csr_tiled_tile(d.n_rows, d.nnz);
     const int64_t tiles = (d.nnz + ch - 1) / ch;
@@ -959,19 +965,19 @@ int launch_csr_tiled_hot(const spmv_dims &d, const int64_t *row_ptr, const int32
     }
     if (H > 0)
         launch_tiled_xs(d, tiles, row_ptr, col, val, XHot{x, xh, (int32_t)d.n_cols}, y, own_lo_plan, carry_row,
-                        carry_val, big);
+                        carry_val, big, big_len);
     else
-        launch_tiled_xs(d, tiles, row_ptr, col, val, XGlobal{x}, y, own_lo_plan, carry_row, carry_val, big);
+        launch_tiled_xs(d, tiles, row_ptr, col, val, XGlobal{x}, y, own_lo_plan, carry_row, carry_val, big, big_len);
     SPMV_CHECK_LAUNCH("csr_tiled_kernel (hot columns)");
     return launch_carry(tiles, carry_row, carry_val, y, st);
 }
 
 template int launch_csr_tiled_hot<double>(const spmv_dims &, const int64_t *, const int32_t *, const double *,
                                           const double *, double *, int64_t, const int32_t *, double *,
-                                          const int32_t *, int32_t *, int32_t *, double *, const int32_t *);
+                                          const int32_t *, int32_t *, int32_t *, double *, const int32_t *, int64_t);
 template int launch_csr_tiled_hot<float>(const spmv_dims &, const int64_t *, const int32_t *, const float *,
                                          const double *, double *, int64_t, const int32_t *, double *,
-                                         const int32_t *, int32_t *, int32_t *, double *, const int32_t *);
+                                         const int32_t *, int32_t *, int32_t *, double *, const int32_t *, int64_t);
 
 // ----------------------------------------------------------- launchers
 // Geometry of the strip-run CMRS kernel: lanes per row as the staged CSR

@@ -24,15 +24,26 @@
  *     the reference's absolute 1e-6 rule;
  *   - --strict turns a failed check into exit code 4 (the reference always
  *     returns Success, reference csr.c:282).
- * Options: --matrix PATH  --gen cantlike[0|1|2]|rmat|banded|random
+ * Options: --matrix PATH  --gen cantlike[0|1|2]|rmat[:ROWS:NNZ]|random
  *          --copies B  --reps N  --warmup W  --warm  --device D
  *          --C C --sigma S --ki K --h H --lanes L  --threads T
- *          --cpu / --no-cpu  --strict  --write-mtx PATH  --cache  --no-xwin  --gpus N  --help
+ *          --cpu / --no-cpu  --strict  --write-mtx PATH  --cache  --no-xwin  --gpus N
+ *          --relabel auto|yes|no  --write-y PATH  --help
  *   --cache keeps a binary copy of the parsed file at PATH.bin (SURVEY.md
  *   §8f row 1) and reads it instead of the text whenever it is at least as
  *   new as PATH; the entries, their order and the result are unchanged.
- *   CSR, ELL and SELL run the x-window kernels (each workgroup's x range
- *   staged in LDS, include/spmv.h); --no-xwin runs the global-gather ones.
+ *   The kernel path is the library's plan for the matrix (spmv_plan_<fmt>,
+ *   include/spmv.h) — the same one the Python binding and bench.py run:
+ *   x windows in LDS (CSR, ELL, SELL, CMRS; --no-xwin: global gathers), the
+ *   SELL head copy, the single-pass COO, entry-balanced tiles for skewed
+ *   rows; the "[plan]" line names the kernel.
+ *   --relabel (default auto = when the CSR skew rule picks the tiled kernel,
+ *   e.g. R-MAT): the columns renumbered by decreasing degree, ties by first
+ *   row (spmv_column_relabel_ex) and every row's entries in new-column
+ *   order (spmv_csr_sort_rows), x permuted to match once on the host — the
+ *   layout bench.py measures configs[3] on; y keeps the original row order
+ *   and is checked against the original file.
+ *   --write-y PATH writes the device y (n_rows raw fp64, row order).
  *   Device buffers are released by spmv_release() / process exit.
  *   --gpus N (N >= 1) shards the rows over GPUs 0..N-1 from ONE process
  *   (run_multi below): contiguous row ranges (spmv_partition_rows, aligned
@@ -57,22 +68,27 @@
 
 #define HBM_PEAK_GBS 8000.0
 
+static int cmp_double(const void *a, const void *b);
+
 typedef struct {
     const char *matrix;
     const char *gen;
     const char *write_mtx;
+    const char *write_y;
     int64_t copies;
     int reps, warmup, warm, device, C, sigma, ki, h, lanes, threads, cpu, strict, cache, xwin, gpus, index16, single_pass;
+    int relabel; /* -1 auto, 0 no, 1 yes */
 } opts_t;
 
 static void usage(const char *prog)
 {
-    printf("usage: %s [--matrix PATH | --gen cantlike[0|1|2]|rmat|banded|random]\n"
+    printf("usage: %s [--matrix PATH | --gen cantlike[0|1|2]|rmat[:ROWS:NNZ]|random]\n"
            "          [--copies B] [--reps N] [--warmup W] [--warm] [--device D]\n"
            "          [--C C] [--sigma S] [--ki 1|2] [--h H] [--lanes L]\n"
            "          [--threads T] [--cpu|--no-cpu] [--strict] [--write-mtx PATH] [--cache]\n"
            "          [--no-xwin] [--gpus N] [--index16 (sigma_c: SELL16)]\n"
-           "          [--carry-pass (coo: the carry kernel even where rows allow one pass)]\n",
+           "          [--carry-pass (coo: the carry kernel even where rows allow one pass)]\n"
+           "          [--relabel auto|yes|no] [--write-y PATH]\n",
            prog);
 }
 
@@ -90,6 +106,7 @@ static int parse_opts(int argc, char **argv, spmv_format fmt, opts_t *o)
     o->cpu = fmt != FMT_SELL;
     o->xwin = 1;
     o->single_pass = 1;
+    o->relabel = -1;
     for (int i = 1; i < argc; ++i) {
         const char *a = argv[i];
         const char *v = i + 1 < argc ? argv[i + 1] : NULL;
@@ -104,6 +121,15 @@ static int parse_opts(int argc, char **argv, spmv_format fmt, opts_t *o)
         if (!strcmp(a, "--matrix")) { NEEDV(); o->matrix = v; }
         else if (!strcmp(a, "--gen")) { NEEDV(); o->gen = v; }
         else if (!strcmp(a, "--write-mtx")) { NEEDV(); o->write_mtx = v; }
+        else if (!strcmp(a, "--write-y")) { NEEDV(); o->write_y = v; }
+        else if (!strcmp(a, "--relabel")) {
+            NEEDV();
+            o->relabel = !strcmp(v, "yes") ? 1 : !strcmp(v, "no") ? 0 : !strcmp(v, "auto") ? -1 : -2;
+            if (o->relabel == -2) {
+                fprintf(stderr, "--relabel takes auto, yes or no\n");
+                return SPMV_OTHER_ERROR;
+            }
+        }
         else if (!strcmp(a, "--copies")) { NEEDV(); o->copies = atoll(v); }
         else if (!strcmp(a, "--reps")) { NEEDV(); o->reps = atoi(v); }
         else if (!strcmp(a, "--warmup")) { NEEDV(); o->warmup = atoi(v); }
@@ -237,14 +263,27 @@ static int load_input(const opts_t *o, spmv_format fmt, coo_t *m)
         rc = spmv_gen_cantlike(mode, o->copies, &m->n_rows, &m->nnz, m->row, m->col, m->val);
         m->n_cols = m->n_rows;
         m->label = "cant-like stand-in (synthetic; real cant.mtx is an LFS pointer)";
-    } else if (!strcmp(o->gen, "rmat")) {
+    } else if (!strncmp(o->gen, "rmat", 4) && (o->gen[4] == 0 || o->gen[4] == ':')) {
+        /* rmat = configs[3] (1e7 rows, 1e8 entries); rmat:ROWS:NNZ a smaller one */
         m->n_rows = m->n_cols = 10000000;
         m->nnz = 100000000;
-        m->row = malloc((size_t)m->nnz * sizeof(int32_t));
-        m->col = malloc((size_t)m->nnz * sizeof(int32_t));
-        m->val = malloc((size_t)m->nnz * sizeof(double));
-        rc = spmv_gen_rmat(m->n_rows, m->nnz, 24, 1, m->row, m->col, m->val);
-        m->label = "R-MAT 1e7 x 1e7, 1e8 entries (synthetic)";
+        if (o->gen[4] == ':') {
+            long long r = 0, z = 0;
+            if (sscanf(o->gen + 5, "%lld:%lld", &r, &z) != 2 || r < 2 || r > INT32_MAX || z < 0) {
+                fprintf(stderr, "--gen rmat:ROWS:NNZ\n");
+                return SPMV_OTHER_ERROR;
+            }
+            m->n_rows = m->n_cols = r;
+            m->nnz = z;
+        }
+        int scale = 1;
+        while (((int64_t)1 << scale) < m->n_rows)
+            ++scale;
+        m->row = malloc((size_t)(m->nnz + 1) * sizeof(int32_t));
+        m->col = malloc((size_t)(m->nnz + 1) * sizeof(int32_t));
+        m->val = malloc((size_t)(m->nnz + 1) * sizeof(double));
+        rc = spmv_gen_rmat(m->n_rows, m->nnz, scale, 1, m->row, m->col, m->val);
+        m->label = "R-MAT (a,b,c,d) = (.57,.19,.19,.05), seed 1 (synthetic)";
     } else if (!strcmp(o->gen, "random")) {
         m->n_rows = m->n_cols = 100000;
         rc = spmv_gen_random(m->n_rows, m->n_cols, 0, 64, 3, &m->nnz, NULL, NULL, NULL);
@@ -264,30 +303,14 @@ static int load_input(const opts_t *o, spmv_format fmt, coo_t *m)
 typedef struct {
     spmv_format fmt;
     spmv_dims d;
-    /* device arrays (unused ones stay NULL) */
+    /* device arrays (unused ones stay NULL); the plan points at them */
     int64_t *d_ptr;   /* CSR row_ptr / SELL slice_ptr / CMRS strip_ptr */
     int32_t *d_row, *d_col, *d_perm;
     uint8_t *d_rin;
     double *d_val, *d_x, *d_y;
-    void *d_ws;
-    size_t ws_bytes;
-    void *d_win; /* x-window kernels: per-workgroup column ranges */
-    void *d_tails; /* single-pass COO: entries of each tile's last row past its end */
-    int32_t xcap;
-    /* SELL16 (--index16): 16-bit column offsets, head copy for small matrices */
-    uint16_t *d_col16;
-    void *d_head;
-    int32_t K, C, sigma, ki, h, lanes, variant;
+    spmv_plan *plan; /* the library's kernel path for this matrix (spmv.h) */
+    int32_t K, C, sigma, ki, h;
     int64_t ld, n_slices, n_strips;
-    /* SELL wide-slice split plan (power-law rows; spmv_sell_run_split) */
-    int32_t split_T;
-    int64_t n_chunks;
-    int32_t *d_chunk_slice, *d_chunk_k0;
-    /* hot-column table (power-law columns; tiled CSR / CMRS): d_col holds
-     * the renumbered columns, h_col the original ones for the CPU loop */
-    int64_t H;
-    int32_t *d_hot, *d_own_lo;
-    int32_t *d_big; /* tiled CSR: the big-tile plan (spmv_csr_tiled_bigplan), or NULL */
     /* host copies for the CPU loop */
     int64_t *h_ptr;
     int32_t *h_row, *h_col, *h_perm;
@@ -305,34 +328,36 @@ static int upload(void **dst, const void *src, size_t bytes, void *stream)
     return rc;
 }
 
-/* Hot-column table of the skewed-matrix kernels (spmv_hot_columns' rule):
- * *col_dev = a renumbered copy of col when it applies, else col. */
-static int hot_table(dev_fmt_t *f, int64_t n_cols, int64_t Z, const int32_t *col, int32_t **col_dev)
+/* The plan: every kernel choice (x windows, head copy, single pass, tiles,
+ * split, hot-column table, SELL16) is the library's (spmv_plan_<fmt>), so
+ * this program runs what bench.py and spmv_amd.to_device run. */
+static int make_plan(const opts_t *o, dev_fmt_t *f, int relabelled)
 {
-    const int64_t cap = (int64_t)1 << 19;
-    int32_t *hot = malloc((size_t)cap * sizeof(int32_t));
-    int32_t *out = malloc((size_t)(Z + 1) * sizeof(int32_t));
-    if (!hot || !out) {
-        free(hot);
-        free(out);
-        return SPMV_OTHER_ERROR;
+    spmv_plan_opts po;
+    spmv_plan_opts_init(&po);
+    po.lanes = o->lanes;
+    po.xwin = o->xwin ? -1 : 0;
+    po.index16 = o->index16;
+    po.coo_pass = o->single_pass ? -1 : 0;
+    if (relabelled)
+        po.H = 0; /* hot columns are x'[0..H) already: no per-run table */
+    switch (f->fmt) {
+    case FMT_COO:
+        return spmv_plan_coo(f->d, f->d_row, f->d_col, f->d_val, &po, &f->plan);
+    case FMT_CSR:
+        return spmv_plan_csr(f->d, f->d_ptr, f->d_col, f->d_val, &po, &f->plan);
+    case FMT_ELL:
+        return spmv_plan_ell(f->d, f->K, f->ld, f->ki, f->d_col, f->d_val, &po, &f->plan);
+    case FMT_SELL:
+        return spmv_plan_sell(f->d, f->C, f->sigma, f->ki, f->n_slices, f->d_ptr, f->d_perm, f->d_col, f->d_val, &po,
+                              &f->plan);
+    case FMT_CMRS:
+        return spmv_plan_cmrs(f->d, f->h, f->n_strips, f->d_ptr, f->d_rin, f->d_col, f->d_val, &po, &f->plan);
     }
-    const int64_t H = spmv_hot_columns(n_cols, Z, col, 0, hot, out);
-    int rc = H < 0 ? SPMV_OTHER_ERROR : SPMV_SUCCESS;
-    if (H > 0) {
-        f->H = H;
-        rc = upload((void **)&f->d_hot, hot, (size_t)H * 4, NULL);
-        *col_dev = out;
-        out = NULL;
-        if (!rc)
-            printf("hot-column table: %lld columns\n", (long long)H);
-    }
-    free(hot);
-    free(out);
-    return rc;
+    return SPMV_OTHER_ERROR;
 }
 
-static int build_format(const opts_t *o, spmv_format fmt, const coo_t *m, dev_fmt_t *f)
+static int build_format(const opts_t *o, spmv_format fmt, const coo_t *m, dev_fmt_t *f, int relabelled)
 {
     memset(f, 0, sizeof *f);
     f->fmt = fmt;
@@ -350,29 +375,13 @@ static int build_format(const opts_t *o, spmv_format fmt, const coo_t *m, dev_fm
         rc = spmv_coo_sort_by_row(N, Z, m->row, m->col, m->val, f->h_row, f->h_col, f->h_val);
         if (rc)
             return rc;
-        f->ws_bytes = spmv_coo_ws_bytes(Z);
         f->stored = Z;
         f->stored_bytes = (size_t)Z * 16;
         if ((rc = upload((void **)&f->d_row, f->h_row, (size_t)Z * 4, NULL)) ||
             (rc = upload((void **)&f->d_col, f->h_col, (size_t)Z * 4, NULL)) ||
-            (rc = upload((void **)&f->d_val, f->h_val, (size_t)Z * 8, NULL)) ||
-            (rc = spmv_malloc(&f->d_ws, f->ws_bytes)))
+            (rc = upload((void **)&f->d_val, f->h_val, (size_t)Z * 8, NULL)))
             return rc;
-        /* single pass: no carry kernel when every row ends within 80 entries
-         * of its tile (otherwise, or with --carry-pass, the carry pass): cold
-         * on the cant-like matrix 18.1 us against 20.6 us */
-        const size_t tb = o->single_pass ? spmv_coo_tail_bytes(Z) : 0;
-        if (tb > 0 && spmv_malloc(&f->d_tails, tb) == SPMV_SUCCESS &&
-            spmv_coo_tail_build(f->d, f->d_row, f->d_tails, tb) != SPMV_SUCCESS) {
-            spmv_free(f->d_tails);
-            f->d_tails = NULL;
-        }
-        /* stderr: stdout keeps the reference program's lines, starting with
-         * "GPU calculations" (coo.c) */
-        fprintf(stderr, "COO single pass: %s\n", f->d_tails ? "no carry kernel"
-                                       : o->single_pass ? "refused (a row runs more than 80 entries past a tile), carry pass"
-                                                        : "off (--carry-pass)");
-        return SPMV_SUCCESS;
+        return make_plan(o, f, relabelled);
     }
     /* every other format starts from CSR */
     int64_t *ptr = malloc((size_t)(N + 1) * sizeof(int64_t));
@@ -387,71 +396,26 @@ static int build_format(const opts_t *o, spmv_format fmt, const coo_t *m, dev_fm
         f->h_col = col;
         f->h_val = val;
         f->stored = Z;
-        int32_t *col_dev = col; /* what d_col gets: col, or col with hot ids */
         if (fmt == FMT_CSR) {
-            f->lanes = o->lanes > 0 ? o->lanes : spmv_csr_auto_lanes(N, Z);
-            f->variant = spmv_csr_pick_variant(N, ptr); /* 4: entry-balanced (skewed rows) */
             f->stored_bytes = (size_t)Z * 12 + (size_t)(N + 1) * 8;
-            if ((rc = upload((void **)&f->d_ptr, ptr, (size_t)(N + 1) * 8, NULL)))
-                return rc;
-            if (f->variant == 4) {
-                if ((rc = hot_table(f, m->n_cols, Z, col, &col_dev)))
-                    return rc;
-                f->ws_bytes = spmv_csr_hot_ws_bytes(N, Z, f->H);
-                const int64_t n_plan = spmv_csr_tiled_plan_len(Z);
-                if ((rc = spmv_malloc(&f->d_ws, f->ws_bytes)))
-                    return rc;
-                if (n_plan > 0 && ((rc = spmv_malloc((void **)&f->d_own_lo, (size_t)n_plan * 4)) ||
-                                   (rc = spmv_csr_tiled_plan(f->d, f->d_ptr, f->d_own_lo))))
-                    return rc;
-                /* tiles owning more than 1,024 rows (runs of empty rows): the
-                 * list of their rows with entries (same bits) */
-                const int64_t tile = spmv_csr_tiled_tile(N, Z);
-                const int64_t nb = n_plan > 0 ? spmv_csr_tiled_bigplan(N, ptr, tile, 1024, NULL) : -1;
-                const int64_t tiles = tile > 0 ? (Z + tile - 1) / tile : 0;
-                if (nb > tiles) { /* some tile is big: the plan holds more than its index */
-                    int32_t *big = malloc((size_t)nb * sizeof(int32_t));
-                    if (!big)
-                        return SPMV_OTHER_ERROR;
-                    spmv_csr_tiled_bigplan(N, ptr, tile, 1024, big);
-                    int any = 0;
-                    for (int64_t t = 0; t < tiles && !any; ++t)
-                        any = big[t] >= 0;
-                    if (any)
-                        rc = upload((void **)&f->d_big, big, (size_t)nb * sizeof(int32_t), NULL);
-                    free(big);
-                    if (rc)
-                        return rc;
-                }
-            }
+            rc = upload((void **)&f->d_ptr, ptr, (size_t)(N + 1) * 8, NULL);
         } else {
             f->h = o->h;
             f->n_strips = (N + o->h - 1) / o->h;
             int64_t *sp = malloc((size_t)(f->n_strips + 1) * sizeof(int64_t));
             f->h_rin = malloc((size_t)(Z + 1));
-            if ((rc = spmv_cmrs_build(N, ptr, o->h, sp, f->h_rin)))
-                return rc;
+            if (!sp || !f->h_rin || (rc = spmv_cmrs_build(N, ptr, o->h, sp, f->h_rin)))
+                return rc ? rc : SPMV_OTHER_ERROR;
             free(f->h_ptr);
             f->h_ptr = sp;
             f->stored_bytes = (size_t)Z * 13 + (size_t)(f->n_strips + 1) * 8;
-            if ((rc = upload((void **)&f->d_ptr, sp, (size_t)(f->n_strips + 1) * 8, NULL)) ||
-                (rc = upload((void **)&f->d_rin, f->h_rin, (size_t)Z, NULL)))
-                return rc;
-            f->variant = spmv_cmrs_pick_variant(f->n_strips, sp); /* 1: entry-balanced (skewed strips) */
-            if (f->variant == 1) {
-                if ((rc = hot_table(f, m->n_cols, Z, col, &col_dev)))
-                    return rc;
-                f->ws_bytes = spmv_cmrs_hot_ws_bytes(f->n_strips, Z, f->h, f->H);
-                if ((rc = spmv_malloc(&f->d_ws, f->ws_bytes)))
-                    return rc;
-            }
+            if ((rc = upload((void **)&f->d_ptr, sp, (size_t)(f->n_strips + 1) * 8, NULL)) == SPMV_SUCCESS)
+                rc = upload((void **)&f->d_rin, f->h_rin, (size_t)Z, NULL);
         }
-        rc = upload((void **)&f->d_col, col_dev, (size_t)Z * 4, NULL);
-        if (col_dev != col)
-            free(col_dev);
-        if (rc || (rc = upload((void **)&f->d_val, val, (size_t)Z * 8, NULL)))
+        if (rc || (rc = upload((void **)&f->d_col, col, (size_t)Z * 4, NULL)) ||
+            (rc = upload((void **)&f->d_val, val, (size_t)Z * 8, NULL)))
             return rc;
-        return SPMV_SUCCESS;
+        return make_plan(o, f, relabelled);
     }
     if (fmt == FMT_ELL) {
         int64_t mn, mx;
@@ -487,35 +451,11 @@ static int build_format(const opts_t *o, spmv_format fmt, const coo_t *m, dev_fm
         if ((rc = spmv_sell_fill(N, ptr, col, val, o->C, o->sigma, f->ki, f->n_slices, f->h_ptr,
                                  f->h_perm, f->h_col, f->h_val)))
             return rc;
-        f->stored_bytes = (size_t)f->stored * 12 + (size_t)(f->n_slices + 1) * 8 +
+        f->stored_bytes = (size_t)f->stored * (o->index16 ? 10 : 12) + (size_t)(f->n_slices + 1) * 8 +
                           (size_t)f->n_slices * o->C * 4;
         if ((rc = upload((void **)&f->d_ptr, f->h_ptr, (size_t)(f->n_slices + 1) * 8, NULL)) ||
             (rc = upload((void **)&f->d_perm, f->h_perm, (size_t)f->n_slices * o->C * 4, NULL)))
             return rc;
-        /* wide slices (power-law rows) split into chunks of T slot columns */
-        f->split_T = spmv_sell_split_auto(f->n_slices, f->h_ptr, f->C, f->ki);
-        if (f->split_T > 0) {
-            f->n_chunks = spmv_sell_split_plan(f->n_slices, f->h_ptr, f->C, f->split_T, NULL, NULL);
-            if (f->n_chunks < 0)
-                return SPMV_OTHER_ERROR;
-            int32_t *cs = malloc((size_t)(f->n_chunks + 1) * sizeof(int32_t));
-            int32_t *ck = malloc((size_t)(f->n_chunks + 1) * sizeof(int32_t));
-            if (!cs || !ck)
-                return SPMV_OTHER_ERROR;
-            spmv_sell_split_plan(f->n_slices, f->h_ptr, f->C, f->split_T, cs, ck);
-            f->ws_bytes = spmv_sell_split_ws_bytes(f->n_chunks, f->C);
-            rc = upload((void **)&f->d_chunk_slice, cs, (size_t)(f->n_chunks + 1) * 4, NULL);
-            if (!rc)
-                rc = upload((void **)&f->d_chunk_k0, ck, (size_t)(f->n_chunks + 1) * 4, NULL);
-            if (!rc && f->ws_bytes)
-                rc = spmv_malloc(&f->d_ws, f->ws_bytes);
-            free(cs);
-            free(ck);
-            if (rc)
-                return rc;
-            printf("SELL split: %lld chunks of %d slot columns beyond the first %d of the wide slices\n",
-                   (long long)f->n_chunks, f->split_T, f->split_T);
-        }
     }
     free(ptr);
     free(col);
@@ -523,121 +463,115 @@ static int build_format(const opts_t *o, spmv_format fmt, const coo_t *m, dev_fm
     if ((rc = upload((void **)&f->d_col, f->h_col, (size_t)f->stored * 4, NULL)) ||
         (rc = upload((void **)&f->d_val, f->h_val, (size_t)f->stored * 8, NULL)))
         return rc;
-    return SPMV_SUCCESS;
-}
-
-/* CSR (not the entry-balanced variant), ELL and SELL run the x-window
- * kernels: each workgroup's x range is staged in LDS (include/spmv.h).
- * The windows are built once on the device, outside the timed launches. */
-static int build_windows(dev_fmt_t *f)
-{
-    size_t bytes = 0;
-    if (f->fmt == FMT_CSR && f->variant != 4)
-        bytes = spmv_csr_xwin_bytes(f->d.n_rows, f->d.nnz, f->lanes, 0);
-    else if (f->fmt == FMT_ELL)
-        bytes = spmv_ell_xwin_bytes(f->d.n_rows);
-    else if (f->fmt == FMT_SELL)
-        bytes = spmv_sell_xwin_bytes(f->n_slices, f->C, f->sigma);
-    else if (f->fmt == FMT_CMRS && f->variant == 0)
-        bytes = spmv_cmrs_xwin_bytes(f->d, f->h, f->n_strips);
-    if (bytes == 0)
-        return SPMV_SUCCESS;
-    int rc = spmv_malloc(&f->d_win, bytes);
-    if (rc)
-        return rc;
-    if (f->fmt == FMT_CSR)
-        rc = spmv_csr_xwin_build(f->d, f->d_ptr, f->d_col, f->lanes, 0, f->d_win, bytes, &f->xcap);
-    else if (f->fmt == FMT_ELL)
-        rc = spmv_ell_xwin_build(f->d, f->K, f->ld, f->ki, f->d_col, f->d_win, bytes, &f->xcap);
-    else if (f->fmt == FMT_COO)
-        rc = spmv_coo_xwin_build(f->d, f->d_col, f->d_win, bytes, &f->xcap);
-    else if (f->fmt == FMT_CMRS)
-        rc = spmv_cmrs_xwin_build(f->d, f->h, f->n_strips, f->d_ptr, f->d_col, f->d_win, bytes, &f->xcap);
-    else
-        rc = spmv_sell_xwin_build(f->d, f->C, f->sigma, f->n_slices, f->d_ptr, f->d_col, f->d_win, bytes,
-                                  &f->xcap);
-    return rc;
-}
-
-/* SELL16 (--index16): the SELL columns rewritten as 16-bit offsets from each
- * workgroup's window base on the device; matrices of the small-matrix
- * kernel also get the head copy.  Refused (exit 4) when a window spans more
- * than 65,536 columns or the split plan is in use (power-law rows). */
-static int build_sell16(dev_fmt_t *f)
-{
-    if (!f->d_win || f->split_T > 0)
-        return SPMV_OTHER_ERROR;
-    int rc = spmv_malloc((void **)&f->d_col16, (size_t)(f->stored > 0 ? f->stored : 1) * sizeof(uint16_t));
-    if (rc == SPMV_SUCCESS)
-        rc = spmv_sell16_fill(f->d, f->C, f->sigma, f->n_slices, f->d_ptr, f->d_col, f->d_win, f->d_col16);
-    const size_t hb = spmv_sell16_head_bytes(f->n_slices, f->C, f->ki);
-    if (rc == SPMV_SUCCESS && hb > 0) {
-        rc = spmv_malloc(&f->d_head, hb);
-        if (rc == SPMV_SUCCESS)
-            rc = spmv_sell16_head_fill(f->d, f->C, f->sigma, f->ki, f->n_slices, f->d_ptr, f->d_val, f->d_col16,
-                                       f->d_head, hb);
-    }
-    if (rc == SPMV_SUCCESS)
-        printf("SELL16: 16-bit column offsets, %.1f MB stored%s\n",
-               (10.0 * (double)f->stored + 8.0 * (double)(f->n_slices + 1) + 4.0 * (double)f->n_slices * f->C) * 1e-6,
-               hb > 0 ? " + head copy" : "");
-    return rc;
+    return make_plan(o, f, relabelled);
 }
 
 static int launch(void *arg)
 {
-    dev_fmt_t *f = (dev_fmt_t *)arg;
-    if (f->fmt == FMT_SELL && f->split_T > 0)
-        return spmv_sell_run_split(f->d, f->C, f->sigma, f->ki, f->n_slices, f->d_ptr, f->d_perm, f->d_col,
-                                   f->d_val, f->d_x, f->d_y, f->d_win, f->xcap, f->split_T, f->n_chunks,
-                                   f->d_chunk_slice, f->d_chunk_k0, f->d_ws, f->ws_bytes);
-    if (f->d_col16)
-        return spmv_sell16_run(f->d, f->C, f->sigma, f->ki, f->n_slices, f->d_ptr, f->d_perm, f->d_col16, f->d_val,
-                               f->d_x, f->d_y, f->d_win, f->xcap, f->d_head);
-    if (f->d_win) {
-        if (f->fmt == FMT_CSR)
-            return spmv_csr_run_xwin(f->d, f->d_ptr, f->d_col, f->d_val, f->d_x, f->d_y, f->lanes, 0,
-                                     f->d_win, f->xcap);
-        if (f->fmt == FMT_ELL)
-            return spmv_ell_run_xwin(f->d, f->K, f->ld, f->ki, f->d_col, f->d_val, f->d_x, f->d_y, f->d_win,
-                                     f->xcap);
-        if (f->fmt == FMT_COO)
-            return spmv_coo_run_xwin(f->d, f->d_row, f->d_col, f->d_val, f->d_x, f->d_y, f->d_ws, f->ws_bytes,
-                                     f->d_win, f->xcap);
-        if (f->fmt == FMT_CMRS)
-            return spmv_cmrs_run_xwin(f->d, f->h, f->n_strips, f->d_ptr, f->d_rin, f->d_col, f->d_val, f->d_x,
-                                      f->d_y, f->d_win, f->xcap);
-        if (f->fmt == FMT_SELL)
-            return spmv_sell_run_xwin(f->d, f->C, f->sigma, f->ki, f->n_slices, f->d_ptr, f->d_perm, f->d_col,
-                                      f->d_val, f->d_x, f->d_y, f->d_win, f->xcap);
+    const dev_fmt_t *f = (const dev_fmt_t *)arg;
+    return spmv_plan_run(f->plan, f->d_x, f->d_y, f->d.stream);
+}
+
+/* the "[plan]" line: the kernel the library chose and its parameters */
+static void print_plan(const dev_fmt_t *f, const char *who)
+{
+    spmv_plan_info info;
+    if (f->plan && spmv_plan_get_info(f->plan, &info) == SPMV_SUCCESS)
+        printf("  [plan]%s kernel %s: %s\n", who, info.kernel, info.desc);
+}
+
+/* The degree-ordered layout (--relabel; bench.py rmat_layout): the matrix
+ * in CSR order with columns renumbered by decreasing degree, ties by first
+ * appearance (spmv_column_relabel_ex), every row's entries by new column
+ * (spmv_csr_sort_rows), and x' = x[order]: the relabelled matrix on x'
+ * gives the original y, row for row (summation order aside). */
+static int relabel_layout(const coo_t *m, const double *x, coo_t *r, double **xr)
+{
+    const int64_t N = m->n_rows, M = m->n_cols, Z = m->nnz;
+    int64_t *ptr = malloc((size_t)(N + 1) * sizeof(int64_t));
+    int32_t *col = malloc((size_t)(Z + 1) * sizeof(int32_t));
+    double *val = malloc((size_t)(Z + 1) * sizeof(double));
+    int32_t *order = malloc((size_t)(M + 1) * sizeof(int32_t));
+    int32_t *newid = malloc((size_t)(M + 1) * sizeof(int32_t));
+    int32_t *row = malloc((size_t)(Z + 1) * sizeof(int32_t));
+    *xr = malloc((size_t)(M + 1) * sizeof(double));
+    if (!ptr || !col || !val || !order || !newid || !row || !*xr)
+        return SPMV_OTHER_ERROR;
+    int rc = spmv_csr_from_coo(N, Z, m->row, m->col, m->val, ptr, col, val);
+    if (rc == SPMV_SUCCESS && spmv_column_relabel_ex(M, Z, col, order, newid, col, 1) < 0)
+        rc = SPMV_OTHER_ERROR;
+    if (rc == SPMV_SUCCESS)
+        rc = spmv_csr_sort_rows(N, ptr, col, val);
+    if (rc != SPMV_SUCCESS)
+        return rc;
+    for (int64_t i = 0; i < N; ++i)
+        for (int64_t e = ptr[i]; e < ptr[i + 1]; ++e)
+            row[e] = (int32_t)i;
+    for (int64_t k = 0; k < M; ++k)
+        (*xr)[k] = x[order[k]];
+    *r = *m;
+    r->row = row;
+    r->col = col;
+    r->val = val;
+    free(ptr);
+    free(order);
+    free(newid);
+    return SPMV_SUCCESS;
+}
+
+/* The SpMV's time over `reps` launches.  cold: (span of reps x (512 MiB
+ * read flush + SpMV) - span of reps flushes) / reps, events on the stream,
+ * the launches queued back to back (the ~80 us flush hides the host);
+ * warm: span of reps back-to-back SpMVs / reps.  *ev_median: the median of
+ * per-launch event pairs (the rounds 1-5 figure, launch gaps included). */
+static int time_spmv(dev_fmt_t *f, int reps, int cold, double *ms, double *ev_median)
+{
+    void *st = f->d.stream;
+    int rc = spmv_flush_cache_read(st, 0); /* allocates the scratch outside the timed spans */
+    double both = 0.0, flush = 0.0;
+    if (rc == SPMV_SUCCESS)
+        rc = spmv_sync(st);
+    void *ev[2] = {NULL, NULL};
+    if (rc == SPMV_SUCCESS)
+        rc = spmv_event_create(&ev[0]);
+    if (rc == SPMV_SUCCESS)
+        rc = spmv_event_create(&ev[1]);
+    for (int pass = 0; pass < 2 && rc == SPMV_SUCCESS; ++pass) {
+        if (!cold && pass == 1)
+            break;
+        rc = spmv_event_record(ev[0], st);
+        for (int i = 0; i < reps && rc == SPMV_SUCCESS; ++i) {
+            if (cold)
+                rc = spmv_flush_cache_read(st, 0);
+            if (rc == SPMV_SUCCESS && pass == 0)
+                rc = launch(f);
+        }
+        if (rc == SPMV_SUCCESS)
+            rc = spmv_event_record(ev[1], st);
+        if (rc == SPMV_SUCCESS)
+            rc = spmv_event_elapsed(ev[0], ev[1], pass == 0 ? &both : &flush);
     }
-    switch (f->fmt) {
-    case FMT_COO:
-        if (f->d_tails)
-            return spmv_coo_run_tail(f->d, f->d_row, f->d_col, f->d_val, f->d_x, f->d_y, f->d_tails);
-        return spmv_coo_run(f->d, f->d_row, f->d_col, f->d_val, f->d_x, f->d_y, f->d_ws,
-                            f->ws_bytes);
-    case FMT_CSR:
-        if (f->variant == 4 && f->d_big && f->d_own_lo)
-            return spmv_csr_run_tiled_plan(f->d, f->d_ptr, f->d_col, f->d_val, f->d_x, f->d_y, f->H, f->d_hot,
-                                           f->d_own_lo, f->d_big, f->d_ws, f->ws_bytes);
-        if (f->variant == 4)
-            return spmv_csr_run_tiled_hot(f->d, f->d_ptr, f->d_col, f->d_val, f->d_x, f->d_y, f->H, f->d_hot,
-                                          f->d_own_lo, f->d_ws, f->ws_bytes);
-        return spmv_csr_run(f->d, f->d_ptr, f->d_col, f->d_val, f->d_x, f->d_y, f->lanes);
-    case FMT_ELL:
-        return spmv_ell_run(f->d, f->K, f->ld, f->ki, f->d_col, f->d_val, f->d_x, f->d_y);
-    case FMT_SELL:
-        return spmv_sell_run(f->d, f->C, f->sigma, f->ki, f->n_slices, f->d_ptr, f->d_perm, f->d_col,
-                             f->d_val, f->d_x, f->d_y);
-    case FMT_CMRS:
-        if (f->variant == 1)
-            return spmv_cmrs_run_tiled_hot(f->d, f->h, f->n_strips, f->d_ptr, f->d_rin, f->d_col, f->d_val,
-                                           f->d_x, f->d_y, f->H, f->d_hot, f->d_ws, f->ws_bytes);
-        return spmv_cmrs_run(f->d, f->h, f->n_strips, f->d_ptr, f->d_rin, f->d_col, f->d_val,
-                             f->d_x, f->d_y);
+    spmv_event_destroy(ev[0]);
+    spmv_event_destroy(ev[1]);
+    if (rc != SPMV_SUCCESS)
+        return rc;
+    *ms = (both - flush) / reps;
+    /* per-launch event pairs beside it */
+    double *t = malloc((size_t)reps * sizeof(double));
+    if (!t)
+        return SPMV_OTHER_ERROR;
+    for (int i = 0; i < reps && rc == SPMV_SUCCESS; ++i) {
+        if (cold)
+            rc = spmv_flush_cache_read(st, 0);
+        if (rc == SPMV_SUCCESS)
+            rc = spmv_time_launch(launch, f, st, &t[i]);
     }
-    return SPMV_OTHER_ERROR;
+    if (rc == SPMV_SUCCESS) {
+        qsort(t, (size_t)reps, sizeof(double), cmp_double);
+        *ev_median = t[reps / 2];
+    }
+    free(t);
+    return rc;
 }
 
 static int run_cpu(const dev_fmt_t *f, const double *x, double *y, int threads)
@@ -732,8 +666,11 @@ static double median_of(double *v, int n)
     return v[n / 2];
 }
 
-static int run_multi(const opts_t *o, spmv_format fmt, const coo_t *m, const double *x, double *y, double *y_cpu)
+static int run_multi(const opts_t *o, spmv_format fmt, const coo_t *m, const double *x, double *y, double *y_cpu,
+                     const coo_t *mr, const double *xr)
 {
+    /* mr / xr: the relabelled matrix and x' the shards run on (= m / x
+     * without --relabel); m / x: the original, for the check */
     const int G = o->gpus;
     const int64_t N = m->n_rows, Z = m->nnz;
     int rc;
@@ -749,7 +686,7 @@ static int run_multi(const opts_t *o, spmv_format fmt, const coo_t *m, const dou
     double *tall = malloc((size_t)o->reps * sizeof(double)), *tdev = malloc((size_t)o->reps * G * sizeof(double));
     if (!ptr || !tc || !tv || !bounds || !f || !y_full || !ms || !t || !tag || !tall || !tdev)
         return SPMV_OTHER_ERROR;
-    if ((rc = spmv_csr_from_coo(N, Z, m->row, m->col, m->val, ptr, tc, tv)) ||
+    if ((rc = spmv_csr_from_coo(N, Z, mr->row, mr->col, mr->val, ptr, tc, tv)) ||
         (rc = spmv_partition_rows(N, ptr, G, 1024, bounds)))
         return rc;
     free(tc);
@@ -762,27 +699,25 @@ static int run_multi(const opts_t *o, spmv_format fmt, const coo_t *m, const dou
     for (int g = 0; g < G; ++g) {
         const int64_t lo = bounds[g], hi = bounds[g + 1];
         coo_t s = {hi - lo, m->n_cols, 0, NULL, NULL, NULL, m->label};
-        s.nnz = spmv_coo_row_shard(Z, m->row, m->col, m->val, lo, hi, NULL, NULL, NULL);
+        s.nnz = spmv_coo_row_shard(Z, mr->row, mr->col, mr->val, lo, hi, NULL, NULL, NULL);
         s.row = malloc((size_t)(s.nnz + 1) * sizeof(int32_t));
         s.col = malloc((size_t)(s.nnz + 1) * sizeof(int32_t));
         s.val = malloc((size_t)(s.nnz + 1) * sizeof(double));
         if (s.nnz < 0 || !s.row || !s.col || !s.val)
             return SPMV_OTHER_ERROR;
-        spmv_coo_row_shard(Z, m->row, m->col, m->val, lo, hi, s.row, s.col, s.val);
+        spmv_coo_row_shard(Z, mr->row, mr->col, mr->val, lo, hi, s.row, s.col, s.val);
         opts_t og = *o;
         og.device = spmv_multi_device(mg, g);
         if ((rc = spmv_set_device(og.device)) != SPMV_SUCCESS)
             return rc;
-        rc = build_format(&og, fmt, &s, &f[g]);
+        rc = build_format(&og, fmt, &s, &f[g], mr != m);
         f[g].d.stream = spmv_multi_stream(mg, g);
-        if (rc == SPMV_SUCCESS && o->xwin)
-            rc = build_windows(&f[g]);
         if (rc != SPMV_SUCCESS) {
             printf("shard %d: format build/upload failed: %s %s\n", g, spmv_strerror(rc), spmv_last_error());
             return rc == SPMV_OTHER_ERROR ? SPMV_OTHER_ERROR : SPMV_PROGRAM_ERROR;
         }
         /* x replicated; this shard's kernel writes rows [lo, hi) of y_full */
-        if ((rc = upload((void **)&f[g].d_x, x, (size_t)m->n_cols * 8, NULL)) ||
+        if ((rc = upload((void **)&f[g].d_x, xr, (size_t)m->n_cols * 8, NULL)) ||
             (rc = spmv_malloc((void **)&y_full[g], (size_t)(N + 1) * 8)) ||
             /* NaN: every row must arrive; queued on the shard's own stream
              * (non-blocking, not ordered with the null stream) so the fill
@@ -856,6 +791,7 @@ static int run_multi(const opts_t *o, spmv_format fmt, const coo_t *m, const dou
         printf("  [multi] GPU %d: rows [%lld, %lld) %lld entries, median %.4f ms\n", spmv_multi_device(mg, g),
                (long long)bounds[g], (long long)bounds[g + 1], (long long)f[g].d.nnz,
                median_of(tdev + (size_t)g * o->reps, o->reps));
+    print_plan(&f[0], " GPU 0");
     printf("  [multi] y all-gather over RCCL (%d broadcasts of the real shard rows, %.1f MB per GPU received): "
            "%.4f ms; SpMV + all-gather %.4f ms = %.1f GB/s aggregate\n",
            G, 8e-6 * (double)N * (G - 1) / G, ag_ms, all_ms, bytes_alg / all_ms * 1e-6);
@@ -879,7 +815,7 @@ static int run_multi(const opts_t *o, spmv_format fmt, const coo_t *m, const dou
         int threads = o->threads > 0 ? o->threads : spmv_cpu_threads();
         double t0 = now_s();
         for (int g = 0; g < G; ++g) /* each shard's loop into its rows: the same reassembly */
-            run_cpu(&f[g], x, y_cpu + bounds[g], threads);
+            run_cpu(&f[g], xr, y_cpu + bounds[g], threads);
         double cms = (now_s() - t0) * 1e3;
         printf("\nCPU calculations\n"); /* reference csr.c:306 */
         print_performance(cms, Z);
@@ -920,20 +856,48 @@ int spmv_driver_main(int argc, char **argv, spmv_format fmt)
         return SPMV_OTHER_ERROR;
     for (int64_t j = 0; j < m.n_cols; ++j)
         x[j] = (double)j; /* reference csr.c:95-99 */
+
+    /* --relabel: the degree-ordered layout bench.py measures configs[3] on */
+    coo_t mr = m;
+    double *xr = x;
+    int relabel = o.relabel;
+    if (relabel < 0) { /* auto: when the CSR skew rule picks the entry-balanced kernel */
+        int64_t *ptr = malloc((size_t)(m.n_rows + 1) * sizeof(int64_t));
+        int32_t *tc = malloc((size_t)(m.nnz + 1) * sizeof(int32_t));
+        double *tv = malloc((size_t)(m.nnz + 1) * sizeof(double));
+        if (!ptr || !tc || !tv || spmv_csr_from_coo(m.n_rows, m.nnz, m.row, m.col, m.val, ptr, tc, tv))
+            return SPMV_OTHER_ERROR;
+        relabel = spmv_csr_pick_variant(m.n_rows, ptr) == 4;
+        free(ptr);
+        free(tc);
+        free(tv);
+    }
+    if (relabel) {
+        if ((rc = relabel_layout(&m, x, &mr, &xr)) != SPMV_SUCCESS) {
+            printf("relabel failed\n");
+            return rc;
+        }
+        printf("  [relabel] columns by decreasing degree (ties by first row), rows in new-column order; "
+               "x permuted to match\n");
+    }
     if (o.gpus >= 1)
-        return run_multi(&o, fmt, &m, x, y, y_cpu);
+        return run_multi(&o, fmt, &m, x, y, y_cpu, &mr, xr);
 
     dev_fmt_t f;
-    rc = build_format(&o, fmt, &m, &f);
-    if (rc == SPMV_SUCCESS && o.xwin)
-        rc = build_windows(&f);
-    if (rc == SPMV_SUCCESS && o.index16)
-        rc = build_sell16(&f);
+    rc = build_format(&o, fmt, &mr, &f, relabel);
     if (rc != SPMV_SUCCESS) {
         printf("format build/upload failed: %s %s\n", spmv_strerror(rc), spmv_last_error());
         return rc == SPMV_OTHER_ERROR ? SPMV_OTHER_ERROR : SPMV_PROGRAM_ERROR;
     }
-    if ((rc = upload((void **)&f.d_x, x, (size_t)m.n_cols * 8, NULL)) ||
+    if (fmt == FMT_COO) { /* stderr: stdout keeps the reference's lines, starting with "GPU calculations" */
+        spmv_plan_info info;
+        if (spmv_plan_get_info(f.plan, &info) == SPMV_SUCCESS)
+            fprintf(stderr, "COO single pass: %s\n",
+                    info.single_pass ? "no carry kernel"
+                    : o.single_pass  ? "refused (a row runs more than 80 entries past a tile), carry pass"
+                                     : "off (--carry-pass)");
+    }
+    if ((rc = upload((void **)&f.d_x, xr, (size_t)m.n_cols * 8, NULL)) ||
         (rc = spmv_malloc((void **)&f.d_y, (size_t)m.n_rows * 8)) ||
         (rc = spmv_memset(f.d_y, 0xFF, (size_t)m.n_rows * 8, NULL))) /* NaN: y must be written */
         return SPMV_PROGRAM_ERROR;
@@ -943,17 +907,15 @@ int spmv_driver_main(int argc, char **argv, spmv_format fmt)
             printf("kernel launch error: %s\n", spmv_last_error());
             return SPMV_PROGRAM_ERROR;
         }
-    double *t = malloc((size_t)o.reps * sizeof(double));
-    for (int i = 0; i < o.reps; ++i) {
-        if (!o.warm && spmv_flush_cache(NULL, 0) != SPMV_SUCCESS)
-            return SPMV_PROGRAM_ERROR;
-        if (spmv_time_launch(launch, &f, NULL, &t[i]) != SPMV_SUCCESS) {
-            printf("kernel launch error: %s\n", spmv_last_error());
-            return SPMV_PROGRAM_ERROR;
-        }
+    /* the SpMV's time: a span of reps x (flush + SpMV) minus a span of reps
+     * flushes, HIP events on the stream (bench.py's in-process method; the
+     * flush reads 512 MiB so nothing the SpMV needs is cached) — or, with
+     * --warm, reps back-to-back launches */
+    double ms = 0.0, ms_min = 0.0;
+    if ((rc = time_spmv(&f, o.reps, !o.warm, &ms, &ms_min)) != SPMV_SUCCESS) {
+        printf("kernel launch error: %s\n", spmv_last_error());
+        return SPMV_PROGRAM_ERROR;
     }
-    qsort(t, (size_t)o.reps, sizeof(double), cmp_double);
-    double ms = t[o.reps / 2];
 
     if (fmt == FMT_COO)
         printf("GPU calculations\n"); /* reference coo.c:201 */
@@ -964,25 +926,38 @@ int spmv_driver_main(int argc, char **argv, spmv_format fmt)
                              8.0 * (double)m.n_cols + 8.0 * (double)m.n_rows;
     char dev[128] = "";
     spmv_device_name(o.device, dev, sizeof dev);
-    printf("  [%s] %s | N=%lld M=%lld Z=%lld | median of %d %s reps (min %.4f ms)\n",
+    printf("  [%s] %s | N=%lld M=%lld Z=%lld | %s, %d reps (per-launch event median %.4f ms)\n",
            fmt_name(fmt), m.label, (long long)m.n_rows, (long long)m.n_cols, (long long)m.nnz,
-           o.reps, o.warm ? "warm (cache-resident)" : "cold (512 MiB flush)", t[0]);
+           o.warm ? "warm (cache-resident): span of back-to-back launches / reps"
+                  : "cold: (span of reps x (512 MiB read flush + SpMV) - span of reps flushes) / reps",
+           o.reps, ms_min);
     printf("  [%s] effective %.1f GB/s (bytes_alg %.1f MB) = %.1f%% of %.0f GB/s HBM3E peak; "
            "stored %.1f MB; %s\n",
            fmt_name(fmt), bytes_alg / ms * 1e-6, bytes_alg * 1e-6,
            100.0 * bytes_alg / ms * 1e-6 / HBM_PEAK_GBS, HBM_PEAK_GBS,
            (double)f.stored_bytes * 1e-6, dev);
+    print_plan(&f, "");
 
     if (spmv_download(y, f.d_y, (size_t)m.n_rows * 8, NULL) != SPMV_SUCCESS) {
         printf("read back error: %s\n", spmv_last_error());
         return SPMV_PROGRAM_ERROR;
+    }
+    if (o.write_y) {
+        FILE *fy = fopen(o.write_y, "wb");
+        if (!fy || fwrite(y, sizeof(double), (size_t)m.n_rows, fy) != (size_t)m.n_rows) {
+            perror(o.write_y);
+            if (fy)
+                fclose(fy);
+            return SPMV_FILE_ERROR;
+        }
+        fclose(fy);
     }
     int ok = check_and_report(&m, x, y, "");
 
     if (o.cpu) {
         int threads = o.threads > 0 ? o.threads : spmv_cpu_threads();
         double t0 = now_s();
-        run_cpu(&f, x, y_cpu, threads);
+        run_cpu(&f, xr, y_cpu, threads);
         double cms = (now_s() - t0) * 1e3;
         printf("\nCPU calculations\n"); /* reference csr.c:306 */
         print_performance(cms, m.nnz);
@@ -990,5 +965,6 @@ int spmv_driver_main(int argc, char **argv, spmv_format fmt)
                bytes_alg / cms * 1e-6);
         ok &= check_and_report(&m, x, y_cpu, "cpu ");
     }
+    spmv_plan_destroy(f.plan);
     return (o.strict && !ok) ? SPMV_OTHER_ERROR : SPMV_SUCCESS;
 }

@@ -138,11 +138,14 @@ static void sort_row(cv_t *a, cv_t *tmp, int64_t n)
 
 int spmv_csr_sort_rows(int64_t n_rows, const int64_t *row_ptr, int32_t *col, double *val)
 {
-    if (n_rows < 0 || !row_ptr || (row_ptr[n_rows] > 0 && (!col || !val)))
+    if (n_rows < 0 || !row_ptr || row_ptr[0] < 0 || (row_ptr[n_rows] > 0 && (!col || !val)))
         return SPMV_OTHER_ERROR;
     int64_t mx = 0;
-    for (int64_t r = 0; r < n_rows; ++r)
+    for (int64_t r = 0; r < n_rows; ++r) {
+        if (row_ptr[r + 1] < row_ptr[r]) /* offsets must not decrease */
+            return SPMV_OTHER_ERROR;
         mx = row_ptr[r + 1] - row_ptr[r] > mx ? row_ptr[r + 1] - row_ptr[r] : mx;
+    }
     int bad = 0;
 #pragma omp parallel reduction(| : bad)
     {
@@ -184,6 +187,11 @@ static int by_count_desc(const void *a, const void *b)
     return (p->col > q->col) - (p->col < q->col);
 }
 
+int spmv_hot_columns_possible(int64_t n_cols, int64_t H_req)
+{
+    return H_req > 0 || n_cols > ((int64_t)1 << 21);
+}
+
 int64_t spmv_hot_columns(int64_t n_cols, int64_t nnz, const int32_t *col, int64_t H_req, int32_t *hot,
                          int32_t *col_out)
 {
@@ -202,7 +210,7 @@ int64_t spmv_hot_columns(int64_t n_cols, int64_t nnz, const int32_t *col, int64_
         return -1;
     if (col_out != col)
         memcpy(col_out, col, (size_t)nnz * sizeof(int32_t));
-    if (H_req == 0 && n_cols <= ((int64_t)1 << 21))
+    if (!spmv_hot_columns_possible(n_cols, H_req))
         return 0;
     int64_t *cnt = (int64_t *)calloc((size_t)n_cols, sizeof(int64_t));
     if (!cnt)
@@ -434,12 +442,17 @@ int64_t spmv_column_relabel_ex(int64_t n_cols, int64_t nnz, const int32_t *col, 
     return nonempty;
 }
 
+int spmv_csr_variant_rule(int64_t n_rows, int64_t nnz, int64_t max_len)
+{
+    const double mean = n_rows > 0 ? (double)nnz / (double)n_rows : 0.0;
+    return (max_len > 4096 && (double)max_len > 64.0 * mean) ? 4 : 0;
+}
+
 int spmv_csr_pick_variant(int64_t n_rows, const int64_t *row_ptr)
 {
     int64_t mx = 0;
-    double mean = 0.0;
-    spmv_csr_row_stats(n_rows, row_ptr, NULL, &mx, &mean);
-    return (mx > 4096 && (double)mx > 64.0 * mean) ? 4 : 0;
+    spmv_csr_row_stats(n_rows, row_ptr, NULL, &mx, NULL);
+    return spmv_csr_variant_rule(n_rows, n_rows > 0 ? row_ptr[n_rows] - row_ptr[0] : 0, mx);
 }
 
 /* ------------------------------------------------------------------ ELL */
@@ -665,6 +678,14 @@ int spmv_cmrs_build(int64_t n_rows, const int64_t *row_ptr, int32_t h,
     return SPMV_SUCCESS;
 }
 
+int spmv_cmrs_variant_rule(int64_t n_strips, int64_t nnz, int64_t max_len)
+{
+    if (n_strips <= 0)
+        return 0;
+    const double mean = (double)nnz / (double)n_strips;
+    return (max_len > 4096 && (double)max_len > 64.0 * mean) ? 1 : 0;
+}
+
 int spmv_cmrs_pick_variant(int64_t n_strips, const int64_t *strip_ptr)
 {
     if (n_strips <= 0)
@@ -674,8 +695,7 @@ int spmv_cmrs_pick_variant(int64_t n_strips, const int64_t *strip_ptr)
         const int64_t l = strip_ptr[s + 1] - strip_ptr[s];
         mx = l > mx ? l : mx;
     }
-    const double mean = (double)(strip_ptr[n_strips] - strip_ptr[0]) / (double)n_strips;
-    return (mx > 4096 && (double)mx > 64.0 * mean) ? 1 : 0;
+    return spmv_cmrs_variant_rule(n_strips, strip_ptr[n_strips] - strip_ptr[0], mx);
 }
 
 /* ------------------------------------------------------------ SELL split */

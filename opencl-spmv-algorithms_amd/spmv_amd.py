@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 from dataclasses import dataclass, field
 from pathlib import Path
 
@@ -76,8 +77,49 @@ class MtxInfo(ctypes.Structure):
     ]
 
 
+class PlanOpts(ctypes.Structure):
+    """``spmv_plan_opts`` (include/spmv.h)."""
+
+    _fields_ = [
+        ("lanes", _c_i32),
+        ("variant", _c_i32),
+        ("xwin", _c_i32),
+        ("xwin_rows", _c_i32),
+        ("head", _c_i32),
+        ("index16", _c_i32),
+        ("coo_pass", _c_i32),
+        ("split", _c_i32),
+        ("bigplan", _c_i32),
+        ("reserved", _c_i32),
+        ("H", _c_i64),
+    ]
+
+
+class PlanInfo(ctypes.Structure):
+    """``spmv_plan_info`` (include/spmv.h)."""
+
+    _fields_ = [(k, _c_i32) for k in ("format", "path", "lanes", "variant", "ki", "xcap", "xwin", "head", "single_pass",
+                                      "index16", "split_T", "reserved")] + \
+               [(k, _c_i64) for k in ("n_chunks", "big_tiles", "head_bytes", "ws_bytes", "owned_bytes", "H")] + \
+               [("kernel", ctypes.c_char * 64), ("desc", ctypes.c_char * 320)]
+
+
+_PP = ctypes.POINTER(_vp)
+_PO = ctypes.POINTER(PlanOpts)
+
 # name -> (restype, argtypes)
 HIP_SYMBOLS = {
+    "spmv_plan_opts_init": (None, [_PO]),
+    "spmv_plan_coo": (ctypes.c_int, [Dims, _vp, _vp, _vp, _PO, _PP]),
+    "spmv_plan_csr": (ctypes.c_int, [Dims, _vp, _vp, _vp, _PO, _PP]),
+    "spmv_plan_ell": (ctypes.c_int, [Dims, _c_i32, _c_i64, _c_i32, _vp, _vp, _PO, _PP]),
+    "spmv_plan_sell": (ctypes.c_int, [Dims, _c_i32, _c_i32, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _PO, _PP]),
+    "spmv_plan_cmrs": (ctypes.c_int, [Dims, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _PO, _PP]),
+    "spmv_plan_run": (ctypes.c_int, [_vp, _vp, _vp, _vp]),
+    "spmv_plan_get_info": (ctypes.c_int, [_vp, ctypes.POINTER(PlanInfo)]),
+    "spmv_plan_destroy": (ctypes.c_int, [_vp]),
+    "spmv_set_option": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+    "spmv_get_option": (ctypes.c_int, [ctypes.c_int]),
     "spmv_coo_ws_bytes": (ctypes.c_size_t, [_c_i64]),
     "spmv_coo_run": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t]),
     "spmv_coo_tail_bytes": (ctypes.c_size_t, [_c_i64]),
@@ -97,8 +139,8 @@ HIP_SYMBOLS = {
     "spmv_csr_tiled_plan_len": (_c_i64, [_c_i64]),
     "spmv_csr_tiled_plan": (ctypes.c_int, [Dims, _vp, _vp]),
     "spmv_csr_tiled_tile": (_c_i64, [_c_i64, _c_i64]),
-    "spmv_csr_run_tiled_plan": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, _c_i64, _vp, _vp, _vp, _vp,
-                                               ctypes.c_size_t]),
+    "spmv_csr_run_tiled_plan": (ctypes.c_int, [Dims, _vp, _vp, _vp, _vp, _vp, _c_i64, _vp, _vp, _vp, _c_i64,
+                                               _c_i64, _vp, ctypes.c_size_t]),
     "spmv_csrg_ws_bytes": (ctypes.c_size_t, [_c_i64, _c_i64]),
     "spmv_csrg_run": (ctypes.c_int, [Dims, _c_i32, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                      ctypes.c_size_t]),
@@ -190,6 +232,11 @@ HIP_SYMBOLS = {
     "spmv_stream_destroy": (ctypes.c_int, [_vp]),
     "spmv_sync": (ctypes.c_int, [_vp]),
     "spmv_flush_cache": (ctypes.c_int, [_vp, ctypes.c_size_t]),
+    "spmv_flush_cache_read": (ctypes.c_int, [_vp, ctypes.c_size_t]),
+    "spmv_event_create": (ctypes.c_int, [ctypes.POINTER(_vp)]),
+    "spmv_event_destroy": (ctypes.c_int, [_vp]),
+    "spmv_event_record": (ctypes.c_int, [_vp, _vp]),
+    "spmv_event_elapsed": (ctypes.c_int, [_vp, _vp, ctypes.POINTER(ctypes.c_double)]),
     "spmv_time_launch": (ctypes.c_int, [_vp, _vp, _vp, ctypes.POINTER(ctypes.c_double)]),
     "spmv_release": (ctypes.c_int, []),
     "spmv_multi_init": (ctypes.c_int, [ctypes.c_int, _vp, _vp]),
@@ -217,6 +264,9 @@ HOST_SYMBOLS = {
     "spmv_csr_sort_rows": (ctypes.c_int, [_c_i64, _vp, _vp, _vp]),
     "spmv_csr_row_stats": (ctypes.c_int, [_c_i64, _vp, ctypes.POINTER(_c_i64), ctypes.POINTER(_c_i64), ctypes.POINTER(ctypes.c_double)]),
     "spmv_csr_pick_variant": (ctypes.c_int, [_c_i64, _vp]),
+    "spmv_csr_variant_rule": (ctypes.c_int, [_c_i64, _c_i64, _c_i64]),
+    "spmv_cmrs_variant_rule": (ctypes.c_int, [_c_i64, _c_i64, _c_i64]),
+    "spmv_hot_columns_possible": (ctypes.c_int, [_c_i64, _c_i64]),
     "spmv_hot_columns": (_c_i64, [_c_i64, _c_i64, _vp, _c_i64, _vp, _vp]),
     "spmv_column_relabel": (_c_i64, [_c_i64, _c_i64, _vp, _vp, _vp, _vp]),
     "spmv_column_relabel_ex": (_c_i64, [_c_i64, _c_i64, _vp, _vp, _vp, _vp, _c_i32]),
@@ -275,6 +325,7 @@ def hip_lib() -> ctypes.CDLL:
     """libspmv_hip.so — raises if it was not built (no CPU fallback)."""
     global _hip
     if _hip is None:
+        host_lib()  # its plans call the host rules: loaded first (RTLD_GLOBAL, soname libspmv_host.so)
         path = Path(os.environ.get("SPMV_HIP_LIB") or LIB_DIR / "libspmv_hip.so")  # override: A/B runs
         if not path.exists():
             raise SpmvError(PROGRAM_ERROR, "load libspmv_hip.so", f"{path} missing: run `make lib`")
@@ -288,7 +339,7 @@ def host_lib() -> ctypes.CDLL:
         path = Path(os.environ.get("SPMV_HOST_LIB", LIB_DIR / "libspmv_host.so"))  # `make test-san` build
         if not path.exists():
             raise SpmvError(PROGRAM_ERROR, "load libspmv_host.so", f"{path} missing: run `make lib`")
-        _host = _bind(ctypes.CDLL(str(path)), HOST_SYMBOLS)
+        _host = _bind(ctypes.CDLL(str(path), mode=ctypes.RTLD_GLOBAL), HOST_SYMBOLS)
     return _host
 
 
@@ -688,7 +739,15 @@ def _dev_tensor(arr: np.ndarray, device):
 
 @dataclass
 class DeviceMatrix:
-    """One format resident in HBM, ready for repeated SpMV launches."""
+    """One format resident in HBM, ready for repeated SpMV launches.
+
+    The reference's five formats run through a C plan (spmv_plan_<fmt>,
+    include/spmv.h): the library chooses and prepares the kernel path once,
+    exactly as ./bin/<fmt> does, and run() is spmv_plan_run.  `arrays`
+    holds the format's device arrays (torch tensors, owned here; the plan
+    keeps pointers to them), `params` the plan's choices (spmv_plan_info).
+    The §8f extra formats (csr16, csrf32, hyb, csrg) call their entry
+    points of include/spmv_ext.h directly."""
 
     fmt: str
     n_rows: int
@@ -698,10 +757,21 @@ class DeviceMatrix:
     arrays: dict = field(default_factory=dict)
     params: dict = field(default_factory=dict)
     stored_bytes: int = 0
+    plan: object = None  # ctypes.c_void_p of an spmv_plan, or None
+
+    def __del__(self):
+        plan, self.plan = self.plan, None
+        if plan is not None and _hip is not None and not sys.is_finalizing():
+            _hip.spmv_plan_destroy(plan)
 
     @property
     def bytes_alg(self) -> int:
         return bytes_alg(self.n_rows, self.n_cols, self.nnz)
+
+    @property
+    def kernel(self) -> str:
+        """The dominant kernel the plan launches (rocprofv3 name, no template args)."""
+        return self.params.get("kernel", "")
 
     def dims(self, stream=None) -> Dims:
         torch = _torch()
@@ -713,10 +783,10 @@ class DeviceMatrix:
     def run(self, x, y, stream=None) -> None:
         """y = A x on `stream` (default: torch's current stream)."""
         lib = hip_lib()
-        d = self.dims(stream)
+        torch = _torch()
         a = self.arrays
         p = self.params
-        if x.dtype != _torch().float64 or y.dtype != _torch().float64:
+        if x.dtype != torch.float64 or y.dtype != torch.float64:
             raise SpmvError(OTHER_ERROR, "run", "x and y must be float64")
         if x.numel() < self.n_cols or y.numel() < self.n_rows:
             raise SpmvError(OTHER_ERROR, "run", "x or y too short")
@@ -724,42 +794,17 @@ class DeviceMatrix:
         # another device would give a wrong y or a GPU fault
         if not (x.is_contiguous() and y.is_contiguous()):
             raise SpmvError(OTHER_ERROR, "run", "x and y must be contiguous")
-        here = _torch().device(self.device)
+        here = torch.device(self.device)
         idx = here.index or 0  # the device dims() passes to the C-ABI
         for t in (x, y):
             if t.device.type != here.type or (t.device.index or 0) != idx:
                 raise SpmvError(OTHER_ERROR, "run", f"x and y must be on {here.type}:{idx}")
-        if self.fmt == "coo" and p.get("H", 0) > 0:
-            rc = lib.spmv_coo_run_hot(d, _ptr(a["row"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y), p["H"],
-                                      _ptr(a["hot"]), _ptr(a["ws"]), a["ws"].numel())
-        elif self.fmt == "coo" and "tails" in a:
-            rc = lib.spmv_coo_run_tail(d, _ptr(a["row"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
-                                       _ptr(a["tails"]))
-        elif self.fmt == "coo" and "win" in a:
-            rc = lib.spmv_coo_run_xwin(d, _ptr(a["row"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
-                                       _ptr(a["ws"]), a["ws"].numel(), _ptr(a["win"]), p["xcap"])
-        elif self.fmt == "coo":
-            rc = lib.spmv_coo_run(d, _ptr(a["row"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
-                                  _ptr(a["ws"]), a["ws"].numel())
-        elif self.fmt == "csr" and "win" in a:
-            rc = lib.spmv_csr_run_xwin(d, _ptr(a["row_ptr"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
-                                       p["lanes"], p.get("xwin_rows", 0), _ptr(a["win"]), p["xcap"])
-        elif self.fmt == "csr":
-            if p.get("variant", 0) == 4 and "big" in a:
-                rc = lib.spmv_csr_run_tiled_plan(d, _ptr(a["row_ptr"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x),
-                                                 _ptr(y), p["H"], _ptr(a.get("hot")), _ptr(a["own_lo"]),
-                                                 _ptr(a["big"]), _ptr(a["ws"]), a["ws"].numel())
-            elif p.get("variant", 0) == 4 and "own_lo" in a:
-                rc = lib.spmv_csr_run_tiled_hot(d, _ptr(a["row_ptr"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x),
-                                                _ptr(y), p["H"], _ptr(a.get("hot")), _ptr(a["own_lo"]), _ptr(a["ws"]),
-                                                a["ws"].numel())
-            elif p.get("variant", 0) == 4:
-                rc = lib.spmv_csr_run_tiled(d, _ptr(a["row_ptr"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x),
-                                            _ptr(y), _ptr(a["ws"]), a["ws"].numel())
-            else:
-                rc = lib.spmv_csr_run_variant(d, _ptr(a["row_ptr"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x),
-                                              _ptr(y), p["lanes"], p.get("variant", 0))
-        elif self.fmt == "csrf32" and p.get("variant") == 4:
+        if self.plan is not None:
+            st = stream if stream is not None else torch.cuda.current_stream(here)
+            _check(lib.spmv_plan_run(self.plan, _ptr(x), _ptr(y), st.cuda_stream), f"spmv_plan_run ({self.fmt})")
+            return
+        d = self.dims(stream)
+        if self.fmt == "csrf32" and p.get("variant") == 4:
             rc = lib.spmv_csr_f32v_run_tiled_hot(d, _ptr(a["row_ptr"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x),
                                                  _ptr(y), p["H"], _ptr(a.get("hot")), _ptr(a.get("own_lo")),
                                                  _ptr(a["ws"]), a["ws"].numel())
@@ -790,180 +835,68 @@ class DeviceMatrix:
             rc = lib.spmv_hyb_run(d, p["K"], p["ld"], p["ki"], _ptr(a["ell_col"]), _ptr(a["ell_val"]), p["tail_nnz"],
                                   _ptr(a["tail_row"]), _ptr(a["tail_col"]), _ptr(a["tail_val"]), _ptr(x), _ptr(y),
                                   _ptr(a["ws"]), a["ws"].numel())
-        elif self.fmt == "ell" and "win" in a:
-            rc = lib.spmv_ell_run_xwin(d, p["K"], p["ld"], p["ki"], _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
-                                       _ptr(a["win"]), p["xcap"])
-        elif self.fmt == "ell":
-            rc = lib.spmv_ell_run(d, p["K"], p["ld"], p["ki"], _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y))
         elif self.fmt == "csrg":
             rc = lib.spmv_csrg_run(d, p["groups"], p["n_pairs"], _ptr(a["pair_ptr"]), _ptr(a["col_g"]),
                                    _ptr(a["val_g"]), _ptr(a.get("own_lo")), _ptr(a["blk_off"]), _ptr(a["pair_row"]),
                                    _ptr(x), _ptr(y), _ptr(a["ws"]), a["ws"].numel())
-        elif self.fmt == "sell16":
-            rc = lib.spmv_sell16_run(d, p["C"], p["sigma"], p["ki"], p["n_slices"], _ptr(a["slice_ptr"]),
-                                     _ptr(a["perm"]), _ptr(a["col16"]), _ptr(a["val"]), _ptr(x), _ptr(y),
-                                     _ptr(a["win"]), p["xcap"], _ptr(a.get("head")))
-        elif self.fmt == "sell" and p.get("H", 0) > 0:
-            split = p.get("split_T", 0) > 0
-            rc = lib.spmv_sell_run_hot(d, p["C"], p["sigma"], p["ki"], p["n_slices"], _ptr(a["slice_ptr"]),
-                                       _ptr(a["perm"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
-                                       p["split_T"] if split else 2**31 - 1, p["n_chunks"] if split else 0,
-                                       _ptr(a.get("chunk_slice")), _ptr(a.get("chunk_k0")), p["H"], _ptr(a["hot"]),
-                                       _ptr(a["hot_ws"]), a["hot_ws"].numel())
-        elif self.fmt == "sell" and p.get("split_T", 0) > 0:
-            rc = lib.spmv_sell_run_split(d, p["C"], p["sigma"], p["ki"], p["n_slices"], _ptr(a["slice_ptr"]),
-                                         _ptr(a["perm"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
-                                         _ptr(a.get("win")), p.get("xcap", 0), p["split_T"], p["n_chunks"],
-                                         _ptr(a["chunk_slice"]), _ptr(a["chunk_k0"]), _ptr(a["split_ws"]),
-                                         a["split_ws"].numel())
-        elif self.fmt == "sell" and "win" in a and "head" in a:
-            rc = lib.spmv_sell_run_xwin_head(d, p["C"], p["sigma"], p["ki"], p["n_slices"], _ptr(a["slice_ptr"]),
-                                             _ptr(a["perm"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
-                                             _ptr(a["win"]), p["xcap"], _ptr(a["head"]))
-        elif self.fmt == "sell" and "win" in a:
-            rc = lib.spmv_sell_run_xwin(d, p["C"], p["sigma"], p["ki"], p["n_slices"], _ptr(a["slice_ptr"]),
-                                        _ptr(a["perm"]), _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y),
-                                        _ptr(a["win"]), p["xcap"])
-        elif self.fmt == "sell":
-            rc = lib.spmv_sell_run(d, p["C"], p["sigma"], p["ki"], p["n_slices"], _ptr(a["slice_ptr"]), _ptr(a["perm"]),
-                                   _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y))
-        elif self.fmt == "cmrs" and p.get("variant", 0) == 1 and p.get("H", 0) > 0:
-            rc = lib.spmv_cmrs_run_tiled_hot(d, p["h"], p["n_strips"], _ptr(a["strip_ptr"]), _ptr(a["row_in_strip"]),
-                                             _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y), p["H"], _ptr(a["hot"]),
-                                             _ptr(a["ws"]), a["ws"].numel())
-        elif self.fmt == "cmrs" and p.get("variant", 0) == 1:
-            rc = lib.spmv_cmrs_run_tiled(d, p["h"], p["n_strips"], _ptr(a["strip_ptr"]), _ptr(a["row_in_strip"]),
-                                         _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y), _ptr(a["ws"]),
-                                         a["ws"].numel())
-        elif self.fmt == "cmrs" and "win" in a:
-            rc = lib.spmv_cmrs_run_xwin(d, p["h"], p["n_strips"], _ptr(a["strip_ptr"]), _ptr(a["row_in_strip"]),
-                                        _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y), _ptr(a["win"]), p["xcap"])
-        elif self.fmt == "cmrs":
-            rc = lib.spmv_cmrs_run(d, p["h"], p["n_strips"], _ptr(a["strip_ptr"]), _ptr(a["row_in_strip"]),
-                                   _ptr(a["col"]), _ptr(a["val"]), _ptr(x), _ptr(y))
         else:
-            raise SpmvError(OTHER_ERROR, "run", f"unknown format {self.fmt}")
+            raise SpmvError(OTHER_ERROR, "run", f"format {self.fmt} has no plan and no entry point")
         _check(rc, f"spmv_{self.fmt}_run")
 
 
-def _sell_xwin(dm: DeviceMatrix) -> None:
-    """Per-workgroup column windows for the x-window SELL kernel (device
-    pass over col; xcap = LDS entries the run stages, 0 = none fits)."""
-    torch = _torch()
-    p, a = dm.params, dm.arrays
-    nbytes = hip_lib().spmv_sell_xwin_bytes(p["n_slices"], p["C"], p["sigma"])
-    a["win"] = torch.empty(max(nbytes, 8), dtype=torch.uint8, device=dm.device)
-    cap = _c_i32(0)
-    _check(hip_lib().spmv_sell_xwin_build(dm.dims(), p["C"], p["sigma"], p["n_slices"], _ptr(a["slice_ptr"]),
-                                          _ptr(a["col"]), _ptr(a["win"]), a["win"].numel(), ctypes.byref(cap)),
-           "spmv_sell_xwin_build")
-    p["xcap"] = cap.value
+# the library's A/B switches (include/spmv_ext.h; placement and load policy only)
+OPTIONS = {"xwin_remap": 1, "xcd_remap": 2, "stream_nt": 3}
 
 
-def _sell_split(dm: DeviceMatrix, slice_ptr: np.ndarray, split: int | None) -> None:
-    """Wide-slice split plan (power-law rows): split None = library rule
-    (spmv_sell_split_auto), 0 = off, T > 0 = keep T slot columns per slice
-    in the main kernel and hand the rest to the chunk kernel."""
-    torch = _torch()
-    p, a = dm.params, dm.arrays
-    if split is not None and split > 0 and split % p["ki"]:
-        raise SpmvError(OTHER_ERROR, "sell split", "T must be a multiple of ki")
-    T, cs, ck = sell_split_plan(dict(slice_ptr=slice_ptr, n_slices=p["n_slices"], C=p["C"], ki=p["ki"]), split)
-    p["split_T"] = 0
-    if T <= 0:
-        return
-    n = len(cs)
-    if n == 0:
-        cs, ck = np.zeros(1, np.int32), np.zeros(1, np.int32)
-    p["split_T"], p["n_chunks"] = T, n
-    a["chunk_slice"] = _dev_tensor(cs, dm.device)
-    a["chunk_k0"] = _dev_tensor(ck, dm.device)
-    a["split_ws"] = torch.empty(max(hip_lib().spmv_sell_split_ws_bytes(n, p["C"]), 8), dtype=torch.uint8,
-                                device=dm.device)
+def set_option(name: str, value: int | None) -> None:
+    """spmv_set_option: None / -1 = each kernel's default, 0 off, 1 on."""
+    _check(hip_lib().spmv_set_option(OPTIONS[name], -1 if value is None else int(value)), f"set_option {name}")
 
 
-def _sell_hot(dm: DeviceMatrix, col: np.ndarray, hot: int | None) -> None:
-    """Hot-column table over the stored SELL columns (None: library rule,
-    0: off).  The renumbered ids are not x positions, so the x windows are
-    dropped; the run gathers globally (spmv_sell_run_hot)."""
-    torch = _torch()
-    p, a = dm.params, dm.arrays
-    p["H"] = 0
-    if hot == 0:
-        return
-    H, hot_cols, col_hot = hot_columns(dm.n_cols, col, hot or 0)
-    if H == 0:
-        return
-    p["H"] = H
-    a["col"] = _dev_tensor(col_hot, dm.device)
-    a["hot"] = _dev_tensor(hot_cols, dm.device)
-    a.pop("win", None)
-    n_chunks = p.get("n_chunks", 0) if p.get("split_T", 0) > 0 else 0
-    a["hot_ws"] = torch.empty(max(hip_lib().spmv_sell_hot_ws_bytes(n_chunks, p["C"], H), 8), dtype=torch.uint8,
-                              device=dm.device)
+def get_option(name: str) -> int:
+    return int(hip_lib().spmv_get_option(OPTIONS[name]))
 
 
-def _cmrs_variant(dm: DeviceMatrix, strip_ptr: np.ndarray, variant: int | None, col=None,
-                  hot: int | None = None) -> None:
-    """variant None = library rule (spmv_cmrs_pick_variant), 0 = strip-run
-    kernel, 1 = entry-balanced tiles (+ workspace, and the hot-column table
-    of `col` unless hot == 0)."""
-    torch = _torch()
-    p = dm.params
-    sp = np.ascontiguousarray(strip_ptr, dtype=np.int64)
-    v = host_lib().spmv_cmrs_pick_variant(p["n_strips"], _ptr(sp)) if variant is None else int(variant)
-    p["variant"] = v
-    p["H"] = 0
-    if v == 1:
-        if col is not None and hot != 0:
-            H, hot_cols, col_hot = hot_columns(dm.n_cols, col, hot or 0)
-            if H > 0:
-                p["H"] = H
-                dm.arrays["col"] = _dev_tensor(col_hot, dm.device)
-                dm.arrays["hot"] = _dev_tensor(hot_cols, dm.device)
-        ws = hip_lib().spmv_cmrs_hot_ws_bytes(p["n_strips"], dm.nnz, p["h"], p["H"])
-        dm.arrays["ws"] = torch.empty(max(ws, 16), dtype=torch.uint8, device=dm.device)
+def _tri(v) -> int:
+    """None -> -1 (the library's rule), else 0 / 1."""
+    return -1 if v is None else int(bool(v))
 
 
-def _coo_xwin(dm: DeviceMatrix) -> None:
-    """Per-tile column windows for the x-window COO kernel."""
-    torch = _torch()
-    p, a = dm.params, dm.arrays
-    nbytes = hip_lib().spmv_coo_xwin_bytes(dm.nnz)
-    a["win"] = torch.empty(max(nbytes, 8), dtype=torch.uint8, device=dm.device)
-    cap = _c_i32(0)
-    _check(hip_lib().spmv_coo_xwin_build(dm.dims(), _ptr(a["col"]), _ptr(a["win"]), a["win"].numel(),
-                                         ctypes.byref(cap)), "spmv_coo_xwin_build")
-    p["xcap"] = cap.value
+def plan_opts(**kw) -> PlanOpts:
+    """spmv_plan_opts with the library defaults, then the given fields."""
+    o = PlanOpts()
+    hip_lib().spmv_plan_opts_init(ctypes.byref(o))
+    for k, v in kw.items():
+        setattr(o, k, v)
+    return o
 
 
-def _cmrs_xwin(dm: DeviceMatrix) -> None:
-    """Per-strip-run column windows for the x-window CMRS kernel."""
-    torch = _torch()
-    p, a = dm.params, dm.arrays
-    nbytes = hip_lib().spmv_cmrs_xwin_bytes(dm.dims(), p["h"], p["n_strips"])
-    a["win"] = torch.empty(max(nbytes, 8), dtype=torch.uint8, device=dm.device)
-    cap = _c_i32(0)
-    _check(hip_lib().spmv_cmrs_xwin_build(dm.dims(), p["h"], p["n_strips"], _ptr(a["strip_ptr"]), _ptr(a["col"]),
-                                          _ptr(a["win"]), a["win"].numel(), ctypes.byref(cap)),
-           "spmv_cmrs_xwin_build")
-    p["xcap"] = cap.value
+_PLAN_INFO_KEYS = ("lanes", "variant", "ki", "xcap", "xwin", "head", "single_pass", "index16", "split_T", "n_chunks",
+                   "big_tiles", "head_bytes", "ws_bytes", "owned_bytes", "H")
 
 
-def _ell_xwin(dm: DeviceMatrix) -> None:
-    """Per-256-row column windows for the x-window ELL kernel."""
-    torch = _torch()
-    p, a = dm.params, dm.arrays
-    nbytes = hip_lib().spmv_ell_xwin_bytes(dm.n_rows)
-    a["win"] = torch.empty(max(nbytes, 8), dtype=torch.uint8, device=dm.device)
-    cap = _c_i32(0)
-    _check(hip_lib().spmv_ell_xwin_build(dm.dims(), p["K"], p["ld"], p["ki"], _ptr(a["col"]), _ptr(a["win"]),
-                                         a["win"].numel(), ctypes.byref(cap)), "spmv_ell_xwin_build")
-    p["xcap"] = cap.value
+def _attach_plan(dm: DeviceMatrix, what: str, create, *args, opts: PlanOpts) -> None:
+    """Create the C plan of dm (spmv_plan_<fmt>) and copy its choices
+    (spmv_plan_info) into dm.params."""
+    plan = _vp()
+    _check(create(dm.dims(), *args, ctypes.byref(opts), ctypes.byref(plan)), what)
+    dm.plan = plan
+    info = PlanInfo()
+    _check(hip_lib().spmv_plan_get_info(plan, ctypes.byref(info)), "spmv_plan_get_info")
+    for k in _PLAN_INFO_KEYS:
+        dm.params[k] = int(getattr(info, k))
+    dm.params["kernel"] = info.kernel.decode()
+    dm.params["plan"] = info.desc.decode()
+
+
+def plan_info(dm: DeviceMatrix) -> dict:
+    """The plan's choices as a dict (the fields of spmv_plan_info)."""
+    return {k: dm.params[k] for k in _PLAN_INFO_KEYS + ("kernel", "plan") if k in dm.params}
 
 
 def _csr_xwin(dm: DeviceMatrix) -> None:
-    """Per-row-group column windows for the x-window CSR kernel."""
+    """Per-row-group column windows for the x-window CSR kernel (the
+    CSR16 / CSR-f32 formats of spmv_ext.h; CSR itself plans its own)."""
     torch = _torch()
     p, a = dm.params, dm.arrays
     rows = p.setdefault("xwin_rows", 0)
@@ -976,94 +909,86 @@ def _csr_xwin(dm: DeviceMatrix) -> None:
     p["variant"] = 3
 
 
+def _plan_coo(dm, row, col, val, *, xwin=None, coo_tail=None, hot=None):
+    dm.arrays = dict(row=_dev_tensor(row, dm.device), col=_dev_tensor(col, dm.device), val=_dev_tensor(val, dm.device))
+    o = plan_opts(xwin=_tri(xwin), coo_pass=_tri(coo_tail), H=-1 if hot is None else int(hot))
+    a = dm.arrays
+    _attach_plan(dm, "spmv_plan_coo", hip_lib().spmv_plan_coo, _ptr(a["row"]), _ptr(a["col"]), _ptr(a["val"]),
+                 opts=o)
+    dm.stored_bytes = 16 * dm.nnz
+
+
+def _plan_csr(dm, *, lanes=0, variant=0, xwin=None, xwin_rows=0, hot=None, bigplan=True):
+    a = dm.arrays
+    o = plan_opts(lanes=int(lanes), variant=int(variant) if variant else -1, xwin=_tri(xwin), xwin_rows=int(xwin_rows),
+                  bigplan=-1 if bigplan else 0, H=-1 if hot is None else int(hot))
+    _attach_plan(dm, "spmv_plan_csr", hip_lib().spmv_plan_csr, _ptr(a["row_ptr"]), _ptr(a["col"]), _ptr(a["val"]),
+                 opts=o)
+    dm.params["xwin_rows"] = int(xwin_rows)
+    dm.stored_bytes = 12 * dm.nnz + 8 * (dm.n_rows + 1)
+
+
+def _plan_ell(dm, *, xwin=None):
+    a, p = dm.arrays, dm.params
+    _attach_plan(dm, "spmv_plan_ell", hip_lib().spmv_plan_ell, p["K"], p["ld"], p["ki"], _ptr(a["col"]), _ptr(a["val"]),
+                 opts=plan_opts(xwin=_tri(xwin)))
+    dm.stored_bytes = 12 * p["stored"]
+
+
+def _plan_sell(dm, *, xwin=None, split=None, hot=None, head=None, index16=False):
+    a, p = dm.arrays, dm.params
+    o = plan_opts(xwin=_tri(xwin), split=-1 if split is None else int(split), H=-1 if hot is None else int(hot),
+                  head=_tri(head), index16=int(bool(index16)))
+    _attach_plan(dm, "spmv_plan_sell", hip_lib().spmv_plan_sell, p["C"], p["sigma"], p["ki"], p["n_slices"],
+                 _ptr(a["slice_ptr"]), _ptr(a["perm"]), _ptr(a["col"]), _ptr(a["val"]), opts=o)
+    per_slot = 10 if index16 else 12
+    dm.stored_bytes = per_slot * p["stored"] + 8 * (p["n_slices"] + 1) + 4 * p["n_slices"] * p["C"]
+
+
+def _plan_cmrs(dm, *, variant=None, xwin=None, hot=None):
+    a, p = dm.arrays, dm.params
+    v = -1 if variant is None else (1 if int(variant) == 0 else 2)  # python 0 strip runs / 1 tiles
+    o = plan_opts(variant=v, xwin=_tri(xwin), H=-1 if hot is None else int(hot))
+    _attach_plan(dm, "spmv_plan_cmrs", hip_lib().spmv_plan_cmrs, p["h"], p["n_strips"], _ptr(a["strip_ptr"]),
+                 _ptr(a["row_in_strip"]), _ptr(a["col"]), _ptr(a["val"]), opts=o)
+    dm.stored_bytes = 13 * dm.nnz + 8 * (p["n_strips"] + 1)
+
+
 def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int = 0, ki: int = 0, C: int = 64,
               sigma: int = 1024, h: int = 8, ell_max_padding: float | None = 64.0,
               xwin: bool | None = None, xwin_rows: int = 0, split: int | None = None,
               cmrs_variant: int | None = None, hot: int | None = None,
               csr16_max_escape: float | None = 0.5, groups: int = 0, head: bool = True,
               sell_head: bool | None = None, coo_tail: bool | None = None, bigplan: bool = True) -> DeviceMatrix:
-    """Build `fmt` on the host (libspmv_host.so) and upload it.  xwin (CSR,
-    ELL, SELL; default on): also build the per-workgroup x windows on the
-    device and run the LDS x-window kernels (same bits as without).  split
-    (SELL) / cmrs_variant (CMRS): None = the library's skew rule.
-    sell_head (SELL): None = the head copy wherever the small-matrix kernel
-    runs (spmv_sell_head_bytes > 0: one cant-like matrix cold 11.9 -> 11.4 us,
-    same bits).  coo_tail (COO, HYB): None = the single pass where the tail
-    plan accepts the matrix, True = it or raise, False = the carry pass.
-    bigplan (tiled CSR): the plan of the tiles that own more than 1,024 rows
-    (spmv_csr_tiled_bigplan); False keeps their global-offset row phase."""
+    """Build `fmt` on the host (libspmv_host.so), upload it and, for the
+    reference's five formats and SELL16, create its C plan (spmv.h): the
+    library picks the kernel path — x windows in LDS (CSR, ELL, SELL, CMRS
+    by default; COO opt-in), the entry-balanced tiles for skewed rows, the
+    SELL head copy / split, the single-pass COO — exactly as ./bin/<fmt>.
+    The keywords override its rules: xwin (None = the library's default),
+    variant (CSR: 0 = the skew rule, 1-4 forced), cmrs_variant (None rule,
+    0 strip runs, 1 tiles), split (SELL: None rule, 0 off, T), hot (None =
+    the hot-column rule, 0 none, H forced), sell_head (None/True = the head
+    copy where the small-matrix kernel runs), coo_tail (None = the single
+    pass where the tail plan accepts the matrix, True = it or raise, False =
+    the carry pass), bigplan (tiled CSR's big-tile plan)."""
     torch = _torch()
-    if xwin is None:
-        # COO: per-tile windows measured slower (0.534 vs 0.491 ms on the
-        # cant-like batch), so they stay opt-in; CMRS 0.352 vs 0.404 ms
-        xwin = fmt in ("csr", "csr16", "ell", "sell", "cmrs", "hyb")
     device = torch.device(device)
     dm = DeviceMatrix(fmt, m.n_rows, m.n_cols, m.nnz, device)
     if fmt == "coo":
         row, col, val = coo_sort_by_row(m)
-        # hot-column table for power-law columns (None: library rule)
-        H, hot_cols, col_hot = hot_columns(m.n_cols, col, hot or 0) if hot != 0 else (0, None, col)
-        ws_bytes = hip_lib().spmv_coo_hot_ws_bytes(m.nnz, H)
-        dm.params["H"] = H
-        dm.arrays = dict(row=_dev_tensor(row, device), col=_dev_tensor(col_hot, device),
-                         val=_dev_tensor(val, device),
-                         ws=torch.empty(ws_bytes, dtype=torch.uint8, device=device))
-        if H > 0:
-            dm.arrays["hot"] = _dev_tensor(hot_cols, device)
-        dm.stored_bytes = 16 * m.nnz
-        if coo_tail and (xwin or H > 0):  # ADVICE r4: never drop an explicit request silently
-            raise SpmvError(OTHER_ERROR, "to_device", "coo_tail=True needs xwin=False and no hot-column table "
-                            "(hot=0): the x-window and hot-table COO paths use the carry pass")
-        if xwin and H == 0:
-            _coo_xwin(dm)
-        elif H == 0 and coo_tail is not False and m.nnz > 0:
-            # single pass (no carry kernel) when every row runs at most 80
-            # entries past its tile (None: where the plan allows; True: or
-            # raise); cant-like cold 18.1 vs 20.6 us for the carry pass
-            tb = hip_lib().spmv_coo_tail_bytes(m.nnz)
-            tails = torch.empty(max(tb, 4), dtype=torch.uint8, device=device)
-            rc = hip_lib().spmv_coo_tail_build(dm.dims(), _ptr(dm.arrays["row"]), _ptr(tails), tails.numel())
-            if rc == SUCCESS:
-                dm.arrays["tails"] = tails
-                dm.params["single_pass"] = 1
-            elif coo_tail:
-                raise SpmvError(rc, "spmv_coo_tail_build", hip_lib().spmv_last_error().decode())
+        _plan_coo(dm, row, col, val, xwin=xwin, coo_tail=coo_tail, hot=hot)
         return dm
     ptr, col, val = csr_from_coo(m)
     if fmt == "csr":
-        if variant == 0:  # host-side choice from the row-length skew
-            variant = host_lib().spmv_csr_pick_variant(m.n_rows, _ptr(ptr))
-        dm.params = dict(lanes=lanes, variant=variant, xwin_rows=xwin_rows)  # 0 = library picks
-        dm.arrays = dict(row_ptr=_dev_tensor(ptr, device), col=_dev_tensor(col, device),
-                         val=_dev_tensor(val, device))
-        if variant == 4:
-            # hot-column table for power-law columns (None: library rule)
-            H, hot_cols, col_hot = hot_columns(m.n_cols, col, 0 if hot is None else hot) if hot != 0 else (0, None, col)
-            dm.params["H"] = H
-            if H > 0:
-                dm.arrays["col"] = _dev_tensor(col_hot, device)
-                dm.arrays["hot"] = _dev_tensor(hot_cols, device)
-            ws = hip_lib().spmv_csr_hot_ws_bytes(m.n_rows, m.nnz, H)
-            dm.arrays["ws"] = torch.empty(ws, dtype=torch.uint8, device=device)
-            n_plan = hip_lib().spmv_csr_tiled_plan_len(m.nnz)
-            if n_plan > 0:  # tile -> first row table, built once (row_ptr only)
-                dm.arrays["own_lo"] = torch.empty(n_plan, dtype=torch.int32, device=device)
-                _check(hip_lib().spmv_csr_tiled_plan(dm.dims(), _ptr(dm.arrays["row_ptr"]), _ptr(dm.arrays["own_lo"])),
-                       "spmv_csr_tiled_plan")
-                # tiles owning more rows than their offset table (runs of
-                # empty rows): the list of their rows with entries
-                bp = csr_tiled_bigplan(m.n_rows, ptr, m.nnz) if bigplan else None
-                if bp is not None:
-                    dm.arrays["big"] = _dev_tensor(bp, device)
-                    dm.params["big_tiles"] = int(np.count_nonzero(bp[: (m.nnz + 511) // 512] >= 0))
-        elif xwin and variant in (0, 3):
-            _csr_xwin(dm)
-        dm.stored_bytes = 12 * m.nnz + 8 * (m.n_rows + 1)
+        dm.arrays = dict(row_ptr=_dev_tensor(ptr, device), col=_dev_tensor(col, device), val=_dev_tensor(val, device))
+        _plan_csr(dm, lanes=lanes, variant=variant, xwin=xwin, xwin_rows=xwin_rows, hot=hot, bigplan=bigplan)
     elif fmt == "csrf32":
         # fp32 values, fp64 products and sums (§8f row 4): the row-group x-window
         # kernel, or for skewed rows the entry-balanced one with the hot table
         v = variant or host_lib().spmv_csr_pick_variant(m.n_rows, _ptr(ptr))
-        dm.params = dict(lanes=lanes, xwin_rows=xwin_rows, variant=4 if v == 4 else 3, H=0)
+        dm.params = dict(lanes=lanes or hip_lib().spmv_csr_auto_lanes(m.n_rows, m.nnz), xwin_rows=xwin_rows,
+                         variant=4 if v == 4 else 3, H=0)
         dm.arrays = dict(row_ptr=_dev_tensor(ptr, device), col=_dev_tensor(col, device),
                          val=_dev_tensor(val.astype(np.float32), device))
         dm.stored_bytes = 8 * m.nnz + 8 * (m.n_rows + 1)
@@ -1089,12 +1014,13 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
             # escapes store more than plain CSR; reported N/A like ELL padding
             raise SpmvError(OTHER_ERROR, "csr16_build", f"{c['n_esc']} of {c['n_blocks']} 64-entry blocks "
                             f"need 32-bit escapes (> {csr16_max_escape:.0%})")
-        dm.params = dict(lanes=lanes, n_blocks=c["n_blocks"], n_esc=c["n_esc"])
+        dm.params = dict(lanes=lanes or hip_lib().spmv_csr_auto_lanes(m.n_rows, m.nnz), n_blocks=c["n_blocks"],
+                         n_esc=c["n_esc"])
         dm.arrays = dict(row_ptr=_dev_tensor(ptr, device), blk_base=_dev_tensor(c["blk_base"], device),
                          col_off=_dev_tensor(c["col_off"], device), col_esc=_dev_tensor(c["col_esc"], device),
                          val=_dev_tensor(val, device))
         dm.stored_bytes = 10 * m.nnz + 4 * c["n_blocks"] + 256 * c["n_esc"] + 8 * (m.n_rows + 1)
-        if xwin:
+        if xwin is None or xwin:
             # windows of the x-window pipeline from the int32 columns (the
             # same values), uploaded only for the build
             dm.arrays["col"] = _dev_tensor(col, device)
@@ -1107,29 +1033,21 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
         e = ell_build(m.n_rows, ptr, col, val, ki=ki, max_padding=ell_max_padding)
         dm.params = dict(K=e["K"], ld=e["ld"], ki=ki, stored=e["stored"])
         dm.arrays = dict(col=_dev_tensor(e["col"], device), val=_dev_tensor(e["val"], device))
-        dm.stored_bytes = 12 * e["stored"]
-        if xwin:
-            _ell_xwin(dm)
-    elif fmt == "sell":
+        _plan_ell(dm, xwin=xwin)
+    elif fmt in ("sell", "sell16"):
+        # sell16: SELL-C-σ with 16-bit column offsets from each workgroup's
+        # window base (§8f row 4), built by the plan on the device; refused
+        # when a window spans > 65,536 columns (R-MAT), like csr16's escapes
         ki = ki or hip_lib().spmv_sell_auto_ki(m.n_rows, C)  # 1 (σ-window kernel) or 2 (small matrices)
         s = sell_build(m.n_rows, ptr, col, val, C=C, sigma=sigma, ki=ki)
         dm.params = dict(C=C, sigma=sigma, ki=ki, n_slices=s["n_slices"], stored=s["stored"])
         dm.arrays = dict(slice_ptr=_dev_tensor(s["slice_ptr"], device), perm=_dev_tensor(s["perm"], device),
                          col=_dev_tensor(s["col"], device), val=_dev_tensor(s["val"], device))
-        dm.stored_bytes = 12 * s["stored"] + 8 * (s["n_slices"] + 1) + 4 * s["n_slices"] * C
-        if xwin:
-            _sell_xwin(dm)
-        _sell_split(dm, s["slice_ptr"], split)
-        _sell_hot(dm, s["col"][: s["stored"]], hot)
-        if sell_head is not False and xwin and dm.params.get("split_T", 0) == 0 and dm.params.get("H", 0) == 0:
-            hb = hip_lib().spmv_sell_head_bytes(s["n_slices"], C, ki)
-            if hb > 0:  # small matrix: the head copy of every wave's first slot groups
-                a = dm.arrays
-                a["head"] = torch.empty(hb, dtype=torch.uint8, device=device)
-                _check(hip_lib().spmv_sell_head_fill(dm.dims(), C, sigma, ki, s["n_slices"], _ptr(a["slice_ptr"]),
-                                                     _ptr(a["val"]), _ptr(a["col"]), _ptr(a["head"]), hb),
-                       "spmv_sell_head_fill")
-                dm.params["head_bytes"] = hb
+        if fmt == "sell":
+            _plan_sell(dm, xwin=xwin, split=split, hot=hot, head=sell_head)
+        else:
+            _plan_sell(dm, xwin=True, split=0, hot=0, head=head, index16=True)
+            del dm.arrays["col"]  # read at plan creation only: the runs read the plan's 16-bit offsets
     elif fmt == "csrg":
         # column-grouped CSR for gather-bound power-law matrices (R-MAT)
         # G = 4 measured best on the R-MAT (0.757-0.785 ms vs 0.768-0.83 at G = 8,
@@ -1147,30 +1065,6 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
             _check(hip_lib().spmv_csr_tiled_plan(pd, _ptr(dm.arrays["pair_ptr"]), _ptr(dm.arrays["own_lo"])),
                    "spmv_csr_tiled_plan")
         dm.stored_bytes = 12 * m.nnz + 10 * g["n_pairs"] + 4 * g["blk_off"].size
-    elif fmt == "sell16":
-        # SELL-C-σ with 16-bit column offsets from each workgroup's window base
-        # (§8f row 4): the SELL build, the x windows, then the device pass
-        # that rewrites col as col16; refused when a window spans > 65,536
-        # columns (R-MAT), like csr16's escape rule
-        ki = ki or hip_lib().spmv_sell_auto_ki(m.n_rows, C)
-        s = sell_build(m.n_rows, ptr, col, val, C=C, sigma=sigma, ki=ki)
-        dm.params = dict(C=C, sigma=sigma, ki=ki, n_slices=s["n_slices"], stored=s["stored"])
-        dm.arrays = dict(slice_ptr=_dev_tensor(s["slice_ptr"], device), perm=_dev_tensor(s["perm"], device),
-                         col=_dev_tensor(s["col"], device), val=_dev_tensor(s["val"], device))
-        _sell_xwin(dm)
-        a = dm.arrays
-        a["col16"] = torch.empty(max(a["col"].numel(), 2), dtype=torch.int16, device=device)
-        _check(hip_lib().spmv_sell16_fill(dm.dims(), C, sigma, s["n_slices"], _ptr(a["slice_ptr"]), _ptr(a["col"]),
-                                          _ptr(a["win"]), _ptr(a["col16"])), "spmv_sell16_fill")
-        del a["col"]
-        dm.stored_bytes = 10 * s["stored"] + 8 * (s["n_slices"] + 1) + 4 * s["n_slices"] * C
-        hb = hip_lib().spmv_sell16_head_bytes(s["n_slices"], C, ki) if head else 0
-        if hb > 0:  # small matrix: the head copy of every wave's first slot groups
-            a["head"] = torch.empty(hb, dtype=torch.uint8, device=device)
-            _check(hip_lib().spmv_sell16_head_fill(dm.dims(), C, sigma, ki, s["n_slices"], _ptr(a["slice_ptr"]),
-                                                   _ptr(a["val"]), _ptr(a["col16"]), _ptr(a["head"]), hb),
-                   "spmv_sell16_head_fill")
-            dm.params["head_bytes"] = hb
     elif fmt == "hyb":
         hb = hyb_build(m.n_rows, ptr, col, val, ki=ki or 2)
         dm.params = dict(K=hb["K"], ld=hb["ld"], ki=hb["ki"], tail_nnz=hb["tail_nnz"], stored=hb["stored"], H=0)
@@ -1200,7 +1094,7 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
                 dm.params["single_pass"] = 1
             elif coo_tail:
                 raise SpmvError(rc, "spmv_coo_tail_build (hyb tail)", hip_lib().spmv_last_error().decode())
-        if xwin and "tails" in dm.arrays and hb["stored"] > 0:
+        if (xwin is None or xwin) and "tails" in dm.arrays and hb["stored"] > 0:
             # the ELL part through the x-window ELL kernel (same bits): one
             # cant-like matrix cold, a full ELL 12.26 vs 13.36 us
             a, p = dm.arrays, dm.params
@@ -1218,10 +1112,7 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
         dm.arrays = dict(strip_ptr=_dev_tensor(c["strip_ptr"], device),
                          row_in_strip=_dev_tensor(c["row_in_strip"], device),
                          col=_dev_tensor(col, device), val=_dev_tensor(val, device))
-        dm.stored_bytes = 13 * m.nnz + 8 * (c["n_strips"] + 1)
-        _cmrs_variant(dm, c["strip_ptr"], cmrs_variant, col, hot)
-        if xwin and dm.params["variant"] == 0:
-            _cmrs_xwin(dm)
+        _plan_cmrs(dm, variant=cmrs_variant, xwin=xwin, hot=hot)
     else:
         raise SpmvError(OTHER_ERROR, "to_device", f"unknown format {fmt}")
     return dm
@@ -1232,13 +1123,12 @@ def device_build(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, ki: int =
                  cmrs_variant: int | None = None) -> DeviceMatrix:
     """Like to_device, but only the raw COO (file order) crosses PCIe: CSR,
     ELL, SELL and CMRS are built on the device by the spmv_dev_* builders
-    (SURVEY.md §8f row 2); the arrays equal the host builders'."""
+    (SURVEY.md §8f row 2); the arrays equal the host builders'.  The same C
+    plans run them."""
     torch = _torch()
     device = torch.device(device)
     if fmt not in ("csr", "ell", "sell", "cmrs"):
         raise SpmvError(OTHER_ERROR, "device_build", "format must be csr, ell, sell or cmrs")
-    if xwin is None:
-        xwin = fmt in ("csr", "csr16", "ell", "sell", "cmrs")
     lib = hip_lib()
     N, Z = m.n_rows, m.nnz
     d_row, d_col, d_val = (_dev_tensor(a, device) for a in (m.row, m.col, m.val))
@@ -1251,11 +1141,8 @@ def device_build(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, ki: int =
            "spmv_dev_csr_from_coo")
     del d_row, d_col, d_val
     if fmt == "csr":
-        dm.params = dict(lanes=lanes, variant=3, xwin_rows=0)
         dm.arrays = dict(row_ptr=ptr, col=col, val=val)
-        dm.stored_bytes = 12 * Z + 8 * (N + 1)
-        if xwin:
-            _csr_xwin(dm)
+        _plan_csr(dm, lanes=lanes, variant=3, xwin=xwin)
     elif fmt == "ell":
         ki = ki or 2
         K, ld = _c_i32(0), _c_i64(0)
@@ -1267,9 +1154,7 @@ def device_build(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, ki: int =
                "spmv_dev_ell_fill")
         dm.params = dict(K=K.value, ld=ld.value, ki=ki, stored=stored)
         dm.arrays = dict(col=ec, val=ev)
-        dm.stored_bytes = 12 * stored
-        if xwin:
-            _ell_xwin(dm)
+        _plan_ell(dm, xwin=xwin)
     elif fmt == "sell":
         ki = ki or hip_lib().spmv_sell_auto_ki(m.n_rows, C)  # as to_device
         ns = (N + C - 1) // C
@@ -1285,10 +1170,7 @@ def device_build(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, ki: int =
                                       _ptr(sc), _ptr(sv)), "spmv_dev_sell_fill")
         dm.params = dict(C=C, sigma=sigma, ki=ki, n_slices=ns, stored=stored.value)
         dm.arrays = dict(slice_ptr=sp, perm=perm, col=sc, val=sv)
-        dm.stored_bytes = 12 * stored.value + 8 * (ns + 1) + 4 * ns * C
-        if xwin:
-            _sell_xwin(dm)
-        _sell_split(dm, sp.cpu().numpy(), split)
+        _plan_sell(dm, xwin=xwin, split=split)
     else:
         ns = (N + h - 1) // h
         stp = torch.empty(ns + 1, dtype=torch.int64, device=device)
@@ -1296,10 +1178,7 @@ def device_build(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, ki: int =
         _check(lib.spmv_dev_cmrs_build(d, _ptr(ptr), h, _ptr(stp), _ptr(rin)), "spmv_dev_cmrs_build")
         dm.params = dict(h=h, n_strips=ns)
         dm.arrays = dict(strip_ptr=stp, row_in_strip=rin, col=col, val=val)
-        dm.stored_bytes = 13 * Z + 8 * (ns + 1)
-        _cmrs_variant(dm, stp.cpu().numpy(), cmrs_variant)
-        if xwin and dm.params["variant"] == 0:
-            _cmrs_xwin(dm)
+        _plan_cmrs(dm, variant=cmrs_variant, xwin=xwin)
     dm.arrays["row_ptr_csr"] = ptr
     return dm
 
@@ -1309,8 +1188,9 @@ def banded_to_device(n: int, fmt: str, device="cuda:0", row_begin: int = 0, row_
                      variant: int = 0, xwin: bool = True, xwin_rows: int = 0) -> DeviceMatrix:
     """Rows [row_begin, row_end) of the banded matrix (BASELINE.json
     configs[4]) generated directly in HBM by spmv_gen_banded_device, as CSR
-    or SELL.  Row ids are local to the shard; columns are global (x is the
-    full, replicated vector)."""
+    or SELL, run by its C plan (no hot-column table: the banded columns
+    are uniform).  Row ids are local to the shard; columns are global (x is
+    the full, replicated vector)."""
     torch = _torch()
     device = torch.device(device)
     row_end = n if row_end is None else row_end
@@ -1323,9 +1203,9 @@ def banded_to_device(n: int, fmt: str, device="cuda:0", row_begin: int = 0, row_
         val = torch.empty(16 * m, dtype=torch.float64, device=device)
         rc = hip_lib().spmv_gen_banded_device(n, seed, row_begin, row_end, 0, 0, 0, _ptr(ptr), None, _ptr(col),
                                               _ptr(val), device.index or 0, stream.cuda_stream)
-        dm.params = dict(lanes=lanes, variant=variant, xwin_rows=xwin_rows)
+        _check(rc, "spmv_gen_banded_device")
         dm.arrays = dict(row_ptr=ptr, col=col, val=val)
-        dm.stored_bytes = 12 * 16 * m + 8 * (m + 1)
+        _plan_csr(dm, lanes=lanes, variant=variant, xwin=xwin, xwin_rows=xwin_rows, hot=0)
     elif fmt == "sell":
         ns = (m + C - 1) // C
         sp = torch.empty(ns + 1, dtype=torch.int64, device=device)
@@ -1334,16 +1214,12 @@ def banded_to_device(n: int, fmt: str, device="cuda:0", row_begin: int = 0, row_
         val = torch.empty(ns * C * 16, dtype=torch.float64, device=device)
         rc = hip_lib().spmv_gen_banded_device(n, seed, row_begin, row_end, 1, C, ki, _ptr(sp), _ptr(perm),
                                               _ptr(col), _ptr(val), device.index or 0, stream.cuda_stream)
+        _check(rc, "spmv_gen_banded_device")
         dm.params = dict(C=C, sigma=sigma, ki=ki, n_slices=ns, stored=ns * C * 16)
         dm.arrays = dict(slice_ptr=sp, perm=perm, col=col, val=val)
-        dm.stored_bytes = 12 * ns * C * 16 + 8 * (ns + 1) + 4 * ns * C
+        _plan_sell(dm, xwin=xwin, split=0, hot=0)
     else:
         raise SpmvError(OTHER_ERROR, "banded_to_device", "format must be csr or sell")
-    _check(rc, "spmv_gen_banded_device")
-    if xwin and fmt == "csr":
-        _csr_xwin(dm)
-    elif xwin:
-        _sell_xwin(dm)
     return dm
 
 

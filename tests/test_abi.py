@@ -11,7 +11,7 @@ import pytest
 import spmv_amd as sa
 from conftest import REPO
 
-HEADERS = {"spmv.h": "libspmv_hip.so", "spmv_host.h": "libspmv_host.so"}
+HEADERS = {"spmv.h": "libspmv_hip.so", "spmv_ext.h": "libspmv_hip.so", "spmv_host.h": "libspmv_host.so"}
 
 
 def declared(header: str) -> set[str]:
@@ -36,6 +36,7 @@ def test_exports_every_declared_symbol(header, lib):
 
 def test_python_binding_covers_headers():
     assert declared("spmv.h") <= set(sa.HIP_SYMBOLS)
+    assert declared("spmv_ext.h") <= set(sa.HIP_SYMBOLS)
     assert declared("spmv_host.h") <= set(sa.HOST_SYMBOLS)
     sa.hip_lib()  # binds every symbol; raises if one is missing
     sa.host_lib()
@@ -89,3 +90,41 @@ def test_drivers_exit_codes_without_gpu(tmp_path):
             subprocess.run(["make", "-C", str(REPO), prog], check=True, capture_output=True)
         r = subprocess.run([str(exe)], cwd=tmp_path, capture_output=True, text=True)
         assert r.returncode == 1, (prog, r.stdout, r.stderr)
+
+
+def test_plan_opts_defaults_and_options():
+    """spmv_plan_opts_init: every switch at "the library's rule" (-1), lanes
+    0 (rule), no SELL16; the A/B switches are set and read through the C-ABI
+    (no environment reads on the launch path) and refuse unknown values."""
+    o = sa.plan_opts()
+    assert (o.variant, o.xwin, o.head, o.coo_pass, o.split, o.bigplan, o.H) == (-1,) * 7
+    assert (o.lanes, o.index16, o.xwin_rows) == (0, 0, 0)
+    lib = sa.hip_lib()
+    for name in sa.OPTIONS:
+        old = sa.get_option(name)
+        for v in (0, 1, None):
+            sa.set_option(name, v)
+            assert sa.get_option(name) == (-1 if v is None else v)
+        sa.set_option(name, old)
+    assert lib.spmv_set_option(99, 0) == sa.OTHER_ERROR and lib.spmv_get_option(99) == -2
+    assert lib.spmv_set_option(1, 2) == sa.OTHER_ERROR
+
+
+def test_plan_without_gpu_is_a_device_error():
+    """Creating a plan without a GPU reports the reference's device error
+    (1) and returns no plan; it never falls back to the CPU."""
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    lib = sa.hip_lib()
+    ptr = (ctypes.c_int64 * 3)(0, 1, 2)
+    d = sa.Dims(2, 2, 2, 0, None)
+    plan = ctypes.c_void_p()
+    o = sa.plan_opts()
+    rc = lib.spmv_plan_csr(d, ctypes.addressof(ptr), ctypes.addressof(ptr), ctypes.addressof(ptr), ctypes.byref(o),
+                           ctypes.byref(plan))
+    assert rc == sa.DEVICE_ERROR and not plan.value
+    assert lib.spmv_plan_csr(d, None, None, None, ctypes.byref(o), ctypes.byref(plan)) == sa.OTHER_ERROR
+    assert lib.spmv_plan_run(None, None, None, None) == sa.OTHER_ERROR
+    assert lib.spmv_plan_destroy(None) == sa.SUCCESS

@@ -235,19 +235,23 @@ def test_csr16_bit_identical_to_csr(torch_dev, case):
 
 @pytest.mark.parametrize("fmt,kw", [("csr", {"variant": 3}), ("csr", {"variant": 3, "xwin": True}), ("csr", {"variant": 2}),
                                     ("sell", {"ki": 1}), ("sell", {"ki": 2}), ("ell", {"ki": 1}), ("ell", {"ki": 2})])
-def test_stream_load_policy_same_bits(torch_dev, monkeypatch, fmt, kw):
-    """SPMV_STREAM_NT only changes the cache policy of the matrix loads."""
+def test_stream_load_policy_same_bits(torch_dev, fmt, kw):
+    """The stream_nt switch (spmv_set_option) only changes the cache policy
+    of the matrix loads."""
     torch, dev = torch_dev
     m = sa.gen_cantlike(0, copies=2)
     x = torch.from_numpy(np.random.default_rng(3).uniform(-1, 1, m.n_cols)).to(dev)
     dm = sa.to_device(m, fmt, dev, **kw)
     out = []
-    for nt in ("0", "1"):
-        monkeypatch.setenv("SPMV_STREAM_NT", nt)
-        y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
-        dm.run(x, y)
-        torch.cuda.synchronize()
-        out.append(y)
+    try:
+        for nt in (0, 1):
+            sa.set_option("stream_nt", nt)
+            y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
+            dm.run(x, y)
+            torch.cuda.synchronize()
+            out.append(y)
+    finally:
+        sa.set_option("stream_nt", None)
     assert torch.equal(out[0].view(torch.int64), out[1].view(torch.int64))
     assert_parity(m, out[1].cpu().numpy(), x.cpu().numpy())
 
@@ -290,6 +294,60 @@ def test_linearity_and_checksum_full_rmat(torch_dev, rmat_full, fmt):
     y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
     dm.run(torch.from_numpy(x).to(dev), y)
     assert_parity(m, y.cpu().numpy(), x, y_ref=y_ref)
+
+
+@pytest.fixture(scope="module")
+def rmat_bench_layout(rmat_full):
+    """bench.py's configs[3] layout, built by bench's own code
+    (bench.rmat_layout: columns relabelled by degree, ties by first row,
+    rows in new-column order, x' = x[order]) as the whole-matrix shard
+    bench.rmat_strong / rmat_per_format run (rows in CSR order)."""
+    import argparse
+
+    import bench
+
+    m, x, y_ref = rmat_full
+    ptr, col, val = sa.csr_from_coo(m)
+    args = argparse.Namespace(relabel="yes", relabel_ties="first", format="csr", lanes=0, variant=0, ki=0, C=64,
+                              sigma=0, h=8, workload="cant")
+    col2, xh, hot, _, order = bench.rmat_layout(args, m.n_rows, ptr, col, val)
+    loc = sa.Coo(m.n_rows, m.n_cols, np.repeat(np.arange(m.n_rows, dtype=np.int32), np.diff(ptr)), col2, val)
+    return args, loc, xh, hot, order
+
+
+@pytest.mark.parametrize("fmt", sa.ALL_FORMATS)
+def test_rmat_bench_layout_every_format(torch_dev, rmat_full, rmat_bench_layout, fmt):
+    """configs[3] at full size (1e7 rows, 1e8 entries) in
+    exactly the layout and with exactly the to_device keywords bench.py
+    times (bench.rmat_fmt_kwargs), every format, against the oracle's
+    file-order sum of the ORIGINAL matrix on the ORIGINAL x (the relabel and
+    the row sort change the summation order: the parity rule, not bits).
+    ELL, CSR16 and SELL16 are refused (padding / 16-bit windows), as the
+    bench reports them N/A; csrf32 is checked against the oracle on its
+    fp32-rounded values."""
+    import bench
+
+    torch, dev = torch_dev
+    m, x, y_ref = rmat_full
+    args, loc, xh, hot, order = rmat_bench_layout
+    assert np.array_equal(xh, x[order])
+    kw = bench.rmat_fmt_kwargs(args, fmt, hot)
+    if fmt in ("ell", "csr16", "sell16"):
+        with pytest.raises(sa.SpmvError):
+            sa.to_device(loc, fmt, dev, **kw)
+        return
+    dm = sa.to_device(loc, fmt, dev, **kw)
+    y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
+    dm.run(torch.from_numpy(xh).to(dev), y)
+    torch.cuda.synchronize()
+    if fmt == "csrf32":
+        v32 = m.val.astype(np.float32).astype(np.float64)
+        assert_parity(sa.Coo(m.n_rows, m.n_cols, m.row, m.col, v32), y.cpu().numpy(), x,
+                      y_ref=oracle.file_order_spmv(m.n_rows, m.row, m.col, v32, x))
+    else:
+        assert_parity(m, y.cpu().numpy(), x, y_ref=y_ref)
+    if fmt == "csr":  # the kernel bench's rmat_strong reports
+        assert dm.kernel == "csr_tiled_kernel" and dm.params["H"] == 0 and dm.params["big_tiles"] > 0
 
 
 def test_banded_shard_full_parity(torch_dev):
@@ -470,7 +528,7 @@ def test_sell16_bit_identical_to_sell(torch_dev, case, ki):
         dm.run(x, y)
         ys.append(y)
         if fmt == "sell16":
-            assert "col" not in dm.arrays and dm.arrays["col16"].dtype == torch.int16
+            assert "col" not in dm.arrays and dm.params["index16"] == 1
             assert dm.stored_bytes < 12 * dm.params["stored"]
     torch.cuda.synchronize()
     assert torch.equal(ys[0].view(torch.int64), ys[1].view(torch.int64))
@@ -500,7 +558,7 @@ def test_sell16_refuses_wide_windows(torch_dev):
     m = sa.gen_rmat(200_000, 2_000_000, scale=18, seed=3)
     with pytest.raises(sa.SpmvError, match="65,536"):
         sa.to_device(m, "sell16", dev, C=64, sigma=1024)
-    with pytest.raises(sa.SpmvError, match="C must be 64"):
+    with pytest.raises(sa.SpmvError, match="needs C = 64"):
         sa.to_device(sa.gen_cantlike(0), "sell16", dev, C=32, sigma=1024)
 
 
@@ -570,7 +628,7 @@ def test_coo_cmrs_xwin_bit_identical(torch_dev, case, fmt, kw):
         a = sa.to_device(m, fmt, dev, xwin=True, **kw)
         extra = {"coo_tail": False} if fmt == "coo" else {}  # the carry path: the same tiles and sums
         b = sa.to_device(m, fmt, dev, xwin=False, **kw, **extra)
-        assert "win" in a.arrays and "win" not in b.arrays
+        assert a.params["xwin"] and not b.params["xwin"]
         if case == "cantlike":
             assert a.params["xcap"] > 0
         x = torch.from_numpy(np.random.default_rng(4).uniform(-1, 1, m.n_cols)).to(dev)
@@ -600,8 +658,9 @@ def test_csr_hot_bit_identical(torch_dev, H):
     b.run(x, yb)
     # and without the build-once tile plan (the per-run pre-pass)
     bb = b.arrays
+    ws = torch.empty(sa.hip_lib().spmv_csr_tiled_ws_bytes(m.n_rows, m.nnz), dtype=torch.uint8, device=dev)
     rc = sa.hip_lib().spmv_csr_run_tiled(b.dims(), sa._ptr(bb["row_ptr"]), sa._ptr(bb["col"]), sa._ptr(bb["val"]),
-                                         sa._ptr(x), sa._ptr(yc), sa._ptr(bb["ws"]), bb["ws"].numel())
+                                         sa._ptr(x), sa._ptr(yc), sa._ptr(ws), ws.numel())
     assert rc == 0
     torch.cuda.synchronize()
     assert torch.equal(ya.view(torch.int64), yb.view(torch.int64))
@@ -663,7 +722,7 @@ def test_csr_tiled_empty_row_runs(torch_dev, H, bigplan):
     mc = sa.Coo(4 * rows.size, m.n_cols, inv[m.row], m.col, m.val)
     x = torch.from_numpy(np.random.default_rng(3).uniform(-1, 1, m.n_cols)).to(dev)
     a = sa.to_device(m, "csr", dev, variant=4, hot=H, bigplan=bigplan)
-    assert ("big" in a.arrays) == bigplan and (not bigplan or a.params["big_tiles"] > 10)
+    assert (a.params["big_tiles"] > 0) == bigplan and (not bigplan or a.params["big_tiles"] > 10)
     c = sa.to_device(mc, "csr", dev, variant=4, hot=H)
     ya = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
     yc = torch.full((mc.n_rows,), float("nan"), dtype=torch.float64, device=dev)
@@ -672,9 +731,9 @@ def test_csr_tiled_empty_row_runs(torch_dev, H, bigplan):
     yp = torch.full_like(ya, float("nan"))
     if H == 0:  # and without the build-once tile plan
         aa = a.arrays
+        ws = torch.empty(sa.hip_lib().spmv_csr_tiled_ws_bytes(m.n_rows, m.nnz), dtype=torch.uint8, device=dev)
         rc = sa.hip_lib().spmv_csr_run_tiled(a.dims(), sa._ptr(aa["row_ptr"]), sa._ptr(aa["col"]),
-                                             sa._ptr(aa["val"]), sa._ptr(x), sa._ptr(yp), sa._ptr(aa["ws"]),
-                                             aa["ws"].numel())
+                                             sa._ptr(aa["val"]), sa._ptr(x), sa._ptr(yp), sa._ptr(ws), ws.numel())
         assert rc == 0
     torch.cuda.synchronize()
     idx = torch.from_numpy(rows.astype(np.int64)).to(dev)
@@ -712,7 +771,7 @@ def test_coo_cmrs_hot_bit_identical(torch_dev, fmt, kw, H):
     assert_parity(m, ya.cpu().numpy(), x.cpu().numpy())
     if fmt == "coo":  # and the plain COO's carry pass: same tiles, same bits
         c = sa.to_device(m, fmt, dev, hot=0, **kw)
-        assert "tails" not in c.arrays  # R-MAT rows run past 80 entries: the carry pass
+        assert not c.params["single_pass"]  # R-MAT rows run past 80 entries: the carry pass
         yc = torch.full_like(ya, float("nan"))
         c.run(x, yc)
         torch.cuda.synchronize()
@@ -896,7 +955,7 @@ def test_sell16_head_same_bits(torch_dev, ki, case):
     ys = []
     for head in (False, True):
         dm = sa.to_device(m, "sell16", dev, C=64, sigma=1024, ki=ki, head=head)
-        assert ("head" in dm.arrays) == head
+        assert bool(dm.params["head"]) == head
         y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
         dm.run(x, y)
         torch.cuda.synchronize()
@@ -923,7 +982,7 @@ def test_sell_int32_head_same_bits(torch_dev, ki, case):
     ys = []
     for head in (False, True):
         dm = sa.to_device(m, "sell", dev, C=64, sigma=1024, ki=ki, sell_head=head)
-        assert ("head" in dm.arrays) == head
+        assert bool(dm.params["head"]) == head
         y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
         dm.run(x, y)
         torch.cuda.synchronize()
@@ -994,9 +1053,9 @@ def test_coo_single_pass(torch_dev, case):
         fits = 0 < longest <= COO_TAIL_CAP + 1 or case == "aligned"
         a = sa.to_device(m, "coo", dev)  # default: single pass where the plan allows
         if fits:
-            assert "tails" in a.arrays, m.label
+            assert a.params["single_pass"], m.label
         b = sa.to_device(m, "coo", dev, coo_tail=False)  # the carry pass
-        assert "tails" not in b.arrays
+        assert not b.params["single_pass"]
         x = torch.from_numpy(rng.uniform(-1, 1, max(m.n_cols, 1))).to(dev)
         ya = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
         ya2, yb = torch.full_like(ya, float("nan")), torch.full_like(ya, float("nan"))
@@ -1080,7 +1139,7 @@ def test_coo_single_pass_empty_row_run_search_path(torch_dev):
     assert m.nnz / m.n_rows >= 12
     a = sa.to_device(m, "coo", dev, coo_tail=True, hot=0)
     b = sa.to_device(m, "coo", dev, coo_tail=False, hot=0)
-    assert "tails" in a.arrays and "tails" not in b.arrays
+    assert a.params["single_pass"] and not b.params["single_pass"]
     x = torch.from_numpy(rng.uniform(-1, 1, m.n_cols)).to(dev)
     ya, yb = (torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev) for _ in range(2))
     a.run(x, ya)
@@ -1112,7 +1171,7 @@ def test_coo_single_pass_refuses_long_rows(torch_dev):
     m = sa.Coo(lens.size, 2000, row, rng.integers(0, 2000, row.size).astype(np.int32), rng.uniform(-1, 1, row.size),
                False, "long")
     dm = sa.to_device(m, "coo", dev)
-    assert "tails" not in dm.arrays
+    assert not dm.params["single_pass"]
     with pytest.raises(sa.SpmvError):
         sa.to_device(m, "coo", dev, coo_tail=True)
     x = torch.from_numpy(rng.uniform(-1, 1, m.n_cols)).to(dev)
@@ -1157,7 +1216,7 @@ def test_csr_tiled_bigplan_rmat_same_bits(torch_dev):
     x = torch.from_numpy(xh).to(dev)
     a = sa.to_device(m, "csr", dev, variant=4, hot=0)
     b = sa.to_device(m, "csr", dev, variant=4, hot=0, bigplan=False)
-    assert "big" in a.arrays and a.params["big_tiles"] > 0 and "big" not in b.arrays
+    assert a.params["big_tiles"] > 0 and b.params["big_tiles"] == 0
     ya, yb = (torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev) for _ in range(2))
     a.run(x, ya)
     b.run(x, yb)

@@ -524,6 +524,103 @@ def test_column_relabel_bad_input():
         sa.column_relabel(5, ok, "degree")
 
 
+def _ref_sort_rows(ptr, col, val):
+    """numpy model of spmv_csr_sort_rows: each row's entries by column,
+    equal columns in their original order (a stable sort)."""
+    c2, v2 = col.copy(), val.copy()
+    for r in range(ptr.size - 1):
+        a, b = int(ptr[r]), int(ptr[r + 1])
+        o = np.argsort(col[a:b], kind="stable")
+        c2[a:b], v2[a:b] = col[a:b][o], val[a:b][o]
+    return c2, v2
+
+
+@pytest.mark.parametrize("kind", ["duplicates", "empty_rows", "long_rows", "rmat_small"])
+def test_csr_sort_rows(kind):
+    """spmv_csr_sort_rows (bench.py's R-MAT layout): every
+    row's entries by increasing column, in place; the (col, val) pairs stay
+    together; equal columns (duplicate entries) keep their file order, which
+    the merge path (rows >= 32 entries) must preserve as well as the
+    insertion path; empty rows and row_ptr are untouched."""
+    rng = np.random.default_rng(17)
+    if kind == "duplicates":  # short rows, many equal columns: insertion sort path
+        lens = rng.integers(0, 20, 300)
+        cols = [rng.integers(0, 6, n) for n in lens]
+    elif kind == "empty_rows":
+        lens = np.where(rng.random(500) < 0.6, 0, rng.integers(1, 50, 500))
+        cols = [rng.integers(0, 1000, n) for n in lens]
+    elif kind == "long_rows":  # merge sort path, with duplicates across the halves
+        lens = np.array([0, 31, 32, 33, 64, 1000, 4097, 1])
+        cols = [rng.integers(0, max(n // 3, 1), n) for n in lens]
+    else:
+        m = sa.gen_rmat(50_000, 500_000, scale=16, seed=8)
+        ptr, col, val = sa.csr_from_coo(m)
+        lens, cols = None, None
+    if lens is not None:
+        ptr = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+        col = np.concatenate([np.asarray(c, np.int32) for c in cols] + [np.zeros(0, np.int32)]).astype(np.int32)
+        val = rng.uniform(-1, 1, col.size)  # distinct values: the pairing and the stability are visible
+    want_c, want_v = _ref_sort_rows(ptr, col, val)
+    ptr0 = ptr.copy()
+    c, v = col.copy(), val.copy()
+    sa.csr_sort_rows(ptr.size - 1, ptr, c, v)
+    assert np.array_equal(ptr, ptr0)
+    assert np.array_equal(c, want_c)
+    assert np.array_equal(v.view(np.int64), want_v.view(np.int64))
+    # every row now ascending, and the multiset of (col, val) pairs per row kept
+    for r in rng.integers(0, ptr.size - 1, 50):
+        a, b = int(ptr[r]), int(ptr[r + 1])
+        assert np.all(np.diff(c[a:b]) >= 0)
+        assert sorted(zip(col[a:b].tolist(), val[a:b].tolist())) == sorted(zip(c[a:b].tolist(), v[a:b].tolist()))
+
+
+def test_csr_sort_rows_bad_arguments():
+    lib = sa.host_lib()
+    ptr = np.array([0, 2, 3], np.int64)
+    col = np.array([1, 0, 2], np.int32)
+    val = np.ones(3)
+    assert lib.spmv_csr_sort_rows(-1, ptr.ctypes.data, col.ctypes.data, val.ctypes.data) == sa.OTHER_ERROR
+    assert lib.spmv_csr_sort_rows(2, None, col.ctypes.data, val.ctypes.data) == sa.OTHER_ERROR
+    assert lib.spmv_csr_sort_rows(2, ptr.ctypes.data, None, val.ctypes.data) == sa.OTHER_ERROR
+    assert lib.spmv_csr_sort_rows(2, ptr.ctypes.data, col.ctypes.data, None) == sa.OTHER_ERROR
+    dec = np.array([0, 3, 2], np.int64)  # decreasing offsets: a negative row length
+    assert lib.spmv_csr_sort_rows(2, dec.ctypes.data, col.ctypes.data, val.ctypes.data) == sa.OTHER_ERROR
+    assert np.array_equal(col, [1, 0, 2])  # refused calls write nothing
+    empty = np.zeros(1, np.int64)
+    assert lib.spmv_csr_sort_rows(0, empty.ctypes.data, None, None) == sa.SUCCESS
+    with pytest.raises(sa.SpmvError):
+        sa.csr_sort_rows(2, dec, col, val)
+
+
+@pytest.mark.parametrize("ties", ["first", "id"])
+def test_rmat_bench_layout_same_y(ties):
+    """bench.py's R-MAT layout (column_relabel + csr_sort_rows, rmat_layout)
+    on a small R-MAT: the relabelled, row-sorted CSR on x[order] gives the
+    original matrix's y within the parity rule (the sort changes each row's
+    summation order, so not bit for bit), and the CPU CSR loop over it too."""
+    import bench
+
+    m = sa.gen_rmat(100_000, 1_000_000, scale=17, seed=2)
+    ptr, col, val = sa.csr_from_coo(m)
+    args = type("A", (), {"relabel": "yes", "relabel_ties": ties})()
+    col2, xh, hot, layout, order2 = bench.rmat_layout(args, m.n_rows, ptr, col, val)
+    assert hot == 0 and "relabelled" in layout
+    order, newid, _ = sa.column_relabel(m.n_cols, sa.csr_from_coo(m)[1], ties)
+    assert np.array_equal(order2, order) and np.array_equal(xh, sa.ramp_x(m.n_cols)[order])
+    for r in range(0, m.n_rows, 997):
+        a, b = int(ptr[r]), int(ptr[r + 1])
+        assert np.all(np.diff(col2[a:b]) >= 0)
+    rows = np.repeat(np.arange(m.n_rows, dtype=np.int32), np.diff(ptr))
+    x0 = sa.ramp_x(m.n_cols)
+    y_ref = oracle.file_order_spmv(m.n_rows, m.row, m.col, m.val, x0)
+    y = oracle.file_order_spmv(m.n_rows, rows, col2, val, xh)
+    assert oracle.parity(y, y_ref, m.row, m.col, m.val, x0, m.n_rows).size == 0
+    yc = np.empty(m.n_rows)
+    assert sa.host_lib().spmv_cpu_csr(m.n_rows, ptr.ctypes.data, col2.ctypes.data, val.ctypes.data,
+                                      xh.ctypes.data, yc.ctypes.data, 0) == sa.SUCCESS
+    assert oracle.parity(yc, y_ref, m.row, m.col, m.val, x0, m.n_rows).size == 0
+
+
 def _rmat_like_ptr(n=200_000, seed=3):
     rng = np.random.default_rng(seed)
     lens = (rng.pareto(1.2, n) * 3).astype(np.int64)

@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
-"""Interleaved A/B of library knobs that are read on every call (SPMV_*
-environment variables) on ONE device matrix built once.
+"""Interleaved A/B of the library's switches (spmv_set_option: xwin_remap,
+xcd_remap, stream_nt; placement and load policy, never a result bit) on
+ONE device matrix built once, and of to_device keywords (one matrix each).
 
-    python tools/ab_env.py --format csr --env SPMV_CSR_XWIN_MODE=0,1,2 [--kw JSON ...] [--rounds 5]
+    python tools/ab_env.py --format csr --opt xwin_remap=0,1 [--kw JSON ...] [--rounds 5]
 
 Every configuration runs `--reps` back-to-back launches per round (HIP events
 on the launch stream), configurations interleaved round by round in one
@@ -14,7 +15,6 @@ from __future__ import annotations
 import argparse
 import itertools
 import json
-import os
 import sys
 from pathlib import Path
 
@@ -31,7 +31,8 @@ def main():
     ap.add_argument("--matrix", default="cantlike", choices=["cantlike", "rmat", "banded"])
     ap.add_argument("--banded-rows", type=int, default=20_000_000, help="banded: rows (16 entries each)")
     ap.add_argument("--copies", type=int, default=32)
-    ap.add_argument("--env", action="append", default=[], help="KEY=v1,v2 (several: cartesian product)")
+    ap.add_argument("--opt", action="append", default=[],
+                    help="NAME=v1,v2 of spmv_amd.OPTIONS, -1 = default (several: cartesian product)")
     ap.add_argument("--kw", action="append", default=[],
                     help="to_device keyword arguments (JSON; several: one device matrix each, crossed with --env)")
     ap.add_argument("--rounds", type=int, default=5)
@@ -52,7 +53,7 @@ def main():
         m = sa.gen_cantlike(0, a.copies) if a.matrix == "cantlike" else sa.gen_rmat()
         b = sa.bytes_alg(m.n_rows, m.n_cols, m.nnz)
     keys, vals = [], []
-    for e in a.env:
+    for e in a.opt:
         k, v = e.split("=", 1)
         keys.append(k)
         vals.append(v.split(","))
@@ -74,8 +75,8 @@ def main():
     for _ in range(a.rounds):
         for i, (di, env) in enumerate(configs):
             dm = dms[di]
-            saved = {k: os.environ.get(k) for k in env}
-            os.environ.update(env)
+            for k, v in env.items():
+                sa.set_option(k, int(v))
             for _ in range(5):
                 dm.run(x, y, s)
             if a.total and a.graph:
@@ -113,11 +114,8 @@ def main():
                 y0 = y.clone()
             elif not torch.equal(y.view(torch.int64), y0.view(torch.int64)):
                 same[i] = False
-            for k, v in saved.items():
-                if v is None:
-                    os.environ.pop(k, None)
-                else:
-                    os.environ[k] = v
+            for k in env:
+                sa.set_option(k, None)
     for i, (di, env) in enumerate(configs):
         ms = float(np.median(res[i]))
         print(json.dumps(dict(fmt=a.format, kw=kws[di], env=env, ms=round(ms, 5), GBs_alg=round(b / ms * 1e-6, 1),

@@ -28,7 +28,6 @@ from __future__ import annotations
 import argparse
 import ctypes
 import json
-import os
 import sys
 from pathlib import Path
 
@@ -52,8 +51,9 @@ def probe_lib():
     lib.spmv_probe_tag.argtypes = [ctypes.c_int, vp]
     lib.spmv_probe_csr_stream.argtypes = [vp, vp, ctypes.c_int64, ctypes.c_int, vp, vp]
     lib.spmv_probe_flush_read.argtypes = [vp, ctypes.c_size_t, vp, vp]
+    lib.spmv_probe_gather_stream.argtypes = [vp, vp, ctypes.c_int64, vp, vp, vp]
     for f in (lib.spmv_probe_stream, lib.spmv_probe_flush, lib.spmv_probe_tag, lib.spmv_probe_csr_stream,
-              lib.spmv_probe_flush_read):
+              lib.spmv_probe_flush_read, lib.spmv_probe_gather_stream):
         f.restype = ctypes.c_int
     return lib
 
@@ -65,8 +65,8 @@ def main():
     ap.add_argument("--formats", default=",".join(sa.ALL_FORMATS))
     ap.add_argument("--extra", action="append", default=[], metavar='FMT@JSON',
                     help='another run of FMT with to_device kwargs, e.g. csr@{"xwin_rows": 64}; '
-                         '"_params" overrides run parameters after the build, e.g. sell16@{"_params": {"xcap": 0}}; '
-                         '"_env" sets library environment switches for that run only')
+                         '"_opt" sets library switches (spmv_set_option) for that run only, e.g. '
+                         'sell@{"_opt": {"xwin_remap": 0}}')
     ap.add_argument("--flush-mode", default="write", choices=["write", "read"],
                     help="cold state: 512 MiB WRITTEN before each launch (default; the caches hold dirty lines) "
                          "or READ (clean lines)")
@@ -126,31 +126,12 @@ def main():
     for i, (label, fmt, kw) in enumerate(formats):
         tag(SETUP_TAG + i)  # builds, fills and the first run land in an ignored phase
         kw = dict(kw)
-        over = kw.pop("_params", {})  # run-parameter overrides after the build, e.g. {"xcap": 0}
-        env = kw.pop("_env", {})  # library environment switches for this run only (A/B of placement / order)
-        saved = {k: os.environ.get(k) for k in env}
-        os.environ.update({k: str(v) for k, v in env.items()})
-        # "_gap_kib": re-place the matrix arrays in ONE allocation, in the
-        # order built, each at a 2 MiB boundary plus this gap after the
-        # previous one (placement A/B: same bits)
-        gap = kw.pop("_gap_kib", None)
+        # "_opt": the library's A/B switches for this run only (spmv_set_option:
+        # placement / load policy, never a result bit), e.g. {"xwin_remap": 0}
+        opt = kw.pop("_opt", {})
+        for k, v in opt.items():
+            sa.set_option(k, v)
         dm = sa.to_device(m, fmt, dev, **kw)
-        dm.params.update(over)
-        if gap is not None:
-            names = [k for k in ("row_ptr", "row", "col", "val") if k in dm.arrays]
-            sizes = [dm.arrays[k].numel() * dm.arrays[k].element_size() for k in names]
-            al = 2 << 20
-            offs, o = [], 0
-            for b in sizes:
-                offs.append(o)
-                o = (o + b + al - 1) // al * al + int(gap) * 1024
-            pool = torch.empty(o + al, dtype=torch.uint8, device=dev)
-            dm._pool = pool
-            for k, off, b in zip(names, offs, sizes):
-                t = dm.arrays[k]
-                view = pool[off:off + b].view(t.dtype)
-                view.copy_(t.reshape(-1))
-                dm.arrays[k] = view
         y = torch.full((m.n_rows,), float("nan"), dtype=torch.float64, device=dev)
         dm.run(x, y)
         torch.cuda.synchronize()
@@ -184,11 +165,8 @@ def main():
             out["formats"][label]["parity"] = "within fp32-value tolerance (values rounded to fp32)"
         out["phases"][label] = [2 * i, 2 * i + 1]
         del dm
-        for k, v in saved.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+        for k in opt:
+            sa.set_option(k, None)
     # the CSR arrays streamed without the kernels' structure (val + col pairs)
     if a.csr_probes:
         _, ccol, cval = sa.csr_from_coo(m)

@@ -8,7 +8,9 @@
 //     the 256 MiB Infinity Cache (evicts it and the L2s: "cold");
 //   * spmv_probe_tag: an empty dispatch whose grid size (id + 1 workgroups)
 //     marks a phase boundary in a rocprofv3 kernel trace, so a trace can be
-//     cut into per-format segments without device timestamps.
+//     cut into per-format segments without device timestamps;
+//   * spmv_probe_gather_stream: the gather ceiling of a column sequence
+//     (values + columns streamed, x gathered, no row structure).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -171,6 +173,44 @@ __global__ __launch_bounds__(512) void probe_layout_kernel(const v2f64 *__restri
         out[blockIdx.x] = s;
 }
 
+// The gather ceiling of a matrix's column sequence (bench.py
+// rmat_per_format): the CSR-shaped stream of probe_csr_stream_kernel<3>
+// (16-byte value pairs + 8-byte column pairs, non-temporal, 3 pairs per lane
+// in flight) plus the gathers x[col] of every entry in entry order, summed
+// per lane — an SpMV's loads and products without any row structure (no
+// row offsets, reductions or y).  Timed on the R-MAT's own (relabelled,
+// row-sorted) col / val / x', it prices the access pattern itself.
+__global__ __launch_bounds__(kBlock) void probe_gather_stream_kernel(const v2f64 *__restrict__ val,
+                                                                     const int2 *__restrict__ col, int64_t npairs,
+                                                                     const double *__restrict__ x,
+                                                                     double *__restrict__ out)
+{
+    typedef int v2i32 __attribute__((ext_vector_type(2)));
+    constexpr int R = 3;
+    const int64_t base = (int64_t)blockIdx.x * kBlock * R + threadIdx.x;
+    v2f64 v[R];
+    v2i32 c[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+        const int64_t i = base + (int64_t)k * kBlock;
+        const int64_t q = i < npairs ? i : npairs - 1;
+        v[k] = __builtin_nontemporal_load(val + q);
+        c[k] = __builtin_nontemporal_load(reinterpret_cast<const v2i32 *>(col) + q);
+    }
+    double xv[2 * R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+        xv[2 * k] = x[c[k].x];
+        xv[2 * k + 1] = x[c[k].y];
+    }
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < R; ++k)
+        s += v[k].x * xv[2 * k] + v[k].y * xv[2 * k + 1];
+    if (s == 1.2345e-300)
+        out[blockIdx.x] = s;
+}
+
 __global__ __launch_bounds__(kBlock) void probe_flush_kernel(uint4 *__restrict__ p, int64_t n16, uint32_t tick)
 {
     for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n16; i += (int64_t)gridDim.x * kBlock)
@@ -266,6 +306,19 @@ int spmv_probe_csr_stream(const void *val, const void *col, int64_t npairs, int 
     else
         hipLaunchKernelGGL(probe_csr_stream_kernel<1>, dim3((unsigned)blocks), dim3(kBlock), 0, (hipStream_t)stream,
                            (const v2f64 *)val, (const int2 *)col, npairs, out);
+    return (int)hipGetLastError();
+}
+
+// the gather ceiling: 2·npairs entries of val / col (entry order) with
+// their x gathers; returns a hipError_t
+int spmv_probe_gather_stream(const void *val, const void *col, int64_t npairs, const double *x, double *out,
+                             void *stream)
+{
+    if (npairs <= 0)
+        return (int)hipErrorInvalidValue;
+    const int64_t blocks = (npairs + kBlock * 3 - 1) / (kBlock * 3);
+    hipLaunchKernelGGL(probe_gather_stream_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, (hipStream_t)stream,
+                       (const v2f64 *)val, (const int2 *)col, npairs, x, out);
     return (int)hipGetLastError();
 }
 

@@ -38,7 +38,7 @@ def main():
     ptr, col, val = sa.csr_from_coo(full)
     n, z = full.n_rows, full.nnz
     del full
-    col, xh, _, _ = bench.rmat_layout(bargs, n, ptr, col, val)
+    col, xh, _, _, _ = bench.rmat_layout(bargs, n, ptr, col, val)
     m = sa.Coo(n, n, np.repeat(np.arange(n, dtype=np.int32), np.diff(ptr)), col, val)
     x = torch.from_numpy(xh).to(dev)
     y = torch.empty(n, dtype=torch.float64, device=dev)

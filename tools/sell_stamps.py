@@ -2,15 +2,16 @@
 """sell_stamps — where the small-matrix SELL (or the CSR x-window) kernel's time goes, per wave.
 
 Lab only.  Runs the library's SELL (int32, head copy) and SELL16 on one
-cant-like matrix with a lab build of libspmv_hip.so compiled with
--DSPMV_SELL_STAMPS (lab/build_variant.sh stamps "-DSPMV_SELL_STAMPS";
+cant-like matrix with the stamps_sell lab build of libspmv_hip.so
+(tools/build_variant.sh stamps_sell, which injects tools/lab_stamps_sell.h;
 SPMV_HIP_LIB points at it), cold (512 MiB read before each launch) and warm,
 and reads the per-wave s_memrealtime stamps (100 MHz, 10 ns) that build
 writes at: 0 start, 1 x window published (barrier), 2 first batch summed,
 3 all batches summed, 4 partial sums published (barrier), 5 y stored.
 Prints medians over launches of the kernel span and of each phase's
 distribution over the waves (p10 / p50 / p90 / max, us).  --kernel csr: the
-CSR x-window kernel of a -DSPMV_CSR_STAMPS build (0 start, 1 window and
+CSR x-window kernel of the stamps_csr lab build (tools/build_variant.sh
+stamps_csr) (0 start, 1 window and
 offsets published, 2 chunk 0's products in LDS, 3 its barrier, 4 its row
 sums read, 5 its second barrier, 6 / 7 chunks 1 / 2's products in LDS)."""
 from __future__ import annotations
@@ -47,7 +48,7 @@ def main():
     if a.kernel == "csr":
         return csr_main(a)
     if not os.environ.get("SPMV_HIP_LIB"):
-        sys.exit("set SPMV_HIP_LIB to a -DSPMV_SELL_STAMPS build")
+        sys.exit("set SPMV_HIP_LIB to a stamps_sell lab build")
     import torch
 
     dev = torch.device("cuda:0")

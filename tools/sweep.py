@@ -11,7 +11,6 @@ from __future__ import annotations
 
 import argparse
 import json
-import os
 import sys
 from pathlib import Path
 
@@ -41,12 +40,12 @@ VARIANTS = [
     ("csr", {"variant": 4, "hot": 0, "env": {}}),
     ("csr", {"variant": 4, "hot": 1 << 18, "env": {}}),
     ("csr", {"variant": 4, "hot": 1 << 20, "env": {}}),
-    ("csr", {"variant": 4, "env": {"SPMV_STREAM_NT": "0"}}),
+    ("csr", {"variant": 4, "env": {"stream_nt": 0}}),
     ("coo", {"xwin": True, "env": {}}),
-    ("csr", {"env": {"SPMV_XWIN_REMAP": "1"}}),
-    ("csr", {"env": {"SPMV_XWIN_REMAP": "0"}}),
-    ("sell", {"env": {"SPMV_XWIN_REMAP": "1"}}),
-    ("sell", {"env": {"SPMV_XWIN_REMAP": "0"}}),
+    ("csr", {"env": {"xwin_remap": 1}}),
+    ("csr", {"env": {"xwin_remap": 0}}),
+    ("sell", {"env": {"xwin_remap": 1}}),
+    ("sell", {"env": {"xwin_remap": 0}}),
     ("sell", {"C": 64, "sigma": 65536, "ki": 1, "env": {}}),
     ("sell", {"C": 64, "sigma": 1 << 20, "ki": 1, "env": {}}),
     ("sell", {"C": 64, "sigma": 1 << 24, "ki": 1, "env": {}}),
@@ -80,9 +79,9 @@ def main():
     for r in range(a.rounds):
         for i, (fmt, kw) in enumerate(variants):
             kw = dict(kw)
-            env = kw.pop("env", {})
-            saved = {k: os.environ.get(k) for k in env}
-            os.environ.update(env)
+            env = kw.pop("env", {})  # spmv_set_option switches for this variant
+            for k, v in env.items():
+                sa.set_option(k, v)
             dm = sa.to_device(m, fmt, dev, **kw)
             stored[i] = dm.stored_bytes
             s = torch.cuda.current_stream()
@@ -97,11 +96,8 @@ def main():
             res[i].append(float(np.mean([ev[k].elapsed_time(ev[k + 1]) for k in range(a.reps)])))
             del dm
             torch.cuda.empty_cache()
-            for k, v in saved.items():
-                if v is None:
-                    os.environ.pop(k, None)
-                else:
-                    os.environ[k] = v
+            for k in env:
+                sa.set_option(k, None)
     out = []
     for i, (fmt, kw) in enumerate(variants):
         ms = float(np.median(res[i]))
@@ -111,7 +107,7 @@ def main():
         out.append(row)
         print(json.dumps(row), flush=True)
     print(json.dumps({"matrix": a.matrix, "copies": a.copies, "bytes_alg": b,
-                      "xcd_remap": os.environ.get("SPMV_XCD_REMAP", "1")}))
+                      "xcd_remap": sa.get_option("xcd_remap")}))
 
 
 if __name__ == "__main__":

@@ -400,11 +400,16 @@ int spmv_gather(int64_t n, const int32_t *order, const double *x, double *out, i
 /* ---------------------------------------------------------- switches ---
  * Placement and load-policy switches for A/B runs; each changes speed,
  * never a result bit (tests/test_gpu_parity.py checks that).  The library
- * reads SPMV_XWIN_REMAP, SPMV_XCD_REMAP and SPMV_STREAM_NT once, when it
- * is loaded, as their initial values; spmv_set_option changes them for
+ * reads SPMV_XWIN_REMAP, SPMV_XCD_REMAP, SPMV_STREAM_NT and
+ * SPMV_CSR_PREFETCH once, when it is loaded, as their initial values; spmv_set_option changes them for
  * the whole process (value -1 = each kernel's measured default, 0 off,
  * 1 on).  Nothing reads the environment on the launch path.             */
-enum spmv_option { SPMV_OPT_XWIN_REMAP = 1, SPMV_OPT_XCD_REMAP = 2, SPMV_OPT_STREAM_NT = 3 };
+enum spmv_option {
+    SPMV_OPT_XWIN_REMAP = 1,  /* XCD-contiguous x-window workgroups        */
+    SPMV_OPT_XCD_REMAP = 2,   /* XCD-contiguous global-gather workgroups   */
+    SPMV_OPT_STREAM_NT = 3,   /* non-temporal matrix loads                 */
+    SPMV_OPT_CSR_PREFETCH = 4 /* CSR x-window: first chunk in the prologue */
+};
 int spmv_set_option(int option, int value);
 int spmv_get_option(int option);
 

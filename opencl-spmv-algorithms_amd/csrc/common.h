@@ -39,6 +39,8 @@ bool xcd_remap_enabled();
 // XCD-contiguous window placement of the x-window kernels; `dflt` = each
 // kernel's measured best.
 bool xwin_remap(bool dflt);
+// CSR x-window kernel: the first chunk prefetched in the prologue (MODE 4)
+bool csr_prefetch(bool dflt);
 // small-matrix SELL geometry (sell.hip): C = 64 and fewer than 14 slices per CU
 bool sell_small(int32_t C, int64_t n_slices);
 

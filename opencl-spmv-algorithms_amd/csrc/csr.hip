@@ -230,6 +230,23 @@ struct StreamRegs {
     typename Cols::Raw c[R];
     int64_t q[R];  // the pair each lane loaded (decode needs it for escaped blocks only)
 
+    // issue() for an array known to hold at least 2 entries: branch-free, so
+    // a caller may issue it inside straight-line code whose later waits must
+    // leave these loads in flight (a branch around loads makes the compiler's
+    // wait counts conservative at the join: vmcnt(0) for everything)
+    __device__ __forceinline__ void issue_nz2(int64_t cb, int64_t ce, int64_t nz, const Cols &cols,
+                                              const V *__restrict__ val)
+    {
+        const int64_t spare = cb + 1 < nz ? cb : (nz - 2) & ~(int64_t)1;  // this chunk's first pair
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const int64_t p = cb + 2 * (int64_t)(threadIdx.x + k * kBlock);
+            q[k] = (p < ce && p + 1 < nz) ? p : spare;
+            v[k] = vpair<NT>(val + q[k]);
+            c[k] = cols.raw(q[k]);
+        }
+    }
+
     __device__ __forceinline__ void issue(int64_t cb, int64_t ce, int64_t nz, const Cols &cols,
                                           const V *__restrict__ val)
     {
@@ -290,11 +307,15 @@ struct StreamRegs {
     do {             \
     } while (0)
 #endif
+// st: the chunk loads in flight; prefetched = the caller already issued
+// group 0's first chunk into st (csr_xwin_kernel MODE 4), so the first issue
+// here is skipped (the same chunk, the same bits).
 template <int L, int R, bool NT, typename XS, typename V, typename Cols = Col32<NT>>
 __device__ __forceinline__ void staged_window_pipelined(int64_t row0, int ngroups, const int64_t *s_off,
                                                         double2 *s_prod, const Cols cols,
                                                         const V *__restrict__ val, const XS xs,
-                                                        double *__restrict__ y, int64_t n_rows, int64_t nz)
+                                                        double *__restrict__ y, int64_t n_rows, int64_t nz,
+                                                        StreamRegs<R, NT, V, Cols> &st, bool prefetched)
 {
     constexpr int RPB = kBlock / L;
     constexpr int CH = 2 * kBlock * R;
@@ -309,9 +330,8 @@ __device__ __forceinline__ void staged_window_pipelined(int64_t row0, int ngroup
             ++j;
         return j;
     };
-    StreamRegs<R, NT, V, Cols> st;
     int jn = next_group(0);
-    if (jn < ngroups) {
+    if (jn < ngroups && !prefetched) {
         const int64_t b = chunk_start(s_off[jn * RPB]), e = s_off[(jn + 1) * RPB];
         st.issue(b, b + CH < e ? b + CH : e, nz, cols, val);
     }
@@ -448,7 +468,12 @@ __global__ __launch_bounds__(kBlock) void csr_window_kernel(int64_t n_rows, int6
 //       x range) and its x range loaded together, 8 loads in flight per
 //       thread, before ONE barrier; the chunks software-pipelined: the next
 //       chunk's loads are issued before the current chunk's barrier and
-//       reduction (staged_window_pipelined).
+//       reduction (staged_window_pipelined);
+//   4 = MODE 3 with the window's first chunk also issued in the prologue,
+//       right behind the x-range and offset loads, from two scalar loads of
+//       its bounds: its HBM round trip overlaps the window's instead of
+//       following the window barrier (a small grid, all windows resident:
+//       the per-window chain is the kernel's time).
 // (Modes 1/2/4/5-7, a prefetched first chunk, a persistent streaming kernel
 // with an x ring and a per-entry-range flat schedule were measured slower
 // or equal and removed: profiles/round2/ab_csr_xwin*.log, ab_csr_flat.log,
@@ -460,11 +485,11 @@ __global__ __launch_bounds__(kBlock) void csr_xwin_kernel(
     const double *__restrict__ x, double *__restrict__ y, const int2 *__restrict__ win, int32_t xcap,
     int remap)
 {
-    static_assert(MODE == 0 || MODE == 3, "csr_xwin_kernel: MODE 0 or 3");
+    static_assert(MODE == 0 || MODE == 3 || MODE == 4, "csr_xwin_kernel: MODE 0, 3 or 4");
     CSR_STAMP(0);
     constexpr int RPB = kBlock / L;
     extern __shared__ double s_x[];
-    __shared__ int64_t s_ptr[MODE == 3 ? 1 : RPB + 1];
+    __shared__ int64_t s_ptr[MODE >= 3 ? 1 : RPB + 1];
     __shared__ double2 s_prod[kBlock * R];
     int64_t *s_off = reinterpret_cast<int64_t *>(s_x + xcap);  // MODE 3: the window's offsets
     const int64_t nz = row_ptr[n_rows];
@@ -473,13 +498,30 @@ __global__ __launch_bounds__(kBlock) void csr_xwin_kernel(
     const int64_t wi = xcd_block(remap);
     const int64_t g_beg = wi * gpw;
     const int64_t g_end = (wi + 1) * gpw < n_groups ? (wi + 1) * gpw : n_groups;
+    // MODE 4: group 0's bounds, uniform addresses (scalar loads, their own
+    // counter), requested together with the window bounds and pinned by the
+    // empty asm (a scheduling boundary) so that ONE scalar round trip
+    // precedes every vector load
+    int64_t pb = 0, pe = 0, b0 = 0;
+    if constexpr (MODE == 4) {
+        const int64_t r0p = g_beg * RPB;
+        const int64_t r1 = r0p + RPB < n_rows ? r0p + RPB : n_rows;
+        b0 = row_ptr[r0p];
+        pe = row_ptr[r1];
+    }
     const int2 wnd = win[wi];
+    if constexpr (MODE == 4) {
+        asm volatile("" ::"s"(b0), "s"(pe), "s"(wnd.x), "s"(wnd.y), "s"(nz));
+        pb = chunk_start(b0);
+    }
     const int32_t span = wnd.y - wnd.x + 1;
     const bool staged = span > 0 && span <= xcap;  // uniform per workgroup
-    if constexpr (MODE == 3) {
+    if constexpr (MODE >= 3) {
         // offsets r0 .. r0 + nr of the window's rows (clamped past n_rows),
         // then the x range: every load issued before the stores
         const int64_t r0 = g_beg * RPB;
+        StreamRegs<R, NT, V, Cols> st;
+        bool pre = MODE == 4 && pb < pe;  // group 0 has a chunk (next_group(0) == 0)
         const int32_t nr = (int32_t)((g_end - g_beg) * RPB) + 1;
         constexpr int U = 2;  // offsets per thread per pass (nr <= U·256 in one pass)
         constexpr int XU = 8;  // window entries per thread (copy_window's default)
@@ -500,6 +542,18 @@ __global__ __launch_bounds__(kBlock) void csr_xwin_kernel(
                 const int32_t i = (int32_t)threadIdx.x + k * kBlock;
                 xv[k] = x[wnd.x + (i < xl ? i : xl)];
             }
+            // MODE 4: the first chunk behind them (loads return in order:
+            // storing the offsets and the window waits for those only).
+            // Unconditional (an empty group 0 loads its spare pair, then the
+            // pipeline issues its real first chunk); the launcher picks MODE
+            // 4 only for nnz >= 2
+            if constexpr (MODE == 4) {
+                st.issue_nz2(pb, pre ? (pb + 2 * kBlock * R < pe ? pb + 2 * kBlock * R : pe) : pb, nz, cols, val);
+                // the offsets' loads stay here, ahead of the chunk's (the
+                // compiler otherwise sinks o[0] into its conditional store,
+                // behind every load of the prologue, and waits for all)
+                asm volatile("" ::"v"(o[0]), "v"(o[1]));
+            }
 #pragma unroll
             for (int k = 0; k < U; ++k) {
                 const int32_t i = (int32_t)threadIdx.x + k * kBlock;
@@ -514,7 +568,8 @@ __global__ __launch_bounds__(kBlock) void csr_xwin_kernel(
                         s_x[i] = xv[k];
                 }
             }
-        } else
+        } else {
+        pre = false;  // a window too big for the one-pass prologue: issued after the barrier
         for (int32_t b = 0; b < nr; b += U * kBlock) {
             int64_t o[U];
 #pragma unroll
@@ -531,14 +586,15 @@ __global__ __launch_bounds__(kBlock) void csr_xwin_kernel(
                     s_off[i] = o[k];
             }
         }
+        }
         __syncthreads();  // window and offsets visible
         CSR_STAMP(1);
         if (staged)
             staged_window_pipelined<L, R, NT, XWindow, V, Cols>(r0, (int)(g_end - g_beg), s_off, s_prod, cols, val,
-                                                               XWindow{s_x, wnd.x}, y, n_rows, nz);
+                                                               XWindow{s_x, wnd.x}, y, n_rows, nz, st, pre);
         else
             staged_window_pipelined<L, R, NT, XGlobal, V, Cols>(r0, (int)(g_end - g_beg), s_off, s_prod, cols, val,
-                                                               XGlobal{x}, y, n_rows, nz);
+                                                               XGlobal{x}, y, n_rows, nz, st, pre);
         return;
     }
     if (staged)
@@ -761,7 +817,19 @@ static bool csr_xwin_remap_rule(int32_t xcap, int64_t rows_per_window, int64_t n
 // row offsets behind it
 static size_t csr_xwin_lds(int mode, int32_t xcap, int64_t gpw, int rpb)
 {
-    return ((size_t)xcap + (mode == 3 ? (size_t)(gpw * rpb + 1) : 0)) * sizeof(double);
+    return ((size_t)xcap + (mode >= 3 ? (size_t)(gpw * rpb + 1) : 0)) * sizeof(double);
+}
+
+// MODE 4 (the first chunk prefetched in the prologue, behind the x window's
+// and offsets' loads) is opt-in: on one cant-like matrix (976 windows of 64
+// rows, all resident at once) it measured 15.6 us cold against MODE 3's
+// 14.8 us (profiles/round6/csr_prefetch_ab.md) — its 90 VGPRs cost a wave per
+// SIMD and the barrier already waits on the x window's HBM round trip.
+// SPMV_OPT_CSR_PREFETCH (spmv_set_option) = 1 selects it (same bits).
+static bool csr_xwin_prefetch_rule(int64_t n_windows)
+{
+    (void)n_windows;
+    return csr_prefetch(false);
 }
 
 // rows per x window: a multiple of the row group (256/L rows), default
@@ -809,7 +877,10 @@ static void launch_csr_xwin(const spmv_dims &d, const int64_t *row_ptr, const Co
         return;
     const int remap = csr_xwin_remap_rule(xcap, gpw * RPB, n_win) ? 1 : 0;
     const hipStream_t st = (hipStream_t)d.stream;
-    if (mode == 3)
+    if (mode == 3 && d.nnz >= 2 && csr_xwin_prefetch_rule(n_win))
+        hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, V, 4, Cols>), dim3((unsigned)n_win), dim3(kBlock), lds, st,
+                           d.n_rows, groups, gpw, row_ptr, cols, val, x, y, win, xcap, remap);
+    else if (mode == 3)
         hipLaunchKernelGGL((csr_xwin_kernel<L, R, NT, V, 3, Cols>), dim3((unsigned)n_win), dim3(kBlock), lds, st,
                            d.n_rows, groups, gpw, row_ptr, cols, val, x, y, win, xcap, remap);
     else

@@ -62,6 +62,7 @@ static int env_switch(const char *name)
 static std::atomic<int> g_opt_xwin_remap{env_switch("SPMV_XWIN_REMAP")};
 static std::atomic<int> g_opt_xcd_remap{env_switch("SPMV_XCD_REMAP")};
 static std::atomic<int> g_opt_stream_nt{env_switch("SPMV_STREAM_NT")};
+static std::atomic<int> g_opt_csr_prefetch{env_switch("SPMV_CSR_PREFETCH")};
 
 static std::atomic<int> *option_slot(int option)
 {
@@ -72,6 +73,8 @@ static std::atomic<int> *option_slot(int option)
         return &g_opt_xcd_remap;
     case SPMV_OPT_STREAM_NT:
         return &g_opt_stream_nt;
+    case SPMV_OPT_CSR_PREFETCH:
+        return &g_opt_csr_prefetch;
     default:
         return nullptr;
     }
@@ -87,6 +90,12 @@ bool xwin_remap(bool dflt)
 // measured 1-2 % faster than the contiguous-per-XCD remap
 // (profiles/round1/sweeps.md).
 bool xcd_remap_enabled() { return g_opt_xcd_remap.load(std::memory_order_relaxed) == 1; }
+
+bool csr_prefetch(bool dflt)
+{
+    const int v = g_opt_csr_prefetch.load(std::memory_order_relaxed);
+    return v < 0 ? dflt : v == 1;
+}
 
 bool stream_nt(bool dflt)
 {

@@ -845,7 +845,7 @@ class DeviceMatrix:
 
 
 # the library's A/B switches (include/spmv_ext.h; placement and load policy only)
-OPTIONS = {"xwin_remap": 1, "xcd_remap": 2, "stream_nt": 3}
+OPTIONS = {"xwin_remap": 1, "xcd_remap": 2, "stream_nt": 3, "csr_prefetch": 4}
 
 
 def set_option(name: str, value: int | None) -> None:

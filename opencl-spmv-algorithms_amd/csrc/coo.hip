@@ -10,8 +10,9 @@
 //           it; a row that began in an EARLIER tile is not stored: its
 //           partial sum goes to carry[tile].
 //   pass 2  coo_carry_kernel (here): one thread per tile; the first tile of
-//           every run of carries for the same row adds the run, in tile
-//           order, to y[row].
+//           every run of carries for the same row adds the run to y[row] —
+//           in tile order for a run of <= 8 tiles, lane-strided over the
+//           wave plus the butterfly for a longer one (a fixed order).
 // No atomics, every y element written by exactly one pass-1 store (plus at
 // most one pass-2 update): results are bitwise reproducible.
 //

@@ -329,21 +329,21 @@ __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
         static_assert(TP <= kBlock, "one tail pair per thread");
         double2 tv = {0.0, 0.0};
         int2 tc = {0, 0}, tk = {0, 0};
-        // a pair, or the lone last entry: its pair is (p - 1, p) when p is
-        // the array's last entry (nnz >= 2 here; used in the products below)
+        // a pair, or the lone last entry p = nnz - 1 (nnz odd): element
+        // loads, so the lone entry is read on its own, aligned, instead of
+        // as an odd pair (p - 1, p) (the tail is < kCooTailCap
+        // entries per tile, the extra instructions are a few per thread)
         const bool tsh = p + 1 >= nnz;
         if (tpair || tone) {  // ONE branch: with two, a merge made the waves wait for the tile's loads first
-            const int64_t q = tsh ? nnz - 2 : p;
-            tv = stream_load2<NT>(val + q);
-            tc = stream_load2<NT>(col + q);
-            tk = stream_load2<NT>(row + q);
+            const int64_t q1 = tsh ? p : p + 1;
+            tv = double2{stream_load<NT>(val + p), stream_load<NT>(val + q1)};
+            tc = int2{stream_load<NT>(col + p), stream_load<NT>(col + q1)};
+            tk = int2{stream_load<NT>(row + p), stream_load<NT>(row + q1)};
         }
         st.commit(t0, t1, nnz, col, val, xs, s_prod, keys);
         if (tpair || tone) {
-            const double v0 = tsh ? tv.y : tv.x;
-            const int32_t c0 = tsh ? tc.y : tc.x;
-            s_prod[n / 2 + j] = tpair ? double2{tv.x * xs(tc.x), tv.y * xs(tc.y)} : double2{v0 * xs(c0), 0.0};
-            s_row2[n / 2 + j] = tsh ? make_int2(tk.y, tk.y) : tk;  // (.y of a lone entry is never read)
+            s_prod[n / 2 + j] = tpair ? double2{tv.x * xs(tc.x), tv.y * xs(tc.y)} : double2{tv.x * xs(tc.x), 0.0};
+            s_row2[n / 2 + j] = tsh ? make_int2(tk.x, tk.x) : tk;  // (.y of a lone entry is never read)
         }
     } else if (staged) {
         stage_chunk<R, NT>(t0, t1, nnz, col, val, XWindow{s_x, wlo}, s_prod, keys);
@@ -702,7 +702,9 @@ __global__ __launch_bounds__(kBlock) void csr_tiled_kernel(
 // from its part of the strip.  The strip running into a tile from an
 // earlier one leaves up to h partial rows: carry[k·tiles + tile] for row
 // key k (k-major, so each row's continuation tiles are consecutive and
-// coo_carry_kernel adds them in tile order).  Needs kBlock / L >= h.
+// coo_carry_kernel adds them: a run of <= 8 tiles in tile order by one
+// thread, a longer run lane-strided over a wave and then the butterfly —
+// a fixed order either way, so bitwise reproducible).  Needs kBlock / L >= h.
 template <int L, int R, typename XS>
 __global__ __launch_bounds__(kBlock) void cmrs_tiled_kernel(
     int64_t n_rows, int32_t h, int64_t n_strips, int64_t nnz, int64_t tiles,

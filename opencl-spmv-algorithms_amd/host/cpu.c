@@ -92,9 +92,13 @@ int spmv_cpu_cmrs(int64_t n_rows, int32_t h, int64_t n_strips,
                   const int32_t *col, const double *val, const double *x,
                   double *y, int threads)
 {
+    if (h < 1 || h > 64) /* the format's strip height (host/formats.c builds 1..64) */
+        return SPMV_OTHER_ERROR;
 #pragma omp parallel for num_threads(nthreads(threads)) schedule(static)
     for (int64_t s = 0; s < n_strips; ++s) {
-        double acc[64];
+        /* one slot per uint8 row tag: a tag >= h (a malformed strip) lands
+         * in a slot that is never stored instead of past the array */
+        double acc[256];
         for (int r = 0; r < h; ++r)
             acc[r] = 0.0;
         for (int64_t j = strip_ptr[s]; j < strip_ptr[s + 1]; ++j)

@@ -1019,7 +1019,7 @@ def test_sell16_head_same_bits_nonfinite_x(torch_dev, ki):
 COO_TAIL_CAP = 80  # csrc/staged.hip kCooTailCap
 
 
-@pytest.mark.parametrize("case", ["cantlike", "ragged_tails", "aligned", "fixtures", "batch"])
+@pytest.mark.parametrize("case", ["cantlike", "ragged_tails", "aligned", "odd_tail", "fixtures", "batch"])
 def test_coo_single_pass(torch_dev, case):
     """The single-pass COO (the default where the plan allows) matches the oracle
     (parity rule) and the carry path within it wherever every row ends
@@ -1042,6 +1042,20 @@ def test_coo_single_pass(torch_dev, case):
         row = np.repeat(np.arange(lens.size, dtype=np.int32), lens)
         ms = [sa.Coo(lens.size, 3000, row, rng.integers(0, 3000, row.size).astype(np.int32),
                      rng.uniform(-1, 1, row.size), False, "aligned")]
+    elif case == "odd_tail":
+        # odd nnz, the last row 30 entries before a tile end and 31 past it:
+        # its tail ends on the lone entry nnz - 1 (once loaded as
+        # the odd pair (nnz - 2, nnz - 1)).  One matrix per candidate tile size.
+        ms = []
+        for ch in (1024, 1536, 2048, 3072, 4096):
+            lead = rng.integers(1, 40, ch)
+            lead = lead[np.cumsum(lead) <= ch - 30]
+            lead[-1] += ch - 30 - int(lead.sum())
+            lens = np.append(lead, 61)
+            row = np.repeat(np.arange(lens.size, dtype=np.int32), lens)
+            assert row.size % 2 == 1
+            ms.append(sa.Coo(lens.size, 500, row, rng.integers(0, 500, row.size).astype(np.int32),
+                             rng.uniform(-1, 1, row.size), False, f"odd_tail_{ch}"))
     else:
         ms = [sa.read_mtx(GOLDEN / f"{c}.mtx") for c in CASES]
     for m in ms:

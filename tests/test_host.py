@@ -592,6 +592,22 @@ def test_csr_sort_rows_bad_arguments():
         sa.csr_sort_rows(2, dec, col, val)
 
 
+@pytest.mark.parametrize("h", [0, -1, 65])
+def test_cpu_cmrs_refuses_strip_heights(h):
+    """spmv_cpu_cmrs keeps per-strip sums in a fixed array: a strip height
+    outside 1..64 (the builder's range) is refused, y untouched."""
+    lib = sa.host_lib()
+    sp = np.array([0, 1], np.int64)
+    tag = np.zeros(1, np.uint8)
+    col = np.zeros(1, np.int32)
+    val = np.ones(1)
+    x = np.ones(1)
+    y = np.full(1, 7.0)
+    rc = lib.spmv_cpu_cmrs(1, h, 1, sp.ctypes.data, tag.ctypes.data, col.ctypes.data, val.ctypes.data,
+                           x.ctypes.data, y.ctypes.data, 1)
+    assert rc == sa.OTHER_ERROR and y[0] == 7.0
+
+
 @pytest.mark.parametrize("ties", ["first", "id"])
 def test_rmat_bench_layout_same_y(ties):
     """bench.py's R-MAT layout (column_relabel + csr_sort_rows, rmat_layout)

@@ -491,10 +491,10 @@ constexpr int kTiledBigRowCap = 65536;
 // (A fused carry — the last-arriving tile of a spanning row finishing it —
 // was bit-identical but slower: 0.890 vs 0.856 ms on R-MAT with the
 // partials passed through RMW atomics, 5.9 ms with agent-scope
-// release/acquire; removed, DESIGN.md §6.  A persistent form with the
+// release/acquire; removed, profiles/HISTORY.md §H6.  A persistent form with the
 // hottest 16 K table entries in LDS, one 1024-thread workgroup per CU:
 // bit-identical, 2.21 vs 0.83 ms — four tiles in flight per CU instead of
-// eight; removed)
+// eight; removed, profiles/HISTORY.md §H9.)
 //
 // Load order: a tile's dependent round trips are the latency the grid
 // waits out.  The value/column pairs need the tile index only, so they are

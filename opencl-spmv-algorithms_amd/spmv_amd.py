@@ -1096,7 +1096,7 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
                 raise SpmvError(rc, "spmv_coo_tail_build (hyb tail)", hip_lib().spmv_last_error().decode())
         if (xwin is None or xwin) and "tails" in dm.arrays and hb["stored"] > 0:
             # the ELL part through the x-window ELL kernel (same bits): one
-            # cant-like matrix cold, a full ELL 12.26 vs 13.36 us
+            # cant-like matrix cold, a full ELL 12.26 vs 13.36 us (profiles/HISTORY.md §H9)
             a, p = dm.arrays, dm.params
             nbytes = hip_lib().spmv_ell_xwin_bytes(dm.n_rows)
             a["win"] = torch.empty(max(nbytes, 8), dtype=torch.uint8, device=device)

@@ -610,9 +610,10 @@ def single_cold(args, torch, dev, rank, world, dist, cdev, prof, fmt=None):
     sell): ONE cant-like matrix on this rank's GPU, cold.  A step = 512 MiB
     flush + one SpMV launch.  W untimed warm-up steps; then the K steps are
     captured in one HIP graph, replayed once untimed, and replayed once
-    between barrier + synchronize on both sides (the timed region); then a
-    graph of K flushes alone is timed the same way, so the in-process cold
-    SpMV time is (span(K x (flush + SpMV)) - span(K x flush)) / K, max over
+    between barrier + synchronize on both sides (the timed region); a graph
+    of K flushes alone is timed the same way right before and right after it,
+    so the in-process cold SpMV time is
+    (span(K x (flush + SpMV)) - mean span(K x flush)) / K, max over
     ranks: the headline.  The rocprofv3 trace median and mean of the same
     kernel cold (`prof`, this rank's cant_single child) go beside it.
     fmt: the format (default --format; "sell" for the sell_single record,
@@ -679,8 +680,14 @@ def single_cold(args, torch, dev, rank, world, dist, cdev, prof, fmt=None):
         step()
     torch.cuda.synchronize()
     K = args.steps
+    # the flush-only graph is timed right before AND right after the timed
+    # region and the two spans averaged, so a drift of the flush's own time
+    # over the run (clocks, power) cancels instead of landing on the SpMV:
+    # 1 % of the ~95 us flush is ~1 us, a tenth of the SpMV
+    _, span_flush0 = spans(flush, K)
     wall, span_both = spans(step, K)
-    _, span_flush = spans(flush, K)
+    _, span_flush1 = spans(flush, K)
+    span_flush = 0.5 * (span_flush0 + span_flush1)
     inproc = max((span_both - span_flush) / K, 1e-6)
     # the other cold state beside it (not the headline; not in --profile runs,
     # whose PMC passes average every launch of the kernel)
@@ -728,6 +735,8 @@ def single_cold(args, torch, dev, rank, world, dist, cdev, prof, fmt=None):
                                      + " between barrier + synchronize",
                              "wall_ms": round(wall * 1e3, 4), "wall_ms_per_step_incl_flush": round(wall_step, 5),
                              "cold_spmv_ms_in_process": round(cold_ms, 5),
+                             "flush_only_ms_per_step_before_after": [round(span_flush0 / K, 5),
+                                                                     round(span_flush1 / K, 5)],
                              "cold_flush": f"{args.cold_flush}: 512 MiB " +
                                            ("written" if args.cold_flush == "write" else "read") +
                                            " before every SpMV (evicts the Infinity Cache and the L2s)",

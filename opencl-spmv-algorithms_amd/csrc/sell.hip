@@ -318,7 +318,10 @@ constexpr int kSellSmallS = SPMV_SELL_SMALL_S;  // sell_small_kernel: waves per 
 #define SPMV_SELL_SMALL_P 4
 #endif
 constexpr int kSellSmallP = SPMV_SELL_SMALL_P;  // sell_small_kernel: slices per workgroup (and per x window)
-constexpr int kSellXCopy = 4;  // sell_small_kernel: waves that copy the x window (HEAD)
+#ifndef SPMV_SELL_XCOPY  // A/B builds only
+#define SPMV_SELL_XCOPY 4
+#endif
+constexpr int kSellXCopy = SPMV_SELL_XCOPY;  // sell_small_kernel: waves that copy the x window (HEAD)
 #ifndef SPMV_SELL_LAST_B  // A/B builds only
 #define SPMV_SELL_LAST_B 8
 #endif
@@ -577,9 +580,21 @@ __global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell_small_
     if constexpr (XWIN) {
         wnd = win[bid];
         const int32_t span = wnd.y - wnd.x + 1;
-        staged = span > 0 && span <= xcap;  // uniform per workgroup
-        if (staged && !xdone)
-            copy_window<kWave * S * P, 4>(s_x, x, wnd.x, span);
+        if constexpr (HEAD && !c16) {
+            // int32 with a head: only windows the first waves copied are
+            // staged; a wider one gathers from global memory (same x values,
+            // same bits).  The fallback copy loop joined the straight-line
+            // path and made the compiler wait for every head load before the
+            // barrier (vmcnt(0): a register of the loop's loads is reused
+            // below).  Without it, one cant-like matrix cold: 13.55 -> 13.30
+            // us (events); SELL16 measured the other way (12.56 -> 12.78 us)
+            // and keeps the loop (profiles/round6/ab_sell_variants.md).
+            staged = xdone;
+        } else {
+            staged = span > 0 && span <= xcap;  // uniform per workgroup
+            if (staged && !xdone)
+                copy_window<kWave * S * P, 4>(s_x, x, wnd.x, span);
+        }
         __syncthreads();
     }
     SELL_STAMP(1);
@@ -588,6 +603,9 @@ __global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell_small_
     // cold, with the scalar bounds (profiles/round5/ab_sell_pipe.md): SELL
     // 10.80 -> 10.28 us, SELL16 9.70 -> 9.55; keeping two batches in flight
     // throughout, or issuing batch 1 before the window barrier, was slower.
+    // (Round 6: every group after the head in ONE batch here — 8 or 16
+    // groups, branch-free — measured slower: 13.80 / 14.36 vs 13.30 us cold,
+    // profiles/round6/ab_sell_variants.md.)
     SlotBatch<KI, NT, 4> nb;
     if (g0 + G < g1)  // uniform per wave
         nb.load(vp, cp, g0 + G, g1, step);

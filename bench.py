@@ -82,6 +82,7 @@ CSR_DEFAULT_VARIANT = 3  # spmv_csr_run_variant's default (csrc/csr.hip)
 # than later ones (headline 0.2659 vs per-format 0.2557 ms
 # for the same kernel in the same process)
 WARM_REPLAY_MS = 100.0
+INPROC_REPS = 5  # timed regions per in-process cold figure (their median is reported)
 
 
 def parse():
@@ -613,7 +614,8 @@ def single_cold(args, torch, dev, rank, world, dist, cdev, prof, fmt=None):
     between barrier + synchronize on both sides (the timed region); a graph
     of K flushes alone is timed the same way right before and right after it,
     so the in-process cold SpMV time is
-    (span(K x (flush + SpMV)) - mean span(K x flush)) / K, max over
+    (span(K x (flush + SpMV)) - mean span(K x flush)) / K; the region is
+    replayed INPROC_REPS times (F B F B ... F) and the median taken, max over
     ranks: the headline.  The rocprofv3 trace median and mean of the same
     kernel cold (`prof`, this rank's cant_single child) go beside it.
     fmt: the format (default --format; "sell" for the sell_single record,
@@ -652,50 +654,64 @@ def single_cold(args, torch, dev, rank, world, dist, cdev, prof, fmt=None):
         flush()
         dm.run(x, y)
 
-    def spans(fn, k):
-        """(wall s, GPU span ms) of k calls of fn between barriers."""
+    def timed(fn, k):
+        """fn's k calls as one graph (None: eager) and a timer: each call of the
+        timer replays it once between barrier + synchronize, returning (wall s,
+        GPU span ms on the launch stream)."""
         g = capture(torch, fn, k) if GRAPH["on"] else None
         if g is not None:
             g.replay()
             torch.cuda.synchronize()
-        a, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        a.record(stream)
-        if g is not None:
-            g.replay()
-        else:
-            for _ in range(k):
-                fn()
-        e.record(stream)
-        torch.cuda.synchronize()
-        if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize()
-        return time.perf_counter() - t0, a.elapsed_time(e)
+
+        def run():
+            a, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            if dist is not None:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            a.record(stream)
+            if g is not None:
+                g.replay()
+            else:
+                for _ in range(k):
+                    fn()
+            e.record(stream)
+            torch.cuda.synchronize()
+            if dist is not None:
+                dist.barrier()
+            torch.cuda.synchronize()
+            return time.perf_counter() - t0, a.elapsed_time(e)
+        return run
+
+    def inprocess(both_fn, flush_fn, k, reps):
+        """Cold SpMV time from `reps` timed regions of k x (flush + SpMV), each
+        between two replays of k flushes alone (F B F B ... F): per region
+        (span_B - mean of its two F spans) / k, and the median of those.  One
+        difference alone moved +-0.5 us between repeats on the same arrays
+        (1 % of the ~95 us flush is ~1 us; tools/inproc_noise.py,
+        profiles/round6/inproc_noise.md); the median of 5 interleaved ones is
+        what the line reports, every difference beside it."""
+        tb, tf = timed(both_fn, k), timed(flush_fn, k)
+        f = [tf()[1]]
+        walls, diffs = [], []
+        for _ in range(reps):
+            w, b_ = tb()
+            f.append(tf()[1])
+            walls.append(w)
+            diffs.append((b_ - 0.5 * (f[-2] + f[-1])) / k)
+        return walls[0], max(float(np.median(diffs)), 1e-6), diffs, [v / k for v in f]
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     K = args.steps
-    # the flush-only graph is timed right before AND right after the timed
-    # region and the two spans averaged, so a drift of the flush's own time
-    # over the run (clocks, power) cancels instead of landing on the SpMV:
-    # 1 % of the ~95 us flush is ~1 us, a tenth of the SpMV
-    _, span_flush0 = spans(flush, K)
-    wall, span_both = spans(step, K)
-    _, span_flush1 = spans(flush, K)
-    span_flush = 0.5 * (span_flush0 + span_flush1)
-    inproc = max((span_both - span_flush) / K, 1e-6)
+    reps = 1 if args.profile else INPROC_REPS
+    wall, inproc, diffs, flush_spans = inprocess(step, flush, K, reps)
     # the other cold state beside it (not the headline; not in --profile runs,
     # whose PMC passes average every launch of the kernel)
     inproc_other = None
     if not args.profile:
-        _, sb2 = spans(lambda: (other(), dm.run(x, y)), K)
-        _, sf2 = spans(other, K)
-        inproc_other = max((sb2 - sf2) / K, 1e-6)
+        _, inproc_other, _, _ = inprocess(lambda: (other(), dm.run(x, y)), other, K, reps)
     bad, first = sa.check(m, xh, y.cpu().numpy())
     all_ok(dist, cdev, torch, bad == 0, f"cant-like single matrix, row {first}", rank)
 
@@ -732,11 +748,14 @@ def single_cold(args, torch, dev, rank, world, dist, cdev, prof, fmt=None):
             "trace": corr,
             "timed_region": {"what": f"{K} x (512 MiB flush + one SpMV), "
                                      + ("one HIP graph replay" if GRAPH["on"] else "eager launches")
-                                     + " between barrier + synchronize",
+                                     + " between barrier + synchronize"
+                                     + (f"; {reps} such regions, interleaved with flush-only ones" if reps > 1 else ""),
                              "wall_ms": round(wall * 1e3, 4), "wall_ms_per_step_incl_flush": round(wall_step, 5),
                              "cold_spmv_ms_in_process": round(cold_ms, 5),
-                             "flush_only_ms_per_step_before_after": [round(span_flush0 / K, 5),
-                                                                     round(span_flush1 / K, 5)],
+                             "in_process_estimator": f"median of {reps} timed regions, each minus the mean of "
+                                                     "the flush-only spans before and after it",
+                             "cold_spmv_ms_each_region": [round(v, 5) for v in diffs],
+                             "flush_only_ms_per_step": [round(v, 5) for v in flush_spans],
                              "cold_flush": f"{args.cold_flush}: 512 MiB " +
                                            ("written" if args.cold_flush == "write" else "read") +
                                            " before every SpMV (evicts the Infinity Cache and the L2s)",

@@ -529,12 +529,16 @@ __global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell_small_
     // SELL16 9.56 -> 9.38 us, SELL 10.33 -> 10.28 (profiles/round5/ab_sell_pipe.md).
     constexpr int XT = kWave * kSellXCopy, XU = 2048 / XT;
     bool xdone = false;
+    // (Round 6: the other waves' heads issued before the window bounds
+    // arrive, instead of after them, measured 11.5 vs 10.85 us in-process:
+    // the x window's loads then queue behind them.)
     if constexpr (HEAD && XWIN) {
+        const int64_t hw = bid * (S * P) + wv;
+        const int wvu = __builtin_amdgcn_readfirstlane(wv);
         const int2 wq = win[bid];
         const int32_t spq = wq.y - wq.x + 1;
         xdone = spq > 0 && spq <= xcap && spq <= XU * XT;  // uniform per workgroup
-        const int64_t hw = bid * (S * P) + wv;
-        if (xdone && __builtin_amdgcn_readfirstlane(wv) < kSellXCopy) {
+        if (xdone && wvu < kSellXCopy) {
             double xv[XU];
 #pragma unroll
             for (int k = 0; k < XU; ++k) {
@@ -656,6 +660,9 @@ __global__ __launch_bounds__(kWave * kSellSmallS * kSellSmallP) void sell_small_
         for (int k = 1; k < S; ++k)
             sum += part[wv + k][lane];
     }
+    // y[perm]: plain stores.  Round 6 (one cant-like matrix cold, in-process):
+    // sc1 (store_y) 11.5 and non-temporal 11.4 against 10.85 us plain
+    // (profiles/round6/ab_sell_variants.md)
     if (row >= 0)
         y[row] = sum;  // scattered by perm: plain stores, as sell_kernel
     SELL_STAMP(5);

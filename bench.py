@@ -710,8 +710,15 @@ def single_cold(args, torch, dev, rank, world, dist, cdev, prof, fmt=None):
     # the other cold state beside it (not the headline; not in --profile runs,
     # whose PMC passes average every launch of the kernel)
     inproc_other = None
+    node_ms = None
     if not args.profile:
         _, inproc_other, _, _ = inprocess(lambda: (other(), dm.run(x, y)), other, K, reps)
+        # what the estimator charges ANY kernel node: the same F B F ... F
+        # measurement of an empty one-workgroup kernel (tools/probe.hip
+        # spmv_probe_tag) — the graph's launch gap plus an empty dispatch,
+        # which the rocprofv3 kernel time does not contain
+        _, node_ms, _, _ = inprocess(lambda: (flush(), probe.spmv_probe_tag(1, torch.cuda.current_stream().cuda_stream)),
+                                     flush, K, reps)
     bad, first = sa.check(m, xh, y.cpu().numpy())
     all_ok(dist, cdev, torch, bad == 0, f"cant-like single matrix, row {first}", rank)
 
@@ -755,6 +762,10 @@ def single_cold(args, torch, dev, rank, world, dist, cdev, prof, fmt=None):
                              "in_process_estimator": f"median of {reps} timed regions, each minus the mean of "
                                                      "the flush-only spans before and after it",
                              "cold_spmv_ms_each_region": [round(v, 5) for v in diffs],
+                             "empty_kernel_node_ms": round(node_ms, 5) if node_ms is not None else None,
+                             "empty_kernel_node_note": "the same estimator applied to an empty one-workgroup kernel: "
+                                                       "the per-node launch gap any kernel is charged here and the "
+                                                       "rocprofv3 kernel time leaves out (a diagnostic; value keeps it)",
                              "flush_only_ms_per_step": [round(v, 5) for v in flush_spans],
                              "cold_flush": f"{args.cold_flush}: 512 MiB " +
                                            ("written" if args.cold_flush == "write" else "read") +

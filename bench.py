@@ -1345,6 +1345,16 @@ def main():
                            "ms": round(sv["cold_ms"], 5), "kernels": sv["kernels"], "params": sv["params"],
                            "source": sv["source"], "trace": sv["trace"], "timed_region": sv["timed_region"],
                            "parity_ok": sv["parity_ok"]}
+            tr = (sv["trace"] or {}).get("kernel_ms_median")
+            if tr:
+                # the north star's own measure: "rocprof-reported achieved HBM GB/s
+                # against the chip's HBM3E peak" (BASELINE.json north_star, target >= 0.60)
+                sell_single["frac_rocprof"] = round(sv["bytes"] / (tr * 1e-3) * 1e-9 / sa.HBM_PEAK_GBS, 4)
+                sell_single["north_star_target"] = ("SELL-C-sigma >= 0.60 of HBM3E peak on cant, 1 GPU, "
+                                                    "rocprof-reported (frac_rocprof: median of 50 cold launches "
+                                                    "in the kernel trace); frac is the in-process figure, which "
+                                                    "also carries the graph node's launch gap "
+                                                    "(timed_region.empty_kernel_node_ms)")
         ms_per_step = s["cold_ms"]
         bytes_step, total_bytes = s["bytes"], s["bytes"] * world
         value = total_bytes / (ms_per_step * 1e-3) * 1e-9

@@ -614,6 +614,8 @@ __global__ __launch_bounds__(kBlock) void csr_xwin_kernel(
     }
 }
 
+// (Round 6, one cant-like matrix cold, events: R = 2 / 5 / 6 pairs per lane
+// 15.5 / 14.9 / 15.6 us against 15.0 us for R = 3, profiles/round6/ab_csr_r.md.)
 // Chunk size of the staged CSR kernels for a matrix: R = 3 (1,536-entry
 // chunks) unless R = 4 (2,048) cuts a row group of 256/L rows of the mean
 // length into FEWER chunks — every chunk is a memory round trip and two

@@ -802,6 +802,11 @@ static void launch_sell_small_any(int32_t ki, bool nt, int64_t n_slices, const i
 // slice's chunks in chunk order to y[perm] (deterministic, no atomics).
 // An R-MAT hub slice (~1.4e5 slot columns) otherwise keeps one wave busy
 // for the whole kernel.
+// slot groups per lane per step in a split chunk.  Round 6, R-MAT (bench
+// layout, kernel trace): U = 4 / 8 / 16 took 311 / 333 / 336 us — the hub
+// chunks' x gathers, not the load chain, set their time
+// (profiles/round6/ab_sell_split.md)
+constexpr int kSellSplitU = 4;
 template <int KI, bool NT, int U, typename XS = XGlobal>
 __global__ __launch_bounds__(kBlock) void sell_split_kernel(
     int32_t C, int64_t n_chunks, int32_t T, const int64_t *__restrict__ slice_ptr,
@@ -1459,8 +1464,8 @@ extern "C" int spmv_sell_run_split(spmv_dims d, int32_t C, int32_t sigma, int32_
     if (n_chunks == 0)
         return SPMV_SUCCESS;
     double *part = (double *)ws;
-    auto sk = ki == 2 ? (nt ? sell_split_kernel<2, true, 4> : sell_split_kernel<2, false, 4>)
-                      : (nt ? sell_split_kernel<1, true, 4> : sell_split_kernel<1, false, 4>);
+    auto sk = ki == 2 ? (nt ? sell_split_kernel<2, true, kSellSplitU> : sell_split_kernel<2, false, kSellSplitU>)
+                      : (nt ? sell_split_kernel<1, true, kSellSplitU> : sell_split_kernel<1, false, kSellSplitU>);
     hipLaunchKernelGGL(sk, dim3((unsigned)cblocks), dim3(kBlock), 0, st, C, n_chunks, T, slice_ptr, chunk_slice,
                        chunk_k0, col, val, XGlobal{x}, part);
     SPMV_CHECK_LAUNCH("sell_split_kernel");
@@ -1521,8 +1526,8 @@ extern "C" int spmv_sell_run_hot(spmv_dims d, int32_t C, int32_t sigma, int32_t 
     SPMV_CHECK_LAUNCH("sell kernel (hot columns)");
     if (n_chunks == 0)
         return SPMV_SUCCESS;
-    auto sk = ki == 2 ? (nt ? sell_split_kernel<2, true, 4, XHot> : sell_split_kernel<2, false, 4, XHot>)
-                      : (nt ? sell_split_kernel<1, true, 4, XHot> : sell_split_kernel<1, false, 4, XHot>);
+    auto sk = ki == 2 ? (nt ? sell_split_kernel<2, true, kSellSplitU, XHot> : sell_split_kernel<2, false, kSellSplitU, XHot>)
+                      : (nt ? sell_split_kernel<1, true, kSellSplitU, XHot> : sell_split_kernel<1, false, kSellSplitU, XHot>);
     hipLaunchKernelGGL(sk, dim3((unsigned)cblocks), dim3(kBlock), 0, st, C, n_chunks, T, slice_ptr, chunk_slice,
                        chunk_k0, col_hot, val, xs, part);
     SPMV_CHECK_LAUNCH("sell_split_kernel (hot columns)");

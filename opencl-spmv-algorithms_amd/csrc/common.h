@@ -217,6 +217,29 @@ __device__ __forceinline__ void copy_window(double *s_x, const double *__restric
     }
 }
 
+// copy_window for span <= U·T in ONE straight-line pass (no loop): loads the
+// caller issued before it stay in flight behind the window's (a loop header
+// merges states and made the compiler wait for them first)
+template <int T = kBlock, int U = 8>
+__device__ __forceinline__ void copy_window_1pass(double *s_x, const double *__restrict__ x, int32_t lo,
+                                                  int32_t span)
+{
+    double v[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+        const int32_t i = (int32_t)threadIdx.x + k * T;
+        v[k] = x[lo + (i < span ? i : span - 1)];
+    }
+    // unconditional stores (lanes past the window write the window's last
+    // entry again, the value they loaded): a store under `if (i < span)` let
+    // the compiler sink that load into the branch, behind the others
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+        const int32_t i = (int32_t)threadIdx.x + k * T;
+        s_x[i < span ? i : span - 1] = v[k];
+    }
+}
+
 // Hot-column CSR (spmv_csr_run_tiled_hot): ids >= M name the compact table
 // xh of the most frequent columns, gathered from x at the start of the run.
 struct XHot {

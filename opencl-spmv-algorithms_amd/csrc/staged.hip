@@ -172,20 +172,31 @@ __global__ __launch_bounds__(kBlock) void cmrs_staged_kernel(
     const double *prod = reinterpret_cast<const double *>(s_prod);
 
     const int64_t s0 = blk * G;
-    if ((int)threadIdx.x <= G) {
-        const int64_t s = s0 + threadIdx.x;
-        s_sp[threadIdx.x] = strip_ptr[s < n_strips ? s : n_strips];
-    }
+    // the entry count bounds every chunk load: requested first, with the
+    // strip offsets and the x window (read after the barrier it was one more
+    // dependent round trip before the first chunk's loads could go out)
+    const int64_t nz = strip_ptr[n_strips];
+    // the run's strip offsets: loaded by every thread (clamped), stored to
+    // LDS only after the window's loads are out — stored right after their
+    // load, inside the branch, the compiler waited for them before
+    // requesting the x window (two dependent round trips instead of one)
+    const int64_t sv = strip_ptr[s0 + threadIdx.x < n_strips ? s0 + threadIdx.x : n_strips];
     bool staged = false;  // uniform per workgroup
     int32_t wlo = 0;
     if constexpr (XW) {
         const int2 wnd = win[blk];
         const int32_t span = wnd.y - wnd.x + 1;
-        staged = span > 0 && span <= xcap;
+        // a window wider than one pass of the copy gathers from global
+        // memory instead (same x values, same bits): a copy loop here would
+        // join the one-pass path and make it wait for the offsets first
+        staged = span > 0 && span <= xcap && span <= 8 * kBlock;
         wlo = wnd.x;
-        if (staged)
-            copy_window(s_x, x, wlo, span);
+        if (staged)  // uniform
+            copy_window_1pass(s_x, x, wlo, span);
     }
+    if ((int)threadIdx.x <= G)
+        s_sp[threadIdx.x] = sv;
+    asm volatile("" ::"s"(nz));  // in a register by the barrier (the read-only load was sunk past it)
     __syncthreads();
 
     const int rl = threadIdx.x / L, lane = threadIdx.x % L;
@@ -196,7 +207,6 @@ __global__ __launch_bounds__(kBlock) void cmrs_staged_kernel(
     const int64_t row = (s0 + si) * h + key;
     const int64_t blk_end = s_sp[G];
     const KeysU8 keys{rin, s_key2};
-    const int64_t nz = strip_ptr[n_strips];
 
     double acc = 0.0;
     // chunks start on a 32-entry boundary: whole 128-B lines per wave (as
@@ -340,6 +350,9 @@ __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
             tc = int2{stream_load<NT>(col + p), stream_load<NT>(col + q1)};
             tk = int2{stream_load<NT>(row + p), stream_load<NT>(row + q1)};
         }
+        // (Round 6: the tail's x values gathered before commit, branch-free
+        // with the tile's, measured 18.72 vs 18.59 us cold on one cant-like
+        // matrix, events; profiles/round6/ab_coo_cmrs.md.)
         st.commit(t0, t1, nnz, col, val, xs, s_prod, keys);
         if (tpair || tone) {
             s_prod[n / 2 + j] = tpair ? double2{tv.x * xs(tc.x), tv.y * xs(tc.y)} : double2{tv.x * xs(tc.x), 0.0};

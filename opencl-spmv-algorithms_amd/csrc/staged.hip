@@ -105,16 +105,6 @@ struct StageRegs {
         }
     }
 
-    // the issued columns in registers here (a scheduling point for callers
-    // that branch between issue and commit, whose join would otherwise make
-    // the compiler wait for every later load before commit's gathers)
-    __device__ __forceinline__ void pin_columns() const
-    {
-#pragma unroll
-        for (int k = 0; k < R; ++k)
-            asm volatile("" ::"v"(c[k].x), "v"(c[k].y));
-    }
-
     template <typename XS>
     __device__ __forceinline__ void commit(int64_t cb, int64_t ce, int64_t nz, const int32_t *__restrict__ col,
                                            const V *__restrict__ val, const XS &xs, double2 *s_prod,
@@ -585,19 +575,15 @@ __global__ __launch_bounds__(kBlock) void csr_tiled_kernel(
     int32_t b_beg = 0, b_end = 0;
     int2 item[2] = {{0, 0}, {0, 0}};
     int64_t rpv[RPK];
-    // the tile's columns (requested with own_lo, so the offsets' addresses
-    // arrive with them) are awaited HERE, before the offsets are requested:
-    // commit's x gathers then go out while the offsets are in flight (the
-    // three-way join below otherwise waited for the offsets too: vmcnt(0))
-    st.pin_columns();
+    // (Round 6: awaiting the tile's columns here, before requesting the
+    // offsets branch-free, so commit's gathers overlap the offsets: R-MAT
+    // 0.700-0.705 vs 0.674 ms, profiles/round6/ab_tiled.md.  With ~8
+    // tiles per CU the other tiles hide this chain; loads in flight count.)
     if (rp_lds) {
-        // branch-free (past nr: the last owned offset again, never stored):
-        // with a guarded load per k the compiler waited for all of them,
-        // offsets included, before commit's x gathers could go out
 #pragma unroll
         for (int k = 0; k < RPK; ++k) {  // r_lo + nr <= n_rows
             const int i = (int)threadIdx.x + k * kBlock;
-            rpv[k] = row_ptr[r_lo + (i <= nr ? i : nr)];
+            rpv[k] = i <= nr ? row_ptr[r_lo + i] : 0;
         }
     } else if (bk >= 0) {
         b_beg = big[tiles + bk];

@@ -249,6 +249,10 @@ __global__ __launch_bounds__(kBlock) void ell_window_kernel(int64_t n_rows, int3
         win[blockIdx.x] = r;
 }
 
+// (Round 6: small grids — one cant-like matrix, 244 workgroups, one wave
+// per SIMD — with every lane's slot loop in batches of 16 groups (SlotBatch)
+// and a one-pass window copy measured slower: 15.3 vs 15.0 us cold with x
+// windows, 29.8 vs 16.4 us without; profiles/round6/ab_ell.md.)
 // ELL with the workgroup's x window staged in LDS (as sell_xwin_kernel).
 // WB: the window copied with 4 loads per thread in flight (copy_window);
 // else a strided copy, one round trip per 256 entries.

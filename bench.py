@@ -1055,6 +1055,10 @@ def rmat_strong(args, torch, dev, rank, world, dist, cdev):
         permute["aggregate_GBs_with_permute"] = gbs(step_ms + permute["warm_ms"])
         if cold and permute.get("cold_ms"):
             permute["spmv_plus_permute_cold_ms"] = round(max(cold) + permute["cold_ms"], 5)
+        # one step of an iterated solver in this layout: SpMV, y all-gather,
+        # then x' = P y on every rank (the relabel is columns-only)
+        permute["spmv_allgather_permute_ms"] = round(both_ms + permute["warm_ms"], 5)
+        permute["aggregate_GBs_iterated_step"] = gbs(both_ms + permute["warm_ms"])
     out["x_permute"] = permute
     out["gather_ceiling"] = gather_ceiling
     out["per_format"] = per_format

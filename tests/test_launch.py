@@ -5,6 +5,7 @@ only print their environment)."""
 from __future__ import annotations
 
 import os
+import re
 import subprocess
 import sys
 import textwrap
@@ -44,7 +45,7 @@ SCRIPT = textwrap.dedent('''
     if launch.needs_spawn(n):
         sys.exit(launch.spawn_ranks(__file__, n))
     r, w = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
-    print(f"rank {{r}} of {{w}} local {{os.environ['LOCAL_RANK']}}", flush=True)
+    os.write(1, f"rank {{r}} of {{w}} local {{os.environ['LOCAL_RANK']}}\\n".encode())  # one write per line
     sys.exit(3 if (len(sys.argv) > 2 and r == 1) else 0)
 ''')
 
@@ -66,7 +67,8 @@ def test_spawn_runs_n_ranks(tmp_path):
     r = subprocess.run([sys.executable, str(_script(tmp_path)), "3"], capture_output=True, text=True,
                        timeout=240, env=_clean_env())
     assert r.returncode == 0, r.stderr[-2000:]
-    lines = sorted(ln for ln in r.stdout.splitlines() if ln.startswith("rank "))
+    # (ranks share the pipe: match each record wherever a line break fell)
+    lines = sorted(re.findall(r"rank \d+ of \d+ local \d+", r.stdout))
     assert lines == ["rank 0 of 3 local 0", "rank 1 of 3 local 1", "rank 2 of 3 local 2"]
     assert "[launch] --gpus 3" in r.stderr
 

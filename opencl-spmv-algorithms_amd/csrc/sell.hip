@@ -394,15 +394,13 @@ __global__ __launch_bounds__(kBlock) void sell_window_kernel(int32_t C, int bt, 
 // workgroup whose window exceeds xcap entries gathers from global memory.
 // CT = uint16_t: SELL16 (columns stored as offsets from wnd.x).
 template <int KI, bool NT, int U, typename CT = int32_t>
-__global__ __launch_bounds__(1024) void sell_xwin_kernel(
-    int32_t C, int64_t n_slices, const int64_t *__restrict__ slice_ptr,
+__device__ __forceinline__ void sell_xwin_body(
+    int64_t blk, int32_t C, int64_t n_slices, const int64_t *__restrict__ slice_ptr,
     const int32_t *__restrict__ perm, const CT *__restrict__ col,
     const double *__restrict__ val, const double *__restrict__ x,
-    double *__restrict__ y, const int2 *__restrict__ win, int32_t xcap, int64_t wcap, int remap,
-    int64_t ystage_rows)
+    double *__restrict__ y, const int2 *__restrict__ win, int32_t xcap, int64_t wcap,
+    int64_t ystage_rows, double *s_x)
 {
-    extern __shared__ double s_x[];
-    const int64_t blk = xcd_block(remap);  // remap: neighbouring windows on one XCD (shared x lines in L2)
     const int2 wnd = win[blk];
     const int32_t span = wnd.y - wnd.x + 1;
     const bool staged = span > 0 && span <= xcap;  // uniform per workgroup
@@ -458,6 +456,54 @@ __global__ __launch_bounds__(1024) void sell_xwin_kernel(
     }
     if (row >= 0)
         y[row] = sum;  // scattered by perm: plain stores (sc1 measured 1.8 % slower, profiles/round2/ab_ystore.log)
+}
+
+template <int KI, bool NT, int U, typename CT = int32_t>
+__global__ __launch_bounds__(1024) void sell_xwin_kernel(
+    int32_t C, int64_t n_slices, const int64_t *__restrict__ slice_ptr,
+    const int32_t *__restrict__ perm, const CT *__restrict__ col,
+    const double *__restrict__ val, const double *__restrict__ x,
+    double *__restrict__ y, const int2 *__restrict__ win, int32_t xcap, int64_t wcap, int remap,
+    int64_t ystage_rows)
+{
+    extern __shared__ double s_x[];
+    const int64_t blk = xcd_block(remap);  // remap: neighbouring windows on one XCD (shared x lines in L2)
+    sell_xwin_body<KI, NT, U, CT>(blk, C, n_slices, slice_ptr, perm, col, val, x, y, win, xcap, wcap, ystage_rows,
+                                  s_x);
+}
+
+// SELL with a split plan in ONE launch (256-slot workgroups, no y staging):
+// the first split_blocks workgroups run the wide slices' chunks
+// (sell_split_body, into part[]), the rest the main x-window kernel's
+// workgroups (every slice's first T columns).  The chunks — an R-MAT's hub
+// rows, long chains of x gathers — then run beside the main stream instead
+// of after it; same arithmetic, same bits (sell_split_fix_kernel still adds
+// the chunks afterwards).
+template <int KI, bool NT, int U, typename XS>
+__device__ __forceinline__ void sell_split_body(int64_t gid, int32_t C, int64_t n_chunks, int32_t T,
+                                                const int64_t *__restrict__ slice_ptr,
+                                                const int32_t *__restrict__ chunk_slice,
+                                                const int32_t *__restrict__ chunk_k0, const int32_t *__restrict__ col,
+                                                const double *__restrict__ val, const XS xs,
+                                                double *__restrict__ part);  // defined with sell_split_kernel
+
+template <int KI, bool NT, int U, int SU>
+__global__ __launch_bounds__(kBlock) void sell_split_fused_kernel(
+    int64_t split_blocks, int32_t C, int64_t n_slices, const int64_t *__restrict__ slice_ptr,
+    const int32_t *__restrict__ perm, const int32_t *__restrict__ col, const double *__restrict__ val,
+    const double *__restrict__ x, double *__restrict__ y, const int2 *__restrict__ win, int32_t xcap, int32_t T,
+    int64_t n_chunks, const int32_t *__restrict__ chunk_slice, const int32_t *__restrict__ chunk_k0,
+    double *__restrict__ part)
+{
+    extern __shared__ double s_x[];
+    const int64_t b = blockIdx.x;
+    if (b < split_blocks) {  // uniform
+        sell_split_body<KI, NT, SU, XGlobal>(b * kBlock + threadIdx.x, C, n_chunks, T, slice_ptr, chunk_slice,
+                                             chunk_k0, col, val, XGlobal{x}, part);
+        return;
+    }
+    sell_xwin_body<KI, NT, U, int32_t>(b - split_blocks, C, n_slices, slice_ptr, perm, col, val, x, y, win, xcap,
+                                       (int64_t)T, 0, s_x);
 }
 
 // Small matrices (BASELINE.json configs[2]: one cant-like matrix is 976
@@ -811,14 +857,17 @@ static void launch_sell_small_any(int32_t ki, bool nt, int64_t n_slices, const i
 // chunks' x gathers, not the load chain, set their time
 // (profiles/round6/ab_sell_split.md)
 constexpr int kSellSplitU = 4;
-template <int KI, bool NT, int U, typename XS = XGlobal>
-__global__ __launch_bounds__(kBlock) void sell_split_kernel(
-    int32_t C, int64_t n_chunks, int32_t T, const int64_t *__restrict__ slice_ptr,
+#ifndef SPMV_SELL_SPLIT_FUSED  // A/B builds only
+#define SPMV_SELL_SPLIT_FUSED 1
+#endif
+constexpr bool kSellSplitFused = SPMV_SELL_SPLIT_FUSED;  // spmv_sell_run_split: one grid (see the fused kernel)
+template <int KI, bool NT, int U, typename XS>
+__device__ __forceinline__ void sell_split_body(
+    int64_t gid, int32_t C, int64_t n_chunks, int32_t T, const int64_t *__restrict__ slice_ptr,
     const int32_t *__restrict__ chunk_slice, const int32_t *__restrict__ chunk_k0,
     const int32_t *__restrict__ col, const double *__restrict__ val, const XS xs,
     double *__restrict__ part)
 {
-    const int64_t gid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const int64_t c = gid / C;
     if (c >= n_chunks)
         return;
@@ -830,6 +879,17 @@ __global__ __launch_bounds__(kBlock) void sell_split_kernel(
     const int64_t n = w - k0 < T ? w - k0 : T;
     const int64_t off = base + k0 * C + r * KI;
     part[gid] = slot_dot<KI, NT, U>(val + off, col + off, n, (int64_t)C * KI, xs);
+}
+
+template <int KI, bool NT, int U, typename XS = XGlobal>
+__global__ __launch_bounds__(kBlock) void sell_split_kernel(
+    int32_t C, int64_t n_chunks, int32_t T, const int64_t *__restrict__ slice_ptr,
+    const int32_t *__restrict__ chunk_slice, const int32_t *__restrict__ chunk_k0,
+    const int32_t *__restrict__ col, const double *__restrict__ val, const XS xs,
+    double *__restrict__ part)
+{
+    sell_split_body<KI, NT, U, XS>((int64_t)blockIdx.x * kBlock + threadIdx.x, C, n_chunks, T, slice_ptr,
+                                   chunk_slice, chunk_k0, col, val, xs, part);
 }
 
 __global__ __launch_bounds__(kBlock) void sell_split_fix_kernel(int32_t C, int64_t n_chunks,
@@ -847,6 +907,7 @@ __global__ __launch_bounds__(kBlock) void sell_split_fix_kernel(int32_t C, int64
         return;  // not the first chunk of its slice
     const int64_t r = gid - c * C;
     double acc = 0.0;  // 8 chunks' loads in flight per step, added in chunk order
+    // (round 6: 32 per step, branch-free, measured 191 vs 57 us on the R-MAT)
     for (int64_t u = c;; u += 8) {
         int32_t ss[8];
         double pp[8];
@@ -1449,6 +1510,23 @@ extern "C" int spmv_sell_run_split(spmv_dims d, int32_t C, int32_t sigma, int32_
         return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_run_split: grid too large");
     const hipStream_t st = (hipStream_t)d.stream;
     const bool nt = stream_nt(kSellStreamNtDefault);
+    double *part = (double *)ws;
+    if (win && n_chunks > 0 && !sell_small(C, n_slices) && bt == kBlock && !sell_ystage(bt, sigma) &&
+        blocks + cblocks <= INT32_MAX && kSellSplitFused) {
+        // chunks and main workgroups in one grid (sell_split_fused_kernel)
+        auto kern = ki == 2 ? (nt ? sell_split_fused_kernel<2, true, 4, kSellSplitU>
+                                  : sell_split_fused_kernel<2, false, 4, kSellSplitU>)
+                            : (nt ? sell_split_fused_kernel<1, true, 4, kSellSplitU>
+                                  : sell_split_fused_kernel<1, false, 4, kSellSplitU>);
+        hipLaunchKernelGGL(kern, dim3((unsigned)(cblocks + blocks)), dim3(kBlock), (size_t)xcap * sizeof(double), st,
+                           cblocks, C, n_slices, slice_ptr, perm, col, val, x, y, (const int2 *)win, xcap, T,
+                           n_chunks, chunk_slice, chunk_k0, part);
+        SPMV_CHECK_LAUNCH("sell_split_fused_kernel");
+        hipLaunchKernelGGL(sell_split_fix_kernel, dim3((unsigned)cblocks), dim3(kBlock), 0, st, C, n_chunks,
+                           chunk_slice, perm, part, y);
+        SPMV_CHECK_LAUNCH("sell_split_fix_kernel");
+        return SPMV_SUCCESS;
+    }
     if (sell_small(C, n_slices)) {
         launch_sell_small_any(ki, nt, n_slices, slice_ptr, perm, col, val, XGlobal{x}, y, (int64_t)T, st, x,
                               (const int2 *)win, xcap);
@@ -1467,7 +1545,6 @@ extern "C" int spmv_sell_run_split(spmv_dims d, int32_t C, int32_t sigma, int32_
     SPMV_CHECK_LAUNCH("sell kernel (split main)");
     if (n_chunks == 0)
         return SPMV_SUCCESS;
-    double *part = (double *)ws;
     auto sk = ki == 2 ? (nt ? sell_split_kernel<2, true, kSellSplitU> : sell_split_kernel<2, false, kSellSplitU>)
                       : (nt ? sell_split_kernel<1, true, kSellSplitU> : sell_split_kernel<1, false, kSellSplitU>);
     hipLaunchKernelGGL(sk, dim3((unsigned)cblocks), dim3(kBlock), 0, st, C, n_chunks, T, slice_ptr, chunk_slice,

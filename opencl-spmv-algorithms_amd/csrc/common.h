@@ -82,7 +82,12 @@ int launch_csr_tiled_hot(const spmv_dims &d, const int64_t *row_ptr, const int32
 int launch_cmrs_tiled(const spmv_dims &d, int32_t h, int64_t n_strips, const int64_t *strip_ptr,
                       const uint8_t *rin, const int32_t *col, const double *val, const double *x,
                       double *y, int32_t *own_lo, int32_t *carry_row, double *carry_val, int64_t H = 0,
-                      const int32_t *hot = nullptr, double *xh = nullptr);
+                      const int32_t *hot = nullptr, double *xh = nullptr, bool own_lo_ready = false);
+int cmrs_tiled_planned(const spmv_dims &d, int32_t h, int64_t n_strips, const int64_t *strip_ptr,
+                       const uint8_t *rin, const int32_t *col, const double *val, const double *x, double *y,
+                       int64_t H, const int32_t *hot, void *ws, bool fill);
+__global__ void csr_tile_rows_kernel(int64_t n_rows, int64_t nnz, int64_t tiles, int64_t ch,
+                                     const int64_t *__restrict__ ptr, int32_t *__restrict__ own_lo);
 struct XHot;
 int launch_coo_staged_acc_hot(const spmv_dims &d, const int32_t *row, const int32_t *col,
                               const double *val, const double *x, double *y, int32_t *carry_row,

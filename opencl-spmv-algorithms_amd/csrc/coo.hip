@@ -36,26 +36,31 @@ __global__ __launch_bounds__(kBlock) void coo_carry_kernel(
 {
     const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const int lane = threadIdx.x & (kWave - 1);
-    // The head test and the first 8 tiles' loads are issued together: one
-    // round trip for a row over <= 8 tiles (the common case), added in tile
-    // order by the head's thread.
+    // The head test first (two row keys per thread, the same lines), then
+    // only a head thread loads its run's first 8 tiles and adds a run of
+    // <= 8 in tile order.  (Every thread loading 8 keys and 8 values up
+    // front read each entry 8 times over: ~25 us for the tiled CMRS's
+    // h x 195 K R-MAT carries, most of them empty.)
     const int32_t prev = t > 0 && t < n_tiles ? carry_row[t - 1] : -1;
-    int32_t rr[8];
-    double vv[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const bool in = t + k < n_tiles;
-        rr[k] = in ? carry_row[t + k] : -2;
-        vv[k] = in ? carry_val[t + k] : 0.0;
-    }
-    const int32_t r = rr[0];
+    const int32_t r = t < n_tiles ? carry_row[t] : -2;
     const bool head = t < n_tiles && r >= 0 && prev != r;  // first tile of a run of carries
-    const bool lng = head && rr[7] == r;                   // the run goes on past 8 tiles
-    if (head && !lng) {
-        double s = 0.0;
-        for (int k = 0; k < 8 && rr[k] == r; ++k)
-            s += vv[k];
-        y[r] += s;
+    bool lng = false;                                      // the run goes on past 8 tiles
+    if (head) {
+        int32_t rr[8];
+        double vv[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const bool in = t + k < n_tiles;
+            rr[k] = in ? carry_row[t + k] : -2;
+            vv[k] = in ? carry_val[t + k] : 0.0;
+        }
+        lng = rr[7] == r;
+        if (!lng) {
+            double s = 0.0;
+            for (int k = 0; k < 8 && rr[k] == r; ++k)
+                s += vv[k];
+            y[r] += s;
+        }
     }
     // A hub row's run (R-MAT rows of 1e5 entries span ~100-150 tiles) is
     // summed by the whole wave: 4 x 64 tiles per round trip, lane-strided,
@@ -249,6 +254,33 @@ extern "C" int spmv_cmrs_run_tiled(spmv_dims d, int32_t h, int64_t n_strips, con
     return launch_cmrs_tiled(d, h, n_strips, strip_ptr, row_in_strip, col, val, x, y, own_lo, carry_row,
                              carry_val);
 }
+
+// The plan's tiled CMRS (csrc/plan.hip): the workspace laid out as
+// spmv_cmrs_run_tiled (H = 0) or spmv_cmrs_run_tiled_hot (H > 0) lay it out,
+// its tile -> first-strip table filled ONCE at plan build (fill = true) and
+// reused by every run (fill = false: no csr_tile_rows_kernel per run).
+namespace spmv {
+int cmrs_tiled_planned(const spmv_dims &d, int32_t h, int64_t n_strips, const int64_t *strip_ptr,
+                       const uint8_t *rin, const int32_t *col, const double *val, const double *x, double *y,
+                       int64_t H, const int32_t *hot, void *ws, bool fill)
+{
+    const int64_t ch = cmrs_tiled_tile(d.n_rows, d.nnz);
+    const int64_t tiles = (d.nnz + ch - 1) / ch;
+    double *xh = (double *)ws;
+    double *carry_val = xh + (H > 0 ? H : 0);
+    int32_t *own_lo = (int32_t *)(carry_val + (int64_t)h * tiles);
+    int32_t *carry_row = own_lo + tiles + 1;
+    const hipStream_t st = (hipStream_t)d.stream;
+    if (fill) {
+        hipLaunchKernelGGL(csr_tile_rows_kernel, dim3((unsigned)((tiles + 1 + kBlock - 1) / kBlock)),
+                           dim3(kBlock), 0, st, n_strips, d.nnz, tiles, ch, strip_ptr, own_lo);
+        SPMV_CHECK_LAUNCH("csr_tile_rows_kernel (CMRS plan)");
+        return SPMV_SUCCESS;
+    }
+    return launch_cmrs_tiled(d, h, n_strips, strip_ptr, rin, col, val, x, y, own_lo, carry_row, carry_val, H,
+                             hot, H > 0 ? xh : nullptr, true);
+}
+}  // namespace spmv
 
 extern "C" int spmv_coo_run_xwin(spmv_dims d, const int32_t *row, const int32_t *col, const double *val,
                                  const double *x, double *y, void *ws, size_t ws_bytes, const void *win,

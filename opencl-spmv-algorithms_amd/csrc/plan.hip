@@ -105,6 +105,7 @@ struct spmv_plan {
     int32_t *big = nullptr;
     int64_t big_len = 0, big_tiles = 0, big_tile = 0;
     int32_t split_T = 0;
+    bool tiles_planned = false;  // tiled CMRS: the tile -> first-strip table filled at build
     int64_t n_chunks = 0;
     int32_t *chunk_slice = nullptr, *chunk_k0 = nullptr;
     uint16_t *col16 = nullptr;
@@ -701,6 +702,18 @@ int spmv_plan_cmrs(spmv_dims d, int32_t h, int64_t n_strips, const int64_t *stri
         p->path = P_CMRS_TILED;
         p->ws_bytes = spmv_cmrs_hot_ws_bytes(n_strips, d.nnz, h, p->H);
         rc = plan_alloc(p, &p->ws, p->ws_bytes);
+        // the tile -> first-strip table once, here, instead of every run
+        // (csr_tile_rows_kernel, ~8 us on the R-MAT)
+        const int64_t ch = cmrs_tiled_tile(d.n_rows, d.nnz);
+        if (rc == SPMV_SUCCESS && d.n_rows > 0 && d.nnz > 0 && h >= 1 && h <= 64 && d.n_rows <= INT32_MAX &&
+            n_strips == (d.n_rows + h - 1) / h && ((d.nnz + ch - 1) / ch) * h <= INT32_MAX) {
+            rc = cmrs_tiled_planned(d, h, n_strips, strip_ptr, row_in_strip, col, val, nullptr, nullptr, p->H,
+                                    p->hot, p->ws, true);
+            // runs may come on any stream: the table is complete when the plan is returned
+            if (rc == SPMV_SUCCESS && hipStreamSynchronize((hipStream_t)d.stream) != hipSuccess)
+                rc = fail_msg(SPMV_PROGRAM_ERROR, "spmv_plan_cmrs: tile table");
+            p->tiles_planned = rc == SPMV_SUCCESS;
+        }
         snprintf(p->kernel, sizeof p->kernel, "cmrs_tiled_kernel");
         snprintf(p->desc, sizeof p->desc, "CMRS h=%d: entry-balanced tiles (skewed strips)%s", h,
                  p->H > 0 ? ", hot-column table" : "");
@@ -777,6 +790,11 @@ int spmv_plan_run(const spmv_plan *p, const double *x, double *y, void *stream)
     case P_CMRS_XWIN:
         return spmv_cmrs_run_xwin(d, p->h, p->n_strips, p->ptr, p->rin, p->col, p->val, x, y, p->win, p->xcap);
     case P_CMRS_TILED:
+        if (p->tiles_planned) {
+            SPMV_GUARD(d);
+            return cmrs_tiled_planned(d, p->h, p->n_strips, p->ptr, p->rin, col, p->val, x, y, H, p->hot, p->ws,
+                                      false);
+        }
         return spmv_cmrs_run_tiled_hot(d, p->h, p->n_strips, p->ptr, p->rin, col, p->val, x, y, H, p->hot, p->ws,
                                        p->ws_bytes);
     }

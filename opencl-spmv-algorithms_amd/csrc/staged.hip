@@ -831,15 +831,17 @@ static void launch_hot_gather(int64_t H, const int32_t *hot, const double *x, do
 int launch_cmrs_tiled(const spmv_dims &d, int32_t h, int64_t n_strips, const int64_t *strip_ptr,
                       const uint8_t *rin, const int32_t *col, const double *val, const double *x,
                       double *y, int32_t *own_lo, int32_t *carry_row, double *carry_val, int64_t H,
-                      const int32_t *hot, double *xh)
+                      const int32_t *hot, double *xh, bool own_lo_ready)
 {
     const int64_t ch = cmrs_tiled_tile(d.n_rows, d.nnz);
     const int64_t tiles = (d.nnz + ch - 1) / ch;
     const hipStream_t st = (hipStream_t)d.stream;
     launch_hot_gather(H, hot, x, xh, st);
-    hipLaunchKernelGGL(csr_tile_rows_kernel, dim3((unsigned)((tiles + 1 + kBlock - 1) / kBlock)),
-                       dim3(kBlock), 0, st, n_strips, d.nnz, tiles, ch, strip_ptr, own_lo);
-    SPMV_CHECK_LAUNCH("csr_tile_rows_kernel (strips)");
+    if (!own_lo_ready) {  // (a plan fills it once: cmrs_tiled_planned)
+        hipLaunchKernelGGL(csr_tile_rows_kernel, dim3((unsigned)((tiles + 1 + kBlock - 1) / kBlock)),
+                           dim3(kBlock), 0, st, n_strips, d.nnz, tiles, ch, strip_ptr, own_lo);
+        SPMV_CHECK_LAUNCH("csr_tile_rows_kernel (strips)");
+    }
     // lanes per row as the staged kernels (one per ~16 entries of the mean
     // row), at most kBlock / h so every carried row key has its group
     int L = spmv_csr_auto_lanes(d.n_rows, d.nnz);

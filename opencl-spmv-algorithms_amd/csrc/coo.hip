@@ -36,31 +36,28 @@ __global__ __launch_bounds__(kBlock) void coo_carry_kernel(
 {
     const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const int lane = threadIdx.x & (kWave - 1);
-    // The head test first (two row keys per thread, the same lines), then
-    // only a head thread loads its run's first 8 tiles and adds a run of
-    // <= 8 in tile order.  (Every thread loading 8 keys and 8 values up
-    // front read each entry 8 times over: ~25 us for the tiled CMRS's
-    // h x 195 K R-MAT carries, most of them empty.)
+    // The head test and the first 8 tiles' loads are issued together: one
+    // round trip for a row over <= 8 tiles (the common case), added in tile
+    // order by the head's thread.  (Round 6: the head test first and the
+    // run's loads only in head threads measured 14.7 vs 13.9 us average on
+    // the R-MAT's CSR / CMRS / COO carries; profiles/round6/ab_cmrs_plan_carry.md.)
     const int32_t prev = t > 0 && t < n_tiles ? carry_row[t - 1] : -1;
-    const int32_t r = t < n_tiles ? carry_row[t] : -2;
-    const bool head = t < n_tiles && r >= 0 && prev != r;  // first tile of a run of carries
-    bool lng = false;                                      // the run goes on past 8 tiles
-    if (head) {
-        int32_t rr[8];
-        double vv[8];
+    int32_t rr[8];
+    double vv[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const bool in = t + k < n_tiles;
-            rr[k] = in ? carry_row[t + k] : -2;
-            vv[k] = in ? carry_val[t + k] : 0.0;
-        }
-        lng = rr[7] == r;
-        if (!lng) {
-            double s = 0.0;
-            for (int k = 0; k < 8 && rr[k] == r; ++k)
-                s += vv[k];
-            y[r] += s;
-        }
+    for (int k = 0; k < 8; ++k) {
+        const bool in = t + k < n_tiles;
+        rr[k] = in ? carry_row[t + k] : -2;
+        vv[k] = in ? carry_val[t + k] : 0.0;
+    }
+    const int32_t r = rr[0];
+    const bool head = t < n_tiles && r >= 0 && prev != r;  // first tile of a run of carries
+    const bool lng = head && rr[7] == r;                   // the run goes on past 8 tiles
+    if (head && !lng) {
+        double s = 0.0;
+        for (int k = 0; k < 8 && rr[k] == r; ++k)
+            s += vv[k];
+        y[r] += s;
     }
     // A hub row's run (R-MAT rows of 1e5 entries span ~100-150 tiles) is
     // summed by the whole wave: 4 x 64 tiles per round trip, lane-strided,

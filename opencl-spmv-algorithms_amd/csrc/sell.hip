@@ -892,40 +892,74 @@ __global__ __launch_bounds__(kBlock) void sell_split_kernel(
                                    chunk_slice, chunk_k0, col, val, xs, part);
 }
 
-__global__ __launch_bounds__(kBlock) void sell_split_fix_kernel(int32_t C, int64_t n_chunks,
-                                                                const int32_t *__restrict__ chunk_slice,
-                                                                const int32_t *__restrict__ perm,
-                                                                const double *__restrict__ part,
-                                                                double *__restrict__ y)
+// One 1024-thread workgroup per chunk; only the first chunk of each slice's
+// run works.  Thread t takes row r = t % C of segment t / C: the run's
+// chunks are cut into W = 1024 / C segments summed side by side (8 loads in
+// flight per thread), and the W partial sums of a row are added in segment
+// order through LDS — a fixed order, so bitwise reproducible; a run of at
+// most W chunks is summed in chunk order exactly as before.  (One wave
+// walking an R-MAT hub slice's ~600 chunks 8 per round trip took 57 us.)
+constexpr int kSellFixThreads = 1024;
+__global__ __launch_bounds__(kSellFixThreads) void sell_split_fix_kernel(int32_t C, int64_t n_chunks,
+                                                                         const int32_t *__restrict__ chunk_slice,
+                                                                         const int32_t *__restrict__ perm,
+                                                                         const double *__restrict__ part,
+                                                                         double *__restrict__ y)
 {
-    const int64_t gid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    const int64_t c = gid / C;
-    if (c >= n_chunks)
-        return;
+    const int64_t c = blockIdx.x;
     const int32_t s = chunk_slice[c];
     if (c > 0 && chunk_slice[c - 1] == s)
-        return;  // not the first chunk of its slice
-    const int64_t r = gid - c * C;
-    double acc = 0.0;  // 8 chunks' loads in flight per step, added in chunk order
-    // (round 6: 32 per step, branch-free, measured 191 vs 57 us on the R-MAT)
-    for (int64_t u = c;; u += 8) {
-        int32_t ss[8];
-        double pp[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const bool in = u + k < n_chunks;
-            ss[k] = in ? chunk_slice[u + k] : -1;
-            pp[k] = in ? part[(u + k) * C + r] : 0.0;
-        }
-        int k = 0;
-        for (; k < 8 && ss[k] == s; ++k)
-            acc += pp[k];
-        if (k < 8)
+        return;  // uniform: not the first chunk of its slice
+    // the run's end: chunk_slice is sorted by slice, so the chunks equal to
+    // s form a prefix of [c, n_chunks); counted 1024 probes at a time
+    __shared__ int64_t s_end;
+    int64_t lo = c + 1, step = 64;
+    for (;;) {  // coarse: probes lo + t * step
+        const int64_t q = lo + (int64_t)threadIdx.x * step;
+        const int n = __syncthreads_count(q < n_chunks && chunk_slice[q] == s);
+        if (n < kSellFixThreads) {  // the end lies in (lo + (n-1)*step, lo + n*step]
+            lo = n > 0 ? lo + (int64_t)(n - 1) * step + 1 : lo;
             break;
+        }
+        lo += (int64_t)kSellFixThreads * step;
     }
-    const int32_t row = perm[(int64_t)s * C + r];
-    if (row >= 0)
-        y[row] += acc;
+    {  // fine: probes lo + t, t < step
+        const int64_t q = lo + threadIdx.x;
+        const int n = __syncthreads_count(threadIdx.x < step && q < n_chunks && chunk_slice[q] == s);
+        if (threadIdx.x == 0)
+            s_end = lo + n;
+    }
+    __syncthreads();
+    const int64_t end = s_end;
+    const int W = kSellFixThreads / C;
+    const int r = threadIdx.x % C, seg = threadIdx.x / C;
+    const int64_t len = end - c;
+    const int64_t sl = (len + W - 1) / W;
+    double acc = 0.0;
+    if (seg < W) {
+        const int64_t b = c + seg * sl, e = b + sl < end ? b + sl : end;
+        for (int64_t u = b; u < e; u += 8) {
+            double pp[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                pp[k] = u + k < e ? part[(u + k) * C + r] : 0.0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                if (u + k < e)
+                    acc += pp[k];
+        }
+    }
+    __shared__ double s_p[kSellFixThreads];
+    s_p[threadIdx.x] = acc;
+    __syncthreads();
+    if (seg == 0) {
+        double tot = 0.0;
+        for (int j = 0; j < W; ++j)
+            tot += s_p[j * C + r];
+        const int32_t row = perm[(int64_t)s * C + r];
+        if (row >= 0)
+            y[row] += tot;
+    }
 }
 
 __global__ __launch_bounds__(kBlock) void sell_hot_gather_kernel(int64_t H, const int32_t *__restrict__ hot,
@@ -1506,7 +1540,7 @@ extern "C" int spmv_sell_run_split(spmv_dims d, int32_t C, int32_t sigma, int32_
     int64_t blocks;
     sell_geometry(C, sigma, n_slices, &bt, &blocks);
     const int64_t cblocks = (n_chunks * C + kBlock - 1) / kBlock;
-    if (blocks > INT32_MAX || cblocks > INT32_MAX)
+    if (blocks > INT32_MAX || cblocks > INT32_MAX || n_chunks > INT32_MAX)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_run_split: grid too large");
     const hipStream_t st = (hipStream_t)d.stream;
     const bool nt = stream_nt(kSellStreamNtDefault);
@@ -1522,7 +1556,7 @@ extern "C" int spmv_sell_run_split(spmv_dims d, int32_t C, int32_t sigma, int32_
                            cblocks, C, n_slices, slice_ptr, perm, col, val, x, y, (const int2 *)win, xcap, T,
                            n_chunks, chunk_slice, chunk_k0, part);
         SPMV_CHECK_LAUNCH("sell_split_fused_kernel");
-        hipLaunchKernelGGL(sell_split_fix_kernel, dim3((unsigned)cblocks), dim3(kBlock), 0, st, C, n_chunks,
+        hipLaunchKernelGGL(sell_split_fix_kernel, dim3((unsigned)n_chunks), dim3(kSellFixThreads), 0, st, C, n_chunks,
                            chunk_slice, perm, part, y);
         SPMV_CHECK_LAUNCH("sell_split_fix_kernel");
         return SPMV_SUCCESS;
@@ -1550,7 +1584,7 @@ extern "C" int spmv_sell_run_split(spmv_dims d, int32_t C, int32_t sigma, int32_
     hipLaunchKernelGGL(sk, dim3((unsigned)cblocks), dim3(kBlock), 0, st, C, n_chunks, T, slice_ptr, chunk_slice,
                        chunk_k0, col, val, XGlobal{x}, part);
     SPMV_CHECK_LAUNCH("sell_split_kernel");
-    hipLaunchKernelGGL(sell_split_fix_kernel, dim3((unsigned)cblocks), dim3(kBlock), 0, st, C, n_chunks,
+    hipLaunchKernelGGL(sell_split_fix_kernel, dim3((unsigned)n_chunks), dim3(kSellFixThreads), 0, st, C, n_chunks,
                        chunk_slice, perm, part, y);
     SPMV_CHECK_LAUNCH("sell_split_fix_kernel");
     return SPMV_SUCCESS;
@@ -1586,7 +1620,7 @@ extern "C" int spmv_sell_run_hot(spmv_dims d, int32_t C, int32_t sigma, int32_t 
     int64_t blocks;
     sell_geometry(C, sigma, n_slices, &bt, &blocks);
     const int64_t cblocks = (n_chunks * C + kBlock - 1) / kBlock;
-    if (blocks > INT32_MAX || cblocks > INT32_MAX)
+    if (blocks > INT32_MAX || cblocks > INT32_MAX || n_chunks > INT32_MAX)
         return fail_msg(SPMV_OTHER_ERROR, "spmv_sell_run_hot: grid too large");
     const hipStream_t st = (hipStream_t)d.stream;
     double *xh = (double *)ws;
@@ -1612,7 +1646,7 @@ extern "C" int spmv_sell_run_hot(spmv_dims d, int32_t C, int32_t sigma, int32_t 
     hipLaunchKernelGGL(sk, dim3((unsigned)cblocks), dim3(kBlock), 0, st, C, n_chunks, T, slice_ptr, chunk_slice,
                        chunk_k0, col_hot, val, xs, part);
     SPMV_CHECK_LAUNCH("sell_split_kernel (hot columns)");
-    hipLaunchKernelGGL(sell_split_fix_kernel, dim3((unsigned)cblocks), dim3(kBlock), 0, st, C, n_chunks,
+    hipLaunchKernelGGL(sell_split_fix_kernel, dim3((unsigned)n_chunks), dim3(kSellFixThreads), 0, st, C, n_chunks,
                        chunk_slice, perm, part, y);
     SPMV_CHECK_LAUNCH("sell_split_fix_kernel");
     return SPMV_SUCCESS;

@@ -438,6 +438,38 @@ __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
     // owned rows: (prev, last], plus the trailing empty rows in the last
     // tile; a continued first row equals prev, so it is excluded here
     const int64_t r_hi = t1 == nnz ? n_rows - 1 : (int64_t)last;
+    if (!heads && span > RC && span <= 32 * (int64_t)(RC + 1)) {  // uniform
+        // A tile over a long run of mostly empty rows (R-MAT: up to ~28 K
+        // rows per 512-entry tile): the rows WITH entries are found at their
+        // first entry (a key change), each summed over [start, end) exactly
+        // as the search path sums it (the same bits), and marked in a bitmap
+        // (s_start's words); then the others are written as zeros,
+        // coalesced.  The search path did two binary searches per owned row.
+        uint32_t *s_bits = reinterpret_cast<uint32_t *>(s_start);
+        const int nw = (int)((span + 31) >> 5);
+        for (int i = threadIdx.x; i < nw; i += kBlock)
+            s_bits[i] = 0u;
+        __syncthreads();
+        for (int j = g; j < n; j += GROUPS) {  // the tile's entries (tail entries continue the last row)
+            const int32_t r = s_row[j];
+            if (r <= prev || (j > 0 && s_row[j - 1] == r))
+                continue;  // uniform over the group: not a row's first entry
+            const int b = lower_bound_lds(s_row, j + 1, ne, r + 1);
+            double sm = slice_sum<L>(prod, j, b, lane);
+            sm = group_sum<L>(sm);
+            if (lane == 0) {
+                store_y(y + r, sm);
+                atomicOr(&s_bits[(r - r_lo) >> 5], 1u << ((r - r_lo) & 31));
+            }
+        }
+        __syncthreads();
+        for (int64_t r = r_lo + threadIdx.x; r <= r_hi; r += kBlock) {
+            const bool has = r <= last && ((s_bits[(r - r_lo) >> 5] >> ((r - r_lo) & 31)) & 1u);
+            if (!has)
+                store_y(y + r, 0.0);
+        }
+        return;
+    }
     for (int64_t r = r_lo + g; r <= r_hi; r += GROUPS) {
         double s = 0.0;
         if (r <= last) {

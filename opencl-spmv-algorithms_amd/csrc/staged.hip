@@ -799,38 +799,28 @@ __global__ __launch_bounds__(kBlock) void cmrs_tiled_kernel(
             carry_val[(int64_t)g * tiles + tile] = c;
         }
     }
-    // owned strips, one L-lane group per row; their offsets staged in LDS
-    // kBlock strips per pass with coalesced loads (a tile over a long run
-    // of empty strips — R-MAT: thousands — read strip_ptr[s], [s + 1] per
-    // row instead: one dependent global round trip per row of every group)
-    __shared__ int64_t s_spc[kBlock + 1];
-    const int64_t n_own = s_hi - s_lo + 1;
-    for (int64_t pb = 0; pb < n_own; pb += kBlock) {
-        const int np = (int)(n_own - pb < kBlock ? n_own - pb : kBlock);
-        __syncthreads();  // the previous pass's readers are done
-        for (int i = threadIdx.x; i <= np; i += kBlock)
-            s_spc[i] = strip_ptr[s_lo + pb + i];  // s_lo + pb + np <= s_hi + 1 <= n_strips
-        __syncthreads();
-        const int64_t items = (int64_t)np * h;
-        for (int64_t it = g; it < items; it += GROUPS) {
-            const int si = (int)(it / h);
-            const int k = (int)(it % h);
-            const int64_t s = s_lo + pb + si;
-            const int64_t sa = s_spc[si];
-            int64_t sb = s_spc[si + 1];
-            sb = sb < t1 ? sb : t1;
-            double acc = 0.0;
-            if (sa < sb) {
-                const int a = lower_bound_lds(s_key, (int)(sa - t0), (int)(sb - t0), k);
-                const int b = lower_bound_lds(s_key, a, (int)(sb - t0), k + 1);
-                for (int j = a + lane; j < b; j += L)
-                    acc += prod[j];
-            }
-            acc = group_sum<L>(acc);
-            const int64_t r = s * h + k;
-            if (lane == 0 && r < n_rows)
-                store_y(y + (r), acc);
+    // owned strips, one L-lane group per row.  (Round 6: staging the offsets
+    // in LDS 256 strips per pass measured slower for every tile, 791 vs 748
+    // us on the R-MAT, and equal when kept to tiles over > 256 strips;
+    // profiles/round6/ab_cmrs_plan_carry.md.)
+    const int64_t items = (s_hi - s_lo + 1) * h;
+    for (int64_t it = g; it < items; it += GROUPS) {
+        const int64_t s = s_lo + it / h;
+        const int k = (int)(it % h);
+        const int64_t sa = strip_ptr[s];
+        int64_t sb = strip_ptr[s + 1];
+        sb = sb < t1 ? sb : t1;
+        double acc = 0.0;
+        if (sa < sb) {
+            const int a = lower_bound_lds(s_key, (int)(sa - t0), (int)(sb - t0), k);
+            const int b = lower_bound_lds(s_key, a, (int)(sb - t0), k + 1);
+            for (int j = a + lane; j < b; j += L)
+                acc += prod[j];
         }
+        acc = group_sum<L>(acc);
+        const int64_t r = s * h + k;
+        if (lane == 0 && r < n_rows)
+            store_y(y + (r), acc);
     }
 }
 

@@ -1268,6 +1268,9 @@ int launch_coo_staged(const spmv_dims &d, const int32_t *row, const int32_t *col
                                dim3(kBlock), 0, st, d.n_rows, d.nnz, row, col, val, x, y, carry_row,      \
                                carry_val, (const int2 *)nullptr, 0, XGlobal{x});                         \
     } while (0)
+    // long rows: 8 lanes. Round 6 on the cant-like single pass, event-cold
+    // µs over two pairs: L=8 18.56/18.60, L=4 18.44/18.54 (noise), L=16
+    // 19.40/19.36 (profiles/round6/ab_coo_lanes.md)
     if (mean >= 48.0) {
         constexpr int RC = kCooRowCapShort;
         SPMV_COO_STAGED(8);

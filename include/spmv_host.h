@@ -184,7 +184,10 @@ int64_t spmv_sell_split_plan(int64_t n_slices, const int64_t *slice_ptr, int32_t
  * row in the column-major ELL layout of spmv_ell_fill (ld, ki), the rest
  * as a row-sorted COO tail.  K_req > 0 forces K (rounded up to ki); 0
  * picks the K that minimises stored bytes (12 per ELL slot, 16 per tail
- * entry).  Fill: ell_col/ell_val[K*ld], tail_row/col/val[tail_nnz].     */
+ * entry) plus 32 MB when both parts are non-empty (the second kernel's
+ * fixed cost): K = 0 (all tail) or the longest row (no tail) where the
+ * split does not save more.  Fill: ell_col/ell_val[K*ld],
+ * tail_row/col/val[tail_nnz].                                            */
 int spmv_hyb_plan(int64_t n_rows, const int64_t *row_ptr, int32_t ki, int32_t K_req, int32_t *K,
                   int64_t *ld, int64_t *tail_nnz);
 int spmv_hyb_fill(int64_t n_rows, const int64_t *row_ptr, const int32_t *col, const double *val,

@@ -750,7 +750,13 @@ int spmv_hyb_plan(int64_t n_rows, const int64_t *row_ptr, int32_t ki, int32_t K_
     int64_t k = K_req;
     if (k <= 0) {
         /* width that minimises stored bytes: 12 per ELL slot (all ld rows),
-         * 16 per tail entry (row, col, val) */
+         * 16 per tail entry (row, col, val), plus kHybTwoKernelBytes when
+         * both parts are non-empty (two kernels in sequence).  One cant-like
+         * matrix cold (events, profiles/round6/ab_hyb_k.md): bytes alone gave
+         * K = 52 (ELL + 866 K-entry tail) 22.2 us; K = 82 (the longest row,
+         * ELL only) 15.1 us, 8.6 MB more bytes.  K = 0 (COO only) and K =
+         * longest row are one kernel each. */
+        const double kHybTwoKernelBytes = 32e6; /* ~4 us of HBM time: a launch gap and a latency ramp */
         const int64_t cap = mx < 65536 ? mx : 65536;
         int64_t *cnt = (int64_t *)calloc((size_t)cap + 2, sizeof(int64_t));
         if (!cnt)
@@ -765,7 +771,8 @@ int spmv_hyb_plan(int64_t n_rows, const int64_t *row_ptr, int32_t ki, int32_t K_
         for (int64_t kk = 1; kk <= cap; ++kk) {
             tail -= gt;           /* every row longer than kk-1 moves one entry */
             gt -= cnt[kk];        /* rows longer than kk */
-            const double cost = 12.0 * (double)ldv * (double)kk + 16.0 * (double)tail;
+            const double cost = 12.0 * (double)ldv * (double)kk + 16.0 * (double)tail +
+                                (tail > 0 ? kHybTwoKernelBytes : 0.0);
             if (cost < best) {
                 best = cost;
                 best_k = kk;

@@ -822,11 +822,11 @@ class DeviceMatrix:
             rc = lib.spmv_hyb_run_hot(d, p["K"], p["ld"], p["ki"], _ptr(a["ell_col"]), _ptr(a["ell_val"]),
                                       p["tail_nnz"], _ptr(a["tail_row"]), _ptr(a["tail_col"]), _ptr(a["tail_val"]),
                                       _ptr(x), _ptr(y), p["H"], _ptr(a["hot"]), _ptr(a["ws"]), a["ws"].numel())
-        elif self.fmt == "hyb" and "tails" in a and "win" in a:
+        elif self.fmt == "hyb" and "win" in a:  # single-pass tail, or no tail (K = the longest row)
             rc = lib.spmv_hyb_run_tail_xwin(d, p["K"], p["ld"], p["ki"], _ptr(a["ell_col"]), _ptr(a["ell_val"]),
                                             p["tail_nnz"], _ptr(a["tail_row"]), _ptr(a["tail_col"]),
-                                            _ptr(a["tail_val"]), _ptr(x), _ptr(y), _ptr(a["tails"]), _ptr(a["win"]),
-                                            p["xcap"])
+                                            _ptr(a["tail_val"]), _ptr(x), _ptr(y), _ptr(a.get("tails")),
+                                            _ptr(a["win"]), p["xcap"])
         elif self.fmt == "hyb" and "tails" in a:
             rc = lib.spmv_hyb_run_tail(d, p["K"], p["ld"], p["ki"], _ptr(a["ell_col"]), _ptr(a["ell_val"]),
                                        p["tail_nnz"], _ptr(a["tail_row"]), _ptr(a["tail_col"]), _ptr(a["tail_val"]),
@@ -959,7 +959,8 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
               xwin: bool | None = None, xwin_rows: int = 0, split: int | None = None,
               cmrs_variant: int | None = None, hot: int | None = None,
               csr16_max_escape: float | None = 0.5, groups: int = 0, head: bool = True,
-              sell_head: bool | None = None, coo_tail: bool | None = None, bigplan: bool = True) -> DeviceMatrix:
+              sell_head: bool | None = None, coo_tail: bool | None = None, bigplan: bool = True,
+              hyb_k: int = 0) -> DeviceMatrix:
     """Build `fmt` on the host (libspmv_host.so), upload it and, for the
     reference's five formats and SELL16, create its C plan (spmv.h): the
     library picks the kernel path — x windows in LDS (CSR, ELL, SELL, CMRS
@@ -971,7 +972,8 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
     the hot-column rule, 0 none, H forced), sell_head (None/True = the head
     copy where the small-matrix kernel runs), coo_tail (None = the single
     pass where the tail plan accepts the matrix, True = it or raise, False =
-    the carry pass), bigplan (tiled CSR's big-tile plan)."""
+    the carry pass), bigplan (tiled CSR's big-tile plan), hyb_k (HYB's ELL
+    width: 0 = spmv_hyb_plan's rule, K > 0 forced)."""
     torch = _torch()
     device = torch.device(device)
     dm = DeviceMatrix(fmt, m.n_rows, m.n_cols, m.nnz, device)
@@ -1066,7 +1068,7 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
                    "spmv_csr_tiled_plan")
         dm.stored_bytes = 12 * m.nnz + 10 * g["n_pairs"] + 4 * g["blk_off"].size
     elif fmt == "hyb":
-        hb = hyb_build(m.n_rows, ptr, col, val, ki=ki or 2)
+        hb = hyb_build(m.n_rows, ptr, col, val, ki=ki or 2, K=hyb_k)
         dm.params = dict(K=hb["K"], ld=hb["ld"], ki=hb["ki"], tail_nnz=hb["tail_nnz"], stored=hb["stored"], H=0)
         if hot != 0:  # one table over the ELL and tail columns together
             ne, nt_ = hb["stored"], hb["tail_nnz"]
@@ -1094,7 +1096,7 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
                 dm.params["single_pass"] = 1
             elif coo_tail:
                 raise SpmvError(rc, "spmv_coo_tail_build (hyb tail)", hip_lib().spmv_last_error().decode())
-        if (xwin is None or xwin) and "tails" in dm.arrays and hb["stored"] > 0:
+        if (xwin is None or xwin) and ("tails" in dm.arrays or hb["tail_nnz"] == 0) and hb["stored"] > 0:
             # the ELL part through the x-window ELL kernel (same bits): one
             # cant-like matrix cold, a full ELL 12.26 vs 13.36 us (profiles/HISTORY.md §H9)
             a, p = dm.arrays, dm.params
@@ -1106,6 +1108,9 @@ def to_device(m: Coo, fmt: str, device="cuda:0", *, lanes: int = 0, variant: int
                    "spmv_ell_xwin_build (hyb)")
             p["xcap"] = cap.value
         dm.stored_bytes = 12 * hb["stored"] + 16 * hb["tail_nnz"]
+        # the first (ELL) kernel; K = 0 runs the tail alone as COO
+        dm.params["kernel"] = ("coo_staged_kernel" if hb["K"] == 0 else
+                               "ell_xwin_kernel" if "win" in dm.arrays else "ell_kernel")
     elif fmt == "cmrs":
         c = cmrs_build(m.n_rows, ptr, h=h)
         dm.params = dict(h=h, n_strips=c["n_strips"])

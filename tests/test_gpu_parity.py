@@ -49,6 +49,10 @@ FMT_PARAMS = [
     ("ell", {"ki": 2, "xwin": True}),
     ("hyb", {}),
     ("hyb", {"ki": 1}),
+    # ELL part + tail forced (the rule picks one part on small matrices: a
+    # second kernel's fixed cost outweighs the bytes the split saves)
+    ("hyb", {"hyb_k": 2}),
+    ("hyb", {"hyb_k": 3, "ki": 1}),
     ("csr", {"xwin": True}),
     ("csr", {"lanes": 2, "xwin": True}),
     ("sell", {"C": 64, "sigma": 1, "ki": 1}),
@@ -68,7 +72,7 @@ FMT_PARAMS = [
     # COO with x windows in LDS (opt-in), CMRS with global x gathers
     ("coo", {"xwin": True}),
     ("coo", {"coo_tail": False}),  # the carry pass (default: single pass where rows allow)
-    ("hyb", {"coo_tail": False}),  # HYB tail through the carry pass
+    ("hyb", {"coo_tail": False, "hyb_k": 2}),  # HYB tail through the carry pass
     ("cmrs", {"h": 8, "xwin": False}),
     # SELL16: 16-bit column offsets from each workgroup's window base
     ("sell16", {"C": 64, "sigma": 1024, "ki": 2}),
@@ -1098,9 +1102,13 @@ def test_hyb_single_pass_tail(torch_dev, case):
     for m in ms:
         if m.n_rows == 0:
             continue
-        a = sa.to_device(m, "hyb", dev)
-        b = sa.to_device(m, "hyb", dev, coo_tail=False)
-        c = sa.to_device(m, "hyb", dev, xwin=False)  # the ELL part without x windows
+        # K = 52 on the cant-like matrices (the stored-bytes optimum; the
+        # rule, which also prices the tail's kernel, picks the longest row
+        # there); fixtures: K = 2, a tail wherever a row is longer
+        K = 2 if case == "fixtures" else 52
+        a = sa.to_device(m, "hyb", dev, hyb_k=K)
+        b = sa.to_device(m, "hyb", dev, coo_tail=False, hyb_k=K)
+        c = sa.to_device(m, "hyb", dev, xwin=False, hyb_k=K)  # the ELL part without x windows
         assert "tails" not in b.arrays and "win" not in c.arrays
         if case != "fixtures":
             assert a.params["tail_nnz"] > 0 and "tails" in a.arrays and "win" in a.arrays, m.label

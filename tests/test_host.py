@@ -275,6 +275,34 @@ def test_csr16_round_trip(kind):
         assert c["n_esc"] > 0.9 * c["n_blocks"]
 
 
+def _hyb_plan(lens, ki=2):
+    import ctypes
+    ptr = np.concatenate([[0], np.cumsum(np.asarray(lens, np.int64))]).astype(np.int64)
+    K, ld, tail = ctypes.c_int32(0), ctypes.c_int64(0), ctypes.c_int64(0)
+    assert sa.host_lib().spmv_hyb_plan(len(lens), sa._ptr(ptr), ki, 0, ctypes.byref(K), ctypes.byref(ld),
+                                       ctypes.byref(tail)) == 0
+    return K.value, ld.value, tail.value
+
+
+def test_hyb_rule_prices_the_second_kernel():
+    """spmv_hyb_plan's K rule: stored bytes (12 per ELL slot, 16 per tail
+    entry) plus 32 MB when both parts are non-empty.  A small matrix gets ONE
+    part: the cant-like rows (64.2 mean, 81 longest) all in the ELL part (the
+    bytes-only optimum, K = 52, ran 22.2 vs 15.1 us, profiles/round6/ab_hyb_k.md);
+    an R-MAT all in the tail (K = 0).  A large matrix with a few long rows
+    still splits."""
+    m = sa.gen_cantlike(0)
+    lens = np.diff(sa.csr_from_coo(m)[0])
+    assert _hyb_plan(lens) == (82, 62464, 0)
+    r = sa.gen_rmat(100_000, 1_000_000, scale=17, seed=2)
+    K, _, tail = _hyb_plan(np.diff(sa.csr_from_coo(r)[0]))
+    assert K == 0 and tail == r.nnz
+    big = np.full(2_000_000, 10, np.int64)
+    big[::2000] = 5000  # 1,000 long rows: 80 MB of tail against 120 GB of ELL padding
+    K, ld, tail = _hyb_plan(big)
+    assert K == 10 and ld == 2_000_000 and tail == 1000 * 4990
+
+
 @pytest.mark.parametrize("kind,K", [("rmat", 0), ("rmat", 3), ("ragged", 0), ("cantlike", 0), ("tiny", 0)])
 def test_hyb_split_round_trip(kind, K):
     """HYB (§8f row 4): ELL part + COO tail hold exactly the CSR entries,

@@ -300,6 +300,7 @@ __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
     __shared__ int2 s_row2[kBlock * R + TP];
     __shared__ int32_t s_prev;
     __shared__ int32_t s_start[RC + 1];  // owned rows' first entries
+    __shared__ double s_sum[ACC ? RC : 1];  // ACC: the owned rows' sums
     const int32_t *s_row = reinterpret_cast<const int32_t *>(s_row2);
     const double *prod = reinterpret_cast<const double *>(s_prod);
 
@@ -417,21 +418,54 @@ __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
         // that begins here; rows without entries in the tail are left
         // untouched.  One L-lane group per row (a hub row's 1,536 tile
         // entries no longer fall to one thread).
-        for (int64_t r = r_lo + g; r <= (int64_t)last; r += GROUPS) {
-            int a, b;
-            if (heads) {
-                a = s_start[r - r_lo];
-                b = s_start[r - r_lo + 1];
-            } else {
-                a = lower_bound_lds(s_row, 0, ne, (int)r);
-                b = lower_bound_lds(s_row, a, ne, (int)r + 1);
+        if (!heads) {  // uniform
+            // a tile over a long run of rows without tail entries (a HYB
+            // tail of a few rows' remainders): each row that begins here is
+            // found at its first entry and summed over [first, end) — the
+            // range the searches gave it, so the same bits — instead of two
+            // binary searches per spanned row, as the non-accumulating path
+            // over long runs of empty rows below
+            for (int j = g; j < n; j += GROUPS) {
+                const int32_t r = s_row[j];
+                if (r <= prev || (j > 0 && s_row[j - 1] == r))
+                    continue;  // uniform over the group: not a row's first entry
+                const int b = lower_bound_lds(s_row, j + 1, ne, r + 1);
+                double s = slice_sum<L>(prod, j, b, lane);
+                s = group_sum<L>(s);
+                if (lane == 0)
+                    y[r] += s;
             }
+            return;
+        }
+        // the row sums into LDS, then y[r] += sum in one coalesced pass with
+        // every thread's y loads in flight together, instead of y[r] += s
+        // inside the row loop (one dependent read of y per row per group):
+        // one cant-like HYB's K = 52 tail 8.92 -> 8.20 us (rocprof trace;
+        // K = 72's tail, 30.4 us, did not move: profiles/round6/ab_hyb_k.md)
+        for (int64_t r = r_lo + g; r <= (int64_t)last; r += GROUPS) {
+            const int a = s_start[r - r_lo], b = s_start[r - r_lo + 1];
             if (a == b)
                 continue;  // uniform over the group
             double s = slice_sum<L>(prod, a, b, lane);
             s = group_sum<L>(s);
             if (lane == 0)
-                y[r] += s;
+                s_sum[r - r_lo] = s;
+        }
+        __syncthreads();
+        const int sp = (int)span;  // <= RC
+        for (int i0 = 0; i0 < sp; i0 += 4 * kBlock) {
+            double yv[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {  // clamped: every load valid, none behind a branch
+                const int i = i0 + (int)threadIdx.x + k * kBlock;
+                yv[k] = y[r_lo + (i < sp ? i : sp - 1)];
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int i = i0 + (int)threadIdx.x + k * kBlock;
+                if (i < sp && s_start[i] != s_start[i + 1])
+                    y[r_lo + i] = yv[k] + s_sum[i];
+            }
         }
         return;
     }

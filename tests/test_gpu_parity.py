@@ -1086,13 +1086,15 @@ def test_coo_single_pass(torch_dev, case):
         assert_parity(m, yb.cpu().numpy(), x.cpu().numpy()[: m.n_cols])
 
 
-@pytest.mark.parametrize("case", ["cantlike", "fixtures", "batch"])
+@pytest.mark.parametrize("case", ["cantlike", "cantlike_k72", "fixtures", "batch"])
 def test_hyb_single_pass_tail(torch_dev, case):
     """HYB's COO tail in one pass (spmv_hyb_run_tail, the default where the
     tail plan allows) against the oracle and the carry pass; y pre-filled
-    with NaN, reproducible run to run."""
+    with NaN, reproducible run to run.  cantlike_k72: tails on scattered
+    rows, tiles spanning thousands of rows (the accumulate path that finds
+    rows at their first entry)."""
     torch, dev = torch_dev
-    if case == "cantlike":
+    if case.startswith("cantlike"):
         ms = [sa.gen_cantlike(0)]
     elif case == "batch":
         ms = [sa.gen_cantlike(1, copies=3)]
@@ -1105,7 +1107,7 @@ def test_hyb_single_pass_tail(torch_dev, case):
         # K = 52 on the cant-like matrices (the stored-bytes optimum; the
         # rule, which also prices the tail's kernel, picks the longest row
         # there); fixtures: K = 2, a tail wherever a row is longer
-        K = 2 if case == "fixtures" else 52
+        K = {"fixtures": 2, "cantlike_k72": 72}.get(case, 52)
         a = sa.to_device(m, "hyb", dev, hyb_k=K)
         b = sa.to_device(m, "hyb", dev, coo_tail=False, hyb_k=K)
         c = sa.to_device(m, "hyb", dev, xwin=False, hyb_k=K)  # the ELL part without x windows

@@ -440,8 +440,9 @@ __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
         // the row sums into LDS, then y[r] += sum in one coalesced pass with
         // every thread's y loads in flight together, instead of y[r] += s
         // inside the row loop (one dependent read of y per row per group):
-        // one cant-like HYB's K = 52 tail 8.92 -> 8.20 us (rocprof trace;
-        // K = 72's tail, 30.4 us, did not move: profiles/round6/ab_hyb_k.md)
+        // one cant-like HYB's K = 52 tail 9.08 / 9.16 -> 8.64 / 8.72 us
+        // (rocprof trace, same box; K = 72's tail, 30.4 us, did not move:
+        // profiles/round6/ab_hyb_k.md)
         for (int64_t r = r_lo + g; r <= (int64_t)last; r += GROUPS) {
             const int a = s_start[r - r_lo], b = s_start[r - r_lo + 1];
             if (a == b)

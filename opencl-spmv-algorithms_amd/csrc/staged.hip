@@ -283,6 +283,20 @@ constexpr bool kCmrsRemapDefault = false;
 // its last row that run past the tile end (tails[tile] of them, at most
 // kCooTailCap, from spmv_coo_tail_build) and finishes that row itself; a row begun
 // in an earlier tile is skipped, so no carry pass runs.
+// COO_STAMP(k) / COO_NOTE(k, v): per-tile phase hooks, no-ops in the
+// product; a lab build (tools/build_variant.sh stamps_coo) injects
+// tools/lab_stamps_coo.h (tools/coo_stamps.py reads them)
+#ifndef COO_STAMP
+#define COO_STAMP(k) \
+    do {             \
+    } while (0)
+#define COO_NOTE(k, v) \
+    do {               \
+    } while (0)
+#define COO_STAMP_END() \
+    do {                \
+    } while (0)
+#endif
 template <int L, int R, bool ACC, bool XW, bool NT = false, typename XS = XGlobal, bool TAIL = false,
           int RC = kCooRowCap>
 __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
@@ -305,6 +319,7 @@ __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
     const double *prod = reinterpret_cast<const double *>(s_prod);
 
     const int64_t tile = xcd_block(remap);  // remap: neighbouring tiles (shared x lines) on one XCD
+    COO_STAMP(0);
     const int64_t t0 = tile * CH;
     const int64_t t1 = t0 + CH < nnz ? t0 + CH : nnz;
     const int n = (int)(t1 - t0);
@@ -365,6 +380,7 @@ __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
         stage_chunk<R, NT>(t0, t1, nnz, col, val, xs, s_prod, keys);
     }
     __syncthreads();
+    COO_STAMP(1);  // products and keys in LDS
 
     const int32_t prev = s_prev;
     const int32_t first = s_row[0], last = s_row[n - 1];
@@ -398,6 +414,63 @@ __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
             __syncthreads();
         }
     }
+    // Tiles over more than RC rows (long runs of rows without entries): the
+    // entries that begin a row after prev as a bitmap over the tile's n
+    // entries (one ballot per 64), so a row's end is the next set bit (or ne)
+    // — the range [first, end) a search over s_row gives it, so the same
+    // bits.  Searching per row-first entry instead (lower_bound over the
+    // rest of the tile, 11 dependent LDS reads, the wave waiting on its
+    // slowest group in nearly every step of a walk over all entries) took
+    // 13-23 us per such tile (tools/coo_stamps.py; profiles/round6/ab_coo_first.md).
+    // (The words live in s_start, behind the span bitmap where there is one:
+    // a __shared__ array of their own took one tile per CU off the
+    // cant-like single pass, 20,592 B of LDS > 160 KiB / 8.)
+    constexpr int FW = (2 * kBlock * R + 63) / 64 * 2;  // row-first words of a tile
+    static_assert(FW < RC, "the row-first words fit in s_start");
+    auto build_first = [&](uint32_t *s_first) {
+        const int lw = (int)threadIdx.x & (kWave - 1);
+        for (int j0 = (int)threadIdx.x - lw; j0 < n; j0 += kBlock) {  // wave-uniform
+            const int j = j0 + lw;
+            bool f = false;
+            if (j < n) {
+                const int32_t r = s_row[j];
+                f = r > prev && (j == 0 || s_row[j - 1] != r);
+            }
+            const uint64_t bal = __ballot(f);
+            if (lw == 0) {
+                s_first[j0 >> 5] = (uint32_t)bal;
+                s_first[(j0 >> 5) + 1] = (uint32_t)(bal >> 32);
+            }
+        }
+    };
+    // fn(first, end) for every row that begins in the tile, one 32-entry
+    // word of s_first per group at a time (uniform over the group)
+    auto for_each_row = [&](const uint32_t *s_first, auto &&fn) {
+        const int nfw = (n + 31) >> 5;
+        for (int w = g; w < nfw; w += GROUPS) {
+            uint32_t m = s_first[w];
+            while (m) {
+                const int j = w * 32 + __builtin_ctz(m);
+                m &= m - 1;
+                int b = ne;
+                if (m) {
+                    b = w * 32 + __builtin_ctz(m);
+                } else {
+                    for (int w2 = w + 1; w2 < nfw; ++w2) {
+                        const uint32_t m2 = s_first[w2];
+                        if (m2) {
+                            b = w2 * 32 + __builtin_ctz(m2);
+                            break;
+                        }
+                    }
+                }
+                fn(j, b);
+            }
+        }
+    };
+    COO_STAMP(2);  // row starts in LDS (heads)
+    COO_NOTE(4, (uint64_t)span);
+    COO_NOTE(5, (uint64_t)(heads ? 0 : span <= 32 * (int64_t)(RC + 1 - FW) ? 1 : 2));
 
     // carry: the first row's entries when it began in an earlier tile (with
     // TAIL the earlier tile summed them from its tail)
@@ -420,21 +493,18 @@ __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
         // entries no longer fall to one thread).
         if (!heads) {  // uniform
             // a tile over a long run of rows without tail entries (a HYB
-            // tail of a few rows' remainders): each row that begins here is
-            // found at its first entry and summed over [first, end) — the
-            // range the searches gave it, so the same bits — instead of two
-            // binary searches per spanned row, as the non-accumulating path
-            // over long runs of empty rows below
-            for (int j = g; j < n; j += GROUPS) {
-                const int32_t r = s_row[j];
-                if (r <= prev || (j > 0 && s_row[j - 1] == r))
-                    continue;  // uniform over the group: not a row's first entry
-                const int b = lower_bound_lds(s_row, j + 1, ne, r + 1);
+            // tail of a few rows' remainders): the rows that begin here from
+            // the row-first bitmap, instead of two binary searches per
+            // spanned row
+            uint32_t *s_first = reinterpret_cast<uint32_t *>(s_start);
+            build_first(s_first);
+            __syncthreads();
+            for_each_row(s_first, [&](int j, int b) {
                 double s = slice_sum<L>(prod, j, b, lane);
                 s = group_sum<L>(s);
                 if (lane == 0)
-                    y[r] += s;
-            }
+                    y[s_row[j]] += s;
+            });
             return;
         }
         // the row sums into LDS, then y[r] += sum in one coalesced pass with
@@ -473,36 +543,36 @@ __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
     // owned rows: (prev, last], plus the trailing empty rows in the last
     // tile; a continued first row equals prev, so it is excluded here
     const int64_t r_hi = t1 == nnz ? n_rows - 1 : (int64_t)last;
-    if (!heads && span > RC && span <= 32 * (int64_t)(RC + 1)) {  // uniform
+    if (!heads && span > RC && span <= 32 * (int64_t)(RC + 1 - FW)) {  // uniform
         // A tile over a long run of mostly empty rows (R-MAT: up to ~28 K
-        // rows per 512-entry tile): the rows WITH entries are found at their
-        // first entry (a key change), each summed over [start, end) exactly
-        // as the search path sums it (the same bits), and marked in a bitmap
-        // (s_start's words); then the others are written as zeros,
+        // rows per 512-entry tile): the rows WITH entries come from the
+        // row-first bitmap, each summed over [first, end) exactly as the
+        // search path sums it (the same bits), and marked in a bitmap over
+        // the span (s_start's words); then the others are written as zeros,
         // coalesced.  The search path did two binary searches per owned row.
         uint32_t *s_bits = reinterpret_cast<uint32_t *>(s_start);
         const int nw = (int)((span + 31) >> 5);
         for (int i = threadIdx.x; i < nw; i += kBlock)
             s_bits[i] = 0u;
+        uint32_t *s_first = s_bits + nw;
+        build_first(s_first);
         __syncthreads();
-        for (int j = g; j < n; j += GROUPS) {  // the tile's entries (tail entries continue the last row)
+        for_each_row(s_first, [&](int j, int b) {
             const int32_t r = s_row[j];
-            if (r <= prev || (j > 0 && s_row[j - 1] == r))
-                continue;  // uniform over the group: not a row's first entry
-            const int b = lower_bound_lds(s_row, j + 1, ne, r + 1);
             double sm = slice_sum<L>(prod, j, b, lane);
             sm = group_sum<L>(sm);
             if (lane == 0) {
                 store_y(y + r, sm);
                 atomicOr(&s_bits[(r - r_lo) >> 5], 1u << ((r - r_lo) & 31));
             }
-        }
+        });
         __syncthreads();
         for (int64_t r = r_lo + threadIdx.x; r <= r_hi; r += kBlock) {
             const bool has = r <= last && ((s_bits[(r - r_lo) >> 5] >> ((r - r_lo) & 31)) & 1u);
             if (!has)
                 store_y(y + r, 0.0);
         }
+        COO_STAMP_END();
         return;
     }
     for (int64_t r = r_lo + g; r <= r_hi; r += GROUPS) {
@@ -522,6 +592,7 @@ __global__ __launch_bounds__(kBlock) void coo_staged_kernel(
         if (lane == 0)
             store_y(y + (r), s);
     }
+    COO_STAMP_END();
 }
 
 // ------------------------------------------------------------ CSR tiled

@@ -1023,7 +1023,7 @@ def test_sell16_head_same_bits_nonfinite_x(torch_dev, ki):
 COO_TAIL_CAP = 80  # csrc/staged.hip kCooTailCap
 
 
-@pytest.mark.parametrize("case", ["cantlike", "ragged_tails", "aligned", "odd_tail", "fixtures", "batch"])
+@pytest.mark.parametrize("case", ["cantlike", "ragged_tails", "aligned", "odd_tail", "fixtures", "batch", "tail52"])
 def test_coo_single_pass(torch_dev, case):
     """The single-pass COO (the default where the plan allows) matches the oracle
     (parity rule) and the carry path within it wherever every row ends
@@ -1035,6 +1035,16 @@ def test_coo_single_pass(torch_dev, case):
         ms = [sa.gen_cantlike(0)]
     elif case == "batch":
         ms = [sa.gen_cantlike(1, copies=3)]
+    elif case == "tail52":
+        # the cant-like rows' entries past 52 (HYB's tail as a COO matrix):
+        # two 1,536-entry tiles span more than 250 rows, the row-first
+        # bitmap path of coo_staged_kernel (profiles/round6/ab_coo_first.md)
+        c = sa.gen_cantlike(0)
+        ptr, col, val = sa.csr_from_coo(c)
+        h = sa.hyb_build(c.n_rows, ptr, col, val, ki=2, K=52)
+        t = h["tail_nnz"]
+        ms = [sa.Coo(c.n_rows, c.n_cols, h["tail_row"][:t].copy(), h["tail_col"][:t].copy(),
+                     h["tail_val"][:t].copy(), False, "cant-like tail past 52")]
     elif case == "ragged_tails":
         lens = rng.integers(0, COO_TAIL_CAP + 1, 4000)
         lens[::53] = 0
